@@ -1,0 +1,51 @@
+# Build of the MI355X renderer (gfx950) and its CLI. No cmake: hipcc only.
+#   make            -> simpleraytracer_amd/lib/libModelRunner.so, bin/test_app
+#   make oracle     -> oracle/build/libsrt_oracle.so (CPU checker; test infrastructure)
+#   make ref        -> oracle/_ref/* (reference test_app built from /root/reference, if present)
+HIPCC    ?= /opt/rocm/bin/hipcc
+ARCH     ?= gfx950
+BUILD    := build/obj
+LIBDIR   := simpleraytracer_amd/lib
+LIB      := $(LIBDIR)/libModelRunner.so
+CSRC     := simpleraytracer_amd/csrc
+
+# -ffp-contract=off: every FMA in the canonical math is an explicit fmaf.
+# -fno-slp-vectorize: keeps hipcc from pairing independent fp32 FMAs into v_pk_fma_f32 plus
+#  register shuffles (packed f32 has no throughput advantage on gfx950).
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -fno-slp-vectorize \
+            -fvisibility=hidden -DRADEONPROML_BUILD -Iinclude -Wall -Wno-unused-result
+LDFLAGS  := -shared -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib -Wl,--no-undefined
+
+OBJS := $(BUILD)/render.o $(BUILD)/renderer.o $(BUILD)/scene.o $(BUILD)/image.o \
+        $(BUILD)/model.o $(BUILD)/context.o $(BUILD)/srt_api.o
+
+HEADERS := $(wildcard $(CSRC)/*.h) include/model_runner.h include/srt_render.h
+
+.PHONY: all oracle ref clean
+all: $(LIB) bin/test_app
+
+$(BUILD)/%.o: $(CSRC)/%.hip $(HEADERS)
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(BUILD)/%.o: $(CSRC)/%.cpp $(HEADERS)
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): $(OBJS)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) --offload-arch=$(ARCH) $(OBJS) -o $@ $(LDFLAGS)
+
+bin/test_app: tools/test_app.cpp $(LIB) include/model_runner.h include/srt_render.h
+	@mkdir -p bin
+	g++ -O2 -std=c++17 -Wall -Iinclude $< -o $@ -L$(LIBDIR) -lModelRunner -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)'
+
+oracle:
+	$(MAKE) -C oracle
+
+ref:
+	$(MAKE) -C oracle ref
+
+clean:
+	rm -rf build bin $(LIBDIR)
+	$(MAKE) -C oracle clean

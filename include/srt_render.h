@@ -1,0 +1,64 @@
+/*
+ * srt_render.h -- extension C ABI of libModelRunner.so (not part of the reference ABI).
+ *
+ * The reference exposes only the 14 ml* entry points of model_runner.h, which take host
+ * images. Benchmarks, parity tests and multi-process (one rank per GPU) callers need the
+ * render stages on device-resident buffers and a way to produce scene files; that is this
+ * header. Plain pointers and sizes only; `stream` is a hipStream_t passed as void*.
+ * Every int-returning function returns 0 on success, -1 on failure; the failure text is
+ * then available from srtGetLastError() (thread-local).
+ */
+#ifndef SRT_RENDER_H
+#define SRT_RENDER_H
+
+#include <stddef.h>
+
+#include "model_runner.h" /* ML_API_ENTRY */
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Scene kinds for srtWriteScene (DESIGN.md "Scene file"). */
+#define SRT_SCENE_TRIANGLE 0 /* one triangle: config C1 */
+#define SRT_SCENE_CORNELL 1  /* 12-triangle Cornell box: config C2 */
+#define SRT_SCENE_SOUP 2     /* synthetic soup: configs C3-C5 */
+
+/* Trace kernel variants for srtTraceAsync. */
+#define SRT_TRACE_LDS 0
+#define SRT_TRACE_SCALAR 1
+
+ML_API_ENTRY const char* srtGetLastError(void);
+
+/* Write a generated scene file. `triangles`, `seed` and `size` (soup half-extent, 0 =
+ * default 0.02 below 1M triangles, 0.01 from 1M) apply to SRT_SCENE_SOUP only. */
+ML_API_ENTRY int srtWriteScene(const char* path, int kind, unsigned long long triangles,
+                               unsigned long long seed, float size);
+
+/* Read a scene file's triangle count. */
+ML_API_ENTRY int srtSceneTriangles(const char* path, unsigned long long* triangles);
+
+/* Affine primary-ray frame of a scene at W x H: 12 floats origin[3] base[3] du[3] dv[3]. */
+ML_API_ENTRY int srtSceneFrame(const char* path, size_t width, size_t height, float* frame12);
+
+/* Device-resident scene (vertices, albedo, edge records) on one HIP device. */
+typedef struct srt_device_scene_t* srt_device_scene;
+
+ML_API_ENTRY srt_device_scene srtDeviceSceneCreate(const char* path, int device);
+ML_API_ENTRY void srtDeviceSceneRelease(srt_device_scene scene);
+ML_API_ENTRY unsigned long long srtDeviceSceneTriangles(srt_device_scene scene);
+
+/* Stage 1: edge-record setup for a W x H frame (one thread per triangle). */
+ML_API_ENTRY int srtPrepareAsync(srt_device_scene scene, size_t width, size_t height, void* stream);
+
+/* Stage 2: trace frame rows [row_begin, row_begin + row_count) of the prepared frame.
+ * d_offsets: row_count x width x 2 float (sample offsets, band-local rows);
+ * d_rgba:    row_count x width x 4 float (r, g, b, float(tri_id)). */
+ML_API_ENTRY int srtTraceAsync(srt_device_scene scene, const float* d_offsets, float* d_rgba,
+                               size_t row_begin, size_t row_count, int variant, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SRT_RENDER_H */

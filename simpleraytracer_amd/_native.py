@@ -1,0 +1,108 @@
+"""ctypes binding of libModelRunner.so (include/model_runner.h + include/srt_render.h).
+
+The shared library is built in-tree by ``make`` (or ``__graft_entry__.build()``) into
+``simpleraytracer_amd/lib/libModelRunner.so``. There is no fallback: importing the renderer
+without the library raises immediately.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+PACKAGE_DIR = Path(__file__).resolve().parent
+LIB_PATH = PACKAGE_DIR / "lib" / "libModelRunner.so"
+
+ML_OK = 0
+ML_FAIL = 1
+ML_FLOAT32 = 0
+ML_FLOAT16 = 1
+
+SRT_SCENE_TRIANGLE = 0
+SRT_SCENE_CORNELL = 1
+SRT_SCENE_SOUP = 2
+SRT_TRACE_LDS = 0
+SRT_TRACE_SCALAR = 1
+
+
+class ImageInfo(ctypes.Structure):
+    """``ml_image_info`` (model_runner.h:100-106): 32 bytes, dtype at 0, width at 8."""
+
+    _fields_ = [
+        ("dtype", ctypes.c_int),
+        ("width", ctypes.c_size_t),
+        ("height", ctypes.c_size_t),
+        ("channels", ctypes.c_size_t),
+    ]
+
+    def as_tuple(self):
+        return (self.dtype, self.width, self.height, self.channels)
+
+
+class ModelParams(ctypes.Structure):
+    """``ml_model_params`` (model_runner.h:53-60): 24 bytes."""
+
+    _fields_ = [
+        ("model_path", ctypes.c_char_p),
+        ("input_node", ctypes.c_char_p),
+        ("output_node", ctypes.c_char_p),
+    ]
+
+
+# name -> (restype, argtypes)
+_SIGNATURES = {
+    "mlCreateContext": (ctypes.c_void_p, []),
+    "mlGetContextError": (ctypes.c_char_p, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t]),
+    "mlReleaseContext": (None, [ctypes.c_void_p]),
+    "mlCreateImage": (ctypes.c_void_p, [ctypes.c_void_p, ctypes.POINTER(ImageInfo)]),
+    "mlGetImageInfo": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ImageInfo)]),
+    "mlMapImage": (ctypes.c_void_p, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_size_t)]),
+    "mlUnmapImage": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "mlReleaseImage": (None, [ctypes.c_void_p]),
+    "mlCreateModel": (ctypes.c_void_p, [ctypes.c_void_p, ctypes.POINTER(ModelParams)]),
+    "mlGetModelError": (ctypes.c_char_p, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t]),
+    "mlGetModelInfo": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ImageInfo), ctypes.POINTER(ImageInfo)]),
+    "mlSetModelInputInfo": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ImageInfo)]),
+    "mlInfer": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "mlReleaseModel": (None, [ctypes.c_void_p]),
+    "srtGetLastError": (ctypes.c_char_p, []),
+    "srtWriteScene": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, ctypes.c_ulonglong, ctypes.c_ulonglong,
+                                     ctypes.c_float]),
+    "srtSceneTriangles": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_ulonglong)]),
+    "srtSceneFrame": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_size_t,
+                                     ctypes.POINTER(ctypes.c_float)]),
+    "srtDeviceSceneCreate": (ctypes.c_void_p, [ctypes.c_char_p, ctypes.c_int]),
+    "srtDeviceSceneRelease": (None, [ctypes.c_void_p]),
+    "srtDeviceSceneTriangles": (ctypes.c_ulonglong, [ctypes.c_void_p]),
+    "srtPrepareAsync": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_void_p]),
+    "srtTraceAsync": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                     ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]),
+}
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load libModelRunner.so once; raise loudly if it has not been built."""
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise RuntimeError(
+                f"{LIB_PATH} is missing: build the HIP library first (`make` at the repo root or "
+                "`python -c 'import __graft_entry__ as g; g.build()'`); there is no CPU fallback")
+        handle = ctypes.CDLL(os.fspath(LIB_PATH), mode=ctypes.RTLD_GLOBAL)
+        for name, (restype, argtypes) in _SIGNATURES.items():
+            fn = getattr(handle, name)
+            fn.restype = restype
+            fn.argtypes = argtypes
+        _lib = handle
+    return _lib
+
+
+def exported_names():
+    return list(_SIGNATURES)
+
+
+def last_error() -> str:
+    msg = lib().srtGetLastError()
+    return msg.decode() if msg else ""

@@ -1,0 +1,195 @@
+#include "model.h"
+
+#include <stdexcept>
+
+#include "image.h"
+#include "utils.h"
+
+namespace ML {
+
+// model.cpp:73-139 order: params, model_path, then the file. The GPU side is created by the
+// first SetInputInfo (it needs the frame size), so a model can be inspected on a host
+// without a GPU; rendering there fails with the HIP error text.
+Model::Model(ml_model_params const* params) {
+    if (params == nullptr) {
+        throw std::runtime_error("Bad parameters argument");
+    }
+    if (params->model_path == nullptr) {
+        throw std::runtime_error("Bad model_path model parameter value");
+    }
+    m_scene = srt::LoadScene(params->model_path);
+}
+
+// model.cpp:141-159 (no "no session" failure here: a constructed model always has a scene).
+ml_status Model::GetInfo(ml_image_info* input_info, ml_image_info* output_info) {
+    if (input_info != nullptr) {
+        *input_info = m_input_info;
+    }
+    if (output_info != nullptr) {
+        *output_info = m_output_info;
+    }
+    return ML_OK;
+}
+
+// model.cpp:161-235 semantics and messages. Deviations (SURVEY.md section 8(b) latent bugs
+// 2 and 3, fixed): a zero dimension is rejected up front instead of after committing it, and
+// the new input info is committed only once the device buffers exist, so a failed call leaves
+// the model unchanged and a retry with the same dims does real work.
+ml_status Model::SetInputInfo(ml_image_info const* info) {
+    m_error_cache.str("");
+    if (info == nullptr) {
+        m_error_cache << "Bad info parameter";
+        return ML_FAIL;
+    }
+    if (m_input_info.dtype != info->dtype) {
+        m_error_cache << "Overriding data type " << static_cast<int>(m_input_info.dtype) << " with "
+                      << static_cast<int>(info->dtype);
+        return ML_FAIL;
+    }
+    const bool dims_ok = ForEachDim([this, info](auto dim, char const* name) {
+        if (m_input_info.*dim != 0 && info->*dim != m_input_info.*dim) {
+            m_error_cache << "Overriding " << name << " dimension " << m_input_info.*dim << " with " << info->*dim;
+            return false;
+        }
+        return true;
+    });
+    if (!dims_ok) {
+        return ML_FAIL;
+    }
+    const bool specified = ForEachDim([this, info](auto dim, char const* name) {
+        if (info->*dim == 0) {
+            m_error_cache << "Input image " << name << " dimension is not specified";
+            return false;
+        }
+        return true;
+    });
+    if (!specified) {
+        return ML_FAIL;
+    }
+    const bool same = ForEachDim([this, info](auto dim, char const*) { return m_input_info.*dim == info->*dim; });
+    if (same && m_renderer && m_renderer->configured()) {
+        return ML_OK;  // nothing changed
+    }
+    try {
+        if (!m_renderer) {
+            m_renderer = std::make_unique<srt::Renderer>(m_scene, srt::VisibleDevices());
+        }
+        m_renderer->Configure(info->width, info->height);
+    } catch (std::exception& e) {
+        m_error_cache << e.what();
+        return ML_FAIL;
+    }
+    m_input_info = *info;
+    m_output_info = ml_image_info{ML_FLOAT32, info->width, info->height, 4};
+    return ML_OK;
+}
+
+// model.cpp:237-294 checks and messages; plus (fix of latent bug 4) the output dtype check.
+ml_status Model::Infer(ml_image input, ml_image output) {
+    m_error_cache.str("");
+    if (Image::FromHandle(input) == nullptr) {
+        m_error_cache << "Bad input image handle";
+        return ML_FAIL;
+    }
+    if (Image::FromHandle(output) == nullptr) {
+        m_error_cache << "Bad output image handle";
+        return ML_FAIL;
+    }
+    ml_image_info out_info{};
+    Image::FromHandle(output)->GetInfo(&out_info);
+    const bool dims_ok = ForEachDim([this, &out_info](auto dim, char const* name) {
+        if (out_info.*dim != m_output_info.*dim) {
+            m_error_cache << "Output image " << name << " dimension " << out_info.*dim << " does not match "
+                          << m_output_info.*dim;
+            return false;
+        }
+        return true;
+    });
+    if (!dims_ok) {
+        return ML_FAIL;
+    }
+    if (out_info.dtype != m_output_info.dtype) {
+        m_error_cache << "Output image data type " << static_cast<int>(out_info.dtype) << " does not match "
+                      << static_cast<int>(m_output_info.dtype);
+        return ML_FAIL;
+    }
+    return RenderToImage(*Image::FromHandle(input), *Image::FromHandle(output)) ? ML_OK : ML_FAIL;
+}
+
+// model.cpp:301-347 (InferToCache) counterpart: input checks, then render straight into the
+// output image's (page-locked) buffer -- no intermediate host cache.
+bool Model::RenderToImage(Image& input, Image& output) {
+    m_error_cache.str("");
+    const bool specified = ForEachDim([this](auto dim, char const* name) {
+        if (m_input_info.*dim == 0) {
+            m_error_cache << "Input image " << name << " dimension is not specified";
+            return false;
+        }
+        return true;
+    });
+    if (!specified) {
+        return false;
+    }
+    const size_t in_expected = m_input_info.width * m_input_info.height * m_input_info.channels * sizeof(float);
+    size_t in_size = 0;
+    void* in_data = input.Map(&in_size);
+    if (in_size != in_expected) {
+        input.Unmap(in_data);
+        m_error_cache << "Internal error: input size does not match: " << in_size << " vs " << in_expected;
+        return false;
+    }
+    const size_t out_expected = m_output_info.width * m_output_info.height * m_output_info.channels * sizeof(float);
+    size_t out_size = 0;
+    void* out_data = output.Map(&out_size);
+    if (out_size != out_expected) {
+        input.Unmap(in_data);
+        output.Unmap(out_data);
+        m_error_cache << "Internal error: output size does not match: " << out_size << " vs " << out_expected;
+        return false;
+    }
+    bool ok = true;
+    try {
+        m_renderer->Render(static_cast<const float*>(in_data), static_cast<float*>(out_data));
+    } catch (std::exception& e) {
+        m_error_cache << "Render error: " << e.what();
+        ok = false;
+    }
+    input.Unmap(in_data);
+    output.Unmap(out_data);
+    return ok;
+}
+
+char* Model::GetError(char* buffer, size_t buffer_size) const {
+    return FillBuffer(buffer, buffer_size, m_error_cache.str());
+}
+
+}  // namespace ML
+
+extern "C" {
+
+ML_API_ENTRY char* mlGetModelError(ml_model model, char* buffer, size_t buffer_size) {
+    ML::Model* m = ML::Model::FromHandle(model);
+    if (m == nullptr) {
+        return ML::FillBuffer(buffer, buffer_size, "Bad model handle");
+    }
+    return m->GetError(buffer, buffer_size);
+}
+
+ML_API_ENTRY ml_status mlGetModelInfo(ml_model model, ml_image_info* input_info, ml_image_info* output_info) {
+    ML::Model* m = ML::Model::FromHandle(model);
+    return m == nullptr ? ML_FAIL : m->GetInfo(input_info, output_info);
+}
+
+ML_API_ENTRY ml_status mlSetModelInputInfo(ml_model model, ml_image_info const* info) {
+    ML::Model* m = ML::Model::FromHandle(model);
+    return m == nullptr ? ML_FAIL : m->SetInputInfo(info);
+}
+
+ML_API_ENTRY ml_status mlInfer(ml_model model, ml_image input, ml_image output) {
+    ML::Model* m = ML::Model::FromHandle(model);
+    return m == nullptr ? ML_FAIL : m->Infer(input, output);
+}
+
+ML_API_ENTRY void mlReleaseModel(ml_model model) { delete ML::Model::FromHandle(model); }
+
+}  // extern "C"

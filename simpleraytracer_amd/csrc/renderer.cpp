@@ -1,0 +1,299 @@
+#include "renderer.h"
+
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <sstream>
+
+#include "render.h"
+
+namespace srt {
+namespace {
+
+// Restores the caller's current HIP device on scope exit (the C ABI must not leak a
+// hipSetDevice into the host application).
+class DeviceGuard {
+public:
+    explicit DeviceGuard(int device) {
+        if (hipGetDevice(&m_prev) != hipSuccess) {
+            m_prev = -1;
+        }
+        HipCheck(hipSetDevice(device), "hipSetDevice");
+    }
+    ~DeviceGuard() {
+        if (m_prev >= 0) {
+            (void)hipSetDevice(m_prev);
+        }
+    }
+
+private:
+    int m_prev = -1;
+};
+
+void NcclCheck(ncclResult_t res, const char* what) {
+    if (res != ncclSuccess) {
+        throw std::runtime_error(std::string("RCCL error: ") + what + ": " + ncclGetErrorString(res));
+    }
+}
+
+template <class T>
+T* DeviceAlloc(std::size_t count, const char* what) {
+    void* p = nullptr;
+    HipCheck(hipMalloc(&p, count * sizeof(T)), what);
+    return static_cast<T*>(p);
+}
+
+bool GatherWithRccl() {
+    const char* mode = std::getenv("SRT_GATHER");
+    return mode == nullptr || std::strcmp(mode, "direct") != 0;
+}
+
+}  // namespace
+
+void HipCheck(hipError_t err, const char* what) {
+    if (err != hipSuccess) {
+        throw std::runtime_error(std::string("HIP error: ") + what + ": " + hipGetErrorString(err));
+    }
+}
+
+std::vector<int> VisibleDevices() {
+    int count = 0;
+    hipError_t err = hipGetDeviceCount(&count);
+    if (err != hipSuccess || count <= 0) {
+        throw std::runtime_error(std::string("HIP error: no HIP device available (") +
+                                 (err != hipSuccess ? hipGetErrorString(err) : "device count 0") +
+                                 "); this renderer has no CPU path");
+    }
+    std::vector<int> devices;
+    const char* env = std::getenv("ML_VISIBLE_DEVICES");
+    if (env == nullptr || *env == '\0') {
+        devices.push_back(0);
+        return devices;
+    }
+    std::stringstream ss(env);
+    std::string item;
+    while (std::getline(ss, item, ',')) {
+        char* end = nullptr;
+        long v = std::strtol(item.c_str(), &end, 10);
+        if (item.empty() || *end != '\0' || v < 0 || v >= count) {
+            throw std::runtime_error("Bad ML_VISIBLE_DEVICES entry '" + item + "' (" + std::to_string(count) +
+                                     " HIP devices present)");
+        }
+        devices.push_back(static_cast<int>(v));
+    }
+    if (devices.empty()) {
+        devices.push_back(0);
+    }
+    return devices;
+}
+
+int TraceVariantFromEnv() {
+    const char* v = std::getenv("SRT_TRACE_VARIANT");
+    if (v != nullptr && (std::strcmp(v, "scalar") == 0 || std::strcmp(v, "1") == 0)) {
+        return kTraceScalar;
+    }
+    return kTraceLds;
+}
+
+DeviceScene::DeviceScene(const Scene& scene, int device)
+    : m_device(device), m_n(scene.triangle_count()), m_camera(scene.camera) {
+    std::memcpy(m_background, scene.background, sizeof(m_background));
+    DeviceGuard guard(device);
+    try {
+        m_vertices = DeviceAlloc<float>(m_n * 9, "hipMalloc(vertices)");
+        m_albedo = DeviceAlloc<float>(m_n * 3, "hipMalloc(albedo)");
+        m_edges = DeviceAlloc<float>(PaddedTriangleCount(m_n) * 12, "hipMalloc(edges)");
+        HipCheck(hipMemcpy(m_vertices, scene.vertices.data(), m_n * 9 * sizeof(float), hipMemcpyHostToDevice),
+                 "hipMemcpy(vertices)");
+        HipCheck(hipMemcpy(m_albedo, scene.albedo.data(), m_n * 3 * sizeof(float), hipMemcpyHostToDevice),
+                 "hipMemcpy(albedo)");
+    } catch (...) {
+        (void)hipFree(m_vertices);
+        (void)hipFree(m_albedo);
+        (void)hipFree(m_edges);
+        throw;
+    }
+}
+
+DeviceScene::~DeviceScene() {
+    int prev = -1;
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(m_device);
+    (void)hipFree(m_vertices);
+    (void)hipFree(m_albedo);
+    (void)hipFree(m_edges);
+    if (prev >= 0) {
+        (void)hipSetDevice(prev);
+    }
+}
+
+void DeviceScene::Prepare(std::size_t width, std::size_t height, hipStream_t stream) {
+    if (width == 0 || height == 0) {
+        throw std::runtime_error("Prepare: frame dimensions must be non-zero");
+    }
+    m_frame = MakeFrame(m_camera, width, height);
+    m_width = width;
+    m_height = height;
+    HipCheck(LaunchPrepare(m_vertices, m_n, m_frame, m_edges, stream), "prepare kernel launch");
+}
+
+void DeviceScene::Trace(const float* d_offsets, float* d_rgba, std::size_t row_begin, std::size_t row_count,
+                        int variant, hipStream_t stream) const {
+    if (m_width == 0) {
+        throw std::runtime_error("Trace: Prepare() has not been called");
+    }
+    if (row_begin + row_count > m_height) {
+        throw std::runtime_error("Trace: row band outside the frame");
+    }
+    BandArgs band{d_offsets, d_rgba, m_width, m_height, row_begin, row_count};
+    HipCheck(LaunchTrace(m_edges, m_n, m_vertices, m_albedo, m_frame, m_background, band, variant, stream),
+             "trace kernel launch");
+}
+
+struct Renderer::Slot {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::unique_ptr<DeviceScene> scene;
+    float* offsets = nullptr;  // band_rows x W x 2
+    float* rgba = nullptr;     // band_rows x W x 4
+    std::size_t row_begin = 0;
+    std::size_t row_count = 0;
+};
+
+Renderer::Renderer(const Scene& scene, std::vector<int> devices) : m_variant(TraceVariantFromEnv()) {
+    for (int d : devices) {
+        auto slot = std::make_unique<Slot>();
+        slot->device = d;
+        DeviceGuard guard(d);
+        HipCheck(hipStreamCreateWithFlags(&slot->stream, hipStreamNonBlocking), "hipStreamCreate");
+        m_slots.push_back(std::move(slot));
+        m_slots.back()->scene = std::make_unique<DeviceScene>(scene, d);
+    }
+    m_use_rccl = m_slots.size() > 1 && GatherWithRccl();
+    if (m_use_rccl) {
+        std::vector<ncclComm_t> comms(m_slots.size());
+        NcclCheck(ncclCommInitAll(comms.data(), static_cast<int>(devices.size()), devices.data()),
+                  "ncclCommInitAll (repeated devices need SRT_GATHER=direct)");
+        m_comms.assign(comms.begin(), comms.end());
+    }
+}
+
+Renderer::~Renderer() {
+    ReleaseBuffers();
+    for (void* c : m_comms) {
+        (void)ncclCommDestroy(static_cast<ncclComm_t>(c));
+    }
+    for (auto& slot : m_slots) {
+        (void)hipSetDevice(slot->device);
+        slot->scene.reset();
+        (void)hipStreamDestroy(slot->stream);
+    }
+}
+
+void Renderer::ReleaseBuffers() {
+    for (auto& slot : m_slots) {
+        (void)hipSetDevice(slot->device);
+        (void)hipFree(slot->offsets);
+        (void)hipFree(slot->rgba);
+        slot->offsets = nullptr;
+        slot->rgba = nullptr;
+    }
+    if (m_gather != nullptr) {
+        (void)hipSetDevice(m_slots.front()->device);
+        (void)hipFree(m_gather);
+        m_gather = nullptr;
+    }
+}
+
+void Renderer::Configure(std::size_t width, std::size_t height) {
+    const std::size_t bands = m_slots.size();
+    const std::size_t band_rows = (height + bands - 1) / bands;
+    // Allocate everything new before releasing the old buffers (strong guarantee).
+    std::vector<float*> offs(bands, nullptr), outs(bands, nullptr);
+    float* gather = nullptr;
+    try {
+        for (std::size_t i = 0; i < bands; ++i) {
+            DeviceGuard guard(m_slots[i]->device);
+            offs[i] = DeviceAlloc<float>(band_rows * width * 2, "hipMalloc(band offsets)");
+            outs[i] = DeviceAlloc<float>(band_rows * width * 4, "hipMalloc(band framebuffer)");
+        }
+        if (m_use_rccl) {
+            DeviceGuard guard(m_slots.front()->device);
+            gather = DeviceAlloc<float>(bands * band_rows * width * 4, "hipMalloc(gather framebuffer)");
+        }
+    } catch (...) {
+        for (std::size_t i = 0; i < bands; ++i) {
+            (void)hipSetDevice(m_slots[i]->device);
+            (void)hipFree(offs[i]);
+            (void)hipFree(outs[i]);
+        }
+        (void)hipFree(gather);
+        throw;
+    }
+    ReleaseBuffers();
+    for (std::size_t i = 0; i < bands; ++i) {
+        Slot& s = *m_slots[i];
+        s.offsets = offs[i];
+        s.rgba = outs[i];
+        s.row_begin = std::min(height, i * band_rows);
+        s.row_count = std::min(height, (i + 1) * band_rows) - s.row_begin;
+    }
+    m_gather = gather;
+    m_width = width;
+    m_height = height;
+    m_band_rows = band_rows;
+}
+
+void Renderer::Render(const float* host_offsets, float* host_rgba) {
+    if (!configured()) {
+        throw std::runtime_error("Renderer used before Configure()");
+    }
+    const std::size_t w = m_width;
+    for (auto& sp : m_slots) {
+        Slot& s = *sp;
+        DeviceGuard guard(s.device);
+        if (s.row_count != 0) {
+            HipCheck(hipMemcpyAsync(s.offsets, host_offsets + s.row_begin * w * 2, s.row_count * w * 2 * sizeof(float),
+                                    hipMemcpyHostToDevice, s.stream),
+                     "hipMemcpyAsync(offsets H2D)");
+        }
+        s.scene->Prepare(w, m_height, s.stream);
+        s.scene->Trace(s.offsets, s.rgba, s.row_begin, s.row_count, m_variant, s.stream);
+    }
+    if (m_use_rccl) {
+        // Equal-size bands (the last one padded) gathered to the first device over xGMI;
+        // frame rows 0..H-1 are then the first H rows of the gather buffer.
+        NcclCheck(ncclGroupStart(), "ncclGroupStart");
+        for (std::size_t i = 0; i < m_slots.size(); ++i) {
+            Slot& s = *m_slots[i];
+            NcclCheck(ncclGather(s.rgba, i == 0 ? m_gather : nullptr, m_band_rows * w * 4, ncclFloat32, 0,
+                                 static_cast<ncclComm_t>(m_comms[i]), s.stream),
+                      "ncclGather");
+        }
+        NcclCheck(ncclGroupEnd(), "ncclGroupEnd");
+        Slot& root = *m_slots.front();
+        DeviceGuard guard(root.device);
+        HipCheck(hipMemcpyAsync(host_rgba, m_gather, m_height * w * 4 * sizeof(float), hipMemcpyDeviceToHost,
+                                root.stream),
+                 "hipMemcpyAsync(frame D2H)");
+    } else {
+        for (auto& sp : m_slots) {
+            Slot& s = *sp;
+            if (s.row_count == 0) {
+                continue;
+            }
+            DeviceGuard guard(s.device);
+            HipCheck(hipMemcpyAsync(host_rgba + s.row_begin * w * 4, s.rgba, s.row_count * w * 4 * sizeof(float),
+                                    hipMemcpyDeviceToHost, s.stream),
+                     "hipMemcpyAsync(band D2H)");
+        }
+    }
+    for (auto& sp : m_slots) {
+        DeviceGuard guard(sp->device);
+        HipCheck(hipStreamSynchronize(sp->stream), "render");
+    }
+}
+
+}  // namespace srt

@@ -1,0 +1,96 @@
+// Device side of an ml_model: per-GPU scene copies, row-band split, RCCL gather.
+//
+// Replaces the reference's compute layer (tensorflow::Session):
+// mlInfer -> Model::Infer -> Renderer::Render = H2D sample offsets per band -> prepare + trace
+// kernels per GPU -> ncclGather of the bands to the first GPU -> D2H into the output Image.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "scene.h"
+
+namespace srt {
+
+// Throws std::runtime_error("HIP error: <what>: <reason>") on failure.
+void HipCheck(hipError_t err, const char* what);
+
+// GPU list from env ML_VISIBLE_DEVICES ("0,1,2"; unset or empty = device 0). Validated
+// against hipGetDeviceCount; throws when no HIP device is present.
+std::vector<int> VisibleDevices();
+
+// One device's resident copy of a scene plus its edge-record buffer.
+class DeviceScene {
+public:
+    DeviceScene(const Scene& scene, int device);
+    ~DeviceScene();
+    DeviceScene(const DeviceScene&) = delete;
+    DeviceScene& operator=(const DeviceScene&) = delete;
+
+    int device() const { return m_device; }
+    std::uint64_t triangles() const { return m_n; }
+    const Camera& camera() const { return m_camera; }
+    const float* background() const { return m_background; }
+
+    // Edge setup for a W x H frame (stream-ordered). Records stay valid until the next call.
+    void Prepare(std::size_t width, std::size_t height, hipStream_t stream);
+    // Trace rows [row_begin, row_begin + row_count) of the prepared frame.
+    void Trace(const float* d_offsets, float* d_rgba, std::size_t row_begin, std::size_t row_count, int variant,
+               hipStream_t stream) const;
+
+    std::size_t width() const { return m_width; }
+    std::size_t height() const { return m_height; }
+
+private:
+    int m_device;
+    std::uint64_t m_n;
+    Camera m_camera;
+    float m_background[3];
+    float* m_vertices = nullptr;
+    float* m_albedo = nullptr;
+    float* m_edges = nullptr;
+    Frame m_frame{};
+    std::size_t m_width = 0;
+    std::size_t m_height = 0;
+};
+
+// Trace kernel variant from env SRT_TRACE_VARIANT ("lds" | "scalar", default lds).
+int TraceVariantFromEnv();
+
+class Renderer {
+public:
+    Renderer(const Scene& scene, std::vector<int> devices);
+    ~Renderer();
+    Renderer(const Renderer&) = delete;
+    Renderer& operator=(const Renderer&) = delete;
+
+    // (Re)allocate band buffers for a W x H frame. Strong guarantee: on failure the previous
+    // configuration is kept.
+    void Configure(std::size_t width, std::size_t height);
+    bool configured() const { return m_width != 0; }
+
+    // Render one frame: host offsets (H x W x 2) -> host RGBA (H x W x 4). Synchronous.
+    void Render(const float* host_offsets, float* host_rgba);
+
+    std::size_t bands() const { return m_slots.size(); }
+
+private:
+    struct Slot;
+    void ReleaseBuffers();
+
+    std::vector<std::unique_ptr<Slot>> m_slots;
+    std::vector<void*> m_comms;  // ncclComm_t per slot when gathering with RCCL
+    bool m_use_rccl = false;
+    int m_variant = 0;
+    std::size_t m_width = 0;
+    std::size_t m_height = 0;
+    std::size_t m_band_rows = 0;
+    float* m_gather = nullptr;  // root device: bands x band_rows x W x 4
+};
+
+}  // namespace srt

@@ -1,0 +1,143 @@
+// Extension C entry points (include/srt_render.h): scene files and device-level stages.
+#include <hip/hip_runtime.h>
+
+#include <exception>
+#include <string>
+
+#include "render.h"
+#include "renderer.h"
+#include "scene.h"
+#include "srt_render.h"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+template <class F>
+int Guarded(F&& f) {
+    try {
+        f();
+        g_last_error.clear();
+        return 0;
+    } catch (std::exception& e) {
+        g_last_error = e.what();
+    } catch (...) {
+        g_last_error = "unknown error";
+    }
+    return -1;
+}
+
+srt::DeviceScene* FromHandle(srt_device_scene s) { return reinterpret_cast<srt::DeviceScene*>(s); }
+
+// Binds the scene's device for the duration of a call, restoring the caller's device.
+class Bind {
+public:
+    explicit Bind(int device) {
+        if (hipGetDevice(&m_prev) != hipSuccess) {
+            m_prev = -1;
+        }
+        srt::HipCheck(hipSetDevice(device), "hipSetDevice");
+    }
+    ~Bind() {
+        if (m_prev >= 0) {
+            (void)hipSetDevice(m_prev);
+        }
+    }
+
+private:
+    int m_prev = -1;
+};
+
+}  // namespace
+
+extern "C" {
+
+ML_API_ENTRY const char* srtGetLastError(void) { return g_last_error.c_str(); }
+
+ML_API_ENTRY int srtWriteScene(const char* path, int kind, unsigned long long triangles, unsigned long long seed,
+                               float size) {
+    return Guarded([&] {
+        if (path == nullptr) {
+            throw std::runtime_error("Bad path argument");
+        }
+        srt::SaveScene(srt::MakeScene(kind, triangles, seed, size), path);
+    });
+}
+
+ML_API_ENTRY int srtSceneTriangles(const char* path, unsigned long long* triangles) {
+    return Guarded([&] {
+        if (path == nullptr || triangles == nullptr) {
+            throw std::runtime_error("Bad argument");
+        }
+        *triangles = srt::LoadScene(path).triangle_count();
+    });
+}
+
+ML_API_ENTRY int srtSceneFrame(const char* path, size_t width, size_t height, float* frame12) {
+    return Guarded([&] {
+        if (path == nullptr || frame12 == nullptr || width == 0 || height == 0) {
+            throw std::runtime_error("Bad argument");
+        }
+        const srt::Frame f = srt::MakeFrame(srt::LoadScene(path).camera, width, height);
+        for (int k = 0; k < 3; ++k) {
+            frame12[k] = f.origin[k];
+            frame12[3 + k] = f.base[k];
+            frame12[6 + k] = f.du[k];
+            frame12[9 + k] = f.dv[k];
+        }
+    });
+}
+
+ML_API_ENTRY srt_device_scene srtDeviceSceneCreate(const char* path, int device) {
+    srt::DeviceScene* out = nullptr;
+    Guarded([&] {
+        if (path == nullptr) {
+            throw std::runtime_error("Bad path argument");
+        }
+        const srt::Scene scene = srt::LoadScene(path);
+        int count = 0;
+        if (hipGetDeviceCount(&count) != hipSuccess || device < 0 || device >= count) {
+            throw std::runtime_error("HIP error: device " + std::to_string(device) + " not available (" +
+                                     std::to_string(count) + " present); this renderer has no CPU path");
+        }
+        out = new srt::DeviceScene(scene, device);
+    });
+    return reinterpret_cast<srt_device_scene>(out);
+}
+
+ML_API_ENTRY void srtDeviceSceneRelease(srt_device_scene scene) { delete FromHandle(scene); }
+
+ML_API_ENTRY unsigned long long srtDeviceSceneTriangles(srt_device_scene scene) {
+    return scene == nullptr ? 0ULL : FromHandle(scene)->triangles();
+}
+
+ML_API_ENTRY int srtPrepareAsync(srt_device_scene scene, size_t width, size_t height, void* stream) {
+    return Guarded([&] {
+        if (scene == nullptr) {
+            throw std::runtime_error("Bad scene handle");
+        }
+        srt::DeviceScene* s = FromHandle(scene);
+        Bind bind(s->device());
+        s->Prepare(width, height, static_cast<hipStream_t>(stream));
+    });
+}
+
+ML_API_ENTRY int srtTraceAsync(srt_device_scene scene, const float* d_offsets, float* d_rgba, size_t row_begin,
+                               size_t row_count, int variant, void* stream) {
+    return Guarded([&] {
+        if (scene == nullptr) {
+            throw std::runtime_error("Bad scene handle");
+        }
+        if ((d_offsets == nullptr || d_rgba == nullptr) && row_count != 0) {
+            throw std::runtime_error("Bad buffer argument");
+        }
+        if (variant != SRT_TRACE_LDS && variant != SRT_TRACE_SCALAR) {
+            throw std::runtime_error("Unknown trace variant " + std::to_string(variant));
+        }
+        srt::DeviceScene* s = FromHandle(scene);
+        Bind bind(s->device());
+        s->Trace(d_offsets, d_rgba, row_begin, row_count, variant, static_cast<hipStream_t>(stream));
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,110 @@
+"""Scene files and the device-level render stages (include/srt_render.h).
+
+``DeviceScene`` keeps a scene resident on one GPU and launches the two stages on a caller's
+HIP stream with caller-owned device buffers (torch tensors or raw pointers):
+
+    scene = DeviceScene(path, device=0)
+    scene.prepare(W, H, stream)                                  # edge records
+    scene.trace(offsets, rgba, row_begin, row_count, stream=s)   # closest hit + shade
+
+This is the path bench.py times (inputs resident in HBM) and the one-process-per-GPU
+band renderer uses; ``runner.render`` is the host-image ml* path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+from . import _native
+from ._native import SRT_SCENE_CORNELL, SRT_SCENE_SOUP, SRT_SCENE_TRIANGLE, SRT_TRACE_LDS, SRT_TRACE_SCALAR
+
+SCENE_KINDS = {"triangle": SRT_SCENE_TRIANGLE, "cornell": SRT_SCENE_CORNELL, "soup": SRT_SCENE_SOUP}
+TRACE_VARIANTS = {"lds": SRT_TRACE_LDS, "scalar": SRT_TRACE_SCALAR}
+SOUP_SEED = 0x5EED  # 100k soup seed; the 1M soup uses SOUP_SEED + 1
+
+
+class SrtError(RuntimeError):
+    pass
+
+
+def _check(rc: int):
+    if rc != 0:
+        raise SrtError(_native.last_error())
+
+
+def write_scene(path: str, kind: str = "soup", triangles: int = 100_000, seed: int | None = None,
+                size: float = 0.0) -> str:
+    """Write a generated scene file; returns ``path``."""
+    if seed is None:
+        seed = SOUP_SEED + (1 if triangles >= 1_000_000 else 0)
+    _check(_native.lib().srtWriteScene(os.fsencode(path), SCENE_KINDS[kind], triangles, seed, size))
+    return path
+
+
+def scene_triangles(path: str) -> int:
+    n = ctypes.c_ulonglong()
+    _check(_native.lib().srtSceneTriangles(os.fsencode(path), ctypes.byref(n)))
+    return n.value
+
+
+def scene_frame(path: str, width: int, height: int):
+    """(origin, base, du, dv) float32 triples of the affine primary-ray frame."""
+    out = (ctypes.c_float * 12)()
+    _check(_native.lib().srtSceneFrame(os.fsencode(path), width, height, out))
+    vals = list(out)
+    return tuple(tuple(vals[3 * k:3 * k + 3]) for k in range(4))
+
+
+def _ptr(x) -> int:
+    if x is None:
+        return 0
+    if hasattr(x, "data_ptr"):
+        return x.data_ptr()
+    return int(x)
+
+
+def _stream(s) -> int:
+    if s is None:
+        return 0
+    if hasattr(s, "cuda_stream"):
+        return s.cuda_stream
+    return int(s)
+
+
+class DeviceScene:
+    """A scene resident on one HIP device."""
+
+    def __init__(self, path: str, device: int = 0):
+        self._lib = _native.lib()
+        self.handle = self._lib.srtDeviceSceneCreate(os.fsencode(path), device)
+        if not self.handle:
+            raise SrtError(_native.last_error())
+        self.device = device
+        self.triangles = self._lib.srtDeviceSceneTriangles(self.handle)
+        self.width = 0
+        self.height = 0
+
+    def prepare(self, width: int, height: int, stream=None):
+        _check(self._lib.srtPrepareAsync(self.handle, width, height, _stream(stream)))
+        self.width, self.height = width, height
+
+    def trace(self, offsets, rgba, row_begin: int = 0, row_count: int | None = None, variant: str = "lds",
+              stream=None):
+        """offsets: (rows, W, 2) float32 device buffer; rgba: (rows, W, 4) float32 device buffer."""
+        if row_count is None:
+            row_count = self.height - row_begin
+        for name, buf, ch in (("offsets", offsets, 2), ("rgba", rgba, 4)):
+            if hasattr(buf, "shape") and tuple(buf.shape) != (row_count, self.width, ch):
+                raise ValueError(f"{name} must be {(row_count, self.width, ch)}, got {tuple(buf.shape)}")
+            if hasattr(buf, "is_contiguous") and not buf.is_contiguous():
+                raise ValueError(f"{name} must be contiguous")
+        _check(self._lib.srtTraceAsync(self.handle, _ptr(offsets), _ptr(rgba), row_begin, row_count,
+                                       TRACE_VARIANTS[variant], _stream(stream)))
+
+    def close(self):
+        if self.handle:
+            self._lib.srtDeviceSceneRelease(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        self.close()
