@@ -82,15 +82,31 @@ _SIGNATURES = {
 _lib = None
 
 
+def _share_torch_hip_runtime():
+    """Load torch's HIP runtime first when torch is installed.
+
+    torch ships its own libamdhip64.so / libhsa-runtime64.so / librccl.so with the same
+    SONAMEs (libamdhip64.so.7, ...) as /opt/rocm. If torch is imported first, the dynamic
+    loader satisfies this library's NEEDED entries with torch's copies, so the process has ONE
+    HIP runtime and torch streams/pointers passed to srt* calls belong to it. Loading this
+    library first would pull /opt/rocm's copies, and torch would then load a second runtime.
+    """
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
 def lib() -> ctypes.CDLL:
     """Load libModelRunner.so once; raise loudly if it has not been built."""
     global _lib
     if _lib is None:
+        _share_torch_hip_runtime()
         if not LIB_PATH.exists():
             raise RuntimeError(
                 f"{LIB_PATH} is missing: build the HIP library first (`make` at the repo root or "
                 "`python -c 'import __graft_entry__ as g; g.build()'`); there is no CPU fallback")
-        handle = ctypes.CDLL(os.fspath(LIB_PATH), mode=ctypes.RTLD_GLOBAL)
+        handle = ctypes.CDLL(os.fspath(LIB_PATH))
         for name, (restype, argtypes) in _SIGNATURES.items():
             fn = getattr(handle, name)
             fn.restype = restype
