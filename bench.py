@@ -37,7 +37,7 @@ def parse():
     p.add_argument("--height", type=int, default=1080)
     p.add_argument("--scene", default="soup", choices=["soup", "cornell", "triangle"])
     p.add_argument("--triangles", type=int, default=100_000)
-    p.add_argument("--variant", default=os.environ.get("SRT_BENCH_VARIANT", "lds"), choices=["lds", "scalar"])
+    p.add_argument("--variant", default=os.environ.get("SRT_BENCH_VARIANT", "lds"), choices=["lds", "scalar", "cull"])
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample length")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive ml* API measurement")
@@ -193,6 +193,7 @@ def main():
                 "spp": 1,
                 "parallelism": f"row-bands x{world}" + (" + RCCL gather" if world > 1 else ""),
                 "trace_variant": a.variant,
+                "cull_shape": os.environ.get("SRT_CULL_SHAPE", "16x8x2") if a.variant == "cull" else None,
             },
             "roofline": {
                 "bound": "hbm",
@@ -201,7 +202,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
                 "traffic": pmc_traffic(wl, a.variant),
-                "kernel": "TraceLdsKernel" if a.variant == "lds" else "TraceScalarKernel",
+                "kernel": {"lds": "TraceLdsKernel", "scalar": "TraceScalarKernel", "cull": "TraceCullKernel"}[a.variant],
                 "kernel_ms": round(trace_ms, 4),
                 "bytes_per_launch": alg_bytes,
                 "note": "north_star HBM roofline: 36 B/triangle/ray + 24 B/ray; LDS tiling re-uses each "

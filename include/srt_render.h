@@ -27,6 +27,7 @@ extern "C" {
 /* Trace kernel variants for srtTraceAsync. */
 #define SRT_TRACE_LDS 0
 #define SRT_TRACE_SCALAR 1
+#define SRT_TRACE_CULL 2 /* hierarchical block/lane/ray cull; bit-identical output */
 
 ML_API_ENTRY const char* srtGetLastError(void);
 

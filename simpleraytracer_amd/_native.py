@@ -23,6 +23,7 @@ SRT_SCENE_CORNELL = 1
 SRT_SCENE_SOUP = 2
 SRT_TRACE_LDS = 0
 SRT_TRACE_SCALAR = 1
+SRT_TRACE_CULL = 2
 
 
 class ImageInfo(ctypes.Structure):

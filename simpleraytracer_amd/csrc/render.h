@@ -17,23 +17,33 @@
 
 namespace srt {
 
-// Triangles per LDS tile; the edge buffer is padded to a multiple of this with disabled
-// (all-NaN) records so the trace loop has no tail.
+// Triangles per edge tile. The edge buffer is padded with disabled (all-NaN) records to a
+// multiple of kPadTriangles (the largest cull step: 512 threads x 4 records) so no trace
+// loop has a tail; the per-ray variants stop after the last tile holding a real record.
 constexpr int kTileTriangles = 256;
+constexpr int kPadTriangles = 2048;
 
-// Edge record layout: 3 x float4 per triangle.
-//   [0] = (c0A, cxA, cyA, c0B)   [1] = (cxB, cyB, c0C, cxC)   [2] = (cyC, vol, 0, 0)
+// Edge records, tile-planar: tile t (256 records, 10 KiB) = four planes, each indexed by the
+// record's position j in the tile, so a lane-per-record load is one coalesced 16-B or 4-B
+// access per plane and an LDS copy of the tile is a straight 10 KiB memcpy.
+//   plane 0: float4[256] (c0A, cxA, cyA, c0B)
+//   plane 1: float4[256] (cxB, cyB, c0C, cxC)
+//   plane 2: float [256] cyC
+//   plane 3: float [256] vol
 // E_k(fx, fy) = fma(fy, cy_k, fma(fx, cx_k, c0_k)) for the three edges k = A, B, C.
-constexpr int kEdgeFloat4PerTriangle = 3;
+constexpr int kTileFloat4 = kTileTriangles * 5 / 2;  // 640 float4 = 10 KiB per tile
+constexpr int kEdgeFloatsPerTriangle = 10;
 
 inline std::uint64_t PaddedTriangleCount(std::uint64_t n) {
-    return (n + kTileTriangles - 1) / kTileTriangles * kTileTriangles;
+    const std::uint64_t p = (n + kPadTriangles - 1) / kPadTriangles * kPadTriangles;
+    return p == 0 ? kPadTriangles : p;
 }
 
 // Trace kernel variants (DESIGN.md "Kernels"); selectable for A/B measurement.
 enum TraceVariant : int {
-    kTraceLds = 0,     // LDS-tiled triangle stream, 4 waves x 8 rows per lane (default)
+    kTraceLds = 0,     // LDS-tiled triangle stream, every ray tests every record
     kTraceScalar = 1,  // wave-uniform scalar-cache triangle stream, no LDS, 1 wave per block
+    kTraceCull = 2,    // hierarchical: block-box cull of every record, compacted survivors in LDS
 };
 
 struct BandArgs {
@@ -45,7 +55,7 @@ struct BandArgs {
     std::size_t row_count;
 };
 
-// Launch the prepare kernel: writes PaddedTriangleCount(n) x 3 float4 into `edges`.
+// Launch the prepare kernel: writes PaddedTriangleCount(n) / kTileTriangles tiles into `edges`.
 hipError_t LaunchPrepare(const float* d_vertices, std::uint64_t n, const Frame& frame, float* d_edges,
                          hipStream_t stream);
 

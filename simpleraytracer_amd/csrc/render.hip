@@ -6,13 +6,15 @@
 #include "render.h"
 
 #include <cmath>
+#include <cstdlib>
+#include <cstring>
 
 namespace srt {
 namespace {
 
 constexpr int kWave = 64;
 constexpr int kLdsWaves = 4;     // waves per block in the LDS variant
-constexpr int kRowsPerLane = 8;  // rays per lane: one image column, 8 consecutive rows
+constexpr int kRowsPerLane = 8;  // rays per lane (LDS / scalar variants): one column, 8 rows
 
 struct TraceParams {
     const float4* __restrict__ edges;
@@ -20,7 +22,8 @@ struct TraceParams {
     const float* __restrict__ albedo;
     const float2* __restrict__ offsets;
     float4* __restrict__ out;
-    unsigned n_pad;
+    unsigned n_pad;   // records in the edge buffer (multiple of kPadTriangles)
+    unsigned n_tiles; // tiles holding at least one real record (>= 1)
     int width;
     int row_count;
     int row_begin;
@@ -43,6 +46,11 @@ struct PrepareParams {
     float dv[3];
 };
 
+// One edge record as the trace kernels consume it.
+struct Record {
+    float c0A, cxA, cyA, c0B, cxB, cyB, c0C, cxC, cyC;
+};
+
 __device__ __forceinline__ float Dot3(float ax, float ay, float az, float bx, float by, float bz) {
     return fmaf(az, bz, fmaf(ay, by, ax * bx));
 }
@@ -54,6 +62,14 @@ __device__ __forceinline__ void Cross3(float ax, float ay, float az, float bx, f
     cz = ax * by - ay * bx;
 }
 
+// Plane addresses of record j of the tile starting at `tile` (render.h "tile-planar").
+__device__ __forceinline__ const float* Plane2(const float4* tile) {
+    return reinterpret_cast<const float*>(tile + 2 * kTileTriangles);
+}
+__device__ __forceinline__ const float* Plane3(const float4* tile) {
+    return reinterpret_cast<const float*>(tile + 2 * kTileTriangles) + kTileTriangles;
+}
+
 // One thread per triangle: origin-relative edge normals nA = B x C, nB = C x A, nC = A x B
 // (A, B, C = vertices - eye), signed volume vol = A . nA, orientation normalised so vol > 0,
 // then each normal projected onto the affine ray frame: E(fx, fy) = n . (base + fx du + fy dv).
@@ -62,47 +78,53 @@ __global__ __launch_bounds__(256) void PrepareKernel(PrepareParams p) {
     if (i >= p.n_pad) {
         return;
     }
-    float4* rec = p.edges + 3ull * i;
+    float4* tile = p.edges + static_cast<size_t>(i / kTileTriangles) * kTileFloat4;
+    const unsigned j = i % kTileTriangles;
+    float* p2 = reinterpret_cast<float*>(tile + 2 * kTileTriangles);
+    float* p3 = p2 + kTileTriangles;
     const float qnan = __builtin_nanf("");
-    if (i >= p.n) {
-        rec[0] = make_float4(qnan, qnan, qnan, qnan);
-        rec[1] = make_float4(qnan, qnan, qnan, qnan);
-        rec[2] = make_float4(qnan, qnan, 0.f, 0.f);
-        return;
+    bool disabled = i >= p.n;
+    float c[9];
+    float vol = qnan;
+    if (!disabled) {
+        const float* v = p.vertices + 9ull * i;
+        const float ax = v[0] - p.origin[0], ay = v[1] - p.origin[1], az = v[2] - p.origin[2];
+        const float bx = v[3] - p.origin[0], by = v[4] - p.origin[1], bz = v[5] - p.origin[2];
+        const float cx = v[6] - p.origin[0], cy = v[7] - p.origin[1], cz = v[8] - p.origin[2];
+        float n[9];
+        Cross3(bx, by, bz, cx, cy, cz, n[0], n[1], n[2]);
+        Cross3(cx, cy, cz, ax, ay, az, n[3], n[4], n[5]);
+        Cross3(ax, ay, az, bx, by, bz, n[6], n[7], n[8]);
+        vol = Dot3(ax, ay, az, n[0], n[1], n[2]);
+        disabled = !(std::isfinite(vol) && vol != 0.f);
+        if (!disabled) {
+            if (vol < 0.f) {
+#pragma unroll
+                for (int k = 0; k < 9; ++k) {
+                    n[k] = -n[k];
+                }
+                vol = -vol;
+            }
+#pragma unroll
+            for (int e = 0; e < 3; ++e) {
+                const float nx = n[3 * e], ny = n[3 * e + 1], nz = n[3 * e + 2];
+                c[3 * e + 0] = Dot3(nx, ny, nz, p.base[0], p.base[1], p.base[2]);
+                c[3 * e + 1] = Dot3(nx, ny, nz, p.du[0], p.du[1], p.du[2]);
+                c[3 * e + 2] = Dot3(nx, ny, nz, p.dv[0], p.dv[1], p.dv[2]);
+            }
+        }
     }
-    const float* v = p.vertices + 9ull * i;
-    const float ax = v[0] - p.origin[0], ay = v[1] - p.origin[1], az = v[2] - p.origin[2];
-    const float bx = v[3] - p.origin[0], by = v[4] - p.origin[1], bz = v[5] - p.origin[2];
-    const float cx = v[6] - p.origin[0], cy = v[7] - p.origin[1], cz = v[8] - p.origin[2];
-    float n[9];
-    Cross3(bx, by, bz, cx, cy, cz, n[0], n[1], n[2]);
-    Cross3(cx, cy, cz, ax, ay, az, n[3], n[4], n[5]);
-    Cross3(ax, ay, az, bx, by, bz, n[6], n[7], n[8]);
-    float vol = Dot3(ax, ay, az, n[0], n[1], n[2]);
-    if (!(std::isfinite(vol) && vol != 0.f)) {
-        rec[0] = make_float4(qnan, qnan, qnan, qnan);
-        rec[1] = make_float4(qnan, qnan, qnan, qnan);
-        rec[2] = make_float4(qnan, qnan, 0.f, 0.f);
-        return;
-    }
-    if (vol < 0.f) {
+    if (disabled) {
 #pragma unroll
         for (int k = 0; k < 9; ++k) {
-            n[k] = -n[k];
+            c[k] = qnan;
         }
-        vol = -vol;
+        vol = qnan;
     }
-    float c[9];
-#pragma unroll
-    for (int e = 0; e < 3; ++e) {
-        const float nx = n[3 * e], ny = n[3 * e + 1], nz = n[3 * e + 2];
-        c[3 * e + 0] = Dot3(nx, ny, nz, p.base[0], p.base[1], p.base[2]);
-        c[3 * e + 1] = Dot3(nx, ny, nz, p.du[0], p.du[1], p.du[2]);
-        c[3 * e + 2] = Dot3(nx, ny, nz, p.dv[0], p.dv[1], p.dv[2]);
-    }
-    rec[0] = make_float4(c[0], c[1], c[2], c[3]);
-    rec[1] = make_float4(c[4], c[5], c[6], c[7]);
-    rec[2] = make_float4(c[8], vol, 0.f, 0.f);
+    tile[j] = make_float4(c[0], c[1], c[2], c[3]);
+    tile[kTileTriangles + j] = make_float4(c[4], c[5], c[6], c[7]);
+    p2[j] = c[8];
+    p3[j] = vol;
 }
 
 // Per-lane ray state: R rays sharing one image column.
@@ -114,7 +136,25 @@ struct Rays {
     int bi[R];    // closest triangle id (-1 = miss)
 };
 
-// Test one triangle's edge record against the lane's R rays.
+// Axis-aligned box in image-position space (fx, fy) containing a set of rays.
+struct Box {
+    float xlo, xhi, ylo, yhi;
+};
+
+// Conservative rejection of a record for every ray whose (fx, fy) lies in the box.
+// E_k = fma(fy, cy, fma(fx, cx, c0)) is monotone in fx (sign of cx) and in fy (sign of cy),
+// because a correctly rounded fma is monotone in each argument; so its maximum over the box
+// is attained at the corner picked by the signs, and a ray in the box can pass the exact
+// test (all E_k >= 0) only if no corner value is < 0. NaN corner values never reject.
+// Exact: a rejected record fails the exact test for every ray of the box, bit for bit.
+__device__ __forceinline__ bool BoxMayHit(const Box& b, const Record& q) {
+    const float eA = fmaf(q.cyA >= 0.f ? b.yhi : b.ylo, q.cyA, fmaf(q.cxA >= 0.f ? b.xhi : b.xlo, q.cxA, q.c0A));
+    const float eB = fmaf(q.cyB >= 0.f ? b.yhi : b.ylo, q.cyB, fmaf(q.cxB >= 0.f ? b.xhi : b.xlo, q.cxB, q.c0B));
+    const float eC = fmaf(q.cyC >= 0.f ? b.yhi : b.ylo, q.cyC, fmaf(q.cxC >= 0.f ? b.xhi : b.xlo, q.cxC, q.c0C));
+    return !(eA < 0.f || eB < 0.f || eC < 0.f);
+}
+
+// Test one triangle's edge record against the lane's R rays (brute force: every ray).
 //   hot path:  E_A, E_B, E_C for every ray, candidate iff min(E) >= 0 for some ray
 //              (one branch per triangle per wave; candidates are rare)
 //   slow path: exact test per ray: all E >= 0, det = (E_A + E_B) + E_C > 0, t = vol / det,
@@ -122,12 +162,11 @@ struct Rays {
 // SHARED: every ray of the lane has the same fx bit pattern, so fma(fx, cx, c0) is one
 // value per edge (common-subexpression elimination; the result is bit-identical).
 template <int R, bool SHARED>
-__device__ __forceinline__ void TestTriangle(Rays<R>& s, float c0A, float cxA, float cyA, float c0B, float cxB,
-                                             float cyB, float c0C, float cxC, float cyC, unsigned id,
-                                             const float* vol_ptr) {
+__device__ __forceinline__ void TestTriangle(Rays<R>& s, const Record& q, unsigned id, const float* vol_ptr) {
     float gA[R], gB[R], gC[R];
     if constexpr (SHARED) {
-        const float a = fmaf(s.fx[0], cxA, c0A), b = fmaf(s.fx[0], cxB, c0B), c = fmaf(s.fx[0], cxC, c0C);
+        const float a = fmaf(s.fx[0], q.cxA, q.c0A), b = fmaf(s.fx[0], q.cxB, q.c0B),
+                    c = fmaf(s.fx[0], q.cxC, q.c0C);
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             gA[r] = a;
@@ -137,17 +176,17 @@ __device__ __forceinline__ void TestTriangle(Rays<R>& s, float c0A, float cxA, f
     } else {
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            gA[r] = fmaf(s.fx[r], cxA, c0A);
-            gB[r] = fmaf(s.fx[r], cxB, c0B);
-            gC[r] = fmaf(s.fx[r], cxC, c0C);
+            gA[r] = fmaf(s.fx[r], q.cxA, q.c0A);
+            gB[r] = fmaf(s.fx[r], q.cxB, q.c0B);
+            gC[r] = fmaf(s.fx[r], q.cxC, q.c0C);
         }
     }
     float m[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        const float eA = fmaf(s.fy[r], cyA, gA[r]);
-        const float eB = fmaf(s.fy[r], cyB, gB[r]);
-        const float eC = fmaf(s.fy[r], cyC, gC[r]);
+        const float eA = fmaf(s.fy[r], q.cyA, gA[r]);
+        const float eB = fmaf(s.fy[r], q.cyB, gB[r]);
+        const float eC = fmaf(s.fy[r], q.cyC, gC[r]);
         m[r] = fminf(fminf(eA, eB), eC);
     }
     // max-tree over the rays (NaN edges from disabled records drop out of fmaxf)
@@ -162,9 +201,9 @@ __device__ __forceinline__ void TestTriangle(Rays<R>& s, float c0A, float cxA, f
         const float vol = *vol_ptr;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            const float eA = fmaf(s.fy[r], cyA, gA[r]);
-            const float eB = fmaf(s.fy[r], cyB, gB[r]);
-            const float eC = fmaf(s.fy[r], cyC, gC[r]);
+            const float eA = fmaf(s.fy[r], q.cyA, gA[r]);
+            const float eB = fmaf(s.fy[r], q.cyB, gB[r]);
+            const float eC = fmaf(s.fy[r], q.cyC, gC[r]);
             if (eA >= 0.f && eB >= 0.f && eC >= 0.f) {
                 const float det = (eA + eB) + eC;
                 if (det > 0.f) {
@@ -179,12 +218,38 @@ __device__ __forceinline__ void TestTriangle(Rays<R>& s, float c0A, float cxA, f
     }
 }
 
-// Ray generation: lane owns column x, rows y0..y0+R-1 of the band (clamped for edge lanes;
-// clamped lanes compute but never store).
+// Exact test of one record against every ray of the lane, for records arriving in any
+// order: keeps the lexicographic minimum of (t, id), which equals the ascending-id strict-<
+// result of TestTriangle (smallest t; among equal t the lowest id).
 template <int R>
-__device__ __forceinline__ bool GenerateRays(const TraceParams& p, int x, int y0, Rays<R>& s) {
+__device__ __forceinline__ void ExactTestAnyOrder(Rays<R>& s, const Record& q, float vol, int id) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const float eA = fmaf(s.fy[r], q.cyA, fmaf(s.fx[r], q.cxA, q.c0A));
+        const float eB = fmaf(s.fy[r], q.cyB, fmaf(s.fx[r], q.cxB, q.c0B));
+        const float eC = fmaf(s.fy[r], q.cyC, fmaf(s.fx[r], q.cxC, q.c0C));
+        if (eA >= 0.f && eB >= 0.f && eC >= 0.f) {
+            const float det = (eA + eB) + eC;
+            if (det > 0.f) {
+                const float t = vol / det;
+                if (t < s.bt[r] || (t == s.bt[r] && id < s.bi[r])) {
+                    s.bt[r] = t;
+                    s.bi[r] = id;
+                }
+            }
+        }
+    }
+}
+
+// Ray generation: lane owns column x, rows y0..y0+R-1 of the band (clamped for edge lanes;
+// clamped lanes compute but never store). Returns whether all R rays share fx's bit
+// pattern; `box` receives the rays' (fx, fy) bounding box (NaN positions drop out: a ray
+// with a NaN position fails every test).
+template <int R>
+__device__ __forceinline__ bool GenerateRays(const TraceParams& p, int x, int y0, Rays<R>& s, Box& box) {
     const int xc = min(x, p.width - 1);
     bool same = true;
+    box = Box{__builtin_inff(), -__builtin_inff(), __builtin_inff(), -__builtin_inff()};
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const int yc = min(y0 + r, p.row_count - 1);
@@ -194,6 +259,10 @@ __device__ __forceinline__ bool GenerateRays(const TraceParams& p, int x, int y0
         s.bt[r] = __builtin_inff();
         s.bi[r] = -1;
         same = same && (__float_as_uint(s.fx[r]) == __float_as_uint(s.fx[0]));
+        box.xlo = fminf(box.xlo, s.fx[r]);
+        box.xhi = fmaxf(box.xhi, s.fx[r]);
+        box.ylo = fminf(box.ylo, s.fy[r]);
+        box.yhi = fmaxf(box.yhi, s.fy[r]);
     }
     return same;
 }
@@ -237,39 +306,41 @@ __device__ __forceinline__ void ShadeAndStore(const TraceParams& p, int x, int y
 }
 
 // ---------------------------------------------------------------------------------------
-// Variant 0: LDS-tiled. Block = 4 waves = 64 columns x 32 rows. Each tile of 256 edge
-// records (12 KB) is loaded by the whole block with coalesced 16-B loads into one half of a
-// double-buffered LDS ring (24 KB), then every wave walks it with broadcast LDS reads.
-// One barrier per tile; the next tile's global loads are in flight during the current one.
+// Variant 0: LDS-tiled brute force. Block = 4 waves = 64 columns x 32 rows. Each 10 KiB
+// tile of edge records is copied by the whole block into one half of a double-buffered LDS
+// ring, then every wave walks it with broadcast LDS reads: every ray tests every record.
+// One barrier per tile; the next tile's copy is in flight during the current one.
 // ---------------------------------------------------------------------------------------
 using LdsVoidPtr = __attribute__((address_space(3))) void*;
 
-// Copy one 12 KB tile of edge records global -> LDS with LDS-DMA (global_load_lds_dwordx4):
-// 12 wave-instructions of 1 KiB per tile, 3 per wave, no VGPR staging; the LDS image is the
-// global image (lane-linear). Issued through inline asm so hipcc does not drain it with a
-// vmcnt(0) in front of every ds_read of the tile being computed (cdna_hip_programming.md
-// section 5 "Pipelining across barriers"); completion is waited for by WaitTile().
+// Copy one 10 KiB tile global -> LDS with LDS-DMA (global_load_lds_dwordx4): 10 wave-
+// instructions of 1 KiB, spread over the block's waves, no VGPR staging; the LDS image is
+// the global image. Issued through inline asm so hipcc does not drain it with a vmcnt(0) in
+// front of every ds_read of the tile being computed (cdna_hip_programming.md section 5
+// "Pipelining across barriers"); completion is waited for by WaitTile().
 __device__ __forceinline__ void StageTile(const float4* __restrict__ src, float4* dst) {
-    constexpr int kTileF4 = kTileTriangles * 3;
-    constexpr int kPerWave = kTileF4 / (kWave * kLdsWaves);
+    constexpr int kChunks = kTileFloat4 / kWave;  // 10
     const int lane = threadIdx.x & (kWave - 1);
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
 #pragma unroll
-    for (int k = 0; k < kPerWave; ++k) {
-        const int chunk = (wave * kPerWave + k) * kWave;
-        const float4* gsrc = src + chunk + lane;
-        const unsigned lds_dst = __builtin_amdgcn_readfirstlane(
-            static_cast<unsigned>(reinterpret_cast<size_t>((LdsVoidPtr)(void*)(dst + chunk))));
-        unsigned keep;
-        asm volatile(
-            "s_mov_b32 %0, m0\n\t"
-            "s_mov_b32 m0, %2\n\t"
-            "s_nop 0\n\t"
-            "global_load_lds_dwordx4 %1, off\n\t"
-            "s_mov_b32 m0, %0"
-            : "=&s"(keep)
-            : "v"(gsrc), "s"(lds_dst)
-            : "memory");
+    for (int k = 0; k < (kChunks + kLdsWaves - 1) / kLdsWaves; ++k) {
+        const int c = wave + k * kLdsWaves;
+        if (c < kChunks) {
+            const int chunk = c * kWave;
+            const float4* gsrc = src + chunk + lane;
+            const unsigned lds_dst = __builtin_amdgcn_readfirstlane(
+                static_cast<unsigned>(reinterpret_cast<size_t>((LdsVoidPtr)(void*)(dst + chunk))));
+            unsigned keep;
+            asm volatile(
+                "s_mov_b32 %0, m0\n\t"
+                "s_mov_b32 m0, %2\n\t"
+                "s_nop 0\n\t"
+                "global_load_lds_dwordx4 %1, off\n\t"
+                "s_mov_b32 m0, %0"
+                : "=&s"(keep)
+                : "v"(gsrc), "s"(lds_dst)
+                : "memory");
+        }
     }
 }
 
@@ -281,24 +352,24 @@ __device__ __forceinline__ void WaitTile() {
 
 template <int R, bool SHARED>
 __device__ __forceinline__ void WalkTilesLds(const TraceParams& p, float4* lds, Rays<R>& s) {
-    constexpr int kTileF4 = kTileTriangles * 3;
-    static_assert(kTileF4 % (kWave * kLdsWaves) == 0, "tile must split evenly over the block");
-    const unsigned ntiles = p.n_pad / kTileTriangles;
+    const unsigned ntiles = p.n_tiles;
     StageTile(p.edges, lds);
     for (unsigned t = 0; t < ntiles; ++t) {
         const unsigned buf = t & 1u;
         WaitTile();  // tile t landed; every wave is done with tile t-1 (the buffer refilled next)
         if (t + 1 < ntiles) {
-            StageTile(p.edges + static_cast<size_t>(t + 1) * kTileF4, lds + (buf ^ 1u) * kTileF4);
+            StageTile(p.edges + static_cast<size_t>(t + 1) * kTileFloat4, lds + (buf ^ 1u) * kTileFloat4);
         }
-        const float4* tile = lds + buf * kTileF4;
+        const float4* tile = lds + buf * kTileFloat4;
+        const float* p2 = Plane2(tile);
+        const float* p3 = Plane3(tile);
         const unsigned id0 = t * kTileTriangles;
 #pragma unroll 2
         for (int j = 0; j < kTileTriangles; ++j) {
-            const float4 q0 = tile[3 * j];
-            const float4 q1 = tile[3 * j + 1];
-            const float* q2 = reinterpret_cast<const float*>(tile + 3 * j + 2);
-            TestTriangle<R, SHARED>(s, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2[0], id0 + j, q2 + 1);
+            const float4 q0 = tile[j];
+            const float4 q1 = tile[kTileTriangles + j];
+            const Record q{q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, p2[j]};
+            TestTriangle<R, SHARED>(s, q, id0 + j, p3 + j);
         }
     }
 }
@@ -307,16 +378,17 @@ __global__ __launch_bounds__(kWave * kLdsWaves) void TraceLdsKernel(TraceParams 
     // ONE __shared__ object: the double-buffered tile ring plus one flag word at the end
     // (a second LDS object next to LDS-DMA staging makes hipcc wait vmcnt(0) before every
     // ds_read; cdna_hip_programming.md section 5 trap 4(a)).
-    __shared__ float4 lds[2 * kTileTriangles * 3 + 1];
+    __shared__ float4 lds[2 * kTileFloat4 + 1];
     constexpr int R = kRowsPerLane;
     const int lane = threadIdx.x & (kWave - 1);
     const int wave = threadIdx.x / kWave;
     const int x = blockIdx.x * kWave + lane;
     const int y0 = (blockIdx.y * kLdsWaves + wave) * R;
     Rays<R> s;
-    const bool same = GenerateRays<R>(p, x, y0, s);
+    Box box;
+    const bool same = GenerateRays<R>(p, x, y0, s, box);
     // Block-uniform choice of loop body (both bodies hold the same barriers).
-    unsigned* flag = reinterpret_cast<unsigned*>(lds + 2 * kTileTriangles * 3);
+    unsigned* flag = reinterpret_cast<unsigned*>(lds + 2 * kTileFloat4);
     if (threadIdx.x == 0) {
         *flag = 1u;
     }
@@ -340,11 +412,18 @@ __global__ __launch_bounds__(kWave * kLdsWaves) void TraceLdsKernel(TraceParams 
 // ---------------------------------------------------------------------------------------
 template <int R, bool SHARED>
 __device__ __forceinline__ void WalkScalar(const TraceParams& p, Rays<R>& s) {
-    const float* e = reinterpret_cast<const float*>(p.edges);
+    const unsigned ntiles = p.n_tiles;
+    for (unsigned t = 0; t < ntiles; ++t) {
+        const float4* tile = p.edges + static_cast<size_t>(t) * kTileFloat4;
+        const float* p2 = Plane2(tile);
+        const float* p3 = Plane3(tile);
 #pragma unroll 4
-    for (unsigned j = 0; j < p.n_pad; ++j) {
-        const float* q = e + 12ull * j;
-        TestTriangle<R, SHARED>(s, q[0], q[1], q[2], q[3], q[4], q[5], q[6], q[7], q[8], j, q + 9);
+        for (int j = 0; j < kTileTriangles; ++j) {
+            const float4 q0 = tile[j];
+            const float4 q1 = tile[kTileTriangles + j];
+            const Record q{q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, p2[j]};
+            TestTriangle<R, SHARED>(s, q, t * kTileTriangles + j, p3 + j);
+        }
     }
 }
 
@@ -353,13 +432,180 @@ __global__ __launch_bounds__(kWave) void TraceScalarKernel(TraceParams p) {
     const int x = blockIdx.x * kWave + static_cast<int>(threadIdx.x);
     const int y0 = blockIdx.y * R;
     Rays<R> s;
-    const bool same = GenerateRays<R>(p, x, y0, s);
+    Box box;
+    const bool same = GenerateRays<R>(p, x, y0, s, box);
     if (__all(same)) {
         WalkScalar<R, true>(p, s);
     } else {
         WalkScalar<R, false>(p, s);
     }
     ShadeAndStore<R>(p, x, y0, s);
+}
+
+// ---------------------------------------------------------------------------------------
+// Variant 2: hierarchical cull ("packet-frustum" brute force). Block = W waves; wave w owns
+// 64 columns x R rows, the block 64 columns x W*R rows. Every record of the scene is still
+// visited by every block, in three exact levels:
+//   1. block: one lane per record (a coalesced stream of the tile-planar edge buffer, one
+//      step ahead in registers) tests it against the block's (fx, fy) box (BoxMayHit);
+//      survivors are compacted (wave ballot + prefix popcount) into the wave's LDS list;
+//   2. lane:  each wave walks every list once it fills (or at the end) with broadcast LDS
+//      reads and tests each survivor against the lane's box (BoxMayHit again; the branch is
+//      skipped when no lane of the wave can hit: the wavefront ballot);
+//   3. ray:   the exact per-ray test, lexicographic (t, id) update (lists are unordered).
+// Levels 1-2 only drop records that provably fail the exact test for every ray they cover,
+// so the frame is bit-identical to the brute-force variants.
+// ---------------------------------------------------------------------------------------
+constexpr int kSurvPerWave = 128;                // LDS survivor slots per wave list
+constexpr int kFlushAt = kSurvPerWave - kWave;  // walk the lists once any holds >= 64
+
+__device__ __forceinline__ Box WaveReduceBox(Box b) {
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+        b.xlo = fminf(b.xlo, __shfl_xor(b.xlo, o));
+        b.xhi = fmaxf(b.xhi, __shfl_xor(b.xhi, o));
+        b.ylo = fminf(b.ylo, __shfl_xor(b.ylo, o));
+        b.yhi = fmaxf(b.yhi, __shfl_xor(b.yhi, o));
+    }
+    return b;
+}
+
+// G records per thread per step are loaded one step ahead (G x 40 B per lane in flight),
+// then culled one 256/512-record sub-step at a time.
+template <int R, int W, int G>
+__global__ __launch_bounds__(kWave * W) void TraceCullKernel(TraceParams p) {
+    constexpr int kThreads = kWave * W;
+    constexpr int kStepRecords = kThreads * G;
+    static_assert(kPadTriangles % kStepRecords == 0, "a cull step must cover whole tiles");
+    __shared__ float4 surv[W * kSurvPerWave * 3];
+    __shared__ int counts[2][W];
+    __shared__ Box wave_box[W];
+    const int tid = threadIdx.x;
+    const int lane = tid & (kWave - 1);
+    const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);
+    const int x = blockIdx.x * kWave + lane;
+    const int y0 = (blockIdx.y * W + wave) * R;
+    Rays<R> s;
+    Box lane_box;
+    (void)GenerateRays<R>(p, x, y0, s, lane_box);
+    const Box wb = WaveReduceBox(lane_box);
+    if (lane == 0) {
+        wave_box[wave] = wb;
+    }
+    __syncthreads();
+    Box bb = wave_box[0];
+#pragma unroll
+    for (int w = 1; w < W; ++w) {
+        const Box o = wave_box[w];
+        bb = Box{fminf(bb.xlo, o.xlo), fmaxf(bb.xhi, o.xhi), fminf(bb.ylo, o.ylo), fmaxf(bb.yhi, o.yhi)};
+    }
+
+    // Record g of this thread in step k: global index k * kStepRecords + g * kThreads + tid,
+    // i.e. tile (k * kStepRecords + g * kThreads + tid) / 256, position tid % 256.
+    const unsigned nsteps = p.n_pad / kStepRecords;
+    const int j = tid % kTileTriangles;
+    const float4* base = p.edges + static_cast<size_t>(tid / kTileTriangles) * kTileFloat4;
+    constexpr size_t kSubF4 = static_cast<size_t>(kThreads / kTileTriangles) * kTileFloat4;
+    constexpr size_t kStepF4 = kSubF4 * G;
+    float4 n0[G], n1[G];
+    float n2[G], n3[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        const float4* t = base + g * kSubF4;
+        n0[g] = t[j];
+        n1[g] = t[kTileTriangles + j];
+        n2[g] = Plane2(t)[j];
+        n3[g] = Plane3(t)[j];
+    }
+    int mine = 0;  // records in this wave's list (wave-uniform)
+    float4* my_list = surv + wave * kSurvPerWave * 3;
+    const unsigned long long lt_mask = (1ull << lane) - 1ull;
+    unsigned phase = 0;
+    for (unsigned k = 0; k < nsteps; ++k) {
+        float4 q0[G], q1[G];
+        float q2[G], q3[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            q0[g] = n0[g];
+            q1[g] = n1[g];
+            q2[g] = n2[g];
+            q3[g] = n3[g];
+        }
+        if (k + 1 < nsteps) {
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                const float4* t = base + (k + 1) * kStepF4 + g * kSubF4;
+                n0[g] = t[j];
+                n1[g] = t[kTileTriangles + j];
+                n2[g] = Plane2(t)[j];
+                n3[g] = Plane3(t)[j];
+            }
+        }
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const Record q{q0[g].x, q0[g].y, q0[g].z, q0[g].w, q1[g].x, q1[g].y, q1[g].z, q1[g].w, q2[g]};
+            const bool pass = BoxMayHit(bb, q);
+            const unsigned long long m = __ballot(pass);
+            if (pass) {
+                float4* d = my_list + (mine + __popcll(m & lt_mask)) * 3;
+                d[0] = q0[g];
+                d[1] = q1[g];
+                d[2] = make_float4(q2[g], q3[g], __int_as_float(static_cast<int>(k * kStepRecords + g * kThreads + tid)),
+                                   0.f);
+            }
+            mine += __popcll(m);
+            if (lane == 0) {
+                counts[phase][wave] = mine;
+            }
+            __syncthreads();
+            int c[W];
+            int most = 0;
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+                c[w] = counts[phase][w];
+                most = max(most, c[w]);
+            }
+            phase ^= 1u;
+            if (most >= kFlushAt || (k + 1 == nsteps && g == G - 1)) {  // block-uniform
+#pragma unroll 1
+                for (int w = 0; w < W; ++w) {
+                    const float4* list = surv + w * kSurvPerWave * 3;
+#pragma unroll 1
+                    for (int i = 0; i < c[w]; ++i) {
+                        const float4 a = list[3 * i];
+                        const float4 b = list[3 * i + 1];
+                        const float4 e = list[3 * i + 2];
+                        const Record r{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, e.x};
+                        if (BoxMayHit(lane_box, r)) {
+                            ExactTestAnyOrder<R>(s, r, e.y, __float_as_int(e.z));
+                        }
+                    }
+                }
+                __syncthreads();  // lists are rewritten from the next sub-step on
+                mine = 0;
+            }
+        }
+    }
+    ShadeAndStore<R>(p, x, y0, s);
+}
+
+// Cull block shape: rows per lane x waves per block x records per thread per step; env
+// SRT_CULL_SHAPE = "16x8x2" (default), "8x4x1", "16x4x2", "16x8x1" or "16x8x4", for measurement.
+struct CullShape {
+    int rows;
+    int waves;
+    int group;
+};
+
+CullShape CullShapeFromEnv() {
+    const char* v = std::getenv("SRT_CULL_SHAPE");
+    if (v != nullptr) {
+        if (std::strcmp(v, "8x4x1") == 0) return {8, 4, 1};
+        if (std::strcmp(v, "16x4x2") == 0) return {16, 4, 2};
+        if (std::strcmp(v, "16x8x1") == 0) return {16, 8, 1};
+        if (std::strcmp(v, "16x8x4") == 0) return {16, 8, 4};
+    }
+    return {16, 8, 2};
 }
 
 }  // namespace
@@ -395,6 +641,7 @@ hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_ver
     p.offsets = reinterpret_cast<const float2*>(band.offsets);
     p.out = reinterpret_cast<float4*>(band.rgba);
     p.n_pad = static_cast<unsigned>(PaddedTriangleCount(n));
+    p.n_tiles = static_cast<unsigned>(n == 0 ? 1 : (n + kTileTriangles - 1) / kTileTriangles);
     p.width = static_cast<int>(band.width);
     p.row_count = static_cast<int>(band.row_count);
     p.row_begin = static_cast<int>(band.row_begin);
@@ -410,6 +657,22 @@ hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_ver
     if (variant == kTraceScalar) {
         const unsigned gy = static_cast<unsigned>((band.row_count + kRowsPerLane - 1) / kRowsPerLane);
         hipLaunchKernelGGL(TraceScalarKernel, dim3(gx, gy), dim3(kWave), 0, stream, p);
+    } else if (variant == kTraceCull) {
+        const CullShape shape = CullShapeFromEnv();
+        const int rows_per_block = shape.rows * shape.waves;
+        const unsigned gy = static_cast<unsigned>((band.row_count + rows_per_block - 1) / rows_per_block);
+        const dim3 grid(gx, gy), block(kWave * shape.waves);
+        if (shape.rows == 8) {
+            hipLaunchKernelGGL((TraceCullKernel<8, 4, 1>), grid, block, 0, stream, p);
+        } else if (shape.waves == 4) {
+            hipLaunchKernelGGL((TraceCullKernel<16, 4, 2>), grid, block, 0, stream, p);
+        } else if (shape.group == 1) {
+            hipLaunchKernelGGL((TraceCullKernel<16, 8, 1>), grid, block, 0, stream, p);
+        } else if (shape.group == 4) {
+            hipLaunchKernelGGL((TraceCullKernel<16, 8, 4>), grid, block, 0, stream, p);
+        } else {
+            hipLaunchKernelGGL((TraceCullKernel<16, 8, 2>), grid, block, 0, stream, p);
+        }
     } else {
         constexpr int kRowsPerBlock = kRowsPerLane * kLdsWaves;
         const unsigned gy = static_cast<unsigned>((band.row_count + kRowsPerBlock - 1) / kRowsPerBlock);

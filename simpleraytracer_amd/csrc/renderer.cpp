@@ -94,6 +94,9 @@ int TraceVariantFromEnv() {
     if (v != nullptr && (std::strcmp(v, "scalar") == 0 || std::strcmp(v, "1") == 0)) {
         return kTraceScalar;
     }
+    if (v != nullptr && (std::strcmp(v, "cull") == 0 || std::strcmp(v, "2") == 0)) {
+        return kTraceCull;
+    }
     return kTraceLds;
 }
 
@@ -104,7 +107,7 @@ DeviceScene::DeviceScene(const Scene& scene, int device)
     try {
         m_vertices = DeviceAlloc<float>(m_n * 9, "hipMalloc(vertices)");
         m_albedo = DeviceAlloc<float>(m_n * 3, "hipMalloc(albedo)");
-        m_edges = DeviceAlloc<float>(PaddedTriangleCount(m_n) * 12, "hipMalloc(edges)");
+        m_edges = DeviceAlloc<float>(PaddedTriangleCount(m_n) * kEdgeFloatsPerTriangle, "hipMalloc(edges)");
         HipCheck(hipMemcpy(m_vertices, scene.vertices.data(), m_n * 9 * sizeof(float), hipMemcpyHostToDevice),
                  "hipMemcpy(vertices)");
         HipCheck(hipMemcpy(m_albedo, scene.albedo.data(), m_n * 3 * sizeof(float), hipMemcpyHostToDevice),

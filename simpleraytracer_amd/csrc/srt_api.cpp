@@ -131,7 +131,7 @@ ML_API_ENTRY int srtTraceAsync(srt_device_scene scene, const float* d_offsets, f
         if ((d_offsets == nullptr || d_rgba == nullptr) && row_count != 0) {
             throw std::runtime_error("Bad buffer argument");
         }
-        if (variant != SRT_TRACE_LDS && variant != SRT_TRACE_SCALAR) {
+        if (variant != SRT_TRACE_LDS && variant != SRT_TRACE_SCALAR && variant != SRT_TRACE_CULL) {
             throw std::runtime_error("Unknown trace variant " + std::to_string(variant));
         }
         srt::DeviceScene* s = FromHandle(scene);

@@ -16,6 +16,8 @@ from scenefile import write_custom_scene
 pytestmark = pytest.mark.gpu
 
 RGB_TOL = 1e-5
+VARIANTS = ("lds", "scalar", "cull")
+CULL_SHAPES = ("8x4x1", "16x4x2", "16x8x1", "16x8x2", "16x8x4")
 
 
 def oracle_render(path, w, h, offsets=None, **kw):
@@ -32,7 +34,9 @@ def assert_parity(got, ref, rows=None):
     bad = np.argwhere(ids_got != ids_ref)
     assert bad.size == 0, f"{len(bad)} tri_id mismatches, first at {bad[:5].tolist()}: " \
                           f"gpu {got[..., 3][tuple(bad[0])]} oracle {ref[..., 3][tuple(bad[0])]}"
-    d = np.abs(got[..., :3] - ref[..., :3])
+    nan_got, nan_ref = np.isnan(got[..., :3]), np.isnan(ref[..., :3])
+    assert np.array_equal(nan_got, nan_ref), "NaN rgb positions differ"
+    d = np.abs(np.where(nan_ref, 0.0, got[..., :3] - ref[..., :3]))
     assert float(d.max(initial=0.0)) <= RGB_TOL, f"max rgb delta {d.max()}"
 
 
@@ -85,7 +89,7 @@ def test_c2_cornell_1080p_ml_api(gpu, scenes):
     assert set(np.unique(got[..., 3]).astype(int)) >= set(range(12))
 
 
-@pytest.mark.parametrize("variant", ["lds", "scalar"])
+@pytest.mark.parametrize("variant", VARIANTS)
 def test_c3_soup100k_1080p_row_sample(gpu, scenes, variant):
     """Headline config: full 1920x1080 frame on the GPU, checked on 24 rows spread over it."""
     got = torch_render(scenes["soup100k"], 1920, 1080, variant=variant)
@@ -99,7 +103,7 @@ def test_c3_soup100k_1080p_row_sample(gpu, scenes, variant):
     assert np.all(got[hit][:, :3] >= 0) and np.all(got[hit][:, :3] <= 1.0)
 
 
-@pytest.mark.parametrize("variant", ["lds", "scalar"])
+@pytest.mark.parametrize("variant", VARIANTS)
 def test_soup_random_offsets_full_frame(gpu, scenes, variant):
     rng = np.random.default_rng(1234)
     w, h = 331, 187  # not multiples of the 64-column / 8- and 32-row tiles
@@ -117,7 +121,7 @@ def test_mixed_offsets_exercise_both_loop_bodies(gpu, scenes):
     offsets = np.full((h, w, 2), 0.5, np.float32)
     offsets[:, 64:128, 0] = rng.random((h, 64), dtype=np.float32)
     offsets[:48, 192:, 1] = rng.random((48, 64), dtype=np.float32)
-    for variant in ("lds", "scalar"):
+    for variant in VARIANTS:
         got = torch_render(scenes["soup300"], w, h, offsets, variant=variant)
         ref = oracle_render(scenes["soup300"], w, h, offsets)
         assert_parity(got, ref)
@@ -126,16 +130,74 @@ def test_mixed_offsets_exercise_both_loop_bodies(gpu, scenes):
 @pytest.mark.parametrize("wh", [(1, 1), (1, 300), (300, 1), (65, 33), (64, 32), (97, 61)])
 def test_odd_sizes(gpu, scenes, wh):
     w, h = wh
-    for variant in ("lds", "scalar"):
+    for variant in VARIANTS:
         got = torch_render(scenes["soup300"], w, h, variant=variant)
         ref = oracle_render(scenes["soup300"], w, h)
         assert_parity(got, ref)
 
 
-def test_band_split_is_bitwise_identical(gpu, scenes):
-    full = torch_render(scenes["soup2k"], 320, 240)
-    banded = torch_render(scenes["soup2k"], 320, 240, bands=[7, 33, 1, 64, 200])
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_band_split_is_bitwise_identical(gpu, scenes, variant):
+    full = torch_render(scenes["soup2k"], 320, 240, variant=variant)
+    banded = torch_render(scenes["soup2k"], 320, 240, bands=[7, 33, 1, 64, 200], variant=variant)
     assert np.array_equal(full.view(np.uint32), banded.view(np.uint32))
+
+
+def test_variants_bitwise_identical_1080p(gpu, scenes):
+    """The three trace kernels produce the same frame, bit for bit (headline config)."""
+    frames = [torch_render(scenes["soup100k"], 1920, 1080, variant=v) for v in VARIANTS]
+    for f in frames[1:]:
+        assert np.array_equal(frames[0].view(np.uint32), f.view(np.uint32))
+
+
+@pytest.mark.parametrize("shape", CULL_SHAPES)
+def test_cull_shapes(gpu, scenes, monkeypatch, shape):
+    """Every cull block shape (rows x waves x records per thread) against the oracle, with
+    random offsets (non-degenerate lane boxes) on a frame that leaves partial blocks."""
+    monkeypatch.setenv("SRT_CULL_SHAPE", shape)
+    rng = np.random.default_rng(5)
+    w, h = 200, 150
+    offsets = rng.random((h, w, 2), dtype=np.float32)
+    got = torch_render(scenes["soup2k"], w, h, offsets, variant="cull")
+    assert_parity(got, oracle_render(scenes["soup2k"], w, h, offsets))
+
+
+def test_cull_survivor_overflow_and_ties(gpu, tmp_path, monkeypatch):
+    """Every record survives the block cull (large overlapping triangles, many exact
+    duplicates spread over several cull steps): survivor lists fill and flush repeatedly,
+    and equal-t ties across lists must still resolve to the lowest id."""
+    rng = np.random.default_rng(17)
+    big = [-2, -2, 3, 2, -2, 3, 0, 2, 3]
+    tris = []
+    for i in range(5000):
+        if i % 7 == 3:
+            tris.append(big)  # exact duplicates: ids 3, 10, 17, ... tie everywhere
+        else:
+            c = rng.uniform([-1, -1, 3.9], [1, 1, 6])
+            tris.append(list((c + rng.uniform(-0.8, 0.8, (3, 3))).ravel()))
+    albedo = rng.uniform(0.2, 1.0, (len(tris), 3))
+    path = write_custom_scene(tmp_path / "dense.srt", tris, albedo)
+    ref = oracle_render(path, 96, 80)
+    assert (ref[..., 3] == 3).mean() > 0.3
+    for shape in CULL_SHAPES:
+        monkeypatch.setenv("SRT_CULL_SHAPE", shape)
+        assert_parity(torch_render(path, 96, 80, variant="cull"), ref)
+
+
+def test_extreme_offsets(gpu, scenes):
+    """Sample offsets far outside [0,1), negative, huge, +-inf and NaN: the box cull must stay
+    conservative (monotone fma bounds, NaN never rejects) and match the oracle bit for bit."""
+    rng = np.random.default_rng(3)
+    w, h = 130, 70
+    offsets = rng.uniform(-40, 40, (h, w, 2)).astype(np.float32)
+    offsets[5, :, 0] = np.inf
+    offsets[6, :, 1] = -np.inf
+    offsets[7, ::3, :] = np.nan
+    offsets[:, 9, 0] = 1e30
+    offsets[:, 10, 1] = -1e30
+    ref = oracle_render(scenes["soup300"], w, h, offsets)
+    for variant in VARIANTS:
+        assert_parity(torch_render(scenes["soup300"], w, h, offsets, variant=variant), ref)
 
 
 def test_repeat_render_deterministic(gpu, scenes):
@@ -153,9 +215,10 @@ def test_ml_visible_devices_bands_direct(gpu, scenes, monkeypatch):
     monkeypatch.setenv("SRT_GATHER", "direct")
     got = srt.render(scenes["soup2k"], 160, 100)
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
-    monkeypatch.setenv("SRT_TRACE_VARIANT", "scalar")
-    got2 = srt.render(scenes["soup2k"], 160, 100)
-    assert np.array_equal(got2.view(np.uint32), ref.view(np.uint32))
+    for variant in ("scalar", "cull"):
+        monkeypatch.setenv("SRT_TRACE_VARIANT", variant)
+        got2 = srt.render(scenes["soup2k"], 160, 100)
+        assert np.array_equal(got2.view(np.uint32), ref.view(np.uint32))
 
 
 def test_edge_cases_scene(gpu, tmp_path):
@@ -180,7 +243,7 @@ def test_edge_cases_scene(gpu, tmp_path):
         [0.5, 0.2, 1.0, 0.7, 0.2, 1.0, 0.6, 0.4, 1.0],
     ]
     path = write_custom_scene(tmp_path / "edge.srt", tris, np.linspace(0.1, 0.9, 24).reshape(8, 3))
-    for variant in ("lds", "scalar"):
+    for variant in VARIANTS:
         got = torch_render(path, 257, 129, variant=variant)
         ref = oracle_render(path, 257, 129)
         assert_parity(got, ref)
@@ -230,4 +293,4 @@ def test_no_cpu_fallback_marker(gpu):
 
     lib = Path(__file__).resolve().parents[1] / "simpleraytracer_amd" / "lib" / "libModelRunner.so"
     assert b"gfx950" in lib.read_bytes()
-    assert os.environ.get("SRT_TRACE_VARIANT") in (None, "lds", "scalar", "0", "1")
+    assert os.environ.get("SRT_TRACE_VARIANT") in (None, "lds", "scalar", "cull", "0", "1", "2")
