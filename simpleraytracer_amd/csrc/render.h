@@ -32,7 +32,13 @@ constexpr int kPadTriangles = 2048;
 //   plane 3: float [256] vol
 // E_k(fx, fy) = fma(fy, cy_k, fma(fx, cx_k, c0_k)) for the three edges k = A, B, C.
 constexpr int kTileFloat4 = kTileTriangles * 5 / 2;  // 640 float4 = 10 KiB per tile
-constexpr int kEdgeFloatsPerTriangle = 10;
+
+// Screen boxes (render.hip ScreenBox): one float4 (xlo, xhi, ylo, yhi) per record, in record
+// order, right after the tiles. They bound only rays with |fx|, |fy| <= kScreenBoxRange.
+constexpr float kScreenBoxRange = 4.0f;
+
+// Floats per record in the edge allocation: 10 (tiles) + 4 (screen box).
+constexpr int kEdgeFloatsPerTriangle = 14;
 
 inline std::uint64_t PaddedTriangleCount(std::uint64_t n) {
     const std::uint64_t p = (n + kPadTriangles - 1) / kPadTriangles * kPadTriangles;

@@ -7,6 +7,7 @@
 
 #include <cmath>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
 
 namespace srt {
@@ -18,6 +19,7 @@ constexpr int kRowsPerLane = 8;  // rays per lane (LDS / scalar variants): one c
 
 struct TraceParams {
     const float4* __restrict__ edges;
+    const float4* __restrict__ screen_boxes;
     const float* __restrict__ vertices;
     const float* __restrict__ albedo;
     const float2* __restrict__ offsets;
@@ -38,6 +40,7 @@ struct TraceParams {
 struct PrepareParams {
     const float* __restrict__ vertices;
     float4* __restrict__ edges;
+    float4* __restrict__ screen_boxes;
     unsigned n;
     unsigned n_pad;
     float origin[3];
@@ -68,6 +71,62 @@ __device__ __forceinline__ const float* Plane2(const float4* tile) {
 }
 __device__ __forceinline__ const float* Plane3(const float4* tile) {
     return reinterpret_cast<const float*>(tile + 2 * kTileTriangles) + kTileTriangles;
+}
+
+// Screen box of a record: an (fx, fy) box containing every ray position with |fx| <= F
+// (F = kScreenBoxRange) at which the float test E_k = fma(fy, cy_k, fma(fx, cx_k, c0_k)) >= 0
+// can pass for all three edges. Derivation (DESIGN.md "Screen box"): with g = fl(fx cx + c0)
+// = (fx cx + c0)(1 + d), |d| <= 2^-24, plus an absolute term for subnormal results, the
+// outer fma only rounds (sign-preserving, -0 passes), so a pass implies
+//     c0 + cx fx + cy fy >= -s,   s = 2^-24 (|c0| + F |cx|) + 2^-120   (exact reals).
+// If the three gradients (cx_k, cy_k) positively span the plane (exact sign tests in double:
+// the products of two floats are exact), the region {c0_k + s_k + cx_k fx + cy_k fy >= 0} is
+// bounded: the triangle whose corners are the pairwise line intersections (empty otherwise,
+// which any box covers). Corners are solved in double, padded for double rounding and
+// rounded outward to float. Otherwise the box is unbounded (never culls).
+__device__ __forceinline__ float DownF(double v) { return __double2float_rd(v); }
+__device__ __forceinline__ float UpF(double v) { return __double2float_ru(v); }
+
+__device__ float4 ScreenBox(const float c[9]) {
+    const float inf = __builtin_inff();
+    const float4 unbounded = make_float4(-inf, inf, -inf, inf);
+    double gx[3], gy[3], k[3];
+    for (int e = 0; e < 3; ++e) {
+        const double c0 = c[3 * e], cx = c[3 * e + 1], cy = c[3 * e + 2];
+        if (!(fabs(c0) < 1e30 && fabs(cx) < 1e30 && fabs(cy) < 1e30)) {
+            return unbounded;
+        }
+        gx[e] = cx;
+        gy[e] = cy;
+        const double slack = (0x1p-24 * (fabs(c0) + kScreenBoxRange * fabs(cx)) + 0x1p-120) * (1.0 + 1e-12);
+        k[e] = c0 + slack;  // shifted constant; |error| of this sum is covered by the pad below
+    }
+    const double dAB = gx[0] * gy[1] - gy[0] * gx[1];
+    const double dBC = gx[1] * gy[2] - gy[1] * gx[2];
+    const double dCA = gx[2] * gy[0] - gy[2] * gx[0];
+    const bool spans = (dAB > 0 && dBC > 0 && dCA > 0) || (dAB < 0 && dBC < 0 && dCA < 0);
+    if (!spans) {
+        return unbounded;
+    }
+    double xlo = 1e300, xhi = -1e300, ylo = 1e300, yhi = -1e300;
+    for (int v = 0; v < 3; ++v) {
+        const int i = (v + 1) % 3, j = (v + 2) % 3;  // corner opposite edge v: lines i and j
+        const double d = gx[i] * gy[j] - gy[i] * gx[j];
+        const double tx1 = -k[i] * gy[j], tx2 = k[j] * gy[i];
+        const double ty1 = -gx[i] * k[j], ty2 = gx[j] * k[i];
+        const double x = (tx1 + tx2) / d, y = (ty1 + ty2) / d;
+        const double ad = fabs(d);
+        const double px = 1e-12 * ((fabs(tx1) + fabs(tx2)) / ad + fabs(x)) + 1e-300;
+        const double py = 1e-12 * ((fabs(ty1) + fabs(ty2)) / ad + fabs(y)) + 1e-300;
+        xlo = fmin(xlo, x - px);
+        xhi = fmax(xhi, x + px);
+        ylo = fmin(ylo, y - py);
+        yhi = fmax(yhi, y + py);
+    }
+    if (!(xlo <= xhi && ylo <= yhi)) {
+        return unbounded;
+    }
+    return make_float4(DownF(xlo), UpF(xhi), DownF(ylo), UpF(yhi));
 }
 
 // One thread per triangle: origin-relative edge normals nA = B x C, nB = C x A, nC = A x B
@@ -125,6 +184,9 @@ __global__ __launch_bounds__(256) void PrepareKernel(PrepareParams p) {
     tile[kTileTriangles + j] = make_float4(c[4], c[5], c[6], c[7]);
     p2[j] = c[8];
     p3[j] = vol;
+    // Disabled records: an empty box (culled by every ray box the screen boxes apply to).
+    p.screen_boxes[i] = disabled ? make_float4(__builtin_inff(), -__builtin_inff(), __builtin_inff(), -__builtin_inff())
+                                 : ScreenBox(c);
 }
 
 // Per-lane ray state: R rays sharing one image column.
@@ -212,29 +274,6 @@ __device__ __forceinline__ void TestTriangle(Rays<R>& s, const Record& q, unsign
                         s.bt[r] = t;
                         s.bi[r] = static_cast<int>(id);
                     }
-                }
-            }
-        }
-    }
-}
-
-// Exact test of one record against every ray of the lane, for records arriving in any
-// order: keeps the lexicographic minimum of (t, id), which equals the ascending-id strict-<
-// result of TestTriangle (smallest t; among equal t the lowest id).
-template <int R>
-__device__ __forceinline__ void ExactTestAnyOrder(Rays<R>& s, const Record& q, float vol, int id) {
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const float eA = fmaf(s.fy[r], q.cyA, fmaf(s.fx[r], q.cxA, q.c0A));
-        const float eB = fmaf(s.fy[r], q.cyB, fmaf(s.fx[r], q.cxB, q.c0B));
-        const float eC = fmaf(s.fy[r], q.cyC, fmaf(s.fx[r], q.cxC, q.c0C));
-        if (eA >= 0.f && eB >= 0.f && eC >= 0.f) {
-            const float det = (eA + eB) + eC;
-            if (det > 0.f) {
-                const float t = vol / det;
-                if (t < s.bt[r] || (t == s.bt[r] && id < s.bi[r])) {
-                    s.bt[r] = t;
-                    s.bi[r] = id;
                 }
             }
         }
@@ -446,19 +485,18 @@ __global__ __launch_bounds__(kWave) void TraceScalarKernel(TraceParams p) {
 // Variant 2: hierarchical cull ("packet-frustum" brute force). Block = W waves; wave w owns
 // 64 columns x R rows, the block 64 columns x W*R rows. Every record of the scene is still
 // visited by every block, in three exact levels:
-//   1. block: one lane per record (a coalesced stream of the tile-planar edge buffer, one
-//      step ahead in registers) tests it against the block's (fx, fy) box (BoxMayHit);
-//      survivors are compacted (wave ballot + prefix popcount) into the wave's LDS list;
-//   2. lane:  each wave walks every list once it fills (or at the end) with broadcast LDS
-//      reads and tests each survivor against the lane's box (BoxMayHit again; the branch is
-//      skipped when no lane of the wave can hit: the wavefront ballot);
-//   3. ray:   the exact per-ray test, lexicographic (t, id) update (lists are unordered).
+//   1. block: one lane per record streams the 16-B screen boxes (PrepareKernel, "Screen
+//      box"), G records per lane per step loaded one step ahead, and tests them against
+//      the block's (fx, fy) box; the ids of survivors are appended (wave ballot + prefix
+//      popcount) to the wave's LDS id list;
+//   2. wave:  once the lists hold a batch (or at the end) the block gathers the survivors'
+//      edge records into LDS; each wave tests them, one per lane, against its own box
+//      (screen box + BoxMayHit) and ballots the result;
+//   3. ray:   for every set bit, the exact per-ray test of all the wave's rays, keeping the
+//      lexicographic (t, id) minimum (survivors arrive out of id order).
 // Levels 1-2 only drop records that provably fail the exact test for every ray they cover,
 // so the frame is bit-identical to the brute-force variants.
 // ---------------------------------------------------------------------------------------
-constexpr int kSurvPerWave = 128;                // LDS survivor slots per wave list
-constexpr int kFlushAt = kSurvPerWave - kWave;  // walk the lists once any holds >= 64
-
 __device__ __forceinline__ Box WaveReduceBox(Box b) {
 #pragma unroll
     for (int o = 1; o < kWave; o <<= 1) {
@@ -470,16 +508,208 @@ __device__ __forceinline__ Box WaveReduceBox(Box b) {
     return b;
 }
 
-// G records per thread per step are loaded one step ahead (G x 40 B per lane in flight),
-// then culled one 256/512-record sub-step at a time.
+// The screen boxes bound only rays with |fx|, |fy| <= kScreenBoxRange (PrepareKernel); a
+// ray box reaching outside that square (or NaN) skips the screen-box test.
+__device__ __forceinline__ bool ScreenBoxUsable(const Box& b) {
+    return b.xlo >= -kScreenBoxRange && b.xhi <= kScreenBoxRange && b.ylo >= -kScreenBoxRange &&
+           b.yhi <= kScreenBoxRange;
+}
+
+// Screen box (xlo, xhi, ylo, yhi) of a record overlaps the ray box.
+__device__ __forceinline__ bool ScreenBoxOverlaps(const Box& b, const float4& sb) {
+    return !(sb.y < b.xlo || sb.x > b.xhi || sb.w < b.ylo || sb.z > b.yhi);
+}
+
+// Exact test of one record against every ray of the lane (records in any order): the
+// lexicographic minimum of (t, id) equals the ascending-id strict-< result of TestTriangle
+// (smallest t; among equal t the lowest id).
+template <int R, bool SHARED>
+__device__ __forceinline__ void ExactTestAnyOrder(Rays<R>& s, const Record& q, float vol, int id) {
+    float gA[R], gB[R], gC[R];
+    if constexpr (SHARED) {
+        const float a = fmaf(s.fx[0], q.cxA, q.c0A), b = fmaf(s.fx[0], q.cxB, q.c0B),
+                    c = fmaf(s.fx[0], q.cxC, q.c0C);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            gA[r] = a;
+            gB[r] = b;
+            gC[r] = c;
+        }
+    } else {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            gA[r] = fmaf(s.fx[r], q.cxA, q.c0A);
+            gB[r] = fmaf(s.fx[r], q.cxB, q.c0B);
+            gC[r] = fmaf(s.fx[r], q.cxC, q.c0C);
+        }
+    }
+    float e[R][3];
+    float m[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        e[r][0] = fmaf(s.fy[r], q.cyA, gA[r]);
+        e[r][1] = fmaf(s.fy[r], q.cyB, gB[r]);
+        e[r][2] = fmaf(s.fy[r], q.cyC, gC[r]);
+        m[r] = fminf(fminf(e[r][0], e[r][1]), e[r][2]);
+    }
+    float mm = m[0];
+#pragma unroll
+    for (int r = 1; r < R; ++r) {
+        mm = fmaxf(mm, m[r]);
+    }
+    if (mm >= 0.f) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            if (e[r][0] >= 0.f && e[r][1] >= 0.f && e[r][2] >= 0.f) {
+                const float det = (e[r][0] + e[r][1]) + e[r][2];
+                if (det > 0.f) {
+                    const float t = vol / det;
+                    if (t < s.bt[r] || (t == s.bt[r] && id < s.bi[r])) {
+                        s.bt[r] = t;
+                        s.bi[r] = id;
+                    }
+                }
+            }
+        }
+    }
+}
+
+// Loads record `id`'s edge planes from the tile-planar buffer.
+__device__ __forceinline__ void LoadRecord(const float4* __restrict__ edges, unsigned id, float4& p0, float4& p1,
+                                           float& cyC, float& vol) {
+    const float4* tile = edges + static_cast<size_t>(id / kTileTriangles) * kTileFloat4;
+    const unsigned j = id % kTileTriangles;
+    p0 = tile[j];
+    p1 = tile[kTileTriangles + j];
+    cyC = Plane2(tile)[j];
+    vol = Plane3(tile)[j];
+}
+
+template <int W, int G>
+struct CullShared {
+    static constexpr int kBatch = W * kWave;              // survivors gathered per flush batch
+    static constexpr int kListCap = kBatch + kWave * G;   // per-wave id list capacity
+    unsigned ids[W][kListCap];
+    float4 st0[kBatch];  // gathered records: plane 0
+    float4 st1[kBatch];  //                   plane 1
+    float4 st2[kBatch];  //                   (cyC, vol, id, 0)
+    float4 st3[kBatch];  //                   screen box
+    int counts[2][W];
+    Box wave_box[W];
+    unsigned shared_fx;
+};
+
+template <int R, int W, int G, bool SHARED>
+__device__ __forceinline__ void CullWalk(const TraceParams& p, CullShared<W, G>& sh, Rays<R>& s, const Box& bb,
+                                         const Box& wb) {
+    constexpr int kThreads = kWave * W;
+    constexpr int kStep = kThreads * G;
+    constexpr int kBatch = CullShared<W, G>::kBatch;
+    const int tid = threadIdx.x;
+    const int lane = tid & (kWave - 1);
+    const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);
+    const float4* __restrict__ sbox = p.screen_boxes;
+    const bool block_sb = ScreenBoxUsable(bb);
+    const bool wave_sb = ScreenBoxUsable(wb);
+    const unsigned long long lt_mask = (1ull << lane) - 1ull;
+    const unsigned nsteps = p.n_pad / kStep;
+
+    float4 nb[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        nb[g] = sbox[g * kThreads + tid];
+    }
+    int mine = 0;  // ids in this wave's list (wave-uniform)
+    for (unsigned k = 0; k < nsteps; ++k) {
+        float4 cb[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            cb[g] = nb[g];
+        }
+        if (k + 1 < nsteps) {
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                nb[g] = sbox[(k + 1) * kStep + g * kThreads + tid];
+            }
+        }
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            // NaN boxes (disabled records) fail every comparison -> overlap -> the wave
+            // level drops them (their edge values are NaN: never a hit).
+            const bool pass = !block_sb || ScreenBoxOverlaps(bb, cb[g]);
+            const unsigned long long m = __ballot(pass);
+            if (pass) {
+                sh.ids[wave][mine + __popcll(m & lt_mask)] = k * kStep + g * kThreads + tid;
+            }
+            mine += __popcll(m);
+        }
+        const unsigned ph = k & 1u;
+        if (lane == 0) {
+            sh.counts[ph][wave] = mine;
+        }
+        __syncthreads();
+        int c[W];
+        int total = 0;
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+            c[w] = sh.counts[ph][w];
+            total += c[w];
+        }
+        if (total < kBatch && k + 1 < nsteps) {  // block-uniform
+            continue;
+        }
+        // Flush: gather every listed record in batches of kBatch, then filter + walk.
+#pragma unroll 1
+        for (int b0 = 0; b0 < total; b0 += kBatch) {
+            const int e = b0 + tid;
+            if (e < total) {
+                int w = 0, j = e;
+#pragma unroll
+                for (int v = 0; v < W - 1; ++v) {
+                    if (w == v && j >= c[v]) {
+                        j -= c[v];
+                        w = v + 1;
+                    }
+                }
+                const unsigned id = sh.ids[w][j];
+                float4 p0, p1;
+                float cyC, vol;
+                LoadRecord(p.edges, id, p0, p1, cyC, vol);
+                sh.st0[tid] = p0;
+                sh.st1[tid] = p1;
+                sh.st2[tid] = make_float4(cyC, vol, __uint_as_float(id), 0.f);
+                sh.st3[tid] = sbox[id];
+            }
+            __syncthreads();
+            const int nb_here = min(kBatch, total - b0);
+#pragma unroll 1
+            for (int c0 = 0; c0 < nb_here; c0 += kWave) {
+                const int i = c0 + lane;
+                bool pass = false;
+                if (i < nb_here) {
+                    const float4 a = sh.st0[i], b = sh.st1[i], x = sh.st2[i];
+                    const Record r{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, x.x};
+                    pass = (!wave_sb || ScreenBoxOverlaps(wb, sh.st3[i])) && BoxMayHit(wb, r);
+                }
+                unsigned long long m = __ballot(pass);
+                while (m != 0ull) {
+                    const int bit = __builtin_ctzll(m);
+                    m &= m - 1ull;
+                    const float4 a = sh.st0[c0 + bit], b = sh.st1[c0 + bit], x = sh.st2[c0 + bit];
+                    const Record r{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, x.x};
+                    ExactTestAnyOrder<R, SHARED>(s, r, x.y, __float_as_int(x.z));
+                }
+            }
+            __syncthreads();  // staging (and, after the last batch, the id lists) reused next
+        }
+        mine = 0;
+    }
+}
+
 template <int R, int W, int G>
 __global__ __launch_bounds__(kWave * W) void TraceCullKernel(TraceParams p) {
-    constexpr int kThreads = kWave * W;
-    constexpr int kStepRecords = kThreads * G;
-    static_assert(kPadTriangles % kStepRecords == 0, "a cull step must cover whole tiles");
-    __shared__ float4 surv[W * kSurvPerWave * 3];
-    __shared__ int counts[2][W];
-    __shared__ Box wave_box[W];
+    static_assert(kPadTriangles % (kWave * W * G) == 0, "a cull step must cover whole pad units");
+    __shared__ CullShared<W, G> sh;
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
     const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);
@@ -487,110 +717,35 @@ __global__ __launch_bounds__(kWave * W) void TraceCullKernel(TraceParams p) {
     const int y0 = (blockIdx.y * W + wave) * R;
     Rays<R> s;
     Box lane_box;
-    (void)GenerateRays<R>(p, x, y0, s, lane_box);
+    const bool same = GenerateRays<R>(p, x, y0, s, lane_box);
     const Box wb = WaveReduceBox(lane_box);
-    if (lane == 0) {
-        wave_box[wave] = wb;
+    if (tid == 0) {
+        sh.shared_fx = 1u;
     }
     __syncthreads();
-    Box bb = wave_box[0];
+    if (lane == 0) {
+        sh.wave_box[wave] = wb;
+    }
+    if (!__all(same) && lane == 0) {
+        sh.shared_fx = 0u;
+    }
+    __syncthreads();
+    Box bb = sh.wave_box[0];
 #pragma unroll
     for (int w = 1; w < W; ++w) {
-        const Box o = wave_box[w];
+        const Box o = sh.wave_box[w];
         bb = Box{fminf(bb.xlo, o.xlo), fmaxf(bb.xhi, o.xhi), fminf(bb.ylo, o.ylo), fmaxf(bb.yhi, o.yhi)};
     }
-
-    // Record g of this thread in step k: global index k * kStepRecords + g * kThreads + tid,
-    // i.e. tile (k * kStepRecords + g * kThreads + tid) / 256, position tid % 256.
-    const unsigned nsteps = p.n_pad / kStepRecords;
-    const int j = tid % kTileTriangles;
-    const float4* base = p.edges + static_cast<size_t>(tid / kTileTriangles) * kTileFloat4;
-    constexpr size_t kSubF4 = static_cast<size_t>(kThreads / kTileTriangles) * kTileFloat4;
-    constexpr size_t kStepF4 = kSubF4 * G;
-    float4 n0[G], n1[G];
-    float n2[G], n3[G];
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-        const float4* t = base + g * kSubF4;
-        n0[g] = t[j];
-        n1[g] = t[kTileTriangles + j];
-        n2[g] = Plane2(t)[j];
-        n3[g] = Plane3(t)[j];
-    }
-    int mine = 0;  // records in this wave's list (wave-uniform)
-    float4* my_list = surv + wave * kSurvPerWave * 3;
-    const unsigned long long lt_mask = (1ull << lane) - 1ull;
-    unsigned phase = 0;
-    for (unsigned k = 0; k < nsteps; ++k) {
-        float4 q0[G], q1[G];
-        float q2[G], q3[G];
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-            q0[g] = n0[g];
-            q1[g] = n1[g];
-            q2[g] = n2[g];
-            q3[g] = n3[g];
-        }
-        if (k + 1 < nsteps) {
-#pragma unroll
-            for (int g = 0; g < G; ++g) {
-                const float4* t = base + (k + 1) * kStepF4 + g * kSubF4;
-                n0[g] = t[j];
-                n1[g] = t[kTileTriangles + j];
-                n2[g] = Plane2(t)[j];
-                n3[g] = Plane3(t)[j];
-            }
-        }
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-            const Record q{q0[g].x, q0[g].y, q0[g].z, q0[g].w, q1[g].x, q1[g].y, q1[g].z, q1[g].w, q2[g]};
-            const bool pass = BoxMayHit(bb, q);
-            const unsigned long long m = __ballot(pass);
-            if (pass) {
-                float4* d = my_list + (mine + __popcll(m & lt_mask)) * 3;
-                d[0] = q0[g];
-                d[1] = q1[g];
-                d[2] = make_float4(q2[g], q3[g], __int_as_float(static_cast<int>(k * kStepRecords + g * kThreads + tid)),
-                                   0.f);
-            }
-            mine += __popcll(m);
-            if (lane == 0) {
-                counts[phase][wave] = mine;
-            }
-            __syncthreads();
-            int c[W];
-            int most = 0;
-#pragma unroll
-            for (int w = 0; w < W; ++w) {
-                c[w] = counts[phase][w];
-                most = max(most, c[w]);
-            }
-            phase ^= 1u;
-            if (most >= kFlushAt || (k + 1 == nsteps && g == G - 1)) {  // block-uniform
-#pragma unroll 1
-                for (int w = 0; w < W; ++w) {
-                    const float4* list = surv + w * kSurvPerWave * 3;
-#pragma unroll 1
-                    for (int i = 0; i < c[w]; ++i) {
-                        const float4 a = list[3 * i];
-                        const float4 b = list[3 * i + 1];
-                        const float4 e = list[3 * i + 2];
-                        const Record r{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, e.x};
-                        if (BoxMayHit(lane_box, r)) {
-                            ExactTestAnyOrder<R>(s, r, e.y, __float_as_int(e.z));
-                        }
-                    }
-                }
-                __syncthreads();  // lists are rewritten from the next sub-step on
-                mine = 0;
-            }
-        }
+    if (sh.shared_fx != 0u) {
+        CullWalk<R, W, G, true>(p, sh, s, bb, wb);
+    } else {
+        CullWalk<R, W, G, false>(p, sh, s, bb, wb);
     }
     ShadeAndStore<R>(p, x, y0, s);
 }
 
-// Cull block shape: rows per lane x waves per block x records per thread per step; env
-// SRT_CULL_SHAPE = "16x8x2" (default), "8x4x1", "16x4x2", "16x8x1" or "16x8x4", for measurement.
+// Cull block shape: rows per lane x waves per block x records per lane per step; env
+// SRT_CULL_SHAPE = "RxWxG" (default 8x4x4; see kShapes), for measurement.
 struct CullShape {
     int rows;
     int waves;
@@ -600,12 +755,16 @@ struct CullShape {
 CullShape CullShapeFromEnv() {
     const char* v = std::getenv("SRT_CULL_SHAPE");
     if (v != nullptr) {
-        if (std::strcmp(v, "8x4x1") == 0) return {8, 4, 1};
-        if (std::strcmp(v, "16x4x2") == 0) return {16, 4, 2};
-        if (std::strcmp(v, "16x8x1") == 0) return {16, 8, 1};
-        if (std::strcmp(v, "16x8x4") == 0) return {16, 8, 4};
+        static const CullShape kShapes[] = {{8, 4, 1}, {8, 4, 2}, {8, 4, 4}, {8, 8, 2}, {8, 8, 4}, {16, 4, 4}};
+        for (const CullShape& c : kShapes) {
+            char name[16];
+            std::snprintf(name, sizeof(name), "%dx%dx%d", c.rows, c.waves, c.group);
+            if (std::strcmp(v, name) == 0) {
+                return c;
+            }
+        }
     }
-    return {16, 8, 2};
+    return {8, 4, 4};
 }
 
 }  // namespace
@@ -615,6 +774,7 @@ hipError_t LaunchPrepare(const float* d_vertices, std::uint64_t n, const Frame& 
     PrepareParams p{};
     p.vertices = d_vertices;
     p.edges = reinterpret_cast<float4*>(d_edges);
+    p.screen_boxes = reinterpret_cast<float4*>(d_edges) + PaddedTriangleCount(n) / kTileTriangles * kTileFloat4;
     p.n = static_cast<unsigned>(n);
     p.n_pad = static_cast<unsigned>(PaddedTriangleCount(n));
     for (int k = 0; k < 3; ++k) {
@@ -636,6 +796,7 @@ hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_ver
     }
     TraceParams p{};
     p.edges = reinterpret_cast<const float4*>(d_edges);
+    p.screen_boxes = reinterpret_cast<const float4*>(d_edges) + PaddedTriangleCount(n) / kTileTriangles * kTileFloat4;
     p.vertices = d_vertices;
     p.albedo = d_albedo;
     p.offsets = reinterpret_cast<const float2*>(band.offsets);
@@ -662,16 +823,14 @@ hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_ver
         const int rows_per_block = shape.rows * shape.waves;
         const unsigned gy = static_cast<unsigned>((band.row_count + rows_per_block - 1) / rows_per_block);
         const dim3 grid(gx, gy), block(kWave * shape.waves);
-        if (shape.rows == 8) {
-            hipLaunchKernelGGL((TraceCullKernel<8, 4, 1>), grid, block, 0, stream, p);
-        } else if (shape.waves == 4) {
-            hipLaunchKernelGGL((TraceCullKernel<16, 4, 2>), grid, block, 0, stream, p);
-        } else if (shape.group == 1) {
-            hipLaunchKernelGGL((TraceCullKernel<16, 8, 1>), grid, block, 0, stream, p);
-        } else if (shape.group == 4) {
-            hipLaunchKernelGGL((TraceCullKernel<16, 8, 4>), grid, block, 0, stream, p);
-        } else {
-            hipLaunchKernelGGL((TraceCullKernel<16, 8, 2>), grid, block, 0, stream, p);
+        const int key = shape.rows * 100 + shape.waves * 10 + shape.group;
+        switch (key) {
+            case 841: hipLaunchKernelGGL((TraceCullKernel<8, 4, 1>), grid, block, 0, stream, p); break;
+            case 842: hipLaunchKernelGGL((TraceCullKernel<8, 4, 2>), grid, block, 0, stream, p); break;
+            case 882: hipLaunchKernelGGL((TraceCullKernel<8, 8, 2>), grid, block, 0, stream, p); break;
+            case 884: hipLaunchKernelGGL((TraceCullKernel<8, 8, 4>), grid, block, 0, stream, p); break;
+            case 1644: hipLaunchKernelGGL((TraceCullKernel<16, 4, 4>), grid, block, 0, stream, p); break;
+            default: hipLaunchKernelGGL((TraceCullKernel<8, 4, 4>), grid, block, 0, stream, p); break;
         }
     } else {
         constexpr int kRowsPerBlock = kRowsPerLane * kLdsWaves;

@@ -17,7 +17,7 @@ pytestmark = pytest.mark.gpu
 
 RGB_TOL = 1e-5
 VARIANTS = ("lds", "scalar", "cull")
-CULL_SHAPES = ("8x4x1", "16x4x2", "16x8x1", "16x8x2", "16x8x4")
+CULL_SHAPES = ("8x4x1", "8x4x2", "8x4x4", "8x8x2", "8x8x4", "16x4x4")
 
 
 def oracle_render(path, w, h, offsets=None, **kw):
@@ -182,6 +182,34 @@ def test_cull_survivor_overflow_and_ties(gpu, tmp_path, monkeypatch):
     for shape in CULL_SHAPES:
         monkeypatch.setenv("SRT_CULL_SHAPE", shape)
         assert_parity(torch_render(path, 96, 80, variant="cull"), ref)
+
+
+def test_cull_nasty_geometry(gpu, tmp_path, monkeypatch):
+    """Triangles around and behind the eye, crossing the camera plane, slivers, needles, huge
+    and tiny ones, near edge-on: the screen boxes (bounded-region case) and the unbounded
+    fallback must never drop a record some ray hits."""
+    rng = np.random.default_rng(23)
+    tris = []
+    for _ in range(600):  # crossing / behind / around the eye
+        tris.append(list(rng.uniform(-3, 3, 9)))
+    for _ in range(600):  # slivers and needles in front
+        a = rng.uniform([-1, -1, 1], [1, 1, 4])
+        d = rng.normal(size=3)
+        b = a + d * rng.uniform(0.01, 2.0)
+        c = a + d * rng.uniform(0.01, 2.0) + rng.normal(size=3) * 10.0 ** rng.uniform(-6, -2)
+        tris.append(list(np.concatenate([a, b, c])))
+    for _ in range(300):  # tiny, far and near
+        a = rng.uniform([-1, -1, 0.05], [1, 1, 50])
+        tris.append(list(np.concatenate([a, a + rng.normal(size=3) * 1e-3, a + rng.normal(size=3) * 1e-3])))
+    albedo = rng.uniform(0.2, 1.0, (len(tris), 3))
+    path = write_custom_scene(tmp_path / "nasty.srt", tris, albedo)
+    rng2 = np.random.default_rng(8)
+    offsets = rng2.random((90, 120, 2), dtype=np.float32)
+    for off in (None, offsets):
+        ref = oracle_render(path, 120, 90, off)
+        for shape in CULL_SHAPES:
+            monkeypatch.setenv("SRT_CULL_SHAPE", shape)
+            assert_parity(torch_render(path, 120, 90, off, variant="cull"), ref)
 
 
 def test_extreme_offsets(gpu, scenes):
