@@ -21,7 +21,12 @@ OBJS := $(BUILD)/render.o $(BUILD)/renderer.o $(BUILD)/scene.o $(BUILD)/image.o 
 
 HEADERS := $(wildcard $(CSRC)/*.h) include/model_runner.h include/srt_render.h
 
-.PHONY: all oracle ref clean
+# Diagnostic build (per-block cull phase counters, srtDiagRead): never the product library.
+DIAG_BUILD := build/diag
+DIAG_LIB   := simpleraytracer_amd/lib_diag/libModelRunner.so
+DIAG_OBJS  := $(patsubst $(BUILD)/%,$(DIAG_BUILD)/%,$(OBJS))
+
+.PHONY: all oracle ref clean diag
 all: $(LIB) bin/test_app
 
 $(BUILD)/%.o: $(CSRC)/%.hip $(HEADERS)
@@ -40,6 +45,20 @@ bin/test_app: tools/test_app.cpp $(LIB) include/model_runner.h include/srt_rende
 	@mkdir -p bin
 	g++ -O2 -std=c++17 -Wall -Iinclude $< -o $@ -L$(LIBDIR) -lModelRunner -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)'
 
+$(DIAG_BUILD)/%.o: $(CSRC)/%.hip $(HEADERS)
+	@mkdir -p $(DIAG_BUILD)
+	$(HIPCC) $(HIPFLAGS) -DSRT_DIAG -c $< -o $@
+
+$(DIAG_BUILD)/%.o: $(CSRC)/%.cpp $(HEADERS)
+	@mkdir -p $(DIAG_BUILD)
+	$(HIPCC) $(HIPFLAGS) -DSRT_DIAG -c $< -o $@
+
+$(DIAG_LIB): $(DIAG_OBJS)
+	@mkdir -p $(dir $(DIAG_LIB))
+	$(HIPCC) --offload-arch=$(ARCH) $(DIAG_OBJS) -o $@ $(LDFLAGS)
+
+diag: $(DIAG_LIB)
+
 oracle:
 	$(MAKE) -C oracle
 
@@ -47,5 +66,5 @@ ref:
 	$(MAKE) -C oracle ref
 
 clean:
-	rm -rf build bin $(LIBDIR)
+	rm -rf build bin $(LIBDIR) $(dir $(DIAG_LIB))
 	$(MAKE) -C oracle clean

@@ -12,6 +12,9 @@ from pathlib import Path
 
 PACKAGE_DIR = Path(__file__).resolve().parent
 LIB_PATH = PACKAGE_DIR / "lib" / "libModelRunner.so"
+# Diagnostic runs only (tools/diag_cull.py): SRT_LIB points at the `make diag` build.
+if os.environ.get("SRT_LIB"):
+    LIB_PATH = Path(os.environ["SRT_LIB"])
 
 ML_OK = 0
 ML_FAIL = 1

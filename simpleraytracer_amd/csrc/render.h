@@ -37,8 +37,13 @@ constexpr int kTileFloat4 = kTileTriangles * 5 / 2;  // 640 float4 = 10 KiB per 
 // order, right after the tiles. They bound only rays with |fx|, |fy| <= kScreenBoxRange.
 constexpr float kScreenBoxRange = 4.0f;
 
-// Floats per record in the edge allocation: 10 (tiles) + 4 (screen box).
-constexpr int kEdgeFloatsPerTriangle = 14;
+// Quantized screen boxes (the cull kernel's streamed copy): one uint2 per record, in record
+// order, after the float boxes: x = lo | hi << 16, y = lo | hi << 16 as int16 fixed point
+// q = v * kQuantScale, lo rounded down and hi up, both clamped to the int16 range.
+constexpr float kQuantScale = 4096.0f;
+
+// Floats per record in the edge allocation: 10 (tiles) + 4 (screen box) + 2 (quantized box).
+constexpr int kEdgeFloatsPerTriangle = 16;
 
 inline std::uint64_t PaddedTriangleCount(std::uint64_t n) {
     const std::uint64_t p = (n + kPadTriangles - 1) / kPadTriangles * kPadTriangles;
@@ -69,5 +74,10 @@ hipError_t LaunchPrepare(const float* d_vertices, std::uint64_t n, const Frame& 
 hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_vertices, const float* d_albedo,
                        const Frame& frame, const float background[3], const BandArgs& band, int variant,
                        hipStream_t stream);
+
+#ifdef SRT_DIAG
+// Diagnostic build only: copy the cull kernel's per-block phase counters to host memory.
+hipError_t DiagRead(void* host, std::size_t bytes);
+#endif
 
 }  // namespace srt

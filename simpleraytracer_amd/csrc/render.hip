@@ -11,6 +11,18 @@
 #include <cstring>
 
 namespace srt {
+
+#ifdef SRT_DIAG
+// Diagnostic build only (make diag): per-block phase cycle counts of the cull kernel.
+// [block][0] stream cycles, [1] gather cycles, [2] filter+walk cycles, [3] block survivors,
+// [4] wave-0 survivors walked, [5] flush batches, [6] total cycles, [7] unused.
+constexpr int kDiagBlocks = 16384;
+__device__ unsigned long long g_srt_diag[kDiagBlocks][8];
+#define SRT_STAMP(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#else
+#define SRT_STAMP(v)
+#endif
+
 namespace {
 
 constexpr int kWave = 64;
@@ -20,6 +32,7 @@ constexpr int kRowsPerLane = 8;  // rays per lane (LDS / scalar variants): one c
 struct TraceParams {
     const float4* __restrict__ edges;
     const float4* __restrict__ screen_boxes;
+    const uint2* __restrict__ qboxes;
     const float* __restrict__ vertices;
     const float* __restrict__ albedo;
     const float2* __restrict__ offsets;
@@ -29,6 +42,7 @@ struct TraceParams {
     int width;
     int row_count;
     int row_begin;
+    int allow_raster;  // cull variant: raster walk for uniform-offset blocks (env SRT_CULL_RASTER=0 disables)
     float wf;
     float hf;
     float base[3];
@@ -41,6 +55,7 @@ struct PrepareParams {
     const float* __restrict__ vertices;
     float4* __restrict__ edges;
     float4* __restrict__ screen_boxes;
+    uint2* __restrict__ qboxes;
     unsigned n;
     unsigned n_pad;
     float origin[3];
@@ -129,6 +144,20 @@ __device__ float4 ScreenBox(const float c[9]) {
     return make_float4(DownF(xlo), UpF(xhi), DownF(ylo), UpF(yhi));
 }
 
+// int16 fixed point of a screen-box coordinate, rounded down (lo) or up (hi), clamped; the
+// map is monotone, so an overlap of two real boxes is an overlap of their quantized boxes.
+__device__ __forceinline__ int QuantLo(float v) {
+    const float q = floorf(v * kQuantScale);  // exact scaling (power of two), NaN -> clamp below
+    return q >= 32767.f ? 32767 : (q >= -32768.f ? static_cast<int>(q) : -32768);
+}
+__device__ __forceinline__ int QuantHi(float v) {
+    const float q = ceilf(v * kQuantScale);
+    return q <= -32768.f ? -32768 : (q <= 32767.f ? static_cast<int>(q) : 32767);
+}
+__device__ __forceinline__ unsigned PackQ(int lo, int hi) {
+    return (static_cast<unsigned>(lo) & 0xFFFFu) | (static_cast<unsigned>(hi) << 16);
+}
+
 // One thread per triangle: origin-relative edge normals nA = B x C, nB = C x A, nC = A x B
 // (A, B, C = vertices - eye), signed volume vol = A . nA, orientation normalised so vol > 0,
 // then each normal projected onto the affine ray frame: E(fx, fy) = n . (base + fx du + fy dv).
@@ -185,8 +214,10 @@ __global__ __launch_bounds__(256) void PrepareKernel(PrepareParams p) {
     p2[j] = c[8];
     p3[j] = vol;
     // Disabled records: an empty box (culled by every ray box the screen boxes apply to).
-    p.screen_boxes[i] = disabled ? make_float4(__builtin_inff(), -__builtin_inff(), __builtin_inff(), -__builtin_inff())
-                                 : ScreenBox(c);
+    const float4 sb = disabled ? make_float4(__builtin_inff(), -__builtin_inff(), __builtin_inff(), -__builtin_inff())
+                               : ScreenBox(c);
+    p.screen_boxes[i] = sb;
+    p.qboxes[i] = make_uint2(PackQ(QuantLo(sb.x), QuantHi(sb.y)), PackQ(QuantLo(sb.z), QuantHi(sb.w)));
 }
 
 // Per-lane ray state: R rays sharing one image column.
@@ -485,7 +516,7 @@ __global__ __launch_bounds__(kWave) void TraceScalarKernel(TraceParams p) {
 // Variant 2: hierarchical cull ("packet-frustum" brute force). Block = W waves; wave w owns
 // 64 columns x R rows, the block 64 columns x W*R rows. Every record of the scene is still
 // visited by every block, in three exact levels:
-//   1. block: one lane per record streams the 16-B screen boxes (PrepareKernel, "Screen
+//   1. block: one lane per record streams the 8-B quantized screen boxes (PrepareKernel, "Screen
 //      box"), G records per lane per step loaded one step ahead, and tests them against
 //      the block's (fx, fy) box; the ids of survivors are appended (wave ballot + prefix
 //      popcount) to the wave's LDS id list;
@@ -518,6 +549,19 @@ __device__ __forceinline__ bool ScreenBoxUsable(const Box& b) {
 // Screen box (xlo, xhi, ylo, yhi) of a record overlaps the ray box.
 __device__ __forceinline__ bool ScreenBoxOverlaps(const Box& b, const float4& sb) {
     return !(sb.y < b.xlo || sb.x > b.xhi || sb.w < b.ylo || sb.z > b.yhi);
+}
+
+// Quantized ray box (lo down, hi up) for the streamed int16 screen boxes.
+struct QBox {
+    int xlo, xhi, ylo, yhi;
+};
+__device__ __forceinline__ QBox Quantize(const Box& b) {
+    return QBox{QuantLo(b.xlo), QuantHi(b.xhi), QuantLo(b.ylo), QuantHi(b.yhi)};
+}
+__device__ __forceinline__ bool QBoxOverlaps(const QBox& b, uint2 q) {
+    const int qxlo = __builtin_amdgcn_sbfe(static_cast<int>(q.x), 0, 16), qxhi = static_cast<int>(q.x) >> 16;
+    const int qylo = __builtin_amdgcn_sbfe(static_cast<int>(q.y), 0, 16), qyhi = static_cast<int>(q.y) >> 16;
+    return !(qxhi < b.xlo || qxlo > b.xhi || qyhi < b.ylo || qylo > b.yhi);
 }
 
 // Exact test of one record against every ray of the lane (records in any order): the
@@ -597,11 +641,68 @@ struct CullShared {
     int counts[2][W];
     Box wave_box[W];
     unsigned shared_fx;
+    unsigned regular;
+    // Raster walk only: per-pixel lexicographic (t, id) keys of each wave's 8 x 64 rays.
+    unsigned long long keys[W][8][kWave];
 };
 
-template <int R, int W, int G, bool SHARED>
+// (t, id) packed so that unsigned order is lexicographic order: t >= 0 here (vol > 0,
+// det > 0), so its bit pattern orders like the value.
+__device__ __forceinline__ unsigned long long HitKey(float t, int id) {
+    return (static_cast<unsigned long long>(__float_as_uint(t)) << 32) | static_cast<unsigned>(id);
+}
+
+// Raster walk of one wave-survivor (blocks whose rays all use the same sample offset: fx
+// depends only on the column = lane, fy only on the row). The screen box picks the
+// contiguous column range (lanes) and row range it can touch; those pixels are tested
+// exactly, lane-parallel, 64 pixels per round (rows packed when the range is narrow), and
+// each hit is merged into the pixel's key with an LDS atomic min. Same exact test and the
+// same lexicographic result as ExactTestAnyOrder.
+template <int R>
+__device__ __forceinline__ void RasterSurvivor(unsigned long long (*keys)[kWave], const Record& q, float vol, int id,
+                                               const float4& sb, bool use_sb, float fx0, float fy_lane, int lane) {
+    static_assert(R == 8, "raster walk packs 8 rows per wave");
+    unsigned long long cm = ~0ull;
+    unsigned rm = 0xFFu;
+    if (use_sb) {
+        cm = __ballot(fx0 >= sb.x && fx0 <= sb.y);
+        rm = static_cast<unsigned>(__ballot(fy_lane >= sb.z && fy_lane <= sb.w)) & 0xFFu;
+        if (cm == 0ull || rm == 0u) {
+            return;
+        }
+    }
+    const int c0 = __builtin_ctzll(cm), c1 = 63 - __builtin_clzll(cm);
+    const int r0 = __builtin_ctz(rm), r1 = 31 - __builtin_clz(rm);
+    const int ncols = c1 - c0 + 1;
+    const int lg = ncols <= 1 ? 0 : 32 - __builtin_clz(static_cast<unsigned>(ncols - 1));  // ceil(log2)
+    const int col = c0 + (lane & ((1 << lg) - 1));
+    const int step = kWave >> lg;
+#pragma unroll 1
+    for (int rr = r0; rr <= r1; rr += step) {
+        const int row = rr + (lane >> lg);
+        const float fx = __shfl(fx0, col);
+        const float fy = __shfl(fy_lane, row & 7);
+        if (col <= c1 && row <= r1) {
+            const float eA = fmaf(fy, q.cyA, fmaf(fx, q.cxA, q.c0A));
+            const float eB = fmaf(fy, q.cyB, fmaf(fx, q.cxB, q.c0B));
+            const float eC = fmaf(fy, q.cyC, fmaf(fx, q.cxC, q.c0C));
+            if (eA >= 0.f && eB >= 0.f && eC >= 0.f) {
+                const float det = (eA + eB) + eC;
+                if (det > 0.f) {
+                    const float t = vol / det;
+                    if (t < __builtin_inff()) {
+                        __hip_atomic_fetch_min(&keys[row][col], HitKey(t, id), __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
+                }
+            }
+        }
+    }
+}
+
+template <int R, int W, int G, bool SHARED, bool RASTER>
 __device__ __forceinline__ void CullWalk(const TraceParams& p, CullShared<W, G>& sh, Rays<R>& s, const Box& bb,
-                                         const Box& wb) {
+                                         const Box& wb, float oy) {
     constexpr int kThreads = kWave * W;
     constexpr int kStep = kThreads * G;
     constexpr int kBatch = CullShared<W, G>::kBatch;
@@ -609,19 +710,38 @@ __device__ __forceinline__ void CullWalk(const TraceParams& p, CullShared<W, G>&
     const int lane = tid & (kWave - 1);
     const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);
     const float4* __restrict__ sbox = p.screen_boxes;
+    const uint2* __restrict__ qbox = p.qboxes;
     const bool block_sb = ScreenBoxUsable(bb);
+    const QBox bq = Quantize(bb);
     const bool wave_sb = ScreenBoxUsable(wb);
     const unsigned long long lt_mask = (1ull << lane) - 1ull;
     const unsigned nsteps = p.n_pad / kStep;
+    // Raster walk: lane r (< 8) carries row r's fy, recomputed with GenerateRays' expression
+    // (bit-identical: every ray of a raster block has the same offset).
+    float fy_lane = 0.f;
+    if constexpr (RASTER) {
+        const int y0 = (blockIdx.y * W + wave) * R;
+        const int yc = min(y0 + (lane & 7), p.row_count - 1);
+        fy_lane = (static_cast<float>(p.row_begin + yc) + oy) / p.hf;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            sh.keys[wave][r][lane] = ~0ull;
+        }
+    }
 
-    float4 nb[G];
+#ifdef SRT_DIAG
+    unsigned long long d_stream = 0, d_gather = 0, d_walk = 0, d_surv = 0, d_wsurv = 0, d_batches = 0;
+    const unsigned long long d_t0 = __builtin_amdgcn_s_memtime();
+    unsigned long long d_mark = d_t0;
+#endif
+    uint2 nb[G];
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-        nb[g] = sbox[g * kThreads + tid];
+        nb[g] = qbox[g * kThreads + tid];
     }
     int mine = 0;  // ids in this wave's list (wave-uniform)
     for (unsigned k = 0; k < nsteps; ++k) {
-        float4 cb[G];
+        uint2 cb[G];
 #pragma unroll
         for (int g = 0; g < G; ++g) {
             cb[g] = nb[g];
@@ -629,14 +749,13 @@ __device__ __forceinline__ void CullWalk(const TraceParams& p, CullShared<W, G>&
         if (k + 1 < nsteps) {
 #pragma unroll
             for (int g = 0; g < G; ++g) {
-                nb[g] = sbox[(k + 1) * kStep + g * kThreads + tid];
+                nb[g] = qbox[(k + 1) * kStep + g * kThreads + tid];
             }
         }
 #pragma unroll
         for (int g = 0; g < G; ++g) {
-            // NaN boxes (disabled records) fail every comparison -> overlap -> the wave
-            // level drops them (their edge values are NaN: never a hit).
-            const bool pass = !block_sb || ScreenBoxOverlaps(bb, cb[g]);
+            // Disabled records carry empty boxes; unbounded ones span the int16 range.
+            const bool pass = !block_sb || QBoxOverlaps(bq, cb[g]);
             const unsigned long long m = __ballot(pass);
             if (pass) {
                 sh.ids[wave][mine + __popcll(m & lt_mask)] = k * kStep + g * kThreads + tid;
@@ -658,6 +777,14 @@ __device__ __forceinline__ void CullWalk(const TraceParams& p, CullShared<W, G>&
         if (total < kBatch && k + 1 < nsteps) {  // block-uniform
             continue;
         }
+#ifdef SRT_DIAG
+        {
+            const unsigned long long now = __builtin_amdgcn_s_memtime();
+            d_stream += now - d_mark;
+            d_mark = now;
+            d_surv += total;
+        }
+#endif
         // Flush: gather every listed record in batches of kBatch, then filter + walk.
 #pragma unroll 1
         for (int b0 = 0; b0 < total; b0 += kBatch) {
@@ -681,6 +808,14 @@ __device__ __forceinline__ void CullWalk(const TraceParams& p, CullShared<W, G>&
                 sh.st3[tid] = sbox[id];
             }
             __syncthreads();
+#ifdef SRT_DIAG
+            {
+                const unsigned long long now = __builtin_amdgcn_s_memtime();
+                d_gather += now - d_mark;
+                d_mark = now;
+                ++d_batches;
+            }
+#endif
             const int nb_here = min(kBatch, total - b0);
 #pragma unroll 1
             for (int c0 = 0; c0 < nb_here; c0 += kWave) {
@@ -692,17 +827,72 @@ __device__ __forceinline__ void CullWalk(const TraceParams& p, CullShared<W, G>&
                     pass = (!wave_sb || ScreenBoxOverlaps(wb, sh.st3[i])) && BoxMayHit(wb, r);
                 }
                 unsigned long long m = __ballot(pass);
-                while (m != 0ull) {
-                    const int bit = __builtin_ctzll(m);
-                    m &= m - 1ull;
-                    const float4 a = sh.st0[c0 + bit], b = sh.st1[c0 + bit], x = sh.st2[c0 + bit];
-                    const Record r{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, x.x};
-                    ExactTestAnyOrder<R, SHARED>(s, r, x.y, __float_as_int(x.z));
+#ifdef SRT_DIAG
+                d_wsurv += __popcll(m);
+#endif
+                if (m != 0ull) {
+                    // Software-pipelined: the next survivor's LDS reads are issued before the
+                    // current one is tested, so their latency hides behind its work.
+                    int bit = __builtin_ctzll(m);
+                    float4 a = sh.st0[c0 + bit], b = sh.st1[c0 + bit], x = sh.st2[c0 + bit];
+                    float4 sb = RASTER ? sh.st3[c0 + bit] : make_float4(0.f, 0.f, 0.f, 0.f);
+                    for (;;) {
+                        m &= m - 1ull;
+                        const bool more = m != 0ull;
+                        const int nbit = more ? __builtin_ctzll(m) : bit;
+                        const float4 an = sh.st0[c0 + nbit], bn = sh.st1[c0 + nbit], xn = sh.st2[c0 + nbit];
+                        const float4 sbn = RASTER ? sh.st3[c0 + nbit] : sb;
+                        const Record r{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, x.x};
+                        if constexpr (RASTER) {
+                            RasterSurvivor<R>(sh.keys[wave], r, x.y, __float_as_int(x.z), sb, wave_sb, s.fx[0],
+                                              fy_lane, lane);
+                        } else {
+                            ExactTestAnyOrder<R, SHARED>(s, r, x.y, __float_as_int(x.z));
+                        }
+                        if (!more) {
+                            break;
+                        }
+                        a = an;
+                        b = bn;
+                        x = xn;
+                        sb = sbn;
+                    }
                 }
             }
             __syncthreads();  // staging (and, after the last batch, the id lists) reused next
+#ifdef SRT_DIAG
+            {
+                const unsigned long long now = __builtin_amdgcn_s_memtime();
+                d_walk += now - d_mark;
+                d_mark = now;
+            }
+#endif
         }
         mine = 0;
+    }
+#ifdef SRT_DIAG
+    const unsigned blk = blockIdx.y * gridDim.x + blockIdx.x;
+    if (tid == 0 && blk < kDiagBlocks) {
+        unsigned long long* d = g_srt_diag[blk];
+        d[0] = d_stream;
+        d[1] = d_gather;
+        d[2] = d_walk;
+        d[3] = d_surv;
+        d[4] = d_wsurv;
+        d[5] = d_batches;
+        d[6] = __builtin_amdgcn_s_memtime() - d_t0;
+        d[7] = RASTER ? 1 : 0;
+    }
+#endif
+    if constexpr (RASTER) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const unsigned long long key = sh.keys[wave][r][lane];
+            if (key != ~0ull) {
+                s.bt[r] = __uint_as_float(static_cast<unsigned>(key >> 32));
+                s.bi[r] = static_cast<int>(static_cast<unsigned>(key));
+            }
+        }
     }
 }
 
@@ -719,8 +909,27 @@ __global__ __launch_bounds__(kWave * W) void TraceCullKernel(TraceParams p) {
     Box lane_box;
     const bool same = GenerateRays<R>(p, x, y0, s, lane_box);
     const Box wb = WaveReduceBox(lane_box);
+    // Raster walk eligibility: every ray of the block has the block's first sample offset
+    // (bit pattern), so fx depends on the column only and fy on the row only.
+    bool regular = R == 8;
+    float oy0;
+    {
+        const int x0 = min(static_cast<int>(blockIdx.x) * kWave, p.width - 1);
+        const int yb = min(static_cast<int>(blockIdx.y) * W * R, p.row_count - 1);
+        const float2 o0 = p.offsets[static_cast<size_t>(yb) * p.width + x0];
+        oy0 = o0.y;
+        const int xc = min(x, p.width - 1);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int yc = min(y0 + r, p.row_count - 1);
+            const float2 o = p.offsets[static_cast<size_t>(yc) * p.width + xc];
+            regular = regular && __float_as_uint(o.x) == __float_as_uint(o0.x) &&
+                      __float_as_uint(o.y) == __float_as_uint(o0.y);
+        }
+    }
     if (tid == 0) {
         sh.shared_fx = 1u;
+        sh.regular = 1u;
     }
     __syncthreads();
     if (lane == 0) {
@@ -729,6 +938,9 @@ __global__ __launch_bounds__(kWave * W) void TraceCullKernel(TraceParams p) {
     if (!__all(same) && lane == 0) {
         sh.shared_fx = 0u;
     }
+    if (!__all(regular) && lane == 0) {
+        sh.regular = 0u;
+    }
     __syncthreads();
     Box bb = sh.wave_box[0];
 #pragma unroll
@@ -736,16 +948,18 @@ __global__ __launch_bounds__(kWave * W) void TraceCullKernel(TraceParams p) {
         const Box o = sh.wave_box[w];
         bb = Box{fminf(bb.xlo, o.xlo), fmaxf(bb.xhi, o.xhi), fminf(bb.ylo, o.ylo), fmaxf(bb.yhi, o.yhi)};
     }
-    if (sh.shared_fx != 0u) {
-        CullWalk<R, W, G, true>(p, sh, s, bb, wb);
+    if (R == 8 && sh.regular != 0u && p.allow_raster != 0) {
+        CullWalk<R, W, G, true, R == 8>(p, sh, s, bb, wb, oy0);
+    } else if (sh.shared_fx != 0u) {
+        CullWalk<R, W, G, true, false>(p, sh, s, bb, wb, 0.f);
     } else {
-        CullWalk<R, W, G, false>(p, sh, s, bb, wb);
+        CullWalk<R, W, G, false, false>(p, sh, s, bb, wb, 0.f);
     }
     ShadeAndStore<R>(p, x, y0, s);
 }
 
 // Cull block shape: rows per lane x waves per block x records per lane per step; env
-// SRT_CULL_SHAPE = "RxWxG" (default 8x4x4; see kShapes), for measurement.
+// SRT_CULL_SHAPE = "RxWxG" (default 8x8x4; see kShapes), for measurement.
 struct CullShape {
     int rows;
     int waves;
@@ -764,10 +978,16 @@ CullShape CullShapeFromEnv() {
             }
         }
     }
-    return {8, 4, 4};
+    return {8, 8, 4};
 }
 
 }  // namespace
+
+#ifdef SRT_DIAG
+hipError_t DiagRead(void* host, std::size_t bytes) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_srt_diag), bytes < sizeof(g_srt_diag) ? bytes : sizeof(g_srt_diag));
+}
+#endif
 
 hipError_t LaunchPrepare(const float* d_vertices, std::uint64_t n, const Frame& frame, float* d_edges,
                          hipStream_t stream) {
@@ -775,6 +995,7 @@ hipError_t LaunchPrepare(const float* d_vertices, std::uint64_t n, const Frame& 
     p.vertices = d_vertices;
     p.edges = reinterpret_cast<float4*>(d_edges);
     p.screen_boxes = reinterpret_cast<float4*>(d_edges) + PaddedTriangleCount(n) / kTileTriangles * kTileFloat4;
+    p.qboxes = reinterpret_cast<uint2*>(p.screen_boxes + PaddedTriangleCount(n));
     p.n = static_cast<unsigned>(n);
     p.n_pad = static_cast<unsigned>(PaddedTriangleCount(n));
     for (int k = 0; k < 3; ++k) {
@@ -797,6 +1018,7 @@ hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_ver
     TraceParams p{};
     p.edges = reinterpret_cast<const float4*>(d_edges);
     p.screen_boxes = reinterpret_cast<const float4*>(d_edges) + PaddedTriangleCount(n) / kTileTriangles * kTileFloat4;
+    p.qboxes = reinterpret_cast<const uint2*>(p.screen_boxes + PaddedTriangleCount(n));
     p.vertices = d_vertices;
     p.albedo = d_albedo;
     p.offsets = reinterpret_cast<const float2*>(band.offsets);
@@ -806,6 +1028,10 @@ hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_ver
     p.width = static_cast<int>(band.width);
     p.row_count = static_cast<int>(band.row_count);
     p.row_begin = static_cast<int>(band.row_begin);
+    {
+        const char* r = std::getenv("SRT_CULL_RASTER");
+        p.allow_raster = (r != nullptr && std::strcmp(r, "0") == 0) ? 0 : 1;
+    }
     p.wf = static_cast<float>(band.width);
     p.hf = static_cast<float>(band.height);
     for (int k = 0; k < 3; ++k) {

@@ -140,4 +140,11 @@ ML_API_ENTRY int srtTraceAsync(srt_device_scene scene, const float* d_offsets, f
     });
 }
 
+#ifdef SRT_DIAG
+// Diagnostic build only (make diag): not part of include/srt_render.h.
+ML_API_ENTRY int srtDiagRead(void* host, size_t bytes) {
+    return Guarded([&] { srt::HipCheck(srt::DiagRead(host, bytes), "srtDiagRead"); });
+}
+#endif
+
 }  // extern "C"

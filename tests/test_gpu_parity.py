@@ -162,6 +162,20 @@ def test_cull_shapes(gpu, scenes, monkeypatch, shape):
     assert_parity(got, oracle_render(scenes["soup2k"], w, h, offsets))
 
 
+@pytest.mark.parametrize("raster", ["1", "0"])
+@pytest.mark.parametrize("offset", [0.5, 0.0, 0.999, -3.25, 7.5])
+def test_cull_uniform_offsets(gpu, scenes, monkeypatch, raster, offset):
+    """Uniform (per-frame constant) sample offsets: the raster walk (blocks whose rays share
+    one offset) and, with SRT_CULL_RASTER=0, the per-lane walk on the same frames."""
+    monkeypatch.setenv("SRT_CULL_RASTER", raster)
+    w, h = 211, 97
+    offsets = np.full((h, w, 2), offset, np.float32)
+    ref = oracle_render(scenes["soup2k"], w, h, offsets)
+    for shape in ("8x4x4", "8x8x2"):
+        monkeypatch.setenv("SRT_CULL_SHAPE", shape)
+        assert_parity(torch_render(scenes["soup2k"], w, h, offsets, variant="cull"), ref)
+
+
 def test_cull_survivor_overflow_and_ties(gpu, tmp_path, monkeypatch):
     """Every record survives the block cull (large overlapping triangles, many exact
     duplicates spread over several cull steps): survivor lists fill and flush repeatedly,
@@ -179,9 +193,11 @@ def test_cull_survivor_overflow_and_ties(gpu, tmp_path, monkeypatch):
     path = write_custom_scene(tmp_path / "dense.srt", tris, albedo)
     ref = oracle_render(path, 96, 80)
     assert (ref[..., 3] == 3).mean() > 0.3
-    for shape in CULL_SHAPES:
-        monkeypatch.setenv("SRT_CULL_SHAPE", shape)
-        assert_parity(torch_render(path, 96, 80, variant="cull"), ref)
+    for raster in ("1", "0"):
+        monkeypatch.setenv("SRT_CULL_RASTER", raster)
+        for shape in CULL_SHAPES:
+            monkeypatch.setenv("SRT_CULL_SHAPE", shape)
+            assert_parity(torch_render(path, 96, 80, variant="cull"), ref)
 
 
 def test_cull_nasty_geometry(gpu, tmp_path, monkeypatch):
