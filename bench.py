@@ -193,7 +193,7 @@ def main():
                 "spp": 1,
                 "parallelism": f"row-bands x{world}" + (" + RCCL gather" if world > 1 else ""),
                 "trace_variant": a.variant,
-                "cull_shape": os.environ.get("SRT_CULL_SHAPE", "8x8x4") if a.variant == "cull" else None,
+                "cull_shape": os.environ.get("SRT_CULL_SHAPE", "8x4x16") if a.variant == "cull" else None,
             },
             "roofline": {
                 "bound": "hbm",

@@ -18,10 +18,10 @@
 namespace srt {
 
 // Triangles per edge tile. The edge buffer is padded with disabled (all-NaN) records to a
-// multiple of kPadTriangles (the largest cull step: 512 threads x 4 records) so no trace
+// multiple of kPadTriangles (the largest cull step: 256 threads x 16 records) so no trace
 // loop has a tail; the per-ray variants stop after the last tile holding a real record.
 constexpr int kTileTriangles = 256;
-constexpr int kPadTriangles = 2048;
+constexpr int kPadTriangles = 4096;
 
 // Edge records, tile-planar: tile t (256 records, 10 KiB) = four planes, each indexed by the
 // record's position j in the tile, so a lane-per-record load is one coalesced 16-B or 4-B
@@ -38,8 +38,8 @@ constexpr int kTileFloat4 = kTileTriangles * 5 / 2;  // 640 float4 = 10 KiB per 
 constexpr float kScreenBoxRange = 4.0f;
 
 // Quantized screen boxes (the cull kernel's streamed copy): one uint2 per record, in record
-// order, after the float boxes: x = lo | hi << 16, y = lo | hi << 16 as int16 fixed point
-// q = v * kQuantScale, lo rounded down and hi up, both clamped to the int16 range.
+// order, after the float boxes: x = hi | (-lo) << 16, y likewise, as int16 fixed point
+// q = v * kQuantScale, lo rounded down and hi up, clamped to [-32767, 32767].
 constexpr float kQuantScale = 4096.0f;
 
 // Floats per record in the edge allocation: 10 (tiles) + 4 (screen box) + 2 (quantized box).

@@ -144,18 +144,20 @@ __device__ float4 ScreenBox(const float c[9]) {
     return make_float4(DownF(xlo), UpF(xhi), DownF(ylo), UpF(yhi));
 }
 
-// int16 fixed point of a screen-box coordinate, rounded down (lo) or up (hi), clamped; the
-// map is monotone, so an overlap of two real boxes is an overlap of their quantized boxes.
+// int16 fixed point of a screen-box coordinate, rounded down (lo) or up (hi), clamped to
+// [-32767, 32767]; the map is monotone, so an overlap of two real boxes is an overlap of
+// their quantized boxes. (Clamping lo upward at -32767 only matters for coordinates below
+// -8, where no ray box the screen boxes apply to, |fx|, |fy| <= 4, reaches.)
 __device__ __forceinline__ int QuantLo(float v) {
-    const float q = floorf(v * kQuantScale);  // exact scaling (power of two), NaN -> clamp below
-    return q >= 32767.f ? 32767 : (q >= -32768.f ? static_cast<int>(q) : -32768);
+    const float q = floorf(v * kQuantScale);  // exact scaling (power of two); NaN -> lowest
+    return q >= 32767.f ? 32767 : (q >= -32767.f ? static_cast<int>(q) : -32767);
 }
 __device__ __forceinline__ int QuantHi(float v) {
     const float q = ceilf(v * kQuantScale);
-    return q <= -32768.f ? -32768 : (q <= 32767.f ? static_cast<int>(q) : 32767);
+    return q <= -32767.f ? -32767 : (q <= 32767.f ? static_cast<int>(q) : 32767);
 }
-__device__ __forceinline__ unsigned PackQ(int lo, int hi) {
-    return (static_cast<unsigned>(lo) & 0xFFFFu) | (static_cast<unsigned>(hi) << 16);
+__device__ __forceinline__ unsigned PackI16(int low, int high) {
+    return (static_cast<unsigned>(low) & 0xFFFFu) | (static_cast<unsigned>(high) << 16);
 }
 
 // One thread per triangle: origin-relative edge normals nA = B x C, nB = C x A, nC = A x B
@@ -217,7 +219,8 @@ __global__ __launch_bounds__(256) void PrepareKernel(PrepareParams p) {
     const float4 sb = disabled ? make_float4(__builtin_inff(), -__builtin_inff(), __builtin_inff(), -__builtin_inff())
                                : ScreenBox(c);
     p.screen_boxes[i] = sb;
-    p.qboxes[i] = make_uint2(PackQ(QuantLo(sb.x), QuantHi(sb.y)), PackQ(QuantLo(sb.z), QuantHi(sb.w)));
+    // Stored as (hi, -lo) pairs so the cull test is one saturating packed add per axis.
+    p.qboxes[i] = make_uint2(PackI16(QuantHi(sb.y), -QuantLo(sb.x)), PackI16(QuantHi(sb.w), -QuantLo(sb.z)));
 }
 
 // Per-lane ray state: R rays sharing one image column.
@@ -551,17 +554,20 @@ __device__ __forceinline__ bool ScreenBoxOverlaps(const Box& b, const float4& sb
     return !(sb.y < b.xlo || sb.x > b.xhi || sb.w < b.ylo || sb.z > b.yhi);
 }
 
-// Quantized ray box (lo down, hi up) for the streamed int16 screen boxes.
+// Quantized ray box for the streamed int16 screen boxes, as the per-axis constants of the
+// packed test: a record's (hi, -lo) + (-box_lo, box_hi) = (hi - box_lo, box_hi - lo), and the
+// boxes overlap iff no half is negative (v_pk_add_i16 with clamp: saturation keeps signs).
+typedef short I16x2 __attribute__((ext_vector_type(2)));
 struct QBox {
-    int xlo, xhi, ylo, yhi;
+    unsigned x, y;
 };
 __device__ __forceinline__ QBox Quantize(const Box& b) {
-    return QBox{QuantLo(b.xlo), QuantHi(b.xhi), QuantLo(b.ylo), QuantHi(b.yhi)};
+    return QBox{PackI16(-QuantLo(b.xlo), QuantHi(b.xhi)), PackI16(-QuantLo(b.ylo), QuantHi(b.yhi))};
 }
-__device__ __forceinline__ bool QBoxOverlaps(const QBox& b, uint2 q) {
-    const int qxlo = __builtin_amdgcn_sbfe(static_cast<int>(q.x), 0, 16), qxhi = static_cast<int>(q.x) >> 16;
-    const int qylo = __builtin_amdgcn_sbfe(static_cast<int>(q.y), 0, 16), qyhi = static_cast<int>(q.y) >> 16;
-    return !(qxhi < b.xlo || qxlo > b.xhi || qyhi < b.ylo || qylo > b.yhi);
+__device__ __forceinline__ bool QBoxOverlaps(const QBox& b, unsigned qx, unsigned qy) {
+    const I16x2 sx = __builtin_elementwise_add_sat(__builtin_bit_cast(I16x2, qx), __builtin_bit_cast(I16x2, b.x));
+    const I16x2 sy = __builtin_elementwise_add_sat(__builtin_bit_cast(I16x2, qy), __builtin_bit_cast(I16x2, b.y));
+    return ((__builtin_bit_cast(unsigned, sx) | __builtin_bit_cast(unsigned, sy)) & 0x80008000u) == 0u;
 }
 
 // Exact test of one record against every ray of the lane (records in any order): the
@@ -734,31 +740,38 @@ __device__ __forceinline__ void CullWalk(const TraceParams& p, CullShared<W, G>&
     const unsigned long long d_t0 = __builtin_amdgcn_s_memtime();
     unsigned long long d_mark = d_t0;
 #endif
-    uint2 nb[G];
+    // Lane tid of step k reads records k * kStep + 2 * (l * kThreads + tid) + {0, 1} for
+    // l < G / 2: one 16-B load per record pair, the whole step one step ahead.
+    constexpr int L = G / 2;
+    const uint4* __restrict__ qbox4 = reinterpret_cast<const uint4*>(qbox);
+    uint4 nb[L];
 #pragma unroll
-    for (int g = 0; g < G; ++g) {
-        nb[g] = qbox[g * kThreads + tid];
+    for (int l = 0; l < L; ++l) {
+        nb[l] = qbox4[l * kThreads + tid];
     }
     int mine = 0;  // ids in this wave's list (wave-uniform)
     for (unsigned k = 0; k < nsteps; ++k) {
-        uint2 cb[G];
+        uint4 cb[L];
 #pragma unroll
-        for (int g = 0; g < G; ++g) {
-            cb[g] = nb[g];
+        for (int l = 0; l < L; ++l) {
+            cb[l] = nb[l];
         }
         if (k + 1 < nsteps) {
 #pragma unroll
-            for (int g = 0; g < G; ++g) {
-                nb[g] = qbox[(k + 1) * kStep + g * kThreads + tid];
+            for (int l = 0; l < L; ++l) {
+                nb[l] = qbox4[(k + 1) * (kStep / 2) + l * kThreads + tid];
             }
         }
 #pragma unroll
         for (int g = 0; g < G; ++g) {
+            const int l = g >> 1;
+            const unsigned qx = (g & 1) ? cb[l].z : cb[l].x;
+            const unsigned qy = (g & 1) ? cb[l].w : cb[l].y;
             // Disabled records carry empty boxes; unbounded ones span the int16 range.
-            const bool pass = !block_sb || QBoxOverlaps(bq, cb[g]);
+            const bool pass = !block_sb || QBoxOverlaps(bq, qx, qy);
             const unsigned long long m = __ballot(pass);
             if (pass) {
-                sh.ids[wave][mine + __popcll(m & lt_mask)] = k * kStep + g * kThreads + tid;
+                sh.ids[wave][mine + __popcll(m & lt_mask)] = k * kStep + 2 * (l * kThreads + tid) + (g & 1);
             }
             mine += __popcll(m);
         }
@@ -959,7 +972,7 @@ __global__ __launch_bounds__(kWave * W) void TraceCullKernel(TraceParams p) {
 }
 
 // Cull block shape: rows per lane x waves per block x records per lane per step; env
-// SRT_CULL_SHAPE = "RxWxG" (default 8x8x4; see kShapes), for measurement.
+// SRT_CULL_SHAPE = "RxWxG" (default 8x4x16; see kShapes), for measurement.
 struct CullShape {
     int rows;
     int waves;
@@ -969,7 +982,7 @@ struct CullShape {
 CullShape CullShapeFromEnv() {
     const char* v = std::getenv("SRT_CULL_SHAPE");
     if (v != nullptr) {
-        static const CullShape kShapes[] = {{8, 4, 1}, {8, 4, 2}, {8, 4, 4}, {8, 8, 2}, {8, 8, 4}, {16, 4, 4}};
+        static const CullShape kShapes[] = {{8, 4, 4}, {8, 4, 8}, {8, 4, 16}, {8, 8, 8}, {16, 4, 8}};
         for (const CullShape& c : kShapes) {
             char name[16];
             std::snprintf(name, sizeof(name), "%dx%dx%d", c.rows, c.waves, c.group);
@@ -978,7 +991,7 @@ CullShape CullShapeFromEnv() {
             }
         }
     }
-    return {8, 8, 4};
+    return {8, 4, 16};
 }
 
 }  // namespace
@@ -1049,14 +1062,13 @@ hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_ver
         const int rows_per_block = shape.rows * shape.waves;
         const unsigned gy = static_cast<unsigned>((band.row_count + rows_per_block - 1) / rows_per_block);
         const dim3 grid(gx, gy), block(kWave * shape.waves);
-        const int key = shape.rows * 100 + shape.waves * 10 + shape.group;
+        const int key = shape.rows * 100 + shape.waves * 10 + (shape.group == 16 ? 9 : shape.group);
         switch (key) {
-            case 841: hipLaunchKernelGGL((TraceCullKernel<8, 4, 1>), grid, block, 0, stream, p); break;
-            case 842: hipLaunchKernelGGL((TraceCullKernel<8, 4, 2>), grid, block, 0, stream, p); break;
-            case 882: hipLaunchKernelGGL((TraceCullKernel<8, 8, 2>), grid, block, 0, stream, p); break;
-            case 884: hipLaunchKernelGGL((TraceCullKernel<8, 8, 4>), grid, block, 0, stream, p); break;
-            case 1644: hipLaunchKernelGGL((TraceCullKernel<16, 4, 4>), grid, block, 0, stream, p); break;
-            default: hipLaunchKernelGGL((TraceCullKernel<8, 4, 4>), grid, block, 0, stream, p); break;
+            case 844: hipLaunchKernelGGL((TraceCullKernel<8, 4, 4>), grid, block, 0, stream, p); break;
+            case 848: hipLaunchKernelGGL((TraceCullKernel<8, 4, 8>), grid, block, 0, stream, p); break;
+            case 888: hipLaunchKernelGGL((TraceCullKernel<8, 8, 8>), grid, block, 0, stream, p); break;
+            case 1648: hipLaunchKernelGGL((TraceCullKernel<16, 4, 8>), grid, block, 0, stream, p); break;
+            default: hipLaunchKernelGGL((TraceCullKernel<8, 4, 16>), grid, block, 0, stream, p); break;
         }
     } else {
         constexpr int kRowsPerBlock = kRowsPerLane * kLdsWaves;

@@ -17,7 +17,7 @@ pytestmark = pytest.mark.gpu
 
 RGB_TOL = 1e-5
 VARIANTS = ("lds", "scalar", "cull")
-CULL_SHAPES = ("8x4x1", "8x4x2", "8x4x4", "8x8x2", "8x8x4", "16x4x4")
+CULL_SHAPES = ("8x4x4", "8x4x8", "8x4x16", "8x8x8", "16x4x8")
 
 
 def oracle_render(path, w, h, offsets=None, **kw):
@@ -171,7 +171,7 @@ def test_cull_uniform_offsets(gpu, scenes, monkeypatch, raster, offset):
     w, h = 211, 97
     offsets = np.full((h, w, 2), offset, np.float32)
     ref = oracle_render(scenes["soup2k"], w, h, offsets)
-    for shape in ("8x4x4", "8x8x2"):
+    for shape in ("8x4x16", "8x8x8"):
         monkeypatch.setenv("SRT_CULL_SHAPE", shape)
         assert_parity(torch_render(scenes["soup2k"], w, h, offsets, variant="cull"), ref)
 

@@ -46,7 +46,7 @@ def main():
         buf = np.zeros((16384, 8), np.uint64)
         assert lib.srtDiagRead(buf.ctypes.data, buf.nbytes) == 0, _native.last_error()
         scene.close()
-    shape = os.environ.get("SRT_CULL_SHAPE", "8x8x4")
+    shape = os.environ.get("SRT_CULL_SHAPE", "8x4x16")
     r, wv, _ = (int(v) for v in shape.split("x"))
     gx, gy = (w + 63) // 64, (h + r * wv - 1) // (r * wv)
     d = buf[: gx * gy].astype(np.float64)
