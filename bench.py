@@ -37,7 +37,7 @@ def parse():
     p.add_argument("--height", type=int, default=1080)
     p.add_argument("--scene", default="soup", choices=["soup", "cornell", "triangle"])
     p.add_argument("--triangles", type=int, default=100_000)
-    p.add_argument("--variant", default=os.environ.get("SRT_BENCH_VARIANT", "lds"), choices=["lds", "scalar", "cull"])
+    p.add_argument("--variant", default=os.environ.get("SRT_BENCH_VARIANT", "cull"), choices=["lds", "scalar", "cull"])
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample length")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive ml* API measurement")
@@ -193,7 +193,7 @@ def main():
                 "spp": 1,
                 "parallelism": f"row-bands x{world}" + (" + RCCL gather" if world > 1 else ""),
                 "trace_variant": a.variant,
-                "cull_shape": os.environ.get("SRT_CULL_SHAPE", "8x4x16") if a.variant == "cull" else None,
+                "cull_bins": os.environ.get("SRT_CULL_BIN", "1") != "0" if a.variant == "cull" else None,
             },
             "roofline": {
                 "bound": "hbm",

@@ -70,10 +70,25 @@ struct BandArgs {
 hipError_t LaunchPrepare(const float* d_vertices, std::uint64_t n, const Frame& frame, float* d_edges,
                          hipStream_t stream);
 
-// Launch the trace kernel over one band.
+// Bin lists of the cull variant's first level (render.hip BinKernel): per super-tile of a
+// band (128 x 32 pixels), up to `capacity` candidate record ids and their count.
+struct CullBins {
+    unsigned* lists;     // supers x capacity (+4 padding) ids
+    unsigned* counts;    // supers
+    unsigned capacity;
+    std::size_t supers;
+};
+
+// Super-tiles of a width x row_count band, and the per-list capacity used for n triangles
+// (a list that overflows makes its tiles stream every record; results are unaffected).
+std::size_t CullSuperTiles(std::size_t width, std::size_t row_count);
+unsigned CullBinCapacity(std::uint64_t n, std::size_t supers);
+
+// Launch the trace kernel over one band (cull variant: bin + trace; bins == nullptr streams
+// every record for every tile).
 hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_vertices, const float* d_albedo,
                        const Frame& frame, const float background[3], const BandArgs& band, int variant,
-                       hipStream_t stream);
+                       const CullBins* bins, hipStream_t stream);
 
 #ifdef SRT_DIAG
 // Diagnostic build only: copy the cull kernel's per-block phase counters to host memory.

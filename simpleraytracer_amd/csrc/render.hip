@@ -42,7 +42,10 @@ struct TraceParams {
     int width;
     int row_count;
     int row_begin;
-    int allow_raster;  // cull variant: raster walk for uniform-offset blocks (env SRT_CULL_RASTER=0 disables)
+    int allow_raster;  // cull variant: raster walk for uniform-offset tiles (env SRT_CULL_RASTER=0 disables)
+    const unsigned* __restrict__ bin_lists;   // cull variant: per super-tile candidate ids (BinKernel)
+    const unsigned* __restrict__ bin_counts;  // null: stream every record
+    unsigned bin_capacity;
     float wf;
     float hf;
     float base[3];
@@ -635,21 +638,36 @@ __device__ __forceinline__ void LoadRecord(const float4* __restrict__ edges, uns
     vol = Plane3(tile)[j];
 }
 
-template <int W, int G>
+// Cull tile = one trace block: 64 columns x 32 rows of rays, W waves (4, 8 or 16) of 64 x R
+// rays, R = 32 / W rays per lane. Constants that depend on W live in CullShape<W>.
+constexpr int kTileRows = 32;
+constexpr int kStreamStep = 4096;  // FULL stream: records per block per step
+constexpr int kListG = 4;          // LIST stream: ids per lane per step
+static_assert(kPadTriangles % kStreamStep == 0, "a stream step must cover whole pad units");
+
+template <int W>
+struct CullShape {
+    static constexpr int kR = kTileRows / W;              // rays per lane
+    static constexpr int kThreads = kWave * W;
+    static constexpr int kStreamG = kStreamStep / kThreads;  // FULL: records per lane per step
+    static constexpr int kBatch = kThreads;               // survivors gathered per flush batch
+    static constexpr int kListCap = kBatch + kStreamStep;  // block id list: < kBatch + one step
+};
+
+template <int W>
 struct CullShared {
-    static constexpr int kBatch = W * kWave;              // survivors gathered per flush batch
-    static constexpr int kListCap = kBatch + kWave * G;   // per-wave id list capacity
-    unsigned ids[W][kListCap];
-    float4 st0[kBatch];  // gathered records: plane 0
-    float4 st1[kBatch];  //                   plane 1
-    float4 st2[kBatch];  //                   (cyC, vol, id, 0)
-    float4 st3[kBatch];  //                   screen box
+    unsigned ids[CullShape<W>::kListCap];
+    float4 st0[CullShape<W>::kBatch];  // gathered records: plane 0
+    float4 st1[CullShape<W>::kBatch];  //                   plane 1
+    float4 st2[CullShape<W>::kBatch];  //                   (cyC, vol, id, 0)
+    float4 st3[CullShape<W>::kBatch];  //                   screen box
+    unsigned hit[CullShape<W>::kBatch];  // raster walk: record may touch the tile (box + edge tests)
     int counts[2][W];
     Box wave_box[W];
     unsigned shared_fx;
     unsigned regular;
-    // Raster walk only: per-pixel lexicographic (t, id) keys of each wave's 8 x 64 rays.
-    unsigned long long keys[W][8][kWave];
+    // Raster walk: per-pixel lexicographic (t, id) keys of the tile's 32 x 64 rays.
+    unsigned long long keys[kTileRows][kWave];
 };
 
 // (t, id) packed so that unsigned order is lexicographic order: t >= 0 here (vol > 0,
@@ -658,21 +676,21 @@ __device__ __forceinline__ unsigned long long HitKey(float t, int id) {
     return (static_cast<unsigned long long>(__float_as_uint(t)) << 32) | static_cast<unsigned>(id);
 }
 
-// Raster walk of one wave-survivor (blocks whose rays all use the same sample offset: fx
-// depends only on the column = lane, fy only on the row). The screen box picks the
-// contiguous column range (lanes) and row range it can touch; those pixels are tested
-// exactly, lane-parallel, 64 pixels per round (rows packed when the range is narrow), and
-// each hit is merged into the pixel's key with an LDS atomic min. Same exact test and the
-// same lexicographic result as ExactTestAnyOrder.
-template <int R>
+// Raster walk of one survivor over the whole tile (tiles whose rays all use the same sample
+// offset: fx depends only on the column = lane, fy only on the row). The screen box picks
+// the contiguous column range (lanes) and row range (of 32) it can touch; those pixels are
+// tested exactly, lane-parallel, 64 pixels per round (rows packed when the column range is
+// narrow), and each hit is merged into the pixel's key with an LDS atomic min. Same exact
+// test and the same lexicographic result as ExactTestAnyOrder; any wave may walk any
+// survivor, so a tile's survivors are shared evenly by its waves.
 __device__ __forceinline__ void RasterSurvivor(unsigned long long (*keys)[kWave], const Record& q, float vol, int id,
-                                               const float4& sb, bool use_sb, float fx0, float fy_lane, int lane) {
-    static_assert(R == 8, "raster walk packs 8 rows per wave");
+                                               const float4& sb, bool use_sb, float fx_lane, float fy_lane,
+                                               int lane) {
     unsigned long long cm = ~0ull;
-    unsigned rm = 0xFFu;
+    unsigned rm = 0xFFFFFFFFu;
     if (use_sb) {
-        cm = __ballot(fx0 >= sb.x && fx0 <= sb.y);
-        rm = static_cast<unsigned>(__ballot(fy_lane >= sb.z && fy_lane <= sb.w)) & 0xFFu;
+        cm = __ballot(fx_lane >= sb.x && fx_lane <= sb.y);
+        rm = static_cast<unsigned>(__ballot(fy_lane >= sb.z && fy_lane <= sb.w));  // lanes >= 32: NaN
         if (cm == 0ull || rm == 0u) {
             return;
         }
@@ -686,110 +704,165 @@ __device__ __forceinline__ void RasterSurvivor(unsigned long long (*keys)[kWave]
 #pragma unroll 1
     for (int rr = r0; rr <= r1; rr += step) {
         const int row = rr + (lane >> lg);
-        const float fx = __shfl(fx0, col);
-        const float fy = __shfl(fy_lane, row & 7);
+        const float fx = __shfl(fx_lane, col);
+        const float fy = __shfl(fy_lane, row & (kTileRows - 1));
         if (col <= c1 && row <= r1) {
             const float eA = fmaf(fy, q.cyA, fmaf(fx, q.cxA, q.c0A));
             const float eB = fmaf(fy, q.cyB, fmaf(fx, q.cxB, q.c0B));
             const float eC = fmaf(fy, q.cyC, fmaf(fx, q.cxC, q.c0C));
-            if (eA >= 0.f && eB >= 0.f && eC >= 0.f) {
-                const float det = (eA + eB) + eC;
-                if (det > 0.f) {
-                    const float t = vol / det;
-                    if (t < __builtin_inff()) {
-                        __hip_atomic_fetch_min(&keys[row][col], HitKey(t, id), __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_WORKGROUP);
-                    }
+            const float det = (eA + eB) + eC;
+            // all E >= 0 and det > 0 (NaN anywhere fails: det is then NaN)
+            if (fminf(fminf(eA, eB), eC) >= 0.f && det > 0.f) {
+                const float t = vol / det;
+                if (t < __builtin_inff()) {
+                    __hip_atomic_fetch_min(&keys[row][col], HitKey(t, id), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
             }
         }
     }
 }
 
-template <int R, int W, int G, bool SHARED, bool RASTER>
-__device__ __forceinline__ void CullWalk(const TraceParams& p, CullShared<W, G>& sh, Rays<R>& s, const Box& bb,
-                                         const Box& wb, float oy) {
-    constexpr int kThreads = kWave * W;
+// Per-tile source of candidate records for the cull stream: every record of the scene
+// (FULL), or the id list the bin kernel built for the tile's super-tile (LIST).
+struct CullSource {
+    const unsigned* list;  // LIST: ids
+    unsigned count;        // LIST: number of ids
+};
+
+// Streams the tile's candidates, keeps those whose quantized screen box overlaps the tile's
+// (bq) in a block-wide LDS id list, and walks the survivors in flushes: gather their records
+// into LDS, then either the raster walk (RASTER: survivors shared by the waves) or, per wave,
+// the wave-box filter and ExactTestAnyOrder over every survivor (the wave's rays only).
+template <int W, bool SHARED, bool RASTER, bool LIST>
+__device__ __forceinline__ void CullWalk(const TraceParams& p, CullShared<W>& sh, Rays<CullShape<W>::kR>& s,
+                                         const Box& bb, const Box& wb, float fx_lane, float fy_lane,
+                                         CullSource src) {
+    using S = CullShape<W>;
+    constexpr int R = S::kR;
+    constexpr int kThreads = S::kThreads;
+    constexpr int kBatch = S::kBatch;
+    constexpr int G = LIST ? kListG : S::kStreamG;
     constexpr int kStep = kThreads * G;
-    constexpr int kBatch = CullShared<W, G>::kBatch;
+    static_assert(G <= 32, "pass bits of a step live in one 32-bit mask");
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
     const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);
     const float4* __restrict__ sbox = p.screen_boxes;
     const uint2* __restrict__ qbox = p.qboxes;
     const bool block_sb = ScreenBoxUsable(bb);
-    const QBox bq = Quantize(bb);
     const bool wave_sb = ScreenBoxUsable(wb);
+    const QBox bq = Quantize(bb);
     const unsigned long long lt_mask = (1ull << lane) - 1ull;
-    const unsigned nsteps = p.n_pad / kStep;
-    // Raster walk: lane r (< 8) carries row r's fy, recomputed with GenerateRays' expression
-    // (bit-identical: every ray of a raster block has the same offset).
-    float fy_lane = 0.f;
-    if constexpr (RASTER) {
-        const int y0 = (blockIdx.y * W + wave) * R;
-        const int yc = min(y0 + (lane & 7), p.row_count - 1);
-        fy_lane = (static_cast<float>(p.row_begin + yc) + oy) / p.hf;
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            sh.keys[wave][r][lane] = ~0ull;
-        }
-    }
+    const unsigned nsteps = LIST ? (src.count + kStep - 1) / kStep : p.n_pad / kStep;
 
+    if constexpr (RASTER) {
+        for (int i = tid; i < kTileRows * kWave; i += kThreads) {
+            (&sh.keys[0][0])[i] = ~0ull;
+        }  // visible to every wave after the first stream barrier
+    }
 #ifdef SRT_DIAG
     unsigned long long d_stream = 0, d_gather = 0, d_walk = 0, d_surv = 0, d_wsurv = 0, d_batches = 0;
     const unsigned long long d_t0 = __builtin_amdgcn_s_memtime();
     unsigned long long d_mark = d_t0;
 #endif
-    // Lane tid of step k reads records k * kStep + 2 * (l * kThreads + tid) + {0, 1} for
-    // l < G / 2: one 16-B load per record pair, the whole step one step ahead.
-    constexpr int L = G / 2;
+    // FULL: lane tid of step k reads records k * kStep + 2 * (l * kThreads + tid) + {0, 1}
+    //       (one 16-B load per record pair); LIST: ids k * kStep + 4 * tid + {0..3} of the
+    //       list (one 16-B load) and their 8-B boxes. The whole step is loaded one step ahead.
+    constexpr int L = LIST ? 1 : G / 2;
     const uint4* __restrict__ qbox4 = reinterpret_cast<const uint4*>(qbox);
     uint4 nb[L];
+    uint4 nid = make_uint4(0u, 0u, 0u, 0u);
+    uint2 nq[LIST ? kListG : 1];
+    auto fetch = [&](unsigned k) {
+        if constexpr (LIST) {
+            const unsigned i0 = k * kStep + 4 * tid;
+            nid = i0 < src.count ? *reinterpret_cast<const uint4*>(src.list + i0) : make_uint4(0u, 0u, 0u, 0u);
+            const unsigned v[4] = {nid.x, nid.y, nid.z, nid.w};
 #pragma unroll
-    for (int l = 0; l < L; ++l) {
-        nb[l] = qbox4[l * kThreads + tid];
+            for (int g = 0; g < kListG; ++g) {
+                nq[g] = (i0 + g < src.count) ? qbox[v[g]] : make_uint2(0x80018001u, 0x80018001u);  // empty box
+            }
+        } else {
+#pragma unroll
+            for (int l = 0; l < L; ++l) {
+                nb[l] = qbox4[k * (kStep / 2) + l * kThreads + tid];
+            }
+        }
+    };
+    if (nsteps > 0) {
+        fetch(0);
     }
-    int mine = 0;  // ids in this wave's list (wave-uniform)
+    int total = 0;  // ids in the block list (block-uniform)
     for (unsigned k = 0; k < nsteps; ++k) {
         uint4 cb[L];
+        uint2 cq[LIST ? kListG : 1];
+        const uint4 cid = nid;
 #pragma unroll
         for (int l = 0; l < L; ++l) {
             cb[l] = nb[l];
         }
-        if (k + 1 < nsteps) {
 #pragma unroll
-            for (int l = 0; l < L; ++l) {
-                nb[l] = qbox4[(k + 1) * (kStep / 2) + l * kThreads + tid];
-            }
+        for (int g = 0; g < (LIST ? kListG : 1); ++g) {
+            cq[g] = nq[g];
         }
+        if (k + 1 < nsteps) {
+            fetch(k + 1);
+        }
+        auto record_id = [&](int g) -> unsigned {
+            if constexpr (LIST) {
+                return g == 0 ? cid.x : (g == 1 ? cid.y : (g == 2 ? cid.z : cid.w));
+            } else {
+                return k * kStep + 2 * ((g >> 1) * kThreads + tid) + (g & 1);
+            }
+        };
+        unsigned bits = 0u;
+        int wave_n = 0;
 #pragma unroll
         for (int g = 0; g < G; ++g) {
-            const int l = g >> 1;
-            const unsigned qx = (g & 1) ? cb[l].z : cb[l].x;
-            const unsigned qy = (g & 1) ? cb[l].w : cb[l].y;
-            // Disabled records carry empty boxes; unbounded ones span the int16 range.
-            const bool pass = !block_sb || QBoxOverlaps(bq, qx, qy);
-            const unsigned long long m = __ballot(pass);
-            if (pass) {
-                sh.ids[wave][mine + __popcll(m & lt_mask)] = k * kStep + 2 * (l * kThreads + tid) + (g & 1);
+            unsigned qx, qy;
+            if constexpr (LIST) {
+                qx = cq[g].x;
+                qy = cq[g].y;
+            } else {
+                qx = (g & 1) ? cb[g >> 1].z : cb[g >> 1].x;
+                qy = (g & 1) ? cb[g >> 1].w : cb[g >> 1].y;
             }
-            mine += __popcll(m);
+            // Disabled records carry empty boxes; unbounded ones span the int16 range. LIST
+            // padding lanes carry an empty box too (and LIST implies a usable tile box).
+            const bool pass = !block_sb || QBoxOverlaps(bq, qx, qy);
+            bits |= pass ? (1u << g) : 0u;
+            wave_n += __popcll(__ballot(pass));
         }
         const unsigned ph = k & 1u;
         if (lane == 0) {
-            sh.counts[ph][wave] = mine;
+            sh.counts[ph][wave] = wave_n;
         }
         __syncthreads();
-        int c[W];
-        int total = 0;
+        int off = total;
+        int step_n = 0;
 #pragma unroll
         for (int w = 0; w < W; ++w) {
-            c[w] = sh.counts[ph][w];
-            total += c[w];
+            const int cw = sh.counts[ph][w];
+            off += w < wave ? cw : 0;
+            step_n += cw;
         }
+        if (bits != 0u || step_n != 0) {
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                const bool pass = (bits >> g) & 1u;
+                const unsigned long long m = __ballot(pass);
+                if (pass) {
+                    sh.ids[off + __popcll(m & lt_mask)] = record_id(g);
+                }
+                off += __popcll(m);
+            }
+        }
+        total += step_n;
         if (total < kBatch && k + 1 < nsteps) {  // block-uniform
             continue;
         }
+        __syncthreads();  // every wave's ids are in the list
 #ifdef SRT_DIAG
         {
             const unsigned long long now = __builtin_amdgcn_s_memtime();
@@ -798,27 +871,26 @@ __device__ __forceinline__ void CullWalk(const TraceParams& p, CullShared<W, G>&
             d_surv += total;
         }
 #endif
-        // Flush: gather every listed record in batches of kBatch, then filter + walk.
+        // Flush: gather every listed record in batches of kBatch, then walk.
 #pragma unroll 1
         for (int b0 = 0; b0 < total; b0 += kBatch) {
             const int e = b0 + tid;
             if (e < total) {
-                int w = 0, j = e;
-#pragma unroll
-                for (int v = 0; v < W - 1; ++v) {
-                    if (w == v && j >= c[v]) {
-                        j -= c[v];
-                        w = v + 1;
-                    }
-                }
-                const unsigned id = sh.ids[w][j];
+                const unsigned id = sh.ids[e];
                 float4 p0, p1;
                 float cyC, vol;
                 LoadRecord(p.edges, id, p0, p1, cyC, vol);
+                const float4 sb = sbox[id];
                 sh.st0[tid] = p0;
                 sh.st1[tid] = p1;
                 sh.st2[tid] = make_float4(cyC, vol, __uint_as_float(id), 0.f);
-                sh.st3[tid] = sbox[id];
+                sh.st3[tid] = sb;
+                if constexpr (RASTER) {
+                    const Record r{p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w, cyC};
+                    sh.hit[tid] = ((!block_sb || ScreenBoxOverlaps(bb, sb)) && BoxMayHit(bb, r)) ? 1u : 0u;
+                }
+            } else if constexpr (RASTER) {
+                sh.hit[tid] = 0u;
             }
             __syncthreads();
 #ifdef SRT_DIAG
@@ -830,38 +902,26 @@ __device__ __forceinline__ void CullWalk(const TraceParams& p, CullShared<W, G>&
             }
 #endif
             const int nb_here = min(kBatch, total - b0);
-#pragma unroll 1
-            for (int c0 = 0; c0 < nb_here; c0 += kWave) {
-                const int i = c0 + lane;
-                bool pass = false;
-                if (i < nb_here) {
-                    const float4 a = sh.st0[i], b = sh.st1[i], x = sh.st2[i];
-                    const Record r{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, x.x};
-                    pass = (!wave_sb || ScreenBoxOverlaps(wb, sh.st3[i])) && BoxMayHit(wb, r);
-                }
-                unsigned long long m = __ballot(pass);
+            if constexpr (RASTER) {
+                // This wave's share of the batch: entries wave * 64 .. wave * 64 + 63.
+                const int c0 = wave * kWave;
+                unsigned long long m = __ballot(sh.hit[c0 + lane] != 0u);
 #ifdef SRT_DIAG
                 d_wsurv += __popcll(m);
 #endif
                 if (m != 0ull) {
                     // Software-pipelined: the next survivor's LDS reads are issued before the
-                    // current one is tested, so their latency hides behind its work.
+                    // current one is walked, so their latency hides behind its work.
                     int bit = __builtin_ctzll(m);
-                    float4 a = sh.st0[c0 + bit], b = sh.st1[c0 + bit], x = sh.st2[c0 + bit];
-                    float4 sb = RASTER ? sh.st3[c0 + bit] : make_float4(0.f, 0.f, 0.f, 0.f);
+                    float4 a = sh.st0[c0 + bit], b = sh.st1[c0 + bit], x = sh.st2[c0 + bit], sb = sh.st3[c0 + bit];
                     for (;;) {
                         m &= m - 1ull;
                         const bool more = m != 0ull;
                         const int nbit = more ? __builtin_ctzll(m) : bit;
-                        const float4 an = sh.st0[c0 + nbit], bn = sh.st1[c0 + nbit], xn = sh.st2[c0 + nbit];
-                        const float4 sbn = RASTER ? sh.st3[c0 + nbit] : sb;
+                        const float4 an = sh.st0[c0 + nbit], bn = sh.st1[c0 + nbit], xn = sh.st2[c0 + nbit],
+                                     sbn = sh.st3[c0 + nbit];
                         const Record r{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, x.x};
-                        if constexpr (RASTER) {
-                            RasterSurvivor<R>(sh.keys[wave], r, x.y, __float_as_int(x.z), sb, wave_sb, s.fx[0],
-                                              fy_lane, lane);
-                        } else {
-                            ExactTestAnyOrder<R, SHARED>(s, r, x.y, __float_as_int(x.z));
-                        }
+                        RasterSurvivor(sh.keys, r, x.y, __float_as_int(x.z), sb, block_sb, fx_lane, fy_lane, lane);
                         if (!more) {
                             break;
                         }
@@ -871,8 +931,41 @@ __device__ __forceinline__ void CullWalk(const TraceParams& p, CullShared<W, G>&
                         sb = sbn;
                     }
                 }
+            } else {
+#pragma unroll 1
+                for (int c0 = 0; c0 < nb_here; c0 += kWave) {
+                    const int i = c0 + lane;
+                    bool pass = false;
+                    if (i < nb_here) {
+                        const float4 a = sh.st0[i], b = sh.st1[i], x = sh.st2[i];
+                        const Record r{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, x.x};
+                        pass = (!wave_sb || ScreenBoxOverlaps(wb, sh.st3[i])) && BoxMayHit(wb, r);
+                    }
+                    unsigned long long m = __ballot(pass);
+#ifdef SRT_DIAG
+                    d_wsurv += __popcll(m);
+#endif
+                    if (m != 0ull) {
+                        int bit = __builtin_ctzll(m);
+                        float4 a = sh.st0[c0 + bit], b = sh.st1[c0 + bit], x = sh.st2[c0 + bit];
+                        for (;;) {
+                            m &= m - 1ull;
+                            const bool more = m != 0ull;
+                            const int nbit = more ? __builtin_ctzll(m) : bit;
+                            const float4 an = sh.st0[c0 + nbit], bn = sh.st1[c0 + nbit], xn = sh.st2[c0 + nbit];
+                            const Record r{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, x.x};
+                            ExactTestAnyOrder<R, SHARED>(s, r, x.y, __float_as_int(x.z));
+                            if (!more) {
+                                break;
+                            }
+                            a = an;
+                            b = bn;
+                            x = xn;
+                        }
+                    }
+                }
             }
-            __syncthreads();  // staging (and, after the last batch, the id lists) reused next
+            __syncthreads();  // staging (and, after the last batch, the id list) reused next
 #ifdef SRT_DIAG
             {
                 const unsigned long long now = __builtin_amdgcn_s_memtime();
@@ -881,7 +974,10 @@ __device__ __forceinline__ void CullWalk(const TraceParams& p, CullShared<W, G>&
             }
 #endif
         }
-        mine = 0;
+        total = 0;
+    }
+    if (nsteps == 0) {
+        __syncthreads();  // raster keys initialised by every wave before the read-back
     }
 #ifdef SRT_DIAG
     const unsigned blk = blockIdx.y * gridDim.x + blockIdx.x;
@@ -894,13 +990,13 @@ __device__ __forceinline__ void CullWalk(const TraceParams& p, CullShared<W, G>&
         d[4] = d_wsurv;
         d[5] = d_batches;
         d[6] = __builtin_amdgcn_s_memtime() - d_t0;
-        d[7] = RASTER ? 1 : 0;
+        d[7] = (RASTER ? 1 : 0) | (LIST ? 2 : 0);
     }
 #endif
     if constexpr (RASTER) {
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            const unsigned long long key = sh.keys[wave][r][lane];
+            const unsigned long long key = sh.keys[wave * R + r][lane];
             if (key != ~0ull) {
                 s.bt[r] = __uint_as_float(static_cast<unsigned>(key >> 32));
                 s.bi[r] = static_cast<int>(static_cast<unsigned>(key));
@@ -909,10 +1005,136 @@ __device__ __forceinline__ void CullWalk(const TraceParams& p, CullShared<W, G>&
     }
 }
 
-template <int R, int W, int G>
+// Super-tile = kSuperTiles tiles side by side (128 x 32 pixels): the unit of the bin lists.
+constexpr int kSuperTiles = 2;
+constexpr int kBinSlices = 2;    // bin blocks per super-tile, each over a slice of the records
+constexpr int kBinThreads = 256;
+constexpr int kBinG = 8;         // records per lane per bin step (4 x 16-B loads)
+constexpr unsigned kUnbinned = 0xFFFFFFFFu;
+static_assert(kPadTriangles % (kBinSlices * kBinThreads * kBinG) == 0, "bin steps must tile the records");
+
+struct BinParams {
+    const uint2* __restrict__ qboxes;
+    const float2* __restrict__ offsets;
+    unsigned* __restrict__ lists;   // per super-tile: capacity ids
+    unsigned* __restrict__ counts;  // per super-tile (zeroed before the launch)
+    unsigned capacity;
+    unsigned n_pad;
+    int width;
+    int row_count;
+    int row_begin;
+    float wf;
+    float hf;
+};
+
+// Bin kernel (level 1 of the cull): block (super-tile, slice) computes the super-tile's ray
+// box from the sample offsets (GenerateRays' expressions, clamped edges included), streams
+// the quantized screen boxes of its slice of the records and appends the id of every record
+// overlapping the box to the super-tile's list (one global atomic per wave-step with
+// survivors). Every record is still tested against every super-tile. A list that overflows
+// its capacity, or a box outside the screen-box range, makes the trace kernel stream every
+// record for that super-tile instead (kUnbinned / count > capacity).
+__global__ __launch_bounds__(kBinThreads) void BinKernel(BinParams p) {
+    constexpr int kWaves = kBinThreads / kWave;
+    constexpr int L = kBinG / 2;
+    __shared__ Box boxes[kWaves];
+    const int tid = threadIdx.x;
+    const int lane = tid & (kWave - 1);
+    const int wave = tid / kWave;
+    const unsigned super = blockIdx.y * gridDim.x + blockIdx.x;
+    const int x0 = blockIdx.x * kSuperTiles * kWave;
+    const int y0 = blockIdx.y * kTileRows;
+    Box box{__builtin_inff(), -__builtin_inff(), __builtin_inff(), -__builtin_inff()};
+    for (int i = tid; i < kSuperTiles * kWave * kTileRows; i += kBinThreads) {
+        const int xc = min(x0 + i % (kSuperTiles * kWave), p.width - 1);
+        const int yc = min(y0 + i / (kSuperTiles * kWave), p.row_count - 1);
+        const float2 o = p.offsets[static_cast<size_t>(yc) * p.width + xc];
+        const float fx = (static_cast<float>(xc) + o.x) / p.wf;
+        const float fy = (static_cast<float>(p.row_begin + yc) + o.y) / p.hf;
+        box = Box{fminf(box.xlo, fx), fmaxf(box.xhi, fx), fminf(box.ylo, fy), fmaxf(box.yhi, fy)};
+    }
+    box = WaveReduceBox(box);
+    if (lane == 0) {
+        boxes[wave] = box;
+    }
+    __syncthreads();
+    box = boxes[0];
+#pragma unroll
+    for (int w = 1; w < kWaves; ++w) {
+        const Box o = boxes[w];
+        box = Box{fminf(box.xlo, o.xlo), fmaxf(box.xhi, o.xhi), fminf(box.ylo, o.ylo), fmaxf(box.yhi, o.yhi)};
+    }
+    if (!ScreenBoxUsable(box)) {
+        if (tid == 0) {
+            p.counts[super] = kUnbinned;
+        }
+        return;
+    }
+    const QBox bq = Quantize(box);
+    const unsigned slice = p.n_pad / kBinSlices;
+    const unsigned first = blockIdx.z * slice;
+    constexpr unsigned kStep = kBinThreads * kBinG;
+    const unsigned nsteps = slice / kStep;
+    const uint4* __restrict__ q4 = reinterpret_cast<const uint4*>(p.qboxes + first);
+    unsigned* list = p.lists + static_cast<size_t>(super) * p.capacity;
+    const unsigned long long lt_mask = (1ull << lane) - 1ull;
+    uint4 nq[L];
+#pragma unroll
+    for (int l = 0; l < L; ++l) {
+        nq[l] = q4[l * kBinThreads + tid];
+    }
+    for (unsigned k = 0; k < nsteps; ++k) {
+        uint4 q[L];
+#pragma unroll
+        for (int l = 0; l < L; ++l) {
+            q[l] = nq[l];
+        }
+        if (k + 1 < nsteps) {
+#pragma unroll
+            for (int l = 0; l < L; ++l) {
+                nq[l] = q4[(k + 1) * (kStep / 2) + l * kBinThreads + tid];
+            }
+        }
+        unsigned bits = 0u;
+#pragma unroll
+        for (int g = 0; g < kBinG; ++g) {
+            const unsigned qx = (g & 1) ? q[g >> 1].z : q[g >> 1].x;
+            const unsigned qy = (g & 1) ? q[g >> 1].w : q[g >> 1].y;
+            bits |= QBoxOverlaps(bq, qx, qy) ? (1u << g) : 0u;
+        }
+        if (__ballot(bits != 0u) == 0ull) {
+            continue;  // nothing in this wave-step (the common case)
+        }
+        unsigned n = 0;
+#pragma unroll
+        for (int g = 0; g < kBinG; ++g) {
+            n += __popcll(__ballot((bits >> g) & 1u));
+        }
+        unsigned base = 0;
+        if (lane == 0) {
+            base = atomicAdd(&p.counts[super], n);
+        }
+        base = __shfl(base, 0);
+#pragma unroll
+        for (int g = 0; g < kBinG; ++g) {
+            const bool pass = (bits >> g) & 1u;
+            const unsigned long long m = __ballot(pass);
+            if (pass) {
+                const unsigned at = base + __popcll(m & lt_mask);
+                if (at < p.capacity) {
+                    list[at] = first + k * kStep + 2 * ((g >> 1) * kBinThreads + tid) + (g & 1);
+                }
+            }
+            base += __popcll(m);
+        }
+    }
+}
+
+template <int W>
 __global__ __launch_bounds__(kWave * W) void TraceCullKernel(TraceParams p) {
-    static_assert(kPadTriangles % (kWave * W * G) == 0, "a cull step must cover whole pad units");
-    __shared__ CullShared<W, G> sh;
+    using S = CullShape<W>;
+    constexpr int R = S::kR;
+    __shared__ CullShared<W> sh;
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
     const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);
@@ -922,13 +1144,13 @@ __global__ __launch_bounds__(kWave * W) void TraceCullKernel(TraceParams p) {
     Box lane_box;
     const bool same = GenerateRays<R>(p, x, y0, s, lane_box);
     const Box wb = WaveReduceBox(lane_box);
-    // Raster walk eligibility: every ray of the block has the block's first sample offset
+    // Raster walk eligibility: every ray of the tile has the tile's first sample offset
     // (bit pattern), so fx depends on the column only and fy on the row only.
-    bool regular = R == 8;
+    bool regular = true;
     float oy0;
     {
         const int x0 = min(static_cast<int>(blockIdx.x) * kWave, p.width - 1);
-        const int yb = min(static_cast<int>(blockIdx.y) * W * R, p.row_count - 1);
+        const int yb = min(static_cast<int>(blockIdx.y) * kTileRows, p.row_count - 1);
         const float2 o0 = p.offsets[static_cast<size_t>(yb) * p.width + x0];
         oy0 = o0.y;
         const int xc = min(x, p.width - 1);
@@ -961,37 +1183,54 @@ __global__ __launch_bounds__(kWave * W) void TraceCullKernel(TraceParams p) {
         const Box o = sh.wave_box[w];
         bb = Box{fminf(bb.xlo, o.xlo), fmaxf(bb.xhi, o.xhi), fminf(bb.ylo, o.ylo), fmaxf(bb.yhi, o.yhi)};
     }
-    if (R == 8 && sh.regular != 0u && p.allow_raster != 0) {
-        CullWalk<R, W, G, true, R == 8>(p, sh, s, bb, wb, oy0);
+    // Candidate source: the super-tile's bin list when it is complete, else every record.
+    CullSource src{nullptr, 0u};
+    bool list = false;
+    if (p.bin_counts != nullptr) {
+        const unsigned super = blockIdx.y * ((gridDim.x + kSuperTiles - 1) / kSuperTiles) + blockIdx.x / kSuperTiles;
+        const unsigned cnt = p.bin_counts[super];
+        if (cnt <= p.bin_capacity) {
+            list = true;
+            src = CullSource{p.bin_lists + static_cast<size_t>(super) * p.bin_capacity, cnt};
+        }
+    }
+    // Raster walk: lane = column (fx), lanes 0..31 carry the tile's 32 rows' fy (the
+    // GenerateRays expression; bit-identical since every ray has the same offset).
+    const float fx_lane = s.fx[0];
+    float fy_lane = __builtin_nanf("");
+    if (lane < kTileRows) {
+        const int yc = min(static_cast<int>(blockIdx.y) * kTileRows + lane, p.row_count - 1);
+        fy_lane = (static_cast<float>(p.row_begin + yc) + oy0) / p.hf;
+    }
+    if (sh.regular != 0u && p.allow_raster != 0) {
+        if (list) {
+            CullWalk<W, true, true, true>(p, sh, s, bb, wb, fx_lane, fy_lane, src);
+        } else {
+            CullWalk<W, true, true, false>(p, sh, s, bb, wb, fx_lane, fy_lane, src);
+        }
     } else if (sh.shared_fx != 0u) {
-        CullWalk<R, W, G, true, false>(p, sh, s, bb, wb, 0.f);
+        if (list) {
+            CullWalk<W, true, false, true>(p, sh, s, bb, wb, fx_lane, fy_lane, src);
+        } else {
+            CullWalk<W, true, false, false>(p, sh, s, bb, wb, fx_lane, fy_lane, src);
+        }
     } else {
-        CullWalk<R, W, G, false, false>(p, sh, s, bb, wb, 0.f);
+        if (list) {
+            CullWalk<W, false, false, true>(p, sh, s, bb, wb, fx_lane, fy_lane, src);
+        } else {
+            CullWalk<W, false, false, false>(p, sh, s, bb, wb, fx_lane, fy_lane, src);
+        }
     }
     ShadeAndStore<R>(p, x, y0, s);
 }
 
-// Cull block shape: rows per lane x waves per block x records per lane per step; env
-// SRT_CULL_SHAPE = "RxWxG" (default 8x4x16; see kShapes), for measurement.
-struct CullShape {
-    int rows;
-    int waves;
-    int group;
-};
-
-CullShape CullShapeFromEnv() {
-    const char* v = std::getenv("SRT_CULL_SHAPE");
-    if (v != nullptr) {
-        static const CullShape kShapes[] = {{8, 4, 4}, {8, 4, 8}, {8, 4, 16}, {8, 8, 8}, {16, 4, 8}};
-        for (const CullShape& c : kShapes) {
-            char name[16];
-            std::snprintf(name, sizeof(name), "%dx%dx%d", c.rows, c.waves, c.group);
-            if (std::strcmp(v, name) == 0) {
-                return c;
-            }
-        }
+// Waves per cull tile; env SRT_CULL_WAVES = 4, 8 or 16 (default 8), for measurement.
+int CullWavesFromEnv() {
+    const char* v = std::getenv("SRT_CULL_WAVES");
+    if (v != nullptr && (std::strcmp(v, "4") == 0 || std::strcmp(v, "16") == 0)) {
+        return std::atoi(v);
     }
-    return {8, 4, 16};
+    return 8;
 }
 
 }  // namespace
@@ -1022,9 +1261,29 @@ hipError_t LaunchPrepare(const float* d_vertices, std::uint64_t n, const Frame& 
     return hipGetLastError();
 }
 
+std::size_t CullSuperTiles(std::size_t width, std::size_t row_count) {
+    const std::size_t gx = (width + kWave - 1) / kWave;
+    const std::size_t gy = (row_count + kTileRows - 1) / kTileRows;
+    return (gx + kSuperTiles - 1) / kSuperTiles * gy;
+}
+
+unsigned CullBinCapacity(std::uint64_t n, std::size_t supers) {
+    const std::uint64_t n_pad = PaddedTriangleCount(n);
+    std::uint64_t cap = supers == 0 ? n_pad : 64 * n_pad / supers;
+    cap = cap < 4096 ? 4096 : cap;
+    cap = cap > n_pad ? n_pad : cap;
+    if (const char* v = std::getenv("SRT_CULL_BIN_CAP")) {  // tests: force list overflow
+        const long forced = std::strtol(v, nullptr, 10);
+        if (forced > 0) {
+            cap = static_cast<std::uint64_t>(forced);
+        }
+    }
+    return static_cast<unsigned>((cap + 3) / 4 * 4);
+}
+
 hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_vertices, const float* d_albedo,
                        const Frame& frame, const float background[3], const BandArgs& band, int variant,
-                       hipStream_t stream) {
+                       const CullBins* bins, hipStream_t stream) {
     if (band.row_count == 0 || band.width == 0) {
         return hipSuccess;
     }
@@ -1058,17 +1317,37 @@ hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_ver
         const unsigned gy = static_cast<unsigned>((band.row_count + kRowsPerLane - 1) / kRowsPerLane);
         hipLaunchKernelGGL(TraceScalarKernel, dim3(gx, gy), dim3(kWave), 0, stream, p);
     } else if (variant == kTraceCull) {
-        const CullShape shape = CullShapeFromEnv();
-        const int rows_per_block = shape.rows * shape.waves;
-        const unsigned gy = static_cast<unsigned>((band.row_count + rows_per_block - 1) / rows_per_block);
-        const dim3 grid(gx, gy), block(kWave * shape.waves);
-        const int key = shape.rows * 100 + shape.waves * 10 + (shape.group == 16 ? 9 : shape.group);
-        switch (key) {
-            case 844: hipLaunchKernelGGL((TraceCullKernel<8, 4, 4>), grid, block, 0, stream, p); break;
-            case 848: hipLaunchKernelGGL((TraceCullKernel<8, 4, 8>), grid, block, 0, stream, p); break;
-            case 888: hipLaunchKernelGGL((TraceCullKernel<8, 8, 8>), grid, block, 0, stream, p); break;
-            case 1648: hipLaunchKernelGGL((TraceCullKernel<16, 4, 8>), grid, block, 0, stream, p); break;
-            default: hipLaunchKernelGGL((TraceCullKernel<8, 4, 16>), grid, block, 0, stream, p); break;
+        const unsigned gy = static_cast<unsigned>((band.row_count + kTileRows - 1) / kTileRows);
+        if (bins != nullptr) {
+            const unsigned sx = (gx + kSuperTiles - 1) / kSuperTiles;
+            if (static_cast<std::size_t>(sx) * gy > bins->supers) {
+                return hipErrorInvalidValue;  // bins sized for another band shape
+            }
+            hipError_t err = hipMemsetAsync(bins->counts, 0, sizeof(unsigned) * sx * gy, stream);
+            if (err != hipSuccess) {
+                return err;
+            }
+            BinParams b{};
+            b.qboxes = p.qboxes;
+            b.offsets = p.offsets;
+            b.lists = bins->lists;
+            b.counts = bins->counts;
+            b.capacity = bins->capacity;
+            b.n_pad = p.n_pad;
+            b.width = p.width;
+            b.row_count = p.row_count;
+            b.row_begin = p.row_begin;
+            b.wf = p.wf;
+            b.hf = p.hf;
+            hipLaunchKernelGGL(BinKernel, dim3(sx, gy, kBinSlices), dim3(kBinThreads), 0, stream, b);
+            p.bin_lists = bins->lists;
+            p.bin_counts = bins->counts;
+            p.bin_capacity = bins->capacity;
+        }
+        switch (CullWavesFromEnv()) {
+            case 4: hipLaunchKernelGGL(TraceCullKernel<4>, dim3(gx, gy), dim3(kWave * 4), 0, stream, p); break;
+            case 16: hipLaunchKernelGGL(TraceCullKernel<16>, dim3(gx, gy), dim3(kWave * 16), 0, stream, p); break;
+            default: hipLaunchKernelGGL(TraceCullKernel<8>, dim3(gx, gy), dim3(kWave * 8), 0, stream, p); break;
         }
     } else {
         constexpr int kRowsPerBlock = kRowsPerLane * kLdsWaves;

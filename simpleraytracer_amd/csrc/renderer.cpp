@@ -45,6 +45,11 @@ T* DeviceAlloc(std::size_t count, const char* what) {
     return static_cast<T*>(p);
 }
 
+bool CullBinningEnabled() {
+    const char* v = std::getenv("SRT_CULL_BIN");
+    return v == nullptr || std::strcmp(v, "0") != 0;
+}
+
 bool GatherWithRccl() {
     const char* mode = std::getenv("SRT_GATHER");
     return mode == nullptr || std::strcmp(mode, "direct") != 0;
@@ -94,10 +99,10 @@ int TraceVariantFromEnv() {
     if (v != nullptr && (std::strcmp(v, "scalar") == 0 || std::strcmp(v, "1") == 0)) {
         return kTraceScalar;
     }
-    if (v != nullptr && (std::strcmp(v, "cull") == 0 || std::strcmp(v, "2") == 0)) {
-        return kTraceCull;
+    if (v != nullptr && (std::strcmp(v, "lds") == 0 || std::strcmp(v, "0") == 0)) {
+        return kTraceLds;
     }
-    return kTraceLds;
+    return kTraceCull;
 }
 
 DeviceScene::DeviceScene(const Scene& scene, int device)
@@ -127,6 +132,8 @@ DeviceScene::~DeviceScene() {
     (void)hipFree(m_vertices);
     (void)hipFree(m_albedo);
     (void)hipFree(m_edges);
+    (void)hipFree(m_bin_lists);
+    (void)hipFree(m_bin_counts);
     if (prev >= 0) {
         (void)hipSetDevice(prev);
     }
@@ -151,7 +158,28 @@ void DeviceScene::Trace(const float* d_offsets, float* d_rgba, std::size_t row_b
         throw std::runtime_error("Trace: row band outside the frame");
     }
     BandArgs band{d_offsets, d_rgba, m_width, m_height, row_begin, row_count};
-    HipCheck(LaunchTrace(m_edges, m_n, m_vertices, m_albedo, m_frame, m_background, band, variant, stream),
+    CullBins bins{};
+    const CullBins* use_bins = nullptr;
+    if (variant == kTraceCull && row_count != 0 && CullBinningEnabled()) {
+        const std::size_t supers = CullSuperTiles(m_width, row_count);
+        const unsigned cap = CullBinCapacity(m_n, supers);
+        const std::size_t entries = supers * cap + 4;
+        if (entries > m_bin_list_entries || supers > m_bin_supers) {
+            HipCheck(hipStreamSynchronize(stream), "hipStreamSynchronize(bin lists)");
+            (void)hipFree(m_bin_lists);
+            (void)hipFree(m_bin_counts);
+            m_bin_lists = nullptr;
+            m_bin_counts = nullptr;
+            m_bin_list_entries = m_bin_supers = 0;
+            m_bin_lists = DeviceAlloc<unsigned>(entries, "hipMalloc(bin lists)");
+            m_bin_counts = DeviceAlloc<unsigned>(supers, "hipMalloc(bin counts)");
+            m_bin_list_entries = entries;
+            m_bin_supers = supers;
+        }
+        bins = CullBins{m_bin_lists, m_bin_counts, cap, supers};
+        use_bins = &bins;
+    }
+    HipCheck(LaunchTrace(m_edges, m_n, m_vertices, m_albedo, m_frame, m_background, band, variant, use_bins, stream),
              "trace kernel launch");
 }
 

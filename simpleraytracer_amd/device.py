@@ -89,7 +89,7 @@ class DeviceScene:
         _check(self._lib.srtPrepareAsync(self.handle, width, height, _stream(stream)))
         self.width, self.height = width, height
 
-    def trace(self, offsets, rgba, row_begin: int = 0, row_count: int | None = None, variant: str = "lds",
+    def trace(self, offsets, rgba, row_begin: int = 0, row_count: int | None = None, variant: str = "cull",
               stream=None):
         """offsets: (rows, W, 2) float32 device buffer; rgba: (rows, W, 4) float32 device buffer."""
         if row_count is None:

@@ -17,7 +17,18 @@ pytestmark = pytest.mark.gpu
 
 RGB_TOL = 1e-5
 VARIANTS = ("lds", "scalar", "cull")
-CULL_SHAPES = ("8x4x4", "8x4x8", "8x4x16", "8x8x8", "16x4x8")
+# cull variant modes: (SRT_CULL_BIN, SRT_CULL_RASTER, SRT_CULL_BIN_CAP)
+CULL_MODES = (("1", "1", ""), ("1", "0", ""), ("0", "1", ""), ("0", "0", ""), ("1", "1", "8"), ("1", "0", "8"))
+
+
+def set_cull_mode(monkeypatch, mode):
+    binning, raster, cap = mode
+    monkeypatch.setenv("SRT_CULL_BIN", binning)
+    monkeypatch.setenv("SRT_CULL_RASTER", raster)
+    if cap:
+        monkeypatch.setenv("SRT_CULL_BIN_CAP", cap)
+    else:
+        monkeypatch.delenv("SRT_CULL_BIN_CAP", raising=False)
 
 
 def oracle_render(path, w, h, offsets=None, **kw):
@@ -40,7 +51,7 @@ def assert_parity(got, ref, rows=None):
     assert float(d.max(initial=0.0)) <= RGB_TOL, f"max rgb delta {d.max()}"
 
 
-def torch_render(path, w, h, offsets=None, variant="lds", bands=None):
+def torch_render(path, w, h, offsets=None, variant="cull", bands=None):
     """DeviceScene path (srtPrepareAsync + srtTraceAsync) on device-resident torch buffers."""
     import torch
 
@@ -150,30 +161,28 @@ def test_variants_bitwise_identical_1080p(gpu, scenes):
         assert np.array_equal(frames[0].view(np.uint32), f.view(np.uint32))
 
 
-@pytest.mark.parametrize("shape", CULL_SHAPES)
-def test_cull_shapes(gpu, scenes, monkeypatch, shape):
-    """Every cull block shape (rows x waves x records per thread) against the oracle, with
-    random offsets (non-degenerate lane boxes) on a frame that leaves partial blocks."""
-    monkeypatch.setenv("SRT_CULL_SHAPE", shape)
+@pytest.mark.parametrize("mode", CULL_MODES)
+def test_cull_modes(gpu, scenes, monkeypatch, mode):
+    """Every cull mode (bin lists on/off, raster walk on/off, forced bin-list overflow) against
+    the oracle, with uniform and random offsets, on a frame that leaves partial tiles."""
+    set_cull_mode(monkeypatch, mode)
     rng = np.random.default_rng(5)
     w, h = 200, 150
-    offsets = rng.random((h, w, 2), dtype=np.float32)
-    got = torch_render(scenes["soup2k"], w, h, offsets, variant="cull")
-    assert_parity(got, oracle_render(scenes["soup2k"], w, h, offsets))
+    for offsets in (None, rng.random((h, w, 2), dtype=np.float32)):
+        got = torch_render(scenes["soup2k"], w, h, offsets, variant="cull")
+        assert_parity(got, oracle_render(scenes["soup2k"], w, h, offsets))
 
 
-@pytest.mark.parametrize("raster", ["1", "0"])
+@pytest.mark.parametrize("mode", CULL_MODES[:4])
 @pytest.mark.parametrize("offset", [0.5, 0.0, 0.999, -3.25, 7.5])
-def test_cull_uniform_offsets(gpu, scenes, monkeypatch, raster, offset):
-    """Uniform (per-frame constant) sample offsets: the raster walk (blocks whose rays share
-    one offset) and, with SRT_CULL_RASTER=0, the per-lane walk on the same frames."""
-    monkeypatch.setenv("SRT_CULL_RASTER", raster)
+def test_cull_uniform_offsets(gpu, scenes, monkeypatch, mode, offset):
+    """Uniform (per-frame constant) sample offsets, including ones that push rays outside
+    the frame and outside the screen-box range (|fx| > 4: no box culling)."""
+    set_cull_mode(monkeypatch, mode)
     w, h = 211, 97
     offsets = np.full((h, w, 2), offset, np.float32)
     ref = oracle_render(scenes["soup2k"], w, h, offsets)
-    for shape in ("8x4x16", "8x8x8"):
-        monkeypatch.setenv("SRT_CULL_SHAPE", shape)
-        assert_parity(torch_render(scenes["soup2k"], w, h, offsets, variant="cull"), ref)
+    assert_parity(torch_render(scenes["soup2k"], w, h, offsets, variant="cull"), ref)
 
 
 def test_cull_survivor_overflow_and_ties(gpu, tmp_path, monkeypatch):
@@ -193,11 +202,9 @@ def test_cull_survivor_overflow_and_ties(gpu, tmp_path, monkeypatch):
     path = write_custom_scene(tmp_path / "dense.srt", tris, albedo)
     ref = oracle_render(path, 96, 80)
     assert (ref[..., 3] == 3).mean() > 0.3
-    for raster in ("1", "0"):
-        monkeypatch.setenv("SRT_CULL_RASTER", raster)
-        for shape in CULL_SHAPES:
-            monkeypatch.setenv("SRT_CULL_SHAPE", shape)
-            assert_parity(torch_render(path, 96, 80, variant="cull"), ref)
+    for mode in CULL_MODES:
+        set_cull_mode(monkeypatch, mode)
+        assert_parity(torch_render(path, 96, 80, variant="cull"), ref)
 
 
 def test_cull_nasty_geometry(gpu, tmp_path, monkeypatch):
@@ -223,8 +230,8 @@ def test_cull_nasty_geometry(gpu, tmp_path, monkeypatch):
     offsets = rng2.random((90, 120, 2), dtype=np.float32)
     for off in (None, offsets):
         ref = oracle_render(path, 120, 90, off)
-        for shape in CULL_SHAPES:
-            monkeypatch.setenv("SRT_CULL_SHAPE", shape)
+        for mode in CULL_MODES:
+            set_cull_mode(monkeypatch, mode)
             assert_parity(torch_render(path, 120, 90, off, variant="cull"), ref)
 
 

@@ -46,11 +46,10 @@ def main():
         buf = np.zeros((16384, 8), np.uint64)
         assert lib.srtDiagRead(buf.ctypes.data, buf.nbytes) == 0, _native.last_error()
         scene.close()
-    shape = os.environ.get("SRT_CULL_SHAPE", "8x4x16")
-    r, wv, _ = (int(v) for v in shape.split("x"))
-    gx, gy = (w + 63) // 64, (h + r * wv - 1) // (r * wv)
+    shape = "8x4 tiles, bins " + os.environ.get("SRT_CULL_BIN", "1")
+    gx, gy = (w + 63) // 64, (h + 31) // 32
     d = buf[: gx * gy].astype(np.float64)
-    names = ["stream", "gather", "walk", "surv", "wsurv0", "batches", "total"]
+    names = ["stream", "gather", "walk", "surv", "wsurv0", "batches", "total", "mode"]
     summary = {"shape": shape, "blocks": gx * gy}
     for i, n in enumerate(names):
         col = d[:, i]

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Quick GPU iteration: parity tests (optionally filtered) then bench lines per variant/shape.
+# Quick GPU iteration: parity tests (optionally filtered) then bench lines per variant / cull mode.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
@@ -19,8 +19,8 @@ step() {
 step pytest_gpu 900 python -m pytest tests -m gpu -q -x ${PYTEST_K:+-k "$PYTEST_K"}
 for v in ${BENCH_VARIANTS:-cull}; do
     if [ "$v" = cull ]; then
-        for sh in ${CULL_SHAPES:-16x8x2}; do
-            SRT_CULL_SHAPE=$sh step "bench_cull_$sh" 300 python bench.py --steps 20 --warmup 3 --variant cull --no-cpu-baseline --no-e2e
+        for b in ${CULL_BINS:-1}; do
+            SRT_CULL_BIN=$b step "bench_cull_bin$b" 300 python bench.py --steps 50 --warmup 5 --variant cull --no-cpu-baseline --no-e2e
         done
     else
         step "bench_$v" 300 python bench.py --steps 10 --warmup 2 --variant "$v" --no-cpu-baseline --no-e2e
