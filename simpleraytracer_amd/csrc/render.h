@@ -75,6 +75,7 @@ hipError_t LaunchPrepare(const float* d_vertices, std::uint64_t n, const Frame& 
 struct CullBins {
     unsigned* lists;     // supers x capacity (+4 padding) ids
     unsigned* counts;    // supers
+    unsigned* super_q;   // supers x 4: quantized super-tile boxes (SuperBoxKernel)
     unsigned capacity;
     std::size_t supers;
 };

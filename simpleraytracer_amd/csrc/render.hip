@@ -8,6 +8,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstdio>
+#include <algorithm>
 #include <cstring>
 
 namespace srt {
@@ -1007,19 +1008,23 @@ __device__ __forceinline__ void CullWalk(const TraceParams& p, CullShared<W>& sh
 
 // Super-tile = kSuperTiles tiles side by side (128 x 32 pixels): the unit of the bin lists.
 constexpr int kSuperTiles = 2;
-constexpr int kBinSlices = 2;    // bin blocks per super-tile, each over a slice of the records
 constexpr int kBinThreads = 256;
-constexpr int kBinG = 8;         // records per lane per bin step (4 x 16-B loads)
+constexpr int kBinG = 8;          // records per lane per bin step (4 x 16-B loads)
+constexpr int kBinStep = kBinThreads * kBinG;
+constexpr int kBinMaxSlices = 32;  // bin blocks per super-tile row, striding over the record steps
+constexpr int kBinRowSupers = 64;  // super-tiles per row handled per pass (LDS box cache)
 constexpr unsigned kUnbinned = 0xFFFFFFFFu;
-static_assert(kPadTriangles % (kBinSlices * kBinThreads * kBinG) == 0, "bin steps must tile the records");
+static_assert(kPadTriangles % kBinStep == 0, "bin steps must tile the records");
 
 struct BinParams {
     const uint2* __restrict__ qboxes;
     const float2* __restrict__ offsets;
+    uint4* __restrict__ super_q;    // per super-tile: (QBox.x, QBox.y, usable, 0)
     unsigned* __restrict__ lists;   // per super-tile: capacity ids
-    unsigned* __restrict__ counts;  // per super-tile (zeroed before the launch)
+    unsigned* __restrict__ counts;  // per super-tile
     unsigned capacity;
     unsigned n_pad;
+    int supers_x;
     int width;
     int row_count;
     int row_begin;
@@ -1027,16 +1032,12 @@ struct BinParams {
     float hf;
 };
 
-// Bin kernel (level 1 of the cull): block (super-tile, slice) computes the super-tile's ray
-// box from the sample offsets (GenerateRays' expressions, clamped edges included), streams
-// the quantized screen boxes of its slice of the records and appends the id of every record
-// overlapping the box to the super-tile's list (one global atomic per wave-step with
-// survivors). Every record is still tested against every super-tile. A list that overflows
-// its capacity, or a box outside the screen-box range, makes the trace kernel stream every
-// record for that super-tile instead (kUnbinned / count > capacity).
-__global__ __launch_bounds__(kBinThreads) void BinKernel(BinParams p) {
+// Level 0 of the cull: one block per super-tile computes its ray box from the sample offsets
+// (GenerateRays' expressions, clamped edges included), stores it quantized for the bin
+// kernel and resets the super-tile's list count (kUnbinned when the box lies outside the
+// screen-box range: its tiles then stream every record).
+__global__ __launch_bounds__(kBinThreads) void SuperBoxKernel(BinParams p) {
     constexpr int kWaves = kBinThreads / kWave;
-    constexpr int L = kBinG / 2;
     __shared__ Box boxes[kWaves];
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
@@ -1058,75 +1059,165 @@ __global__ __launch_bounds__(kBinThreads) void BinKernel(BinParams p) {
         boxes[wave] = box;
     }
     __syncthreads();
-    box = boxes[0];
+    if (tid == 0) {
+        box = boxes[0];
 #pragma unroll
-    for (int w = 1; w < kWaves; ++w) {
-        const Box o = boxes[w];
-        box = Box{fminf(box.xlo, o.xlo), fmaxf(box.xhi, o.xhi), fminf(box.ylo, o.ylo), fmaxf(box.yhi, o.yhi)};
-    }
-    if (!ScreenBoxUsable(box)) {
-        if (tid == 0) {
-            p.counts[super] = kUnbinned;
+        for (int w = 1; w < kWaves; ++w) {
+            const Box o = boxes[w];
+            box = Box{fminf(box.xlo, o.xlo), fmaxf(box.xhi, o.xhi), fminf(box.ylo, o.ylo), fmaxf(box.yhi, o.yhi)};
         }
-        return;
+        const bool usable = ScreenBoxUsable(box);
+        const QBox q = Quantize(box);
+        p.super_q[super] = make_uint4(q.x, q.y, usable ? 1u : 0u, 0u);
+        p.counts[super] = usable ? 0u : kUnbinned;
     }
-    const QBox bq = Quantize(box);
-    const unsigned slice = p.n_pad / kBinSlices;
-    const unsigned first = blockIdx.z * slice;
-    constexpr unsigned kStep = kBinThreads * kBinG;
-    const unsigned nsteps = slice / kStep;
-    const uint4* __restrict__ q4 = reinterpret_cast<const uint4*>(p.qboxes + first);
-    unsigned* list = p.lists + static_cast<size_t>(super) * p.capacity;
+}
+
+// Level 1 of the cull (bin kernel): block (super-tile row, slice) streams the quantized
+// screen boxes of its share of the records once and tests each against the row's box (the
+// union of its super-tiles' boxes); each record that passes (a few percent) is then tested
+// against every super-tile of the row at once, lane j taking super-tile j. Survivors are
+// collected as (super-tile, id) pairs in wave-private LDS regions and flushed to the global
+// lists with one atomic per super-tile per flush. Every record is still tested against
+// every super-tile. A list that overflows its capacity makes the trace kernel stream every
+// record for that super-tile instead.
+constexpr int kBinWaves = kBinThreads / kWave;
+constexpr int kBinWavePairs = 1024;                      // LDS pairs per wave region
+constexpr int kBinPairCap = kBinWaves * kBinWavePairs;   // 4096
+static_assert(kBinRowSupers <= kWave, "one super-tile per lane");
+__global__ __launch_bounds__(kBinThreads) void BinKernel(BinParams p) {
+    __shared__ unsigned pair_super[kBinPairCap];
+    __shared__ unsigned pair_id[kBinPairCap];
+    __shared__ unsigned wave_count[kBinWaves];
+    __shared__ unsigned hist[kBinRowSupers];
+    __shared__ unsigned gbase[kBinRowSupers];
+    const int tid = threadIdx.x;
+    const int lane = tid & (kWave - 1);
+    const int wave = tid / kWave;
+    const unsigned row = blockIdx.x;
     const unsigned long long lt_mask = (1ull << lane) - 1ull;
-    uint4 nq[L];
-#pragma unroll
-    for (int l = 0; l < L; ++l) {
-        nq[l] = q4[l * kBinThreads + tid];
-    }
-    for (unsigned k = 0; k < nsteps; ++k) {
-        uint4 q[L];
-#pragma unroll
-        for (int l = 0; l < L; ++l) {
-            q[l] = nq[l];
-        }
-        if (k + 1 < nsteps) {
-#pragma unroll
-            for (int l = 0; l < L; ++l) {
-                nq[l] = q4[(k + 1) * (kStep / 2) + l * kBinThreads + tid];
-            }
-        }
-        unsigned bits = 0u;
-#pragma unroll
-        for (int g = 0; g < kBinG; ++g) {
-            const unsigned qx = (g & 1) ? q[g >> 1].z : q[g >> 1].x;
-            const unsigned qy = (g & 1) ? q[g >> 1].w : q[g >> 1].y;
-            bits |= QBoxOverlaps(bq, qx, qy) ? (1u << g) : 0u;
-        }
-        if (__ballot(bits != 0u) == 0ull) {
-            continue;  // nothing in this wave-step (the common case)
-        }
-        unsigned n = 0;
-#pragma unroll
-        for (int g = 0; g < kBinG; ++g) {
-            n += __popcll(__ballot((bits >> g) & 1u));
-        }
-        unsigned base = 0;
+    const unsigned nsteps = p.n_pad / kBinStep;
+    const uint4* __restrict__ q4 = reinterpret_cast<const uint4*>(p.qboxes);
+    constexpr int L = kBinG / 2;
+    unsigned* my_super = pair_super + wave * kBinWavePairs;
+    unsigned* my_id = pair_id + wave * kBinWavePairs;
+
+    // Flush every wave's pairs: histogram per super-tile (LDS atomics give each pair its
+    // rank), one global atomic per super-tile reserves list space, then scatter.
+    auto flush = [&](int j0, int nj, unsigned mine) {
         if (lane == 0) {
-            base = atomicAdd(&p.counts[super], n);
+            wave_count[wave] = mine;
         }
-        base = __shfl(base, 0);
+        if (tid < nj) {
+            hist[tid] = 0u;
+        }
+        __syncthreads();
+        unsigned rank[kBinPairCap / kBinThreads];
 #pragma unroll
-        for (int g = 0; g < kBinG; ++g) {
-            const bool pass = (bits >> g) & 1u;
-            const unsigned long long m = __ballot(pass);
-            if (pass) {
-                const unsigned at = base + __popcll(m & lt_mask);
+        for (int i = 0; i < kBinPairCap / kBinThreads; ++i) {
+            const unsigned e = i * kBinThreads + tid;
+            const bool valid = e % kBinWavePairs < wave_count[e / kBinWavePairs];
+            rank[i] = valid ? atomicAdd(&hist[pair_super[e]], 1u) : 0u;
+        }
+        __syncthreads();
+        if (tid < nj && hist[tid] != 0u) {
+            gbase[tid] = atomicAdd(&p.counts[row * p.supers_x + j0 + tid], hist[tid]);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < kBinPairCap / kBinThreads; ++i) {
+            const unsigned e = i * kBinThreads + tid;
+            if (e % kBinWavePairs < wave_count[e / kBinWavePairs]) {
+                const unsigned j = pair_super[e];
+                const unsigned at = gbase[j] + rank[i];
                 if (at < p.capacity) {
-                    list[at] = first + k * kStep + 2 * ((g >> 1) * kBinThreads + tid) + (g & 1);
+                    p.lists[static_cast<size_t>(row * p.supers_x + j0 + j) * p.capacity + at] = pair_id[e];
                 }
             }
-            base += __popcll(m);
         }
+        __syncthreads();  // pair regions reused
+    };
+
+    for (int j0 = 0; j0 < p.supers_x; j0 += kBinRowSupers) {
+        const int nj = min(kBinRowSupers, p.supers_x - j0);
+        // Lane j < nj holds super-tile j's packed box (usable flag in .z).
+        uint4 my_q = make_uint4(0x80008000u, 0x80008000u, 0u, 0u);
+        if (lane < nj) {
+            my_q = p.super_q[row * p.supers_x + j0 + lane];
+        }
+        const bool my_usable = my_q.z != 0u;
+        const QBox my_box{my_q.x, my_q.y};
+        // Row box: union of the usable super-tile boxes (in the packed (-lo, hi) form the
+        // union is the per-half maximum).
+        I16x2 ux = __builtin_bit_cast(I16x2, my_usable ? my_q.x : 0x80008000u);
+        I16x2 uy = __builtin_bit_cast(I16x2, my_usable ? my_q.y : 0x80008000u);
+#pragma unroll
+        for (int o = 1; o < kWave; o <<= 1) {
+            ux = __builtin_elementwise_max(ux, __builtin_bit_cast(I16x2, __shfl_xor(__builtin_bit_cast(unsigned, ux), o)));
+            uy = __builtin_elementwise_max(uy, __builtin_bit_cast(I16x2, __shfl_xor(__builtin_bit_cast(unsigned, uy), o)));
+        }
+        if (__ballot(my_usable) == 0ull) {
+            continue;  // no usable super-tile in this part of the row
+        }
+        const QBox rq{__builtin_bit_cast(unsigned, ux), __builtin_bit_cast(unsigned, uy)};
+        unsigned mine = 0;  // pairs in this wave's region (wave-uniform)
+        for (unsigned k0 = blockIdx.y; k0 < nsteps; k0 += gridDim.y) {
+            uint4 q[L];
+#pragma unroll
+            for (int l = 0; l < L; ++l) {
+                q[l] = q4[k0 * (kBinStep / 2) + l * kBinThreads + tid];
+            }
+#pragma unroll
+            for (int g = 0; g < kBinG; ++g) {
+                const unsigned qx = (g & 1) ? q[g >> 1].z : q[g >> 1].x;
+                const unsigned qy = (g & 1) ? q[g >> 1].w : q[g >> 1].y;
+                unsigned long long m = __ballot(QBoxOverlaps(rq, qx, qy));
+                // Each record of the row: every super-tile at once (lane j: super-tile j).
+                while (m != 0ull) {
+                    const int src = __builtin_ctzll(m);
+                    m &= m - 1ull;
+                    const unsigned rx = __builtin_amdgcn_readlane(qx, src);
+                    const unsigned ry = __builtin_amdgcn_readlane(qy, src);
+                    const bool hit = my_usable && QBoxOverlaps(my_box, rx, ry);
+                    const unsigned long long hm = __ballot(hit);
+                    if (hit) {
+                        const unsigned at = mine + __popcll(hm & lt_mask);
+                        my_super[at] = static_cast<unsigned>(lane);
+                        my_id[at] = k0 * kBinStep + 2 * ((g >> 1) * kBinThreads + (wave * kWave + src)) + (g & 1);
+                    }
+                    mine += __popcll(hm);
+                    if (mine + kWave > kBinWavePairs) {
+                        // Region full: this wave's pairs go straight to the global lists.
+                        unsigned gb = 0;
+                        for (unsigned e = lane; e < mine; e += kWave) {
+                            const unsigned j = my_super[e];
+                            const unsigned at = atomicAdd(&p.counts[row * p.supers_x + j0 + j], 1u);
+                            if (at < p.capacity) {
+                                p.lists[static_cast<size_t>(row * p.supers_x + j0 + j) * p.capacity + at] = my_id[e];
+                            }
+                        }
+                        (void)gb;
+                        mine = 0;
+                    }
+                }
+            }
+            // Flush once some region is half full (block-uniform decision via LDS).
+            if (lane == 0) {
+                wave_count[wave] = mine;
+            }
+            __syncthreads();
+            unsigned most = 0;
+#pragma unroll
+            for (int w = 0; w < kBinWaves; ++w) {
+                most = max(most, wave_count[w]);
+            }
+            __syncthreads();
+            if (most > kBinWavePairs / 2) {
+                flush(j0, nj, mine);
+                mine = 0;
+            }
+        }
+        flush(j0, nj, mine);
     }
 }
 
@@ -1323,23 +1414,23 @@ hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_ver
             if (static_cast<std::size_t>(sx) * gy > bins->supers) {
                 return hipErrorInvalidValue;  // bins sized for another band shape
             }
-            hipError_t err = hipMemsetAsync(bins->counts, 0, sizeof(unsigned) * sx * gy, stream);
-            if (err != hipSuccess) {
-                return err;
-            }
             BinParams b{};
             b.qboxes = p.qboxes;
             b.offsets = p.offsets;
+            b.super_q = reinterpret_cast<uint4*>(bins->super_q);
             b.lists = bins->lists;
             b.counts = bins->counts;
             b.capacity = bins->capacity;
             b.n_pad = p.n_pad;
+            b.supers_x = static_cast<int>(sx);
             b.width = p.width;
             b.row_count = p.row_count;
             b.row_begin = p.row_begin;
             b.wf = p.wf;
             b.hf = p.hf;
-            hipLaunchKernelGGL(BinKernel, dim3(sx, gy, kBinSlices), dim3(kBinThreads), 0, stream, b);
+            hipLaunchKernelGGL(SuperBoxKernel, dim3(sx, gy), dim3(kBinThreads), 0, stream, b);
+            const unsigned slices = std::min<unsigned>(kBinMaxSlices, p.n_pad / kBinStep);
+            hipLaunchKernelGGL(BinKernel, dim3(gy, slices), dim3(kBinThreads), 0, stream, b);
             p.bin_lists = bins->lists;
             p.bin_counts = bins->counts;
             p.bin_capacity = bins->capacity;

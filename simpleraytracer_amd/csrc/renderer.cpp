@@ -172,11 +172,12 @@ void DeviceScene::Trace(const float* d_offsets, float* d_rgba, std::size_t row_b
             m_bin_counts = nullptr;
             m_bin_list_entries = m_bin_supers = 0;
             m_bin_lists = DeviceAlloc<unsigned>(entries, "hipMalloc(bin lists)");
-            m_bin_counts = DeviceAlloc<unsigned>(supers, "hipMalloc(bin counts)");
+            m_bin_counts = DeviceAlloc<unsigned>(supers * 5, "hipMalloc(bin counts)");
             m_bin_list_entries = entries;
             m_bin_supers = supers;
         }
-        bins = CullBins{m_bin_lists, m_bin_counts, cap, supers};
+        // super_q first (uint4 per super-tile, 16-B aligned), then the counts.
+        bins = CullBins{m_bin_lists, m_bin_counts + 4 * supers, m_bin_counts, cap, supers};
         use_bins = &bins;
     }
     HipCheck(LaunchTrace(m_edges, m_n, m_vertices, m_albedo, m_frame, m_background, band, variant, use_bins, stream),

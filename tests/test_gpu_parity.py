@@ -205,6 +205,12 @@ def test_cull_survivor_overflow_and_ties(gpu, tmp_path, monkeypatch):
     for mode in CULL_MODES:
         set_cull_mode(monkeypatch, mode)
         assert_parity(torch_render(path, 96, 80, variant="cull"), ref)
+    # 3 super-tiles per row, every record in each: the bin kernel's LDS pair buffer overflows
+    # (pairs then go straight to the global lists) and the lists exceed small capacities.
+    ref = oracle_render(path, 300, 40)
+    for mode in CULL_MODES:
+        set_cull_mode(monkeypatch, mode)
+        assert_parity(torch_render(path, 300, 40, variant="cull"), ref)
 
 
 def test_cull_nasty_geometry(gpu, tmp_path, monkeypatch):

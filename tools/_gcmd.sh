@@ -1,1 +1,5 @@
-CULL_BINS="1" bash tools/gpu_iter.sh && for w in 4 16; do SRT_CULL_WAVES=$w timeout -k 10 300 python bench.py --steps 50 --warmup 5 --variant cull --no-cpu-baseline --no-e2e > gpurun_out/bench_w$w.log 2>&1 || exit 1; done && export SRT_LIB=simpleraytracer_amd/lib_diag/libModelRunner.so && timeout -k 10 200 python tools/diag_cull.py > gpurun_out/diag_bin.json 2>>gpurun_out/diag.err
+set -u
+cd "${GRAFT_REPO_ROOT:-.}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS GRBM_GUI_ACTIVE --kernel-include-regex "Bin|Trace|Super" -d gpurun_out/pmc_sq2 -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-e2e > gpurun_out/pmc_sq2.log 2>&1
