@@ -73,12 +73,17 @@ hipError_t LaunchPrepare(const float* d_vertices, std::uint64_t n, const Frame& 
 // Bin lists of the cull variant's first level (render.hip BinKernel): per super-tile of a
 // band (128 x 32 pixels), up to `capacity` candidate record ids and their count.
 struct CullBins {
-    unsigned* lists;     // supers x capacity (+4 padding) ids
-    unsigned* counts;    // supers
-    unsigned* super_q;   // supers x 4: quantized super-tile boxes (SuperBoxKernel)
+    unsigned* lists;      // supers x capacity (+4 padding) ids
+    unsigned* counts;     // supers
+    unsigned* super_q;    // supers x 4: quantized super-tile boxes (SuperBoxKernel)
+    void* tile_keys;      // row_count x width u64: (t, id) keys of tiles split over blocks
+    unsigned* tile_done;  // tiles: finished blocks of a split tile
     unsigned capacity;
     std::size_t supers;
 };
+
+// Tiles (64 x 32 pixels) of a width x row_count band.
+std::size_t CullTiles(std::size_t width, std::size_t row_count);
 
 // Super-tiles of a width x row_count band, and the per-list capacity used for n triangles
 // (a list that overflows makes its tiles stream every record; results are unaffected).

@@ -17,7 +17,7 @@ namespace srt {
 // Diagnostic build only (make diag): per-block phase cycle counts of the cull kernel.
 // [block][0] stream cycles, [1] gather cycles, [2] filter+walk cycles, [3] block survivors,
 // [4] wave-0 survivors walked, [5] flush batches, [6] total cycles, [7] unused.
-constexpr int kDiagBlocks = 16384;
+constexpr int kDiagBlocks = 65536;
 __device__ unsigned long long g_srt_diag[kDiagBlocks][8];
 #define SRT_STAMP(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
 #else
@@ -47,6 +47,9 @@ struct TraceParams {
     const unsigned* __restrict__ bin_lists;   // cull variant: per super-tile candidate ids (BinKernel)
     const unsigned* __restrict__ bin_counts;  // null: stream every record
     unsigned bin_capacity;
+    unsigned chunk_ids;                          // cull: list ids per block of a split tile
+    unsigned long long* __restrict__ tile_keys;  // cull, split tiles: per-pixel (t, id) keys (band)
+    unsigned* __restrict__ tile_done;            // cull, split tiles: finished blocks per tile
     float wf;
     float hf;
     float base[3];
@@ -642,7 +645,7 @@ __device__ __forceinline__ void LoadRecord(const float4* __restrict__ edges, uns
 // Cull tile = one trace block: 64 columns x 32 rows of rays, W waves (4, 8 or 16) of 64 x R
 // rays, R = 32 / W rays per lane. Constants that depend on W live in CullShape<W>.
 constexpr int kTileRows = 32;
-constexpr int kStreamStep = 4096;  // FULL stream: records per block per step
+constexpr int kStreamStep = 2048;  // FULL stream: records per block per step
 constexpr int kListG = 4;          // LIST stream: ids per lane per step
 static_assert(kPadTriangles % kStreamStep == 0, "a stream step must cover whole pad units");
 
@@ -651,7 +654,8 @@ struct CullShape {
     static constexpr int kR = kTileRows / W;              // rays per lane
     static constexpr int kThreads = kWave * W;
     static constexpr int kStreamG = kStreamStep / kThreads;  // FULL: records per lane per step
-    static constexpr int kBatch = kThreads;               // survivors gathered per flush batch
+    static constexpr int kBatch = 256;                    // survivors gathered per flush batch
+    static constexpr int kShare = kBatch / W;             // raster walk: batch entries per wave
     static constexpr int kListCap = kBatch + kStreamStep;  // block id list: < kBatch + one step
 };
 
@@ -727,8 +731,10 @@ __device__ __forceinline__ void RasterSurvivor(unsigned long long (*keys)[kWave]
 // Per-tile source of candidate records for the cull stream: every record of the scene
 // (FULL), or the id list the bin kernel built for the tile's super-tile (LIST).
 struct CullSource {
-    const unsigned* list;  // LIST: ids
+    const unsigned* list;  // LIST: ids (this block's chunk of the super-tile list)
     unsigned count;        // LIST: number of ids
+    unsigned step0;        // FULL: first record step of this block's chunk
+    unsigned steps;        // FULL: record steps of this block's chunk
 };
 
 // Streams the tile's candidates, keeps those whose quantized screen box overlaps the tile's
@@ -755,7 +761,7 @@ __device__ __forceinline__ void CullWalk(const TraceParams& p, CullShared<W>& sh
     const bool wave_sb = ScreenBoxUsable(wb);
     const QBox bq = Quantize(bb);
     const unsigned long long lt_mask = (1ull << lane) - 1ull;
-    const unsigned nsteps = LIST ? (src.count + kStep - 1) / kStep : p.n_pad / kStep;
+    const unsigned nsteps = LIST ? (src.count + kStep - 1) / kStep : src.steps;
 
     if constexpr (RASTER) {
         for (int i = tid; i < kTileRows * kWave; i += kThreads) {
@@ -787,7 +793,7 @@ __device__ __forceinline__ void CullWalk(const TraceParams& p, CullShared<W>& sh
         } else {
 #pragma unroll
             for (int l = 0; l < L; ++l) {
-                nb[l] = qbox4[k * (kStep / 2) + l * kThreads + tid];
+                nb[l] = qbox4[(src.step0 + k) * (kStep / 2) + l * kThreads + tid];
             }
         }
     };
@@ -814,7 +820,7 @@ __device__ __forceinline__ void CullWalk(const TraceParams& p, CullShared<W>& sh
             if constexpr (LIST) {
                 return g == 0 ? cid.x : (g == 1 ? cid.y : (g == 2 ? cid.z : cid.w));
             } else {
-                return k * kStep + 2 * ((g >> 1) * kThreads + tid) + (g & 1);
+                return (src.step0 + k) * kStep + 2 * ((g >> 1) * kThreads + tid) + (g & 1);
             }
         };
         unsigned bits = 0u;
@@ -876,7 +882,9 @@ __device__ __forceinline__ void CullWalk(const TraceParams& p, CullShared<W>& sh
 #pragma unroll 1
         for (int b0 = 0; b0 < total; b0 += kBatch) {
             const int e = b0 + tid;
-            if (e < total) {
+            if (tid >= kBatch) {
+                // not a gathering thread
+            } else if (e < total) {
                 const unsigned id = sh.ids[e];
                 float4 p0, p1;
                 float cyC, vol;
@@ -905,8 +913,8 @@ __device__ __forceinline__ void CullWalk(const TraceParams& p, CullShared<W>& sh
             const int nb_here = min(kBatch, total - b0);
             if constexpr (RASTER) {
                 // This wave's share of the batch: entries wave * 64 .. wave * 64 + 63.
-                const int c0 = wave * kWave;
-                unsigned long long m = __ballot(sh.hit[c0 + lane] != 0u);
+                const int c0 = wave * S::kShare;
+                unsigned long long m = __ballot(lane < S::kShare && sh.hit[c0 + lane] != 0u);
 #ifdef SRT_DIAG
                 d_wsurv += __popcll(m);
 #endif
@@ -981,7 +989,7 @@ __device__ __forceinline__ void CullWalk(const TraceParams& p, CullShared<W>& sh
         __syncthreads();  // raster keys initialised by every wave before the read-back
     }
 #ifdef SRT_DIAG
-    const unsigned blk = blockIdx.y * gridDim.x + blockIdx.x;
+    const unsigned blk = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
     if (tid == 0 && blk < kDiagBlocks) {
         unsigned long long* d = g_srt_diag[blk];
         d[0] = d_stream;
@@ -991,7 +999,7 @@ __device__ __forceinline__ void CullWalk(const TraceParams& p, CullShared<W>& sh
         d[4] = d_wsurv;
         d[5] = d_batches;
         d[6] = __builtin_amdgcn_s_memtime() - d_t0;
-        d[7] = (RASTER ? 1 : 0) | (LIST ? 2 : 0);
+        d[7] = (RASTER ? 1 : 0) | (LIST ? 2 : 0) | 4;
     }
 #endif
     if constexpr (RASTER) {
@@ -1022,6 +1030,8 @@ struct BinParams {
     uint4* __restrict__ super_q;    // per super-tile: (QBox.x, QBox.y, usable, 0)
     unsigned* __restrict__ lists;   // per super-tile: capacity ids
     unsigned* __restrict__ counts;  // per super-tile
+    unsigned long long* __restrict__ tile_keys;  // reset to "no hit" here
+    unsigned* __restrict__ tile_done;            // reset to 0 here
     unsigned capacity;
     unsigned n_pad;
     int supers_x;
@@ -1070,6 +1080,21 @@ __global__ __launch_bounds__(kBinThreads) void SuperBoxKernel(BinParams p) {
         const QBox q = Quantize(box);
         p.super_q[super] = make_uint4(q.x, q.y, usable ? 1u : 0u, 0u);
         p.counts[super] = usable ? 0u : kUnbinned;
+    }
+    // Split-tile state of the super-tile's pixels and tiles for this frame.
+    const int tiles_x = (p.width + kWave - 1) / kWave;
+    if (tid < kSuperTiles) {
+        const int tx = blockIdx.x * kSuperTiles + tid;
+        if (tx < tiles_x) {
+            p.tile_done[blockIdx.y * tiles_x + tx] = 0u;
+        }
+    }
+    for (int i = tid; i < kSuperTiles * kWave * kTileRows; i += kBinThreads) {
+        const int xx = x0 + i % (kSuperTiles * kWave);
+        const int yy = y0 + i / (kSuperTiles * kWave);
+        if (xx < p.width && yy < p.row_count) {
+            p.tile_keys[static_cast<size_t>(yy) * p.width + xx] = ~0ull;
+        }
     }
 }
 
@@ -1221,11 +1246,52 @@ __global__ __launch_bounds__(kBinThreads) void BinKernel(BinParams p) {
     }
 }
 
+// How the blocks of one tile split its candidates: block z of chunks (blocks z >= chunks
+// return at once). LIST: chunks of >= p.chunk_ids list ids (16-B aligned); FULL (a tile whose
+// bin list overflowed, or no usable box): kMaxChunks slices of the record steps; without
+// bins: one block.
+constexpr unsigned kMaxChunks = 8;
+struct CullPlan {
+    CullSource src;
+    unsigned chunks;
+    bool list;
+};
+__device__ __forceinline__ CullPlan PlanTile(const TraceParams& p) {
+    CullPlan plan{CullSource{nullptr, 0u, 0u, p.n_pad / kStreamStep}, 1u, false};
+    if (p.bin_counts == nullptr) {
+        return plan;
+    }
+    const unsigned super = blockIdx.y * ((gridDim.x + kSuperTiles - 1) / kSuperTiles) + blockIdx.x / kSuperTiles;
+    const unsigned cnt = p.bin_counts[super];
+    const unsigned z = blockIdx.z;
+    if (cnt <= p.bin_capacity) {
+        plan.list = true;
+        plan.chunks = min(kMaxChunks, max(1u, (cnt + p.chunk_ids - 1) / p.chunk_ids));
+        const unsigned per = ((cnt + plan.chunks - 1) / plan.chunks + 3u) & ~3u;
+        const unsigned first = min(cnt, z * per);
+        plan.src.list = p.bin_lists + static_cast<size_t>(super) * p.bin_capacity + first;
+        plan.src.count = min(per, cnt - first);
+    } else {
+        const unsigned total = p.n_pad / kStreamStep;
+        plan.chunks = min(kMaxChunks, total);
+        const unsigned a = z * total / plan.chunks, b = (z + 1) * total / plan.chunks;
+        plan.src.step0 = a;
+        plan.src.steps = z < plan.chunks ? b - a : 0u;
+    }
+    return plan;
+}
+
 template <int W>
-__global__ __launch_bounds__(kWave * W) void TraceCullKernel(TraceParams p) {
+__global__ __launch_bounds__(kWave * W, (48 / W > 8 ? 8 : 48 / W)) void TraceCullKernel(TraceParams p) {
     using S = CullShape<W>;
     constexpr int R = S::kR;
     __shared__ CullShared<W> sh;
+    if (p.bin_counts != nullptr) {
+        const CullPlan early = PlanTile(p);
+        if (blockIdx.z >= early.chunks) {
+            return;  // this tile needs fewer blocks
+        }
+    }
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
     const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);
@@ -1274,17 +1340,11 @@ __global__ __launch_bounds__(kWave * W) void TraceCullKernel(TraceParams p) {
         const Box o = sh.wave_box[w];
         bb = Box{fminf(bb.xlo, o.xlo), fmaxf(bb.xhi, o.xhi), fminf(bb.ylo, o.ylo), fmaxf(bb.yhi, o.yhi)};
     }
-    // Candidate source: the super-tile's bin list when it is complete, else every record.
-    CullSource src{nullptr, 0u};
-    bool list = false;
-    if (p.bin_counts != nullptr) {
-        const unsigned super = blockIdx.y * ((gridDim.x + kSuperTiles - 1) / kSuperTiles) + blockIdx.x / kSuperTiles;
-        const unsigned cnt = p.bin_counts[super];
-        if (cnt <= p.bin_capacity) {
-            list = true;
-            src = CullSource{p.bin_lists + static_cast<size_t>(super) * p.bin_capacity, cnt};
-        }
-    }
+    // Candidate source: the super-tile's bin list when it is complete, else every record;
+    // split into `chunks` pieces taken by blocks z = 0 .. chunks-1 of this tile.
+    const CullPlan plan = PlanTile(p);
+    const CullSource& src = plan.src;
+    const bool list = plan.list;
     // Raster walk: lane = column (fx), lanes 0..31 carry the tile's 32 rows' fy (the
     // GenerateRays expression; bit-identical since every ray has the same offset).
     const float fx_lane = s.fx[0];
@@ -1310,6 +1370,40 @@ __global__ __launch_bounds__(kWave * W) void TraceCullKernel(TraceParams p) {
             CullWalk<W, false, false, true>(p, sh, s, bb, wb, fx_lane, fy_lane, src);
         } else {
             CullWalk<W, false, false, false>(p, sh, s, bb, wb, fx_lane, fy_lane, src);
+        }
+    }
+    if (plan.chunks > 1) {
+        // Several blocks share this tile: merge this block's hits into the tile's global
+        // keys (atomic min = the same lexicographic (t, id) rule), and the last block to
+        // finish (agent-scope release/acquire around a per-tile counter) shades the tile.
+        const int xc = min(x, p.width - 1);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int yc = min(y0 + r, p.row_count - 1);
+            if (s.bi[r] >= 0) {
+                atomicMin(&p.tile_keys[static_cast<size_t>(yc) * p.width + xc], HitKey(s.bt[r], s.bi[r]));
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            const unsigned done = atomicAdd(&p.tile_done[blockIdx.y * gridDim.x + blockIdx.x], 1u);
+            sh.shared_fx = done + 1u == plan.chunks ? 1u : 0u;  // reused as the "last block" flag
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
+        if (sh.shared_fx == 0u) {
+            return;
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int yc = min(y0 + r, p.row_count - 1);
+            const unsigned long long key = __hip_atomic_load(&p.tile_keys[static_cast<size_t>(yc) * p.width + xc],
+                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s.bt[r] = key == ~0ull ? __builtin_inff() : __uint_as_float(static_cast<unsigned>(key >> 32));
+            s.bi[r] = key == ~0ull ? -1 : static_cast<int>(static_cast<unsigned>(key));
         }
     }
     ShadeAndStore<R>(p, x, y0, s);
@@ -1350,6 +1444,10 @@ hipError_t LaunchPrepare(const float* d_vertices, std::uint64_t n, const Frame& 
     const unsigned blocks = (p.n_pad + 255) / 256;
     hipLaunchKernelGGL(PrepareKernel, dim3(blocks), dim3(256), 0, stream, p);
     return hipGetLastError();
+}
+
+std::size_t CullTiles(std::size_t width, std::size_t row_count) {
+    return (width + kWave - 1) / kWave * ((row_count + kTileRows - 1) / kTileRows);
 }
 
 std::size_t CullSuperTiles(std::size_t width, std::size_t row_count) {
@@ -1394,6 +1492,9 @@ hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_ver
     {
         const char* r = std::getenv("SRT_CULL_RASTER");
         p.allow_raster = (r != nullptr && std::strcmp(r, "0") == 0) ? 0 : 1;
+        const char* c = std::getenv("SRT_CULL_CHUNK");
+        const long chunk = c != nullptr ? std::strtol(c, nullptr, 10) : 0;
+        p.chunk_ids = chunk >= 64 ? static_cast<unsigned>(chunk) : 512u;
     }
     p.wf = static_cast<float>(band.width);
     p.hf = static_cast<float>(band.height);
@@ -1420,6 +1521,8 @@ hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_ver
             b.super_q = reinterpret_cast<uint4*>(bins->super_q);
             b.lists = bins->lists;
             b.counts = bins->counts;
+            b.tile_keys = reinterpret_cast<unsigned long long*>(bins->tile_keys);
+            b.tile_done = bins->tile_done;
             b.capacity = bins->capacity;
             b.n_pad = p.n_pad;
             b.supers_x = static_cast<int>(sx);
@@ -1434,11 +1537,14 @@ hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_ver
             p.bin_lists = bins->lists;
             p.bin_counts = bins->counts;
             p.bin_capacity = bins->capacity;
+            p.tile_keys = b.tile_keys;
+            p.tile_done = b.tile_done;
         }
+        const unsigned gz = bins != nullptr ? kMaxChunks : 1u;
         switch (CullWavesFromEnv()) {
-            case 4: hipLaunchKernelGGL(TraceCullKernel<4>, dim3(gx, gy), dim3(kWave * 4), 0, stream, p); break;
-            case 16: hipLaunchKernelGGL(TraceCullKernel<16>, dim3(gx, gy), dim3(kWave * 16), 0, stream, p); break;
-            default: hipLaunchKernelGGL(TraceCullKernel<8>, dim3(gx, gy), dim3(kWave * 8), 0, stream, p); break;
+            case 4: hipLaunchKernelGGL(TraceCullKernel<4>, dim3(gx, gy, gz), dim3(kWave * 4), 0, stream, p); break;
+            case 16: hipLaunchKernelGGL(TraceCullKernel<16>, dim3(gx, gy, gz), dim3(kWave * 16), 0, stream, p); break;
+            default: hipLaunchKernelGGL(TraceCullKernel<8>, dim3(gx, gy, gz), dim3(kWave * 8), 0, stream, p); break;
         }
     } else {
         constexpr int kRowsPerBlock = kRowsPerLane * kLdsWaves;

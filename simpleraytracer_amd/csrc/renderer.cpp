@@ -132,8 +132,7 @@ DeviceScene::~DeviceScene() {
     (void)hipFree(m_vertices);
     (void)hipFree(m_albedo);
     (void)hipFree(m_edges);
-    (void)hipFree(m_bin_lists);
-    (void)hipFree(m_bin_counts);
+    (void)hipFree(m_cull_work);
     if (prev >= 0) {
         (void)hipSetDevice(prev);
     }
@@ -161,23 +160,32 @@ void DeviceScene::Trace(const float* d_offsets, float* d_rgba, std::size_t row_b
     CullBins bins{};
     const CullBins* use_bins = nullptr;
     if (variant == kTraceCull && row_count != 0 && CullBinningEnabled()) {
+        // One grow-only allocation: super-tile boxes | tile keys | lists | counts | tile counters.
         const std::size_t supers = CullSuperTiles(m_width, row_count);
+        const std::size_t tiles = CullTiles(m_width, row_count);
         const unsigned cap = CullBinCapacity(m_n, supers);
-        const std::size_t entries = supers * cap + 4;
-        if (entries > m_bin_list_entries || supers > m_bin_supers) {
-            HipCheck(hipStreamSynchronize(stream), "hipStreamSynchronize(bin lists)");
-            (void)hipFree(m_bin_lists);
-            (void)hipFree(m_bin_counts);
-            m_bin_lists = nullptr;
-            m_bin_counts = nullptr;
-            m_bin_list_entries = m_bin_supers = 0;
-            m_bin_lists = DeviceAlloc<unsigned>(entries, "hipMalloc(bin lists)");
-            m_bin_counts = DeviceAlloc<unsigned>(supers * 5, "hipMalloc(bin counts)");
-            m_bin_list_entries = entries;
-            m_bin_supers = supers;
+        const std::size_t q_bytes = supers * 16;
+        const std::size_t key_bytes = row_count * m_width * 8;
+        const std::size_t list_bytes = (supers * cap + 4) * 4;
+        const std::size_t count_bytes = supers * 4;
+        const std::size_t done_bytes = tiles * 4;
+        const std::size_t bytes = q_bytes + key_bytes + list_bytes + count_bytes + done_bytes;
+        if (bytes > m_cull_bytes) {
+            HipCheck(hipStreamSynchronize(stream), "hipStreamSynchronize(cull work)");
+            (void)hipFree(m_cull_work);
+            m_cull_work = nullptr;
+            m_cull_bytes = 0;
+            m_cull_work = DeviceAlloc<unsigned char>(bytes, "hipMalloc(cull work)");
+            m_cull_bytes = bytes;
         }
-        // super_q first (uint4 per super-tile, 16-B aligned), then the counts.
-        bins = CullBins{m_bin_lists, m_bin_counts + 4 * supers, m_bin_counts, cap, supers};
+        unsigned char* w = m_cull_work;
+        bins.super_q = reinterpret_cast<unsigned*>(w);
+        bins.tile_keys = w + q_bytes;
+        bins.lists = reinterpret_cast<unsigned*>(w + q_bytes + key_bytes);
+        bins.counts = reinterpret_cast<unsigned*>(w + q_bytes + key_bytes + list_bytes);
+        bins.tile_done = reinterpret_cast<unsigned*>(w + q_bytes + key_bytes + list_bytes + count_bytes);
+        bins.capacity = cap;
+        bins.supers = supers;
         use_bins = &bins;
     }
     HipCheck(LaunchTrace(m_edges, m_n, m_vertices, m_albedo, m_frame, m_background, band, variant, use_bins, stream),

@@ -57,12 +57,10 @@ private:
     Frame m_frame{};
     std::size_t m_width = 0;
     std::size_t m_height = 0;
-    // Cull variant bin lists (render.h CullBins), grown on demand by Trace; disabled by env
-    // SRT_CULL_BIN=0 (every tile then streams every record).
-    mutable unsigned* m_bin_lists = nullptr;
-    mutable unsigned* m_bin_counts = nullptr;
-    mutable std::size_t m_bin_list_entries = 0;
-    mutable std::size_t m_bin_supers = 0;
+    // Cull variant work buffers (render.h CullBins: bin lists, split-tile keys), grown on
+    // demand by Trace; disabled by env SRT_CULL_BIN=0 (every tile then streams every record).
+    mutable unsigned char* m_cull_work = nullptr;
+    mutable std::size_t m_cull_bytes = 0;
 };
 
 // Trace kernel variant from env SRT_TRACE_VARIANT ("lds" | "scalar" | "cull", default cull).

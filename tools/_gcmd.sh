@@ -2,4 +2,10 @@ set -u
 cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS GRBM_GUI_ACTIVE --kernel-include-regex "Bin|Trace|Super" -d gpurun_out/pmc_sq2 -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-e2e > gpurun_out/pmc_sq2.log 2>&1
+timeout -k 10 600 python -m pytest tests -m gpu -q -x > gpurun_out/pytest_gpu.log 2>&1; rc=$?; tail -2 gpurun_out/pytest_gpu.log; [ $rc -le 1 ] || exit $rc
+for w in 8 16 4; do
+  SRT_CULL_WAVES=$w timeout -k 10 300 python bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-e2e > gpurun_out/bench_w$w.log 2>&1 || exit 1
+done
+for c in 512 2048; do
+  SRT_CULL_CHUNK=$c timeout -k 10 300 python bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-e2e > gpurun_out/bench_chunk$c.log 2>&1 || exit 1
+done

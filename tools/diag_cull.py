@@ -43,21 +43,28 @@ def main():
         for _ in range(3):
             scene.trace(off, out, 0, h, variant="cull", stream=stream)
         torch.cuda.synchronize()
-        buf = np.zeros((16384, 8), np.uint64)
+        buf = np.zeros((65536, 8), np.uint64)
         assert lib.srtDiagRead(buf.ctypes.data, buf.nbytes) == 0, _native.last_error()
         scene.close()
     shape = "8x4 tiles, bins " + os.environ.get("SRT_CULL_BIN", "1")
     gx, gy = (w + 63) // 64, (h + 31) // 32
-    d = buf[: gx * gy].astype(np.float64)
+    allb = buf[: gx * gy * 8].astype(np.float64)
+    ran = (allb[:, 7].astype(np.int64) & 4) != 0
+    d = allb[ran]
+    chunks = ran.reshape(8, gy * gx).sum(0)
+    tile_max = allb[:, 6].reshape(8, gy * gx).max(0)
     names = ["stream", "gather", "walk", "surv", "wsurv0", "batches", "total", "mode"]
     summary = {"shape": shape, "blocks": gx * gy}
     for i, n in enumerate(names):
         col = d[:, i]
         summary[n] = {"mean": float(col.mean()), "p50": float(np.median(col)), "p90": float(np.percentile(col, 90)),
                       "max": float(col.max())}
-    heavy = np.argsort(-d[:, 6])[:8]
-    summary["heaviest"] = [{"block": int(b), "bx": int(b % gx), "by": int(b // gx),
-                            **{n: int(d[b, i]) for i, n in enumerate(names)}} for b in heavy]
+    summary["chunks_hist"] = {int(c): int((chunks == c).sum()) for c in np.unique(chunks)}
+    summary["blocks_run"] = int(ran.sum())
+    idx = np.nonzero(ran)[0]
+    heavy = idx[np.argsort(-allb[idx, 6])[:8]]
+    summary["heaviest"] = [{"block": int(b), "z": int(b // (gx * gy)), "bx": int(b % gx), "by": int((b // gx) % gy),
+                            **{n: int(allb[b, i]) for i, n in enumerate(names)}} for b in heavy]
     print(json.dumps(summary, indent=1))
 
 
