@@ -94,7 +94,9 @@ def test_oracle_matches_float64_moller_trumbore(tmp_path, tris, rays):
         valid = [(hh[0], i) for i, hh in enumerate(hits) if hh is not None and hh[0] is not None]
         want = min(valid)[1] if valid else -1
         if got == want:
-            if got >= 0:
+            # depth accuracy away from edges; on an edge (or vertex) of a sliver, float32
+            # edge functions cancel and t = vol / det is ill-conditioned
+            if got >= 0 and margin(hits[got]) >= EDGE_EPS:
                 assert abs(t32 - hits[got][0]) <= 1e-4 * hits[got][0]
             continue
         # disagreement: must be a float32-undecidable configuration
