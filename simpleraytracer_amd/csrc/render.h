@@ -42,8 +42,11 @@ constexpr float kScreenBoxRange = 4.0f;
 // q = v * kQuantScale, lo rounded down and hi up, clamped to [-32767, 32767].
 constexpr float kQuantScale = 4096.0f;
 
-// Floats per record in the edge allocation: 10 (tiles) + 4 (screen box) + 2 (quantized box).
-constexpr int kEdgeFloatsPerTriangle = 16;
+// Cull records (render.hip CullRecord): 64 B per record, at the record's rank in the scene's
+// spatial order, after the quantized boxes.
+// Floats per record in the edge allocation: 10 (tiles) + 4 (screen box) + 2 (quantized box)
+// + 16 (cull record).
+constexpr int kEdgeFloatsPerTriangle = 32;
 
 inline std::uint64_t PaddedTriangleCount(std::uint64_t n) {
     const std::uint64_t p = (n + kPadTriangles - 1) / kPadTriangles * kPadTriangles;
@@ -66,29 +69,43 @@ struct BandArgs {
     std::size_t row_count;
 };
 
-// Launch the prepare kernel: writes PaddedTriangleCount(n) / kTileTriangles tiles into `edges`.
-hipError_t LaunchPrepare(const float* d_vertices, std::uint64_t n, const Frame& frame, float* d_edges,
-                         hipStream_t stream);
+// Launch the prepare kernel: writes PaddedTriangleCount(n) / kTileTriangles tiles into `edges`,
+// then the screen boxes, quantized boxes and cull records (d_rank: id -> spatial-order rank).
+hipError_t LaunchPrepare(const float* d_vertices, const unsigned* d_rank, std::uint64_t n, const Frame& frame,
+                         float* d_edges, hipStream_t stream);
 
-// Bin lists of the cull variant's first level (render.hip BinKernel): per super-tile of a
-// band (128 x 32 pixels), up to `capacity` candidate record ids and their count.
+// Cull tiles: 64 columns x 32 rows of rays, one trace block each (render.hip "Cull bins").
+constexpr int kCullTileCols = 64;
+constexpr int kCullTileRows = 32;
+constexpr int kMaxBoundTiles = 2048;  // binning needs tiles_x + tiles_y <= this
+constexpr int kMaxBinTiles = 8192;    // and tiles_x * tiles_y <= this (bin kernel LDS histogram)
+
+// Work buffers of the cull variant's bins for one band shape (one allocation, carved by
+// CullBinLayout; it must be zero-filled when allocated: the counters reset themselves).
 struct CullBins {
-    unsigned* lists;      // supers x capacity (+4 padding) ids
-    unsigned* counts;     // supers
-    unsigned* super_q;    // supers x 4: quantized super-tile boxes (SuperBoxKernel)
-    void* tile_keys;      // row_count x width u64: (t, id) keys of tiles split over blocks
-    unsigned* tile_done;  // tiles: finished blocks of a split tile
+    const unsigned* order; // the scene's record ids in spatial order (DeviceScene; not in the buffer)
+    void* tile_info;       // tiles x 32 B: ray box, uniform offset (TileInfoKernel)
+    unsigned* counts;      // tiles + 1: list lengths, then the large-list length
+    unsigned* lists;       // tiles x capacity candidate ids (BinTrianglesKernel)
+    unsigned* large_list;  // PaddedTriangleCount(n) ids binned to every tile
+    unsigned* tile_order;  // tiles x parts: trace launch order of (tile, part), most work first
     unsigned capacity;
-    std::size_t supers;
+    std::size_t tiles;
 };
 
-// Tiles (64 x 32 pixels) of a width x row_count band.
+// Tiles (64 x 32 rays) of a width x row_count band.
 std::size_t CullTiles(std::size_t width, std::size_t row_count);
 
-// Super-tiles of a width x row_count band, and the per-list capacity used for n triangles
-// (a list that overflows makes its tiles stream every record; results are unaffected).
-std::size_t CullSuperTiles(std::size_t width, std::size_t row_count);
-unsigned CullBinCapacity(std::uint64_t n, std::size_t supers);
+// Whether a band shape can be binned (its tile grid fits the bin kernel's LDS).
+bool CullBinnable(std::size_t width, std::size_t row_count);
+
+// Per-tile list capacity for n triangles (a list that overflows makes its tile stream every
+// record; results are unaffected). Env SRT_CULL_BIN_CAP overrides it (tests).
+unsigned CullBinCapacity(std::uint64_t n, std::size_t tiles);
+
+// Bytes of the bin work buffer for n triangles and a band shape, and its carve-up.
+std::size_t CullBinBytes(std::uint64_t n, std::size_t width, std::size_t row_count);
+CullBins CullBinLayout(void* base, std::uint64_t n, std::size_t width, std::size_t row_count);
 
 // Launch the trace kernel over one band (cull variant: bin + trace; bins == nullptr streams
 // every record for every tile).

@@ -30,6 +30,21 @@ constexpr int kWave = 64;
 constexpr int kLdsWaves = 4;     // waves per block in the LDS variant
 constexpr int kRowsPerLane = 8;  // rays per lane (LDS / scalar variants): one column, 8 rows
 
+// Cull record (the binned cull path's copy of one edge record, 64 B, stored at the record's
+// rank in the scene's spatial order): a = (c0A, cxA, cyA, c0B), b = (cxB, cyB, c0C, cxC),
+// x = (cyC, vol, id bits, 0), sb = screen box.
+struct CullRecord {
+    float4 a, b, x, sb;
+};
+
+// Per-tile facts the cull trace and the bin kernel share (TileInfoKernel), 32 B.
+struct TileInfo {
+    float4 box;         // (xlo, xhi, ylo, yhi) of the tile's ray positions (NaN positions drop out)
+    float ox, oy;       // sample offset of the tile's first ray
+    unsigned regular;   // every ray of the tile has offset (ox, oy), bit for bit
+    unsigned usable;    // box within the screen-box range (else the tile streams every record)
+};
+
 struct TraceParams {
     const float4* __restrict__ edges;
     const float4* __restrict__ screen_boxes;
@@ -44,12 +59,17 @@ struct TraceParams {
     int row_count;
     int row_begin;
     int allow_raster;  // cull variant: raster walk for uniform-offset tiles (env SRT_CULL_RASTER=0 disables)
-    const unsigned* __restrict__ bin_lists;   // cull variant: per super-tile candidate ids (BinKernel)
-    const unsigned* __restrict__ bin_counts;  // null: stream every record
+    // Cull variant with bins (render.h CullBins); tile_info == null: no bins, every tile
+    // computes its own ray box and streams every record.
+    const TileInfo* __restrict__ tile_info;   // per tile: ray box, uniform offset (TileInfoKernel)
+    const CullRecord* __restrict__ cull;      // cull records in spatial order (the lists hold positions)
+    const unsigned* __restrict__ order;       // spatial-order position -> record id
+    const unsigned* __restrict__ tile_order;  // block -> tile, most work first (TileOrderKernel)
+    const unsigned* __restrict__ bin_lists;   // per tile: candidate ids (BinTrianglesKernel)
+    const unsigned* __restrict__ bin_counts;  // per tile: list length; [tiles]: large-list length
+    const unsigned* __restrict__ large_list;  // ids of records binned to every tile
     unsigned bin_capacity;
-    unsigned chunk_ids;                          // cull: list ids per block of a split tile
-    unsigned long long* __restrict__ tile_keys;  // cull, split tiles: per-pixel (t, id) keys (band)
-    unsigned* __restrict__ tile_done;            // cull, split tiles: finished blocks per tile
+    unsigned exp;                                // diagnostic build: experiment bits (env SRT_EXP), 0 in the product
     float wf;
     float hf;
     float base[3];
@@ -60,9 +80,11 @@ struct TraceParams {
 
 struct PrepareParams {
     const float* __restrict__ vertices;
+    const unsigned* __restrict__ rank;  // record id -> position in the spatial order
     float4* __restrict__ edges;
     float4* __restrict__ screen_boxes;
     uint2* __restrict__ qboxes;
+    CullRecord* __restrict__ cull;
     unsigned n;
     unsigned n_pad;
     float origin[3];
@@ -228,6 +250,14 @@ __global__ __launch_bounds__(256) void PrepareKernel(PrepareParams p) {
     p.screen_boxes[i] = sb;
     // Stored as (hi, -lo) pairs so the cull test is one saturating packed add per axis.
     p.qboxes[i] = make_uint2(PackI16(QuantHi(sb.y), -QuantLo(sb.x)), PackI16(QuantHi(sb.w), -QuantLo(sb.z)));
+    if (i < p.n) {
+        CullRecord r;
+        r.a = make_float4(c[0], c[1], c[2], c[3]);
+        r.b = make_float4(c[4], c[5], c[6], c[7]);
+        r.x = make_float4(c[8], vol, __uint_as_float(i), 0.f);
+        r.sb = sb;
+        p.cull[p.rank[i]] = r;
+    }
 }
 
 // Per-lane ray state: R rays sharing one image column.
@@ -644,35 +674,54 @@ __device__ __forceinline__ void LoadRecord(const float4* __restrict__ edges, uns
 
 // Cull tile = one trace block: 64 columns x 32 rows of rays, W waves (4, 8 or 16) of 64 x R
 // rays, R = 32 / W rays per lane. Constants that depend on W live in CullShape<W>.
-constexpr int kTileRows = 32;
+constexpr int kTileRows = 32;   // cull tile (bins): 64 columns x 32 rows
+constexpr int kBlockRows = 16;  // trace block: one part of a cull tile
+constexpr int kParts = kTileRows / kBlockRows;
 constexpr int kStreamStep = 2048;  // FULL stream: records per block per step
 constexpr int kListG = 4;          // LIST stream: ids per lane per step
+constexpr int kPacketBatch = 512;  // packet walk: survivors gathered per batch
 static_assert(kPadTriangles % kStreamStep == 0, "a stream step must cover whole pad units");
 
 template <int W>
 struct CullShape {
-    static constexpr int kR = kTileRows / W;              // rays per lane
+    static constexpr int kR = kBlockRows / W;             // rays per lane
     static constexpr int kThreads = kWave * W;
     static constexpr int kStreamG = kStreamStep / kThreads;  // FULL: records per lane per step
     static constexpr int kBatch = 256;                    // survivors gathered per flush batch
     static constexpr int kShare = kBatch / W;             // raster walk: batch entries per wave
-    static constexpr int kListCap = kBatch + kStreamStep;  // block id list: < kBatch + one step
+    static constexpr int kListStep = kThreads * kListG;     // LIST stream: ids per block per step
+    static constexpr int kPBatch = kThreads > kPacketBatch ? kThreads : kPacketBatch;  // packet walk batch
+    static constexpr int kListCap = kBatch + (kListStep > kStreamStep ? kListStep : kStreamStep);  // < kBatch + one step
 };
 
 template <int W>
 struct CullShared {
-    unsigned ids[CullShape<W>::kListCap];
-    float4 st0[CullShape<W>::kBatch];  // gathered records: plane 0
-    float4 st1[CullShape<W>::kBatch];  //                   plane 1
-    float4 st2[CullShape<W>::kBatch];  //                   (cyC, vol, id, 0)
-    float4 st3[CullShape<W>::kBatch];  //                   screen box
-    unsigned hit[CullShape<W>::kBatch];  // raster walk: record may touch the tile (box + edge tests)
-    int counts[2][W];
+    union {
+        struct {  // stream walk (CullWalk)
+            unsigned ids[CullShape<W>::kListCap];
+            float4 st0[CullShape<W>::kBatch];  // gathered records: plane 0
+            float4 st1[CullShape<W>::kBatch];  //                   plane 1
+            float4 st2[CullShape<W>::kBatch];  //                   (cyC, vol, id, 0)
+            float4 st3[CullShape<W>::kBatch];  //                   screen box
+            unsigned hit[CullShape<W>::kBatch];  // raster walk: record may touch the tile (box + edge tests)
+            int counts[2][W];
+        } s;
+        struct {  // packet walk (PacketWalk): one batch of compacted survivors
+            float4 sv0[CullShape<W>::kPBatch];  // plane 0
+            float4 sv1[CullShape<W>::kPBatch];  // plane 1
+            float4 sv2[CullShape<W>::kPBatch];  // (cyC, vol, id, pixel range bits)
+            unsigned pre[CullShape<W>::kPBatch + 1];  // exclusive packet prefix, pre[S] = packets
+            unsigned wave_n[CullShape<W>::kPBatch / kWave];   // survivors per (slice, wave)
+            unsigned wave_pk[CullShape<W>::kPBatch / kWave];  // packets per (slice, wave)
+            float fxs[kWave];                // fx of the tile's columns
+            float fys[kBlockRows];           // fy of the block's rows
+        } k;
+    } u;
     Box wave_box[W];
     unsigned shared_fx;
     unsigned regular;
-    // Raster walk: per-pixel lexicographic (t, id) keys of the tile's 32 x 64 rays.
-    unsigned long long keys[kTileRows][kWave];
+    // Raster walks: per-pixel lexicographic (t, id) keys of the tile's 32 x 64 rays.
+    unsigned long long keys[kBlockRows][kWave];
 };
 
 // (t, id) packed so that unsigned order is lexicographic order: t >= 0 here (vol > 0,
@@ -710,7 +759,7 @@ __device__ __forceinline__ void RasterSurvivor(unsigned long long (*keys)[kWave]
     for (int rr = r0; rr <= r1; rr += step) {
         const int row = rr + (lane >> lg);
         const float fx = __shfl(fx_lane, col);
-        const float fy = __shfl(fy_lane, row & (kTileRows - 1));
+        const float fy = __shfl(fy_lane, row & (kBlockRows - 1));
         if (col <= c1 && row <= r1) {
             const float eA = fmaf(fy, q.cyA, fmaf(fx, q.cxA, q.c0A));
             const float eB = fmaf(fy, q.cyB, fmaf(fx, q.cxB, q.c0B));
@@ -729,12 +778,16 @@ __device__ __forceinline__ void RasterSurvivor(unsigned long long (*keys)[kWave]
 }
 
 // Per-tile source of candidate records for the cull stream: every record of the scene
-// (FULL), or the id list the bin kernel built for the tile's super-tile (LIST).
+// (FULL), or (LIST) the tile's bin list followed by the large list (records binned to every
+// tile), as one virtual list of which this block takes positions [begin, end).
 struct CullSource {
-    const unsigned* list;  // LIST: ids (this block's chunk of the super-tile list)
-    unsigned count;        // LIST: number of ids
-    unsigned step0;        // FULL: first record step of this block's chunk
-    unsigned steps;        // FULL: record steps of this block's chunk
+    const unsigned* list;   // LIST: the tile's ids (virtual positions < count1)
+    const unsigned* list2;  // LIST: large-list ids (virtual position v >= count1: list2[v - count1])
+    unsigned count1;        // LIST: ids in the tile's list
+    unsigned begin;         // LIST: this block's virtual positions [begin, end)
+    unsigned end;
+    unsigned step0;         // FULL: first record step of this block's chunk
+    unsigned steps;         // FULL: record steps of this block's chunk
 };
 
 // Streams the tile's candidates, keeps those whose quantized screen box overlaps the tile's
@@ -744,7 +797,7 @@ struct CullSource {
 template <int W, bool SHARED, bool RASTER, bool LIST>
 __device__ __forceinline__ void CullWalk(const TraceParams& p, CullShared<W>& sh, Rays<CullShape<W>::kR>& s,
                                          const Box& bb, const Box& wb, float fx_lane, float fy_lane,
-                                         CullSource src) {
+                                         CullSource src, unsigned tile) {
     using S = CullShape<W>;
     constexpr int R = S::kR;
     constexpr int kThreads = S::kThreads;
@@ -761,10 +814,10 @@ __device__ __forceinline__ void CullWalk(const TraceParams& p, CullShared<W>& sh
     const bool wave_sb = ScreenBoxUsable(wb);
     const QBox bq = Quantize(bb);
     const unsigned long long lt_mask = (1ull << lane) - 1ull;
-    const unsigned nsteps = LIST ? (src.count + kStep - 1) / kStep : src.steps;
+    const unsigned nsteps = LIST ? (src.end - src.begin + kStep - 1) / kStep : src.steps;
 
     if constexpr (RASTER) {
-        for (int i = tid; i < kTileRows * kWave; i += kThreads) {
+        for (int i = tid; i < kBlockRows * kWave; i += kThreads) {
             (&sh.keys[0][0])[i] = ~0ull;
         }  // visible to every wave after the first stream barrier
     }
@@ -774,21 +827,26 @@ __device__ __forceinline__ void CullWalk(const TraceParams& p, CullShared<W>& sh
     unsigned long long d_mark = d_t0;
 #endif
     // FULL: lane tid of step k reads records k * kStep + 2 * (l * kThreads + tid) + {0, 1}
-    //       (one 16-B load per record pair); LIST: ids k * kStep + 4 * tid + {0..3} of the
-    //       list (one 16-B load) and their 8-B boxes. The whole step is loaded one step ahead.
+    //       (one 16-B load per record pair); LIST: virtual positions begin + k * kStep +
+    //       g * kThreads + tid (coalesced 4-B id loads) and their 8-B boxes. The whole step is
+    //       loaded one step ahead.
     constexpr int L = LIST ? 1 : G / 2;
     const uint4* __restrict__ qbox4 = reinterpret_cast<const uint4*>(qbox);
     uint4 nb[L];
-    uint4 nid = make_uint4(0u, 0u, 0u, 0u);
+    unsigned nid[LIST ? kListG : 1];
     uint2 nq[LIST ? kListG : 1];
     auto fetch = [&](unsigned k) {
         if constexpr (LIST) {
-            const unsigned i0 = k * kStep + 4 * tid;
-            nid = i0 < src.count ? *reinterpret_cast<const uint4*>(src.list + i0) : make_uint4(0u, 0u, 0u, 0u);
-            const unsigned v[4] = {nid.x, nid.y, nid.z, nid.w};
 #pragma unroll
             for (int g = 0; g < kListG; ++g) {
-                nq[g] = (i0 + g < src.count) ? qbox[v[g]] : make_uint2(0x80018001u, 0x80018001u);  // empty box
+                const unsigned v = src.begin + k * kStep + g * kThreads + tid;
+                const bool in = v < src.end;
+                nid[g] = in ? p.order[v < src.count1 ? src.list[v] : src.list2[v - src.count1]] : 0u;
+            }
+#pragma unroll
+            for (int g = 0; g < kListG; ++g) {
+                const unsigned v = src.begin + k * kStep + g * kThreads + tid;
+                nq[g] = v < src.end ? qbox[nid[g]] : make_uint2(0x80018001u, 0x80018001u);  // empty box
             }
         } else {
 #pragma unroll
@@ -804,7 +862,7 @@ __device__ __forceinline__ void CullWalk(const TraceParams& p, CullShared<W>& sh
     for (unsigned k = 0; k < nsteps; ++k) {
         uint4 cb[L];
         uint2 cq[LIST ? kListG : 1];
-        const uint4 cid = nid;
+        unsigned cid[LIST ? kListG : 1];
 #pragma unroll
         for (int l = 0; l < L; ++l) {
             cb[l] = nb[l];
@@ -812,13 +870,14 @@ __device__ __forceinline__ void CullWalk(const TraceParams& p, CullShared<W>& sh
 #pragma unroll
         for (int g = 0; g < (LIST ? kListG : 1); ++g) {
             cq[g] = nq[g];
+            cid[g] = nid[g];
         }
         if (k + 1 < nsteps) {
             fetch(k + 1);
         }
         auto record_id = [&](int g) -> unsigned {
             if constexpr (LIST) {
-                return g == 0 ? cid.x : (g == 1 ? cid.y : (g == 2 ? cid.z : cid.w));
+                return cid[g];
             } else {
                 return (src.step0 + k) * kStep + 2 * ((g >> 1) * kThreads + tid) + (g & 1);
             }
@@ -843,14 +902,14 @@ __device__ __forceinline__ void CullWalk(const TraceParams& p, CullShared<W>& sh
         }
         const unsigned ph = k & 1u;
         if (lane == 0) {
-            sh.counts[ph][wave] = wave_n;
+            sh.u.s.counts[ph][wave] = wave_n;
         }
         __syncthreads();
         int off = total;
         int step_n = 0;
 #pragma unroll
         for (int w = 0; w < W; ++w) {
-            const int cw = sh.counts[ph][w];
+            const int cw = sh.u.s.counts[ph][w];
             off += w < wave ? cw : 0;
             step_n += cw;
         }
@@ -860,7 +919,7 @@ __device__ __forceinline__ void CullWalk(const TraceParams& p, CullShared<W>& sh
                 const bool pass = (bits >> g) & 1u;
                 const unsigned long long m = __ballot(pass);
                 if (pass) {
-                    sh.ids[off + __popcll(m & lt_mask)] = record_id(g);
+                    sh.u.s.ids[off + __popcll(m & lt_mask)] = record_id(g);
                 }
                 off += __popcll(m);
             }
@@ -885,21 +944,21 @@ __device__ __forceinline__ void CullWalk(const TraceParams& p, CullShared<W>& sh
             if (tid >= kBatch) {
                 // not a gathering thread
             } else if (e < total) {
-                const unsigned id = sh.ids[e];
+                const unsigned id = sh.u.s.ids[e];
                 float4 p0, p1;
                 float cyC, vol;
                 LoadRecord(p.edges, id, p0, p1, cyC, vol);
                 const float4 sb = sbox[id];
-                sh.st0[tid] = p0;
-                sh.st1[tid] = p1;
-                sh.st2[tid] = make_float4(cyC, vol, __uint_as_float(id), 0.f);
-                sh.st3[tid] = sb;
+                sh.u.s.st0[tid] = p0;
+                sh.u.s.st1[tid] = p1;
+                sh.u.s.st2[tid] = make_float4(cyC, vol, __uint_as_float(id), 0.f);
+                sh.u.s.st3[tid] = sb;
                 if constexpr (RASTER) {
                     const Record r{p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w, cyC};
-                    sh.hit[tid] = ((!block_sb || ScreenBoxOverlaps(bb, sb)) && BoxMayHit(bb, r)) ? 1u : 0u;
+                    sh.u.s.hit[tid] = ((!block_sb || ScreenBoxOverlaps(bb, sb)) && BoxMayHit(bb, r)) ? 1u : 0u;
                 }
             } else if constexpr (RASTER) {
-                sh.hit[tid] = 0u;
+                sh.u.s.hit[tid] = 0u;
             }
             __syncthreads();
 #ifdef SRT_DIAG
@@ -914,7 +973,7 @@ __device__ __forceinline__ void CullWalk(const TraceParams& p, CullShared<W>& sh
             if constexpr (RASTER) {
                 // This wave's share of the batch: entries wave * 64 .. wave * 64 + 63.
                 const int c0 = wave * S::kShare;
-                unsigned long long m = __ballot(lane < S::kShare && sh.hit[c0 + lane] != 0u);
+                unsigned long long m = __ballot(lane < S::kShare && sh.u.s.hit[c0 + lane] != 0u);
 #ifdef SRT_DIAG
                 d_wsurv += __popcll(m);
 #endif
@@ -922,13 +981,13 @@ __device__ __forceinline__ void CullWalk(const TraceParams& p, CullShared<W>& sh
                     // Software-pipelined: the next survivor's LDS reads are issued before the
                     // current one is walked, so their latency hides behind its work.
                     int bit = __builtin_ctzll(m);
-                    float4 a = sh.st0[c0 + bit], b = sh.st1[c0 + bit], x = sh.st2[c0 + bit], sb = sh.st3[c0 + bit];
+                    float4 a = sh.u.s.st0[c0 + bit], b = sh.u.s.st1[c0 + bit], x = sh.u.s.st2[c0 + bit], sb = sh.u.s.st3[c0 + bit];
                     for (;;) {
                         m &= m - 1ull;
                         const bool more = m != 0ull;
                         const int nbit = more ? __builtin_ctzll(m) : bit;
-                        const float4 an = sh.st0[c0 + nbit], bn = sh.st1[c0 + nbit], xn = sh.st2[c0 + nbit],
-                                     sbn = sh.st3[c0 + nbit];
+                        const float4 an = sh.u.s.st0[c0 + nbit], bn = sh.u.s.st1[c0 + nbit], xn = sh.u.s.st2[c0 + nbit],
+                                     sbn = sh.u.s.st3[c0 + nbit];
                         const Record r{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, x.x};
                         RasterSurvivor(sh.keys, r, x.y, __float_as_int(x.z), sb, block_sb, fx_lane, fy_lane, lane);
                         if (!more) {
@@ -946,9 +1005,9 @@ __device__ __forceinline__ void CullWalk(const TraceParams& p, CullShared<W>& sh
                     const int i = c0 + lane;
                     bool pass = false;
                     if (i < nb_here) {
-                        const float4 a = sh.st0[i], b = sh.st1[i], x = sh.st2[i];
+                        const float4 a = sh.u.s.st0[i], b = sh.u.s.st1[i], x = sh.u.s.st2[i];
                         const Record r{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, x.x};
-                        pass = (!wave_sb || ScreenBoxOverlaps(wb, sh.st3[i])) && BoxMayHit(wb, r);
+                        pass = (!wave_sb || ScreenBoxOverlaps(wb, sh.u.s.st3[i])) && BoxMayHit(wb, r);
                     }
                     unsigned long long m = __ballot(pass);
 #ifdef SRT_DIAG
@@ -956,12 +1015,12 @@ __device__ __forceinline__ void CullWalk(const TraceParams& p, CullShared<W>& sh
 #endif
                     if (m != 0ull) {
                         int bit = __builtin_ctzll(m);
-                        float4 a = sh.st0[c0 + bit], b = sh.st1[c0 + bit], x = sh.st2[c0 + bit];
+                        float4 a = sh.u.s.st0[c0 + bit], b = sh.u.s.st1[c0 + bit], x = sh.u.s.st2[c0 + bit];
                         for (;;) {
                             m &= m - 1ull;
                             const bool more = m != 0ull;
                             const int nbit = more ? __builtin_ctzll(m) : bit;
-                            const float4 an = sh.st0[c0 + nbit], bn = sh.st1[c0 + nbit], xn = sh.st2[c0 + nbit];
+                            const float4 an = sh.u.s.st0[c0 + nbit], bn = sh.u.s.st1[c0 + nbit], xn = sh.u.s.st2[c0 + nbit];
                             const Record r{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, x.x};
                             ExactTestAnyOrder<R, SHARED>(s, r, x.y, __float_as_int(x.z));
                             if (!more) {
@@ -989,7 +1048,7 @@ __device__ __forceinline__ void CullWalk(const TraceParams& p, CullShared<W>& sh
         __syncthreads();  // raster keys initialised by every wave before the read-back
     }
 #ifdef SRT_DIAG
-    const unsigned blk = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+    const unsigned blk = blockIdx.z * gridDim.y * gridDim.x + tile;
     if (tid == 0 && blk < kDiagBlocks) {
         unsigned long long* d = g_srt_diag[blk];
         d[0] = d_stream;
@@ -999,7 +1058,10 @@ __device__ __forceinline__ void CullWalk(const TraceParams& p, CullShared<W>& sh
         d[4] = d_wsurv;
         d[5] = d_batches;
         d[6] = __builtin_amdgcn_s_memtime() - d_t0;
-        d[7] = (RASTER ? 1 : 0) | (LIST ? 2 : 0) | 4;
+        d[7] = (RASTER ? 1 : 0) | (LIST ? 2 : 0) | 4 |
+               (p.bin_counts != nullptr ? (static_cast<unsigned long long>(p.bin_counts[tile]) << 16) |
+                                              (static_cast<unsigned long long>(p.bin_counts[gridDim.x * gridDim.y]) << 40)
+                                        : 0ull);
     }
 #endif
     if constexpr (RASTER) {
@@ -1014,27 +1076,368 @@ __device__ __forceinline__ void CullWalk(const TraceParams& p, CullShared<W>& sh
     }
 }
 
-// Super-tile = kSuperTiles tiles side by side (128 x 32 pixels): the unit of the bin lists.
-constexpr int kSuperTiles = 2;
+// ---------------------------------------------------------------------------------------
+// Packet walk: binned tiles (LIST) whose rays all share one sample offset, so fx depends on
+// the column only and fy on the row only, both monotone. Per batch of kPacketBatch list
+// entries:
+//   gather:  one thread per entry loads the record and its screen box, keeps it if it passes
+//            the tile-box tests (ScreenBoxOverlaps, BoxMayHit), and finds the exact column
+//            and row ranges of the tile whose ray positions lie inside the screen box (binary
+//            searches in the tile's fx / fy tables). Pixels outside those ranges cannot pass
+//            the exact test (screen-box guarantee), so skipping them is exact. The range is cut
+//            into packets of 64 pixels (2^lg columns x 64 >> lg rows, 2^lg >= the width).
+//   compact: survivors are compacted block-wide in any order, with an exclusive prefix of
+//            their packet counts;
+//   walk:    wave w takes the packets [w P / W, (w + 1) P / W) of the batch's P, two per
+//            iteration (independent dependency chains for the scheduler): each lane tests
+//            its pixel exactly and merges a hit into the pixel's key with an LDS atomic min.
+// Same exact test and lexicographic (t, id) result as ExactTestAnyOrder.
+// ---------------------------------------------------------------------------------------
+// One packet (64 pixels of one survivor's range) evaluated without branches: the pixel's
+// key and LDS address, and whether it is a hit (all E >= 0, det > 0, t finite; NaN anywhere
+// fails). `bits` = the survivor's packed pixel range (wave-uniform), `j` = packet index.
+struct PacketHit {
+    unsigned long long key;
+    unsigned addr;  // element index into the tile's keys
+    bool hit;
+};
+
+struct PacketPixel {
+    int col, row;
+    bool in;
+};
+
+__device__ __forceinline__ PacketPixel PacketLane(unsigned bits, unsigned j, int lane) {
+    const int c0 = bits & 63u, c1 = (bits >> 6) & 63u, r0 = (bits >> 12) & 31u, r1 = (bits >> 17) & 31u;
+    const int lg = (bits >> 22) & 7u;
+    const int col_u = c0 + (lane & ((1 << lg) - 1));
+    const int row_u = r0 + static_cast<int>(j << (6 - lg)) + (lane >> lg);
+    return PacketPixel{min(col_u, c1), min(row_u, r1), static_cast<bool>((col_u <= c1) & (row_u <= r1))};
+}
+
+__device__ __forceinline__ PacketHit EvalPacket(const float4& a, const float4& b, const float4& x, float fx, float fy,
+                                                const PacketPixel& px) {
+    const float eA = fmaf(fy, a.z, fmaf(fx, a.y, a.x));
+    const float eB = fmaf(fy, b.y, fmaf(fx, b.x, a.w));
+    const float eC = fmaf(fy, x.x, fmaf(fx, b.w, b.z));
+    const float det = (eA + eB) + eC;
+    const float t = x.y / det;
+    PacketHit h;
+    h.hit = static_cast<bool>(px.in & (fminf(fminf(eA, eB), eC) >= 0.f) & (det > 0.f) & (t < __builtin_inff()));
+    h.key = HitKey(t, __float_as_int(x.z));
+    h.addr = static_cast<unsigned>(px.row * kWave + px.col);
+    return h;
+}
+
+// Range search in a nondecreasing table t[0..n): an index guess from a linear model, clamped
+// to [0, n], then exact unit steps (a guess off by a few entries costs a few LDS reads).
+__device__ __forceinline__ int GuessIndex(float v, float first, float scale, int n) {
+    const float g = fminf(fmaxf((v - first) * scale, -1.f), static_cast<float>(n) + 1.f);  // NaN -> -1
+    return g != g ? 0 : static_cast<int>(g);
+}
+// First i with t[i] >= v (n if none).
+__device__ __forceinline__ int FirstAtLeast(const float* t, int n, float v, int g) {
+    g = min(max(g, 0), n);
+    while (g > 0 && t[g - 1] >= v) {
+        --g;
+    }
+    while (g < n && t[g] < v) {
+        ++g;
+    }
+    return g;
+}
+// Last i with t[i] <= v (-1 if none); g guesses the first i with t[i] > v.
+__device__ __forceinline__ int LastAtMost(const float* t, int n, float v, int g) {
+    g = min(max(g, 0), n);
+    while (g > 0 && t[g - 1] > v) {
+        --g;
+    }
+    while (g < n && t[g] <= v) {
+        ++g;
+    }
+    return g - 1;
+}
+
+template <int W>
+__device__ __forceinline__ void PacketWalk(const TraceParams& p, CullShared<W>& sh, Rays<CullShape<W>::kR>& s,
+                                           const Box& bb, float fx_lane, float fy_lane, const CullSource& src, int tx,
+                                           int row0) {
+    using S = CullShape<W>;
+    constexpr int R = S::kR;
+    constexpr int kThreads = S::kThreads;
+    constexpr int kBatchN = S::kPBatch;
+    constexpr int kSlices = kBatchN / kThreads;  // batch entries per thread
+    static_assert(kBatchN % kThreads == 0, "whole slices");
+    const int tid = threadIdx.x;
+    const int lane = tid & (kWave - 1);
+    const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);
+    const unsigned long long lt_mask = (1ull << lane) - 1ull;
+    auto& k = sh.u.k;
+    const int nc = min(kWave, p.width - tx * kWave);
+    const int nr = min(kBlockRows, p.row_count - row0);
+    if (tid < kWave) {
+        k.fxs[tid] = fx_lane;
+    }
+    if (tid < kBlockRows) {
+        k.fys[tid] = fy_lane;
+    }
+    for (int i = tid; i < kBlockRows * kWave; i += kThreads) {
+        (&sh.keys[0][0])[i] = ~0ull;
+    }
+    // Linear models of the (nondecreasing) column / row tables for the range guesses.
+    const float fx_first = __shfl(fx_lane, 0), fx_last = __shfl(fx_lane, nc - 1);
+    const float fy_first = __shfl(fy_lane, 0), fy_last = __shfl(fy_lane, nr - 1);
+    const float fx_scale = nc > 1 && fx_last > fx_first ? static_cast<float>(nc - 1) / (fx_last - fx_first) : 0.f;
+    const float fy_scale = nr > 1 && fy_last > fy_first ? static_cast<float>(nr - 1) / (fy_last - fy_first) : 0.f;
+    __syncthreads();
+    const unsigned total = src.end - src.begin;
+#ifdef SRT_DIAG
+    unsigned long long d_gather = 0, d_walk = 0, d_surv = 0, d_pk = 0, d_batches = 0;
+    const unsigned long long d_t0 = __builtin_amdgcn_s_memtime();
+    unsigned long long d_mark = d_t0;
+#endif
+#pragma unroll 1
+    for (unsigned b0 = 0; b0 < total; b0 += kBatchN) {
+        // Gather: entries b0 + e * kThreads + tid of the block's virtual list, all loads first.
+        CullRecord cr[kSlices];
+        bool pass[kSlices];
+#pragma unroll
+        for (int e = 0; e < kSlices; ++e) {
+            const unsigned v = b0 + e * kThreads + tid;
+            pass[e] = v < total;
+            const unsigned vv = src.begin + (pass[e] ? v : 0u);
+            cr[e] = p.cull[vv < src.count1 ? src.list[vv] : src.list2[vv - src.count1]];
+        }
+        unsigned bits[kSlices], npk[kSlices];
+#pragma unroll
+        for (int e = 0; e < kSlices; ++e) {
+            bits[e] = 0u;
+            npk[e] = 0u;
+            const float4 sb = cr[e].sb;
+            const Record r{cr[e].a.x, cr[e].a.y, cr[e].a.z, cr[e].a.w, cr[e].b.x, cr[e].b.y, cr[e].b.z, cr[e].b.w,
+                           cr[e].x.x};
+            pass[e] = pass[e] && ScreenBoxOverlaps(bb, sb) && BoxMayHit(bb, r);
+            if (pass[e]) {
+                // Columns c with sb.xlo <= fx[c] <= sb.xhi (fx nondecreasing in c); rows likewise.
+                // Interpolated guesses, then exact steps in the tables.
+                const int c0 = FirstAtLeast(k.fxs, nc, sb.x, GuessIndex(sb.x, fx_first, fx_scale, nc));
+                const int c1 = LastAtMost(k.fxs, nc, sb.y, GuessIndex(sb.y, fx_first, fx_scale, nc) + 1);
+                const int r0 = FirstAtLeast(k.fys, nr, sb.z, GuessIndex(sb.z, fy_first, fy_scale, nr));
+                const int r1 = LastAtMost(k.fys, nr, sb.w, GuessIndex(sb.w, fy_first, fy_scale, nr) + 1);
+                pass[e] = c0 <= c1 && r0 <= r1;
+                if (pass[e]) {
+                    const int ncols = c1 - c0 + 1;
+                    const int lg = ncols <= 1 ? 0 : 32 - __builtin_clz(static_cast<unsigned>(ncols - 1));
+                    const int rpp = kWave >> lg;
+                    npk[e] = static_cast<unsigned>((r1 - r0 + rpp) / rpp);
+                    bits[e] = static_cast<unsigned>(c0) | static_cast<unsigned>(c1) << 6 |
+                              static_cast<unsigned>(r0) << 12 | static_cast<unsigned>(r1) << 17 |
+                              static_cast<unsigned>(lg) << 22;
+                }
+            }
+        }
+        // Compact the survivors block-wide ((slice, wave, lane) order); exclusive packet
+        // prefix in compacted order.
+        unsigned wpos[kSlices], incl[kSlices];
+#pragma unroll
+        for (int e = 0; e < kSlices; ++e) {
+            const unsigned long long m = __ballot(pass[e]);
+            wpos[e] = __popcll(m & lt_mask);
+            incl[e] = npk[e];
+#pragma unroll
+            for (int o = 1; o < kWave; o <<= 1) {
+                const unsigned t = __shfl_up(incl[e], o);
+                if (lane >= o) {
+                    incl[e] += t;
+                }
+            }
+            if (lane == kWave - 1) {
+                k.wave_n[e * W + wave] = __popcll(m);
+                k.wave_pk[e * W + wave] = incl[e];
+            }
+        }
+        __syncthreads();
+        // Bases of (slice e, this wave): the virtual waves (e', w') before it, in order.
+        unsigned n_surv = 0, n_pk = 0;
+        unsigned sbase[kSlices], pbase[kSlices];
+#pragma unroll
+        for (int e = 0; e < kSlices; ++e) {
+            sbase[e] = 0u;
+            pbase[e] = 0u;
+        }
+#pragma unroll
+        for (int vw = 0; vw < kSlices * W; ++vw) {
+            const unsigned wn = k.wave_n[vw], wp = k.wave_pk[vw];
+#pragma unroll
+            for (int e = 0; e < kSlices; ++e) {
+                const bool before = vw < e * W + wave;
+                sbase[e] += before ? wn : 0u;
+                pbase[e] += before ? wp : 0u;
+            }
+            n_surv += wn;
+            n_pk += wp;
+        }
+#pragma unroll
+        for (int e = 0; e < kSlices; ++e) {
+            if (pass[e]) {
+                const unsigned slot = sbase[e] + wpos[e];
+                k.sv0[slot] = cr[e].a;
+                k.sv1[slot] = cr[e].b;
+                k.sv2[slot] = make_float4(cr[e].x.x, cr[e].x.y, cr[e].x.z, __uint_as_float(bits[e]));
+                k.pre[slot] = pbase[e] + incl[e] - npk[e];
+            }
+        }
+        if (tid == 0) {
+            k.pre[n_surv] = n_pk;
+        }
+        __syncthreads();
+#ifdef SRT_DIAG
+        {
+            const unsigned long long now = __builtin_amdgcn_s_memtime();
+            d_gather += now - d_mark;
+            d_mark = now;
+            d_surv += n_surv;
+            d_pk += n_pk;
+            ++d_batches;
+        }
+#endif
+        // Walk this wave's packets [q_begin, q_end), 64 at a time: lane l finds packet q0 + l's
+        // survivor (binary search in pre) and fetches its range bits, then the wave takes the
+        // packets kPacketIlp at a time (independent chains: all LDS reads issued together; a
+        // tail repeats the last packet, harmless under an atomic min) and applies the hits.
+        constexpr int kPacketIlp = 4;
+        unsigned q_begin = wave * n_pk / W, q_end = (wave + 1) * n_pk / W;
+#ifdef SRT_DIAG
+        if (p.exp & 64u) {
+            q_end = q_begin;
+        }
+#endif
+        unsigned long long* keys = &sh.keys[0][0];
+#pragma unroll 1
+        for (unsigned q0 = q_begin; q0 < q_end; q0 += kWave) {
+            const unsigned mine = min(q0 + static_cast<unsigned>(lane), q_end - 1u);
+            int lo = 0, hi = static_cast<int>(n_surv) - 1;  // last survivor with pre <= mine
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (k.pre[mid] <= mine) {
+                    lo = mid;
+                } else {
+                    hi = mid - 1;
+                }
+            }
+            const unsigned my_s = static_cast<unsigned>(lo);
+            const unsigned my_j = mine - k.pre[lo];
+            const unsigned my_bits = __float_as_uint(k.sv2[lo].w);
+            const unsigned n = min(static_cast<unsigned>(kWave), q_end - q0);
+#pragma unroll 1
+            for (unsigned i = 0; i < n; i += kPacketIlp) {
+                unsigned ps[kPacketIlp];
+                PacketPixel px[kPacketIlp];
+                float4 ra[kPacketIlp], rb[kPacketIlp], rx[kPacketIlp];
+                float fx[kPacketIlp], fy[kPacketIlp];
+#pragma unroll
+                for (int u = 0; u < kPacketIlp; ++u) {
+                    const unsigned li = min(i + u, n - 1u);
+                    ps[u] = __builtin_amdgcn_readlane(my_s, li);
+                    px[u] = PacketLane(__builtin_amdgcn_readlane(my_bits, li), __builtin_amdgcn_readlane(my_j, li), lane);
+                }
+#pragma unroll
+                for (int u = 0; u < kPacketIlp; ++u) {
+                    ra[u] = k.sv0[ps[u]];
+                    rb[u] = k.sv1[ps[u]];
+                    rx[u] = k.sv2[ps[u]];
+                    fx[u] = k.fxs[px[u].col];
+                    fy[u] = k.fys[px[u].row];
+                }
+                PacketHit h[kPacketIlp];
+#pragma unroll
+                for (int u = 0; u < kPacketIlp; ++u) {
+                    h[u] = EvalPacket(ra[u], rb[u], rx[u], fx[u], fy[u], px[u]);
+                }
+#pragma unroll
+                for (int u = 0; u < kPacketIlp; ++u) {
+#ifdef SRT_DIAG
+                    if (p.exp & 32u) {
+                        continue;
+                    }
+#endif
+                    if (h[u].hit) {
+                        __hip_atomic_fetch_min(keys + h[u].addr, h[u].key, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
+                }
+            }
+        }
+        __syncthreads();  // batch storage reused; after the last batch: keys complete
+#ifdef SRT_DIAG
+        {
+            const unsigned long long now = __builtin_amdgcn_s_memtime();
+            d_walk += now - d_mark;
+            d_mark = now;
+        }
+#endif
+    }
+#ifdef SRT_DIAG
+    const unsigned blk = blockIdx.y * gridDim.x + blockIdx.x;
+    if (tid == 0 && blk < kDiagBlocks) {
+        unsigned long long* d = g_srt_diag[blk];
+        d[0] = 0;
+        d[1] = d_gather;
+        d[2] = d_walk;
+        d[3] = d_surv;
+        d[4] = d_pk;
+        d[5] = d_batches;
+        d[6] = __builtin_amdgcn_s_memtime() - d_t0;
+        d[7] = 1 | 2 | 4 | 8 | (static_cast<unsigned long long>(src.count1) << 16) |
+               (static_cast<unsigned long long>(src.end - src.count1) << 40);
+    }
+#endif
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const unsigned long long key = sh.keys[wave * R + r][lane];
+        if (key != ~0ull) {
+            s.bt[r] = __uint_as_float(static_cast<unsigned>(key >> 32));
+            s.bi[r] = static_cast<int>(static_cast<unsigned>(key));
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// Cull bins: the first cull level, built per band before the trace. A tile is 64 x 32 rays
+// (one trace block).
+//   TileInfoKernel:     one block per tile reads the tile's sample offsets once: the ray
+//                       box, "regular" (every offset equal to the first, bit for bit) and the
+//                       first offset; it clears the tile's bin count.
+//   BinTrianglesKernel: every block first reduces the tile boxes to per tile-column and per
+//                       tile-row bounds, made monotone (suffix minimum of lo, prefix maximum
+//                       of hi). Then one thread per record: binary searches in them give
+//                       the contiguous range of tile columns and rows whose boxes can overlap
+//                       the record's screen box; every tile of the range whose own box passes
+//                       the screen-box overlap and the edge-function corner test (BoxMayHit)
+//                       gets the id appended to its list. A record whose range spans more than
+//                       kLargeTiles tiles (big, or an unbounded screen box) goes to the large
+//                       list, which every binned tile walks after its own list.
+// Both steps drop only (record, tile) pairs that provably fail the exact test for every ray
+// of the tile, so the frame stays bit-identical to brute force. A tile whose box is outside
+// the screen-box range, or whose list overflowed, streams every record instead.
+// ---------------------------------------------------------------------------------------
 constexpr int kBinThreads = 256;
-constexpr int kBinG = 8;          // records per lane per bin step (4 x 16-B loads)
-constexpr int kBinStep = kBinThreads * kBinG;
-constexpr int kBinMaxSlices = 32;  // bin blocks per super-tile row, striding over the record steps
-constexpr int kBinRowSupers = 64;  // super-tiles per row handled per pass (LDS box cache)
-constexpr unsigned kUnbinned = 0xFFFFFFFFu;
-static_assert(kPadTriangles % kBinStep == 0, "bin steps must tile the records");
+constexpr int kLargeTiles = 16;  // records spanning more tiles go to the large list
+static_assert(kTileRows == kCullTileRows && kWave == kCullTileCols, "render.h tile shape");
 
 struct BinParams {
-    const uint2* __restrict__ qboxes;
     const float2* __restrict__ offsets;
-    uint4* __restrict__ super_q;    // per super-tile: (QBox.x, QBox.y, usable, 0)
-    unsigned* __restrict__ lists;   // per super-tile: capacity ids
-    unsigned* __restrict__ counts;  // per super-tile
-    unsigned long long* __restrict__ tile_keys;  // reset to "no hit" here
-    unsigned* __restrict__ tile_done;            // reset to 0 here
+    const CullRecord* __restrict__ cull;  // cull records in spatial order
+    TileInfo* __restrict__ tile_info;
+    unsigned* __restrict__ counts;      // tiles + 1 (the last one: large list)
+    unsigned* __restrict__ lists;       // tiles x capacity
+    unsigned* __restrict__ large_list;  // n_pad
+    unsigned* __restrict__ tile_order;  // tiles: trace block -> tile (TileOrderKernel)
     unsigned capacity;
-    unsigned n_pad;
-    int supers_x;
+    unsigned n;
+    unsigned exp;  // diagnostic build: experiment bits (env SRT_EXP), 0 in the product
+    int tiles_x;
+    int tiles_y;
     int width;
     int row_count;
     int row_begin;
@@ -1042,273 +1445,376 @@ struct BinParams {
     float hf;
 };
 
-// Level 0 of the cull: one block per super-tile computes its ray box from the sample offsets
-// (GenerateRays' expressions, clamped edges included), stores it quantized for the bin
-// kernel and resets the super-tile's list count (kUnbinned when the box lies outside the
-// screen-box range: its tiles then stream every record).
-__global__ __launch_bounds__(kBinThreads) void SuperBoxKernel(BinParams p) {
+// Order-preserving map float -> unsigned, for LDS atomic min / max (no NaNs reach it).
+__device__ __forceinline__ unsigned OrderedBits(float v) {
+    const unsigned b = __float_as_uint(v);
+    return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+__device__ __forceinline__ float FromOrderedBits(unsigned k) {
+    return __uint_as_float((k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k);
+}
+
+// In-place inclusive scan (max, or min) of a[0..n) by one wave; `reverse` scans from the end.
+template <bool MAX>
+__device__ void WaveScanOrdered(unsigned* a, int n, bool reverse, int lane) {
+    const unsigned ident = MAX ? OrderedBits(-__builtin_inff()) : OrderedBits(__builtin_inff());
+    unsigned carry = ident;
+    for (int c0 = 0; c0 < n; c0 += kWave) {
+        const int i = c0 + lane;
+        const int j = reverse ? n - 1 - i : i;
+        unsigned v = i < n ? a[j] : ident;
+#pragma unroll
+        for (int o = 1; o < kWave; o <<= 1) {
+            const unsigned u = __shfl_up(v, o);
+            if (lane >= o) {
+                v = MAX ? max(v, u) : min(v, u);
+            }
+        }
+        v = MAX ? max(v, carry) : min(v, carry);
+        if (i < n) {
+            a[j] = v;
+        }
+        carry = __shfl(v, kWave - 1);
+    }
+}
+
+__global__ __launch_bounds__(kBinThreads) void TileInfoKernel(BinParams p) {
     constexpr int kWaves = kBinThreads / kWave;
+    constexpr int kPer = kWave * kTileRows / kBinThreads;  // offsets per thread (8)
     __shared__ Box boxes[kWaves];
+    __shared__ unsigned irregular;
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
     const int wave = tid / kWave;
-    const unsigned super = blockIdx.y * gridDim.x + blockIdx.x;
-    const int x0 = blockIdx.x * kSuperTiles * kWave;
+    const int x0 = blockIdx.x * kWave;
     const int y0 = blockIdx.y * kTileRows;
+    if (tid == 0) {
+        irregular = 0u;
+    }
+    // All loads first (clamped addresses: duplicates of real pixels), then the box. Same
+    // expressions as GenerateRays; NaN positions drop out of the box (fminf / fmaxf).
+    const float2 o0 = p.offsets[static_cast<size_t>(y0) * p.width + x0];
+    const int xx = min(x0 + lane, p.width - 1);
+    float2 o[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const int yy = min(y0 + wave + k * kWaves, p.row_count - 1);
+        o[k] = p.offsets[static_cast<size_t>(yy) * p.width + xx];
+    }
     Box box{__builtin_inff(), -__builtin_inff(), __builtin_inff(), -__builtin_inff()};
-    for (int i = tid; i < kSuperTiles * kWave * kTileRows; i += kBinThreads) {
-        const int xc = min(x0 + i % (kSuperTiles * kWave), p.width - 1);
-        const int yc = min(y0 + i / (kSuperTiles * kWave), p.row_count - 1);
-        const float2 o = p.offsets[static_cast<size_t>(yc) * p.width + xc];
-        const float fx = (static_cast<float>(xc) + o.x) / p.wf;
-        const float fy = (static_cast<float>(p.row_begin + yc) + o.y) / p.hf;
+    bool regular = true;
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const int yy = min(y0 + wave + k * kWaves, p.row_count - 1);
+        const float fx = (static_cast<float>(xx) + o[k].x) / p.wf;
+        const float fy = (static_cast<float>(p.row_begin + yy) + o[k].y) / p.hf;
         box = Box{fminf(box.xlo, fx), fmaxf(box.xhi, fx), fminf(box.ylo, fy), fmaxf(box.yhi, fy)};
+        regular = regular && __float_as_uint(o[k].x) == __float_as_uint(o0.x) &&
+                  __float_as_uint(o[k].y) == __float_as_uint(o0.y);
     }
     box = WaveReduceBox(box);
+    const bool wave_regular = __all(regular);
+    __syncthreads();  // `irregular` initialised
     if (lane == 0) {
         boxes[wave] = box;
+        if (!wave_regular) {
+            irregular = 1u;
+        }
     }
     __syncthreads();
     if (tid == 0) {
         box = boxes[0];
 #pragma unroll
         for (int w = 1; w < kWaves; ++w) {
-            const Box o = boxes[w];
-            box = Box{fminf(box.xlo, o.xlo), fmaxf(box.xhi, o.xhi), fminf(box.ylo, o.ylo), fmaxf(box.yhi, o.yhi)};
+            const Box b = boxes[w];
+            box = Box{fminf(box.xlo, b.xlo), fmaxf(box.xhi, b.xhi), fminf(box.ylo, b.ylo), fmaxf(box.yhi, b.yhi)};
         }
-        const bool usable = ScreenBoxUsable(box);
-        const QBox q = Quantize(box);
-        p.super_q[super] = make_uint4(q.x, q.y, usable ? 1u : 0u, 0u);
-        p.counts[super] = usable ? 0u : kUnbinned;
-    }
-    // Split-tile state of the super-tile's pixels and tiles for this frame.
-    const int tiles_x = (p.width + kWave - 1) / kWave;
-    if (tid < kSuperTiles) {
-        const int tx = blockIdx.x * kSuperTiles + tid;
-        if (tx < tiles_x) {
-            p.tile_done[blockIdx.y * tiles_x + tx] = 0u;
-        }
-    }
-    for (int i = tid; i < kSuperTiles * kWave * kTileRows; i += kBinThreads) {
-        const int xx = x0 + i % (kSuperTiles * kWave);
-        const int yy = y0 + i / (kSuperTiles * kWave);
-        if (xx < p.width && yy < p.row_count) {
-            p.tile_keys[static_cast<size_t>(yy) * p.width + xx] = ~0ull;
+        TileInfo ti;
+        ti.box = make_float4(box.xlo, box.xhi, box.ylo, box.yhi);
+        ti.ox = o0.x;
+        ti.oy = o0.y;
+        ti.regular = irregular == 0u ? 1u : 0u;
+        ti.usable = ScreenBoxUsable(box) ? 1u : 0u;
+        const unsigned tile = blockIdx.y * p.tiles_x + blockIdx.x;
+        p.tile_info[tile] = ti;
+        p.counts[tile] = 0u;  // the bin kernel runs after this one (stream order)
+        if (tile == 0) {
+            p.counts[p.tiles_x * p.tiles_y] = 0u;  // large list
         }
     }
 }
 
-// Level 1 of the cull (bin kernel): block (super-tile row, slice) streams the quantized
-// screen boxes of its share of the records once and tests each against the row's box (the
-// union of its super-tiles' boxes); each record that passes (a few percent) is then tested
-// against every super-tile of the row at once, lane j taking super-tile j. Survivors are
-// collected as (super-tile, id) pairs in wave-private LDS regions and flushed to the global
-// lists with one atomic per super-tile per flush. Every record is still tested against
-// every super-tile. A list that overflows its capacity makes the trace kernel stream every
-// record for that super-tile instead.
-constexpr int kBinWaves = kBinThreads / kWave;
-constexpr int kBinWavePairs = 1024;                      // LDS pairs per wave region
-constexpr int kBinPairCap = kBinWaves * kBinWavePairs;   // 4096
-static_assert(kBinRowSupers <= kWave, "one super-tile per lane");
-__global__ __launch_bounds__(kBinThreads) void BinKernel(BinParams p) {
-    __shared__ unsigned pair_super[kBinPairCap];
-    __shared__ unsigned pair_id[kBinPairCap];
-    __shared__ unsigned wave_count[kBinWaves];
-    __shared__ unsigned hist[kBinRowSupers];
-    __shared__ unsigned gbase[kBinRowSupers];
+// First index i of the nondecreasing hi'[0..n) with hi'[i] >= v (n if none).
+__device__ __forceinline__ int FirstHiAtLeast(const float2* b, int n, float v) {
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (b[mid].y >= v) {
+            hi = mid;
+        } else {
+            lo = mid + 1;
+        }
+    }
+    return lo;
+}
+// Last index i of the nondecreasing lo'[0..n) with lo'[i] <= v (-1 if none).
+__device__ __forceinline__ int LastLoAtMost(const float2* b, int n, float v) {
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (b[mid].x > v) {
+            hi = mid;
+        } else {
+            lo = mid + 1;
+        }
+    }
+    return lo - 1;
+}
+
+// One thread per record, records taken in the scene's spatial order (p.order: sorted by the
+// screen position of their centroid at scene load), so a block's records fall in few tiles:
+// the block counts its (tile, record) pairs in an LDS histogram, reserves each touched
+// tile's share of its list with ONE global atomic, then writes the ids. (Per-pair global
+// atomics serialise on the busy tiles' counters at the memory side.)
+static_assert(2 * kMaxBoundTiles <= kMaxBinTiles, "bounds scratch lives in the histogram");
+__global__ __launch_bounds__(kBinThreads) void BinTrianglesKernel(BinParams p) {
+    __shared__ float2 b[kMaxBoundTiles];
+    __shared__ unsigned hist[kMaxBinTiles];  // prologue: ordered-bit bounds scratch
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
     const int wave = tid / kWave;
-    const unsigned row = blockIdx.x;
-    const unsigned long long lt_mask = (1ull << lane) - 1ull;
-    const unsigned nsteps = p.n_pad / kBinStep;
-    const uint4* __restrict__ q4 = reinterpret_cast<const uint4*>(p.qboxes);
-    constexpr int L = kBinG / 2;
-    unsigned* my_super = pair_super + wave * kBinWavePairs;
-    unsigned* my_id = pair_id + wave * kBinWavePairs;
+    const int nx = p.tiles_x, ny = p.tiles_y;
+    const int tiles = nx * ny;
 
-    // Flush every wave's pairs: histogram per super-tile (LDS atomics give each pair its
-    // rank), one global atomic per super-tile reserves list space, then scatter.
-    auto flush = [&](int j0, int nj, unsigned mine) {
-        if (lane == 0) {
-            wave_count[wave] = mine;
+    // Prologue: monotone tile-column and tile-row bounds of the usable tiles' boxes
+    // (lo' = suffix minimum, hi' = prefix maximum; both nondecreasing).
+    unsigned* col_lo = hist;
+    unsigned* col_hi = hist + nx;
+    unsigned* row_lo = hist + 2 * nx;
+    unsigned* row_hi = hist + 2 * nx + ny;
+    for (int i = tid; i < nx + ny; i += kBinThreads) {
+        const bool col = i < nx;
+        const int j = col ? i : i - nx;
+        (col ? col_lo : row_lo)[j] = OrderedBits(__builtin_inff());
+        (col ? col_hi : row_hi)[j] = OrderedBits(-__builtin_inff());
+    }
+    __syncthreads();
+    for (int t = tid; t < tiles; t += kBinThreads) {
+        const TileInfo ti = p.tile_info[t];
+        if (ti.usable != 0u && ti.box.x <= ti.box.y && ti.box.z <= ti.box.w) {
+            const int c = t % nx, r = t / nx;
+            atomicMin(&col_lo[c], OrderedBits(ti.box.x));
+            atomicMax(&col_hi[c], OrderedBits(ti.box.y));
+            atomicMin(&row_lo[r], OrderedBits(ti.box.z));
+            atomicMax(&row_hi[r], OrderedBits(ti.box.w));
         }
-        if (tid < nj) {
-            hist[tid] = 0u;
-        }
-        __syncthreads();
-        unsigned rank[kBinPairCap / kBinThreads];
-#pragma unroll
-        for (int i = 0; i < kBinPairCap / kBinThreads; ++i) {
-            const unsigned e = i * kBinThreads + tid;
-            const bool valid = e % kBinWavePairs < wave_count[e / kBinWavePairs];
-            rank[i] = valid ? atomicAdd(&hist[pair_super[e]], 1u) : 0u;
-        }
-        __syncthreads();
-        if (tid < nj && hist[tid] != 0u) {
-            gbase[tid] = atomicAdd(&p.counts[row * p.supers_x + j0 + tid], hist[tid]);
-        }
-        __syncthreads();
-#pragma unroll
-        for (int i = 0; i < kBinPairCap / kBinThreads; ++i) {
-            const unsigned e = i * kBinThreads + tid;
-            if (e % kBinWavePairs < wave_count[e / kBinWavePairs]) {
-                const unsigned j = pair_super[e];
-                const unsigned at = gbase[j] + rank[i];
-                if (at < p.capacity) {
-                    p.lists[static_cast<size_t>(row * p.supers_x + j0 + j) * p.capacity + at] = pair_id[e];
-                }
-            }
-        }
-        __syncthreads();  // pair regions reused
-    };
+    }
+    __syncthreads();
+    if (wave == 0) {
+        WaveScanOrdered<false>(col_lo, nx, true, lane);
+    } else if (wave == 1) {
+        WaveScanOrdered<true>(col_hi, nx, false, lane);
+    } else if (wave == 2) {
+        WaveScanOrdered<false>(row_lo, ny, true, lane);
+    } else {
+        WaveScanOrdered<true>(row_hi, ny, false, lane);
+    }
+    __syncthreads();
+    for (int i = tid; i < nx + ny; i += kBinThreads) {
+        const bool col = i < nx;
+        const int j = col ? i : i - nx;
+        b[i] = make_float2(FromOrderedBits(col ? col_lo[j] : row_lo[j]), FromOrderedBits(col ? col_hi[j] : row_hi[j]));
+    }
+    __syncthreads();
+    for (int t = tid; t < tiles; t += kBinThreads) {
+        hist[t] = 0u;
+    }
 
-    for (int j0 = 0; j0 < p.supers_x; j0 += kBinRowSupers) {
-        const int nj = min(kBinRowSupers, p.supers_x - j0);
-        // Lane j < nj holds super-tile j's packed box (usable flag in .z).
-        uint4 my_q = make_uint4(0x80008000u, 0x80008000u, 0u, 0u);
-        if (lane < nj) {
-            my_q = p.super_q[row * p.supers_x + j0 + lane];
-        }
-        const bool my_usable = my_q.z != 0u;
-        const QBox my_box{my_q.x, my_q.y};
-        // Row box: union of the usable super-tile boxes (in the packed (-lo, hi) form the
-        // union is the per-half maximum).
-        I16x2 ux = __builtin_bit_cast(I16x2, my_usable ? my_q.x : 0x80008000u);
-        I16x2 uy = __builtin_bit_cast(I16x2, my_usable ? my_q.y : 0x80008000u);
-#pragma unroll
-        for (int o = 1; o < kWave; o <<= 1) {
-            ux = __builtin_elementwise_max(ux, __builtin_bit_cast(I16x2, __shfl_xor(__builtin_bit_cast(unsigned, ux), o)));
-            uy = __builtin_elementwise_max(uy, __builtin_bit_cast(I16x2, __shfl_xor(__builtin_bit_cast(unsigned, uy), o)));
-        }
-        if (__ballot(my_usable) == 0ull) {
-            continue;  // no usable super-tile in this part of the row
-        }
-        const QBox rq{__builtin_bit_cast(unsigned, ux), __builtin_bit_cast(unsigned, uy)};
-        unsigned mine = 0;  // pairs in this wave's region (wave-uniform)
-        for (unsigned k0 = blockIdx.y; k0 < nsteps; k0 += gridDim.y) {
-            uint4 q[L];
-#pragma unroll
-            for (int l = 0; l < L; ++l) {
-                q[l] = q4[k0 * (kBinStep / 2) + l * kBinThreads + tid];
-            }
-#pragma unroll
-            for (int g = 0; g < kBinG; ++g) {
-                const unsigned qx = (g & 1) ? q[g >> 1].z : q[g >> 1].x;
-                const unsigned qy = (g & 1) ? q[g >> 1].w : q[g >> 1].y;
-                unsigned long long m = __ballot(QBoxOverlaps(rq, qx, qy));
-                // Each record of the row: every super-tile at once (lane j: super-tile j).
-                while (m != 0ull) {
-                    const int src = __builtin_ctzll(m);
-                    m &= m - 1ull;
-                    const unsigned rx = __builtin_amdgcn_readlane(qx, src);
-                    const unsigned ry = __builtin_amdgcn_readlane(qy, src);
-                    const bool hit = my_usable && QBoxOverlaps(my_box, rx, ry);
-                    const unsigned long long hm = __ballot(hit);
-                    if (hit) {
-                        const unsigned at = mine + __popcll(hm & lt_mask);
-                        my_super[at] = static_cast<unsigned>(lane);
-                        my_id[at] = k0 * kBinStep + 2 * ((g >> 1) * kBinThreads + (wave * kWave + src)) + (g & 1);
-                    }
-                    mine += __popcll(hm);
-                    if (mine + kWave > kBinWavePairs) {
-                        // Region full: this wave's pairs go straight to the global lists.
-                        unsigned gb = 0;
-                        for (unsigned e = lane; e < mine; e += kWave) {
-                            const unsigned j = my_super[e];
-                            const unsigned at = atomicAdd(&p.counts[row * p.supers_x + j0 + j], 1u);
-                            if (at < p.capacity) {
-                                p.lists[static_cast<size_t>(row * p.supers_x + j0 + j) * p.capacity + at] = my_id[e];
-                            }
+    // This thread's record: its tile range and the tiles of it that pass (bit k = tile
+    // (r0 + k / w, c0 + k % w) of the range, at most kLargeTiles of them).
+    const unsigned i = blockIdx.x * kBinThreads + tid;  // spatial-order position (list entry)
+    unsigned mask = 0u;
+    int c0 = 0, r0 = 0, w = 1;
+    if (i < p.n) {
+        const CullRecord cr = p.cull[i];
+        const float4 sb = cr.sb;
+        if (sb.x <= sb.y && sb.z <= sb.w && (p.exp & 1u) == 0u) {  // else disabled: empty box
+            // Any tile (c, r) whose box overlaps sb has hi'[c] >= hi[c] >= sb.xlo and
+            // lo'[c] <= lo[c] <= sb.xhi, so c lies in [c0, c1]; rows likewise.
+            c0 = FirstHiAtLeast(b, nx, sb.x);
+            const int c1 = LastLoAtMost(b, nx, sb.y);
+            r0 = FirstHiAtLeast(b + nx, ny, sb.z);
+            const int r1 = LastLoAtMost(b + nx, ny, sb.w);
+            w = c1 - c0 + 1;
+            const int h = r1 - r0 + 1;
+            if (w > 0 && h > 0 && (p.exp & 2u) == 0u) {
+                if (w * h > kLargeTiles) {
+                    p.large_list[atomicAdd(&p.counts[tiles], 1u)] = i;
+                } else {
+                    const Record rec{cr.a.x, cr.a.y, cr.a.z, cr.a.w, cr.b.x, cr.b.y, cr.b.z, cr.b.w, cr.x.x};
+                    for (int k = 0; k < w * h; ++k) {
+                        const TileInfo ti = p.tile_info[(r0 + k / w) * nx + c0 + k % w];
+                        const Box tb{ti.box.x, ti.box.y, ti.box.z, ti.box.w};
+                        if (ti.usable != 0u && ScreenBoxOverlaps(tb, sb) && BoxMayHit(tb, rec)) {
+                            mask |= 1u << k;
                         }
-                        (void)gb;
-                        mine = 0;
                     }
                 }
             }
-            // Flush once some region is half full (block-uniform decision via LDS).
-            if (lane == 0) {
-                wave_count[wave] = mine;
-            }
-            __syncthreads();
-            unsigned most = 0;
-#pragma unroll
-            for (int w = 0; w < kBinWaves; ++w) {
-                most = max(most, wave_count[w]);
-            }
-            __syncthreads();
-            if (most > kBinWavePairs / 2) {
-                flush(j0, nj, mine);
-                mine = 0;
-            }
         }
-        flush(j0, nj, mine);
+    }
+    __syncthreads();  // histogram zeroed
+    for (unsigned m = mask; m != 0u; m &= m - 1u) {
+        const int k = __builtin_ctz(m);
+        atomicAdd(&hist[(r0 + k / w) * nx + c0 + k % w], 1u);
+    }
+    __syncthreads();
+    for (int t = tid; t < tiles; t += kBinThreads) {
+        const unsigned h = hist[t];
+        if (h != 0u) {
+            hist[t] = (p.exp & 4u) ? 0u : atomicAdd(&p.counts[t], h);  // this block's base in the list
+        }
+    }
+    __syncthreads();
+    for (unsigned m = mask; m != 0u; m &= m - 1u) {
+        const int k = __builtin_ctz(m);
+        const unsigned t = static_cast<unsigned>((r0 + k / w) * nx + c0 + k % w);
+        const unsigned at = atomicAdd(&hist[t], 1u);
+        if (at < p.capacity) {
+            p.lists[static_cast<size_t>(t) * p.capacity + at] = i;
+        }
     }
 }
 
-// How the blocks of one tile split its candidates: block z of chunks (blocks z >= chunks
-// return at once). LIST: chunks of >= p.chunk_ids list ids (16-B aligned); FULL (a tile whose
-// bin list overflowed, or no usable box): kMaxChunks slices of the record steps; without
-// bins: one block.
-constexpr unsigned kMaxChunks = 8;
-struct CullPlan {
-    CullSource src;
-    unsigned chunks;
-    bool list;
-};
-__device__ __forceinline__ CullPlan PlanTile(const TraceParams& p) {
-    CullPlan plan{CullSource{nullptr, 0u, 0u, p.n_pad / kStreamStep}, 1u, false};
-    if (p.bin_counts == nullptr) {
-        return plan;
+// Longest-processing-time-first launch order of the trace blocks: tiles sorted by their work,
+// descending (FULL-stream tiles first, then by the log2 of their candidate count), so the
+// heavy tiles start first and the light ones fill in behind them. One block; a counting sort
+// over 64 buckets (order within a bucket arbitrary: the frame does not depend on it).
+constexpr int kOrderThreads = 1024;
+__device__ __forceinline__ unsigned TileWorkBucket(const BinParams& p, unsigned t, unsigned large) {
+    const unsigned cnt = p.counts[t];
+    if (p.tile_info[t].usable == 0u || cnt > p.capacity) {
+        return 63u;
     }
-    const unsigned super = blockIdx.y * ((gridDim.x + kSuperTiles - 1) / kSuperTiles) + blockIdx.x / kSuperTiles;
-    const unsigned cnt = p.bin_counts[super];
-    const unsigned z = blockIdx.z;
-    if (cnt <= p.bin_capacity) {
-        plan.list = true;
-        plan.chunks = min(kMaxChunks, max(1u, (cnt + p.chunk_ids - 1) / p.chunk_ids));
-        const unsigned per = ((cnt + plan.chunks - 1) / plan.chunks + 3u) & ~3u;
-        const unsigned first = min(cnt, z * per);
-        plan.src.list = p.bin_lists + static_cast<size_t>(super) * p.bin_capacity + first;
-        plan.src.count = min(per, cnt - first);
-    } else {
-        const unsigned total = p.n_pad / kStreamStep;
-        plan.chunks = min(kMaxChunks, total);
-        const unsigned a = z * total / plan.chunks, b = (z + 1) * total / plan.chunks;
-        plan.src.step0 = a;
-        plan.src.steps = z < plan.chunks ? b - a : 0u;
+    const unsigned total = cnt + large;
+    return total == 0u ? 0u : 32u - __builtin_clz(total);
+}
+__global__ __launch_bounds__(kOrderThreads) void TileOrderKernel(BinParams p) {
+    __shared__ unsigned start[64];
+    const int tid = threadIdx.x;
+    const unsigned tiles = static_cast<unsigned>(p.tiles_x * p.tiles_y);
+    const unsigned large = p.counts[tiles];
+    if (tid < 64) {
+        start[tid] = 0u;
     }
-    return plan;
+    __syncthreads();
+    for (unsigned t = tid; t < tiles; t += kOrderThreads) {
+        atomicAdd(&start[TileWorkBucket(p, t, large)], static_cast<unsigned>(kParts));
+    }
+    __syncthreads();
+    unsigned first = 0u;  // tiles in heavier buckets
+    if (tid < 64) {
+        for (int b = 63; b > tid; --b) {
+            first += start[b];
+        }
+    }
+    __syncthreads();
+    if (tid < 64) {
+        start[tid] = first;
+    }
+    __syncthreads();
+    for (unsigned t = tid; t < tiles; t += kOrderThreads) {
+        const unsigned at = atomicAdd(&start[TileWorkBucket(p, t, large)], static_cast<unsigned>(kParts));
+        for (int part = 0; part < kParts; ++part) {
+            p.tile_order[at + part] = t * kParts + part;  // trace work items (tile, part)
+        }
+    }
+}
+
+// Candidate source of a tile: LIST (binned, usable box, list complete): the tile's list then
+// the large list; FULL (no bins, an unusable tile box, or an overflowed list): every record.
+__device__ __forceinline__ CullSource TileSource(const TraceParams& p, const TileInfo& ti, unsigned tile) {
+    CullSource src{nullptr, nullptr, 0u, 0u, 0u, 0u, p.n_pad / kStreamStep};
+    if (p.tile_info == nullptr) {
+        return src;
+    }
+    const unsigned cnt = p.bin_counts[tile];
+    if (ti.usable != 0u && cnt <= p.bin_capacity) {
+        src.list = p.bin_lists + static_cast<size_t>(tile) * p.bin_capacity;
+        src.list2 = p.large_list;
+        src.count1 = cnt;
+        src.end = cnt + p.bin_counts[gridDim.x * gridDim.y / kParts];
+    }
+    return src;
+}
+
+// Rays of a regular tile (every offset equal to (ox, oy), bit for bit): GenerateRays'
+// expressions without reading the offsets.
+template <int R>
+__device__ __forceinline__ void UniformRays(const TraceParams& p, int x, int y0, float ox, float oy, Rays<R>& s,
+                                            Box& box) {
+    const int xc = min(x, p.width - 1);
+    const float fx = (static_cast<float>(xc) + ox) / p.wf;
+    box = Box{__builtin_inff(), -__builtin_inff(), __builtin_inff(), -__builtin_inff()};
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int yc = min(y0 + r, p.row_count - 1);
+        s.fx[r] = fx;
+        s.fy[r] = (static_cast<float>(p.row_begin + yc) + oy) / p.hf;
+        s.bt[r] = __builtin_inff();
+        s.bi[r] = -1;
+        box.xlo = fminf(box.xlo, s.fx[r]);
+        box.xhi = fmaxf(box.xhi, s.fx[r]);
+        box.ylo = fminf(box.ylo, s.fy[r]);
+        box.yhi = fmaxf(box.yhi, s.fy[r]);
+    }
 }
 
 template <int W>
-__global__ __launch_bounds__(kWave * W, (48 / W > 8 ? 8 : 48 / W)) void TraceCullKernel(TraceParams p) {
+__global__ __launch_bounds__(kWave * W, 4) void TraceCullKernel(TraceParams p) {
     using S = CullShape<W>;
     constexpr int R = S::kR;
     __shared__ CullShared<W> sh;
-    if (p.bin_counts != nullptr) {
-        const CullPlan early = PlanTile(p);
-        if (blockIdx.z >= early.chunks) {
-            return;  // this tile needs fewer blocks
-        }
+    // Block = one part (kBlockRows rows) of a cull tile (kTileRows rows); launched in the
+    // tile order's work order when the frame is binned.
+    const unsigned linear = blockIdx.y * gridDim.x + blockIdx.x;
+    const unsigned item = p.tile_order != nullptr ? p.tile_order[linear] : linear;
+    const unsigned tile = item / kParts;
+    const int tx = static_cast<int>(tile % gridDim.x), ty = static_cast<int>(tile / gridDim.x);
+    const int row0 = ty * kTileRows + static_cast<int>(item % kParts) * kBlockRows;  // band row of the block
+    if (row0 >= p.row_count) {
+        return;  // the last tile row's empty part
     }
+    const bool binned = p.tile_info != nullptr;
+    TileInfo ti{};
+    if (binned) {
+        ti = p.tile_info[tile];
+    }
+    const CullSource src = TileSource(p, ti, tile);
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
     const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);
-    const int x = blockIdx.x * kWave + lane;
-    const int y0 = (blockIdx.y * W + wave) * R;
+    const int x = tx * kWave + lane;
+    const int y0 = row0 + wave * R;
     Rays<R> s;
     Box lane_box;
-    const bool same = GenerateRays<R>(p, x, y0, s, lane_box);
+    bool same = true;
+    if (binned && ti.regular != 0u) {
+        UniformRays<R>(p, x, y0, ti.ox, ti.oy, s, lane_box);
+    } else {
+        same = GenerateRays<R>(p, x, y0, s, lane_box);
+    }
     const Box wb = WaveReduceBox(lane_box);
-    // Raster walk eligibility: every ray of the tile has the tile's first sample offset
-    // (bit pattern), so fx depends on the column only and fy on the row only.
+    // Raster walk eligibility: every ray of the block has the tile's first sample offset (bit
+    // pattern), so fx depends on the column only and fy on the row only.
     bool regular = true;
     float oy0;
-    {
-        const int x0 = min(static_cast<int>(blockIdx.x) * kWave, p.width - 1);
-        const int yb = min(static_cast<int>(blockIdx.y) * kTileRows, p.row_count - 1);
-        const float2 o0 = p.offsets[static_cast<size_t>(yb) * p.width + x0];
+    if (binned) {
+        regular = ti.regular != 0u;
+        oy0 = ti.oy;
+    } else {
+        const int x0 = min(tx * kWave, p.width - 1);
+        const float2 o0 = p.offsets[static_cast<size_t>(row0) * p.width + x0];
         oy0 = o0.y;
         const int xc = min(x, p.width - 1);
 #pragma unroll
@@ -1334,88 +1840,52 @@ __global__ __launch_bounds__(kWave * W, (48 / W > 8 ? 8 : 48 / W)) void TraceCul
         sh.regular = 0u;
     }
     __syncthreads();
-    Box bb = sh.wave_box[0];
+    Box bb = sh.wave_box[0];  // the block's ray box
 #pragma unroll
     for (int w = 1; w < W; ++w) {
         const Box o = sh.wave_box[w];
         bb = Box{fminf(bb.xlo, o.xlo), fmaxf(bb.xhi, o.xhi), fminf(bb.ylo, o.ylo), fmaxf(bb.yhi, o.yhi)};
     }
-    // Candidate source: the super-tile's bin list when it is complete, else every record;
-    // split into `chunks` pieces taken by blocks z = 0 .. chunks-1 of this tile.
-    const CullPlan plan = PlanTile(p);
-    const CullSource& src = plan.src;
-    const bool list = plan.list;
-    // Raster walk: lane = column (fx), lanes 0..31 carry the tile's 32 rows' fy (the
+    const bool list = src.list != nullptr;
+    const bool raster = sh.regular != 0u && p.allow_raster != 0;
+    const bool shared_fx = sh.shared_fx != 0u;
+    // Raster walks: lane = column (fx), lanes 0..kBlockRows-1 carry the block's rows' fy (the
     // GenerateRays expression; bit-identical since every ray has the same offset).
     const float fx_lane = s.fx[0];
     float fy_lane = __builtin_nanf("");
-    if (lane < kTileRows) {
-        const int yc = min(static_cast<int>(blockIdx.y) * kTileRows + lane, p.row_count - 1);
+    if (lane < kBlockRows) {
+        const int yc = min(row0 + lane, p.row_count - 1);
         fy_lane = (static_cast<float>(p.row_begin + yc) + oy0) / p.hf;
     }
-    if (sh.regular != 0u && p.allow_raster != 0) {
+    if (raster) {
         if (list) {
-            CullWalk<W, true, true, true>(p, sh, s, bb, wb, fx_lane, fy_lane, src);
+            PacketWalk<W>(p, sh, s, bb, fx_lane, fy_lane, src, tx, row0);
         } else {
-            CullWalk<W, true, true, false>(p, sh, s, bb, wb, fx_lane, fy_lane, src);
+            CullWalk<W, true, true, false>(p, sh, s, bb, wb, fx_lane, fy_lane, src, tile);
         }
-    } else if (sh.shared_fx != 0u) {
+    } else if (shared_fx) {
         if (list) {
-            CullWalk<W, true, false, true>(p, sh, s, bb, wb, fx_lane, fy_lane, src);
+            CullWalk<W, true, false, true>(p, sh, s, bb, wb, fx_lane, fy_lane, src, tile);
         } else {
-            CullWalk<W, true, false, false>(p, sh, s, bb, wb, fx_lane, fy_lane, src);
+            CullWalk<W, true, false, false>(p, sh, s, bb, wb, fx_lane, fy_lane, src, tile);
         }
     } else {
         if (list) {
-            CullWalk<W, false, false, true>(p, sh, s, bb, wb, fx_lane, fy_lane, src);
+            CullWalk<W, false, false, true>(p, sh, s, bb, wb, fx_lane, fy_lane, src, tile);
         } else {
-            CullWalk<W, false, false, false>(p, sh, s, bb, wb, fx_lane, fy_lane, src);
-        }
-    }
-    if (plan.chunks > 1) {
-        // Several blocks share this tile: merge this block's hits into the tile's global
-        // keys (atomic min = the same lexicographic (t, id) rule), and the last block to
-        // finish (agent-scope release/acquire around a per-tile counter) shades the tile.
-        const int xc = min(x, p.width - 1);
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const int yc = min(y0 + r, p.row_count - 1);
-            if (s.bi[r] >= 0) {
-                atomicMin(&p.tile_keys[static_cast<size_t>(yc) * p.width + xc], HitKey(s.bt[r], s.bi[r]));
-            }
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (tid == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            const unsigned done = atomicAdd(&p.tile_done[blockIdx.y * gridDim.x + blockIdx.x], 1u);
-            sh.shared_fx = done + 1u == plan.chunks ? 1u : 0u;  // reused as the "last block" flag
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        __syncthreads();
-        if (sh.shared_fx == 0u) {
-            return;
-        }
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const int yc = min(y0 + r, p.row_count - 1);
-            const unsigned long long key = __hip_atomic_load(&p.tile_keys[static_cast<size_t>(yc) * p.width + xc],
-                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            s.bt[r] = key == ~0ull ? __builtin_inff() : __uint_as_float(static_cast<unsigned>(key >> 32));
-            s.bi[r] = key == ~0ull ? -1 : static_cast<int>(static_cast<unsigned>(key));
+            CullWalk<W, false, false, false>(p, sh, s, bb, wb, fx_lane, fy_lane, src, tile);
         }
     }
     ShadeAndStore<R>(p, x, y0, s);
 }
 
-// Waves per cull tile; env SRT_CULL_WAVES = 4, 8 or 16 (default 8), for measurement.
+// Waves per trace block; env SRT_CULL_WAVES = 4, 8 or 16 (default 4), for measurement.
 int CullWavesFromEnv() {
     const char* v = std::getenv("SRT_CULL_WAVES");
-    if (v != nullptr && (std::strcmp(v, "4") == 0 || std::strcmp(v, "16") == 0)) {
+    if (v != nullptr && (std::strcmp(v, "8") == 0 || std::strcmp(v, "16") == 0)) {
         return std::atoi(v);
     }
-    return 8;
+    return 4;
 }
 
 }  // namespace
@@ -1426,13 +1896,15 @@ hipError_t DiagRead(void* host, std::size_t bytes) {
 }
 #endif
 
-hipError_t LaunchPrepare(const float* d_vertices, std::uint64_t n, const Frame& frame, float* d_edges,
-                         hipStream_t stream) {
+hipError_t LaunchPrepare(const float* d_vertices, const unsigned* d_rank, std::uint64_t n, const Frame& frame,
+                         float* d_edges, hipStream_t stream) {
     PrepareParams p{};
     p.vertices = d_vertices;
+    p.rank = d_rank;
     p.edges = reinterpret_cast<float4*>(d_edges);
     p.screen_boxes = reinterpret_cast<float4*>(d_edges) + PaddedTriangleCount(n) / kTileTriangles * kTileFloat4;
     p.qboxes = reinterpret_cast<uint2*>(p.screen_boxes + PaddedTriangleCount(n));
+    p.cull = reinterpret_cast<CullRecord*>(p.qboxes + PaddedTriangleCount(n));
     p.n = static_cast<unsigned>(n);
     p.n_pad = static_cast<unsigned>(PaddedTriangleCount(n));
     for (int k = 0; k < 3; ++k) {
@@ -1450,15 +1922,14 @@ std::size_t CullTiles(std::size_t width, std::size_t row_count) {
     return (width + kWave - 1) / kWave * ((row_count + kTileRows - 1) / kTileRows);
 }
 
-std::size_t CullSuperTiles(std::size_t width, std::size_t row_count) {
-    const std::size_t gx = (width + kWave - 1) / kWave;
-    const std::size_t gy = (row_count + kTileRows - 1) / kTileRows;
-    return (gx + kSuperTiles - 1) / kSuperTiles * gy;
+bool CullBinnable(std::size_t width, std::size_t row_count) {
+    const std::size_t tx = (width + kWave - 1) / kWave, ty = (row_count + kTileRows - 1) / kTileRows;
+    return tx + ty <= kMaxBoundTiles && tx * ty <= kMaxBinTiles;
 }
 
-unsigned CullBinCapacity(std::uint64_t n, std::size_t supers) {
+unsigned CullBinCapacity(std::uint64_t n, std::size_t tiles) {
     const std::uint64_t n_pad = PaddedTriangleCount(n);
-    std::uint64_t cap = supers == 0 ? n_pad : 64 * n_pad / supers;
+    std::uint64_t cap = tiles == 0 ? n_pad : 64 * n_pad / tiles;
     cap = cap < 4096 ? 4096 : cap;
     cap = cap > n_pad ? n_pad : cap;
     if (const char* v = std::getenv("SRT_CULL_BIN_CAP")) {  // tests: force list overflow
@@ -1468,6 +1939,47 @@ unsigned CullBinCapacity(std::uint64_t n, std::size_t supers) {
         }
     }
     return static_cast<unsigned>((cap + 3) / 4 * 4);
+}
+
+namespace {
+struct BinSizes {
+    std::size_t info, counts, lists, large, order;
+};
+BinSizes CullBinSizes(std::uint64_t n, std::size_t width, std::size_t row_count) {
+    const std::size_t tx = (width + kWave - 1) / kWave, ty = (row_count + kTileRows - 1) / kTileRows;
+    const std::size_t tiles = tx * ty;
+    const auto al = [](std::size_t b) { return (b + 255) / 256 * 256; };
+    BinSizes z;
+    z.info = al(tiles * sizeof(TileInfo));
+    z.counts = al((tiles + 1) * 4);
+    z.lists = al(tiles * static_cast<std::size_t>(CullBinCapacity(n, tiles)) * 4);
+    z.large = al(PaddedTriangleCount(n) * 4);
+    z.order = al(tiles * kParts * 4);
+    return z;
+}
+}  // namespace
+
+std::size_t CullBinBytes(std::uint64_t n, std::size_t width, std::size_t row_count) {
+    const BinSizes z = CullBinSizes(n, width, row_count);
+    return z.info + z.counts + z.lists + z.large + z.order;
+}
+
+CullBins CullBinLayout(void* base, std::uint64_t n, std::size_t width, std::size_t row_count) {
+    const BinSizes z = CullBinSizes(n, width, row_count);
+    unsigned char* w = static_cast<unsigned char*>(base);
+    CullBins b{};
+    b.tile_info = w;
+    w += z.info;
+    b.counts = reinterpret_cast<unsigned*>(w);
+    w += z.counts;
+    b.lists = reinterpret_cast<unsigned*>(w);
+    w += z.lists;
+    b.large_list = reinterpret_cast<unsigned*>(w);
+    w += z.large;
+    b.tile_order = reinterpret_cast<unsigned*>(w);
+    b.tiles = CullTiles(width, row_count);
+    b.capacity = CullBinCapacity(n, b.tiles);
+    return b;
 }
 
 hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_vertices, const float* d_albedo,
@@ -1480,6 +1992,7 @@ hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_ver
     p.edges = reinterpret_cast<const float4*>(d_edges);
     p.screen_boxes = reinterpret_cast<const float4*>(d_edges) + PaddedTriangleCount(n) / kTileTriangles * kTileFloat4;
     p.qboxes = reinterpret_cast<const uint2*>(p.screen_boxes + PaddedTriangleCount(n));
+    p.cull = reinterpret_cast<const CullRecord*>(p.qboxes + PaddedTriangleCount(n));
     p.vertices = d_vertices;
     p.albedo = d_albedo;
     p.offsets = reinterpret_cast<const float2*>(band.offsets);
@@ -1492,9 +2005,6 @@ hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_ver
     {
         const char* r = std::getenv("SRT_CULL_RASTER");
         p.allow_raster = (r != nullptr && std::strcmp(r, "0") == 0) ? 0 : 1;
-        const char* c = std::getenv("SRT_CULL_CHUNK");
-        const long chunk = c != nullptr ? std::strtol(c, nullptr, 10) : 0;
-        p.chunk_ids = chunk >= 64 ? static_cast<unsigned>(chunk) : 512u;
     }
     p.wf = static_cast<float>(band.width);
     p.hf = static_cast<float>(band.height);
@@ -1511,40 +2021,52 @@ hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_ver
     } else if (variant == kTraceCull) {
         const unsigned gy = static_cast<unsigned>((band.row_count + kTileRows - 1) / kTileRows);
         if (bins != nullptr) {
-            const unsigned sx = (gx + kSuperTiles - 1) / kSuperTiles;
-            if (static_cast<std::size_t>(sx) * gy > bins->supers) {
+            if (bins->tiles != static_cast<std::size_t>(gx) * gy || !CullBinnable(band.width, band.row_count)) {
                 return hipErrorInvalidValue;  // bins sized for another band shape
             }
             BinParams b{};
-            b.qboxes = p.qboxes;
             b.offsets = p.offsets;
-            b.super_q = reinterpret_cast<uint4*>(bins->super_q);
-            b.lists = bins->lists;
+            b.cull = p.cull;
+            b.tile_info = static_cast<TileInfo*>(bins->tile_info);
             b.counts = bins->counts;
-            b.tile_keys = reinterpret_cast<unsigned long long*>(bins->tile_keys);
-            b.tile_done = bins->tile_done;
+            b.lists = bins->lists;
+            b.large_list = bins->large_list;
+            b.tile_order = bins->tile_order;
             b.capacity = bins->capacity;
-            b.n_pad = p.n_pad;
-            b.supers_x = static_cast<int>(sx);
+            b.n = static_cast<unsigned>(n);
+            b.tiles_x = static_cast<int>(gx);
+            b.tiles_y = static_cast<int>(gy);
             b.width = p.width;
             b.row_count = p.row_count;
             b.row_begin = p.row_begin;
             b.wf = p.wf;
             b.hf = p.hf;
-            hipLaunchKernelGGL(SuperBoxKernel, dim3(sx, gy), dim3(kBinThreads), 0, stream, b);
-            const unsigned slices = std::min<unsigned>(kBinMaxSlices, p.n_pad / kBinStep);
-            hipLaunchKernelGGL(BinKernel, dim3(gy, slices), dim3(kBinThreads), 0, stream, b);
+#ifdef SRT_DIAG
+            if (const char* e = std::getenv("SRT_EXP")) {
+                b.exp = static_cast<unsigned>(std::strtoul(e, nullptr, 0));
+                p.exp = b.exp;
+            }
+#endif
+            hipLaunchKernelGGL(TileInfoKernel, dim3(gx, gy), dim3(kBinThreads), 0, stream, b);
+            if (n != 0) {
+                const unsigned blocks = static_cast<unsigned>((n + kBinThreads - 1) / kBinThreads);
+                hipLaunchKernelGGL(BinTrianglesKernel, dim3(blocks), dim3(kBinThreads), 0, stream, b);
+            }
+            hipLaunchKernelGGL(TileOrderKernel, dim3(1), dim3(kOrderThreads), 0, stream, b);
+            p.tile_info = b.tile_info;
+            p.order = bins->order;
+            p.tile_order = bins->tile_order;
             p.bin_lists = bins->lists;
             p.bin_counts = bins->counts;
+            p.large_list = bins->large_list;
             p.bin_capacity = bins->capacity;
-            p.tile_keys = b.tile_keys;
-            p.tile_done = b.tile_done;
         }
-        const unsigned gz = bins != nullptr ? kMaxChunks : 1u;
+        // One block per (tile, part): gridDim.x = tile columns, gridDim.y = tile rows x parts.
+        const dim3 grid(gx, gy * kParts);
         switch (CullWavesFromEnv()) {
-            case 4: hipLaunchKernelGGL(TraceCullKernel<4>, dim3(gx, gy, gz), dim3(kWave * 4), 0, stream, p); break;
-            case 16: hipLaunchKernelGGL(TraceCullKernel<16>, dim3(gx, gy, gz), dim3(kWave * 16), 0, stream, p); break;
-            default: hipLaunchKernelGGL(TraceCullKernel<8>, dim3(gx, gy, gz), dim3(kWave * 8), 0, stream, p); break;
+            case 8: hipLaunchKernelGGL(TraceCullKernel<8>, grid, dim3(kWave * 8), 0, stream, p); break;
+            case 16: hipLaunchKernelGGL(TraceCullKernel<16>, grid, dim3(kWave * 16), 0, stream, p); break;
+            default: hipLaunchKernelGGL(TraceCullKernel<4>, grid, dim3(kWave * 4), 0, stream, p); break;
         }
     } else {
         constexpr int kRowsPerBlock = kRowsPerLane * kLdsWaves;

@@ -113,6 +113,15 @@ DeviceScene::DeviceScene(const Scene& scene, int device)
         m_vertices = DeviceAlloc<float>(m_n * 9, "hipMalloc(vertices)");
         m_albedo = DeviceAlloc<float>(m_n * 3, "hipMalloc(albedo)");
         m_edges = DeviceAlloc<float>(PaddedTriangleCount(m_n) * kEdgeFloatsPerTriangle, "hipMalloc(edges)");
+        const std::vector<std::uint32_t> order = SpatialOrder(scene);
+        std::vector<std::uint32_t> rank(order.size());
+        for (std::size_t i = 0; i < order.size(); ++i) {
+            rank[order[i]] = static_cast<std::uint32_t>(i);
+        }
+        m_order = DeviceAlloc<unsigned>(m_n == 0 ? 1 : m_n, "hipMalloc(order)");
+        m_rank = DeviceAlloc<unsigned>(m_n == 0 ? 1 : m_n, "hipMalloc(rank)");
+        HipCheck(hipMemcpy(m_order, order.data(), m_n * sizeof(unsigned), hipMemcpyHostToDevice), "hipMemcpy(order)");
+        HipCheck(hipMemcpy(m_rank, rank.data(), m_n * sizeof(unsigned), hipMemcpyHostToDevice), "hipMemcpy(rank)");
         HipCheck(hipMemcpy(m_vertices, scene.vertices.data(), m_n * 9 * sizeof(float), hipMemcpyHostToDevice),
                  "hipMemcpy(vertices)");
         HipCheck(hipMemcpy(m_albedo, scene.albedo.data(), m_n * 3 * sizeof(float), hipMemcpyHostToDevice),
@@ -121,6 +130,8 @@ DeviceScene::DeviceScene(const Scene& scene, int device)
         (void)hipFree(m_vertices);
         (void)hipFree(m_albedo);
         (void)hipFree(m_edges);
+        (void)hipFree(m_order);
+        (void)hipFree(m_rank);
         throw;
     }
 }
@@ -132,6 +143,8 @@ DeviceScene::~DeviceScene() {
     (void)hipFree(m_vertices);
     (void)hipFree(m_albedo);
     (void)hipFree(m_edges);
+    (void)hipFree(m_order);
+    (void)hipFree(m_rank);
     (void)hipFree(m_cull_work);
     if (prev >= 0) {
         (void)hipSetDevice(prev);
@@ -145,7 +158,7 @@ void DeviceScene::Prepare(std::size_t width, std::size_t height, hipStream_t str
     m_frame = MakeFrame(m_camera, width, height);
     m_width = width;
     m_height = height;
-    HipCheck(LaunchPrepare(m_vertices, m_n, m_frame, m_edges, stream), "prepare kernel launch");
+    HipCheck(LaunchPrepare(m_vertices, m_rank, m_n, m_frame, m_edges, stream), "prepare kernel launch");
 }
 
 void DeviceScene::Trace(const float* d_offsets, float* d_rgba, std::size_t row_begin, std::size_t row_count,
@@ -159,17 +172,9 @@ void DeviceScene::Trace(const float* d_offsets, float* d_rgba, std::size_t row_b
     BandArgs band{d_offsets, d_rgba, m_width, m_height, row_begin, row_count};
     CullBins bins{};
     const CullBins* use_bins = nullptr;
-    if (variant == kTraceCull && row_count != 0 && CullBinningEnabled()) {
-        // One grow-only allocation: super-tile boxes | tile keys | lists | counts | tile counters.
-        const std::size_t supers = CullSuperTiles(m_width, row_count);
-        const std::size_t tiles = CullTiles(m_width, row_count);
-        const unsigned cap = CullBinCapacity(m_n, supers);
-        const std::size_t q_bytes = supers * 16;
-        const std::size_t key_bytes = row_count * m_width * 8;
-        const std::size_t list_bytes = (supers * cap + 4) * 4;
-        const std::size_t count_bytes = supers * 4;
-        const std::size_t done_bytes = tiles * 4;
-        const std::size_t bytes = q_bytes + key_bytes + list_bytes + count_bytes + done_bytes;
+    if (variant == kTraceCull && row_count != 0 && CullBinningEnabled() && CullBinnable(m_width, row_count)) {
+        // One grow-only, zero-filled allocation (render.h CullBins); its counters reset themselves.
+        const std::size_t bytes = CullBinBytes(m_n, m_width, row_count);
         if (bytes > m_cull_bytes) {
             HipCheck(hipStreamSynchronize(stream), "hipStreamSynchronize(cull work)");
             (void)hipFree(m_cull_work);
@@ -177,15 +182,16 @@ void DeviceScene::Trace(const float* d_offsets, float* d_rgba, std::size_t row_b
             m_cull_bytes = 0;
             m_cull_work = DeviceAlloc<unsigned char>(bytes, "hipMalloc(cull work)");
             m_cull_bytes = bytes;
+            m_cull_shape = 0;
         }
-        unsigned char* w = m_cull_work;
-        bins.super_q = reinterpret_cast<unsigned*>(w);
-        bins.tile_keys = w + q_bytes;
-        bins.lists = reinterpret_cast<unsigned*>(w + q_bytes + key_bytes);
-        bins.counts = reinterpret_cast<unsigned*>(w + q_bytes + key_bytes + list_bytes);
-        bins.tile_done = reinterpret_cast<unsigned*>(w + q_bytes + key_bytes + list_bytes + count_bytes);
-        bins.capacity = cap;
-        bins.supers = supers;
+        const std::uint64_t shape = (static_cast<std::uint64_t>(m_width) << 32) | row_count;
+        if (shape != m_cull_shape) {
+            // A new carve-up: zero it so the self-resetting counters start at 0.
+            HipCheck(hipMemsetAsync(m_cull_work, 0, bytes, stream), "hipMemsetAsync(cull work)");
+            m_cull_shape = shape;
+        }
+        bins = CullBinLayout(m_cull_work, m_n, m_width, row_count);
+        bins.order = m_order;
         use_bins = &bins;
     }
     HipCheck(LaunchTrace(m_edges, m_n, m_vertices, m_albedo, m_frame, m_background, band, variant, use_bins, stream),

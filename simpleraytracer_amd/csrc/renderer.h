@@ -54,13 +54,16 @@ private:
     float* m_vertices = nullptr;
     float* m_albedo = nullptr;
     float* m_edges = nullptr;
+    unsigned* m_order = nullptr;  // record ids in spatial order (SpatialOrder), for the cull bins
+    unsigned* m_rank = nullptr;   // its inverse: record id -> position
     Frame m_frame{};
     std::size_t m_width = 0;
     std::size_t m_height = 0;
-    // Cull variant work buffers (render.h CullBins: bin lists, split-tile keys), grown on
+    // Cull variant work buffers (render.h CullBins: tile info, bin lists, split-tile keys), grown on
     // demand by Trace; disabled by env SRT_CULL_BIN=0 (every tile then streams every record).
     mutable unsigned char* m_cull_work = nullptr;
     mutable std::size_t m_cull_bytes = 0;
+    mutable std::uint64_t m_cull_shape = 0;  // (width << 32) | rows of the current carve-up
 };
 
 // Trace kernel variant from env SRT_TRACE_VARIANT ("lds" | "scalar" | "cull", default cull).

@@ -60,6 +60,10 @@ def main():
         summary[n] = {"mean": float(col.mean()), "p50": float(np.median(col)), "p90": float(np.percentile(col, 90)),
                       "max": float(col.max())}
     summary["chunks_hist"] = {int(c): int((chunks == c).sum()) for c in np.unique(chunks)}
+    mode = buf[: gx * gy, 7].astype(np.int64)  # z = 0 blocks: bin list length, large-list length
+    cnt = (mode >> 16) & 0xFFFFFF
+    summary["tile_list"] = {"mean": float(cnt.mean()), "p50": float(np.median(cnt)), "p90": float(np.percentile(cnt, 90)),
+                            "max": int(cnt.max()), "sum": int(cnt.sum()), "large": int((mode >> 40).max())}
     summary["blocks_run"] = int(ran.sum())
     idx = np.nonzero(ran)[0]
     heavy = idx[np.argsort(-allb[idx, 6])[:8]]

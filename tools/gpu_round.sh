@@ -32,6 +32,9 @@ fi
 if [[ $STEPS == *bench* ]]; then
     run bench 600 python bench.py
 fi
+if [[ $STEPS == *quick* ]]; then
+    run bench_quick 300 "${BENCH[@]}"
+fi
 if [[ $STEPS == *prof* ]]; then
     run prof_stats 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- "${BENCH[@]}"
 fi
