@@ -3,10 +3,22 @@
 
     python bench.py [--gpus N --steps K --warmup W]        (N > 1: launched by torch.distributed.run)
 
-One step = one frame of the hot path on device-resident inputs: edge setup (prepare kernel)
-+ brute-force closest hit + shade (trace kernel) for this rank's row band, and for N > 1 the
-band gather to rank 0 over RCCL (strong scaling: the frame is fixed, N GPUs split its rows).
-Prints ONE JSON line on rank 0 (contract in the task statement; fields in DESIGN.md "Bench").
+One step = one frame of the hot path on device-resident inputs (SURVEY.md section 8 rows
+a9-a12): edge-record setup (prepare kernel) + the closest-hit trace with its cull bins
+(TileInfo / BinTriangles / TileOrder kernels, then TraceCullKernel, which also shades and
+stores the framebuffer). The trace result is bit-identical to brute force (every ray against
+every triangle; DESIGN.md section 5, tests/test_gpu_parity.py).
+
+Multi-GPU, one rank per GPU:
+  --mode frames (default): every rank renders whole 1920x1080 frames of a temporal-jitter
+      sequence (rank r's frames use the uniform sub-pixel offset J_r; J_0 = 0.5 = the headline
+      frame); no collective in the timed region; "scaling": "weak".
+  --mode bands: the frame's rows are split into P bands (north_star row bands), each rank
+      traces its band, and the bands are gathered to rank 0 over RCCL every step (double
+      buffered, so step k's gather overlaps step k+1's render); "scaling": "strong".
+  For N > 1 the line also carries the other mode's measurement under "bands" / "frames".
+
+Prints ONE JSON line on rank 0 (fields in DESIGN.md section 6).
 """
 from __future__ import annotations
 
@@ -22,23 +34,27 @@ REPO = Path(__file__).resolve().parent
 sys.path.insert(0, str(REPO))
 
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md chip table (spec)
-FP32_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md chip table (spec, vector fp32)
-EDGE_BYTES_PER_TRI = 36      # 9 fp32 edge-function coefficients read per ray-triangle test
+FP32_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md chip table (spec, vector fp32, packed)
+EDGE_BYTES_PER_TRI = 36      # 9 fp32 edge coefficients per ray-triangle test
 PIXEL_IO_BYTES = 8 + 16      # sample offsets in + RGBA out per ray
-FLOPS_PER_TEST = 12          # 3 edge functions x 2 FMA (DESIGN.md "Roofline")
+FLOPS_PER_TEST = 12          # 3 edge functions x 2 FMA
+GOLDEN = 0.6180339887498949  # temporal jitter sequence step
+KERNEL_NAMES = {"lds": "TraceLdsKernel", "scalar": "TraceScalarKernel", "cull": "TraceCullKernel"}
 
 
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--width", type=int, default=1920)
     p.add_argument("--height", type=int, default=1080)
     p.add_argument("--scene", default="soup", choices=["soup", "cornell", "triangle"])
     p.add_argument("--triangles", type=int, default=100_000)
-    p.add_argument("--variant", default=os.environ.get("SRT_BENCH_VARIANT", "cull"), choices=["lds", "scalar", "cull"])
+    p.add_argument("--variant", default=os.environ.get("SRT_BENCH_VARIANT", "cull"), choices=list(KERNEL_NAMES))
+    p.add_argument("--mode", default="frames", choices=["frames", "bands"], help="multi-GPU split (see module doc)")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample length")
+    p.add_argument("--brute-steps", type=int, default=5, help="timed frames of the brute-force LDS kernel (0 = skip)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive ml* API measurement")
     return p.parse_args()
@@ -51,17 +67,23 @@ def workload_name(a):
     return f"{a.scene} {a.width}x{a.height} 1spp"
 
 
-def cpu_baseline(scene_path, a, rank_rows):
+def jitter(rank: int) -> float:
+    """Uniform sub-pixel offset of rank r's frames (r = 0: 0.5, the headline frame)."""
+    import numpy as np
+
+    return float(np.float32((0.5 + rank * GOLDEN) % 1.0))
+
+
+def cpu_baseline(scene_path, a):
     """The oracle ('port') on this host's cores over a bounded, evenly spaced row sample."""
     from oracle import srt_oracle
 
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
     sc = srt_oracle.OracleScene(scene_path)
     h = a.height
-    # calibration: one row per thread
-    step = max(1, h // threads)
+    step = max(1, h // threads)  # calibration: one row per thread
     t0 = time.perf_counter()
-    n0 = sc.render(a.width, h, row_begin=0, row_count=h, row_step=step, threads=threads)
+    sc.render(a.width, h, row_begin=0, row_count=h, row_step=step, threads=threads)
     cal = time.perf_counter() - t0
     rows_cal = (h + step - 1) // step
     per_row = cal / rows_cal
@@ -71,14 +93,13 @@ def cpu_baseline(scene_path, a, rank_rows):
     sc.render(a.width, h, row_begin=0, row_count=h, row_step=step, threads=threads)
     dt = time.perf_counter() - t0
     rows = (h + step - 1) // step
-    del n0
     return {
         "value": round(rows * a.width / dt / 1e6, 6),
         "unit": "Mrays/s",
         "cores": srt_oracle.threads(threads),
         "kind": "port",
         "sample": f"{rows} of {h} rows (every {step}th, all {a.width} columns) of {workload_name(a)}; "
-                  f"{dt:.1f} s; OpenMP scalar C oracle (oracle/srt_oracle.c)",
+                  f"{dt:.1f} s; OpenMP scalar C oracle (oracle/srt_oracle.c), brute force",
     }
 
 
@@ -88,11 +109,99 @@ def pmc_traffic(workload, variant):
     if not f.exists():
         return None
     try:
-        d = json.loads(f.read_text())
-        e = d.get(f"{workload}|{variant}")
+        e = json.loads(f.read_text()).get(f"{workload}|{variant}")
         return None if e is None else float(e["hbm_bytes_per_launch"])
     except Exception:
         return None
+
+
+class Frames:
+    """Timed loop of one multi-GPU mode on this rank (module doc)."""
+
+    def __init__(self, torch, dist, srt, scene, a, mode, world, rank, dev, variant):
+        from simpleraytracer_amd.bands import band_range, band_rows
+
+        self.torch, self.dist, self.scene, self.a = torch, dist, scene, a
+        self.mode, self.world, self.rank, self.variant = mode, world, rank, variant
+        W, H = a.width, a.height
+        if mode == "bands":
+            self.row_begin, self.row_count = band_range(H, world, rank)
+            B = band_rows(H, world)
+            off = 0.5
+        else:
+            self.row_begin, self.row_count = 0, H
+            B = H
+            off = jitter(rank)
+        self.offsets = torch.full((B, W, 2), off, dtype=torch.float32, device=dev)
+        nbuf = 2 if (mode == "bands" and world > 1) else 1
+        self.bands = [torch.zeros((B, W, 4), dtype=torch.float32, device=dev) for _ in range(nbuf)]
+        self.frames = None
+        if mode == "bands" and world > 1 and rank == 0:
+            self.frames = [torch.empty((world * B, W, 4), dtype=torch.float32, device=dev) for _ in range(nbuf)]
+        self.pending = [None] * nbuf
+        self.stream = torch.cuda.current_stream(dev)
+        self.dev = dev
+
+    def step(self, k, ev=None):
+        from simpleraytracer_amd.bands import gather_bands
+
+        a, W, H = self.a, self.a.width, self.a.height
+        slot = k % len(self.bands)
+        if self.pending[slot] is not None:
+            self.pending[slot].wait()  # the gather still reading this band buffer
+            self.pending[slot] = None
+        if ev is not None:
+            ev[0].record(self.stream)
+        self.scene.prepare(W, H, self.stream)
+        if ev is not None:
+            ev[1].record(self.stream)
+        band = self.bands[slot]
+        self.scene.trace(self.offsets[:self.row_count], band[:self.row_count], self.row_begin, self.row_count,
+                         variant=self.variant, stream=self.stream)
+        if self.mode == "bands" and self.world > 1:
+            out = self.frames[slot] if self.frames is not None else None
+            if self.dist.get_backend() == "gloo":  # CPU rehearsal only: gloo gathers host tensors
+                gather_bands(band.cpu(), H, dst=0)
+            else:
+                self.pending[slot] = self.dist.gather(band, gather_list=None if out is None else
+                                                      [out[r * band.shape[0]:(r + 1) * band.shape[0]]
+                                                       for r in range(self.world)], dst=0, async_op=True)
+
+    def run(self, steps, warmup, timing=True):
+        torch, dist = self.torch, self.dist
+        for k in range(warmup):
+            self.step(k)
+        self.drain()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        self.scene.take_stage_times()
+        self.scene.set_stage_timing(timing)
+        if self.world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(self.dev)
+        t0 = time.perf_counter()
+        for k in range(steps):
+            self.step(warmup + k, ev[k])
+        self.drain()
+        torch.cuda.synchronize(self.dev)
+        if self.world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        self.scene.set_stage_timing(False)
+        if self.world > 1:
+            t = torch.tensor([elapsed], dtype=torch.float64, device=self.dev if dist.get_backend() != "gloo" else "cpu")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+        launches, bin_ms, trace_ms = self.scene.take_stage_times()
+        prep_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / steps
+        units = self.a.width * self.a.height * steps * (self.world if self.mode == "frames" else 1)
+        return {"elapsed": elapsed, "mrays": units / elapsed / 1e6, "prepare_ms": prep_ms, "bin_ms": bin_ms,
+                "trace_ms": trace_ms, "launches": launches, "ms_per_step": elapsed / steps * 1e3}
+
+    def drain(self):
+        for i, h in enumerate(self.pending):
+            if h is not None:
+                h.wait()
+                self.pending[i] = None
 
 
 def main():
@@ -101,17 +210,22 @@ def main():
     import torch.distributed as dist
 
     import simpleraytracer_amd as srt
-    from simpleraytracer_amd.bands import band_range, band_rows, gather_bands
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("SRT_BENCH_ONE_DEVICE"):  # rehearsal of N > 1 ranks on a one-GPU box (with gloo)
+        local = 0
     if world != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("SRT_BENCH_BACKEND", "nccl")  # gloo: CPU-side rehearsal on one GPU
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     tmp = tempfile.TemporaryDirectory()
     scene_path = os.path.join(tmp.name, f"scene_rank{rank}.srt")
@@ -121,77 +235,47 @@ def main():
         srt.write_scene(scene_path, a.scene)
     scene = srt.DeviceScene(scene_path, local)
     n_tri = scene.triangles
-
     W, H = a.width, a.height
-    row_begin, row_count = band_range(H, world, rank)
-    B = band_rows(H, world)
-    offsets = torch.full((B, W, 2), 0.5, dtype=torch.float32, device=dev)
-    band = torch.zeros((B, W, 4), dtype=torch.float32, device=dev)
-    stream = torch.cuda.current_stream(dev)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
-           torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    wl = workload_name(a)
 
-    def step(i=None):
-        e = ev[i] if i is not None else None
-        if e:
-            e[0].record(stream)
-        scene.prepare(W, H, stream)
-        if e:
-            e[1].record(stream)
-        scene.trace(offsets[:row_count], band[:row_count], row_begin, row_count, variant=a.variant, stream=stream)
-        if e:
-            e[2].record(stream)
-        if world > 1:
-            gather_bands(band, H, dst=0)
-
-    for _ in range(a.warmup):
-        step()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for i in range(a.steps):
-        step(i)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
-    prep_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / a.steps
-    trace_ms = sum(e[1].elapsed_time(e[2]) for e in ev) / a.steps
-    rays_total = W * H * a.steps
-    value = rays_total / elapsed / 1e6
+    main_run = Frames(torch, dist, srt, scene, a, a.mode, world, rank, dev, a.variant)
+    r = main_run.run(a.steps, a.warmup)
+    other = None
+    if world > 1:  # the other multi-GPU mode, same steps
+        om = "bands" if a.mode == "frames" else "frames"
+        other = (om, Frames(torch, dist, srt, scene, a, om, world, rank, dev, a.variant).run(a.steps, a.warmup))
+    brute = None
+    if world == 1 and a.brute_steps > 0 and a.variant != "lds":
+        brute = Frames(torch, dist, srt, scene, a, "frames", 1, 0, dev, "lds").run(a.brute_steps, 1)
 
     if rank == 0:
-        launch_rays = row_count * W
-        wl = workload_name(a)
+        launch_rays = main_run.row_count * W
+        rays_tests = launch_rays * n_tri
         alg_bytes = launch_rays * (EDGE_BYTES_PER_TRI * n_tri + PIXEL_IO_BYTES)
-        achieved_gbs = alg_bytes / (trace_ms * 1e-3) / 1e9
-        achieved_tf = launch_rays * n_tri * FLOPS_PER_TEST / (trace_ms * 1e-3) / 1e12
+        kernel_s = r["trace_ms"] * 1e-3
+        achieved_gbs = alg_bytes / kernel_s / 1e9
+        io_gbs = launch_rays * PIXEL_IO_BYTES / kernel_s / 1e9
+        achieved_tf = rays_tests * FLOPS_PER_TEST / kernel_s / 1e12
         line = {
             "metric": "Mrays/s at 1920x1080 on 100k-tri synthetic mesh",
-            "value": round(value, 4),
+            "value": round(r["mrays"], 4),
             "unit": "Mrays/s",
             "n_gpus": world,
             "steps": a.steps,
             "warmup": a.warmup,
-            "ms_per_step": round(elapsed / a.steps * 1e3, 4),
+            "ms_per_step": round(r["ms_per_step"], 4),
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": "weak" if a.mode == "frames" else "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (PCG32 triangle soup, seed 0x5EED; sample offsets 0.5 resident in HBM)",
+            "data": "synthetic (PCG32 triangle soup, seed 0x5EED; uniform sample offsets resident in HBM)",
             "config": {
                 "workload": wl,
                 "triangles": int(n_tri),
                 "width": W,
                 "height": H,
                 "spp": 1,
-                "parallelism": f"row-bands x{world}" + (" + RCCL gather" if world > 1 else ""),
+                "parallelism": (f"{a.mode} x{world}" + (" + RCCL gather" if a.mode == "bands" and world > 1 else "")),
                 "trace_variant": a.variant,
                 "cull_bins": os.environ.get("SRT_CULL_BIN", "1") != "0" if a.variant == "cull" else None,
             },
@@ -202,11 +286,17 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
                 "traffic": pmc_traffic(wl, a.variant),
-                "kernel": {"lds": "TraceLdsKernel", "scalar": "TraceScalarKernel", "cull": "TraceCullKernel"}[a.variant],
-                "kernel_ms": round(trace_ms, 4),
+                "kernel": KERNEL_NAMES[a.variant],
+                "kernel_ms": round(r["trace_ms"], 5),
                 "bytes_per_launch": alg_bytes,
-                "note": "north_star HBM roofline: 36 B/triangle/ray + 24 B/ray; LDS tiling re-uses each "
-                        "record across 2048 rays, so frac > 1 (see DESIGN.md Roofline)",
+                "note": "north_star HBM roofline (SURVEY 8d): 36 B per ray-triangle test + 24 B per ray, over the "
+                        "trace kernel's HIP-event time (bin kernels excluded). frac > 1: the kernel skips "
+                        "(record, tile) pairs that provably miss and re-uses records through LDS (DESIGN.md 6)",
+            },
+            "pixel_io_roofline": {
+                "achieved": round(io_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(io_gbs / HBM_PEAK_GBS, 4),
+                "note": "offsets in + RGBA out (24 B/ray) over the trace kernel time: the bytes no design avoids",
             },
             "compute_roofline": {
                 "bound": "valu-fp32",
@@ -215,13 +305,32 @@ def main():
                 "unit": "TFLOP/s",
                 "frac": round(achieved_tf / FP32_PEAK_TFLOPS, 4),
                 "flops_per_test": FLOPS_PER_TEST,
+                "note": "brute-force-equivalent flops (every ray x every triangle)",
             },
-            "prepare_ms": round(prep_ms, 4),
+            "stages_ms": {"prepare": round(r["prepare_ms"], 5), "bin": round(r["bin_ms"], 5),
+                          "trace_kernel": round(r["trace_ms"], 5), "frame": round(r["ms_per_step"], 5),
+                          "timed_launches": r["launches"]},
         }
+        if brute is not None:
+            bs = brute["trace_ms"] * 1e-3
+            tf = rays_tests * FLOPS_PER_TEST / bs / 1e12
+            line["brute_force"] = {
+                "variant": "lds", "kernel": "TraceLdsKernel", "mrays_per_s": round(brute["mrays"], 3),
+                "kernel_ms": round(brute["trace_ms"], 4), "steps": a.brute_steps,
+                "hbm_roofline_frac": round(alg_bytes / bs / 1e9 / HBM_PEAK_GBS, 4),
+                "valu_tflops": round(tf, 2), "valu_frac": round(tf / FP32_PEAK_TFLOPS, 4),
+                "note": "north_star design taken literally: every ray tests every triangle, records tiled through LDS",
+            }
+        if other is not None:
+            om, o = other
+            line[om] = {"mrays_per_s": round(o["mrays"], 4), "ms_per_step": round(o["ms_per_step"], 4),
+                        "scaling": "weak" if om == "frames" else "strong",
+                        "trace_kernel_ms": round(o["trace_ms"], 5), "bin_ms": round(o["bin_ms"], 5),
+                        "prepare_ms": round(o["prepare_ms"], 5)}
         if world == 1 and not a.no_e2e:
             line["e2e_ml_api"] = e2e_ml_api(scene_path, W, H)
         if world == 1 and not a.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(scene_path, a, (row_begin, row_count))
+            line["cpu_baseline"] = cpu_baseline(scene_path, a)
         print(json.dumps(line), flush=True)
     scene.close()
     if world > 1:

@@ -58,6 +58,14 @@ ML_API_ENTRY int srtPrepareAsync(srt_device_scene scene, size_t width, size_t he
 ML_API_ENTRY int srtTraceAsync(srt_device_scene scene, const float* d_offsets, float* d_rgba,
                                size_t row_begin, size_t row_count, int variant, void* stream);
 
+/* Stage timing (measurement): while enabled, every srtTraceAsync on the scene records HIP
+ * events on its stream before the cull bin kernels and immediately around the trace kernel.
+ * srtTakeStageTimes waits for the recorded events, writes the number of timed calls and the
+ * mean milliseconds of the bin stage (0 for variants without one) and of the trace kernel
+ * alone, and forgets them. */
+ML_API_ENTRY int srtSetStageTiming(srt_device_scene scene, int enable);
+ML_API_ENTRY int srtTakeStageTimes(srt_device_scene scene, unsigned* launches, double* bin_ms, double* trace_ms);
+
 #ifdef __cplusplus
 }
 #endif

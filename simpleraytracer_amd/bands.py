@@ -22,18 +22,27 @@ def band_range(height: int, world: int, rank: int) -> tuple[int, int]:
     return begin, end - begin
 
 
-def gather_bands(band, height: int, dst: int = 0, group=None):
-    """Gather every rank's (B, W, C) band to ``dst``; returns the (H, W, C) frame on dst, else None."""
+def gather_bands(band, height: int, dst: int = 0, group=None, out=None):
+    """Gather every rank's (B, W, C) band to ``dst``; returns the (H, W, C) frame on dst, else None.
+
+    ``out`` (dst only, optional): a (P * B, W, C) buffer the bands are received into in place
+    (its row slices are the gather list, so no concatenation copy); allocated when omitted.
+    """
     import torch
     import torch.distributed as dist
 
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
-    if band.shape[0] != band_rows(height, world):
-        raise ValueError(f"band buffer must have {band_rows(height, world)} rows, got {band.shape[0]}")
+    b = band_rows(height, world)
+    if band.shape[0] != b:
+        raise ValueError(f"band buffer must have {b} rows, got {band.shape[0]}")
     if rank == dst:
-        parts = [torch.empty_like(band) for _ in range(world)]
+        if out is None:
+            out = torch.empty((world * b,) + tuple(band.shape[1:]), dtype=band.dtype, device=band.device)
+        elif tuple(out.shape) != (world * b,) + tuple(band.shape[1:]) or not out.is_contiguous():
+            raise ValueError(f"out must be a contiguous {(world * b,) + tuple(band.shape[1:])} buffer")
+        parts = [out[r * b:(r + 1) * b] for r in range(world)]
         dist.gather(band, gather_list=parts, dst=dst, group=group)
-        return torch.cat(parts, dim=0)[:height]
+        return out[:height]
     dist.gather(band, gather_list=None, dst=dst, group=group)
     return None

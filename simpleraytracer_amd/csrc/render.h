@@ -107,11 +107,19 @@ unsigned CullBinCapacity(std::uint64_t n, std::size_t tiles);
 std::size_t CullBinBytes(std::uint64_t n, std::size_t width, std::size_t row_count);
 CullBins CullBinLayout(void* base, std::uint64_t n, std::size_t width, std::size_t row_count);
 
+// Optional stage events recorded on the launch stream (null = not recorded): `bin` before the
+// cull bin kernels, `begin` / `end` immediately around the trace kernel itself.
+struct StageEvents {
+    hipEvent_t bin = nullptr;
+    hipEvent_t begin = nullptr;
+    hipEvent_t end = nullptr;
+};
+
 // Launch the trace kernel over one band (cull variant: bin + trace; bins == nullptr streams
 // every record for every tile).
 hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_vertices, const float* d_albedo,
                        const Frame& frame, const float background[3], const BandArgs& band, int variant,
-                       const CullBins* bins, hipStream_t stream);
+                       const CullBins* bins, hipStream_t stream, const StageEvents* events = nullptr);
 
 #ifdef SRT_DIAG
 // Diagnostic build only: copy the cull kernel's per-block phase counters to host memory.

@@ -1984,9 +1984,16 @@ CullBins CullBinLayout(void* base, std::uint64_t n, std::size_t width, std::size
 
 hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_vertices, const float* d_albedo,
                        const Frame& frame, const float background[3], const BandArgs& band, int variant,
-                       const CullBins* bins, hipStream_t stream) {
+                       const CullBins* bins, hipStream_t stream, const StageEvents* events) {
     if (band.row_count == 0 || band.width == 0) {
         return hipSuccess;
+    }
+    const StageEvents ev = events != nullptr ? *events : StageEvents{};
+    if (ev.bin != nullptr) {
+        const hipError_t e = hipEventRecord(ev.bin, stream);
+        if (e != hipSuccess) {
+            return e;
+        }
     }
     TraceParams p{};
     p.edges = reinterpret_cast<const float4*>(d_edges);
@@ -2015,8 +2022,14 @@ hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_ver
         p.bg[k] = background[k];
     }
     const unsigned gx = static_cast<unsigned>((band.width + kWave - 1) / kWave);
+    auto mark = [&](hipEvent_t e) {
+        if (e != nullptr) {
+            (void)hipEventRecord(e, stream);
+        }
+    };
     if (variant == kTraceScalar) {
         const unsigned gy = static_cast<unsigned>((band.row_count + kRowsPerLane - 1) / kRowsPerLane);
+        mark(ev.begin);
         hipLaunchKernelGGL(TraceScalarKernel, dim3(gx, gy), dim3(kWave), 0, stream, p);
     } else if (variant == kTraceCull) {
         const unsigned gy = static_cast<unsigned>((band.row_count + kTileRows - 1) / kTileRows);
@@ -2063,6 +2076,7 @@ hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_ver
         }
         // One block per (tile, part): gridDim.x = tile columns, gridDim.y = tile rows x parts.
         const dim3 grid(gx, gy * kParts);
+        mark(ev.begin);
         switch (CullWavesFromEnv()) {
             case 8: hipLaunchKernelGGL(TraceCullKernel<8>, grid, dim3(kWave * 8), 0, stream, p); break;
             case 16: hipLaunchKernelGGL(TraceCullKernel<16>, grid, dim3(kWave * 16), 0, stream, p); break;
@@ -2071,9 +2085,14 @@ hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_ver
     } else {
         constexpr int kRowsPerBlock = kRowsPerLane * kLdsWaves;
         const unsigned gy = static_cast<unsigned>((band.row_count + kRowsPerBlock - 1) / kRowsPerBlock);
+        mark(ev.begin);
         hipLaunchKernelGGL(TraceLdsKernel, dim3(gx, gy), dim3(kWave * kLdsWaves), 0, stream, p);
     }
-    return hipGetLastError();
+    const hipError_t launch = hipGetLastError();
+    if (launch != hipSuccess) {
+        return launch;
+    }
+    return ev.end != nullptr ? hipEventRecord(ev.end, stream) : hipSuccess;
 }
 
 }  // namespace srt

@@ -146,6 +146,11 @@ DeviceScene::~DeviceScene() {
     (void)hipFree(m_order);
     (void)hipFree(m_rank);
     (void)hipFree(m_cull_work);
+    for (auto& e : m_events) {
+        for (hipEvent_t x : e) {
+            (void)hipEventDestroy(x);
+        }
+    }
     if (prev >= 0) {
         (void)hipSetDevice(prev);
     }
@@ -194,8 +199,45 @@ void DeviceScene::Trace(const float* d_offsets, float* d_rgba, std::size_t row_b
         bins.order = m_order;
         use_bins = &bins;
     }
-    HipCheck(LaunchTrace(m_edges, m_n, m_vertices, m_albedo, m_frame, m_background, band, variant, use_bins, stream),
+    StageEvents ev{};
+    if (m_timing) {
+        if (m_timed == m_events.size()) {
+            std::array<hipEvent_t, 3> e{};
+            for (auto& x : e) {
+                HipCheck(hipEventCreate(&x), "hipEventCreate(stage timing)");
+            }
+            m_events.push_back(e);
+        }
+        const auto& e = m_events[m_timed++];
+        ev = StageEvents{e[0], e[1], e[2]};
+    }
+    HipCheck(LaunchTrace(m_edges, m_n, m_vertices, m_albedo, m_frame, m_background, band, variant, use_bins, stream,
+                         m_timing ? &ev : nullptr),
              "trace kernel launch");
+}
+
+void DeviceScene::SetTiming(bool on) {
+    m_timing = on;
+}
+
+DeviceScene::StageTimes DeviceScene::TakeTimes() {
+    StageTimes t;
+    for (std::size_t i = 0; i < m_timed; ++i) {
+        const auto& e = m_events[i];
+        HipCheck(hipEventSynchronize(e[2]), "hipEventSynchronize(stage timing)");
+        float bin = 0.f, kernel = 0.f;
+        HipCheck(hipEventElapsedTime(&bin, e[0], e[1]), "hipEventElapsedTime(bin)");
+        HipCheck(hipEventElapsedTime(&kernel, e[1], e[2]), "hipEventElapsedTime(trace)");
+        t.bin_ms += bin;
+        t.kernel_ms += kernel;
+    }
+    t.launches = static_cast<unsigned>(m_timed);
+    if (m_timed != 0) {
+        t.bin_ms /= static_cast<double>(m_timed);
+        t.kernel_ms /= static_cast<double>(m_timed);
+    }
+    m_timed = 0;
+    return t;
 }
 
 struct Renderer::Slot {

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstddef>
+#include <array>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -46,6 +47,17 @@ public:
     std::size_t width() const { return m_width; }
     std::size_t height() const { return m_height; }
 
+    // Stage timing: while on, every Trace records HIP events on its stream before the cull bin
+    // kernels and around the trace kernel itself. TakeTimes waits for them and returns the mean
+    // durations (ms) of the Trace calls timed since the previous TakeTimes, then forgets them.
+    struct StageTimes {
+        unsigned launches = 0;
+        double bin_ms = 0.0;     // bin stage (cull: TileInfo + BinTriangles + TileOrder); 0 otherwise
+        double kernel_ms = 0.0;  // the trace kernel alone
+    };
+    void SetTiming(bool on);
+    StageTimes TakeTimes();
+
 private:
     int m_device;
     std::uint64_t m_n;
@@ -64,6 +76,10 @@ private:
     mutable unsigned char* m_cull_work = nullptr;
     mutable std::size_t m_cull_bytes = 0;
     mutable std::uint64_t m_cull_shape = 0;  // (width << 32) | rows of the current carve-up
+    // Stage-timing event triples (bin, begin, end), reused; m_timed of them hold a pending launch.
+    bool m_timing = false;
+    mutable std::vector<std::array<hipEvent_t, 3>> m_events;
+    mutable std::size_t m_timed = 0;
 };
 
 // Trace kernel variant from env SRT_TRACE_VARIANT ("lds" | "scalar" | "cull", default cull).

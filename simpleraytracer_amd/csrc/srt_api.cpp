@@ -140,6 +140,35 @@ ML_API_ENTRY int srtTraceAsync(srt_device_scene scene, const float* d_offsets, f
     });
 }
 
+ML_API_ENTRY int srtSetStageTiming(srt_device_scene scene, int enable) {
+    return Guarded([&] {
+        if (scene == nullptr) {
+            throw std::runtime_error("Bad scene handle");
+        }
+        FromHandle(scene)->SetTiming(enable != 0);
+    });
+}
+
+ML_API_ENTRY int srtTakeStageTimes(srt_device_scene scene, unsigned* launches, double* bin_ms, double* trace_ms) {
+    return Guarded([&] {
+        if (scene == nullptr) {
+            throw std::runtime_error("Bad scene handle");
+        }
+        srt::DeviceScene* s = FromHandle(scene);
+        Bind bind(s->device());
+        const srt::DeviceScene::StageTimes t = s->TakeTimes();
+        if (launches != nullptr) {
+            *launches = t.launches;
+        }
+        if (bin_ms != nullptr) {
+            *bin_ms = t.bin_ms;
+        }
+        if (trace_ms != nullptr) {
+            *trace_ms = t.kernel_ms;
+        }
+    });
+}
+
 #ifdef SRT_DIAG
 // Diagnostic build only (make diag): not part of include/srt_render.h.
 ML_API_ENTRY int srtDiagRead(void* host, size_t bytes) {

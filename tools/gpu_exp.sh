@@ -1,16 +1,19 @@
 #!/bin/bash
-# Diagnostic GPU session: the `make diag` library's per-block cull phase counters
-# (tools/diag_cull.py) and rocprofv3 kernel stats of bench.py under SRT_EXP experiment bits
-# (render.hip BinParams::exp; timing only, results are wrong with any bit set).
+# Experiment GPU session: parity tests, then bench lines + rocprofv3 kernel stats under each
+# env configuration in $CFGS (space-separated; each entry's '+' separates VAR=VALUE pairs).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-export SRT_LIB=simpleraytracer_amd/lib_diag/libModelRunner.so
-timeout -k 10 120 python tools/diag_cull.py > gpurun_out/diag.json 2> gpurun_out/diag.err || { echo "diag rc=$?"; tail -5 gpurun_out/diag.err; exit 1; }
-for e in ${EXPS:-0 1 2 4 8}; do
-    SRT_EXP=$e timeout -k 10 120 rocprofv3 --kernel-trace --stats -d gpurun_out/exp$e -o run --output-format csv -- \
-        python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-e2e > gpurun_out/exp$e.log 2>&1 || { echo "exp $e rc=$?"; exit 1; }
-    echo "exp $e"; cut -d, -f1,4 gpurun_out/exp$e/run_kernel_stats.csv | cut -c1-120
+if [ "${TESTS:-1}" = 1 ]; then
+    timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
+    rc=$?; tail -3 gpurun_out/pytest_gpu.log; [ $rc -le 1 ] || exit $rc
+fi
+for cfg in ${CFGS:-NONE=0}; do
+    tag=$(echo "$cfg" | tr '+=' '__')
+    env $(echo "$cfg" | tr '+' ' ') timeout -k 10 120 rocprofv3 --kernel-trace --stats -d gpurun_out/e_$tag -o run --output-format csv -- \
+        python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-e2e ${BENCH_ARGS:-} > gpurun_out/e_$tag.log 2>&1 || { echo "rc=$? $cfg"; exit 1; }
+    echo "== $cfg"; grep -o '"value": [0-9.]*' gpurun_out/e_$tag.log
+    cut -d, -f1,3,4 gpurun_out/e_$tag/run_kernel_stats.csv | sed 's/(srt::(anonymous namespace)::[A-Za-z]*)//; s/srt::(anonymous namespace):://' | head -8
 done
 echo done

@@ -22,7 +22,7 @@ run() {
 }
 STEPS=${STEPS:-tests,smoke,bench,prof,pmc}
 KERNEL_RE=${KERNEL_RE:-TraceCullKernel}
-BENCH=(python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-e2e)
+BENCH=(python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-e2e --brute-steps 0)
 if [[ $STEPS == *tests* ]]; then
     run pytest_gpu 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
 fi
@@ -31,6 +31,10 @@ if [[ $STEPS == *smoke* ]]; then
 fi
 if [[ $STEPS == *bench* ]]; then
     run bench 600 python bench.py
+fi
+if [[ $STEPS == *rehearse* ]]; then
+    SRT_BENCH_BACKEND=gloo SRT_BENCH_ONE_DEVICE=1 run rehearse2 300 python -m torch.distributed.run --nnodes=1 \
+        --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 10 --warmup 2
 fi
 if [[ $STEPS == *quick* ]]; then
     run bench_quick 300 "${BENCH[@]}"
