@@ -142,7 +142,7 @@ class Frames:
         self.stream = torch.cuda.current_stream(dev)
         self.dev = dev
 
-    def step(self, k, ev=None):
+    def step(self, k):
         from simpleraytracer_amd.bands import gather_bands
 
         a, W, H = self.a, self.a.width, self.a.height
@@ -150,11 +150,7 @@ class Frames:
         if self.pending[slot] is not None:
             self.pending[slot].wait()  # the gather still reading this band buffer
             self.pending[slot] = None
-        if ev is not None:
-            ev[0].record(self.stream)
         self.scene.prepare(W, H, self.stream)
-        if ev is not None:
-            ev[1].record(self.stream)
         band = self.bands[slot]
         self.scene.trace(self.offsets[:self.row_count], band[:self.row_count], self.row_begin, self.row_count,
                          variant=self.variant, stream=self.stream)
@@ -172,7 +168,6 @@ class Frames:
         for k in range(warmup):
             self.step(k)
         self.drain()
-        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
         self.scene.take_stage_times()
         self.scene.set_stage_timing(timing)
         if self.world > 1:
@@ -180,7 +175,7 @@ class Frames:
         torch.cuda.synchronize(self.dev)
         t0 = time.perf_counter()
         for k in range(steps):
-            self.step(warmup + k, ev[k])
+            self.step(warmup + k)
         self.drain()
         torch.cuda.synchronize(self.dev)
         if self.world > 1:
@@ -191,8 +186,7 @@ class Frames:
             t = torch.tensor([elapsed], dtype=torch.float64, device=self.dev if dist.get_backend() != "gloo" else "cpu")
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             elapsed = float(t.item())
-        launches, bin_ms, trace_ms = self.scene.take_stage_times()
-        prep_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / steps
+        launches, prep_ms, bin_ms, trace_ms = self.scene.take_stage_times()
         units = self.a.width * self.a.height * steps * (self.world if self.mode == "frames" else 1)
         return {"elapsed": elapsed, "mrays": units / elapsed / 1e6, "prepare_ms": prep_ms, "bin_ms": bin_ms,
                 "trace_ms": trace_ms, "launches": launches, "ms_per_step": elapsed / steps * 1e3}
@@ -239,14 +233,25 @@ def main():
     wl = workload_name(a)
 
     main_run = Frames(torch, dist, srt, scene, a, a.mode, world, rank, dev, a.variant)
-    r = main_run.run(a.steps, a.warmup)
+    # value: uninstrumented frames. Stage times: the same K frames again with HIP events bound
+    # to the kernels' dispatch packets (each event-bound dispatch leaves a 5-10 us bubble on
+    # the stream, so the instrumented frame is slower; both are reported).
+    r = main_run.run(a.steps, a.warmup, timing=False)
+    rt = main_run.run(a.steps, 0, timing=True)
+    for k in ("prepare_ms", "bin_ms", "trace_ms", "launches"):
+        r[k] = rt[k]
+    r["ms_per_step_instrumented"] = rt["ms_per_step"]
     other = None
     if world > 1:  # the other multi-GPU mode, same steps
         om = "bands" if a.mode == "frames" else "frames"
-        other = (om, Frames(torch, dist, srt, scene, a, om, world, rank, dev, a.variant).run(a.steps, a.warmup))
+        orun = Frames(torch, dist, srt, scene, a, om, world, rank, dev, a.variant)
+        other = (om, orun.run(a.steps, a.warmup, timing=False))
+        ot = orun.run(a.steps, 0, timing=True)
+        for k in ("prepare_ms", "bin_ms", "trace_ms"):
+            other[1][k] = ot[k]
     brute = None
     if world == 1 and a.brute_steps > 0 and a.variant != "lds":
-        brute = Frames(torch, dist, srt, scene, a, "frames", 1, 0, dev, "lds").run(a.brute_steps, 1)
+        brute = Frames(torch, dist, srt, scene, a, "frames", 1, 0, dev, "lds").run(a.brute_steps, 1, timing=True)
 
     if rank == 0:
         launch_rays = main_run.row_count * W
@@ -309,7 +314,11 @@ def main():
             },
             "stages_ms": {"prepare": round(r["prepare_ms"], 5), "bin": round(r["bin_ms"], 5),
                           "trace_kernel": round(r["trace_ms"], 5), "frame": round(r["ms_per_step"], 5),
-                          "timed_launches": r["launches"]},
+                          "frame_instrumented": round(r["ms_per_step_instrumented"], 5),
+                          "timed_launches": r["launches"],
+                          "note": "cull variant: prepare = PrepareInfoKernel (edge records + per-tile info, one "
+                                  "launch), bin = BinTrianglesKernel (its last block orders the tiles), trace_kernel "
+                                  "= TraceCullKernel; frame = uninstrumented, frame_instrumented = with the events"},
         }
         if brute is not None:
             bs = brute["trace_ms"] * 1e-3

@@ -49,7 +49,9 @@ ML_API_ENTRY srt_device_scene srtDeviceSceneCreate(const char* path, int device)
 ML_API_ENTRY void srtDeviceSceneRelease(srt_device_scene scene);
 ML_API_ENTRY unsigned long long srtDeviceSceneTriangles(srt_device_scene scene);
 
-/* Stage 1: edge-record setup for a W x H frame (one thread per triangle). */
+/* Stage 1: edge-record setup for a W x H frame (one thread per triangle). The work is
+ * enqueued by the next srtTraceAsync, on that call's stream, fused into its first kernel; the
+ * records then serve every srtTraceAsync until the next srtPrepareAsync. */
 ML_API_ENTRY int srtPrepareAsync(srt_device_scene scene, size_t width, size_t height, void* stream);
 
 /* Stage 2: trace frame rows [row_begin, row_begin + row_count) of the prepared frame.
@@ -58,13 +60,14 @@ ML_API_ENTRY int srtPrepareAsync(srt_device_scene scene, size_t width, size_t he
 ML_API_ENTRY int srtTraceAsync(srt_device_scene scene, const float* d_offsets, float* d_rgba,
                                size_t row_begin, size_t row_count, int variant, void* stream);
 
-/* Stage timing (measurement): while enabled, every srtTraceAsync on the scene records HIP
- * events on its stream before the cull bin kernels and immediately around the trace kernel.
- * srtTakeStageTimes waits for the recorded events, writes the number of timed calls and the
- * mean milliseconds of the bin stage (0 for variants without one) and of the trace kernel
- * alone, and forgets them. */
+/* Stage timing (measurement): while enabled, srtPrepareAsync and srtTraceAsync bind HIP events
+ * to their kernels' own dispatch packets (hipExtLaunchKernelGGL start/stop events: no extra
+ * packets on the stream). srtTakeStageTimes waits for them, writes the number of timed trace
+ * calls and the mean milliseconds of the prepare kernel, the bin stage (TileInfo start to
+ * TileOrder end; 0 for variants without one) and the trace kernel alone, and forgets them. */
 ML_API_ENTRY int srtSetStageTiming(srt_device_scene scene, int enable);
-ML_API_ENTRY int srtTakeStageTimes(srt_device_scene scene, unsigned* launches, double* bin_ms, double* trace_ms);
+ML_API_ENTRY int srtTakeStageTimes(srt_device_scene scene, unsigned* launches, double* prepare_ms, double* bin_ms,
+                                   double* trace_ms);
 
 #ifdef __cplusplus
 }

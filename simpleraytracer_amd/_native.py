@@ -82,7 +82,7 @@ _SIGNATURES = {
     "srtTraceAsync": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
                                      ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]),
     "srtSetStageTiming": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
-    "srtTakeStageTimes": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint),
+    "srtTakeStageTimes": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint), ctypes.POINTER(ctypes.c_double),
                                          ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
 }
 

@@ -72,7 +72,8 @@ struct BandArgs {
 // Launch the prepare kernel: writes PaddedTriangleCount(n) / kTileTriangles tiles into `edges`,
 // then the screen boxes, quantized boxes and cull records (d_rank: id -> spatial-order rank).
 hipError_t LaunchPrepare(const float* d_vertices, const unsigned* d_rank, std::uint64_t n, const Frame& frame,
-                         float* d_edges, hipStream_t stream);
+                         float* d_edges, hipStream_t stream, hipEvent_t ev_begin = nullptr,
+                         hipEvent_t ev_end = nullptr);
 
 // Cull tiles: 64 columns x 32 rows of rays, one trace block each (render.hip "Cull bins").
 constexpr int kCullTileCols = 64;
@@ -89,6 +90,7 @@ struct CullBins {
     unsigned* lists;       // tiles x capacity candidate ids (BinTrianglesKernel)
     unsigned* large_list;  // PaddedTriangleCount(n) ids binned to every tile
     unsigned* tile_order;  // tiles x parts: trace launch order of (tile, part), most work first
+    unsigned* sync;        // self-resetting counter of finished bin blocks (SRT_ORDER_IN_BIN=1)
     unsigned capacity;
     std::size_t tiles;
 };
@@ -107,19 +109,28 @@ unsigned CullBinCapacity(std::uint64_t n, std::size_t tiles);
 std::size_t CullBinBytes(std::uint64_t n, std::size_t width, std::size_t row_count);
 CullBins CullBinLayout(void* base, std::uint64_t n, std::size_t width, std::size_t row_count);
 
-// Optional stage events recorded on the launch stream (null = not recorded): `bin` before the
-// cull bin kernels, `begin` / `end` immediately around the trace kernel itself.
+// Optional stage timing events (null = not recorded). They are bound to the kernels' own
+// dispatch packets (hipExtLaunchKernelGGL start / stop events), so timing adds no marker
+// packets to the stream: `prep_*` = the prepare kernel (fused with the tile-info blocks in
+// the binned cull variant: PrepareInfoKernel; TileInfoKernel alone when no prepare is
+// pending), `bin_*` = BinTrianglesKernel (its last block also orders the tiles),
+// `begin` / `end` = the trace kernel.
 struct StageEvents {
-    hipEvent_t bin = nullptr;
+    hipEvent_t prep_begin = nullptr;
+    hipEvent_t prep_end = nullptr;
+    hipEvent_t bin_begin = nullptr;
+    hipEvent_t bin_end = nullptr;
     hipEvent_t begin = nullptr;
     hipEvent_t end = nullptr;
 };
 
 // Launch the trace kernel over one band (cull variant: bin + trace; bins == nullptr streams
-// every record for every tile).
+// every record for every tile). prepare_rank != null: first (re)compute the edge records for
+// `frame` (LaunchPrepare's work; fused with the tile-info blocks when binning).
 hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_vertices, const float* d_albedo,
                        const Frame& frame, const float background[3], const BandArgs& band, int variant,
-                       const CullBins* bins, hipStream_t stream, const StageEvents* events = nullptr);
+                       const CullBins* bins, hipStream_t stream, const StageEvents* events = nullptr,
+                       const unsigned* prepare_rank = nullptr);
 
 #ifdef SRT_DIAG
 // Diagnostic build only: copy the cull kernel's per-block phase counters to host memory.

@@ -5,6 +5,8 @@
 // fmaf, so CPU (oracle/srt_oracle.c) and GPU evaluate bit-identical float expressions.
 #include "render.h"
 
+#include <hip/hip_ext.h>
+
 #include <cmath>
 #include <cstdlib>
 #include <cstdio>
@@ -192,8 +194,7 @@ __device__ __forceinline__ unsigned PackI16(int low, int high) {
 // One thread per triangle: origin-relative edge normals nA = B x C, nB = C x A, nC = A x B
 // (A, B, C = vertices - eye), signed volume vol = A . nA, orientation normalised so vol > 0,
 // then each normal projected onto the affine ray frame: E(fx, fy) = n . (base + fx du + fy dv).
-__global__ __launch_bounds__(256) void PrepareKernel(PrepareParams p) {
-    const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void PrepareRecord(const PrepareParams& p, unsigned i) {
     if (i >= p.n_pad) {
         return;
     }
@@ -258,6 +259,10 @@ __global__ __launch_bounds__(256) void PrepareKernel(PrepareParams p) {
         r.sb = sb;
         p.cull[p.rank[i]] = r;
     }
+}
+
+__global__ __launch_bounds__(256) void PrepareKernel(PrepareParams p) {
+    PrepareRecord(p, blockIdx.x * blockDim.x + threadIdx.x);
 }
 
 // Per-lane ray state: R rays sharing one image column.
@@ -1433,6 +1438,8 @@ struct BinParams {
     unsigned* __restrict__ lists;       // tiles x capacity
     unsigned* __restrict__ large_list;  // n_pad
     unsigned* __restrict__ tile_order;  // tiles: trace block -> tile (TileOrderKernel)
+    unsigned* __restrict__ sync;        // [0] bin blocks done (self-resetting)
+    unsigned order_in_bin;              // the bin kernel's last block computes the tile order
     unsigned capacity;
     unsigned n;
     unsigned exp;  // diagnostic build: experiment bits (env SRT_EXP), 0 in the product
@@ -1478,7 +1485,8 @@ __device__ void WaveScanOrdered(unsigned* a, int n, bool reverse, int lane) {
     }
 }
 
-__global__ __launch_bounds__(kBinThreads) void TileInfoKernel(BinParams p) {
+// One block per tile (bx, by).
+__device__ __forceinline__ void TileInfoBlock(const BinParams& p, int bx, int by) {
     constexpr int kWaves = kBinThreads / kWave;
     constexpr int kPer = kWave * kTileRows / kBinThreads;  // offsets per thread (8)
     __shared__ Box boxes[kWaves];
@@ -1486,8 +1494,8 @@ __global__ __launch_bounds__(kBinThreads) void TileInfoKernel(BinParams p) {
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
     const int wave = tid / kWave;
-    const int x0 = blockIdx.x * kWave;
-    const int y0 = blockIdx.y * kTileRows;
+    const int x0 = bx * kWave;
+    const int y0 = by * kTileRows;
     if (tid == 0) {
         irregular = 0u;
     }
@@ -1535,13 +1543,38 @@ __global__ __launch_bounds__(kBinThreads) void TileInfoKernel(BinParams p) {
         ti.oy = o0.y;
         ti.regular = irregular == 0u ? 1u : 0u;
         ti.usable = ScreenBoxUsable(box) ? 1u : 0u;
-        const unsigned tile = blockIdx.y * p.tiles_x + blockIdx.x;
+        const unsigned tile = by * p.tiles_x + bx;
         p.tile_info[tile] = ti;
         p.counts[tile] = 0u;  // the bin kernel runs after this one (stream order)
         if (tile == 0) {
             p.counts[p.tiles_x * p.tiles_y] = 0u;  // large list
         }
     }
+}
+
+__global__ __launch_bounds__(kBinThreads) void TileInfoKernel(BinParams p) {
+    TileInfoBlock(p, blockIdx.x, blockIdx.y);
+}
+
+// Prepare (one thread per record) and tile info (one block per tile) in one launch: block
+// b < prep_blocks prepares records, the others are tile blocks. The two are independent
+// (records vs sample offsets), so the latency-bound prepare blocks overlap the
+// bandwidth-bound tile blocks.
+struct PrepareInfoParams {
+    PrepareParams prep;
+    BinParams bin;
+    unsigned prep_blocks;
+};
+__global__ __launch_bounds__(kBinThreads) void PrepareInfoKernel(PrepareInfoParams p) {
+    static_assert(kBinThreads == 256, "prepare blocks are 256 threads");
+    const unsigned b = blockIdx.x;
+    if (b < p.prep_blocks) {
+        PrepareRecord(p.prep, b * kBinThreads + threadIdx.x);
+        return;
+    }
+    const unsigned t = b - p.prep_blocks;
+    TileInfoBlock(p.bin, static_cast<int>(t % static_cast<unsigned>(p.bin.tiles_x)),
+                  static_cast<int>(t / static_cast<unsigned>(p.bin.tiles_x)));
 }
 
 // First index i of the nondecreasing hi'[0..n) with hi'[i] >= v (n if none).
@@ -1576,56 +1609,110 @@ __device__ __forceinline__ int LastLoAtMost(const float2* b, int n, float v) {
 // the block counts its (tile, record) pairs in an LDS histogram, reserves each touched
 // tile's share of its list with ONE global atomic, then writes the ids. (Per-pair global
 // atomics serialise on the busy tiles' counters at the memory side.)
-static_assert(2 * kMaxBoundTiles <= kMaxBinTiles, "bounds scratch lives in the histogram");
+// Longest-processing-time-first launch order of the trace blocks: tiles sorted by their work,
+// descending (FULL-stream tiles first, then by the log2 of their candidate count), so the
+// heavy tiles start first and the light ones fill in behind them. One block; a counting sort
+// over 64 buckets (order within a bucket arbitrary: the frame does not depend on it).
+constexpr int kOrderThreads = 1024;
+__device__ __forceinline__ unsigned LoadCount(const unsigned* c) {
+    return __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned TileWorkBucket(const BinParams& p, unsigned t, unsigned large) {
+    const unsigned cnt = LoadCount(&p.counts[t]);
+    if (p.tile_info[t].usable == 0u || cnt > p.capacity) {
+        return 63u;
+    }
+    const unsigned total = cnt + large;
+    return total == 0u ? 0u : 32u - __builtin_clz(total);
+}
+// One block of any size computes the whole order.
+__device__ void TileOrderBlock(const BinParams& p) {
+    __shared__ unsigned start[64];
+    const int tid = threadIdx.x;
+    const unsigned nthreads = blockDim.x;
+    const unsigned tiles = static_cast<unsigned>(p.tiles_x * p.tiles_y);
+    const unsigned large = LoadCount(&p.counts[tiles]);
+    if (tid < 64) {
+        start[tid] = 0u;
+    }
+    __syncthreads();
+    for (unsigned t = tid; t < tiles; t += nthreads) {
+        atomicAdd(&start[TileWorkBucket(p, t, large)], static_cast<unsigned>(kParts));
+    }
+    __syncthreads();
+    unsigned first = 0u;  // tiles in heavier buckets
+    if (tid < 64) {
+        for (int b = 63; b > tid; --b) {
+            first += start[b];
+        }
+    }
+    __syncthreads();
+    if (tid < 64) {
+        start[tid] = first;
+    }
+    __syncthreads();
+    for (unsigned t = tid; t < tiles; t += nthreads) {
+        const unsigned at = atomicAdd(&start[TileWorkBucket(p, t, large)], static_cast<unsigned>(kParts));
+        for (int part = 0; part < kParts; ++part) {
+            p.tile_order[at + part] = t * kParts + part;  // trace work items (tile, part)
+        }
+    }
+}
+
 __global__ __launch_bounds__(kBinThreads) void BinTrianglesKernel(BinParams p) {
     __shared__ float2 b[kMaxBoundTiles];
-    __shared__ unsigned hist[kMaxBinTiles];  // prologue: ordered-bit bounds scratch
+    __shared__ unsigned hist[kMaxBinTiles];
     const int tid = threadIdx.x;
-    const int lane = tid & (kWave - 1);
-    const int wave = tid / kWave;
     const int nx = p.tiles_x, ny = p.tiles_y;
     const int tiles = nx * ny;
 
     // Prologue: monotone tile-column and tile-row bounds of the usable tiles' boxes
-    // (lo' = suffix minimum, hi' = prefix maximum; both nondecreasing).
-    unsigned* col_lo = hist;
-    unsigned* col_hi = hist + nx;
-    unsigned* row_lo = hist + 2 * nx;
-    unsigned* row_hi = hist + 2 * nx + ny;
-    for (int i = tid; i < nx + ny; i += kBinThreads) {
-        const bool col = i < nx;
-        const int j = col ? i : i - nx;
-        (col ? col_lo : row_lo)[j] = OrderedBits(__builtin_inff());
-        (col ? col_hi : row_hi)[j] = OrderedBits(-__builtin_inff());
-    }
-    __syncthreads();
-    for (int t = tid; t < tiles; t += kBinThreads) {
-        const TileInfo ti = p.tile_info[t];
-        if (ti.usable != 0u && ti.box.x <= ti.box.y && ti.box.z <= ti.box.w) {
-            const int c = t % nx, r = t / nx;
-            atomicMin(&col_lo[c], OrderedBits(ti.box.x));
-            atomicMax(&col_hi[c], OrderedBits(ti.box.y));
-            atomicMin(&row_lo[r], OrderedBits(ti.box.z));
-            atomicMax(&row_hi[r], OrderedBits(ti.box.w));
+    // (lo' = suffix minimum, hi' = prefix maximum; both nondecreasing). Every block reduces
+    // the tile infos itself (reading 32 B per tile from L2): cheaper than device-scope
+    // atomics on a few shared addresses, which serialise at the memory side.
+    {
+        const int lane = tid & (kWave - 1);
+        const int wave = tid / kWave;
+        unsigned* col_lo = hist;
+        unsigned* col_hi = hist + nx;
+        unsigned* row_lo = hist + 2 * nx;
+        unsigned* row_hi = hist + 2 * nx + ny;
+        for (int i = tid; i < nx + ny; i += kBinThreads) {
+            const bool col = i < nx;
+            const int j = col ? i : i - nx;
+            (col ? col_lo : row_lo)[j] = OrderedBits(__builtin_inff());
+            (col ? col_hi : row_hi)[j] = OrderedBits(-__builtin_inff());
         }
+        __syncthreads();
+        for (int t = tid; t < tiles; t += kBinThreads) {
+            const float4 tb = p.tile_info[t].box;
+            if (p.tile_info[t].usable != 0u && tb.x <= tb.y && tb.z <= tb.w) {
+                const int c = t % nx, r = t / nx;
+                atomicMin(&col_lo[c], OrderedBits(tb.x));
+                atomicMax(&col_hi[c], OrderedBits(tb.y));
+                atomicMin(&row_lo[r], OrderedBits(tb.z));
+                atomicMax(&row_hi[r], OrderedBits(tb.w));
+            }
+        }
+        __syncthreads();
+        if (wave == 0) {
+            WaveScanOrdered<false>(col_lo, nx, true, lane);
+        } else if (wave == 1) {
+            WaveScanOrdered<true>(col_hi, nx, false, lane);
+        } else if (wave == 2) {
+            WaveScanOrdered<false>(row_lo, ny, true, lane);
+        } else {
+            WaveScanOrdered<true>(row_hi, ny, false, lane);
+        }
+        __syncthreads();
+        for (int i = tid; i < nx + ny; i += kBinThreads) {
+            const bool col = i < nx;
+            const int j = col ? i : i - nx;
+            b[i] = make_float2(FromOrderedBits(col ? col_lo[j] : row_lo[j]),
+                               FromOrderedBits(col ? col_hi[j] : row_hi[j]));
+        }
+        __syncthreads();
     }
-    __syncthreads();
-    if (wave == 0) {
-        WaveScanOrdered<false>(col_lo, nx, true, lane);
-    } else if (wave == 1) {
-        WaveScanOrdered<true>(col_hi, nx, false, lane);
-    } else if (wave == 2) {
-        WaveScanOrdered<false>(row_lo, ny, true, lane);
-    } else {
-        WaveScanOrdered<true>(row_hi, ny, false, lane);
-    }
-    __syncthreads();
-    for (int i = tid; i < nx + ny; i += kBinThreads) {
-        const bool col = i < nx;
-        const int j = col ? i : i - nx;
-        b[i] = make_float2(FromOrderedBits(col ? col_lo[j] : row_lo[j]), FromOrderedBits(col ? col_hi[j] : row_hi[j]));
-    }
-    __syncthreads();
     for (int t = tid; t < tiles; t += kBinThreads) {
         hist[t] = 0u;
     }
@@ -1684,51 +1771,31 @@ __global__ __launch_bounds__(kBinThreads) void BinTrianglesKernel(BinParams p) {
             p.lists[static_cast<size_t>(t) * p.capacity + at] = i;
         }
     }
+    // The last block to finish computes the trace launch order from the final list counts.
+    // Every count update of a block is an atomic whose returned value the block consumed
+    // before this barrier, so it has been performed at the device coherence point; the last
+    // block reads the counts with device-scope atomic loads (no L2-wide fences needed).
+    __shared__ unsigned last;
+    if (p.order_in_bin == 0u) {
+        return;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        last = atomicAdd(&p.sync[0], 1u) == gridDim.x - 1u ? 1u : 0u;
+    }
+    __syncthreads();
+    if (last != 0u) {
+        TileOrderBlock(p);
+        if (tid == 0) {
+            p.sync[0] = 0u;  // ready for the next frame (the kernel boundary orders it)
+        }
+    }
 }
 
-// Longest-processing-time-first launch order of the trace blocks: tiles sorted by their work,
-// descending (FULL-stream tiles first, then by the log2 of their candidate count), so the
-// heavy tiles start first and the light ones fill in behind them. One block; a counting sort
-// over 64 buckets (order within a bucket arbitrary: the frame does not depend on it).
-constexpr int kOrderThreads = 1024;
-__device__ __forceinline__ unsigned TileWorkBucket(const BinParams& p, unsigned t, unsigned large) {
-    const unsigned cnt = p.counts[t];
-    if (p.tile_info[t].usable == 0u || cnt > p.capacity) {
-        return 63u;
-    }
-    const unsigned total = cnt + large;
-    return total == 0u ? 0u : 32u - __builtin_clz(total);
-}
+// Standalone order (a band with no records: the bin kernel, which normally computes the
+// order in its last block, is not launched).
 __global__ __launch_bounds__(kOrderThreads) void TileOrderKernel(BinParams p) {
-    __shared__ unsigned start[64];
-    const int tid = threadIdx.x;
-    const unsigned tiles = static_cast<unsigned>(p.tiles_x * p.tiles_y);
-    const unsigned large = p.counts[tiles];
-    if (tid < 64) {
-        start[tid] = 0u;
-    }
-    __syncthreads();
-    for (unsigned t = tid; t < tiles; t += kOrderThreads) {
-        atomicAdd(&start[TileWorkBucket(p, t, large)], static_cast<unsigned>(kParts));
-    }
-    __syncthreads();
-    unsigned first = 0u;  // tiles in heavier buckets
-    if (tid < 64) {
-        for (int b = 63; b > tid; --b) {
-            first += start[b];
-        }
-    }
-    __syncthreads();
-    if (tid < 64) {
-        start[tid] = first;
-    }
-    __syncthreads();
-    for (unsigned t = tid; t < tiles; t += kOrderThreads) {
-        const unsigned at = atomicAdd(&start[TileWorkBucket(p, t, large)], static_cast<unsigned>(kParts));
-        for (int part = 0; part < kParts; ++part) {
-            p.tile_order[at + part] = t * kParts + part;  // trace work items (tile, part)
-        }
-    }
+    TileOrderBlock(p);
 }
 
 // Candidate source of a tile: LIST (binned, usable box, list complete): the tile's list then
@@ -1879,6 +1946,12 @@ __global__ __launch_bounds__(kWave * W, 4) void TraceCullKernel(TraceParams p) {
     ShadeAndStore<R>(p, x, y0, s);
 }
 
+// Boolean env switch ("0" = off), for measurement of alternatives.
+bool EnvFlag(const char* name, bool dflt) {
+    const char* v = std::getenv(name);
+    return v == nullptr || *v == '\0' ? dflt : std::strcmp(v, "0") != 0;
+}
+
 // Waves per trace block; env SRT_CULL_WAVES = 4, 8 or 16 (default 4), for measurement.
 int CullWavesFromEnv() {
     const char* v = std::getenv("SRT_CULL_WAVES");
@@ -1886,6 +1959,17 @@ int CullWavesFromEnv() {
         return std::atoi(v);
     }
     return 4;
+}
+
+// Launch on `stream`; with timing events, through hipExtLaunchKernelGGL so that the events
+// take the dispatch packet's own start / end timestamps (no extra stream packets).
+template <class K, class P>
+void Launch(K kernel, dim3 grid, dim3 block, hipStream_t stream, hipEvent_t start, hipEvent_t stop, const P& p) {
+    if (start != nullptr || stop != nullptr) {
+        hipExtLaunchKernelGGL(kernel, grid, block, 0, stream, start, stop, 0, p);
+    } else {
+        hipLaunchKernelGGL(kernel, grid, block, 0, stream, p);
+    }
 }
 
 }  // namespace
@@ -1896,8 +1980,9 @@ hipError_t DiagRead(void* host, std::size_t bytes) {
 }
 #endif
 
-hipError_t LaunchPrepare(const float* d_vertices, const unsigned* d_rank, std::uint64_t n, const Frame& frame,
-                         float* d_edges, hipStream_t stream) {
+namespace {
+PrepareParams MakePrepareParams(const float* d_vertices, const unsigned* d_rank, std::uint64_t n, const Frame& frame,
+                                float* d_edges) {
     PrepareParams p{};
     p.vertices = d_vertices;
     p.rank = d_rank;
@@ -1913,8 +1998,15 @@ hipError_t LaunchPrepare(const float* d_vertices, const unsigned* d_rank, std::u
         p.du[k] = frame.du[k];
         p.dv[k] = frame.dv[k];
     }
+    return p;
+}
+}  // namespace
+
+hipError_t LaunchPrepare(const float* d_vertices, const unsigned* d_rank, std::uint64_t n, const Frame& frame,
+                         float* d_edges, hipStream_t stream, hipEvent_t ev_begin, hipEvent_t ev_end) {
+    const PrepareParams p = MakePrepareParams(d_vertices, d_rank, n, frame, d_edges);
     const unsigned blocks = (p.n_pad + 255) / 256;
-    hipLaunchKernelGGL(PrepareKernel, dim3(blocks), dim3(256), 0, stream, p);
+    Launch(PrepareKernel, dim3(blocks), dim3(256), stream, ev_begin, ev_end, p);
     return hipGetLastError();
 }
 
@@ -1943,7 +2035,7 @@ unsigned CullBinCapacity(std::uint64_t n, std::size_t tiles) {
 
 namespace {
 struct BinSizes {
-    std::size_t info, counts, lists, large, order;
+    std::size_t info, counts, lists, large, order, sync;
 };
 BinSizes CullBinSizes(std::uint64_t n, std::size_t width, std::size_t row_count) {
     const std::size_t tx = (width + kWave - 1) / kWave, ty = (row_count + kTileRows - 1) / kTileRows;
@@ -1955,13 +2047,14 @@ BinSizes CullBinSizes(std::uint64_t n, std::size_t width, std::size_t row_count)
     z.lists = al(tiles * static_cast<std::size_t>(CullBinCapacity(n, tiles)) * 4);
     z.large = al(PaddedTriangleCount(n) * 4);
     z.order = al(tiles * kParts * 4);
+    z.sync = al(4);
     return z;
 }
 }  // namespace
 
 std::size_t CullBinBytes(std::uint64_t n, std::size_t width, std::size_t row_count) {
     const BinSizes z = CullBinSizes(n, width, row_count);
-    return z.info + z.counts + z.lists + z.large + z.order;
+    return z.info + z.counts + z.lists + z.large + z.order + z.sync;
 }
 
 CullBins CullBinLayout(void* base, std::uint64_t n, std::size_t width, std::size_t row_count) {
@@ -1977,6 +2070,8 @@ CullBins CullBinLayout(void* base, std::uint64_t n, std::size_t width, std::size
     b.large_list = reinterpret_cast<unsigned*>(w);
     w += z.large;
     b.tile_order = reinterpret_cast<unsigned*>(w);
+    w += z.order;
+    b.sync = reinterpret_cast<unsigned*>(w);
     b.tiles = CullTiles(width, row_count);
     b.capacity = CullBinCapacity(n, b.tiles);
     return b;
@@ -1984,13 +2079,17 @@ CullBins CullBinLayout(void* base, std::uint64_t n, std::size_t width, std::size
 
 hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_vertices, const float* d_albedo,
                        const Frame& frame, const float background[3], const BandArgs& band, int variant,
-                       const CullBins* bins, hipStream_t stream, const StageEvents* events) {
+                       const CullBins* bins, hipStream_t stream, const StageEvents* events,
+                       const unsigned* prepare_rank) {
     if (band.row_count == 0 || band.width == 0) {
         return hipSuccess;
     }
     const StageEvents ev = events != nullptr ? *events : StageEvents{};
-    if (ev.bin != nullptr) {
-        const hipError_t e = hipEventRecord(ev.bin, stream);
+    const bool fuse_prepare =
+        prepare_rank != nullptr && variant == kTraceCull && bins != nullptr && EnvFlag("SRT_FUSE_PREPARE", true);
+    if (prepare_rank != nullptr && !fuse_prepare) {
+        const hipError_t e = LaunchPrepare(d_vertices, prepare_rank, n, frame, const_cast<float*>(d_edges), stream,
+                                           ev.prep_begin, ev.prep_end);
         if (e != hipSuccess) {
             return e;
         }
@@ -2022,15 +2121,9 @@ hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_ver
         p.bg[k] = background[k];
     }
     const unsigned gx = static_cast<unsigned>((band.width + kWave - 1) / kWave);
-    auto mark = [&](hipEvent_t e) {
-        if (e != nullptr) {
-            (void)hipEventRecord(e, stream);
-        }
-    };
     if (variant == kTraceScalar) {
         const unsigned gy = static_cast<unsigned>((band.row_count + kRowsPerLane - 1) / kRowsPerLane);
-        mark(ev.begin);
-        hipLaunchKernelGGL(TraceScalarKernel, dim3(gx, gy), dim3(kWave), 0, stream, p);
+        Launch(TraceScalarKernel, dim3(gx, gy), dim3(kWave), stream, ev.begin, ev.end, p);
     } else if (variant == kTraceCull) {
         const unsigned gy = static_cast<unsigned>((band.row_count + kTileRows - 1) / kTileRows);
         if (bins != nullptr) {
@@ -2045,6 +2138,7 @@ hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_ver
             b.lists = bins->lists;
             b.large_list = bins->large_list;
             b.tile_order = bins->tile_order;
+            b.sync = bins->sync;
             b.capacity = bins->capacity;
             b.n = static_cast<unsigned>(n);
             b.tiles_x = static_cast<int>(gx);
@@ -2060,12 +2154,26 @@ hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_ver
                 p.exp = b.exp;
             }
 #endif
-            hipLaunchKernelGGL(TileInfoKernel, dim3(gx, gy), dim3(kBinThreads), 0, stream, b);
+            if (fuse_prepare) {
+                PrepareInfoParams f{};
+                f.prep = MakePrepareParams(d_vertices, prepare_rank, n, frame, const_cast<float*>(d_edges));
+                f.bin = b;
+                f.prep_blocks = (f.prep.n_pad + kBinThreads - 1) / kBinThreads;
+                Launch(PrepareInfoKernel, dim3(f.prep_blocks + gx * gy), dim3(kBinThreads), stream, ev.prep_begin,
+                       ev.prep_end, f);
+            } else {
+                Launch(TileInfoKernel, dim3(gx, gy), dim3(kBinThreads), stream, ev.prep_begin, ev.prep_end, b);
+            }
+            b.order_in_bin = n != 0 && EnvFlag("SRT_ORDER_IN_BIN", false) ? 1u : 0u;
             if (n != 0) {
                 const unsigned blocks = static_cast<unsigned>((n + kBinThreads - 1) / kBinThreads);
-                hipLaunchKernelGGL(BinTrianglesKernel, dim3(blocks), dim3(kBinThreads), 0, stream, b);
+                Launch(BinTrianglesKernel, dim3(blocks), dim3(kBinThreads), stream, ev.bin_begin,
+                       b.order_in_bin != 0u ? ev.bin_end : nullptr, b);
             }
-            hipLaunchKernelGGL(TileOrderKernel, dim3(1), dim3(kOrderThreads), 0, stream, b);
+            if (b.order_in_bin == 0u) {
+                Launch(TileOrderKernel, dim3(1), dim3(kOrderThreads), stream, n != 0 ? nullptr : ev.bin_begin,
+                       ev.bin_end, b);
+            }
             p.tile_info = b.tile_info;
             p.order = bins->order;
             p.tile_order = bins->tile_order;
@@ -2076,23 +2184,17 @@ hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_ver
         }
         // One block per (tile, part): gridDim.x = tile columns, gridDim.y = tile rows x parts.
         const dim3 grid(gx, gy * kParts);
-        mark(ev.begin);
         switch (CullWavesFromEnv()) {
-            case 8: hipLaunchKernelGGL(TraceCullKernel<8>, grid, dim3(kWave * 8), 0, stream, p); break;
-            case 16: hipLaunchKernelGGL(TraceCullKernel<16>, grid, dim3(kWave * 16), 0, stream, p); break;
-            default: hipLaunchKernelGGL(TraceCullKernel<4>, grid, dim3(kWave * 4), 0, stream, p); break;
+            case 8: Launch(TraceCullKernel<8>, grid, dim3(kWave * 8), stream, ev.begin, ev.end, p); break;
+            case 16: Launch(TraceCullKernel<16>, grid, dim3(kWave * 16), stream, ev.begin, ev.end, p); break;
+            default: Launch(TraceCullKernel<4>, grid, dim3(kWave * 4), stream, ev.begin, ev.end, p); break;
         }
     } else {
         constexpr int kRowsPerBlock = kRowsPerLane * kLdsWaves;
         const unsigned gy = static_cast<unsigned>((band.row_count + kRowsPerBlock - 1) / kRowsPerBlock);
-        mark(ev.begin);
-        hipLaunchKernelGGL(TraceLdsKernel, dim3(gx, gy), dim3(kWave * kLdsWaves), 0, stream, p);
+        Launch(TraceLdsKernel, dim3(gx, gy), dim3(kWave * kLdsWaves), stream, ev.begin, ev.end, p);
     }
-    const hipError_t launch = hipGetLastError();
-    if (launch != hipSuccess) {
-        return launch;
-    }
-    return ev.end != nullptr ? hipEventRecord(ev.end, stream) : hipSuccess;
+    return hipGetLastError();
 }
 
 }  // namespace srt

@@ -146,10 +146,11 @@ DeviceScene::~DeviceScene() {
     (void)hipFree(m_order);
     (void)hipFree(m_rank);
     (void)hipFree(m_cull_work);
-    for (auto& e : m_events) {
-        for (hipEvent_t x : e) {
-            (void)hipEventDestroy(x);
-        }
+    for (hipEvent_t e : m_events) {
+        (void)hipEventDestroy(e);
+    }
+    for (hipEvent_t e : m_prep_events) {
+        (void)hipEventDestroy(e);
     }
     if (prev >= 0) {
         (void)hipSetDevice(prev);
@@ -163,7 +164,10 @@ void DeviceScene::Prepare(std::size_t width, std::size_t height, hipStream_t str
     m_frame = MakeFrame(m_camera, width, height);
     m_width = width;
     m_height = height;
-    HipCheck(LaunchPrepare(m_vertices, m_rank, m_n, m_frame, m_edges, stream), "prepare kernel launch");
+    // Deferred: the next Trace enqueues the record setup on its stream, fused with its first
+    // bin kernel when it bins (render.hip PrepareInfoKernel).
+    (void)stream;
+    m_prepare_pending = true;
 }
 
 void DeviceScene::Trace(const float* d_offsets, float* d_rgba, std::size_t row_begin, std::size_t row_count,
@@ -199,21 +203,40 @@ void DeviceScene::Trace(const float* d_offsets, float* d_rgba, std::size_t row_b
         bins.order = m_order;
         use_bins = &bins;
     }
+    const bool prepare = m_prepare_pending && row_count != 0;
     StageEvents ev{};
+    if (m_timing && prepare) {
+        ev.prep_begin = TimingEvent(m_prep_events, 2 * m_prep_timed);
+        ev.prep_end = TimingEvent(m_prep_events, 2 * m_prep_timed + 1);
+        ++m_prep_timed;
+    }
     if (m_timing) {
-        if (m_timed == m_events.size()) {
-            std::array<hipEvent_t, 3> e{};
-            for (auto& x : e) {
-                HipCheck(hipEventCreate(&x), "hipEventCreate(stage timing)");
-            }
-            m_events.push_back(e);
+        const std::size_t k = 4 * m_timed;
+        ev.bin_begin = use_bins != nullptr ? TimingEvent(m_events, k) : nullptr;
+        ev.bin_end = use_bins != nullptr ? TimingEvent(m_events, k + 1) : nullptr;
+        ev.begin = TimingEvent(m_events, k + 2);
+        ev.end = TimingEvent(m_events, k + 3);
+        if (m_binned.size() <= m_timed) {
+            m_binned.resize(m_timed + 1);
         }
-        const auto& e = m_events[m_timed++];
-        ev = StageEvents{e[0], e[1], e[2]};
+        m_binned[m_timed] = use_bins != nullptr;
+        ++m_timed;
     }
     HipCheck(LaunchTrace(m_edges, m_n, m_vertices, m_albedo, m_frame, m_background, band, variant, use_bins, stream,
-                         m_timing ? &ev : nullptr),
+                         m_timing ? &ev : nullptr, prepare ? m_rank : nullptr),
              "trace kernel launch");
+    if (prepare) {
+        m_prepare_pending = false;
+    }
+}
+
+hipEvent_t DeviceScene::TimingEvent(std::vector<hipEvent_t>& pool, std::size_t i) const {
+    while (pool.size() <= i) {
+        hipEvent_t e = nullptr;
+        HipCheck(hipEventCreate(&e), "hipEventCreate(stage timing)");
+        pool.push_back(e);
+    }
+    return pool[i];
 }
 
 void DeviceScene::SetTiming(bool on) {
@@ -221,21 +244,29 @@ void DeviceScene::SetTiming(bool on) {
 }
 
 DeviceScene::StageTimes DeviceScene::TakeTimes() {
+    auto elapsed = [](hipEvent_t a, hipEvent_t b) {
+        HipCheck(hipEventSynchronize(b), "hipEventSynchronize(stage timing)");
+        float ms = 0.f;
+        HipCheck(hipEventElapsedTime(&ms, a, b), "hipEventElapsedTime(stage timing)");
+        return static_cast<double>(ms);
+    };
     StageTimes t;
+    for (std::size_t i = 0; i < m_prep_timed; ++i) {
+        t.prepare_ms += elapsed(m_prep_events[2 * i], m_prep_events[2 * i + 1]);
+    }
+    std::size_t binned = 0;
     for (std::size_t i = 0; i < m_timed; ++i) {
-        const auto& e = m_events[i];
-        HipCheck(hipEventSynchronize(e[2]), "hipEventSynchronize(stage timing)");
-        float bin = 0.f, kernel = 0.f;
-        HipCheck(hipEventElapsedTime(&bin, e[0], e[1]), "hipEventElapsedTime(bin)");
-        HipCheck(hipEventElapsedTime(&kernel, e[1], e[2]), "hipEventElapsedTime(trace)");
-        t.bin_ms += bin;
-        t.kernel_ms += kernel;
+        if (m_binned[i]) {
+            t.bin_ms += elapsed(m_events[4 * i], m_events[4 * i + 1]);
+            ++binned;
+        }
+        t.kernel_ms += elapsed(m_events[4 * i + 2], m_events[4 * i + 3]);
     }
     t.launches = static_cast<unsigned>(m_timed);
-    if (m_timed != 0) {
-        t.bin_ms /= static_cast<double>(m_timed);
-        t.kernel_ms /= static_cast<double>(m_timed);
-    }
+    t.prepare_ms /= m_prep_timed != 0 ? static_cast<double>(m_prep_timed) : 1.0;
+    t.bin_ms /= binned != 0 ? static_cast<double>(binned) : 1.0;
+    t.kernel_ms /= m_timed != 0 ? static_cast<double>(m_timed) : 1.0;
+    m_prep_timed = 0;
     m_timed = 0;
     return t;
 }

@@ -8,7 +8,6 @@
 #include <hip/hip_runtime.h>
 
 #include <cstddef>
-#include <array>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -38,7 +37,8 @@ public:
     const Camera& camera() const { return m_camera; }
     const float* background() const { return m_background; }
 
-    // Edge setup for a W x H frame (stream-ordered). Records stay valid until the next call.
+    // Edge setup for a W x H frame. The records are computed by the next Trace, on its stream
+    // (fused into its first kernel); they stay valid until the next Prepare.
     void Prepare(std::size_t width, std::size_t height, hipStream_t stream);
     // Trace rows [row_begin, row_begin + row_count) of the prepared frame.
     void Trace(const float* d_offsets, float* d_rgba, std::size_t row_begin, std::size_t row_count, int variant,
@@ -47,13 +47,14 @@ public:
     std::size_t width() const { return m_width; }
     std::size_t height() const { return m_height; }
 
-    // Stage timing: while on, every Trace records HIP events on its stream before the cull bin
-    // kernels and around the trace kernel itself. TakeTimes waits for them and returns the mean
-    // durations (ms) of the Trace calls timed since the previous TakeTimes, then forgets them.
+    // Stage timing: while on, Prepare and Trace bind HIP events to their kernels' dispatch
+    // packets (render.h StageEvents). TakeTimes waits for them and returns the mean durations
+    // (ms) of the calls timed since the previous TakeTimes, then forgets them.
     struct StageTimes {
-        unsigned launches = 0;
-        double bin_ms = 0.0;     // bin stage (cull: TileInfo + BinTriangles + TileOrder); 0 otherwise
-        double kernel_ms = 0.0;  // the trace kernel alone
+        unsigned launches = 0;     // timed Trace calls
+        double prepare_ms = 0.0;   // PrepareKernel (mean over timed Prepare calls)
+        double bin_ms = 0.0;       // bin stage (cull: TileInfo start .. TileOrder end); 0 otherwise
+        double kernel_ms = 0.0;    // the trace kernel alone
     };
     void SetTiming(bool on);
     StageTimes TakeTimes();
@@ -76,9 +77,15 @@ private:
     mutable unsigned char* m_cull_work = nullptr;
     mutable std::size_t m_cull_bytes = 0;
     mutable std::uint64_t m_cull_shape = 0;  // (width << 32) | rows of the current carve-up
-    // Stage-timing event triples (bin, begin, end), reused; m_timed of them hold a pending launch.
+    // Stage-timing events, reused: per timed Prepare (begin, end), per timed Trace (bin begin,
+    // bin end, begin, end); the first m_prep_timed / m_timed entries hold pending launches.
+    hipEvent_t TimingEvent(std::vector<hipEvent_t>& pool, std::size_t i) const;
     bool m_timing = false;
-    mutable std::vector<std::array<hipEvent_t, 3>> m_events;
+    mutable std::vector<hipEvent_t> m_prep_events;
+    mutable std::vector<hipEvent_t> m_events;
+    mutable std::vector<bool> m_binned;
+    mutable std::size_t m_prep_timed = 0;
+    mutable bool m_prepare_pending = false;
     mutable std::size_t m_timed = 0;
 };
 

@@ -1,10 +1,16 @@
-#include <algorithm>
 #include "scene.h"
 
+#include <algorithm>
+#include <array>
+#include <cctype>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <fstream>
+#include <map>
 #include <memory>
+#include <sstream>
 #include <stdexcept>
 
 namespace srt {
@@ -138,9 +144,205 @@ Scene MakeSoup(std::uint64_t n, std::uint64_t seed, float size) {
     return s;
 }
 
+[[noreturn]] void ObjError(const std::string& path, std::size_t line, const std::string& what) {
+    throw std::runtime_error("Error reading scene file: " + path + ": line " + std::to_string(line) + ": " + what);
+}
+
+bool EndsWithObj(const std::string& path) {
+    if (path.size() < 4) {
+        return false;
+    }
+    std::string ext = path.substr(path.size() - 4);
+    for (char& c : ext) {
+        c = static_cast<char>(std::tolower(static_cast<unsigned char>(c)));
+    }
+    return ext == ".obj";
+}
+
+// Parses `count` floats from the rest of a line; false if fewer are present or one is malformed.
+bool ReadFloats(std::istringstream& in, float* out, int count) {
+    for (int k = 0; k < count; ++k) {
+        std::string tok;
+        if (!(in >> tok)) {
+            return false;
+        }
+        char* end = nullptr;
+        out[k] = std::strtof(tok.c_str(), &end);
+        if (end == tok.c_str() || *end != '\0') {
+            return false;
+        }
+    }
+    return true;
+}
+
+// Diffuse colours (Kd) of the materials of an .mtl file; a missing file yields none.
+std::map<std::string, std::array<float, 3>> ReadMtl(const std::string& path) {
+    std::map<std::string, std::array<float, 3>> out;
+    std::ifstream f(path);
+    std::string line, current;
+    while (std::getline(f, line)) {
+        std::istringstream in(line);
+        std::string key;
+        if (!(in >> key)) {
+            continue;
+        }
+        if (key == "newmtl") {
+            in >> current;
+            out[current] = {0.8f, 0.8f, 0.8f};
+        } else if (key == "Kd" && !current.empty()) {
+            float kd[3];
+            if (ReadFloats(in, kd, 3)) {
+                out[current] = {kd[0], kd[1], kd[2]};
+            }
+        }
+    }
+    return out;
+}
+
+// Wavefront OBJ subset: `v x y z [w]`, `f a b c ...` with `i`, `i/t`,
+// `i//n`, `i/t/n` and negative (relative) indices, polygons fan-triangulated (v0, vk, vk+1);
+// `mtllib` + `usemtl` give per-face albedo from the materials' Kd (default 0.8 grey);
+// every other statement (vt, vn, o, g, s, l, p, ...) is ignored. Two comment directives set
+// what OBJ cannot express: `# srt camera ex ey ez lx ly lz ux uy uz vfov_deg` and
+// `# srt background r g b`. Without a camera directive the camera looks along +z at the
+// centre of the bounding box from where the box's bounding sphere fills a 60-degree view.
+Scene LoadObj(const std::string& path) {
+    std::ifstream f(path);
+    if (!f) {
+        throw std::runtime_error("Error reading scene file: " + path + ": cannot open");
+    }
+    const std::string dir = path.find('/') == std::string::npos ? "" : path.substr(0, path.rfind('/') + 1);
+    std::vector<float> pos;  // 3 per vertex
+    std::map<std::string, std::array<float, 3>> materials;
+    std::array<float, 3> albedo = {0.8f, 0.8f, 0.8f};
+    Scene s;
+    bool have_camera = false;
+    std::string line;
+    std::size_t lineno = 0;
+    while (std::getline(f, line)) {
+        ++lineno;
+        if (!line.empty() && line.back() == '\r') {
+            line.pop_back();
+        }
+        std::istringstream in(line);
+        std::string key;
+        if (!(in >> key)) {
+            continue;
+        }
+        if (key[0] == '#') {
+            std::string tag, what;
+            std::istringstream c(line.substr(line.find('#') + 1));
+            if ((c >> tag >> what) && tag == "srt") {
+                if (what == "camera") {
+                    float cam[10];
+                    if (!ReadFloats(c, cam, 10)) {
+                        ObjError(path, lineno, "srt camera needs 10 numbers");
+                    }
+                    std::memcpy(s.camera.eye, cam, 3 * sizeof(float));
+                    std::memcpy(s.camera.lookat, cam + 3, 3 * sizeof(float));
+                    std::memcpy(s.camera.up, cam + 6, 3 * sizeof(float));
+                    s.camera.vfov_deg = cam[9];
+                    have_camera = true;
+                } else if (what == "background") {
+                    if (!ReadFloats(c, s.background, 3)) {
+                        ObjError(path, lineno, "srt background needs 3 numbers");
+                    }
+                } else {
+                    ObjError(path, lineno, "unknown srt directive '" + what + "'");
+                }
+            }
+            continue;
+        }
+        if (key == "v") {
+            float v[3];
+            if (!ReadFloats(in, v, 3)) {
+                ObjError(path, lineno, "vertex needs 3 coordinates");
+            }
+            pos.insert(pos.end(), v, v + 3);
+        } else if (key == "f") {
+            std::vector<std::uint64_t> idx;
+            std::string tok;
+            const long long nv = static_cast<long long>(pos.size() / 3);
+            while (in >> tok) {
+                char* end = nullptr;
+                const long long i = std::strtoll(tok.c_str(), &end, 10);
+                if (end == tok.c_str() || (*end != '\0' && *end != '/')) {
+                    ObjError(path, lineno, "bad face index '" + tok + "'");
+                }
+                const long long r = i > 0 ? i - 1 : nv + i;  // 1-based, or relative when negative
+                if (i == 0 || r < 0 || r >= nv) {
+                    ObjError(path, lineno, "face index " + std::to_string(i) + " out of range (" +
+                                               std::to_string(nv) + " vertices so far)");
+                }
+                idx.push_back(static_cast<std::uint64_t>(r));
+            }
+            if (idx.size() < 3) {
+                ObjError(path, lineno, "face needs at least 3 vertices");
+            }
+            for (std::size_t k = 1; k + 1 < idx.size(); ++k) {
+                const std::uint64_t c[3] = {idx[0], idx[k], idx[k + 1]};
+                for (std::uint64_t v : c) {
+                    s.vertices.insert(s.vertices.end(), pos.begin() + 3 * v, pos.begin() + 3 * v + 3);
+                }
+                s.albedo.insert(s.albedo.end(), albedo.begin(), albedo.end());
+            }
+        } else if (key == "mtllib") {
+            std::string name;
+            while (in >> name) {
+                for (const auto& m : ReadMtl(dir + name)) {
+                    materials[m.first] = m.second;
+                }
+            }
+        } else if (key == "usemtl") {
+            std::string name;
+            in >> name;
+            const auto it = materials.find(name);
+            albedo = it != materials.end() ? it->second : std::array<float, 3>{0.8f, 0.8f, 0.8f};
+        }
+    }
+    if (s.vertices.empty()) {
+        throw std::runtime_error("Error reading scene file: " + path + ": no faces");
+    }
+    if (s.triangle_count() > (1ULL << 31)) {
+        throw std::runtime_error("Error reading scene file: " + path + ": too many triangles");
+    }
+    if (!have_camera) {
+        double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
+        for (std::size_t i = 0; i < s.vertices.size(); i += 3) {
+            for (int k = 0; k < 3; ++k) {
+                if (std::isfinite(s.vertices[i + k])) {
+                    lo[k] = std::fmin(lo[k], s.vertices[i + k]);
+                    hi[k] = std::fmax(hi[k], s.vertices[i + k]);
+                }
+            }
+        }
+        if (!(lo[0] <= hi[0] && lo[1] <= hi[1] && lo[2] <= hi[2])) {
+            throw std::runtime_error("Error reading scene file: " + path + ": no finite vertices");
+        }
+        const double c[3] = {(lo[0] + hi[0]) / 2, (lo[1] + hi[1]) / 2, (lo[2] + hi[2]) / 2};
+        const double r = 0.5 * std::sqrt((hi[0] - lo[0]) * (hi[0] - lo[0]) + (hi[1] - lo[1]) * (hi[1] - lo[1]) +
+                                         (hi[2] - lo[2]) * (hi[2] - lo[2]));
+        const double dist = (r > 0.0 ? r : 1.0) / std::sin(30.0 * 3.14159265358979323846 / 180.0);
+        const float cam[10] = {static_cast<float>(c[0]), static_cast<float>(c[1]), static_cast<float>(c[2] - dist),
+                               static_cast<float>(c[0]), static_cast<float>(c[1]), static_cast<float>(c[2]),
+                               0.f, 1.f, 0.f, 60.f};
+        std::memcpy(s.camera.eye, cam, 3 * sizeof(float));
+        std::memcpy(s.camera.lookat, cam + 3, 3 * sizeof(float));
+        std::memcpy(s.camera.up, cam + 6, 3 * sizeof(float));
+        s.camera.vfov_deg = cam[9];
+    }
+    if (!(s.camera.vfov_deg > 0.f && s.camera.vfov_deg < 180.f)) {
+        throw std::runtime_error("Error reading scene file: " + path + ": bad camera vfov");
+    }
+    return s;
+}
+
 }  // namespace
 
 Scene LoadScene(const std::string& path) {
+    if (EndsWithObj(path)) {
+        return LoadObj(path);
+    }
     File f(std::fopen(path.c_str(), "rb"));
     if (!f) {
         throw std::runtime_error("Error reading scene file: " + path + ": cannot open");
@@ -173,6 +375,13 @@ Scene LoadScene(const std::string& path) {
         std::fread(s.albedo.data(), sizeof(float), s.albedo.size(), f.get()) != s.albedo.size()) {
         throw std::runtime_error("Error reading scene file: " + path + ": truncated triangle data");
     }
+    if (std::fgetc(f.get()) != EOF) {
+        throw std::runtime_error("Error reading scene file: " + path + ": trailing bytes after the triangle data");
+    }
+    if ((h.flags & ~kKnownFlags) != 0u) {
+        throw std::runtime_error("Error reading scene file: " + path + ": unknown flags " + std::to_string(h.flags));
+    }
+    s.flags = h.flags;
     if (!(s.camera.vfov_deg > 0.f && s.camera.vfov_deg < 180.f)) {
         throw std::runtime_error("Error reading scene file: " + path + ": bad camera vfov");
     }
@@ -187,6 +396,7 @@ void SaveScene(const Scene& s, const std::string& path) {
     std::memcpy(h.magic, kMagic, sizeof(kMagic));
     h.version = kVersion;
     h.triangles = s.triangle_count();
+    h.flags = s.flags;
     std::memcpy(h.camera, s.camera.eye, 3 * sizeof(float));
     std::memcpy(h.camera + 3, s.camera.lookat, 3 * sizeof(float));
     std::memcpy(h.camera + 6, s.camera.up, 3 * sizeof(float));

@@ -33,8 +33,15 @@ struct Frame {
     float dv[3];
 };
 
+// Scene file header flags: the data types of the model's images (the role a TF graph's
+// input / output node dtypes had in the reference, model.cpp:23-56).
+constexpr std::uint32_t kFlagOutputFloat16 = 1u;  // output image ML_FLOAT16 (else ML_FLOAT32)
+constexpr std::uint32_t kFlagInputFloat16 = 2u;   // input image ML_FLOAT16 (else ML_FLOAT32)
+constexpr std::uint32_t kKnownFlags = kFlagOutputFloat16 | kFlagInputFloat16;
+
 struct Scene {
     Camera camera{};
+    std::uint32_t flags = 0;  // kFlag*
     float background[3] = {0.f, 0.f, 0.f};
     std::vector<float> vertices;  // N x 9: v0.xyz v1.xyz v2.xyz
     std::vector<float> albedo;    // N x 3: r g b
@@ -42,7 +49,8 @@ struct Scene {
     std::uint64_t triangle_count() const { return vertices.size() / 9; }
 };
 
-// Binary scene file. Throws std::runtime_error with a descriptive message on failure.
+// Scene file: the binary format, or Wavefront OBJ when the path ends in
+// ".obj" (scene.cpp LoadObj). Throws std::runtime_error with a descriptive message on failure.
 Scene LoadScene(const std::string& path);
 void SaveScene(const Scene& scene, const std::string& path);
 

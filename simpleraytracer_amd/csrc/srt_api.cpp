@@ -149,7 +149,8 @@ ML_API_ENTRY int srtSetStageTiming(srt_device_scene scene, int enable) {
     });
 }
 
-ML_API_ENTRY int srtTakeStageTimes(srt_device_scene scene, unsigned* launches, double* bin_ms, double* trace_ms) {
+ML_API_ENTRY int srtTakeStageTimes(srt_device_scene scene, unsigned* launches, double* prepare_ms, double* bin_ms,
+                                   double* trace_ms) {
     return Guarded([&] {
         if (scene == nullptr) {
             throw std::runtime_error("Bad scene handle");
@@ -159,6 +160,9 @@ ML_API_ENTRY int srtTakeStageTimes(srt_device_scene scene, unsigned* launches, d
         const srt::DeviceScene::StageTimes t = s->TakeTimes();
         if (launches != nullptr) {
             *launches = t.launches;
+        }
+        if (prepare_ms != nullptr) {
+            *prepare_ms = t.prepare_ms;
         }
         if (bin_ms != nullptr) {
             *bin_ms = t.bin_ms;

@@ -103,14 +103,16 @@ class DeviceScene:
                                        TRACE_VARIANTS[variant], _stream(stream)))
 
     def set_stage_timing(self, enable: bool = True):
-        """Record HIP events around the bin stage and the trace kernel of every trace() call."""
+        """Bind HIP events to the prepare, bin and trace kernels' dispatches (no extra packets)."""
         _check(self._lib.srtSetStageTiming(self.handle, 1 if enable else 0))
 
     def take_stage_times(self):
-        """(timed calls, mean bin-stage ms, mean trace-kernel ms) since the last take; waits for them."""
-        n, b, t = ctypes.c_uint(), ctypes.c_double(), ctypes.c_double()
-        _check(self._lib.srtTakeStageTimes(self.handle, ctypes.byref(n), ctypes.byref(b), ctypes.byref(t)))
-        return n.value, b.value, t.value
+        """(timed trace calls, mean prepare ms, mean bin-stage ms, mean trace-kernel ms) since the
+        last take; waits for the events."""
+        n, p, b, t = ctypes.c_uint(), ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+        _check(self._lib.srtTakeStageTimes(self.handle, ctypes.byref(n), ctypes.byref(p), ctypes.byref(b),
+                                           ctypes.byref(t)))
+        return n.value, p.value, b.value, t.value
 
     def close(self):
         if self.handle:

@@ -351,3 +351,31 @@ def test_no_cpu_fallback_marker(gpu):
     lib = Path(__file__).resolve().parents[1] / "simpleraytracer_amd" / "lib" / "libModelRunner.so"
     assert b"gfx950" in lib.read_bytes()
     assert os.environ.get("SRT_TRACE_VARIANT") in (None, "lds", "scalar", "cull", "0", "1", "2")
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_stage_timing_does_not_change_the_frame(gpu, scenes, variant):
+    """srtSetStageTiming binds events to the kernels' dispatches: same frame, sane times."""
+    import torch
+
+    import simpleraytracer_amd as srt
+
+    w, h = 200, 70
+    ref = torch_render(scenes["soup300"], w, h, variant=variant)
+    scene = srt.DeviceScene(scenes["soup300"], 0)
+    stream = torch.cuda.current_stream()
+    off = torch.full((h, w, 2), 0.5, dtype=torch.float32, device="cuda")
+    out = torch.empty((h, w, 4), dtype=torch.float32, device="cuda")
+    scene.set_stage_timing(True)
+    for _ in range(3):
+        scene.prepare(w, h, stream)
+        scene.trace(off, out, 0, h, variant=variant, stream=stream)
+    scene.set_stage_timing(False)
+    n, prep, binning, trace = scene.take_stage_times()
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    scene.close()
+    assert n == 3
+    assert 0.0 < prep < 1000.0 and 0.0 < trace < 1000.0
+    assert (binning > 0.0) == (variant == "cull")
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))

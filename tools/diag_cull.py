@@ -47,28 +47,29 @@ def main():
         assert lib.srtDiagRead(buf.ctypes.data, buf.nbytes) == 0, _native.last_error()
         scene.close()
     shape = "8x4 tiles, bins " + os.environ.get("SRT_CULL_BIN", "1")
+    parts = int(os.environ.get("PARTS", 2))  # trace blocks per cull tile (render.hip kParts)
     gx, gy = (w + 63) // 64, (h + 31) // 32
-    allb = buf[: gx * gy * 8].astype(np.float64)
-    ran = (allb[:, 7].astype(np.int64) & 4) != 0
+    nb = gx * gy * parts
+    allb = buf[:nb].astype(np.float64)
+    ran = allb[:, 6] > 0
     d = allb[ran]
-    chunks = ran.reshape(8, gy * gx).sum(0)
-    tile_max = allb[:, 6].reshape(8, gy * gx).max(0)
-    names = ["stream", "gather", "walk", "surv", "wsurv0", "batches", "total", "mode"]
-    summary = {"shape": shape, "blocks": gx * gy}
+    # packet-walk blocks: [1] gather, [2] walk, [3] survivors, [4] packets, [5] batches, [6] total
+    names = ["stream", "gather", "walk", "surv", "packets", "batches", "total"]
+    summary = {"shape": f"{gx}x{gy} tiles x {parts} parts, bins " + os.environ.get("SRT_CULL_BIN", "1"),
+               "blocks": nb, "blocks_run": int(ran.sum())}
     for i, n in enumerate(names):
         col = d[:, i]
         summary[n] = {"mean": float(col.mean()), "p50": float(np.median(col)), "p90": float(np.percentile(col, 90)),
-                      "max": float(col.max())}
-    summary["chunks_hist"] = {int(c): int((chunks == c).sum()) for c in np.unique(chunks)}
-    mode = buf[: gx * gy, 7].astype(np.int64)  # z = 0 blocks: bin list length, large-list length
+                      "max": float(col.max()), "sum": float(col.sum())}
+    mode = buf[:nb, 7].astype(np.int64)
     cnt = (mode >> 16) & 0xFFFFFF
     summary["tile_list"] = {"mean": float(cnt.mean()), "p50": float(np.median(cnt)), "p90": float(np.percentile(cnt, 90)),
-                            "max": int(cnt.max()), "sum": int(cnt.sum()), "large": int((mode >> 40).max())}
-    summary["blocks_run"] = int(ran.sum())
+                            "max": int(cnt.max()), "sum": int(cnt.sum()) // parts, "large": int((mode >> 40).max())}
+    # Balance: total block-cycles spread over 256 CUs x 4 SIMDs vs the heaviest block.
+    summary["balance"] = {"sum_cycles_per_simd": float(d[:, 6].sum() / 1024), "max_block_cycles": float(d[:, 6].max())}
     idx = np.nonzero(ran)[0]
     heavy = idx[np.argsort(-allb[idx, 6])[:8]]
-    summary["heaviest"] = [{"block": int(b), "z": int(b // (gx * gy)), "bx": int(b % gx), "by": int((b // gx) % gy),
-                            **{n: int(allb[b, i]) for i, n in enumerate(names)}} for b in heavy]
+    summary["heaviest"] = [{"block": int(b), **{n: int(allb[b, i]) for i, n in enumerate(names)}} for b in heavy]
     print(json.dumps(summary, indent=1))
 
 
