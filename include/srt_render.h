@@ -39,6 +39,20 @@ ML_API_ENTRY int srtWriteScene(const char* path, int kind, unsigned long long tr
 /* Read a scene file's triangle count. */
 ML_API_ENTRY int srtSceneTriangles(const char* path, unsigned long long* triangles);
 
+/* Load a scene file (binary, or Wavefront OBJ when the path ends in ".obj") and copy its
+ * contents out: vertices (triangles x 9 floats), albedo (triangles x 3), camera (10 floats:
+ * eye, lookat, up, vfov_deg), background (3) and the header flags (data types of the model's
+ * images, 1 = FLOAT16 output, 2 = FLOAT16 input). Any output pointer may be NULL; `capacity`
+ * is the number of triangles the vertex / albedo arrays hold (fewer than the scene's: fail). */
+ML_API_ENTRY int srtReadScene(const char* path, unsigned long long capacity, unsigned long long* triangles,
+                              float* vertices, float* albedo, float* camera10, float* background3,
+                              unsigned* flags);
+
+/* Load src_path (binary or OBJ) and write it as a binary scene file to dst_path, with the
+ * data types of the model's images set: input_dtype / output_dtype = ML_FLOAT32 or
+ * ML_FLOAT16, or -1 to keep the source's. */
+ML_API_ENTRY int srtConvertScene(const char* src_path, const char* dst_path, int input_dtype, int output_dtype);
+
 /* Affine primary-ray frame of a scene at W x H: 12 floats origin[3] base[3] du[3] dv[3]. */
 ML_API_ENTRY int srtSceneFrame(const char* path, size_t width, size_t height, float* frame12);
 

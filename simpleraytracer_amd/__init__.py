@@ -8,10 +8,11 @@ Layers:
   device.py    scene files + device-level stages on caller buffers (DeviceScene)
   bands.py     row-band partition and the one-process-per-GPU band gather
 """
-from .device import DeviceScene, SrtError, scene_frame, scene_triangles, write_scene  # noqa: F401
+from .device import (DeviceScene, SrtError, convert_scene, read_scene, scene_frame, scene_triangles,  # noqa: F401
+                     write_scene)
 from .runner import Context, Image, MLError, Model, default_offsets, render  # noqa: F401
 
 __all__ = [
     "Context", "Image", "Model", "MLError", "render", "default_offsets",
-    "DeviceScene", "SrtError", "write_scene", "scene_triangles", "scene_frame",
+    "DeviceScene", "SrtError", "write_scene", "scene_triangles", "scene_frame", "read_scene", "convert_scene",
 ]

@@ -73,6 +73,10 @@ _SIGNATURES = {
     "srtWriteScene": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, ctypes.c_ulonglong, ctypes.c_ulonglong,
                                      ctypes.c_float]),
     "srtSceneTriangles": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_ulonglong)]),
+    "srtReadScene": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_ulonglong, ctypes.POINTER(ctypes.c_ulonglong),
+                                    ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                    ctypes.POINTER(ctypes.c_uint)]),
+    "srtConvertScene": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int]),
     "srtSceneFrame": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_size_t,
                                      ctypes.POINTER(ctypes.c_float)]),
     "srtDeviceSceneCreate": (ctypes.c_void_p, [ctypes.c_char_p, ctypes.c_int]),

@@ -1,6 +1,7 @@
 // Extension C entry points (include/srt_render.h): scene files and device-level stages.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <exception>
 #include <string>
 
@@ -70,6 +71,64 @@ ML_API_ENTRY int srtSceneTriangles(const char* path, unsigned long long* triangl
             throw std::runtime_error("Bad argument");
         }
         *triangles = srt::LoadScene(path).triangle_count();
+    });
+}
+
+ML_API_ENTRY int srtReadScene(const char* path, unsigned long long capacity, unsigned long long* triangles,
+                              float* vertices, float* albedo, float* camera10, float* background3,
+                              unsigned* flags) {
+    return Guarded([&] {
+        if (path == nullptr) {
+            throw std::runtime_error("Bad path argument");
+        }
+        const srt::Scene s = srt::LoadScene(path);
+        const unsigned long long n = s.triangle_count();
+        if (triangles != nullptr) {
+            *triangles = n;
+        }
+        if ((vertices != nullptr || albedo != nullptr) && capacity < n) {
+            throw std::runtime_error("Buffer too small: " + std::to_string(capacity) + " triangles for " +
+                                     std::to_string(n));
+        }
+        if (vertices != nullptr) {
+            std::copy(s.vertices.begin(), s.vertices.end(), vertices);
+        }
+        if (albedo != nullptr) {
+            std::copy(s.albedo.begin(), s.albedo.end(), albedo);
+        }
+        if (camera10 != nullptr) {
+            std::copy(s.camera.eye, s.camera.eye + 3, camera10);
+            std::copy(s.camera.lookat, s.camera.lookat + 3, camera10 + 3);
+            std::copy(s.camera.up, s.camera.up + 3, camera10 + 6);
+            camera10[9] = s.camera.vfov_deg;
+        }
+        if (background3 != nullptr) {
+            std::copy(s.background, s.background + 3, background3);
+        }
+        if (flags != nullptr) {
+            *flags = s.flags;
+        }
+    });
+}
+
+ML_API_ENTRY int srtConvertScene(const char* src_path, const char* dst_path, int input_dtype, int output_dtype) {
+    return Guarded([&] {
+        if (src_path == nullptr || dst_path == nullptr) {
+            throw std::runtime_error("Bad path argument");
+        }
+        srt::Scene s = srt::LoadScene(src_path);
+        auto set = [&](int dtype, std::uint32_t bit, const char* what) {
+            if (dtype == -1) {
+                return;
+            }
+            if (dtype != ML_FLOAT32 && dtype != ML_FLOAT16) {
+                throw std::runtime_error(std::string("Bad ") + what + " data type " + std::to_string(dtype));
+            }
+            s.flags = dtype == ML_FLOAT16 ? (s.flags | bit) : (s.flags & ~bit);
+        };
+        set(input_dtype, srt::kFlagInputFloat16, "input");
+        set(output_dtype, srt::kFlagOutputFloat16, "output");
+        srt::SaveScene(s, dst_path);
     });
 }
 

@@ -48,6 +48,28 @@ def scene_triangles(path: str) -> int:
     return n.value
 
 
+def read_scene(path: str):
+    """Load a scene file (binary or .obj) through the library: dict of numpy arrays."""
+    import numpy as np
+
+    n = ctypes.c_ulonglong()
+    _check(_native.lib().srtReadScene(os.fsencode(path), 0, ctypes.byref(n), None, None, None, None, None))
+    v = np.empty((n.value, 9), np.float32)
+    a = np.empty((n.value, 3), np.float32)
+    cam = np.empty(10, np.float32)
+    bg = np.empty(3, np.float32)
+    flags = ctypes.c_uint()
+    _check(_native.lib().srtReadScene(os.fsencode(path), n.value, ctypes.byref(n), v.ctypes.data, a.ctypes.data,
+                                      cam.ctypes.data, bg.ctypes.data, ctypes.byref(flags)))
+    return {"vertices": v, "albedo": a, "camera": cam, "background": bg, "flags": flags.value}
+
+
+def convert_scene(src: str, dst: str, input_dtype: int = -1, output_dtype: int = -1) -> str:
+    """Write src (binary or .obj) as a binary scene file with the given image data types."""
+    _check(_native.lib().srtConvertScene(os.fsencode(src), os.fsencode(dst), input_dtype, output_dtype))
+    return dst
+
+
 def scene_frame(path: str, width: int, height: int):
     """(origin, base, du, dv) float32 triples of the affine primary-ray frame."""
     out = (ctypes.c_float * 12)()

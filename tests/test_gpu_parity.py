@@ -379,3 +379,26 @@ def test_stage_timing_does_not_change_the_frame(gpu, scenes, variant):
     assert 0.0 < prep < 1000.0 and 0.0 < trace < 1000.0
     assert (binning > 0.0) == (variant == "cull")
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+
+
+def test_obj_scene_renders_like_its_binary_conversion(gpu, tmp_path):
+    """An OBJ model_path renders through ml* exactly like the oracle on its binary conversion."""
+    import simpleraytracer_amd as srt
+
+    rng = np.random.default_rng(5)
+    lines = ["mtllib m.mtl", "usemtl a"]
+    for i in range(60):
+        c = rng.uniform([-1, -1, 2], [1, 1, 4])
+        for _ in range(4):
+            lines.append("v %.6f %.6f %.6f" % tuple(c + rng.uniform(-0.15, 0.15, 3)))
+        lines.append(f"f {4 * i + 1} {4 * i + 2}/1 {4 * i + 3}//2 {4 * i + 4}/3/4")
+        if i == 30:
+            lines.append("usemtl b")
+    (tmp_path / "m.mtl").write_text("newmtl a\nKd 0.9 0.5 0.2\nnewmtl b\nKd 0.2 0.4 0.9\n")
+    obj = tmp_path / "quads.obj"
+    obj.write_text("\n".join(lines) + "\n")
+    binary = srt.convert_scene(str(obj), str(tmp_path / "quads.srt"))
+    w, h = 160, 96
+    got = srt.render(str(obj), w, h)
+    assert_parity(got, oracle_render(binary, w, h))
+    assert (got[..., 3] >= 0).sum() > 1000  # the quads are in view
