@@ -2,6 +2,7 @@
 
 #include <stdexcept>
 
+#include "dtype.h"
 #include "image.h"
 #include "utils.h"
 
@@ -18,6 +19,9 @@ Model::Model(ml_model_params const* params) {
         throw std::runtime_error("Bad model_path model parameter value");
     }
     m_scene = srt::LoadScene(params->model_path);
+    // The scene's flags give the image data types (a TF graph's node dtypes in the reference).
+    m_input_info.dtype = (m_scene.flags & srt::kFlagInputFloat16) != 0u ? ML_FLOAT16 : ML_FLOAT32;
+    m_output_info.dtype = (m_scene.flags & srt::kFlagOutputFloat16) != 0u ? ML_FLOAT16 : ML_FLOAT32;
 }
 
 // model.cpp:141-159 (no "no session" failure here: a constructed model always has a scene).
@@ -80,7 +84,7 @@ ml_status Model::SetInputInfo(ml_image_info const* info) {
         return ML_FAIL;
     }
     m_input_info = *info;
-    m_output_info = ml_image_info{ML_FLOAT32, info->width, info->height, 4};
+    m_output_info = ml_image_info{m_output_info.dtype, info->width, info->height, 4};
     return ML_OK;
 }
 
@@ -130,7 +134,8 @@ bool Model::RenderToImage(Image& input, Image& output) {
     if (!specified) {
         return false;
     }
-    const size_t in_expected = m_input_info.width * m_input_info.height * m_input_info.channels * sizeof(float);
+    const size_t in_expected =
+        m_input_info.width * m_input_info.height * m_input_info.channels * DataTypeSize(m_input_info.dtype);
     size_t in_size = 0;
     void* in_data = input.Map(&in_size);
     if (in_size != in_expected) {
@@ -138,7 +143,8 @@ bool Model::RenderToImage(Image& input, Image& output) {
         m_error_cache << "Internal error: input size does not match: " << in_size << " vs " << in_expected;
         return false;
     }
-    const size_t out_expected = m_output_info.width * m_output_info.height * m_output_info.channels * sizeof(float);
+    const size_t out_expected =
+        m_output_info.width * m_output_info.height * m_output_info.channels * DataTypeSize(m_output_info.dtype);
     size_t out_size = 0;
     void* out_data = output.Map(&out_size);
     if (out_size != out_expected) {
@@ -149,7 +155,7 @@ bool Model::RenderToImage(Image& input, Image& output) {
     }
     bool ok = true;
     try {
-        m_renderer->Render(static_cast<const float*>(in_data), static_cast<float*>(out_data));
+        m_renderer->Render(in_data, out_data);
     } catch (std::exception& e) {
         m_error_cache << "Render error: " << e.what();
         ok = false;

@@ -132,6 +132,12 @@ hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_ver
                        const CullBins* bins, hipStream_t stream, const StageEvents* events = nullptr,
                        const unsigned* prepare_rank = nullptr);
 
+// Element-wise IEEE binary16 <-> binary32 conversion on the device (ML_FLOAT16 images):
+// float -> half rounds to nearest even (overflow -> inf, NaN stays NaN); half -> float is exact.
+// `half` buffers are uint16 bit patterns on the host side.
+hipError_t LaunchFloatToHalf(const float* src, std::uint16_t* dst, std::size_t count, hipStream_t stream);
+hipError_t LaunchHalfToFloat(const std::uint16_t* src, float* dst, std::size_t count, hipStream_t stream);
+
 #ifdef SRT_DIAG
 // Diagnostic build only: copy the cull kernel's per-block phase counters to host memory.
 hipError_t DiagRead(void* host, std::size_t bytes);

@@ -1961,6 +1961,29 @@ int CullWavesFromEnv() {
     return 4;
 }
 
+// ML_FLOAT16 images: 4 elements per thread (8-B half / 16-B float vectors), scalar tail.
+__global__ __launch_bounds__(256) void FloatToHalfKernel(const float* __restrict__ src, _Float16* __restrict__ dst,
+                                                         std::size_t count) {
+    const std::size_t i = (static_cast<std::size_t>(blockIdx.x) * blockDim.x + threadIdx.x) * 4;
+    if (i + 4 <= count) {
+        const float4 v = *reinterpret_cast<const float4*>(src + i);
+        typedef _Float16 H4 __attribute__((ext_vector_type(4)));
+        *reinterpret_cast<H4*>(dst + i) = H4{static_cast<_Float16>(v.x), static_cast<_Float16>(v.y),
+                                             static_cast<_Float16>(v.z), static_cast<_Float16>(v.w)};
+    } else {
+        for (std::size_t k = i; k < count; ++k) {
+            dst[k] = static_cast<_Float16>(src[k]);
+        }
+    }
+}
+__global__ __launch_bounds__(256) void HalfToFloatKernel(const _Float16* __restrict__ src, float* __restrict__ dst,
+                                                         std::size_t count) {
+    const std::size_t i = (static_cast<std::size_t>(blockIdx.x) * blockDim.x + threadIdx.x) * 4;
+    for (std::size_t k = i; k < i + 4 && k < count; ++k) {
+        dst[k] = static_cast<float>(src[k]);
+    }
+}
+
 // Launch on `stream`; with timing events, through hipExtLaunchKernelGGL so that the events
 // take the dispatch packet's own start / end timestamps (no extra stream packets).
 template <class K, class P>
@@ -2001,6 +2024,26 @@ PrepareParams MakePrepareParams(const float* d_vertices, const unsigned* d_rank,
     return p;
 }
 }  // namespace
+
+hipError_t LaunchFloatToHalf(const float* src, std::uint16_t* dst, std::size_t count, hipStream_t stream) {
+    if (count == 0) {
+        return hipSuccess;
+    }
+    const unsigned blocks = static_cast<unsigned>((count + 1023) / 1024);
+    hipLaunchKernelGGL(FloatToHalfKernel, dim3(blocks), dim3(256), 0, stream, src, reinterpret_cast<_Float16*>(dst),
+                       count);
+    return hipGetLastError();
+}
+
+hipError_t LaunchHalfToFloat(const std::uint16_t* src, float* dst, std::size_t count, hipStream_t stream) {
+    if (count == 0) {
+        return hipSuccess;
+    }
+    const unsigned blocks = static_cast<unsigned>((count + 1023) / 1024);
+    hipLaunchKernelGGL(HalfToFloatKernel, dim3(blocks), dim3(256), 0, stream,
+                       reinterpret_cast<const _Float16*>(src), dst, count);
+    return hipGetLastError();
+}
 
 hipError_t LaunchPrepare(const float* d_vertices, const unsigned* d_rank, std::uint64_t n, const Frame& frame,
                          float* d_edges, hipStream_t stream, hipEvent_t ev_begin, hipEvent_t ev_end) {

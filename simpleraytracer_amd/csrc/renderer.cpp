@@ -277,11 +277,16 @@ struct Renderer::Slot {
     std::unique_ptr<DeviceScene> scene;
     float* offsets = nullptr;  // band_rows x W x 2
     float* rgba = nullptr;     // band_rows x W x 4
+    std::uint16_t* offsets16 = nullptr;  // FLOAT16 input: band_rows x W x 2 halves (H2D staging)
+    std::uint16_t* rgba16 = nullptr;     // FLOAT16 output: band_rows x W x 4 halves
     std::size_t row_begin = 0;
     std::size_t row_count = 0;
 };
 
-Renderer::Renderer(const Scene& scene, std::vector<int> devices) : m_variant(TraceVariantFromEnv()) {
+Renderer::Renderer(const Scene& scene, std::vector<int> devices)
+    : m_variant(TraceVariantFromEnv()),
+      m_in_half((scene.flags & kFlagInputFloat16) != 0u),
+      m_out_half((scene.flags & kFlagOutputFloat16) != 0u) {
     for (int d : devices) {
         auto slot = std::make_unique<Slot>();
         slot->device = d;
@@ -316,8 +321,12 @@ void Renderer::ReleaseBuffers() {
         (void)hipSetDevice(slot->device);
         (void)hipFree(slot->offsets);
         (void)hipFree(slot->rgba);
+        (void)hipFree(slot->offsets16);
+        (void)hipFree(slot->rgba16);
         slot->offsets = nullptr;
         slot->rgba = nullptr;
+        slot->offsets16 = nullptr;
+        slot->rgba16 = nullptr;
     }
     if (m_gather != nullptr) {
         (void)hipSetDevice(m_slots.front()->device);
@@ -331,22 +340,32 @@ void Renderer::Configure(std::size_t width, std::size_t height) {
     const std::size_t band_rows = (height + bands - 1) / bands;
     // Allocate everything new before releasing the old buffers (strong guarantee).
     std::vector<float*> offs(bands, nullptr), outs(bands, nullptr);
-    float* gather = nullptr;
+    std::vector<std::uint16_t*> offs16(bands, nullptr), outs16(bands, nullptr);
+    void* gather = nullptr;
+    const std::size_t out_elem = m_out_half ? 2 : 4;
     try {
         for (std::size_t i = 0; i < bands; ++i) {
             DeviceGuard guard(m_slots[i]->device);
             offs[i] = DeviceAlloc<float>(band_rows * width * 2, "hipMalloc(band offsets)");
             outs[i] = DeviceAlloc<float>(band_rows * width * 4, "hipMalloc(band framebuffer)");
+            if (m_in_half) {
+                offs16[i] = DeviceAlloc<std::uint16_t>(band_rows * width * 2, "hipMalloc(band offsets f16)");
+            }
+            if (m_out_half) {
+                outs16[i] = DeviceAlloc<std::uint16_t>(band_rows * width * 4, "hipMalloc(band framebuffer f16)");
+            }
         }
         if (m_use_rccl) {
             DeviceGuard guard(m_slots.front()->device);
-            gather = DeviceAlloc<float>(bands * band_rows * width * 4, "hipMalloc(gather framebuffer)");
+            gather = DeviceAlloc<unsigned char>(bands * band_rows * width * 4 * out_elem, "hipMalloc(gather framebuffer)");
         }
     } catch (...) {
         for (std::size_t i = 0; i < bands; ++i) {
             (void)hipSetDevice(m_slots[i]->device);
             (void)hipFree(offs[i]);
             (void)hipFree(outs[i]);
+            (void)hipFree(offs16[i]);
+            (void)hipFree(outs16[i]);
         }
         (void)hipFree(gather);
         throw;
@@ -356,6 +375,8 @@ void Renderer::Configure(std::size_t width, std::size_t height) {
         Slot& s = *m_slots[i];
         s.offsets = offs[i];
         s.rgba = outs[i];
+        s.offsets16 = offs16[i];
+        s.rgba16 = outs16[i];
         s.row_begin = std::min(height, i * band_rows);
         s.row_count = std::min(height, (i + 1) * band_rows) - s.row_begin;
     }
@@ -365,21 +386,33 @@ void Renderer::Configure(std::size_t width, std::size_t height) {
     m_band_rows = band_rows;
 }
 
-void Renderer::Render(const float* host_offsets, float* host_rgba) {
+void Renderer::Render(const void* host_offsets, void* host_rgba) {
     if (!configured()) {
         throw std::runtime_error("Renderer used before Configure()");
     }
     const std::size_t w = m_width;
+    const std::size_t in_elem = m_in_half ? 2 : 4, out_elem = m_out_half ? 2 : 4;
+    const auto* in_bytes = static_cast<const unsigned char*>(host_offsets);
+    auto* out_bytes = static_cast<unsigned char*>(host_rgba);
     for (auto& sp : m_slots) {
         Slot& s = *sp;
         DeviceGuard guard(s.device);
         if (s.row_count != 0) {
-            HipCheck(hipMemcpyAsync(s.offsets, host_offsets + s.row_begin * w * 2, s.row_count * w * 2 * sizeof(float),
+            const std::size_t count = s.row_count * w * 2;
+            void* dst = m_in_half ? static_cast<void*>(s.offsets16) : static_cast<void*>(s.offsets);
+            HipCheck(hipMemcpyAsync(dst, in_bytes + s.row_begin * w * 2 * in_elem, count * in_elem,
                                     hipMemcpyHostToDevice, s.stream),
                      "hipMemcpyAsync(offsets H2D)");
+            if (m_in_half) {
+                HipCheck(LaunchHalfToFloat(s.offsets16, s.offsets, count, s.stream), "offsets f16 -> f32");
+            }
         }
         s.scene->Prepare(w, m_height, s.stream);
         s.scene->Trace(s.offsets, s.rgba, s.row_begin, s.row_count, m_variant, s.stream);
+        if (m_out_half) {
+            // Whole padded band (rows past row_count are gathered but never copied out).
+            HipCheck(LaunchFloatToHalf(s.rgba, s.rgba16, m_band_rows * w * 4, s.stream), "framebuffer f32 -> f16");
+        }
     }
     if (m_use_rccl) {
         // Equal-size bands (the last one padded) gathered to the first device over xGMI;
@@ -387,15 +420,16 @@ void Renderer::Render(const float* host_offsets, float* host_rgba) {
         NcclCheck(ncclGroupStart(), "ncclGroupStart");
         for (std::size_t i = 0; i < m_slots.size(); ++i) {
             Slot& s = *m_slots[i];
-            NcclCheck(ncclGather(s.rgba, i == 0 ? m_gather : nullptr, m_band_rows * w * 4, ncclFloat32, 0,
-                                 static_cast<ncclComm_t>(m_comms[i]), s.stream),
+            const void* send = m_out_half ? static_cast<const void*>(s.rgba16) : static_cast<const void*>(s.rgba);
+            NcclCheck(ncclGather(send, i == 0 ? m_gather : nullptr, m_band_rows * w * 4,
+                                 m_out_half ? ncclFloat16 : ncclFloat32, 0, static_cast<ncclComm_t>(m_comms[i]),
+                                 s.stream),
                       "ncclGather");
         }
         NcclCheck(ncclGroupEnd(), "ncclGroupEnd");
         Slot& root = *m_slots.front();
         DeviceGuard guard(root.device);
-        HipCheck(hipMemcpyAsync(host_rgba, m_gather, m_height * w * 4 * sizeof(float), hipMemcpyDeviceToHost,
-                                root.stream),
+        HipCheck(hipMemcpyAsync(out_bytes, m_gather, m_height * w * 4 * out_elem, hipMemcpyDeviceToHost, root.stream),
                  "hipMemcpyAsync(frame D2H)");
     } else {
         for (auto& sp : m_slots) {
@@ -404,7 +438,8 @@ void Renderer::Render(const float* host_offsets, float* host_rgba) {
                 continue;
             }
             DeviceGuard guard(s.device);
-            HipCheck(hipMemcpyAsync(host_rgba + s.row_begin * w * 4, s.rgba, s.row_count * w * 4 * sizeof(float),
+            const void* src = m_out_half ? static_cast<const void*>(s.rgba16) : static_cast<const void*>(s.rgba);
+            HipCheck(hipMemcpyAsync(out_bytes + s.row_begin * w * 4 * out_elem, src, s.row_count * w * 4 * out_elem,
                                     hipMemcpyDeviceToHost, s.stream),
                      "hipMemcpyAsync(band D2H)");
         }

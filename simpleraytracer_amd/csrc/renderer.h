@@ -105,7 +105,12 @@ public:
     bool configured() const { return m_width != 0; }
 
     // Render one frame: host offsets (H x W x 2) -> host RGBA (H x W x 4). Synchronous.
-    void Render(const float* host_offsets, float* host_rgba);
+    // Element types from the scene's flags (kFlagInputFloat16 / kFlagOutputFloat16): float,
+    // or IEEE binary16 bit patterns, converted on the device (the gather and the D2H then
+    // move half the bytes).
+    void Render(const void* host_offsets, void* host_rgba);
+    bool input_half() const { return m_in_half; }
+    bool output_half() const { return m_out_half; }
 
     std::size_t bands() const { return m_slots.size(); }
 
@@ -120,7 +125,9 @@ private:
     std::size_t m_width = 0;
     std::size_t m_height = 0;
     std::size_t m_band_rows = 0;
-    float* m_gather = nullptr;  // root device: bands x band_rows x W x 4
+    void* m_gather = nullptr;  // root device: bands x band_rows x W x 4 (float, or half)
+    bool m_in_half = false;
+    bool m_out_half = false;
 };
 
 }  // namespace srt

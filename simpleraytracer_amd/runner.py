@@ -141,11 +141,14 @@ def default_offsets(width: int, height: int) -> np.ndarray:
 
 
 def render(scene_path: str, width: int, height: int, offsets: np.ndarray | None = None) -> np.ndarray:
-    """Render one frame through the ml* API; returns an H x W x 4 float32 copy."""
+    """Render one frame through the ml* API; returns an H x W x 4 copy (float32, or float16
+    for a scene whose output data type is ML_FLOAT16; FLOAT16 input scenes take the offsets
+    rounded to float16)."""
     ctx = Context()
     model = ctx.create_model(scene_path)
     try:
-        model.set_input_info(width, height)
+        (idt0, _, _, _), _ = model.info()
+        model.set_input_info(width, height, dtype=idt0)
         (idt, iw, ih, ic), (odt, ow, oh, oc) = model.info()
         inp = ctx.create_image(idt, iw, ih, ic)
         out = ctx.create_image(odt, ow, oh, oc)
