@@ -26,7 +26,7 @@ DIAG_BUILD := build/diag
 DIAG_LIB   := simpleraytracer_amd/lib_diag/libModelRunner.so
 DIAG_OBJS  := $(patsubst $(BUILD)/%,$(DIAG_BUILD)/%,$(OBJS))
 
-.PHONY: all oracle ref clean diag
+.PHONY: all oracle ref clean diag exp
 all: $(LIB) bin/test_app
 
 $(BUILD)/%.o: $(CSRC)/%.hip $(HEADERS)
@@ -59,6 +59,17 @@ $(DIAG_LIB): $(DIAG_OBJS)
 
 diag: $(DIAG_LIB)
 
+# Experiment builds (measurement only): make exp EXP_NAME=x EXP_FLAGS="-DSRT_...=..." ->
+# simpleraytracer_amd/lib_exp/x/libModelRunner.so (select with env SRT_LIB).
+EXP_NAME  ?= default
+EXP_FLAGS ?=
+EXP_BUILD := build/exp/$(EXP_NAME)
+EXP_LIB   := simpleraytracer_amd/lib_exp/$(EXP_NAME)/libModelRunner.so
+exp:
+	@mkdir -p $(EXP_BUILD) $(dir $(EXP_LIB))
+	$(HIPCC) $(HIPFLAGS) $(EXP_FLAGS) -c $(CSRC)/render.hip -o $(EXP_BUILD)/render.o
+	$(HIPCC) --offload-arch=$(ARCH) $(EXP_BUILD)/render.o $(filter-out $(BUILD)/render.o,$(OBJS)) -o $(EXP_LIB) $(LDFLAGS)
+
 oracle:
 	$(MAKE) -C oracle
 
@@ -66,5 +77,5 @@ ref:
 	$(MAKE) -C oracle ref
 
 clean:
-	rm -rf build bin $(LIBDIR) $(dir $(DIAG_LIB))
+	rm -rf build bin $(LIBDIR) $(dir $(DIAG_LIB)) simpleraytracer_amd/lib_exp
 	$(MAKE) -C oracle clean

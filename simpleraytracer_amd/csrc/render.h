@@ -77,7 +77,10 @@ hipError_t LaunchPrepare(const float* d_vertices, const unsigned* d_rank, std::u
 
 // Cull tiles: 64 columns x 32 rows of rays, one trace block each (render.hip "Cull bins").
 constexpr int kCullTileCols = 64;
-constexpr int kCullTileRows = 32;
+#ifndef SRT_TILE_ROWS
+#define SRT_TILE_ROWS 32
+#endif
+constexpr int kCullTileRows = SRT_TILE_ROWS;
 constexpr int kMaxBoundTiles = 2048;  // binning needs tiles_x + tiles_y <= this
 constexpr int kMaxBinTiles = 8192;    // and tiles_x * tiles_y <= this (bin kernel LDS histogram)
 

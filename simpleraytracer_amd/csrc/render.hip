@@ -679,8 +679,11 @@ __device__ __forceinline__ void LoadRecord(const float4* __restrict__ edges, uns
 
 // Cull tile = one trace block: 64 columns x 32 rows of rays, W waves (4, 8 or 16) of 64 x R
 // rays, R = 32 / W rays per lane. Constants that depend on W live in CullShape<W>.
-constexpr int kTileRows = 32;   // cull tile (bins): 64 columns x 32 rows
-constexpr int kBlockRows = 16;  // trace block: one part of a cull tile
+constexpr int kTileRows = kCullTileRows;  // cull tile (bins): 64 columns x 32 rows
+#ifndef SRT_BLOCK_ROWS
+#define SRT_BLOCK_ROWS 16
+#endif
+constexpr int kBlockRows = SRT_BLOCK_ROWS;  // trace block: one part of a cull tile
 constexpr int kParts = kTileRows / kBlockRows;
 constexpr int kStreamStep = 2048;  // FULL stream: records per block per step
 constexpr int kListG = 4;          // LIST stream: ids per lane per step
@@ -2227,11 +2230,20 @@ hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_ver
         }
         // One block per (tile, part): gridDim.x = tile columns, gridDim.y = tile rows x parts.
         const dim3 grid(gx, gy * kParts);
-        switch (CullWavesFromEnv()) {
-            case 8: Launch(TraceCullKernel<8>, grid, dim3(kWave * 8), stream, ev.begin, ev.end, p); break;
-            case 16: Launch(TraceCullKernel<16>, grid, dim3(kWave * 16), stream, ev.begin, ev.end, p); break;
-            default: Launch(TraceCullKernel<4>, grid, dim3(kWave * 4), stream, ev.begin, ev.end, p); break;
+        const int waves = CullWavesFromEnv();
+        if constexpr (kBlockRows >= 16) {
+            if (waves == 16) {
+                Launch(TraceCullKernel<16>, grid, dim3(kWave * 16), stream, ev.begin, ev.end, p);
+                return hipGetLastError();
+            }
         }
+        if constexpr (kBlockRows >= 8) {
+            if (waves == 8) {
+                Launch(TraceCullKernel<8>, grid, dim3(kWave * 8), stream, ev.begin, ev.end, p);
+                return hipGetLastError();
+            }
+        }
+        Launch(TraceCullKernel<4>, grid, dim3(kWave * 4), stream, ev.begin, ev.end, p);
     } else {
         constexpr int kRowsPerBlock = kRowsPerLane * kLdsWaves;
         const unsigned gy = static_cast<unsigned>((band.row_count + kRowsPerBlock - 1) / kRowsPerBlock);

@@ -10,7 +10,7 @@ if [ "${TESTS:-1}" = 1 ]; then
     rc=$?; tail -3 gpurun_out/pytest_gpu.log; [ $rc -le 1 ] || exit $rc
 fi
 for cfg in ${CFGS:-NONE=0}; do
-    tag=$(echo "$cfg" | tr '+=' '__')
+    tag=$(echo "$cfg" | tr '+=/' '___' | cut -c1-80)
     env $(echo "$cfg" | tr '+' ' ') timeout -k 10 120 rocprofv3 --kernel-trace --stats -d gpurun_out/e_$tag -o run --output-format csv -- \
         python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-e2e ${BENCH_ARGS:-} > gpurun_out/e_$tag.log 2>&1 || { echo "rc=$? $cfg"; exit 1; }
     echo "== $cfg"; grep -o '"value": [0-9.]*' gpurun_out/e_$tag.log
