@@ -1617,11 +1617,19 @@ __device__ __forceinline__ int LastLoAtMost(const float2* b, int n, float v) {
 // heavy tiles start first and the light ones fill in behind them. One block; a counting sort
 // over 64 buckets (order within a bucket arbitrary: the frame does not depend on it).
 constexpr int kOrderThreads = 1024;
+// Counts written by device-scope atomics of the same kernel (the bin kernel's last block) need
+// device-scope loads; a later kernel (TileOrderKernel) reads them with plain loads.
+template <bool kSameKernel>
 __device__ __forceinline__ unsigned LoadCount(const unsigned* c) {
-    return __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if constexpr (kSameKernel) {
+        return __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+        return *c;
+    }
 }
+template <bool kSameKernel>
 __device__ __forceinline__ unsigned TileWorkBucket(const BinParams& p, unsigned t, unsigned large) {
-    const unsigned cnt = LoadCount(&p.counts[t]);
+    const unsigned cnt = LoadCount<kSameKernel>(&p.counts[t]);
     if (p.tile_info[t].usable == 0u || cnt > p.capacity) {
         return 63u;
     }
@@ -1629,18 +1637,19 @@ __device__ __forceinline__ unsigned TileWorkBucket(const BinParams& p, unsigned 
     return total == 0u ? 0u : 32u - __builtin_clz(total);
 }
 // One block of any size computes the whole order.
+template <bool kSameKernel>
 __device__ void TileOrderBlock(const BinParams& p) {
     __shared__ unsigned start[64];
     const int tid = threadIdx.x;
     const unsigned nthreads = blockDim.x;
     const unsigned tiles = static_cast<unsigned>(p.tiles_x * p.tiles_y);
-    const unsigned large = LoadCount(&p.counts[tiles]);
+    const unsigned large = LoadCount<kSameKernel>(&p.counts[tiles]);
     if (tid < 64) {
         start[tid] = 0u;
     }
     __syncthreads();
     for (unsigned t = tid; t < tiles; t += nthreads) {
-        atomicAdd(&start[TileWorkBucket(p, t, large)], static_cast<unsigned>(kParts));
+        atomicAdd(&start[TileWorkBucket<kSameKernel>(p, t, large)], static_cast<unsigned>(kParts));
     }
     __syncthreads();
     unsigned first = 0u;  // tiles in heavier buckets
@@ -1655,7 +1664,7 @@ __device__ void TileOrderBlock(const BinParams& p) {
     }
     __syncthreads();
     for (unsigned t = tid; t < tiles; t += nthreads) {
-        const unsigned at = atomicAdd(&start[TileWorkBucket(p, t, large)], static_cast<unsigned>(kParts));
+        const unsigned at = atomicAdd(&start[TileWorkBucket<kSameKernel>(p, t, large)], static_cast<unsigned>(kParts));
         for (int part = 0; part < kParts; ++part) {
             p.tile_order[at + part] = t * kParts + part;  // trace work items (tile, part)
         }
@@ -1788,7 +1797,7 @@ __global__ __launch_bounds__(kBinThreads) void BinTrianglesKernel(BinParams p) {
     }
     __syncthreads();
     if (last != 0u) {
-        TileOrderBlock(p);
+        TileOrderBlock<true>(p);
         if (tid == 0) {
             p.sync[0] = 0u;  // ready for the next frame (the kernel boundary orders it)
         }
@@ -1798,7 +1807,7 @@ __global__ __launch_bounds__(kBinThreads) void BinTrianglesKernel(BinParams p) {
 // Standalone order (a band with no records: the bin kernel, which normally computes the
 // order in its last block, is not launched).
 __global__ __launch_bounds__(kOrderThreads) void TileOrderKernel(BinParams p) {
-    TileOrderBlock(p);
+    TileOrderBlock<false>(p);
 }
 
 // Candidate source of a tile: LIST (binned, usable box, list complete): the tile's list then
