@@ -56,6 +56,9 @@ struct TraceParams {
     const float2* __restrict__ offsets;
     float4* __restrict__ out;
     unsigned n_pad;   // records in the edge buffer (multiple of kPadTriangles)
+    int tiles_x;         // cull tiles per tile row of the band
+    unsigned tiles;      // cull tiles of the band
+    unsigned item_base;  // cull trace: first work item (position in the tile order) of this launch
     unsigned n_tiles; // tiles holding at least one real record (>= 1)
     int width;
     int row_count;
@@ -1068,7 +1071,7 @@ __device__ __forceinline__ void CullWalk(const TraceParams& p, CullShared<W>& sh
         d[6] = __builtin_amdgcn_s_memtime() - d_t0;
         d[7] = (RASTER ? 1 : 0) | (LIST ? 2 : 0) | 4 |
                (p.bin_counts != nullptr ? (static_cast<unsigned long long>(p.bin_counts[tile]) << 16) |
-                                              (static_cast<unsigned long long>(p.bin_counts[gridDim.x * gridDim.y]) << 40)
+                                              (static_cast<unsigned long long>(p.bin_counts[p.tiles]) << 40)
                                         : 0ull);
     }
 #endif
@@ -1822,7 +1825,7 @@ __device__ __forceinline__ CullSource TileSource(const TraceParams& p, const Til
         src.list = p.bin_lists + static_cast<size_t>(tile) * p.bin_capacity;
         src.list2 = p.large_list;
         src.count1 = cnt;
-        src.end = cnt + p.bin_counts[gridDim.x * gridDim.y / kParts];
+        src.end = cnt + p.bin_counts[p.tiles];
     }
     return src;
 }
@@ -1856,10 +1859,11 @@ __global__ __launch_bounds__(kWave * W, 4) void TraceCullKernel(TraceParams p) {
     __shared__ CullShared<W> sh;
     // Block = one part (kBlockRows rows) of a cull tile (kTileRows rows); launched in the
     // tile order's work order when the frame is binned.
-    const unsigned linear = blockIdx.y * gridDim.x + blockIdx.x;
+    const unsigned linear = blockIdx.y * gridDim.x + blockIdx.x + p.item_base;
     const unsigned item = p.tile_order != nullptr ? p.tile_order[linear] : linear;
     const unsigned tile = item / kParts;
-    const int tx = static_cast<int>(tile % gridDim.x), ty = static_cast<int>(tile / gridDim.x);
+    const int tx = static_cast<int>(tile % static_cast<unsigned>(p.tiles_x));
+    const int ty = static_cast<int>(tile / static_cast<unsigned>(p.tiles_x));
     const int row0 = ty * kTileRows + static_cast<int>(item % kParts) * kBlockRows;  // band row of the block
     if (row0 >= p.row_count) {
         return;  // the last tile row's empty part
@@ -1962,6 +1966,17 @@ __global__ __launch_bounds__(kWave * W, 4) void TraceCullKernel(TraceParams p) {
 bool EnvFlag(const char* name, bool dflt) {
     const char* v = std::getenv(name);
     return v == nullptr || *v == '\0' ? dflt : std::strcmp(v, "0") != 0;
+}
+
+// Heavy-tile launch of the binned cull trace (work items, waves per block); measurement knobs.
+unsigned HeavyItemsFromEnv() {
+    const char* v = std::getenv("SRT_CULL_HEAVY");
+    return v == nullptr || *v == '\0' ? 0u : static_cast<unsigned>(std::strtoul(v, nullptr, 10));
+}
+int HeavyWavesFromEnv() {
+    const char* v = std::getenv("SRT_CULL_HEAVY_WAVES");
+    const int w = v == nullptr || *v == '\0' ? 16 : std::atoi(v);
+    return w == 4 || w == 8 ? w : 16;
 }
 
 // Waves per trace block; env SRT_CULL_WAVES = 4, 8 or 16 (default 4), for measurement.
@@ -2236,6 +2251,36 @@ hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_ver
             p.bin_counts = bins->counts;
             p.large_list = bins->large_list;
             p.bin_capacity = bins->capacity;
+        }
+        p.tiles_x = static_cast<int>(gx);
+        p.tiles = gx * gy;
+        p.item_base = 0u;
+        // Binned, measurement option (env SRT_CULL_HEAVY = n > 0, default off): the first n
+        // work items of the tile order (the heaviest) run as their own launch with wide blocks
+        // (SRT_CULL_HEAVY_WAVES: 16 or 8 waves), the rest follow with 4-wave blocks; the trace
+        // events span both launches. Measured slower at every split tried (n = 128..512: the
+        // heavy blocks are latency-bound, 16 waves cut their time only 1.4x), so it is off.
+        const unsigned items = gx * gy * kParts;
+        const unsigned heavy = p.tile_order != nullptr ? std::min(items, HeavyItemsFromEnv()) : 0u;
+        if (heavy != 0u) {
+            const int hw = HeavyWavesFromEnv();
+            hipEvent_t stop = heavy == items ? ev.end : nullptr;
+            if constexpr (kBlockRows >= 16) {
+                if (hw == 16) {
+                    Launch(TraceCullKernel<16>, dim3(heavy), dim3(kWave * 16), stream, ev.begin, stop, p);
+                }
+            }
+            if (hw == 8 || (hw == 16 && kBlockRows < 16)) {
+                Launch(TraceCullKernel<8>, dim3(heavy), dim3(kWave * 8), stream, ev.begin, stop, p);
+            } else if (hw == 4) {
+                Launch(TraceCullKernel<4>, dim3(heavy), dim3(kWave * 4), stream, ev.begin, stop, p);
+            }
+            if (heavy == items) {
+                return hipGetLastError();
+            }
+            p.item_base = heavy;
+            Launch(TraceCullKernel<4>, dim3(items - heavy), dim3(kWave * 4), stream, nullptr, ev.end, p);
+            return hipGetLastError();
         }
         // One block per (tile, part): gridDim.x = tile columns, gridDim.y = tile rows x parts.
         const dim3 grid(gx, gy * kParts);
