@@ -39,7 +39,8 @@ EDGE_BYTES_PER_TRI = 36      # 9 fp32 edge coefficients per ray-
 PIXEL_IO_BYTES = 8 + 16      # sample offsets in + RGBA out per ray
 FLOPS_PER_TEST = 12          # 3 edge functions x 2 FMA
 GOLDEN = 0.6180339887498949  # temporal jitter sequence step
-KERNEL_NAMES = {"lds": "TraceLdsKernel", "scalar": "TraceScalarKernel", "cull": "TraceCullKernel"}
+KERNEL_NAMES = {"lds": "TraceLdsKernel", "scalar": "TraceScalarKernel", "cull": "TraceCullKernel",
+                "bvh": "TraceBvhKernel"}
 
 
 def parse():

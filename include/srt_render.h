@@ -28,6 +28,7 @@ extern "C" {
 #define SRT_TRACE_LDS 0
 #define SRT_TRACE_SCALAR 1
 #define SRT_TRACE_CULL 2 /* hierarchical block/lane/ray cull; bit-identical output */
+#define SRT_TRACE_BVH 3  /* screen-space 8-wide BVH, wave-packet traversal; bit-identical output */
 
 ML_API_ENTRY const char* srtGetLastError(void);
 

@@ -27,6 +27,7 @@ SRT_SCENE_SOUP = 2
 SRT_TRACE_LDS = 0
 SRT_TRACE_SCALAR = 1
 SRT_TRACE_CULL = 2
+SRT_TRACE_BVH = 3
 
 
 class ImageInfo(ctypes.Structure):

@@ -58,6 +58,7 @@ enum TraceVariant : int {
     kTraceLds = 0,     // LDS-tiled triangle stream, every ray tests every record
     kTraceScalar = 1,  // wave-uniform scalar-cache triangle stream, no LDS, 1 wave per block
     kTraceCull = 2,    // hierarchical: block-box cull of every record, compacted survivors in LDS
+    kTraceBvh = 3,     // screen-space 8-wide BVH over the records in spatial order, wave-packet traversal
 };
 
 struct BandArgs {
@@ -133,7 +134,21 @@ struct StageEvents {
 hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_vertices, const float* d_albedo,
                        const Frame& frame, const float background[3], const BandArgs& band, int variant,
                        const CullBins* bins, hipStream_t stream, const StageEvents* events = nullptr,
-                       const unsigned* prepare_rank = nullptr);
+                       const unsigned* prepare_rank = nullptr, void* bvh = nullptr);
+
+// Screen-space BVH (render.hip "BVH variant"): an implicit 8-wide tree over the cull records
+// in spatial order. Level 0 node i = records [8i, 8i+8); level L node i = level L-1 nodes
+// [8i, 8i+8); the top level has one node. Per node: screen box (float4) + depth lower bound.
+constexpr int kBvhWidth = 8;
+constexpr int kBvhMaxLevels = 16;
+struct BvhLayout {
+    unsigned levels = 0;                  // levels (the last one holds the root)
+    unsigned count[kBvhMaxLevels] = {};   // nodes per level
+    unsigned offset[kBvhMaxLevels] = {};  // first node of each level in the node arrays
+    unsigned nodes = 0;                   // total
+};
+BvhLayout MakeBvhLayout(std::uint64_t n);
+std::size_t BvhBytes(std::uint64_t n);  // node boxes (16 B) + depth bounds (4 B), 256-B aligned
 
 // Element-wise IEEE binary16 <-> binary32 conversion on the device (ML_FLOAT16 images):
 // float -> half rounds to nearest even (overflow -> inf, NaN stays NaN); half -> float is exact.

@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <algorithm>
 #include <cstring>
+#include <stdexcept>
 
 namespace srt {
 
@@ -56,6 +57,7 @@ struct TraceParams {
     const float2* __restrict__ offsets;
     float4* __restrict__ out;
     unsigned n_pad;   // records in the edge buffer (multiple of kPadTriangles)
+    unsigned n;       // records in the scene
     int tiles_x;         // cull tiles per tile row of the band
     unsigned tiles;      // cull tiles of the band
     unsigned item_base;  // cull trace: first work item (position in the tile order) of this launch
@@ -1962,6 +1964,262 @@ __global__ __launch_bounds__(kWave * W, 4) void TraceCullKernel(TraceParams p) {
     ShadeAndStore<R>(p, x, y0, s);
 }
 
+// ---------------------------------------------------------------------------------------
+// BVH variant: primary rays share the eye, so the closest-hit search
+// is a 2-D query over the records' screen boxes. The tree is implicit and 8 wide over the
+// cull records in the scene's spatial (Morton) order -- no sort, no topology arrays; only the
+// node boxes and depth bounds are refitted per frame (BvhLeafKernel: leaves + level 1 in one
+// pass; BvhUpperKernel: one block for the remaining levels). Traversal is wave-uniform: a
+// wave owns a 16 x 16 square of rays (4 per lane), tests child boxes against the wave's ray
+// box, keeps its stack in LDS and reads node data with wave-uniform loads; at a leaf every
+// ray runs the exact test on the records that pass the wave-box tests (ExactTestAnyOrder:
+// (t, id) minimum in any order). A child whose depth lower bound exceeds the largest best t
+// of the wave's rays is skipped: it can neither win nor tie at any of them. Bit-identical to
+// brute force by the same arguments as the cull variant.
+// ---------------------------------------------------------------------------------------
+struct BvhParams {
+    const CullRecord* __restrict__ cull;  // records in spatial order
+    float4* __restrict__ boxes;           // all levels
+    float* __restrict__ tlo;              // all levels
+    BvhLayout layout;
+    unsigned n;
+};
+
+// Exact lower bound of the t any pixel of the box can compute for a record. With u = 2^-24
+// and M = sum_k (|c0_k| + max|fx| |cx_k| + max|fy| |cy_k|) over the box: each computed edge
+// function (two fma roundings) is within 2.01 u M_k of the exact affine E_k; a hit has all
+// computed E_k >= 0, so the computed det = (E_A + E_B) + E_C (two rounded adds of nonnegative
+// terms) is <= (1 + 2.01 u) (det_exact + 2.01 u M), and det_exact = S0 + Sx fx + Sy fy is at
+// most its value at the box corner picked by the signs of (Sx, Sy). Evaluated in double with
+// a 1e-15 relative pad for the double roundings; then every hit in the box has det <= det_max
+// and t = fl(vol / det) >= round_down(vol / det_max) (vol > 0; rounding is monotone).
+// No hit possible: +inf. Unbounded box or non-finite data: 0 (never culls).
+__device__ __forceinline__ float DepthLowerBound(const float4& box, const CullRecord& r) {
+    constexpr double u = 0x1p-24;
+    const float c0[3] = {r.a.x, r.a.w, r.b.z}, cx[3] = {r.a.y, r.b.x, r.b.w}, cy[3] = {r.a.z, r.b.y, r.x.x};
+    double s0 = 0.0, sx = 0.0, sy = 0.0, m0 = 0.0, mx = 0.0, my = 0.0;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        s0 += c0[k];
+        sx += cx[k];
+        sy += cy[k];
+        m0 += fabs(static_cast<double>(c0[k]));
+        mx += fabs(static_cast<double>(cx[k]));
+        my += fabs(static_cast<double>(cy[k]));
+    }
+    const double fx = sx >= 0.0 ? box.y : box.x;
+    const double fy = sy >= 0.0 ? box.w : box.z;
+    const double ax = fmax(fabs(static_cast<double>(box.x)), fabs(static_cast<double>(box.y)));
+    const double ay = fmax(fabs(static_cast<double>(box.z)), fabs(static_cast<double>(box.w)));
+    const double m = m0 + ax * mx + ay * my;
+    const double det = s0 + sx * fx + sy * fy;
+    const double x = det + 1e-15 * (fabs(det) + m) + 2.01 * u * m + 1e-300;
+    if (!(x > 0.0)) {
+        return x <= 0.0 ? __builtin_inff() : 0.f;
+    }
+    const double t = static_cast<double>(r.x.y) / (x * (1.0 + 2.01 * u) * (1.0 + 1e-15));
+    return t == t ? __double2float_rd(t) : 0.f;
+}
+
+__device__ __forceinline__ float4 BoxUnion(const float4& a, const float4& b) {
+    return make_float4(fminf(a.x, b.x), fmaxf(a.y, b.y), fminf(a.z, b.z), fmaxf(a.w, b.w));
+}
+
+// Leaves (one thread each) and level 1 (the first 32 threads of each 256-thread block).
+__global__ __launch_bounds__(256) void BvhLeafKernel(BvhParams p) {
+    __shared__ float4 box[256];
+    __shared__ float lo[256];
+    const unsigned tid = threadIdx.x;
+    const unsigned leaf = blockIdx.x * 256 + tid;
+    const unsigned nleaf = p.layout.count[0];
+    float4 b = make_float4(__builtin_inff(), -__builtin_inff(), __builtin_inff(), -__builtin_inff());
+    float t = __builtin_inff();
+    if (leaf < nleaf) {
+        const unsigned r1 = min(p.n, (leaf + 1) * kBvhWidth);
+        for (unsigned r = leaf * kBvhWidth; r < r1; ++r) {
+            const CullRecord cr = p.cull[r];
+            if (cr.sb.x <= cr.sb.y && cr.sb.z <= cr.sb.w) {  // else disabled: never hit
+                b = BoxUnion(b, cr.sb);
+                t = fminf(t, DepthLowerBound(cr.sb, cr));
+            }
+        }
+        p.boxes[p.layout.offset[0] + leaf] = b;
+        p.tlo[p.layout.offset[0] + leaf] = t;
+    }
+    box[tid] = b;
+    lo[tid] = t;
+    __syncthreads();
+    if (p.layout.levels > 1 && tid < 256 / kBvhWidth) {
+        const unsigned node = blockIdx.x * (256 / kBvhWidth) + tid;
+        if (node < p.layout.count[1]) {
+            float4 u = box[tid * kBvhWidth];
+            float v = lo[tid * kBvhWidth];
+#pragma unroll
+            for (int c = 1; c < kBvhWidth; ++c) {
+                u = BoxUnion(u, box[tid * kBvhWidth + c]);
+                v = fminf(v, lo[tid * kBvhWidth + c]);
+            }
+            p.boxes[p.layout.offset[1] + node] = u;
+            p.tlo[p.layout.offset[1] + node] = v;
+        }
+    }
+}
+
+// Levels 2.. in one block, level by level (one workgroup: the barrier orders a level's
+// writes before the next level's reads).
+__global__ __launch_bounds__(1024) void BvhUpperKernel(BvhParams p) {
+    for (unsigned L = 2; L < p.layout.levels; ++L) {
+        const unsigned below = p.layout.offset[L - 1], nb = p.layout.count[L - 1];
+        for (unsigned i = threadIdx.x; i < p.layout.count[L]; i += blockDim.x) {
+            float4 u = make_float4(__builtin_inff(), -__builtin_inff(), __builtin_inff(), -__builtin_inff());
+            float v = __builtin_inff();
+            const unsigned c1 = min(nb, (i + 1) * kBvhWidth);
+            for (unsigned c = i * kBvhWidth; c < c1; ++c) {
+                u = BoxUnion(u, p.boxes[below + c]);
+                v = fminf(v, p.tlo[below + c]);
+            }
+            p.boxes[p.layout.offset[L] + i] = u;
+            p.tlo[p.layout.offset[L] + i] = v;
+        }
+        __threadfence_block();
+        __syncthreads();
+    }
+}
+
+constexpr int kBvhWaves = 4;  // block = 4 waves side by side, 64 columns x 16 rows
+constexpr int kBvhRows = 4;   // rays per lane (lane = one column of a 16 x 16 wave square)
+// Per-wave traversal stack: a pop pushes at most kBvhWidth children, so depth <= 7 L + 1 for
+// L levels; 11 levels cover 8^11 > 2^31 records (the scene-file limit).
+constexpr int kBvhStack = (kBvhWidth - 1) * 11 + 1;
+
+struct BvhTraceArgs {
+    TraceParams t;
+    const float4* __restrict__ boxes;
+    const float* __restrict__ tlo;
+    BvhLayout layout;
+};
+
+// Largest best t over the wave's rays; +inf while any of them has no hit.
+template <int R>
+__device__ __forceinline__ float WaveMaxBestT(const Rays<R>& s) {
+    float m = s.bt[0];
+#pragma unroll
+    for (int r = 1; r < R; ++r) {
+        m = fmaxf(m, s.bt[r]);
+    }
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+        m = fmaxf(m, __shfl_xor(m, o));
+    }
+    return m;
+}
+
+template <bool SHARED>
+__device__ __forceinline__ void BvhWalk(const BvhTraceArgs& a, Rays<kBvhRows>& s, const Box& wb, bool wb_usable,
+                                        unsigned* stack) {
+    const TraceParams& p = a.t;
+    const int lane = threadIdx.x & (kWave - 1);
+    const unsigned top = a.layout.levels - 1;
+    if (lane == 0) {
+        stack[0] = top << 28;
+    }
+    int sp = 1;
+    // Depth cut, only with a usable wave box: the screen boxes (and the depth bounds computed
+    // over them) bound only rays with |fx|, |fy| <= kScreenBoxRange.
+    float wave_t = __builtin_inff();
+    while (sp > 0) {
+        --sp;
+        const unsigned e = __builtin_amdgcn_readfirstlane(stack[sp]);
+        const unsigned level = e >> 28, idx = e & 0x0FFFFFFFu;
+        if (level == 0) {
+            const unsigned r1 = min(p.n, (idx + 1) * kBvhWidth);
+            bool tested = false;
+            for (unsigned r = idx * kBvhWidth; r < r1; ++r) {
+                const CullRecord cr = p.cull[r];
+                const Record q{cr.a.x, cr.a.y, cr.a.z, cr.a.w, cr.b.x, cr.b.y, cr.b.z, cr.b.w, cr.x.x};
+                if ((wb_usable && !ScreenBoxOverlaps(wb, cr.sb)) || !BoxMayHit(wb, q)) {
+                    continue;
+                }
+                ExactTestAnyOrder<kBvhRows, SHARED>(s, q, cr.x.y, __float_as_int(cr.x.z));
+                tested = true;
+            }
+            if (tested && wb_usable) {
+                wave_t = WaveMaxBestT<kBvhRows>(s);
+            }
+            continue;
+        }
+        const unsigned below = a.layout.offset[level - 1], nb = a.layout.count[level - 1];
+        const unsigned c0 = idx * kBvhWidth;
+        // The kept children sorted by depth bound, largest first (a fixed 19-comparator
+        // network on wave-uniform values), then pushed in that order: the nearest pops first,
+        // so the depth cut tightens early. Not kept: key -1 (bounds are >= 0).
+        float kt[kBvhWidth];
+        unsigned ki[kBvhWidth];
+#pragma unroll
+        for (int j = 0; j < kBvhWidth; ++j) {
+            const unsigned c = c0 + j;
+            bool keep = false;
+            float ct = 0.f;
+            if (c < nb) {
+                const float4 cb = a.boxes[below + c];
+                ct = a.tlo[below + c];
+                keep = wb_usable ? (ScreenBoxOverlaps(wb, cb) && !(ct > wave_t)) : true;
+            }
+            kt[j] = keep ? ct : -1.f;
+            ki[j] = c;
+        }
+        auto ce = [&](int i, int j) {
+            if (kt[i] < kt[j]) {
+                const float t = kt[i];
+                kt[i] = kt[j];
+                kt[j] = t;
+                const unsigned u = ki[i];
+                ki[i] = ki[j];
+                ki[j] = u;
+            }
+        };
+        ce(0, 2); ce(1, 3); ce(4, 6); ce(5, 7);
+        ce(0, 4); ce(1, 5); ce(2, 6); ce(3, 7);
+        ce(0, 1); ce(2, 3); ce(4, 5); ce(6, 7);
+        ce(2, 4); ce(3, 5);
+        ce(1, 4); ce(3, 6);
+        ce(1, 2); ce(3, 4); ce(5, 6);
+#pragma unroll
+        for (int j = 0; j < kBvhWidth; ++j) {
+            if (kt[j] >= 0.f) {
+                if (lane == 0) {
+                    stack[sp] = ((level - 1) << 28) | ki[j];
+                }
+                ++sp;
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(kWave * kBvhWaves) void TraceBvhKernel(BvhTraceArgs a) {
+    __shared__ unsigned stacks[kBvhWaves][kBvhStack];
+    constexpr int R = kBvhRows;
+    const TraceParams& p = a.t;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    // Wave footprint: a 16 x 16 square of rays (the fewest records overlap a square); lane =
+    // column lane % 16, rows (lane / 16) * 4 .. + 3.
+    const int x = blockIdx.x * kWave + wave * 16 + (lane & 15);
+    const int y0 = blockIdx.y * (4 * R) + (lane >> 4) * R;
+    Rays<R> s;
+    Box lane_box;
+    const bool same = GenerateRays<R>(p, x, y0, s, lane_box);
+    const Box wb = WaveReduceBox(lane_box);
+    if (p.n != 0u && static_cast<int>(blockIdx.y) * 4 * R < p.row_count) {
+        if (__all(same)) {
+            BvhWalk<true>(a, s, wb, ScreenBoxUsable(wb), stacks[wave]);
+        } else {
+            BvhWalk<false>(a, s, wb, ScreenBoxUsable(wb), stacks[wave]);
+        }
+    }
+    ShadeAndStore<R>(p, x, y0, s);
+}
+
 // Boolean env switch ("0" = off), for measurement of alternatives.
 bool EnvFlag(const char* name, bool dflt) {
     const char* v = std::getenv(name);
@@ -2080,6 +2338,34 @@ hipError_t LaunchPrepare(const float* d_vertices, const unsigned* d_rank, std::u
     return hipGetLastError();
 }
 
+BvhLayout MakeBvhLayout(std::uint64_t n) {
+    BvhLayout l;
+    std::uint64_t below = n == 0 ? 1 : n;
+    unsigned offset = 0;
+    do {
+        const std::uint64_t c = (below + kBvhWidth - 1) / kBvhWidth;
+        if (l.levels == kBvhMaxLevels) {
+            throw std::runtime_error("BVH too deep");
+        }
+        l.count[l.levels] = static_cast<unsigned>(c);
+        l.offset[l.levels] = offset;
+        offset += static_cast<unsigned>(c);
+        ++l.levels;
+        below = c;
+    } while (below > 1);
+    l.nodes = offset;
+    return l;
+}
+
+namespace {
+std::size_t BvhBoxBytes(const BvhLayout& l) { return (static_cast<std::size_t>(l.nodes) * 16 + 255) / 256 * 256; }
+}  // namespace
+
+std::size_t BvhBytes(std::uint64_t n) {
+    const BvhLayout l = MakeBvhLayout(n);
+    return BvhBoxBytes(l) + (static_cast<std::size_t>(l.nodes) * 4 + 255) / 256 * 256;
+}
+
 std::size_t CullTiles(std::size_t width, std::size_t row_count) {
     return (width + kWave - 1) / kWave * ((row_count + kTileRows - 1) / kTileRows);
 }
@@ -2150,7 +2436,7 @@ CullBins CullBinLayout(void* base, std::uint64_t n, std::size_t width, std::size
 hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_vertices, const float* d_albedo,
                        const Frame& frame, const float background[3], const BandArgs& band, int variant,
                        const CullBins* bins, hipStream_t stream, const StageEvents* events,
-                       const unsigned* prepare_rank) {
+                       const unsigned* prepare_rank, void* bvh) {
     if (band.row_count == 0 || band.width == 0) {
         return hipSuccess;
     }
@@ -2190,7 +2476,35 @@ hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_ver
         p.dv[k] = frame.dv[k];
         p.bg[k] = background[k];
     }
+    p.n = static_cast<unsigned>(n);
     const unsigned gx = static_cast<unsigned>((band.width + kWave - 1) / kWave);
+    if (variant == kTraceBvh) {
+        if (bvh == nullptr) {
+            return hipErrorInvalidValue;
+        }
+        BvhParams bp{};
+        bp.cull = p.cull;
+        bp.layout = MakeBvhLayout(n);
+        bp.boxes = static_cast<float4*>(bvh);
+        bp.tlo = reinterpret_cast<float*>(static_cast<unsigned char*>(bvh) + BvhBoxBytes(bp.layout));
+        bp.n = static_cast<unsigned>(n);
+        if (n != 0) {
+            Launch(BvhLeafKernel, dim3((bp.layout.count[0] + 255) / 256), dim3(256), stream, ev.bin_begin,
+                   bp.layout.levels > 2 ? nullptr : ev.bin_end, bp);
+            if (bp.layout.levels > 2) {
+                Launch(BvhUpperKernel, dim3(1), dim3(1024), stream, nullptr, ev.bin_end, bp);
+            }
+        }
+        BvhTraceArgs a{};
+        a.t = p;
+        a.boxes = bp.boxes;
+        a.tlo = bp.tlo;
+        a.layout = bp.layout;
+        constexpr int kRowsPerBlock = kBvhRows * 4;
+        const unsigned gy = static_cast<unsigned>((band.row_count + kRowsPerBlock - 1) / kRowsPerBlock);
+        Launch(TraceBvhKernel, dim3(gx, gy), dim3(kWave * kBvhWaves), stream, ev.begin, ev.end, a);
+        return hipGetLastError();
+    }
     if (variant == kTraceScalar) {
         const unsigned gy = static_cast<unsigned>((band.row_count + kRowsPerLane - 1) / kRowsPerLane);
         Launch(TraceScalarKernel, dim3(gx, gy), dim3(kWave), stream, ev.begin, ev.end, p);

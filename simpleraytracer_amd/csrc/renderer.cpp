@@ -102,6 +102,9 @@ int TraceVariantFromEnv() {
     if (v != nullptr && (std::strcmp(v, "lds") == 0 || std::strcmp(v, "0") == 0)) {
         return kTraceLds;
     }
+    if (v != nullptr && (std::strcmp(v, "bvh") == 0 || std::strcmp(v, "3") == 0)) {
+        return kTraceBvh;
+    }
     return kTraceCull;
 }
 
@@ -146,6 +149,7 @@ DeviceScene::~DeviceScene() {
     (void)hipFree(m_order);
     (void)hipFree(m_rank);
     (void)hipFree(m_cull_work);
+    (void)hipFree(m_bvh);
     for (hipEvent_t e : m_events) {
         (void)hipEventDestroy(e);
     }
@@ -203,6 +207,9 @@ void DeviceScene::Trace(const float* d_offsets, float* d_rgba, std::size_t row_b
         bins.order = m_order;
         use_bins = &bins;
     }
+    if (variant == kTraceBvh && m_bvh == nullptr && row_count != 0) {
+        m_bvh = DeviceAlloc<unsigned char>(BvhBytes(m_n), "hipMalloc(bvh)");
+    }
     const bool prepare = m_prepare_pending && row_count != 0;
     StageEvents ev{};
     if (m_timing && prepare) {
@@ -212,18 +219,19 @@ void DeviceScene::Trace(const float* d_offsets, float* d_rgba, std::size_t row_b
     }
     if (m_timing) {
         const std::size_t k = 4 * m_timed;
-        ev.bin_begin = use_bins != nullptr ? TimingEvent(m_events, k) : nullptr;
-        ev.bin_end = use_bins != nullptr ? TimingEvent(m_events, k + 1) : nullptr;
+        const bool staged = use_bins != nullptr || (variant == kTraceBvh && m_n != 0);
+        ev.bin_begin = staged ? TimingEvent(m_events, k) : nullptr;
+        ev.bin_end = staged ? TimingEvent(m_events, k + 1) : nullptr;
         ev.begin = TimingEvent(m_events, k + 2);
         ev.end = TimingEvent(m_events, k + 3);
         if (m_binned.size() <= m_timed) {
             m_binned.resize(m_timed + 1);
         }
-        m_binned[m_timed] = use_bins != nullptr;
+        m_binned[m_timed] = staged;
         ++m_timed;
     }
     HipCheck(LaunchTrace(m_edges, m_n, m_vertices, m_albedo, m_frame, m_background, band, variant, use_bins, stream,
-                         m_timing ? &ev : nullptr, prepare ? m_rank : nullptr),
+                         m_timing ? &ev : nullptr, prepare ? m_rank : nullptr, m_bvh),
              "trace kernel launch");
     if (prepare) {
         m_prepare_pending = false;

@@ -77,6 +77,8 @@ private:
     mutable unsigned char* m_cull_work = nullptr;
     mutable std::size_t m_cull_bytes = 0;
     mutable std::uint64_t m_cull_shape = 0;  // (width << 32) | rows of the current carve-up
+    // BVH variant: node boxes + depth bounds (render.h BvhLayout), allocated by the first bvh Trace.
+    mutable unsigned char* m_bvh = nullptr;
     // Stage-timing events, reused: per timed Prepare (begin, end), per timed Trace (bin begin,
     // bin end, begin, end); the first m_prep_timed / m_timed entries hold pending launches.
     hipEvent_t TimingEvent(std::vector<hipEvent_t>& pool, std::size_t i) const;

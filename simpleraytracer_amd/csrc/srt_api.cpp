@@ -190,7 +190,8 @@ ML_API_ENTRY int srtTraceAsync(srt_device_scene scene, const float* d_offsets, f
         if ((d_offsets == nullptr || d_rgba == nullptr) && row_count != 0) {
             throw std::runtime_error("Bad buffer argument");
         }
-        if (variant != SRT_TRACE_LDS && variant != SRT_TRACE_SCALAR && variant != SRT_TRACE_CULL) {
+        if (variant != SRT_TRACE_LDS && variant != SRT_TRACE_SCALAR && variant != SRT_TRACE_CULL &&
+            variant != SRT_TRACE_BVH) {
             throw std::runtime_error("Unknown trace variant " + std::to_string(variant));
         }
         srt::DeviceScene* s = FromHandle(scene);

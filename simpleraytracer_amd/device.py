@@ -16,11 +16,11 @@ import ctypes
 import os
 
 from . import _native
-from ._native import (SRT_SCENE_CORNELL, SRT_SCENE_SOUP, SRT_SCENE_TRIANGLE, SRT_TRACE_CULL, SRT_TRACE_LDS,
-                      SRT_TRACE_SCALAR)
+from ._native import (SRT_SCENE_CORNELL, SRT_SCENE_SOUP, SRT_SCENE_TRIANGLE, SRT_TRACE_BVH, SRT_TRACE_CULL,
+                      SRT_TRACE_LDS, SRT_TRACE_SCALAR)
 
 SCENE_KINDS = {"triangle": SRT_SCENE_TRIANGLE, "cornell": SRT_SCENE_CORNELL, "soup": SRT_SCENE_SOUP}
-TRACE_VARIANTS = {"lds": SRT_TRACE_LDS, "scalar": SRT_TRACE_SCALAR, "cull": SRT_TRACE_CULL}
+TRACE_VARIANTS = {"lds": SRT_TRACE_LDS, "scalar": SRT_TRACE_SCALAR, "cull": SRT_TRACE_CULL, "bvh": SRT_TRACE_BVH}
 SOUP_SEED = 0x5EED  # 100k soup seed; the 1M soup uses SOUP_SEED + 1
 
 

@@ -16,7 +16,7 @@ from scenefile import write_custom_scene
 pytestmark = pytest.mark.gpu
 
 RGB_TOL = 1e-5
-VARIANTS = ("lds", "scalar", "cull")
+VARIANTS = ("lds", "scalar", "cull", "bvh")
 # cull variant modes: (SRT_CULL_BIN, SRT_CULL_RASTER, SRT_CULL_BIN_CAP)
 CULL_MODES = (("1", "1", ""), ("1", "0", ""), ("0", "1", ""), ("0", "0", ""), ("1", "1", "8"), ("1", "0", "8"))
 
@@ -211,6 +211,7 @@ def test_cull_survivor_overflow_and_ties(gpu, tmp_path, monkeypatch):
     for mode in CULL_MODES:
         set_cull_mode(monkeypatch, mode)
         assert_parity(torch_render(path, 300, 40, variant="cull"), ref)
+    assert_parity(torch_render(path, 300, 40, variant="bvh"), ref)
 
 
 def test_cull_nasty_geometry(gpu, tmp_path, monkeypatch):
@@ -239,6 +240,7 @@ def test_cull_nasty_geometry(gpu, tmp_path, monkeypatch):
         for mode in CULL_MODES:
             set_cull_mode(monkeypatch, mode)
             assert_parity(torch_render(path, 120, 90, off, variant="cull"), ref)
+        assert_parity(torch_render(path, 120, 90, off, variant="bvh"), ref)
 
 
 def test_extreme_offsets(gpu, scenes):
@@ -272,7 +274,7 @@ def test_ml_visible_devices_bands_direct(gpu, scenes, monkeypatch):
     monkeypatch.setenv("SRT_GATHER", "direct")
     got = srt.render(scenes["soup2k"], 160, 100)
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
-    for variant in ("scalar", "cull"):
+    for variant in ("scalar", "cull", "bvh"):
         monkeypatch.setenv("SRT_TRACE_VARIANT", variant)
         got2 = srt.render(scenes["soup2k"], 160, 100)
         assert np.array_equal(got2.view(np.uint32), ref.view(np.uint32))
@@ -350,7 +352,7 @@ def test_no_cpu_fallback_marker(gpu):
 
     lib = Path(__file__).resolve().parents[1] / "simpleraytracer_amd" / "lib" / "libModelRunner.so"
     assert b"gfx950" in lib.read_bytes()
-    assert os.environ.get("SRT_TRACE_VARIANT") in (None, "lds", "scalar", "cull", "0", "1", "2")
+    assert os.environ.get("SRT_TRACE_VARIANT") in (None, "lds", "scalar", "cull", "bvh", "0", "1", "2", "3")
 
 
 @pytest.mark.parametrize("variant", VARIANTS)
@@ -377,7 +379,7 @@ def test_stage_timing_does_not_change_the_frame(gpu, scenes, variant):
     scene.close()
     assert n == 3
     assert 0.0 < prep < 1000.0 and 0.0 < trace < 1000.0
-    assert (binning > 0.0) == (variant == "cull")
+    assert (binning > 0.0) == (variant in ("cull", "bvh"))
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
 
 
