@@ -94,7 +94,25 @@ def cpu_baseline(scene_path, a):
     sc.render(a.width, h, row_begin=0, row_count=h, row_step=step, threads=threads)
     dt = time.perf_counter() - t0
     rows = (h + step - 1) // step
+    # single-thread scalar variant (BASELINE.md CPU plan (1)): a short row sample
+    step1 = max(1, h // max(1, int(min(a.cpu_seconds / 3.0, 3.0) / max(per_row * threads, 1e-9))))
+    t1 = time.perf_counter()
+    sc.render(a.width, h, row_begin=0, row_count=h, row_step=step1, threads=1)
+    dt1 = time.perf_counter() - t1
+    rows1 = (h + step1 - 1) // step1
+    model = ""
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
     return {
+        "single_thread": {"value": round(rows1 * a.width / dt1 / 1e6, 6), "unit": "Mrays/s", "cores": 1,
+                          "sample": f"{rows1} rows (every {step1}th), {dt1:.1f} s"},
+        "cpu_model": model,
+        "host_cpus": os.cpu_count(),
         "value": round(rows * a.width / dt / 1e6, 6),
         "unit": "Mrays/s",
         "cores": srt_oracle.threads(threads),
@@ -253,6 +271,14 @@ def main():
     brute = None
     if world == 1 and a.brute_steps > 0 and a.variant != "lds":
         brute = Frames(torch, dist, srt, scene, a, "frames", 1, 0, dev, "lds").run(a.brute_steps, 1, timing=True)
+    alt = {}
+    if world == 1 and a.brute_steps > 0:  # the other exact accelerator, same frame
+        for v in ("cull", "bvh"):
+            if v != a.variant:
+                fr = Frames(torch, dist, srt, scene, a, "frames", 1, 0, dev, v)
+                alt[v] = fr.run(a.steps, a.warmup, timing=False)
+                t = fr.run(a.steps, 0, timing=True)
+                alt[v].update({k: t[k] for k in ("prepare_ms", "bin_ms", "trace_ms")})
 
     if rank == 0:
         launch_rays = main_run.row_count * W
@@ -318,7 +344,7 @@ def main():
                           "frame_instrumented": round(r["ms_per_step_instrumented"], 5),
                           "timed_launches": r["launches"],
                           "note": "cull variant: prepare = PrepareInfoKernel (edge records + per-tile info, one "
-                                  "launch), bin = BinTrianglesKernel (its last block orders the tiles), trace_kernel "
+                                  "launch), bin = BinTrianglesKernel + TileOrderKernel, trace_kernel "
                                   "= TraceCullKernel; frame = uninstrumented, frame_instrumented = with the events"},
         }
         if brute is not None:
@@ -331,6 +357,12 @@ def main():
                 "valu_tflops": round(tf, 2), "valu_frac": round(tf / FP32_PEAK_TFLOPS, 4),
                 "note": "north_star design taken literally: every ray tests every triangle, records tiled through LDS",
             }
+        for v, o in alt.items():
+            line[f"variant_{v}"] = {"kernel": KERNEL_NAMES[v], "mrays_per_s": round(o["mrays"], 3),
+                                    "ms_per_step": round(o["ms_per_step"], 5),
+                                    "stages_ms": {"prepare": round(o["prepare_ms"], 5), "bin": round(o["bin_ms"], 5),
+                                                  "trace_kernel": round(o["trace_ms"], 5)},
+                                    "note": "bit-identical frame (tests/test_gpu_parity.py); uninstrumented rate"}
         if other is not None:
             om, o = other
             line[om] = {"mrays_per_s": round(o["mrays"], 4), "ms_per_step": round(o["ms_per_step"], 4),
