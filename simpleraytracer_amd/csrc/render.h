@@ -95,6 +95,7 @@ struct CullBins {
     unsigned* large_list;  // PaddedTriangleCount(n) ids binned to every tile
     unsigned* tile_order;  // tiles x parts: trace launch order of (tile, part), most work first
     unsigned* sync;        // self-resetting counter of finished bin blocks (SRT_ORDER_IN_BIN=1)
+    void* bounds;          // (tiles_x + tiles_y) float2: monotone tile column / row bounds
     unsigned capacity;
     std::size_t tiles;
 };

@@ -1447,6 +1447,7 @@ struct BinParams {
     unsigned* __restrict__ large_list;  // n_pad
     unsigned* __restrict__ tile_order;  // tiles: trace block -> tile (TileOrderKernel)
     unsigned* __restrict__ sync;        // [0] bin blocks done (self-resetting)
+    float2* __restrict__ bounds;        // tiles_x + tiles_y monotone tile column / row bounds (TileBoundsKernel)
     unsigned order_in_bin;              // the bin kernel's last block computes the tile order
     unsigned capacity;
     unsigned n;
@@ -1676,6 +1677,63 @@ __device__ void TileOrderBlock(const BinParams& p) {
     }
 }
 
+// Monotone tile-column and tile-row bounds of the usable tiles' boxes (lo' = suffix minimum,
+// hi' = prefix maximum; both nondecreasing) into out[0 .. nx + ny) (LDS or global). One block
+// of >= 4 waves; `scratch` = 2 (nx + ny) LDS words. Ends with a barrier.
+__device__ void TileBounds(const BinParams& p, unsigned* scratch, float2* out) {
+    const int tid = threadIdx.x;
+    const int nthreads = blockDim.x;
+    const int lane = tid & (kWave - 1);
+    const int wave = tid / kWave;
+    const int nx = p.tiles_x, ny = p.tiles_y;
+    const int tiles = nx * ny;
+    unsigned* col_lo = scratch;
+    unsigned* col_hi = scratch + nx;
+    unsigned* row_lo = scratch + 2 * nx;
+    unsigned* row_hi = scratch + 2 * nx + ny;
+    for (int i = tid; i < nx + ny; i += nthreads) {
+        const bool col = i < nx;
+        const int j = col ? i : i - nx;
+        (col ? col_lo : row_lo)[j] = OrderedBits(__builtin_inff());
+        (col ? col_hi : row_hi)[j] = OrderedBits(-__builtin_inff());
+    }
+    __syncthreads();
+    for (int t = tid; t < tiles; t += nthreads) {
+        const float4 tb = p.tile_info[t].box;
+        if (p.tile_info[t].usable != 0u && tb.x <= tb.y && tb.z <= tb.w) {
+            const int c = t % nx, r = t / nx;
+            atomicMin(&col_lo[c], OrderedBits(tb.x));
+            atomicMax(&col_hi[c], OrderedBits(tb.y));
+            atomicMin(&row_lo[r], OrderedBits(tb.z));
+            atomicMax(&row_hi[r], OrderedBits(tb.w));
+        }
+    }
+    __syncthreads();
+    if (wave == 0) {
+        WaveScanOrdered<false>(col_lo, nx, true, lane);
+    } else if (wave == 1) {
+        WaveScanOrdered<true>(col_hi, nx, false, lane);
+    } else if (wave == 2) {
+        WaveScanOrdered<false>(row_lo, ny, true, lane);
+    } else if (wave == 3) {
+        WaveScanOrdered<true>(row_hi, ny, false, lane);
+    }
+    __syncthreads();
+    for (int i = tid; i < nx + ny; i += nthreads) {
+        const bool col = i < nx;
+        const int j = col ? i : i - nx;
+        out[i] = make_float2(FromOrderedBits(col ? col_lo[j] : row_lo[j]), FromOrderedBits(col ? col_hi[j] : row_hi[j]));
+    }
+    __syncthreads();
+}
+
+// One block: the frame's tile bounds, once, for every bin block (a bin block reducing all
+// tile infos itself costs O(tiles) L2 reads per block: 0.5 GB per frame at C5).
+__global__ __launch_bounds__(1024) void TileBoundsKernel(BinParams p) {
+    __shared__ unsigned scratch[2 * kMaxBoundTiles];
+    TileBounds(p, scratch, p.bounds);
+}
+
 __global__ __launch_bounds__(kBinThreads) void BinTrianglesKernel(BinParams p) {
     __shared__ float2 b[kMaxBoundTiles];
     __shared__ unsigned hist[kMaxBinTiles];
@@ -1683,53 +1741,16 @@ __global__ __launch_bounds__(kBinThreads) void BinTrianglesKernel(BinParams p) {
     const int nx = p.tiles_x, ny = p.tiles_y;
     const int tiles = nx * ny;
 
-    // Prologue: monotone tile-column and tile-row bounds of the usable tiles' boxes
-    // (lo' = suffix minimum, hi' = prefix maximum; both nondecreasing). Every block reduces
-    // the tile infos itself (reading 32 B per tile from L2): cheaper than device-scope
-    // atomics on a few shared addresses, which serialise at the memory side.
-    {
-        const int lane = tid & (kWave - 1);
-        const int wave = tid / kWave;
-        unsigned* col_lo = hist;
-        unsigned* col_hi = hist + nx;
-        unsigned* row_lo = hist + 2 * nx;
-        unsigned* row_hi = hist + 2 * nx + ny;
+    // Prologue: the monotone tile-column and tile-row bounds -- precomputed once per frame by
+    // TileBoundsKernel (p.bounds), or reduced here by every block (SRT_TILE_BOUNDS=0).
+    if (p.bounds != nullptr) {
         for (int i = tid; i < nx + ny; i += kBinThreads) {
-            const bool col = i < nx;
-            const int j = col ? i : i - nx;
-            (col ? col_lo : row_lo)[j] = OrderedBits(__builtin_inff());
-            (col ? col_hi : row_hi)[j] = OrderedBits(-__builtin_inff());
+            b[i] = p.bounds[i];
         }
-        __syncthreads();
-        for (int t = tid; t < tiles; t += kBinThreads) {
-            const float4 tb = p.tile_info[t].box;
-            if (p.tile_info[t].usable != 0u && tb.x <= tb.y && tb.z <= tb.w) {
-                const int c = t % nx, r = t / nx;
-                atomicMin(&col_lo[c], OrderedBits(tb.x));
-                atomicMax(&col_hi[c], OrderedBits(tb.y));
-                atomicMin(&row_lo[r], OrderedBits(tb.z));
-                atomicMax(&row_hi[r], OrderedBits(tb.w));
-            }
-        }
-        __syncthreads();
-        if (wave == 0) {
-            WaveScanOrdered<false>(col_lo, nx, true, lane);
-        } else if (wave == 1) {
-            WaveScanOrdered<true>(col_hi, nx, false, lane);
-        } else if (wave == 2) {
-            WaveScanOrdered<false>(row_lo, ny, true, lane);
-        } else {
-            WaveScanOrdered<true>(row_hi, ny, false, lane);
-        }
-        __syncthreads();
-        for (int i = tid; i < nx + ny; i += kBinThreads) {
-            const bool col = i < nx;
-            const int j = col ? i : i - nx;
-            b[i] = make_float2(FromOrderedBits(col ? col_lo[j] : row_lo[j]),
-                               FromOrderedBits(col ? col_hi[j] : row_hi[j]));
-        }
-        __syncthreads();
+    } else {
+        TileBounds(p, hist, b);
     }
+    __syncthreads();
     for (int t = tid; t < tiles; t += kBinThreads) {
         hist[t] = 0u;
     }
@@ -2391,7 +2412,7 @@ unsigned CullBinCapacity(std::uint64_t n, std::size_t tiles) {
 
 namespace {
 struct BinSizes {
-    std::size_t info, counts, lists, large, order, sync;
+    std::size_t info, counts, lists, large, order, sync, bounds;
 };
 BinSizes CullBinSizes(std::uint64_t n, std::size_t width, std::size_t row_count) {
     const std::size_t tx = (width + kWave - 1) / kWave, ty = (row_count + kTileRows - 1) / kTileRows;
@@ -2404,13 +2425,14 @@ BinSizes CullBinSizes(std::uint64_t n, std::size_t width, std::size_t row_count)
     z.large = al(PaddedTriangleCount(n) * 4);
     z.order = al(tiles * kParts * 4);
     z.sync = al(4);
+    z.bounds = al((tx + ty) * 8);
     return z;
 }
 }  // namespace
 
 std::size_t CullBinBytes(std::uint64_t n, std::size_t width, std::size_t row_count) {
     const BinSizes z = CullBinSizes(n, width, row_count);
-    return z.info + z.counts + z.lists + z.large + z.order + z.sync;
+    return z.info + z.counts + z.lists + z.large + z.order + z.sync + z.bounds;
 }
 
 CullBins CullBinLayout(void* base, std::uint64_t n, std::size_t width, std::size_t row_count) {
@@ -2428,6 +2450,8 @@ CullBins CullBinLayout(void* base, std::uint64_t n, std::size_t width, std::size
     b.tile_order = reinterpret_cast<unsigned*>(w);
     w += z.order;
     b.sync = reinterpret_cast<unsigned*>(w);
+    w += z.sync;
+    b.bounds = w;
     b.tiles = CullTiles(width, row_count);
     b.capacity = CullBinCapacity(n, b.tiles);
     return b;
@@ -2523,6 +2547,7 @@ hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_ver
             b.large_list = bins->large_list;
             b.tile_order = bins->tile_order;
             b.sync = bins->sync;
+            b.bounds = EnvFlag("SRT_TILE_BOUNDS", true) ? static_cast<float2*>(bins->bounds) : nullptr;
             b.capacity = bins->capacity;
             b.n = static_cast<unsigned>(n);
             b.tiles_x = static_cast<int>(gx);
@@ -2549,9 +2574,13 @@ hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_ver
                 Launch(TileInfoKernel, dim3(gx, gy), dim3(kBinThreads), stream, ev.prep_begin, ev.prep_end, b);
             }
             b.order_in_bin = n != 0 && EnvFlag("SRT_ORDER_IN_BIN", false) ? 1u : 0u;
+            if (n != 0 && b.bounds != nullptr) {
+                Launch(TileBoundsKernel, dim3(1), dim3(1024), stream, ev.bin_begin, nullptr, b);
+            }
             if (n != 0) {
                 const unsigned blocks = static_cast<unsigned>((n + kBinThreads - 1) / kBinThreads);
-                Launch(BinTrianglesKernel, dim3(blocks), dim3(kBinThreads), stream, ev.bin_begin,
+                Launch(BinTrianglesKernel, dim3(blocks), dim3(kBinThreads), stream,
+                       b.bounds != nullptr ? nullptr : ev.bin_begin,
                        b.order_in_bin != 0u ? ev.bin_end : nullptr, b);
             }
             if (b.order_in_bin == 0u) {
