@@ -1209,17 +1209,29 @@ __device__ __forceinline__ void PacketWalk(const TraceParams& p, CullShared<W>& 
     const unsigned long long d_t0 = __builtin_amdgcn_s_memtime();
     unsigned long long d_mark = d_t0;
 #endif
+    // Gather loads are software-pipelined one batch ahead: batch b+1's records are requested
+    // before batch b's walk, so their latency hides behind it (heavy tiles take 2 batches).
+    CullRecord nxt[kSlices];
+    auto load_batch = [&](unsigned b0) {
+#pragma unroll
+        for (int e = 0; e < kSlices; ++e) {
+            const unsigned v = b0 + e * kThreads + tid;
+            const unsigned vv = src.begin + (v < total ? v : 0u);
+            nxt[e] = p.cull[vv < src.count1 ? src.list[vv] : src.list2[vv - src.count1]];
+        }
+    };
+    if (total != 0u) {
+        load_batch(0u);
+    }
 #pragma unroll 1
     for (unsigned b0 = 0; b0 < total; b0 += kBatchN) {
-        // Gather: entries b0 + e * kThreads + tid of the block's virtual list, all loads first.
+        // Gather: entries b0 + e * kThreads + tid of the block's virtual list.
         CullRecord cr[kSlices];
         bool pass[kSlices];
 #pragma unroll
         for (int e = 0; e < kSlices; ++e) {
-            const unsigned v = b0 + e * kThreads + tid;
-            pass[e] = v < total;
-            const unsigned vv = src.begin + (pass[e] ? v : 0u);
-            cr[e] = p.cull[vv < src.count1 ? src.list[vv] : src.list2[vv - src.count1]];
+            pass[e] = b0 + e * kThreads + tid < total;
+            cr[e] = nxt[e];
         }
         unsigned bits[kSlices], npk[kSlices];
 #pragma unroll
@@ -1314,6 +1326,9 @@ __device__ __forceinline__ void PacketWalk(const TraceParams& p, CullShared<W>& 
             ++d_batches;
         }
 #endif
+        if (b0 + kBatchN < total) {
+            load_batch(b0 + kBatchN);
+        }
         // Walk this wave's packets [q_begin, q_end), 64 at a time: lane l finds packet q0 + l's
         // survivor (binary search in pre) and fetches its range bits, then the wave takes the
         // packets kPacketIlp at a time (independent chains: all LDS reads issued together; a
@@ -2547,7 +2562,16 @@ hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_ver
             b.large_list = bins->large_list;
             b.tile_order = bins->tile_order;
             b.sync = bins->sync;
-            b.bounds = EnvFlag("SRT_TILE_BOUNDS", true) ? static_cast<float2*>(bins->bounds) : nullptr;
+            // Tile bounds once per frame (TileBoundsKernel) when the bin blocks' own reductions
+            // would cost more: (bin blocks) x (tiles) tile-info reads above 2M (C5: 16M; C3:
+            // 0.4M, where the extra launch costs more than it saves). Env SRT_TILE_BOUNDS=0/1
+            // forces either way.
+            {
+                const std::uint64_t reads = (n + kBinThreads - 1) / kBinThreads * static_cast<std::uint64_t>(gx) * gy;
+                const char* v = std::getenv("SRT_TILE_BOUNDS");
+                const bool once = v != nullptr && *v != '\0' ? std::strcmp(v, "0") != 0 : reads > 2000000ull;
+                b.bounds = once ? static_cast<float2*>(bins->bounds) : nullptr;
+            }
             b.capacity = bins->capacity;
             b.n = static_cast<unsigned>(n);
             b.tiles_x = static_cast<int>(gx);
