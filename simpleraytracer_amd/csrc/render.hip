@@ -690,17 +690,31 @@ constexpr int kTileRows = kCullTileRows;  // cull tile (bins): 64 columns x 32 r
 #endif
 constexpr int kBlockRows = SRT_BLOCK_ROWS;  // trace block: one part of a cull tile
 constexpr int kParts = kTileRows / kBlockRows;
-constexpr int kStreamStep = 2048;  // FULL stream: records per block per step
+// Batch sizes of the cull walks (measured: these keep the trace block at 22 KB of LDS, up to
+// 7 blocks per CU; the earlier 2048 / 512 / 256 took 35 KB, 4 blocks per CU, and 1.7 % longer).
+#ifndef SRT_STREAM_STEP
+#define SRT_STREAM_STEP 1024
+#endif
+#ifndef SRT_PACKET_BATCH
+#define SRT_PACKET_BATCH 256
+#endif
+#ifndef SRT_FLUSH_BATCH
+#define SRT_FLUSH_BATCH 128
+#endif
+constexpr int kStreamStep = SRT_STREAM_STEP;  // FULL stream: records per block per step
 constexpr int kListG = 4;          // LIST stream: ids per lane per step
-constexpr int kPacketBatch = 512;  // packet walk: survivors gathered per batch
+constexpr int kPacketBatch = SRT_PACKET_BATCH;  // packet walk: survivors gathered per batch
 static_assert(kPadTriangles % kStreamStep == 0, "a stream step must cover whole pad units");
+
+// Block widths a build supports: at least one ray per lane and two streamed records per lane.
+constexpr bool CullWavesOk(int w) { return kBlockRows / w >= 1 && kStreamStep / (kWave * w) >= 2; }
 
 template <int W>
 struct CullShape {
     static constexpr int kR = kBlockRows / W;             // rays per lane
     static constexpr int kThreads = kWave * W;
     static constexpr int kStreamG = kStreamStep / kThreads;  // FULL: records per lane per step
-    static constexpr int kBatch = 256;                    // survivors gathered per flush batch
+    static constexpr int kBatch = SRT_FLUSH_BATCH;        // survivors gathered per flush batch
     static constexpr int kShare = kBatch / W;             // raster walk: batch entries per wave
     static constexpr int kListStep = kThreads * kListG;     // LIST stream: ids per block per step
     static constexpr int kPBatch = kThreads > kPacketBatch ? kThreads : kPacketBatch;  // packet walk batch
@@ -2632,12 +2646,12 @@ hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_ver
         if (heavy != 0u) {
             const int hw = HeavyWavesFromEnv();
             hipEvent_t stop = heavy == items ? ev.end : nullptr;
-            if constexpr (kBlockRows >= 16) {
+            if constexpr (CullWavesOk(16)) {
                 if (hw == 16) {
                     Launch(TraceCullKernel<16>, dim3(heavy), dim3(kWave * 16), stream, ev.begin, stop, p);
                 }
             }
-            if (hw == 8 || (hw == 16 && kBlockRows < 16)) {
+            if (hw == 8 || (hw == 16 && !CullWavesOk(16))) {
                 Launch(TraceCullKernel<8>, dim3(heavy), dim3(kWave * 8), stream, ev.begin, stop, p);
             } else if (hw == 4) {
                 Launch(TraceCullKernel<4>, dim3(heavy), dim3(kWave * 4), stream, ev.begin, stop, p);
@@ -2652,13 +2666,13 @@ hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_ver
         // One block per (tile, part): gridDim.x = tile columns, gridDim.y = tile rows x parts.
         const dim3 grid(gx, gy * kParts);
         const int waves = CullWavesFromEnv();
-        if constexpr (kBlockRows >= 16) {
+        if constexpr (CullWavesOk(16)) {
             if (waves == 16) {
                 Launch(TraceCullKernel<16>, grid, dim3(kWave * 16), stream, ev.begin, ev.end, p);
                 return hipGetLastError();
             }
         }
-        if constexpr (kBlockRows >= 8) {
+        if constexpr (CullWavesOk(8)) {
             if (waves == 8) {
                 Launch(TraceCullKernel<8>, grid, dim3(kWave * 8), stream, ev.begin, ev.end, p);
                 return hipGetLastError();
