@@ -60,7 +60,6 @@ struct TraceParams {
     unsigned n;       // records in the scene
     int tiles_x;         // cull tiles per tile row of the band
     unsigned tiles;      // cull tiles of the band
-    unsigned item_base;  // cull trace: first work item (position in the tile order) of this launch
     unsigned n_tiles; // tiles holding at least one real record (>= 1)
     int width;
     int row_count;
@@ -1911,7 +1910,7 @@ __global__ __launch_bounds__(kWave * W, 4) void TraceCullKernel(TraceParams p) {
     __shared__ CullShared<W> sh;
     // Block = one part (kBlockRows rows) of a cull tile (kTileRows rows); launched in the
     // tile order's work order when the frame is binned.
-    const unsigned linear = blockIdx.y * gridDim.x + blockIdx.x + p.item_base;
+    const unsigned linear = blockIdx.y * gridDim.x + blockIdx.x;
     const unsigned item = p.tile_order != nullptr ? p.tile_order[linear] : linear;
     const unsigned tile = item / kParts;
     const int tx = static_cast<int>(tile % static_cast<unsigned>(p.tiles_x));
@@ -2276,17 +2275,6 @@ bool EnvFlag(const char* name, bool dflt) {
     return v == nullptr || *v == '\0' ? dflt : std::strcmp(v, "0") != 0;
 }
 
-// Heavy-tile launch of the binned cull trace (work items, waves per block); measurement knobs.
-unsigned HeavyItemsFromEnv() {
-    const char* v = std::getenv("SRT_CULL_HEAVY");
-    return v == nullptr || *v == '\0' ? 0u : static_cast<unsigned>(std::strtoul(v, nullptr, 10));
-}
-int HeavyWavesFromEnv() {
-    const char* v = std::getenv("SRT_CULL_HEAVY_WAVES");
-    const int w = v == nullptr || *v == '\0' ? 16 : std::atoi(v);
-    return w == 4 || w == 8 ? w : 16;
-}
-
 // Waves per trace block; env SRT_CULL_WAVES = 4, 8 or 16 (default 4), for measurement.
 int CullWavesFromEnv() {
     const char* v = std::getenv("SRT_CULL_WAVES");
@@ -2635,34 +2623,6 @@ hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_ver
         }
         p.tiles_x = static_cast<int>(gx);
         p.tiles = gx * gy;
-        p.item_base = 0u;
-        // Binned, measurement option (env SRT_CULL_HEAVY = n > 0, default off): the first n
-        // work items of the tile order (the heaviest) run as their own launch with wide blocks
-        // (SRT_CULL_HEAVY_WAVES: 16 or 8 waves), the rest follow with 4-wave blocks; the trace
-        // events span both launches. Measured slower at every split tried (n = 128..512: the
-        // heavy blocks are latency-bound, 16 waves cut their time only 1.4x), so it is off.
-        const unsigned items = gx * gy * kParts;
-        const unsigned heavy = p.tile_order != nullptr ? std::min(items, HeavyItemsFromEnv()) : 0u;
-        if (heavy != 0u) {
-            const int hw = HeavyWavesFromEnv();
-            hipEvent_t stop = heavy == items ? ev.end : nullptr;
-            if constexpr (CullWavesOk(16)) {
-                if (hw == 16) {
-                    Launch(TraceCullKernel<16>, dim3(heavy), dim3(kWave * 16), stream, ev.begin, stop, p);
-                }
-            }
-            if (hw == 8 || (hw == 16 && !CullWavesOk(16))) {
-                Launch(TraceCullKernel<8>, dim3(heavy), dim3(kWave * 8), stream, ev.begin, stop, p);
-            } else if (hw == 4) {
-                Launch(TraceCullKernel<4>, dim3(heavy), dim3(kWave * 4), stream, ev.begin, stop, p);
-            }
-            if (heavy == items) {
-                return hipGetLastError();
-            }
-            p.item_base = heavy;
-            Launch(TraceCullKernel<4>, dim3(items - heavy), dim3(kWave * 4), stream, nullptr, ev.end, p);
-            return hipGetLastError();
-        }
         // One block per (tile, part): gridDim.x = tile columns, gridDim.y = tile rows x parts.
         const dim3 grid(gx, gy * kParts);
         const int waves = CullWavesFromEnv();
