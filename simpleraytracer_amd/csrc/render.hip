@@ -697,6 +697,9 @@ constexpr int kParts = kTileRows / kBlockRows;
 #ifndef SRT_PACKET_BATCH
 #define SRT_PACKET_BATCH 256
 #endif
+#ifndef SRT_PACKET_ILP
+#define SRT_PACKET_ILP 4  // packet walk: packets evaluated together per wave (independent chains)
+#endif
 #ifndef SRT_FLUSH_BATCH
 #define SRT_FLUSH_BATCH 128
 #endif
@@ -1230,6 +1233,12 @@ __device__ __forceinline__ void PacketWalk(const TraceParams& p, CullShared<W>& 
         for (int e = 0; e < kSlices; ++e) {
             const unsigned v = b0 + e * kThreads + tid;
             const unsigned vv = src.begin + (v < total ? v : 0u);
+#ifdef SRT_DIAG
+            if (p.exp & 256u) {  // timing experiment: coalesced loads (results wrong)
+                nxt[e] = p.cull[(vv & 0xFFFFu) % p.n];
+                continue;
+            }
+#endif
             nxt[e] = p.cull[vv < src.count1 ? src.list[vv] : src.list2[vv - src.count1]];
         }
     };
@@ -1346,7 +1355,7 @@ __device__ __forceinline__ void PacketWalk(const TraceParams& p, CullShared<W>& 
         // survivor (binary search in pre) and fetches its range bits, then the wave takes the
         // packets kPacketIlp at a time (independent chains: all LDS reads issued together; a
         // tail repeats the last packet, harmless under an atomic min) and applies the hits.
-        constexpr int kPacketIlp = 4;
+        constexpr int kPacketIlp = SRT_PACKET_ILP;
         unsigned q_begin = wave * n_pk / W, q_end = (wave + 1) * n_pk / W;
 #ifdef SRT_DIAG
         if (p.exp & 64u) {
