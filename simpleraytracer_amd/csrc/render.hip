@@ -97,6 +97,7 @@ struct PrepareParams {
     float base[3];
     float du[3];
     float dv[3];
+    unsigned exp;  // diagnostic build: experiment bits (env SRT_EXP), 0 in the product
 };
 
 // One edge record as the trace kernels consume it.
@@ -250,8 +251,17 @@ __device__ __forceinline__ void PrepareRecord(const PrepareParams& p, unsigned i
     p2[j] = c[8];
     p3[j] = vol;
     // Disabled records: an empty box (culled by every ray box the screen boxes apply to).
-    const float4 sb = disabled ? make_float4(__builtin_inff(), -__builtin_inff(), __builtin_inff(), -__builtin_inff())
-                               : ScreenBox(c);
+    float4 sb = disabled ? make_float4(__builtin_inff(), -__builtin_inff(), __builtin_inff(), -__builtin_inff())
+                         : make_float4(0.f, 0.f, 0.f, 0.f);
+#ifdef SRT_DIAG
+    if ((p.exp & 512u) == 0u && !disabled) {  // timing experiment: 512 skips the screen box
+        sb = ScreenBox(c);
+    }
+#else
+    if (!disabled) {
+        sb = ScreenBox(c);
+    }
+#endif
     p.screen_boxes[i] = sb;
     // Stored as (hi, -lo) pairs so the cull test is one saturating packed add per axis.
     p.qboxes[i] = make_uint2(PackI16(QuantHi(sb.y), -QuantLo(sb.x)), PackI16(QuantHi(sb.w), -QuantLo(sb.z)));
@@ -261,6 +271,12 @@ __device__ __forceinline__ void PrepareRecord(const PrepareParams& p, unsigned i
         r.b = make_float4(c[4], c[5], c[6], c[7]);
         r.x = make_float4(c[8], vol, __uint_as_float(i), 0.f);
         r.sb = sb;
+#ifdef SRT_DIAG
+        if (p.exp & 1024u) {  // timing experiment: coalesced record writes (wrong order)
+            p.cull[i] = r;
+            return;
+        }
+#endif
         p.cull[p.rank[i]] = r;
     }
 }
@@ -2353,6 +2369,11 @@ PrepareParams MakePrepareParams(const float* d_vertices, const unsigned* d_rank,
         p.du[k] = frame.du[k];
         p.dv[k] = frame.dv[k];
     }
+#ifdef SRT_DIAG
+    if (const char* e = std::getenv("SRT_EXP")) {
+        p.exp = static_cast<unsigned>(std::strtoul(e, nullptr, 0));
+    }
+#endif
     return p;
 }
 }  // namespace
