@@ -1695,20 +1695,32 @@ __device__ __forceinline__ unsigned TileWorkBucket(const BinParams& p, unsigned 
     const unsigned total = cnt + large;
     return total == 0u ? 0u : 32u - __builtin_clz(total);
 }
-// One block of any size computes the whole order.
-template <bool kSameKernel>
+// One block of kThreads threads computes the whole order.
+template <bool kSameKernel, int kThreads>
 __device__ void TileOrderBlock(const BinParams& p) {
     __shared__ unsigned start[64];
     const int tid = threadIdx.x;
-    const unsigned nthreads = blockDim.x;
+    const unsigned nthreads = kThreads;  // == blockDim.x
     const unsigned tiles = static_cast<unsigned>(p.tiles_x * p.tiles_y);
     const unsigned large = LoadCount<kSameKernel>(&p.counts[tiles]);
     if (tid < 64) {
         start[tid] = 0u;
     }
+    // Buckets computed once (counts and tile info loaded once), kept in registers for the
+    // placement pass: kMaxBinTiles / blockDim.x tiles per thread at most.
+    constexpr int kPer = kMaxBinTiles / kThreads;
+    unsigned bucket[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const unsigned t = tid + k * nthreads;
+        bucket[k] = t < tiles ? TileWorkBucket<kSameKernel>(p, t, large) : 0u;
+    }
     __syncthreads();
-    for (unsigned t = tid; t < tiles; t += nthreads) {
-        atomicAdd(&start[TileWorkBucket<kSameKernel>(p, t, large)], static_cast<unsigned>(kParts));
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        if (tid + k * nthreads < tiles) {
+            atomicAdd(&start[bucket[k]], static_cast<unsigned>(kParts));
+        }
     }
     __syncthreads();
     unsigned first = 0u;  // tiles in heavier buckets
@@ -1722,10 +1734,14 @@ __device__ void TileOrderBlock(const BinParams& p) {
         start[tid] = first;
     }
     __syncthreads();
-    for (unsigned t = tid; t < tiles; t += nthreads) {
-        const unsigned at = atomicAdd(&start[TileWorkBucket<kSameKernel>(p, t, large)], static_cast<unsigned>(kParts));
-        for (int part = 0; part < kParts; ++part) {
-            p.tile_order[at + part] = t * kParts + part;  // trace work items (tile, part)
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const unsigned t = tid + k * nthreads;
+        if (t < tiles) {
+            const unsigned at = atomicAdd(&start[bucket[k]], static_cast<unsigned>(kParts));
+            for (int part = 0; part < kParts; ++part) {
+                p.tile_order[at + part] = t * kParts + part;  // trace work items (tile, part)
+            }
         }
     }
 }
@@ -1876,7 +1892,7 @@ __global__ __launch_bounds__(kBinThreads) void BinTrianglesKernel(BinParams p) {
     }
     __syncthreads();
     if (last != 0u) {
-        TileOrderBlock<true>(p);
+        TileOrderBlock<true, kBinThreads>(p);
         if (tid == 0) {
             p.sync[0] = 0u;  // ready for the next frame (the kernel boundary orders it)
         }
@@ -1886,7 +1902,7 @@ __global__ __launch_bounds__(kBinThreads) void BinTrianglesKernel(BinParams p) {
 // Standalone order (a band with no records: the bin kernel, which normally computes the
 // order in its last block, is not launched).
 __global__ __launch_bounds__(kOrderThreads) void TileOrderKernel(BinParams p) {
-    TileOrderBlock<false>(p);
+    TileOrderBlock<false, kOrderThreads>(p);
 }
 
 // Candidate source of a tile: LIST (binned, usable box, list complete): the tile's list then
