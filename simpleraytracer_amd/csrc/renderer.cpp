@@ -289,7 +289,22 @@ struct Renderer::Slot {
     std::uint16_t* rgba16 = nullptr;     // FLOAT16 output: band_rows x W x 4 halves
     std::size_t row_begin = 0;
     std::size_t row_count = 0;
+    // Pipelined single-device render (Renderer::RenderPipelined): copy streams and per-chunk
+    // events (H2D done, chunk traced).
+    hipStream_t copy_in = nullptr;
+    hipStream_t copy_out = nullptr;
+    std::vector<hipEvent_t> in_done;
+    std::vector<hipEvent_t> traced;
 };
+
+namespace {
+// Row chunks of the pipelined single-device render: env SRT_E2E_CHUNKS (1 = no pipelining).
+std::size_t E2eChunks() {
+    const char* v = std::getenv("SRT_E2E_CHUNKS");
+    const long c = v == nullptr || *v == '\0' ? 4 : std::strtol(v, nullptr, 10);
+    return c < 1 ? 1 : (c > 16 ? 16 : static_cast<std::size_t>(c));
+}
+}  // namespace
 
 Renderer::Renderer(const Scene& scene, std::vector<int> devices)
     : m_variant(TraceVariantFromEnv()),
@@ -320,6 +335,18 @@ Renderer::~Renderer() {
     for (auto& slot : m_slots) {
         (void)hipSetDevice(slot->device);
         slot->scene.reset();
+        for (hipEvent_t e : slot->in_done) {
+            (void)hipEventDestroy(e);
+        }
+        for (hipEvent_t e : slot->traced) {
+            (void)hipEventDestroy(e);
+        }
+        if (slot->copy_in != nullptr) {
+            (void)hipStreamDestroy(slot->copy_in);
+        }
+        if (slot->copy_out != nullptr) {
+            (void)hipStreamDestroy(slot->copy_out);
+        }
         (void)hipStreamDestroy(slot->stream);
     }
 }
@@ -398,6 +425,10 @@ void Renderer::Render(const void* host_offsets, void* host_rgba) {
     if (!configured()) {
         throw std::runtime_error("Renderer used before Configure()");
     }
+    if (m_slots.size() == 1 && E2eChunks() > 1 && m_height >= 2 * E2eChunks()) {
+        RenderPipelined(host_offsets, host_rgba, E2eChunks());
+        return;
+    }
     const std::size_t w = m_width;
     const std::size_t in_elem = m_in_half ? 2 : 4, out_elem = m_out_half ? 2 : 4;
     const auto* in_bytes = static_cast<const unsigned char*>(host_offsets);
@@ -456,6 +487,62 @@ void Renderer::Render(const void* host_offsets, void* host_rgba) {
         DeviceGuard guard(sp->device);
         HipCheck(hipStreamSynchronize(sp->stream), "render");
     }
+}
+
+// One device: the frame in row chunks, H2D of chunk c+1 and D2H of chunk c-1 overlapping the
+// trace of chunk c (three streams, event-ordered). Every chunk is an ordinary band trace of
+// the same prepared frame, so the image is bit-identical to the unchunked render.
+void Renderer::RenderPipelined(const void* host_offsets, void* host_rgba, std::size_t chunks) {
+    Slot& s = *m_slots.front();
+    DeviceGuard guard(s.device);
+    const std::size_t w = m_width, h = m_height;
+    const std::size_t in_elem = m_in_half ? 2 : 4, out_elem = m_out_half ? 2 : 4;
+    const auto* in_bytes = static_cast<const unsigned char*>(host_offsets);
+    auto* out_bytes = static_cast<unsigned char*>(host_rgba);
+    if (s.copy_in == nullptr) {
+        HipCheck(hipStreamCreateWithFlags(&s.copy_in, hipStreamNonBlocking), "hipStreamCreate(copy in)");
+        HipCheck(hipStreamCreateWithFlags(&s.copy_out, hipStreamNonBlocking), "hipStreamCreate(copy out)");
+    }
+    while (s.in_done.size() < chunks) {
+        hipEvent_t a = nullptr, b = nullptr;
+        HipCheck(hipEventCreateWithFlags(&a, hipEventDisableTiming), "hipEventCreate(chunk)");
+        HipCheck(hipEventCreateWithFlags(&b, hipEventDisableTiming), "hipEventCreate(chunk)");
+        s.in_done.push_back(a);
+        s.traced.push_back(b);
+    }
+    const std::size_t rows = (h + chunks - 1) / chunks;
+    s.scene->Prepare(w, h, s.stream);
+    for (std::size_t c = 0; c < chunks; ++c) {
+        const std::size_t r0 = c * rows;
+        if (r0 >= h) {
+            break;
+        }
+        const std::size_t n = std::min(rows, h - r0);
+        const std::size_t count = n * w * 2;
+        void* dst = m_in_half ? static_cast<void*>(s.offsets16 + r0 * w * 2) : static_cast<void*>(s.offsets + r0 * w * 2);
+        HipCheck(hipMemcpyAsync(dst, in_bytes + r0 * w * 2 * in_elem, count * in_elem, hipMemcpyHostToDevice, s.copy_in),
+                 "hipMemcpyAsync(offsets chunk H2D)");
+        HipCheck(hipEventRecord(s.in_done[c], s.copy_in), "hipEventRecord(chunk in)");
+        HipCheck(hipStreamWaitEvent(s.stream, s.in_done[c], 0), "hipStreamWaitEvent(chunk in)");
+        if (m_in_half) {
+            HipCheck(LaunchHalfToFloat(s.offsets16 + r0 * w * 2, s.offsets + r0 * w * 2, count, s.stream),
+                     "offsets f16 -> f32");
+        }
+        s.scene->Trace(s.offsets + r0 * w * 2, s.rgba + r0 * w * 4, r0, n, m_variant, s.stream);
+        if (m_out_half) {
+            HipCheck(LaunchFloatToHalf(s.rgba + r0 * w * 4, s.rgba16 + r0 * w * 4, n * w * 4, s.stream),
+                     "framebuffer f32 -> f16");
+        }
+        HipCheck(hipEventRecord(s.traced[c], s.stream), "hipEventRecord(chunk traced)");
+        HipCheck(hipStreamWaitEvent(s.copy_out, s.traced[c], 0), "hipStreamWaitEvent(chunk traced)");
+        const void* src = m_out_half ? static_cast<const void*>(s.rgba16 + r0 * w * 4)
+                                     : static_cast<const void*>(s.rgba + r0 * w * 4);
+        HipCheck(hipMemcpyAsync(out_bytes + r0 * w * 4 * out_elem, src, n * w * 4 * out_elem, hipMemcpyDeviceToHost,
+                                s.copy_out),
+                 "hipMemcpyAsync(frame chunk D2H)");
+    }
+    HipCheck(hipStreamSynchronize(s.copy_out), "render (copy out)");
+    HipCheck(hipStreamSynchronize(s.stream), "render");
 }
 
 }  // namespace srt

@@ -119,6 +119,7 @@ public:
 private:
     struct Slot;
     void ReleaseBuffers();
+    void RenderPipelined(const void* host_offsets, void* host_rgba, std::size_t chunks);
 
     std::vector<std::unique_ptr<Slot>> m_slots;
     std::vector<void*> m_comms;  // ncclComm_t per slot when gathering with RCCL

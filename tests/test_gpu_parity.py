@@ -470,3 +470,24 @@ def test_random_cameras_all_variants(gpu, tmp_path):
         assert (ref[..., 3] >= 0).mean() > 0.02, "camera sees the soup"
         for variant in VARIANTS:
             assert_parity(torch_render(path, w, h, offs, variant=variant), ref)
+
+
+@pytest.mark.parametrize("out_dtype", [0, 1])
+def test_ml_pipelined_chunks_bitwise(gpu, scenes, tmp_path, monkeypatch, out_dtype):
+    """The single-device mlInfer pipeline (row chunks: H2D / trace / D2H overlapped on three
+    streams) gives the unchunked image bit for bit, for chunk counts that do and do not divide
+    the height."""
+    import simpleraytracer_amd as srt
+
+    path = srt.convert_scene(scenes["soup2k"], str(tmp_path / "s.srt"), output_dtype=out_dtype)
+    rng = np.random.default_rng(11)
+    w, h = 150, 101
+    offs = rng.random((h, w, 2), dtype=np.float32)
+    monkeypatch.setenv("SRT_E2E_CHUNKS", "1")
+    ref = srt.render(path, w, h, offs)
+    for chunks in ("2", "4", "7", "16"):
+        monkeypatch.setenv("SRT_E2E_CHUNKS", chunks)
+        got = srt.render(path, w, h, offs)
+        assert np.array_equal(got.view(np.uint8), ref.view(np.uint8)), chunks
+    if out_dtype == 0:
+        assert_parity(ref, oracle_render(path, w, h, offs))
