@@ -12,7 +12,11 @@ every triangle; DESIGN.md section 5, tests/test_gpu_parity.py).
 Multi-GPU, one rank per GPU:
   --mode frames (default): every rank renders whole 1920x1080 frames of a temporal-jitter
       sequence (rank r's frames use the uniform sub-pixel offset J_r; J_0 = 0.5 = the headline
-      frame); no collective in the timed region; "scaling": "weak".
+      frame); no collective in the timed region; "scaling": "weak". Each rank keeps --queues
+      frames in flight (default 3): frame k goes to queue k % Q, a DeviceScene with its own edge
+      records, bins and framebuffer on its own HIP stream, so one frame's stages fill the CUs
+      another frame's heavy-tile tail leaves idle. The one-frame-in-flight rate is reported
+      beside it ("single_queue").
   --mode bands: the frame's rows are split into P bands (north_star row bands), each rank
       traces its band, and the bands are gathered to rank 0 over RCCL every step (double
       buffered, so step k's gather overlaps step k+1's render); "scaling": "strong".
@@ -46,7 +50,7 @@ KERNEL_NAMES = {"lds": "TraceLdsKernel", "scalar": "TraceScalarKernel", "cull": 
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--width", type=int, default=1920)
     p.add_argument("--height", type=int, default=1080)
@@ -54,6 +58,8 @@ def parse():
     p.add_argument("--triangles", type=int, default=100_000)
     p.add_argument("--variant", default=os.environ.get("SRT_BENCH_VARIANT", "cull"), choices=list(KERNEL_NAMES))
     p.add_argument("--mode", default="frames", choices=["frames", "bands"], help="multi-GPU split (see module doc)")
+    p.add_argument("--queues", type=int, default=int(os.environ.get("SRT_BENCH_QUEUES", "3")),
+                   help="frames mode: frame queues in flight per GPU (own scene buffers + HIP stream each)")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample length")
     p.add_argument("--brute-steps", type=int, default=5, help="timed frames of the brute-force LDS kernel (0 = skip)")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -137,7 +143,7 @@ def pmc_traffic(workload, variant):
 class Frames:
     """Timed loop of one multi-GPU mode on this rank (module doc)."""
 
-    def __init__(self, torch, dist, srt, scene, a, mode, world, rank, dev, variant):
+    def __init__(self, torch, dist, srt, scene, a, mode, world, rank, dev, variant, queues=1):
         from simpleraytracer_amd.bands import band_range, band_rows
 
         self.torch, self.dist, self.scene, self.a = torch, dist, scene, a
@@ -160,11 +166,25 @@ class Frames:
         self.pending = [None] * nbuf
         self.stream = torch.cuda.current_stream(dev)
         self.dev = dev
+        # Frame queues (frames mode): queue q = its own DeviceScene (edge records, bins, BVH)
+        # + framebuffer + HIP stream; frame k goes to queue k % Q, so up to Q frames are in
+        # flight and one frame's prepare/bin/trace fills the CUs another frame's heavy-tile
+        # tail leaves idle. Queue 0 is `scene` on the current stream (the Q = 1 loop).
+        self.queues = [(scene, self.stream, self.offsets, self.bands[0])]
+        if mode == "frames":
+            for _ in range(max(1, queues) - 1):
+                self.queues.append((srt.DeviceScene(scene.path, dev.index), torch.cuda.Stream(dev),
+                                    self.offsets.clone(), torch.zeros_like(self.bands[0])))
 
-    def step(self, k):
+    def step(self, k, queues=1):
         from simpleraytracer_amd.bands import gather_bands
 
         a, W, H = self.a, self.a.width, self.a.height
+        if queues > 1:  # frames mode, no collective
+            scene, stream, offsets, band = self.queues[k % queues]
+            scene.prepare(W, H, stream)
+            scene.trace(offsets, band, 0, H, variant=self.variant, stream=stream)
+            return
         slot = k % len(self.bands)
         if self.pending[slot] is not None:
             self.pending[slot].wait()  # the gather still reading this band buffer
@@ -182,10 +202,13 @@ class Frames:
                                                       [out[r * band.shape[0]:(r + 1) * band.shape[0]]
                                                        for r in range(self.world)], dst=0, async_op=True)
 
-    def run(self, steps, warmup, timing=True):
+    def run(self, steps, warmup, timing=True, queues=1):
+        """K timed frames over `queues` frame queues (stage timing: queue 0's events, so
+        timing runs use queues=1)."""
         torch, dist = self.torch, self.dist
-        for k in range(warmup):
-            self.step(k)
+        queues = min(queues, len(self.queues))
+        for k in range(warmup * queues):
+            self.step(k, queues)
         self.drain()
         self.scene.take_stage_times()
         self.scene.set_stage_timing(timing)
@@ -194,7 +217,7 @@ class Frames:
         torch.cuda.synchronize(self.dev)
         t0 = time.perf_counter()
         for k in range(steps):
-            self.step(warmup + k)
+            self.step(warmup * queues + k, queues)
         self.drain()
         torch.cuda.synchronize(self.dev)
         if self.world > 1:
@@ -208,7 +231,12 @@ class Frames:
         launches, prep_ms, bin_ms, trace_ms = self.scene.take_stage_times()
         units = self.a.width * self.a.height * steps * (self.world if self.mode == "frames" else 1)
         return {"elapsed": elapsed, "mrays": units / elapsed / 1e6, "prepare_ms": prep_ms, "bin_ms": bin_ms,
-                "trace_ms": trace_ms, "launches": launches, "ms_per_step": elapsed / steps * 1e3}
+                "trace_ms": trace_ms, "launches": launches, "ms_per_step": elapsed / steps * 1e3, "queues": queues}
+
+    def close(self):
+        for q in self.queues[1:]:
+            q[0].close()
+        self.queues = self.queues[:1]
 
     def drain(self):
         for i, h in enumerate(self.pending):
@@ -251,12 +279,15 @@ def main():
     W, H = a.width, a.height
     wl = workload_name(a)
 
-    main_run = Frames(torch, dist, srt, scene, a, a.mode, world, rank, dev, a.variant)
-    # value: uninstrumented frames. Stage times: the same K frames again with HIP events bound
-    # to the kernels' dispatch packets (each event-bound dispatch leaves a 5-10 us bubble on
-    # the stream, so the instrumented frame is slower; both are reported).
-    r = main_run.run(a.steps, a.warmup, timing=False)
+    main_run = Frames(torch, dist, srt, scene, a, a.mode, world, rank, dev, a.variant, a.queues)
+    # value: uninstrumented frames over the frame queues. Then the same K frames on one queue
+    # (one frame in flight: the per-frame latency), and again with HIP events bound to the
+    # kernels' dispatch packets for the stage times (each event-bound dispatch leaves a 5-10 us
+    # bubble on the stream, so the instrumented frame is slower; all three are reported).
+    r = main_run.run(a.steps, a.warmup, timing=False, queues=a.queues)
+    r1 = main_run.run(a.steps, a.warmup, timing=False) if r["queues"] > 1 else r
     rt = main_run.run(a.steps, 0, timing=True)
+    main_run.close()
     for k in ("prepare_ms", "bin_ms", "trace_ms", "launches"):
         r[k] = rt[k]
     r["ms_per_step_instrumented"] = rt["ms_per_step"]
@@ -264,9 +295,10 @@ def main():
     if world > 1:  # the other multi-GPU mode, same steps (secondary: a failure is reported, not fatal)
         om = "bands" if a.mode == "frames" else "frames"
         try:
-            orun = Frames(torch, dist, srt, scene, a, om, world, rank, dev, a.variant)
-            other = (om, orun.run(a.steps, a.warmup, timing=False))
+            orun = Frames(torch, dist, srt, scene, a, om, world, rank, dev, a.variant, a.queues)
+            other = (om, orun.run(a.steps, a.warmup, timing=False, queues=a.queues))
             ot = orun.run(a.steps, 0, timing=True)
+            orun.close()
             for k in ("prepare_ms", "bin_ms", "trace_ms"):
                 other[1][k] = ot[k]
         except Exception as e:  # noqa: BLE001 -- the primary line must still be printed
@@ -278,9 +310,10 @@ def main():
     if world == 1 and a.brute_steps > 0:  # the other exact accelerator, same frame
         for v in ("cull", "bvh"):
             if v != a.variant:
-                fr = Frames(torch, dist, srt, scene, a, "frames", 1, 0, dev, v)
-                alt[v] = fr.run(a.steps, a.warmup, timing=False)
+                fr = Frames(torch, dist, srt, scene, a, "frames", 1, 0, dev, v, a.queues)
+                alt[v] = fr.run(a.steps, a.warmup, timing=False, queues=a.queues)
                 t = fr.run(a.steps, 0, timing=True)
+                fr.close()
                 alt[v].update({k: t[k] for k in ("prepare_ms", "bin_ms", "trace_ms")})
 
     if rank == 0:
@@ -312,6 +345,7 @@ def main():
                 "spp": 1,
                 "parallelism": (f"{a.mode} x{world}" + (" + RCCL gather" if a.mode == "bands" and world > 1 else "")),
                 "trace_variant": a.variant,
+                "frame_queues": r["queues"],
                 "cull_bins": os.environ.get("SRT_CULL_BIN", "1") != "0" if a.variant == "cull" else None,
             },
             "roofline": {
@@ -350,6 +384,11 @@ def main():
                                   "launch), bin = BinTrianglesKernel + TileOrderKernel, trace_kernel "
                                   "= TraceCullKernel; frame = uninstrumented, frame_instrumented = with the events"},
         }
+        line["single_queue"] = {
+            "mrays_per_s": round(r1["mrays"], 4), "ms_per_step": round(r1["ms_per_step"], 5),
+            "note": "the same frames with one frame in flight per GPU (per-frame latency); value keeps "
+                    "config.frame_queues frames in flight, each queue with its own scene buffers and HIP stream",
+        }
         if brute is not None:
             bs = brute["trace_ms"] * 1e-3
             tf = rays_tests * FLOPS_PER_TEST / bs / 1e12
@@ -371,7 +410,7 @@ def main():
         elif other is not None:
             om, o = other
             line[om] = {"mrays_per_s": round(o["mrays"], 4), "ms_per_step": round(o["ms_per_step"], 4),
-                        "scaling": "weak" if om == "frames" else "strong",
+                        "scaling": "weak" if om == "frames" else "strong", "queues": o["queues"],
                         "trace_kernel_ms": round(o["trace_ms"], 5), "bin_ms": round(o["bin_ms"], 5),
                         "prepare_ms": round(o["prepare_ms"], 5)}
         if world == 1 and not a.no_e2e:

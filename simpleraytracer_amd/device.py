@@ -103,6 +103,7 @@ class DeviceScene:
         if not self.handle:
             raise SrtError(_native.last_error())
         self.device = device
+        self.path = path
         self.triangles = self._lib.srtDeviceSceneTriangles(self.handle)
         self.width = 0
         self.height = 0

@@ -491,3 +491,30 @@ def test_ml_pipelined_chunks_bitwise(gpu, scenes, tmp_path, monkeypatch, out_dty
         assert np.array_equal(got.view(np.uint8), ref.view(np.uint8)), chunks
     if out_dtype == 0:
         assert_parity(ref, oracle_render(path, w, h, offs))
+
+
+@pytest.mark.parametrize("variant", ("cull", "bvh"))
+def test_concurrent_frame_queues(gpu, scenes, variant):
+    """bench.py's frame queues: scenes on their own HIP streams with frames interleaved
+    (prepare of one overlapping trace of another) give the single-stream frames bit-for-bit."""
+    import torch
+
+    import simpleraytracer_amd as srt
+
+    w, h = 640, 360
+    jobs = [(scenes["soup2k"], 0.5), (scenes["soup300"], 0.25), (scenes["soup2k"], 0.8)]
+    refs = []
+    for path, j in jobs:
+        refs.append(torch_render(path, w, h, np.full((h, w, 2), j, np.float32), variant=variant))
+    qs = [(srt.DeviceScene(path, 0), torch.cuda.Stream(),
+           torch.full((h, w, 2), j, dtype=torch.float32, device="cuda"),
+           torch.empty((h, w, 4), dtype=torch.float32, device="cuda")) for path, j in jobs]
+    torch.cuda.synchronize()
+    for k in range(4 * len(qs)):
+        scene, stream, off, out = qs[k % len(qs)]
+        scene.prepare(w, h, stream)
+        scene.trace(off, out, 0, h, variant=variant, stream=stream)
+    torch.cuda.synchronize()
+    for (scene, _, _, out), ref in zip(qs, refs):
+        assert np.array_equal(out.cpu().numpy().view(np.uint32), ref.view(np.uint32))
+        scene.close()
