@@ -169,9 +169,10 @@ class Frames:
         # Frame queues (frames mode): queue q = its own DeviceScene (edge records, bins, BVH)
         # + framebuffer + HIP stream; frame k goes to queue k % Q, so up to Q frames are in
         # flight and one frame's prepare/bin/trace fills the CUs another frame's heavy-tile
-        # tail leaves idle. Queue 0 is `scene` on the current stream (the Q = 1 loop).
+        # tail leaves idle. Queue 0 is `scene` (on the current stream in the Q = 1 loop).
         self.queues = [(scene, self.stream, self.offsets, self.bands[0])]
-        if mode == "frames":
+        if mode == "frames" and queues > 1:
+            self.queues[0] = (scene, torch.cuda.Stream(dev), self.offsets, self.bands[0])  # all on side streams
             for _ in range(max(1, queues) - 1):
                 self.queues.append((srt.DeviceScene(scene.path, dev.index), torch.cuda.Stream(dev),
                                     self.offsets.clone(), torch.zeros_like(self.bands[0])))

@@ -714,7 +714,7 @@ constexpr int kParts = kTileRows / kBlockRows;
 #define SRT_PACKET_BATCH 256
 #endif
 #ifndef SRT_PACKET_ILP
-#define SRT_PACKET_ILP 4  // packet walk: packets evaluated together per wave (independent chains)
+#define SRT_PACKET_ILP 2  // packet walk: packets evaluated together per wave (independent chains)
 #endif
 #ifndef SRT_FLUSH_BATCH
 #define SRT_FLUSH_BATCH 128
@@ -1944,8 +1944,11 @@ __device__ __forceinline__ void UniformRays(const TraceParams& p, int x, int y0,
     }
 }
 
+#ifndef SRT_TRACE_OCC
+#define SRT_TRACE_OCC 4
+#endif
 template <int W>
-__global__ __launch_bounds__(kWave * W, 4) void TraceCullKernel(TraceParams p) {
+__global__ __launch_bounds__(kWave * W, SRT_TRACE_OCC) void TraceCullKernel(TraceParams p) {
     using S = CullShape<W>;
     constexpr int R = S::kR;
     __shared__ CullShared<W> sh;

@@ -13,7 +13,7 @@ for cfg in ${CFGS:-NONE=0}; do
     tag=$(echo "$cfg" | tr '+=/' '___' | cut -c1-80)
     env $(echo "$cfg" | tr '+' ' ') timeout -k 10 120 rocprofv3 --kernel-trace --stats -d gpurun_out/e_$tag -o run --output-format csv -- \
         python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-e2e ${BENCH_ARGS:-} > gpurun_out/e_$tag.log 2>&1 || { echo "rc=$? $cfg"; exit 1; }
-    echo "== $cfg"; grep -o '"value": [0-9.]*' gpurun_out/e_$tag.log
+    echo "== $cfg"; grep -o '"value": [0-9.]*\|"single_queue": {"mrays_per_s": [0-9.]*' gpurun_out/e_$tag.log | tr '\n' ' '; echo
     cut -d, -f1,3,4 gpurun_out/e_$tag/run_kernel_stats.csv | sed 's/(srt::(anonymous namespace)::[A-Za-z]*)//; s/srt::(anonymous namespace):://' | head -8
 done
 echo done
