@@ -50,7 +50,7 @@ KERNEL_NAMES = {"lds": "TraceLdsKernel", "scalar": "TraceScalarKernel", "cull": 
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--steps", type=int, default=1000)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--width", type=int, default=1920)
     p.add_argument("--height", type=int, default=1080)

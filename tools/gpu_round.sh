@@ -41,6 +41,10 @@ if [[ $STEPS == *quick* ]]; then
 fi
 if [[ $STEPS == *prof* ]]; then
     run prof_stats 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- "${BENCH[@]}"
+    # one frame in flight: per-kernel durations without the frame-queue overlap (the bench's
+    # roofline/stage times come from its single-queue instrumented pass)
+    run prof_stats_q1 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_q1 -o run --output-format csv -- \
+        "${BENCH[@]}" --queues 1
 fi
 if [[ $STEPS == *pmc* ]]; then
     run pmc_fetch 120 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$KERNEL_RE" -d gpurun_out/pmc_fetch -o run --output-format csv -- "${BENCH[@]}"

@@ -3,6 +3,11 @@
 the idle gap before it (the last N kernels), plus mean busy / gap per frame.
 
     python tools/trace_gaps.py gpurun_out/prof/run_kernel_trace.csv [--last 12]
+    python tools/trace_gaps.py gpurun_out/prof/run_kernel_trace.csv --overlap 150 --skip 100
+
+--overlap N: over the last N kernels (frame queues: kernels of different streams overlap),
+the wall time they span, the time with at least one kernel running, and the mean number of
+kernels running while any is.
 """
 import argparse
 import csv
@@ -13,9 +18,14 @@ def main():
     ap.add_argument("csv")
     ap.add_argument("--last", type=int, default=12)
     ap.add_argument("--frame-kernel", default="PrepareKernel", help="kernel that starts a frame")
+    ap.add_argument("--overlap", type=int, default=0)
+    ap.add_argument("--skip", type=int, default=-1, help="--overlap over kernels [skip, skip + N) instead")
     a = ap.parse_args()
     rows = sorted(csv.DictReader(open(a.csv)), key=lambda r: int(r["Start_Timestamp"]))
     rows = [r for r in rows if "srt::" in r["Kernel_Name"]]
+    if a.overlap:
+        overlap(rows[a.skip:a.skip + a.overlap] if a.skip >= 0 else rows[-a.overlap:])
+        return
     prev = None
     frames, cur = [], None
     for r in rows:
@@ -37,6 +47,22 @@ def main():
         busy = sum(f["busy"] for f in full) / len(full) / 1e3
         gap = sum(f["gap"] for f in full) / len(full) / 1e3
         print(f"frames {len(full)}: mean kernel time {busy:.2f} us, mean in-frame gaps {gap:.2f} us")
+
+
+def overlap(rows):
+    ev = sorted([(int(r["Start_Timestamp"]), 1) for r in rows] + [(int(r["End_Timestamp"]), -1) for r in rows])
+    active, last, busy, weighted = 0, ev[0][0], 0, 0
+    for t, d in ev:
+        if active:
+            busy += t - last
+            weighted += active * (t - last)
+        active += d
+        last = t
+    span = ev[-1][0] - ev[0][0]
+    kern = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows)
+    print(f"{len(rows)} kernels over {span / 1e3:.1f} us: some kernel running {100 * busy / span:.1f} % of it, "
+          f"{weighted / max(busy, 1):.2f} kernels running on average meanwhile; summed kernel durations "
+          f"{kern / 1e3:.1f} us")
 
 
 if __name__ == "__main__":
