@@ -713,6 +713,9 @@ constexpr int kParts = kTileRows / kBlockRows;
 #ifndef SRT_PACKET_BATCH
 #define SRT_PACKET_BATCH 256
 #endif
+#ifndef SRT_PIN_LOADS
+#define SRT_PIN_LOADS 1  // packet walk: pin loop-invariant lane values and keys (ISA scheduling)
+#endif
 #ifndef SRT_PACKET_ILP
 #define SRT_PACKET_ILP 2  // packet walk: packets evaluated together per wave (independent chains)
 #endif
@@ -1395,6 +1398,11 @@ __device__ __forceinline__ void PacketWalk(const TraceParams& p, CullShared<W>& 
             const unsigned my_j = mine - k.pre[lo];
             const unsigned my_bits = __float_as_uint(k.sv2[lo].w);
             const unsigned n = min(static_cast<unsigned>(kWave), q_end - q0);
+#if SRT_PIN_LOADS
+            // Resolve the per-lane packet table before the loop, so the loop header does not
+            // wait for the previous iteration's LDS atomics (conservative waitcnt merge).
+            asm volatile("" ::"v"(my_s), "v"(my_bits), "v"(my_j));
+#endif
 #pragma unroll 1
             for (unsigned i = 0; i < n; i += kPacketIlp) {
                 unsigned ps[kPacketIlp];
@@ -1420,6 +1428,14 @@ __device__ __forceinline__ void PacketWalk(const TraceParams& p, CullShared<W>& 
                 for (int u = 0; u < kPacketIlp; ++u) {
                     h[u] = EvalPacket(ra[u], rb[u], rx[u], fx[u], fy[u], px[u]);
                 }
+#if SRT_PIN_LOADS
+                // Keys built before the hit branches: the record id is loaded with the rest of
+                // the record instead of by a separate LDS read (and full wait) inside the branch.
+#pragma unroll
+                for (int u = 0; u < kPacketIlp; ++u) {
+                    asm volatile("" ::"v"(h[u].key));
+                }
+#endif
 #pragma unroll
                 for (int u = 0; u < kPacketIlp; ++u) {
 #ifdef SRT_DIAG
