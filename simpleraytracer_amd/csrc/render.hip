@@ -713,6 +713,11 @@ constexpr int kParts = kTileRows / kBlockRows;
 #ifndef SRT_PACKET_BATCH
 #define SRT_PACKET_BATCH 256
 #endif
+#ifndef SRT_PACKET_FLAT
+// packet walk: 1 = a survivor's pixel range is cut row-major into packets of 64 pixels
+// (ceil(cols*rows/64) packets); 0 = power-of-two-wide packets (2^lg columns x 64>>lg rows)
+#define SRT_PACKET_FLAT 1
+#endif
 #ifndef SRT_PIN_LOADS
 #define SRT_PIN_LOADS 1  // packet walk: pin loop-invariant lane values and keys (ISA scheduling)
 #endif
@@ -1163,6 +1168,24 @@ __device__ __forceinline__ PacketPixel PacketLane(unsigned bits, unsigned j, int
     return PacketPixel{min(col_u, c1), min(row_u, r1), static_cast<bool>((col_u <= c1) & (row_u <= r1))};
 }
 
+// Row-major packing: packet j of a survivor with range [c0, c0 + nc) x [r0, r0 + nr) covers
+// range pixels p = 64 j + lane, p < nc * nr, at (c0 + p % nc, r0 + p / nc). p / nc is
+// (p * m) >> 17 with m = ceil(2^17 / nc): exact, because p < 1088 and nc <= 64 keep
+// p * (m - 2^17 / nc) / 2^17 < 1/nc (and p * m < 2^24 * 2^24 fits v_mul_u32_u24's low word,
+// p * m < 2^32). Lanes past the range read padding-free table entries but are not `in`.
+__device__ __forceinline__ unsigned PacketMagic(unsigned bits) {
+    const unsigned nc = ((bits >> 6) & 63u) + 1u;
+    return (131071u + nc) / nc;
+}
+__device__ __forceinline__ PacketPixel PacketLaneFlat(unsigned bits, unsigned j, unsigned m, int lane) {
+    const unsigned c0 = bits & 63u, nc = ((bits >> 6) & 63u) + 1u, r0 = (bits >> 12) & 31u;
+    const unsigned nr = ((bits >> 17) & 31u) + 1u;
+    const unsigned pix = (j << 6) + static_cast<unsigned>(lane);
+    const unsigned row_in = __umul24(pix, m) >> 17;  // pix < 2^11, m <= 2^17
+    const unsigned col_in = pix - row_in * nc;
+    return PacketPixel{static_cast<int>(c0 + col_in), static_cast<int>(r0 + row_in), pix < nc * nr};
+}
+
 __device__ __forceinline__ PacketHit EvalPacket(const float4& a, const float4& b, const float4& x, float fx, float fy,
                                                 const PacketPixel& px) {
     const float eA = fmaf(fy, a.z, fmaf(fx, a.y, a.x));
@@ -1293,12 +1316,18 @@ __device__ __forceinline__ void PacketWalk(const TraceParams& p, CullShared<W>& 
                 pass[e] = c0 <= c1 && r0 <= r1;
                 if (pass[e]) {
                     const int ncols = c1 - c0 + 1;
+#if SRT_PACKET_FLAT
+                    npk[e] = static_cast<unsigned>((ncols * (r1 - r0 + 1) + kWave - 1) / kWave);
+                    bits[e] = static_cast<unsigned>(c0) | static_cast<unsigned>(ncols - 1) << 6 |
+                              static_cast<unsigned>(r0) << 12 | static_cast<unsigned>(r1 - r0) << 17;
+#else
                     const int lg = ncols <= 1 ? 0 : 32 - __builtin_clz(static_cast<unsigned>(ncols - 1));
                     const int rpp = kWave >> lg;
                     npk[e] = static_cast<unsigned>((r1 - r0 + rpp) / rpp);
                     bits[e] = static_cast<unsigned>(c0) | static_cast<unsigned>(c1) << 6 |
                               static_cast<unsigned>(r0) << 12 | static_cast<unsigned>(r1) << 17 |
                               static_cast<unsigned>(lg) << 22;
+#endif
                 }
             }
         }
@@ -1398,10 +1427,16 @@ __device__ __forceinline__ void PacketWalk(const TraceParams& p, CullShared<W>& 
             const unsigned my_j = mine - k.pre[lo];
             const unsigned my_bits = __float_as_uint(k.sv2[lo].w);
             const unsigned n = min(static_cast<unsigned>(kWave), q_end - q0);
+#if SRT_PACKET_FLAT
+            const unsigned my_m = PacketMagic(my_bits);
+#endif
 #if SRT_PIN_LOADS
             // Resolve the per-lane packet table before the loop, so the loop header does not
             // wait for the previous iteration's LDS atomics (conservative waitcnt merge).
             asm volatile("" ::"v"(my_s), "v"(my_bits), "v"(my_j));
+#if SRT_PACKET_FLAT
+            asm volatile("" ::"v"(my_m));
+#endif
 #endif
 #pragma unroll 1
             for (unsigned i = 0; i < n; i += kPacketIlp) {
@@ -1413,7 +1448,12 @@ __device__ __forceinline__ void PacketWalk(const TraceParams& p, CullShared<W>& 
                 for (int u = 0; u < kPacketIlp; ++u) {
                     const unsigned li = min(i + u, n - 1u);
                     ps[u] = __builtin_amdgcn_readlane(my_s, li);
+#if SRT_PACKET_FLAT
+                    px[u] = PacketLaneFlat(__builtin_amdgcn_readlane(my_bits, li), __builtin_amdgcn_readlane(my_j, li),
+                                           __builtin_amdgcn_readlane(my_m, li), lane);
+#else
                     px[u] = PacketLane(__builtin_amdgcn_readlane(my_bits, li), __builtin_amdgcn_readlane(my_j, li), lane);
+#endif
                 }
 #pragma unroll
                 for (int u = 0; u < kPacketIlp; ++u) {
