@@ -2670,13 +2670,14 @@ hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_ver
             b.tile_order = bins->tile_order;
             b.sync = bins->sync;
             // Tile bounds once per frame (TileBoundsKernel) when the bin blocks' own reductions
-            // would cost more: (bin blocks) x (tiles) tile-info reads above 2M (C5: 16M; C3:
-            // 0.4M, where the extra launch costs more than it saves). Env SRT_TILE_BOUNDS=0/1
-            // forces either way.
+            // would cost more: (bin blocks) x (tiles) tile-info reads above 200k (C5: 16M, bin
+            // stage 164 -> 75 us; C3: 0.4M, where the extra launch adds ~1 % to one frame's
+            // latency but the chip time it saves gives +3 % with frame queues in flight; C2 and
+            // small frames: 1k, no extra launch). Env SRT_TILE_BOUNDS=0/1 forces either way.
             {
                 const std::uint64_t reads = (n + kBinThreads - 1) / kBinThreads * static_cast<std::uint64_t>(gx) * gy;
                 const char* v = std::getenv("SRT_TILE_BOUNDS");
-                const bool once = v != nullptr && *v != '\0' ? std::strcmp(v, "0") != 0 : reads > 2000000ull;
+                const bool once = v != nullptr && *v != '\0' ? std::strcmp(v, "0") != 0 : reads > 200000ull;
                 b.bounds = once ? static_cast<float2*>(bins->bounds) : nullptr;
             }
             b.capacity = bins->capacity;

@@ -173,6 +173,22 @@ def test_cull_modes(gpu, scenes, monkeypatch, mode):
         assert_parity(got, oracle_render(scenes["soup2k"], w, h, offsets))
 
 
+@pytest.mark.parametrize("bounds", ["0", "1"])
+def test_cull_tile_bounds_paths(gpu, scenes, monkeypatch, bounds):
+    """Tile column/row bounds reduced by every bin block (SRT_TILE_BOUNDS=0) or once per frame
+    by TileBoundsKernel (=1): the same frame, bit for bit, and oracle parity on a row sample."""
+    monkeypatch.delenv("SRT_TILE_BOUNDS", raising=False)
+    ref = torch_render(scenes["soup100k"], 1920, 1080, variant="lds")
+    monkeypatch.setenv("SRT_TILE_BOUNDS", bounds)
+    got = torch_render(scenes["soup100k"], 1920, 1080, variant="cull")
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+    rng = np.random.default_rng(23)
+    w, h = 257, 131
+    offsets = rng.random((h, w, 2), dtype=np.float32)
+    assert_parity(torch_render(scenes["soup2k"], w, h, offsets, variant="cull"),
+                  oracle_render(scenes["soup2k"], w, h, offsets))
+
+
 @pytest.mark.parametrize("mode", CULL_MODES[:4])
 @pytest.mark.parametrize("offset", [0.5, 0.0, 0.999, -3.25, 7.5])
 def test_cull_uniform_offsets(gpu, scenes, monkeypatch, mode, offset):
