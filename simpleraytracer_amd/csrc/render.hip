@@ -718,6 +718,10 @@ constexpr int kParts = kTileRows / kBlockRows;
 // (ceil(cols*rows/64) packets); 0 = power-of-two-wide packets (2^lg columns x 64>>lg rows)
 #define SRT_PACKET_FLAT 1
 #endif
+#ifndef SRT_PACKET_WORD
+// packet walk (row-major packets, blocks of <= 16 rows): one packed word per packet
+#define SRT_PACKET_WORD (SRT_PACKET_FLAT && SRT_BLOCK_ROWS <= 16)
+#endif
 #ifndef SRT_PIN_LOADS
 #define SRT_PIN_LOADS 1  // packet walk: pin loop-invariant lane values and keys (ISA scheduling)
 #endif
@@ -1151,21 +1155,22 @@ __device__ __forceinline__ void CullWalk(const TraceParams& p, CullShared<W>& sh
 // fails). `bits` = the survivor's packed pixel range (wave-uniform), `j` = packet index.
 struct PacketHit {
     unsigned long long key;
-    unsigned addr;  // element index into the tile's keys
+    unsigned addr;  // byte offset of the pixel's 8-B key in the tile's keys
     bool hit;
 };
 
 struct PacketPixel {
-    int col, row;
+    unsigned colb, rowb;  // byte offsets of the pixel's column / row in the fx / fy tables
     bool in;
 };
 
-__device__ __forceinline__ PacketPixel PacketLane(unsigned bits, unsigned j, int lane) {
+[[maybe_unused]] __device__ __forceinline__ PacketPixel PacketLane(unsigned bits, unsigned j, int lane) {
     const int c0 = bits & 63u, c1 = (bits >> 6) & 63u, r0 = (bits >> 12) & 31u, r1 = (bits >> 17) & 31u;
     const int lg = (bits >> 22) & 7u;
     const int col_u = c0 + (lane & ((1 << lg) - 1));
     const int row_u = r0 + static_cast<int>(j << (6 - lg)) + (lane >> lg);
-    return PacketPixel{min(col_u, c1), min(row_u, r1), static_cast<bool>((col_u <= c1) & (row_u <= r1))};
+    return PacketPixel{static_cast<unsigned>(min(col_u, c1)) * 4u, static_cast<unsigned>(min(row_u, r1)) * 4u,
+                       static_cast<bool>((col_u <= c1) & (row_u <= r1))};
 }
 
 // Row-major packing: packet j of a survivor with range [c0, c0 + nc) x [r0, r0 + nr) covers
@@ -1183,7 +1188,21 @@ __device__ __forceinline__ PacketPixel PacketLaneFlat(unsigned bits, unsigned j,
     const unsigned pix = (j << 6) + static_cast<unsigned>(lane);
     const unsigned row_in = __umul24(pix, m) >> 17;  // pix < 2^11, m <= 2^17
     const unsigned col_in = pix - row_in * nc;
-    return PacketPixel{static_cast<int>(c0 + col_in), static_cast<int>(r0 + row_in), pix < nc * nr};
+    return PacketPixel{(c0 + col_in) * 4u, (r0 + row_in) * 4u, pix < nc * nr};
+}
+
+// One word per packet for the walk loop (one readlane instead of three): the range fields of
+// PacketLaneFlat's `bits` narrowed to 4-bit rows, the survivor slot and the packet index.
+// Needs rows < 16 (kBlockRows <= 16), slots < 256 and packets per survivor <= 16.
+__device__ __forceinline__ unsigned PacketWord(unsigned bits, unsigned slot, unsigned j) {
+    return (bits & 0xFFFu) | ((bits >> 12) & 15u) << 12 | ((bits >> 17) & 15u) << 16 | slot << 20 | j << 28;
+}
+__device__ __forceinline__ PacketPixel PacketLaneWord(unsigned w, unsigned m, int lane) {
+    // In byte units (4 pix): (4 pix m) >> 19 == (pix m) >> 17, 4 pix m < 2^32.
+    const unsigned c0 = w & 63u, nc = ((w >> 6) & 63u) + 1u, r0 = (w >> 12) & 15u, nr = ((w >> 16) & 15u) + 1u;
+    const unsigned pix4 = (w >> 28 << 8) | (static_cast<unsigned>(lane) << 2);
+    const unsigned row_in = __umul24(pix4, m) >> 19;
+    return PacketPixel{pix4 + c0 * 4u - row_in * (nc * 4u), row_in * 4u + r0 * 4u, pix4 < nc * nr * 4u};
 }
 
 __device__ __forceinline__ PacketHit EvalPacket(const float4& a, const float4& b, const float4& x, float fx, float fy,
@@ -1196,7 +1215,7 @@ __device__ __forceinline__ PacketHit EvalPacket(const float4& a, const float4& b
     PacketHit h;
     h.hit = static_cast<bool>(px.in & (fminf(fminf(eA, eB), eC) >= 0.f) & (det > 0.f) & (t < __builtin_inff()));
     h.key = HitKey(t, __float_as_int(x.z));
-    h.addr = static_cast<unsigned>(px.row * kWave + px.col);
+    h.addr = px.rowb * (kWave * 2u) + px.colb * 2u;
     return h;
 }
 
@@ -1430,6 +1449,13 @@ __device__ __forceinline__ void PacketWalk(const TraceParams& p, CullShared<W>& 
 #if SRT_PACKET_FLAT
             const unsigned my_m = PacketMagic(my_bits);
 #endif
+#if SRT_PACKET_WORD
+            constexpr bool kWord = kBlockRows <= 16 && S::kPBatch <= 256;  // field widths
+            const unsigned my_w = kWord ? PacketWord(my_bits, my_s, my_j) : 0u;
+            if constexpr (kWord) {
+                asm volatile("" ::"v"(my_w));
+            }
+#endif
 #if SRT_PIN_LOADS
             // Resolve the per-lane packet table before the loop, so the loop header does not
             // wait for the previous iteration's LDS atomics (conservative waitcnt merge).
@@ -1447,11 +1473,23 @@ __device__ __forceinline__ void PacketWalk(const TraceParams& p, CullShared<W>& 
 #pragma unroll
                 for (int u = 0; u < kPacketIlp; ++u) {
                     const unsigned li = min(i + u, n - 1u);
+#if SRT_PACKET_WORD
+                    if constexpr (kWord) {
+                        const unsigned w = __builtin_amdgcn_readlane(my_w, li);
+                        ps[u] = (w >> 20) & 255u;
+                        px[u] = PacketLaneWord(w, __builtin_amdgcn_readlane(my_m, li), lane);
+                    } else {
+                        ps[u] = __builtin_amdgcn_readlane(my_s, li);
+                        px[u] = PacketLaneFlat(__builtin_amdgcn_readlane(my_bits, li),
+                                               __builtin_amdgcn_readlane(my_j, li), __builtin_amdgcn_readlane(my_m, li),
+                                               lane);
+                    }
+#elif SRT_PACKET_FLAT
                     ps[u] = __builtin_amdgcn_readlane(my_s, li);
-#if SRT_PACKET_FLAT
                     px[u] = PacketLaneFlat(__builtin_amdgcn_readlane(my_bits, li), __builtin_amdgcn_readlane(my_j, li),
                                            __builtin_amdgcn_readlane(my_m, li), lane);
 #else
+                    ps[u] = __builtin_amdgcn_readlane(my_s, li);
                     px[u] = PacketLane(__builtin_amdgcn_readlane(my_bits, li), __builtin_amdgcn_readlane(my_j, li), lane);
 #endif
                 }
@@ -1460,8 +1498,8 @@ __device__ __forceinline__ void PacketWalk(const TraceParams& p, CullShared<W>& 
                     ra[u] = k.sv0[ps[u]];
                     rb[u] = k.sv1[ps[u]];
                     rx[u] = k.sv2[ps[u]];
-                    fx[u] = k.fxs[px[u].col];
-                    fy[u] = k.fys[px[u].row];
+                    fx[u] = *reinterpret_cast<const float*>(reinterpret_cast<const char*>(k.fxs) + px[u].colb);
+                    fy[u] = *reinterpret_cast<const float*>(reinterpret_cast<const char*>(k.fys) + px[u].rowb);
                 }
                 PacketHit h[kPacketIlp];
 #pragma unroll
@@ -1484,7 +1522,9 @@ __device__ __forceinline__ void PacketWalk(const TraceParams& p, CullShared<W>& 
                     }
 #endif
                     if (h[u].hit) {
-                        __hip_atomic_fetch_min(keys + h[u].addr, h[u].key, __ATOMIC_RELAXED,
+                        __hip_atomic_fetch_min(reinterpret_cast<unsigned long long*>(
+                                                   reinterpret_cast<char*>(keys) + h[u].addr),
+                                               h[u].key, __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_WORKGROUP);
                     }
                 }
