@@ -718,6 +718,13 @@ constexpr int kParts = kTileRows / kBlockRows;
 // (ceil(cols*rows/64) packets); 0 = power-of-two-wide packets (2^lg columns x 64>>lg rows)
 #define SRT_PACKET_FLAT 1
 #endif
+#ifndef SRT_PACKET_SPLIT
+// packet walk (row-major packets): a survivor's range may be cut into two row bands, each with
+// its own exact column range, when that takes fewer packets. Exact (GPU parity green) but
+// measured slower: the six column searches in the gather phase cost more than the packets
+// they save (trace 36.4 -> 43 us), so off by default.
+#define SRT_PACKET_SPLIT 0
+#endif
 #ifndef SRT_PACKET_WORD
 // packet walk (row-major packets, blocks of <= 16 rows): one packed word per packet
 #define SRT_PACKET_WORD (SRT_PACKET_FLAT && SRT_BLOCK_ROWS <= 16)
@@ -767,6 +774,9 @@ struct CullShared {
             float4 sv0[CullShape<W>::kPBatch];  // plane 0
             float4 sv1[CullShape<W>::kPBatch];  // plane 1
             float4 sv2[CullShape<W>::kPBatch];  // (cyC, vol, id, pixel range bits)
+#if SRT_PACKET_SPLIT
+            unsigned band2[CullShape<W>::kPBatch];  // second row band's range bits (split survivors)
+#endif
             unsigned pre[CullShape<W>::kPBatch + 1];  // exclusive packet prefix, pre[S] = packets
             unsigned wave_n[CullShape<W>::kPBatch / kWave];   // survivors per (slice, wave)
             unsigned wave_pk[CullShape<W>::kPBatch / kWave];  // packets per (slice, wave)
@@ -1191,6 +1201,53 @@ __device__ __forceinline__ PacketPixel PacketLaneFlat(unsigned bits, unsigned j,
     return PacketPixel{(c0 + col_in) * 4u, (r0 + row_in) * 4u, pix < nc * nr};
 }
 
+// Row band split (SRT_PACKET_SPLIT). For rows [ra, rb] of the range, an edge function
+// E = fma(fy, cy, fma(fx, cx, c0)) is monotone in fy (fma is monotone in each argument and the
+// fy table is nondecreasing in the row), so its largest value over the band at column c is at
+// fy* = fys[rb] (cy > 0) or fys[ra]; and at fixed fy* it is monotone in the column. The
+// columns where E(fx_c, fy*) >= 0 are therefore a prefix or suffix of [lo, hi], found by
+// binary search, and a column outside it fails that edge on every row of the band: dropping it
+// is exact. NaN coefficients: E is NaN everywhere (no pixel passes), any cut is exact.
+__device__ __forceinline__ void BandEdgeCut(const float* fxs, float fys_a, float fys_b, float cx, float cy, float c0,
+                                            int c_lo, int c_hi, int& lo, int& hi) {
+    // Branch-free lower bound over [c_lo, c_hi] (<= 64 columns, 7 fixed steps) of the first
+    // column that does not "advance": for cx > 0 advance while E < 0 (the passing columns are
+    // a suffix), for cx < 0 while E >= 0 (a prefix). cx == 0 (E constant in c) or NaN: one test.
+    const float fy = cy > 0.f ? fys_b : fys_a;
+    const bool inc = cx > 0.f;
+    int pos = c_lo;
+#pragma unroll
+    for (int step = 64; step >= 1; step >>= 1) {
+        const int c = pos + step - 1;
+        const float e = fmaf(fy, cy, fmaf(fxs[min(c, c_hi)], cx, c0));
+        pos += (c <= c_hi && ((e >= 0.f) != inc)) ? step : 0;
+    }
+    if (inc) {
+        lo = pos;
+        hi = c_hi;
+    } else if (cx < 0.f) {
+        lo = c_lo;
+        hi = pos - 1;
+    } else {
+        const bool pass = fmaf(fy, cy, fmaf(fxs[c_lo], cx, c0)) >= 0.f;
+        lo = c_lo;
+        hi = pass ? c_hi : c_lo - 1;
+    }
+}
+
+// Column range of rows [ra, rb] inside [c0, c1] (empty: c1 < c0 on return). The three edge
+// cuts are independent searches over [c0, c1] (their LDS reads overlap), then intersected.
+[[maybe_unused]] __device__ __forceinline__ void BandColumns(const float* fxs, const float* fys, const CullRecord& cr, int ra, int rb,
+                                            int& c0, int& c1) {
+    const float fa = fys[ra], fb = fys[rb];
+    int l0, h0, l1, h1, l2, h2;
+    BandEdgeCut(fxs, fa, fb, cr.a.y, cr.a.z, cr.a.x, c0, c1, l0, h0);
+    BandEdgeCut(fxs, fa, fb, cr.b.x, cr.b.y, cr.a.w, c0, c1, l1, h1);
+    BandEdgeCut(fxs, fa, fb, cr.b.w, cr.x.x, cr.b.z, c0, c1, l2, h2);
+    c0 = max(max(l0, l1), l2);
+    c1 = min(min(h0, h1), h2);
+}
+
 // One word per packet for the walk loop (one readlane instead of three): the range fields of
 // PacketLaneFlat's `bits` narrowed to 4-bit rows, the survivor slot and the packet index.
 // Needs rows < 16 (kBlockRows <= 16), slots < 256 and packets per survivor <= 16.
@@ -1316,11 +1373,12 @@ __device__ __forceinline__ void PacketWalk(const TraceParams& p, CullShared<W>& 
             pass[e] = b0 + e * kThreads + tid < total;
             cr[e] = nxt[e];
         }
-        unsigned bits[kSlices], npk[kSlices];
+        unsigned bits[kSlices], npk[kSlices], band2[kSlices];
 #pragma unroll
         for (int e = 0; e < kSlices; ++e) {
             bits[e] = 0u;
             npk[e] = 0u;
+            band2[e] = 0u;
             const float4 sb = cr[e].sb;
             const Record r{cr[e].a.x, cr[e].a.y, cr[e].a.z, cr[e].a.w, cr[e].b.x, cr[e].b.y, cr[e].b.z, cr[e].b.w,
                            cr[e].x.x};
@@ -1339,6 +1397,32 @@ __device__ __forceinline__ void PacketWalk(const TraceParams& p, CullShared<W>& 
                     npk[e] = static_cast<unsigned>((ncols * (r1 - r0 + 1) + kWave - 1) / kWave);
                     bits[e] = static_cast<unsigned>(c0) | static_cast<unsigned>(ncols - 1) << 6 |
                               static_cast<unsigned>(r0) << 12 | static_cast<unsigned>(r1 - r0) << 17;
+#if SRT_PACKET_SPLIT
+                    if (npk[e] > 1u) {  // a one-packet range cannot get cheaper
+                        const int rm = r0 + ((r1 - r0 + 1) >> 1);  // bands [r0, rm - 1], [rm, r1]
+                        int a0 = c0, a1 = c1, b0 = c0, b1 = c1;
+                        BandColumns(k.fxs, k.fys, cr[e], r0, rm - 1, a0, a1);
+                        BandColumns(k.fxs, k.fys, cr[e], rm, r1, b0, b1);
+                        const unsigned na = a0 <= a1 ? static_cast<unsigned>(((a1 - a0 + 1) * (rm - r0) + kWave - 1) / kWave) : 0u;
+                        const unsigned nb = b0 <= b1 ? static_cast<unsigned>(((b1 - b0 + 1) * (r1 - rm + 1) + kWave - 1) / kWave) : 0u;
+                        const unsigned bits_a = static_cast<unsigned>(a0) | static_cast<unsigned>(a1 - a0) << 6 |
+                                                static_cast<unsigned>(r0) << 12 | static_cast<unsigned>(rm - 1 - r0) << 17;
+                        const unsigned bits_b = static_cast<unsigned>(b0) | static_cast<unsigned>(b1 - b0) << 6 |
+                                                static_cast<unsigned>(rm) << 12 | static_cast<unsigned>(r1 - rm) << 17;
+                        if (na + nb < npk[e]) {
+                            npk[e] = na + nb;
+                            if (na == 0u) {
+                                bits[e] = bits_b;
+                            } else if (nb == 0u) {
+                                bits[e] = bits_a;
+                            } else {
+                                bits[e] = bits_a | 1u << 22;
+                                band2[e] = bits_b;
+                            }
+                            pass[e] = npk[e] != 0u;
+                        }
+                    }
+#endif
 #else
                     const int lg = ncols <= 1 ? 0 : 32 - __builtin_clz(static_cast<unsigned>(ncols - 1));
                     const int rpp = kWave >> lg;
@@ -1398,6 +1482,9 @@ __device__ __forceinline__ void PacketWalk(const TraceParams& p, CullShared<W>& 
                 k.sv0[slot] = cr[e].a;
                 k.sv1[slot] = cr[e].b;
                 k.sv2[slot] = make_float4(cr[e].x.x, cr[e].x.y, cr[e].x.z, __uint_as_float(bits[e]));
+#if SRT_PACKET_SPLIT
+                k.band2[slot] = band2[e];
+#endif
                 k.pre[slot] = pbase[e] + incl[e] - npk[e];
             }
         }
@@ -1443,8 +1530,17 @@ __device__ __forceinline__ void PacketWalk(const TraceParams& p, CullShared<W>& 
                 }
             }
             const unsigned my_s = static_cast<unsigned>(lo);
-            const unsigned my_j = mine - k.pre[lo];
-            const unsigned my_bits = __float_as_uint(k.sv2[lo].w);
+            unsigned my_j = mine - k.pre[lo];
+            unsigned my_bits = __float_as_uint(k.sv2[lo].w);
+#if SRT_PACKET_FLAT && SRT_PACKET_SPLIT
+            if (my_bits & (1u << 22)) {  // two row bands: the first band's packets come first
+                const unsigned na = ((((my_bits >> 6) & 63u) + 1u) * (((my_bits >> 17) & 31u) + 1u) + kWave - 1) / kWave;
+                if (my_j >= na) {
+                    my_bits = k.band2[lo];
+                    my_j -= na;
+                }
+            }
+#endif
             const unsigned n = min(static_cast<unsigned>(kWave), q_end - q0);
 #if SRT_PACKET_FLAT
             const unsigned my_m = PacketMagic(my_bits);
