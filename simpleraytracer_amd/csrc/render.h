@@ -44,9 +44,11 @@ constexpr float kQuantScale = 4096.0f;
 
 // Cull records (render.hip CullRecord): 64 B per record, at the record's rank in the scene's
 // spatial order, after the quantized boxes.
+// Shading normals (render.hip PrepareRecord): one float4 (n = e1 x e2, |n|) per triangle id,
+// after the cull records; the shade epilogue reads 16 B per hit instead of 36 B of vertices.
 // Floats per record in the edge allocation: 10 (tiles) + 4 (screen box) + 2 (quantized box)
-// + 16 (cull record).
-constexpr int kEdgeFloatsPerTriangle = 32;
+// + 16 (cull record) + 4 (shading normal).
+constexpr int kEdgeFloatsPerTriangle = 36;
 
 inline std::uint64_t PaddedTriangleCount(std::uint64_t n) {
     const std::uint64_t p = (n + kPadTriangles - 1) / kPadTriangles * kPadTriangles;

@@ -54,6 +54,7 @@ struct TraceParams {
     const uint2* __restrict__ qboxes;
     const float* __restrict__ vertices;
     const float* __restrict__ albedo;
+    const float4* __restrict__ normals;  // shading normals (PrepareRecord), by triangle id
     const float2* __restrict__ offsets;
     float4* __restrict__ out;
     unsigned n_pad;   // records in the edge buffer (multiple of kPadTriangles)
@@ -91,6 +92,7 @@ struct PrepareParams {
     float4* __restrict__ screen_boxes;
     uint2* __restrict__ qboxes;
     CullRecord* __restrict__ cull;
+    float4* __restrict__ normals;  // shading normal (e1 x e2, |e1 x e2|) per triangle id
     unsigned n;
     unsigned n_pad;
     float origin[3];
@@ -266,6 +268,13 @@ __device__ __forceinline__ void PrepareRecord(const PrepareParams& p, unsigned i
     // Stored as (hi, -lo) pairs so the cull test is one saturating packed add per axis.
     p.qboxes[i] = make_uint2(PackI16(QuantHi(sb.y), -QuantLo(sb.x)), PackI16(QuantHi(sb.w), -QuantLo(sb.z)));
     if (i < p.n) {
+        // Shading normal, the exact expressions ShadeAndStore used to evaluate per hit.
+        const float* v = p.vertices + 9ull * i;
+        const float e1x = v[3] - v[0], e1y = v[4] - v[1], e1z = v[5] - v[2];
+        const float e2x = v[6] - v[0], e2y = v[7] - v[1], e2z = v[8] - v[2];
+        float nx, ny, nz;
+        Cross3(e1x, e1y, e1z, e2x, e2y, e2z, nx, ny, nz);
+        p.normals[i] = make_float4(nx, ny, nz, sqrtf(Dot3(nx, ny, nz, nx, ny, nz)));
         CullRecord r;
         r.a = make_float4(c[0], c[1], c[2], c[3]);
         r.b = make_float4(c[4], c[5], c[6], c[7]);
@@ -422,15 +431,10 @@ __device__ __forceinline__ void ShadeAndStore(const TraceParams& p, int x, int y
             const float dx = fmaf(fy, p.dv[0], fmaf(fx, p.du[0], p.base[0]));
             const float dy = fmaf(fy, p.dv[1], fmaf(fx, p.du[1], p.base[1]));
             const float dz = fmaf(fy, p.dv[2], fmaf(fx, p.du[2], p.base[2]));
-            const float* v = p.vertices + 9ull * id;
-            const float e1x = v[3] - v[0], e1y = v[4] - v[1], e1z = v[5] - v[2];
-            const float e2x = v[6] - v[0], e2y = v[7] - v[1], e2z = v[8] - v[2];
-            float nx, ny, nz;
-            Cross3(e1x, e1y, e1z, e2x, e2y, e2z, nx, ny, nz);
-            const float nd = Dot3(nx, ny, nz, dx, dy, dz);
-            const float nn = Dot3(nx, ny, nz, nx, ny, nz);
+            const float4 nr = p.normals[id];  // (e1 x e2, |e1 x e2|) from the prepare kernel
+            const float nd = Dot3(nr.x, nr.y, nr.z, dx, dy, dz);
             const float dd = Dot3(dx, dy, dz, dx, dy, dz);
-            const float cosv = fminf(fabsf(nd) / (sqrtf(nn) * sqrtf(dd)), 1.f);
+            const float cosv = fminf(fabsf(nd) / (nr.w * sqrtf(dd)), 1.f);
             const float* a = p.albedo + 3ull * id;
             o = make_float4(a[0] * cosv, a[1] * cosv, a[2] * cosv, static_cast<float>(id));
         } else {
@@ -2572,6 +2576,7 @@ PrepareParams MakePrepareParams(const float* d_vertices, const unsigned* d_rank,
     p.screen_boxes = reinterpret_cast<float4*>(d_edges) + PaddedTriangleCount(n) / kTileTriangles * kTileFloat4;
     p.qboxes = reinterpret_cast<uint2*>(p.screen_boxes + PaddedTriangleCount(n));
     p.cull = reinterpret_cast<CullRecord*>(p.qboxes + PaddedTriangleCount(n));
+    p.normals = reinterpret_cast<float4*>(p.cull + PaddedTriangleCount(n));
     p.n = static_cast<unsigned>(n);
     p.n_pad = static_cast<unsigned>(PaddedTriangleCount(n));
     for (int k = 0; k < 3; ++k) {
@@ -2737,6 +2742,7 @@ hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_ver
     p.screen_boxes = reinterpret_cast<const float4*>(d_edges) + PaddedTriangleCount(n) / kTileTriangles * kTileFloat4;
     p.qboxes = reinterpret_cast<const uint2*>(p.screen_boxes + PaddedTriangleCount(n));
     p.cull = reinterpret_cast<const CullRecord*>(p.qboxes + PaddedTriangleCount(n));
+    p.normals = reinterpret_cast<const float4*>(p.cull + PaddedTriangleCount(n));
     p.vertices = d_vertices;
     p.albedo = d_albedo;
     p.offsets = reinterpret_cast<const float2*>(band.offsets);
