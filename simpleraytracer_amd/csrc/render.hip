@@ -2121,16 +2121,17 @@ __device__ __forceinline__ CullSource TileSource(const TraceParams& p, const Til
 // Rays of a regular tile (every offset equal to (ox, oy), bit for bit): GenerateRays'
 // expressions without reading the offsets.
 template <int R>
-__device__ __forceinline__ void UniformRays(const TraceParams& p, int x, int y0, float ox, float oy, Rays<R>& s,
-                                            Box& box) {
+__device__ __forceinline__ void UniformRays(const TraceParams& p, int x, int y_in_block, float ox, float fy_rows,
+                                            Rays<R>& s, Box& box) {
     const int xc = min(x, p.width - 1);
     const float fx = (static_cast<float>(xc) + ox) / p.wf;
     box = Box{__builtin_inff(), -__builtin_inff(), __builtin_inff(), -__builtin_inff()};
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        const int yc = min(y0 + r, p.row_count - 1);
         s.fx[r] = fx;
-        s.fy[r] = (static_cast<float>(p.row_begin + yc) + oy) / p.hf;
+        // Row r's fy is wave-uniform: lane (y0 - row0) + r of fy_rows computed it (the same
+        // expression, (float(row_begin + yc) + oy) / hf), one division per lane instead of R.
+        s.fy[r] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(fy_rows), y_in_block + r));
         s.bt[r] = __builtin_inff();
         s.bi[r] = -1;
         box.xlo = fminf(box.xlo, s.fx[r]);
@@ -2173,8 +2174,16 @@ __global__ __launch_bounds__(kWave * W, SRT_TRACE_OCC) void TraceCullKernel(Trac
     Rays<R> s;
     Box lane_box;
     bool same = true;
-    if (binned && ti.regular != 0u) {
-        UniformRays<R>(p, x, y0, ti.ox, ti.oy, s, lane_box);
+    // Raster walks: lane = column (fx), lanes 0..kBlockRows-1 carry the block's rows' fy (the
+    // GenerateRays expression; bit-identical since every ray has the same offset).
+    float fy_lane = __builtin_nanf("");
+    const bool uniform_rays = binned && ti.regular != 0u;
+    if (uniform_rays) {
+        if (lane < kBlockRows) {
+            const int yc = min(row0 + lane, p.row_count - 1);
+            fy_lane = (static_cast<float>(p.row_begin + yc) + ti.oy) / p.hf;
+        }
+        UniformRays<R>(p, x, wave * R, ti.ox, fy_lane, s, lane_box);
     } else {
         same = GenerateRays<R>(p, x, y0, s, lane_box);
     }
@@ -2223,11 +2232,8 @@ __global__ __launch_bounds__(kWave * W, SRT_TRACE_OCC) void TraceCullKernel(Trac
     const bool list = src.list != nullptr;
     const bool raster = sh.regular != 0u && p.allow_raster != 0;
     const bool shared_fx = sh.shared_fx != 0u;
-    // Raster walks: lane = column (fx), lanes 0..kBlockRows-1 carry the block's rows' fy (the
-    // GenerateRays expression; bit-identical since every ray has the same offset).
     const float fx_lane = s.fx[0];
-    float fy_lane = __builtin_nanf("");
-    if (lane < kBlockRows) {
+    if (!uniform_rays && lane < kBlockRows) {
         const int yc = min(row0 + lane, p.row_count - 1);
         fy_lane = (static_cast<float>(p.row_begin + yc) + oy0) / p.hf;
     }
