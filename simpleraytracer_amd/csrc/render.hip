@@ -1324,6 +1324,11 @@ __device__ __forceinline__ void PacketWalk(const TraceParams& p, CullShared<W>& 
     const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);
     const unsigned long long lt_mask = (1ull << lane) - 1ull;
     auto& k = sh.u.k;
+#ifndef SRT_DIAG  // (the diag build records every block's counters)
+    if (src.end == src.begin) {
+        return;  // no candidates (block-uniform): every ray keeps its miss
+    }
+#endif
     const int nc = min(kWave, p.width - tx * kWave);
     const int nr = min(kBlockRows, p.row_count - row0);
     if (tid < kWave) {
