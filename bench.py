@@ -50,8 +50,10 @@ KERNEL_NAMES = {"lds": "TraceLdsKernel", "scalar": "TraceScalarKernel", "cull": 
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=1000)
-    p.add_argument("--warmup", type=int, default=5)
+    # 3000 frames = ~0.1 s timed at C3: 1000 frames (36 ms) read ~2.5 % low, the clocks still
+    # settling (profiles/r01/ab/README.md)
+    p.add_argument("--steps", type=int, default=3000)
+    p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--width", type=int, default=1920)
     p.add_argument("--height", type=int, default=1080)
     p.add_argument("--scene", default="soup", choices=["soup", "cornell", "triangle"])
