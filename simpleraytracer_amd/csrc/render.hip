@@ -733,6 +733,14 @@ constexpr int kParts = kTileRows / kBlockRows;
 // packet walk (row-major packets, blocks of <= 16 rows): one packed word per packet
 #define SRT_PACKET_WORD (SRT_PACKET_FLAT && SRT_BLOCK_ROWS <= 16)
 #endif
+#ifndef SRT_FAST_DIV
+// packet walk (packed word path): t = vol / det by the IEEE sequence without its range
+// scaling / fixup steps when vol and every candidate lane's det are in range (see
+// EvalPacketFast). Exact (GPU parity green with it on) but measured slower: the per-packet
+// ballot + uniform branch and the per-lane vol flag cost more than the 3 VALU they save
+// (trace 36.5 -> 42.3 us), so off by default.
+#define SRT_FAST_DIV 0
+#endif
 #ifndef SRT_PIN_LOADS
 #define SRT_PIN_LOADS 1  // packet walk: pin loop-invariant lane values and keys (ISA scheduling)
 #endif
@@ -1280,6 +1288,44 @@ __device__ __forceinline__ PacketHit EvalPacket(const float4& a, const float4& b
     return h;
 }
 
+// EvalPacket with a cheaper exact division. The compiler's IEEE f32 division is
+//   s = div_scale(det), n = div_scale(vol) [vcc], y = rcp(s), y = fma(fma(-s, y, 1), y, y),
+//   q = n y, q = fma(fma(-s, q, n), y, q), q = div_fmas(fma(-s, q, n), y, q), div_fixup(q, det, vol)
+// and div_scale leaves its operand unchanged (vcc = 0), div_fmas is then a plain fma, and
+// div_fixup returns q, whenever vol and det are normal, nonzero, |exponent difference| < 96
+// and the quotient is normal: true for vol in [2^-48, 2^48) and det in [2^-47, 2^47). Then
+// the 8 instructions below give the same bits. vol is per survivor (vol_slow: outside its
+// range), det per lane: if any lane that passes the edge tests has det outside its range (or
+// vol_slow), the whole wave takes the IEEE division (a uniform branch) -- the fast path is an
+// evaluation shortcut, never a change of result. On the fast path every passing lane has
+// 0 < det and a finite t, so the hit is (edges pass) & (det in range).
+[[maybe_unused]] __device__ __forceinline__ PacketHit EvalPacketFast(const float4& a, const float4& b, const float4& x, float fx,
+                                                    float fy, const PacketPixel& px, bool vol_slow) {
+    const float eA = fmaf(fy, a.z, fmaf(fx, a.y, a.x));
+    const float eB = fmaf(fy, b.y, fmaf(fx, b.x, a.w));
+    const float eC = fmaf(fy, x.x, fmaf(fx, b.w, b.z));
+    const float det = (eA + eB) + eC;
+    const bool e_ok = static_cast<bool>(px.in & (fminf(fminf(eA, eB), eC) >= 0.f));
+    constexpr unsigned kLo = 0x28000000u, kHi = 0x57000000u;  // 2^-47, 2^47
+    const bool det_ok = __float_as_uint(det) - kLo < kHi - kLo;
+    PacketHit h;
+    float t;
+    if (vol_slow || __ballot(e_ok && !det_ok) != 0ull) {
+        t = x.y / det;
+        h.hit = static_cast<bool>(e_ok & (det > 0.f) & (t < __builtin_inff()));
+    } else {
+        const float y0 = __builtin_amdgcn_rcpf(det);
+        const float y1 = fmaf(fmaf(-det, y0, 1.f), y0, y0);
+        const float q0 = x.y * y1;
+        const float q1 = fmaf(fmaf(-det, q0, x.y), y1, q0);
+        t = fmaf(fmaf(-det, q1, x.y), y1, q1);
+        h.hit = e_ok & det_ok;
+    }
+    h.key = HitKey(t, __float_as_int(x.z));
+    h.addr = px.rowb * (kWave * 2u) + px.colb * 2u;
+    return h;
+}
+
 // Range search in a nondecreasing table t[0..n): an index guess from a linear model, clamped
 // to [0, n], then exact unit steps (a guess off by a few entries costs a few LDS reads).
 __device__ __forceinline__ int GuessIndex(float v, float first, float scale, int n) {
@@ -1552,7 +1598,13 @@ __device__ __forceinline__ void PacketWalk(const TraceParams& p, CullShared<W>& 
 #endif
             const unsigned n = min(static_cast<unsigned>(kWave), q_end - q0);
 #if SRT_PACKET_FLAT
-            const unsigned my_m = PacketMagic(my_bits);
+            unsigned my_m = PacketMagic(my_bits);  // < 2^18; bit 31: vol outside the fast-division range
+#if SRT_FAST_DIV
+            {
+                const unsigned vb = __float_as_uint(k.sv2[my_s].y);
+                my_m |= vb - 0x27800000u < 0x57800000u - 0x27800000u ? 0u : 0x80000000u;  // [2^-48, 2^48)
+            }
+#endif
 #endif
 #if SRT_PACKET_WORD
             constexpr bool kWord = kBlockRows <= 16 && S::kPBatch <= 256;  // field widths
@@ -1575,14 +1627,18 @@ __device__ __forceinline__ void PacketWalk(const TraceParams& p, CullShared<W>& 
                 PacketPixel px[kPacketIlp];
                 float4 ra[kPacketIlp], rb[kPacketIlp], rx[kPacketIlp];
                 float fx[kPacketIlp], fy[kPacketIlp];
+                bool vol_slow[kPacketIlp];
 #pragma unroll
                 for (int u = 0; u < kPacketIlp; ++u) {
                     const unsigned li = min(i + u, n - 1u);
+                    vol_slow[u] = true;
 #if SRT_PACKET_WORD
                     if constexpr (kWord) {
                         const unsigned w = __builtin_amdgcn_readlane(my_w, li);
+                        const unsigned mm = __builtin_amdgcn_readlane(my_m, li);
                         ps[u] = (w >> 20) & 255u;
-                        px[u] = PacketLaneWord(w, __builtin_amdgcn_readlane(my_m, li), lane);
+                        vol_slow[u] = (mm >> 31) != 0u;
+                        px[u] = PacketLaneWord(w, mm, lane);
                     } else {
                         ps[u] = __builtin_amdgcn_readlane(my_s, li);
                         px[u] = PacketLaneFlat(__builtin_amdgcn_readlane(my_bits, li),
@@ -1609,7 +1665,12 @@ __device__ __forceinline__ void PacketWalk(const TraceParams& p, CullShared<W>& 
                 PacketHit h[kPacketIlp];
 #pragma unroll
                 for (int u = 0; u < kPacketIlp; ++u) {
+#if SRT_FAST_DIV && SRT_PACKET_FLAT
+                    h[u] = EvalPacketFast(ra[u], rb[u], rx[u], fx[u], fy[u], px[u], vol_slow[u]);
+#else
+                    (void)vol_slow[u];
                     h[u] = EvalPacket(ra[u], rb[u], rx[u], fx[u], fy[u], px[u]);
+#endif
                 }
 #if SRT_PIN_LOADS
                 // Keys built before the hit branches: the record id is loaded with the rest of
