@@ -3,24 +3,26 @@
 
     python bench.py [--gpus N --steps K --warmup W]        (N > 1: launched by torch.distributed.run)
 
-One step = one frame of the hot path on device-resident inputs (SURVEY.md section 8 rows
-a9-a12): edge-record setup (prepare kernel) + the closest-hit trace with its cull bins
-(TileInfo / BinTriangles / TileOrder kernels, then TraceCullKernel, which also shades and
-stores the framebuffer). The trace result is bit-identical to brute force (every ray against
-every triangle; DESIGN.md section 5, tests/test_gpu_parity.py).
+One step = one complete frame of the hot path on device-resident inputs (SURVEY.md section 8
+rows a9-a13): edge-record setup (prepare kernel), the cull bins (tile bounds / bin / work-list
+kernels), the closest-hit trace (TraceCullKernel; its frame is bit-identical to brute force,
+DESIGN.md section 5, tests/test_gpu_parity.py), shading and the framebuffer store. Nothing is
+cached across frames.
 
-Multi-GPU, one rank per GPU:
-  --mode frames (default): every rank renders whole 1920x1080 frames of a temporal-jitter
-      sequence (rank r's frames use the uniform sub-pixel offset J_r; J_0 = 0.5 = the headline
-      frame); no collective in the timed region; "scaling": "weak". Each rank keeps --queues
-      frames in flight (default 3): frame k goes to queue k % Q, a DeviceScene with its own edge
-      records, bins and framebuffer on its own HIP stream, so one frame's stages fill the CUs
-      another frame's heavy-tile tail leaves idle. The one-frame-in-flight rate is reported
-      beside it ("single_queue").
-  --mode bands: the frame's rows are split into P bands (north_star row bands), each rank
-      traces its band, and the bands are gathered to rank 0 over RCCL every step (double
-      buffered, so step k's gather overlaps step k+1's render); "scaling": "strong".
-  For N > 1 the line also carries the other mode's measurement under "bands" / "frames".
+Multi-GPU, one rank per GPU over RCCL:
+  --mode bands (default; BASELINE config C4): every frame is tiled into P row bands, rank r
+      traces band r, the bands are gathered over RCCL to the frame's compositing rank, which
+      shades and stores the whole frame. The gather moves each band's hit ids (int32, 4 B per
+      pixel; deferred shading, bit-identical); the compositor is rank k % P for frame k
+      (--root rotate, default) or rank 0 (--root fixed). Each rank keeps --queues frames in
+      flight: queue q = its own DeviceScene (edge records, bins), HIP stream, band / frame
+      buffers and RCCL process group, so one frame's setup, trace, gather and shading overlap
+      the others'. value = frames x W x H / the max-over-ranks time: "scaling": "strong".
+      After the timed loop every compositing rank compares its last frame with a one-GPU
+      render of the same frame bit for bit ("verified").
+  --mode frames: every rank renders whole frames of a temporal-jitter sequence (no collective);
+      "scaling": "weak". Reported beside the bands line at N > 1 ("frames").
+At N = 1 the two modes coincide (one band = the frame, shaded in the trace).
 
 Prints ONE JSON line on rank 0 (fields in DESIGN.md section 6).
 """
@@ -39,12 +41,15 @@ sys.path.insert(0, str(REPO))
 
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md chip table (spec)
 FP32_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md chip table (spec, vector fp32, packed)
+SIMDS, CLOCK_GHZ = 1024, 2.4  # 256 CUs x 4 SIMD-32; wave64 VALU issue = 2 cycles per instruction
 EDGE_BYTES_PER_TRI = 36      # 9 fp32 edge coefficients per ray-triangle test
+CULL_RECORD_BYTES = 64       # one cull record per triangle (render.hip CullRecord)
 PIXEL_IO_BYTES = 8 + 16      # sample offsets in + RGBA out per ray
 FLOPS_PER_TEST = 12          # 3 edge functions x 2 FMA
 GOLDEN = 0.6180339887498949  # temporal jitter sequence step
 KERNEL_NAMES = {"lds": "TraceLdsKernel", "scalar": "TraceScalarKernel", "cull": "TraceCullKernel",
                 "bvh": "TraceBvhKernel"}
+PROFILES = REPO / "profiles"
 
 
 def parse():
@@ -59,34 +64,230 @@ def parse():
     p.add_argument("--scene", default="soup", choices=["soup", "cornell", "triangle"])
     p.add_argument("--triangles", type=int, default=100_000)
     p.add_argument("--variant", default=os.environ.get("SRT_BENCH_VARIANT", "cull"), choices=list(KERNEL_NAMES))
-    p.add_argument("--mode", default="frames", choices=["frames", "bands"], help="multi-GPU split (see module doc)")
+    p.add_argument("--mode", default="bands", choices=["bands", "frames"], help="multi-GPU split (module doc)")
+    p.add_argument("--root", default="rotate", choices=["rotate", "fixed"], help="bands: compositing rank")
     p.add_argument("--queues", type=int, default=int(os.environ.get("SRT_BENCH_QUEUES", "3")),
-                   help="frames mode: frame queues in flight per GPU (own scene buffers + HIP stream each)")
+                   help="frames in flight per GPU (own scene buffers, HIP stream, process group each)")
+    p.add_argument("--offsets", default="uniform", choices=["uniform", "random"],
+                   help="sample offsets: uniform 0.5 (headline) or seeded U[0,1) per-pixel jitter")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample length")
     p.add_argument("--brute-steps", type=int, default=5, help="timed frames of the brute-force LDS kernel (0 = skip)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive ml* API measurement")
+    p.add_argument("--no-extras", action="store_true", help="only the main line (no secondary legs)")
     return p.parse_args()
 
 
-def workload_name(a):
-    if a.scene == "soup":
-        tri = f"{a.triangles // 1000}k" if a.triangles % 1000 == 0 else str(a.triangles)
+def workload_name(a, scene=None, triangles=None):
+    scene = scene or a.scene
+    triangles = triangles or a.triangles
+    if scene == "soup":
+        tri = f"{triangles // 1000}k" if triangles % 1000 == 0 else str(triangles)
         return f"soup-{tri} {a.width}x{a.height} 1spp"
-    return f"{a.scene} {a.width}x{a.height} 1spp"
+    return f"{scene} {a.width}x{a.height} 1spp"
 
 
 def jitter(rank: int) -> float:
-    """Uniform sub-pixel offset of rank r's frames (r = 0: 0.5, the headline frame)."""
+    """Uniform sub-pixel offset of rank r's frames in frames mode (r = 0: 0.5, the headline frame)."""
     import numpy as np
 
     return float(np.float32((0.5 + rank * GOLDEN) % 1.0))
+
+
+def make_offsets(torch, a, dev, value=0.5, kind="uniform", seed=0x5EED):
+    if kind == "random":  # seeded per-pixel jitter, U[0, 1)
+        g = torch.Generator(device="cpu").manual_seed(seed)
+        return torch.rand((a.height, a.width, 2), generator=g, dtype=torch.float32).to(dev)
+    return torch.full((a.height, a.width, 2), value, dtype=torch.float32, device=dev)
+
+
+class Ctx:
+    """This rank's process-wide state: torch, the process groups, the device, the scene files."""
+
+    def __init__(self, a):
+        import torch
+        import torch.distributed as dist
+
+        import simpleraytracer_amd as srt
+
+        self.torch, self.dist, self.srt, self.a = torch, dist, srt, a
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        if os.environ.get("SRT_BENCH_ONE_DEVICE"):  # rehearsal of N > 1 ranks on a one-GPU box (with gloo)
+            local = 0
+        if self.world != a.gpus:
+            raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={self.world}")
+        torch.cuda.set_device(local)
+        self.dev = torch.device("cuda", local)
+        self.backend = None
+        self.groups = []
+        if self.world > 1:
+            self.backend = os.environ.get("SRT_BENCH_BACKEND", "nccl")  # gloo: CPU-side rehearsal on one GPU
+            if self.backend == "nccl":
+                dist.init_process_group("nccl", device_id=self.dev)
+            else:
+                dist.init_process_group(self.backend)
+            # one process group (RCCL communicator, NCCL stream) per frame queue: the gathers of
+            # different frames in flight run concurrently
+            self.groups = [dist.new_group(list(range(self.world))) for _ in range(max(1, a.queues))]
+        self.tmp = tempfile.TemporaryDirectory()
+        self.paths = {}
+
+    def scene_path(self, kind, triangles=None):
+        key = (kind, triangles)
+        if key not in self.paths:
+            path = os.path.join(self.tmp.name, f"{kind}_{triangles}_rank{self.rank}.srt")
+            if kind == "soup":
+                self.srt.write_scene(path, "soup", triangles)
+            else:
+                self.srt.write_scene(path, kind)
+            self.paths[key] = path
+        return self.paths[key]
+
+    def max_over_ranks(self, x):
+        if self.world == 1:
+            return x
+        t = self.torch.tensor([x], dtype=self.torch.float64,
+                              device=self.dev if self.backend != "gloo" else "cpu")
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def barrier(self):
+        if self.world > 1:
+            self.dist.barrier()
+
+
+class Pipeline:
+    """Frames over `queues` frame queues on this rank (module doc). mode "bands": rank r traces
+    band r of every frame (P > 1: hit ids, gathered to the compositor, which shades); mode
+    "frames": whole frames, each rank its own jitter; P == 1: the two coincide."""
+
+    def __init__(self, ctx, path, mode="bands", queues=3, variant="cull", offsets="uniform", rotate=True):
+        from simpleraytracer_amd.bands import band_range, band_rows
+
+        torch, a = ctx.torch, ctx.a
+        self.ctx, self.mode, self.variant, self.rotate = ctx, mode, variant, rotate
+        self.W, self.H = a.width, a.height
+        P = ctx.world if mode == "bands" else 1
+        self.P = P
+        self.row_begin, self.row_count = band_range(self.H, P, ctx.rank) if P > 1 else (0, self.H)
+        self.B = band_rows(self.H, P)
+        self.offsets = make_offsets(torch, a, ctx.dev, jitter(ctx.rank) if mode == "frames" else 0.5, offsets,
+                                    seed=0x5EED + (ctx.rank if mode == "frames" else 0))
+        self.band_off = self.offsets[self.row_begin:self.row_begin + self.row_count]
+        self.queues = []
+        for q in range(max(1, queues)):
+            qd = {"scene": ctx.srt.DeviceScene(path, ctx.dev.index), "stream": torch.cuda.Stream(ctx.dev),
+                  "rgba": torch.zeros((self.H, self.W, 4), dtype=torch.float32, device=ctx.dev), "root": None}
+            if P > 1:
+                qd["band_ids"] = torch.full((self.B, self.W), -1, dtype=torch.int32, device=ctx.dev)
+                qd["frame_ids"] = torch.empty((P * self.B, self.W), dtype=torch.int32, device=ctx.dev)
+                qd["group"] = ctx.groups[q % len(ctx.groups)]
+            self.queues.append(qd)
+        self.triangles = self.queues[0]["scene"].triangles
+
+    def step(self, k, nq):
+        from simpleraytracer_amd.bands import compositor, gather_band_ids
+
+        ctx, torch = self.ctx, self.ctx.torch
+        q = self.queues[k % nq]
+        sc, st = q["scene"], q["stream"]
+        sc.prepare(self.W, self.H, st)
+        if self.P == 1:
+            sc.trace(self.offsets, q["rgba"], 0, self.H, variant=self.variant, stream=st)
+            q["root"] = 0
+            return
+        rows = self.row_count
+        if rows:
+            sc.trace_ids(self.band_off, q["band_ids"][:rows], self.row_begin, rows, variant=self.variant, stream=st)
+        root = compositor(k, self.P, self.rotate)
+        if ctx.backend == "gloo":  # CPU rehearsal: gloo gathers host tensors, synchronously
+            st.synchronize()
+            frame, _ = gather_band_ids(q["band_ids"].cpu(), self.H, dst=root, group=q["group"])
+            if frame is not None:
+                q["frame_ids"][:self.H].copy_(frame.to(ctx.dev))
+                torch.cuda.synchronize(ctx.dev)
+        else:
+            with torch.cuda.stream(st):
+                _, work = gather_band_ids(q["band_ids"], self.H, dst=root, group=q["group"], out=q["frame_ids"],
+                                          async_op=True)
+                work.wait()  # the queue's stream waits for the gather (ids consumed / band reusable)
+        if ctx.rank == root:
+            sc.shade(self.offsets, q["frame_ids"][:self.H], q["rgba"], 0, self.H, stream=st)
+        q["root"] = root
+
+    def drain(self):
+        for q in self.queues:
+            q["stream"].synchronize()
+
+    def run(self, steps, warmup, queues=None, timing=False):
+        """`steps` timed frames after `warmup` per queue; stage timing binds events on queue 0's
+        scene (use queues=1 then)."""
+        torch, ctx = self.ctx.torch, self.ctx
+        nq = min(queues or len(self.queues), len(self.queues))
+        for k in range(warmup * nq):
+            self.step(k, nq)
+        self.drain()
+        sc0 = self.queues[0]["scene"]
+        sc0.take_stage_times()
+        sc0.set_stage_timing(timing)
+        ctx.barrier()
+        torch.cuda.synchronize(ctx.dev)
+        t0 = time.perf_counter()
+        for k in range(steps):
+            self.step(warmup * nq + k, nq)
+        self.drain()
+        torch.cuda.synchronize(ctx.dev)
+        ctx.barrier()
+        elapsed = ctx.max_over_ranks(time.perf_counter() - t0)
+        sc0.set_stage_timing(False)
+        launches, prep_ms, bin_ms, trace_ms = sc0.take_stage_times()
+        units = self.W * self.H * steps * (ctx.world if self.mode == "frames" else 1)
+        return {"elapsed": elapsed, "mrays": units / elapsed / 1e6, "prepare_ms": prep_ms, "bin_ms": bin_ms,
+                "trace_ms": trace_ms, "launches": launches, "ms_per_step": elapsed / steps * 1e3, "queues": nq}
+
+    def verify(self):
+        """Every rank that composited a frame compares its last one with a one-GPU render of the
+        same frame (fused trace, this device), bit for bit; True on every rank iff all agree."""
+        ctx, torch = self.ctx, self.ctx.torch
+        ok = True
+        for q in self.queues:
+            if q["root"] == ctx.rank:
+                ref_scene = ctx.srt.DeviceScene(q["scene"].path, ctx.dev.index)
+                ref = torch.empty_like(q["rgba"])
+                st = torch.cuda.current_stream(ctx.dev)
+                ref_scene.prepare(self.W, self.H, st)
+                ref_scene.trace(self.offsets, ref, 0, self.H, variant=self.variant, stream=st)
+                torch.cuda.synchronize(ctx.dev)
+                ok = ok and bool(torch.equal(ref.view(torch.int32), q["rgba"].view(torch.int32)))
+                ref_scene.close()
+                break
+        return ctx.max_over_ranks(0.0 if ok else 1.0) == 0.0
+
+    def close(self):
+        for q in self.queues:
+            q["scene"].close()
+
+
+def stage_times_all_ranks(ctx, r):
+    """[prepare, bin, trace] ms of every rank (instrumented single-queue pass)."""
+    torch = ctx.torch
+    mine = torch.tensor([r["prepare_ms"], r["bin_ms"], r["trace_ms"]], dtype=torch.float64,
+                        device=ctx.dev if ctx.backend != "gloo" else "cpu")
+    if ctx.world == 1:
+        return [mine.tolist()]
+    out = [torch.zeros_like(mine) for _ in range(ctx.world)]
+    ctx.dist.all_gather(out, mine)
+    return [t.tolist() for t in out]
 
 
 def cpu_baseline(scene_path, a):
     """The oracle ('port') on this host's cores over a bounded, evenly spaced row sample."""
     from oracle import srt_oracle
 
+    # OMP_NUM_THREADS is the GPU box's CPU share for one GPU (16 of its 256 host CPUs; gpurun
+    # and the driver set it); os.cpu_count() reports the whole machine.
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
     sc = srt_oracle.OracleScene(scene_path)
     h = a.height
@@ -127,206 +328,142 @@ def cpu_baseline(scene_path, a):
         "kind": "port",
         "sample": f"{rows} of {h} rows (every {step}th, all {a.width} columns) of {workload_name(a)}; "
                   f"{dt:.1f} s; OpenMP scalar C oracle (oracle/srt_oracle.c), brute force",
+        "cores_note": "OMP_NUM_THREADS = this GPU's share of the box's host CPUs (host_cpus counts the "
+                      "whole machine)",
     }
 
 
-def pmc_traffic(workload, variant):
-    """HBM bytes per trace launch from the committed rocprofv3 PMC summary (profiles/), or None."""
-    f = REPO / "profiles" / "pmc_traffic.json"
+def committed_profile(name, key):
+    """An entry of a committed profiles/ summary (rocprofv3 PMC passes), or None."""
+    f = PROFILES / name
     if not f.exists():
         return None
     try:
-        e = json.loads(f.read_text()).get(f"{workload}|{variant}")
-        return None if e is None else float(e["hbm_bytes_per_launch"])
+        return json.loads(f.read_text()).get(key)
     except Exception:
         return None
 
 
-class Frames:
-    """Timed loop of one multi-GPU mode on this rank (module doc)."""
+def roofline_fields(wl, variant, launch_rays, n_tri, kernel_ms, band_ids):
+    """The trace kernel's roofline (algorithmic bytes: each ray's offsets in + its output, each
+    triangle's cull record once), the measured VALU issue from the committed PMC summary, and
+    the section 8(d) brute-force-equivalent figures, clearly separated."""
+    kernel_s = kernel_ms * 1e-3
+    out_bytes = 4 if band_ids else 16
+    alg = launch_rays * (8 + out_bytes) + n_tri * CULL_RECORD_BYTES
+    achieved = alg / kernel_s / 1e9
+    pmc = committed_profile("pmc_traffic.json", f"{wl}|{variant}") or {}
+    roof = {
+        "bound": "hbm",
+        "achieved": round(achieved, 1),
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 4),
+        "traffic": pmc.get("hbm_bytes_per_launch"),
+        "kernel": KERNEL_NAMES[variant],
+        "kernel_ms": round(kernel_ms, 5),
+        "bytes_per_launch": alg,
+        "note": f"algorithmic bytes = launch rays x (8 B offsets in + {out_bytes} B out) + triangles x 64 B "
+                "(each cull record once), over the trace kernel's HIP-event time; traffic = measured HBM "
+                "bytes per launch (rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE, profiles/pmc_traffic.json)",
+    }
+    sq = committed_profile("pmc_sq.json", f"{wl}|{variant}")
+    valu = None
+    if sq and sq.get("sq_insts_valu_per_launch"):
+        issue_s = sq["sq_insts_valu_per_launch"] * 2 / (SIMDS * CLOCK_GHZ * 1e9)
+        valu = {"valu_insts_per_launch": sq["sq_insts_valu_per_launch"], "issue_us": round(issue_s * 1e6, 2),
+                "frac": round(issue_s / kernel_s, 4),
+                "note": "SQ_INSTS_VALU (rocprofv3, profiles/pmc_sq.json) x 2 cycles per wave64 instruction "
+                        "/ (1024 SIMDs x 2.4 GHz), over the kernel time"}
+    tests = launch_rays * n_tri
+    bf_bytes = launch_rays * (EDGE_BYTES_PER_TRI * n_tri + PIXEL_IO_BYTES)
+    bfe = {"bytes_per_launch": bf_bytes, "tests_per_launch": tests,
+           "hbm_equivalent_gbs": round(bf_bytes / kernel_s / 1e9, 1),
+           "hbm_equivalent_frac": round(bf_bytes / kernel_s / 1e9 / HBM_PEAK_GBS, 2),
+           "valu_equivalent_tflops": round(tests * FLOPS_PER_TEST / kernel_s / 1e12, 1),
+           "note": "SURVEY 8(d) brute-force figures (36 B and 12 flops per ray-triangle test) over the cull "
+                   "kernel's time: the work a brute-force kernel would do for the same bit-identical frame; "
+                   "not a utilisation (the cull kernel proves most pairs miss without testing them)"}
+    return roof, valu, bfe
 
-    def __init__(self, torch, dist, srt, scene, a, mode, world, rank, dev, variant, queues=1):
-        from simpleraytracer_amd.bands import band_range, band_rows
 
-        self.torch, self.dist, self.scene, self.a = torch, dist, scene, a
-        self.mode, self.world, self.rank, self.variant = mode, world, rank, variant
-        W, H = a.width, a.height
-        if mode == "bands":
-            self.row_begin, self.row_count = band_range(H, world, rank)
-            B = band_rows(H, world)
-            off = 0.5
-        else:
-            self.row_begin, self.row_count = 0, H
-            B = H
-            off = jitter(rank)
-        self.offsets = torch.full((B, W, 2), off, dtype=torch.float32, device=dev)
-        nbuf = 2 if (mode == "bands" and world > 1) else 1
-        self.bands = [torch.zeros((B, W, 4), dtype=torch.float32, device=dev) for _ in range(nbuf)]
-        self.frames = None
-        if mode == "bands" and world > 1 and rank == 0:
-            self.frames = [torch.empty((world * B, W, 4), dtype=torch.float32, device=dev) for _ in range(nbuf)]
-        self.pending = [None] * nbuf
-        self.stream = torch.cuda.current_stream(dev)
-        self.dev = dev
-        # Frame queues (frames mode): queue q = its own DeviceScene (edge records, bins, BVH)
-        # + framebuffer + HIP stream; frame k goes to queue k % Q, so up to Q frames are in
-        # flight and one frame's prepare/bin/trace fills the CUs another frame's heavy-tile
-        # tail leaves idle. Queue 0 is `scene` (on the current stream in the Q = 1 loop).
-        self.queues = [(scene, self.stream, self.offsets, self.bands[0])]
-        if mode == "frames" and queues > 1:
-            self.queues[0] = (scene, torch.cuda.Stream(dev), self.offsets, self.bands[0])  # all on side streams
-            for _ in range(max(1, queues) - 1):
-                self.queues.append((srt.DeviceScene(scene.path, dev.index), torch.cuda.Stream(dev),
-                                    self.offsets.clone(), torch.zeros_like(self.bands[0])))
-
-    def step(self, k, queues=1):
-        from simpleraytracer_amd.bands import gather_bands
-
-        a, W, H = self.a, self.a.width, self.a.height
-        if queues > 1:  # frames mode, no collective
-            scene, stream, offsets, band = self.queues[k % queues]
-            scene.prepare(W, H, stream)
-            scene.trace(offsets, band, 0, H, variant=self.variant, stream=stream)
-            return
-        slot = k % len(self.bands)
-        if self.pending[slot] is not None:
-            self.pending[slot].wait()  # the gather still reading this band buffer
-            self.pending[slot] = None
-        self.scene.prepare(W, H, self.stream)
-        band = self.bands[slot]
-        self.scene.trace(self.offsets[:self.row_count], band[:self.row_count], self.row_begin, self.row_count,
-                         variant=self.variant, stream=self.stream)
-        if self.mode == "bands" and self.world > 1:
-            out = self.frames[slot] if self.frames is not None else None
-            if self.dist.get_backend() == "gloo":  # CPU rehearsal only: gloo gathers host tensors
-                gather_bands(band.cpu(), H, dst=0)
-            else:
-                self.pending[slot] = self.dist.gather(band, gather_list=None if out is None else
-                                                      [out[r * band.shape[0]:(r + 1) * band.shape[0]]
-                                                       for r in range(self.world)], dst=0, async_op=True)
-
-    def run(self, steps, warmup, timing=True, queues=1):
-        """K timed frames over `queues` frame queues (stage timing: queue 0's events, so
-        timing runs use queues=1)."""
-        torch, dist = self.torch, self.dist
-        queues = min(queues, len(self.queues))
-        for k in range(warmup * queues):
-            self.step(k, queues)
-        self.drain()
-        self.scene.take_stage_times()
-        self.scene.set_stage_timing(timing)
-        if self.world > 1:
-            dist.barrier()
-        torch.cuda.synchronize(self.dev)
-        t0 = time.perf_counter()
-        for k in range(steps):
-            self.step(warmup * queues + k, queues)
-        self.drain()
-        torch.cuda.synchronize(self.dev)
-        if self.world > 1:
-            dist.barrier()
-        elapsed = time.perf_counter() - t0
-        self.scene.set_stage_timing(False)
-        if self.world > 1:
-            t = torch.tensor([elapsed], dtype=torch.float64, device=self.dev if dist.get_backend() != "gloo" else "cpu")
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            elapsed = float(t.item())
-        launches, prep_ms, bin_ms, trace_ms = self.scene.take_stage_times()
-        units = self.a.width * self.a.height * steps * (self.world if self.mode == "frames" else 1)
-        return {"elapsed": elapsed, "mrays": units / elapsed / 1e6, "prepare_ms": prep_ms, "bin_ms": bin_ms,
-                "trace_ms": trace_ms, "launches": launches, "ms_per_step": elapsed / steps * 1e3, "queues": queues}
-
-    def close(self):
-        for q in self.queues[1:]:
-            q[0].close()
-        self.queues = self.queues[:1]
-
-    def drain(self):
-        for i, h in enumerate(self.pending):
-            if h is not None:
-                h.wait()
-                self.pending[i] = None
+def leg_summary(r):
+    return {"mrays_per_s": round(r["mrays"], 3), "ms_per_step": round(r["ms_per_step"], 5), "queues": r["queues"]}
 
 
 def main():
     a = parse()
-    import torch
-    import torch.distributed as dist
-
-    import simpleraytracer_amd as srt
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if os.environ.get("SRT_BENCH_ONE_DEVICE"):  # rehearsal of N > 1 ranks on a one-GPU box (with gloo)
-        local = 0
-    if world != a.gpus:
-        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        backend = os.environ.get("SRT_BENCH_BACKEND", "nccl")  # gloo: CPU-side rehearsal on one GPU
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group(backend)
-
-    tmp = tempfile.TemporaryDirectory()
-    scene_path = os.path.join(tmp.name, f"scene_rank{rank}.srt")
-    if a.scene == "soup":
-        srt.write_scene(scene_path, "soup", a.triangles)
-    else:
-        srt.write_scene(scene_path, a.scene)
-    scene = srt.DeviceScene(scene_path, local)
-    n_tri = scene.triangles
-    W, H = a.width, a.height
+    ctx = Ctx(a)
+    world, rank = ctx.world, ctx.rank
+    path = ctx.scene_path(a.scene, a.triangles if a.scene == "soup" else None)
     wl = workload_name(a)
-
-    main_run = Frames(torch, dist, srt, scene, a, a.mode, world, rank, dev, a.variant, a.queues)
-    # value: uninstrumented frames over the frame queues. Then the same K frames on one queue
-    # (one frame in flight: the per-frame latency), and again with HIP events bound to the
-    # kernels' dispatch packets for the stage times (each event-bound dispatch leaves a 5-10 us
-    # bubble on the stream, so the instrumented frame is slower; all three are reported).
-    r = main_run.run(a.steps, a.warmup, timing=False, queues=a.queues)
-    r1 = main_run.run(a.steps, a.warmup, timing=False) if r["queues"] > 1 else r
-    rt = main_run.run(a.steps, 0, timing=True)
+    rotate = a.root == "rotate"
+    main_run = Pipeline(ctx, path, a.mode, a.queues, a.variant, a.offsets, rotate)
+    n_tri = main_run.triangles
+    W, H = a.width, a.height
+    extras = not a.no_extras
+    # Secondary passes first (they also bring the clocks up before the timed value loop): one
+    # frame in flight (per-frame latency), then the same with HIP events bound to the kernels'
+    # dispatch packets for the stage times (each event-bound dispatch leaves a 5-10 us bubble,
+    # so that pass is slower; its kernel durations are not inflated by frame overlap).
+    r1 = main_run.run(a.steps, a.warmup, queues=1) if len(main_run.queues) > 1 else None
+    rt = main_run.run(min(a.steps, 1000), 2, queues=1, timing=True)
+    ranks_stages = stage_times_all_ranks(ctx, rt)
+    # value: uninstrumented frames over the frame queues
+    r = main_run.run(a.steps, a.warmup)
+    verified = main_run.verify() if (world > 1 and a.mode == "bands") else None
     main_run.close()
-    for k in ("prepare_ms", "bin_ms", "trace_ms", "launches"):
-        r[k] = rt[k]
-    r["ms_per_step_instrumented"] = rt["ms_per_step"]
-    other = None
-    if world > 1:  # the other multi-GPU mode, same steps (secondary: a failure is reported, not fatal)
-        om = "bands" if a.mode == "frames" else "frames"
+    legs = {}
+    if world > 1 and extras:  # the other split and the other compositor choice, same steps
         try:
-            orun = Frames(torch, dist, srt, scene, a, om, world, rank, dev, a.variant, a.queues)
-            other = (om, orun.run(a.steps, a.warmup, timing=False, queues=a.queues))
-            ot = orun.run(a.steps, 0, timing=True)
-            orun.close()
-            for k in ("prepare_ms", "bin_ms", "trace_ms"):
-                other[1][k] = ot[k]
+            om = "frames" if a.mode == "bands" else "bands"
+            o = Pipeline(ctx, path, om, a.queues, a.variant, a.offsets, rotate)
+            legs[om] = {**leg_summary(o.run(a.steps, a.warmup)), "scaling": "weak" if om == "frames" else "strong"}
+            o.close()
+            if a.mode == "bands":
+                o = Pipeline(ctx, path, "bands", a.queues, a.variant, a.offsets, not rotate)
+                legs["fixed_root" if rotate else "rotating_root"] = leg_summary(o.run(a.steps, a.warmup))
+                o.close()
         except Exception as e:  # noqa: BLE001 -- the primary line must still be printed
-            other = (om, {"error": f"{type(e).__name__}: {e}"})
-    brute = None
-    if world == 1 and a.brute_steps > 0 and a.variant != "lds":
-        brute = Frames(torch, dist, srt, scene, a, "frames", 1, 0, dev, "lds").run(a.brute_steps, 1, timing=True)
-    alt = {}
-    if world == 1 and a.brute_steps > 0:  # the other exact accelerator, same frame
-        for v in ("cull", "bvh"):
-            if v != a.variant:
-                fr = Frames(torch, dist, srt, scene, a, "frames", 1, 0, dev, v, a.queues)
-                alt[v] = fr.run(a.steps, a.warmup, timing=False, queues=a.queues)
-                t = fr.run(a.steps, 0, timing=True)
-                fr.close()
-                alt[v].update({k: t[k] for k in ("prepare_ms", "bin_ms", "trace_ms")})
+            legs["secondary_error"] = f"{type(e).__name__}: {e}"
+    if world == 1 and extras:
+        if a.offsets == "uniform":  # per-pixel jitter: the irregular-offset path
+            o = Pipeline(ctx, path, "bands", a.queues, a.variant, "random")
+            rr = o.run(min(a.steps, 1000), a.warmup)
+            rt2 = o.run(min(a.steps, 300), 2, queues=1, timing=True)
+            o.close()
+            legs["offsets_random"] = {**leg_summary(rr), "trace_kernel_ms": round(rt2["trace_ms"], 5),
+                                      "note": "seeded U[0,1) per-pixel sample offsets (every tile irregular)"}
+        if a.scene == "soup":  # C2: the Cornell box at the same resolution
+            o = Pipeline(ctx, ctx.scene_path("cornell"), "bands", a.queues, a.variant, a.offsets)
+            legs["c2_cornell"] = {**leg_summary(o.run(min(a.steps, 1000), a.warmup)),
+                                  "workload": workload_name(a, "cornell")}
+            o.close()
+        if a.brute_steps > 0 and a.variant != "lds":
+            o = Pipeline(ctx, path, "bands", 1, "lds", a.offsets)
+            legs["brute_force"] = o.run(a.brute_steps, 1, queues=1, timing=True)
+            o.close()
+        if a.brute_steps > 0:  # the other exact accelerator, same frame
+            for v in ("cull", "bvh"):
+                if v != a.variant:
+                    o = Pipeline(ctx, path, "bands", a.queues, v, a.offsets)
+                    vr = o.run(min(a.steps, 1000), a.warmup)
+                    vt = o.run(min(a.steps, 300), 2, queues=1, timing=True)
+                    o.close()
+                    legs[f"variant_{v}"] = {**leg_summary(vr), "kernel": KERNEL_NAMES[v],
+                                            "stages_ms": {"prepare": round(vt["prepare_ms"], 5),
+                                                          "bin": round(vt["bin_ms"], 5),
+                                                          "trace_kernel": round(vt["trace_ms"], 5)},
+                                            "note": "bit-identical frame (tests/test_gpu_parity.py)"}
 
     if rank == 0:
+        band_ids = world > 1 and a.mode == "bands"
         launch_rays = main_run.row_count * W
-        rays_tests = launch_rays * n_tri
-        alg_bytes = launch_rays * (EDGE_BYTES_PER_TRI * n_tri + PIXEL_IO_BYTES)
-        kernel_s = r["trace_ms"] * 1e-3
-        achieved_gbs = alg_bytes / kernel_s / 1e9
-        io_gbs = launch_rays * PIXEL_IO_BYTES / kernel_s / 1e9
-        achieved_tf = rays_tests * FLOPS_PER_TEST / kernel_s / 1e12
+        roof, valu, bfe = roofline_fields(wl, a.variant, launch_rays, n_tri, rt["trace_ms"], band_ids)
+        if band_ids:
+            par = f"bands x{world} + RCCL gather of hit ids to the {'rotating' if rotate else 'rank-0'} compositor"
+        else:
+            par = f"{a.mode} x{world}"
         line = {
             "metric": "Mrays/s at 1920x1080 on 100k-tri synthetic mesh",
             "value": round(r["mrays"], 4),
@@ -334,97 +471,67 @@ def main():
             "n_gpus": world,
             "steps": a.steps,
             "warmup": a.warmup,
-            "ms_per_step": round(r["ms_per_step"], 4),
+            "ms_per_step": round(r["ms_per_step"], 5),
             "higher_is_better": True,
-            "scaling": "weak" if a.mode == "frames" else "strong",
+            "scaling": "strong" if a.mode == "bands" else "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (PCG32 triangle soup, seed 0x5EED; uniform sample offsets resident in HBM)",
+            "data": f"synthetic (PCG32 triangle soup, seed 0x5EED; {a.offsets} sample offsets resident in HBM)",
             "config": {
                 "workload": wl,
                 "triangles": int(n_tri),
                 "width": W,
                 "height": H,
                 "spp": 1,
-                "parallelism": (f"{a.mode} x{world}" + (" + RCCL gather" if a.mode == "bands" and world > 1 else "")),
+                "parallelism": par,
                 "trace_variant": a.variant,
                 "frame_queues": r["queues"],
-                "cull_bins": os.environ.get("SRT_CULL_BIN", "1") != "0" if a.variant == "cull" else None,
+                "offsets": a.offsets,
             },
-            "roofline": {
-                "bound": "hbm",
-                "achieved": round(achieved_gbs, 1),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
-                "traffic": pmc_traffic(wl, a.variant),
-                "kernel": KERNEL_NAMES[a.variant],
-                "kernel_ms": round(r["trace_ms"], 5),
-                "bytes_per_launch": alg_bytes,
-                "note": "north_star HBM roofline (SURVEY 8d): 36 B per ray-triangle test + 24 B per ray, over the "
-                        "trace kernel's HIP-event time (bin kernels excluded). frac > 1: the kernel skips "
-                        "(record, tile) pairs that provably miss and re-uses records through LDS (DESIGN.md 6)",
-            },
-            "pixel_io_roofline": {
-                "achieved": round(io_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(io_gbs / HBM_PEAK_GBS, 4),
-                "note": "offsets in + RGBA out (24 B/ray) over the trace kernel time: the bytes no design avoids",
-            },
-            "compute_roofline": {
-                "bound": "valu-fp32",
-                "achieved": round(achieved_tf, 2),
-                "peak": FP32_PEAK_TFLOPS,
-                "unit": "TFLOP/s",
-                "frac": round(achieved_tf / FP32_PEAK_TFLOPS, 4),
-                "flops_per_test": FLOPS_PER_TEST,
-                "note": "brute-force-equivalent flops (every ray x every triangle)",
-            },
-            "stages_ms": {"prepare": round(r["prepare_ms"], 5), "bin": round(r["bin_ms"], 5),
-                          "trace_kernel": round(r["trace_ms"], 5), "frame": round(r["ms_per_step"], 5),
-                          "frame_instrumented": round(r["ms_per_step_instrumented"], 5),
-                          "timed_launches": r["launches"],
-                          "note": "cull variant: prepare = PrepareInfoKernel (edge records + per-tile info, one "
-                                  "launch), bin = BinTrianglesKernel + TileOrderKernel, trace_kernel "
-                                  "= TraceCullKernel; frame = uninstrumented, frame_instrumented = with the events"},
+            "roofline": roof,
+            "stages_ms": {"prepare": round(rt["prepare_ms"], 5), "bin": round(rt["bin_ms"], 5),
+                          "trace_kernel": round(rt["trace_ms"], 5), "frame": round(r["ms_per_step"], 5),
+                          "frame_instrumented": round(rt["ms_per_step"], 5), "timed_launches": rt["launches"],
+                          "note": "one frame in flight, HIP events bound to the kernels' dispatches: prepare = "
+                                  "PrepareInfoKernel, bin = TileBounds + BinTriangles + TileOrder (work list), "
+                                  "trace_kernel = TraceCullKernel (rank 0's band at N > 1); frame = uninstrumented "
+                                  "time per frame with config.frame_queues in flight"},
         }
-        line["single_queue"] = {
-            "mrays_per_s": round(r1["mrays"], 4), "ms_per_step": round(r1["ms_per_step"], 5),
-            "note": "the same frames with one frame in flight per GPU (per-frame latency); value keeps "
-                    "config.frame_queues frames in flight, each queue with its own scene buffers and HIP stream",
-        }
-        if brute is not None:
-            bs = brute["trace_ms"] * 1e-3
-            tf = rays_tests * FLOPS_PER_TEST / bs / 1e12
-            line["brute_force"] = {
-                "variant": "lds", "kernel": "TraceLdsKernel", "mrays_per_s": round(brute["mrays"], 3),
-                "kernel_ms": round(brute["trace_ms"], 4), "steps": a.brute_steps,
-                "hbm_roofline_frac": round(alg_bytes / bs / 1e9 / HBM_PEAK_GBS, 4),
-                "valu_tflops": round(tf, 2), "valu_frac": round(tf / FP32_PEAK_TFLOPS, 4),
-                "note": "north_star design taken literally: every ray tests every triangle, records tiled through LDS",
-            }
-        for v, o in alt.items():
-            line[f"variant_{v}"] = {"kernel": KERNEL_NAMES[v], "mrays_per_s": round(o["mrays"], 3),
-                                    "ms_per_step": round(o["ms_per_step"], 5),
-                                    "stages_ms": {"prepare": round(o["prepare_ms"], 5), "bin": round(o["bin_ms"], 5),
-                                                  "trace_kernel": round(o["trace_ms"], 5)},
-                                    "note": "bit-identical frame (tests/test_gpu_parity.py); uninstrumented rate"}
-        if other is not None and "error" in other[1]:
-            line[other[0]] = other[1]
-        elif other is not None:
-            om, o = other
-            line[om] = {"mrays_per_s": round(o["mrays"], 4), "ms_per_step": round(o["ms_per_step"], 4),
-                        "scaling": "weak" if om == "frames" else "strong", "queues": o["queues"],
-                        "trace_kernel_ms": round(o["trace_ms"], 5), "bin_ms": round(o["bin_ms"], 5),
-                        "prepare_ms": round(o["prepare_ms"], 5)}
-        if world == 1 and not a.no_e2e:
-            line["e2e_ml_api"] = e2e_ml_api(scene_path, W, H)
+        if valu is not None:
+            line["valu_issue"] = valu
+        line["brute_force_equivalent"] = bfe
+        if r1 is not None:
+            line["single_queue"] = {"mrays_per_s": round(r1["mrays"], 4), "ms_per_step": round(r1["ms_per_step"], 5),
+                                    "note": "the same frames with one frame in flight (per-frame latency)"}
+        if world > 1:
+            line["ranks_stages_ms"] = [{"rank": i, "prepare": round(s[0], 5), "bin": round(s[1], 5),
+                                        "trace_kernel": round(s[2], 5)} for i, s in enumerate(ranks_stages)]
+            line["verified"] = verified
+            if band_ids:
+                line["gather"] = {"payload": "int32 hit id per pixel (deferred shading on the compositor)",
+                                  "bytes_per_frame": (world - 1) * main_run.B * W * 4,
+                                  "rgba_f32_equivalent": (world - 1) * main_run.B * W * 16}
+        for k, v in legs.items():
+            if k == "brute_force":
+                bs = v["trace_ms"] * 1e-3
+                tf = launch_rays * n_tri * FLOPS_PER_TEST / bs / 1e12
+                line["brute_force"] = {
+                    "variant": "lds", "kernel": "TraceLdsKernel", "mrays_per_s": round(v["mrays"], 3),
+                    "kernel_ms": round(v["trace_ms"], 4), "steps": a.brute_steps,
+                    "valu_equivalent_tflops": round(tf, 2), "valu_equivalent_frac": round(tf / FP32_PEAK_TFLOPS, 4),
+                    "note": "north_star design taken literally: every ray tests every triangle, records tiled "
+                            "through LDS; valu_equivalent counts 12 flops per test (DESIGN.md 5: ~5.25 VALU "
+                            "instructions per test are issued)"}
+            else:
+                line[k] = v
+        if world == 1 and not a.no_e2e and extras:
+            line["e2e_ml_api"] = e2e_ml_api(path, W, H)
         if world == 1 and not a.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(scene_path, a)
+            line["cpu_baseline"] = cpu_baseline(path, a)
         print(json.dumps(line), flush=True)
-    scene.close()
     if world > 1:
-        dist.destroy_process_group()
-    tmp.cleanup()
+        ctx.dist.destroy_process_group()
+    ctx.tmp.cleanup()
 
 
 def e2e_ml_api(scene_path, W, H, reps=10, warmup=3):

@@ -75,6 +75,22 @@ ML_API_ENTRY int srtPrepareAsync(srt_device_scene scene, size_t width, size_t he
 ML_API_ENTRY int srtTraceAsync(srt_device_scene scene, const float* d_offsets, float* d_rgba,
                                size_t row_begin, size_t row_count, int variant, void* stream);
 
+/* Stage 2 for deferred shading: the same trace, storing only each pixel's hit triangle id
+ * (-1 = miss) into d_ids (row_count x width int32, band-local rows); 4 B per pixel instead of 16,
+ * the payload a multi-GPU band gather moves. */
+ML_API_ENTRY int srtTraceIdsAsync(srt_device_scene scene, const float* d_offsets, int* d_ids,
+                                  size_t row_begin, size_t row_count, int variant, void* stream);
+
+/* Stage 3 (deferred shading): rows [row_begin, row_begin + row_count) of the prepared frame
+ * shaded from hit ids (as srtTraceIdsAsync writes them) and sample offsets (both band-local,
+ * row_count x width) into d_rgba: bit-identical to srtTraceAsync's RGBA. */
+ML_API_ENTRY int srtShadeAsync(srt_device_scene scene, const float* d_offsets, const int* d_ids, float* d_rgba,
+                               size_t row_begin, size_t row_count, void* stream);
+
+/* Calls on one srt_device_scene are ordered: the per-frame edge records and the cull work
+ * buffer are shared, so a call on a different stream than the previous call first waits (HIP
+ * event) for the work enqueued before it. Use one scene per stream for concurrent frames. */
+
 /* Stage timing (measurement): while enabled, srtPrepareAsync and srtTraceAsync bind HIP events
  * to their kernels' own dispatch packets (hipExtLaunchKernelGGL start/stop events: no extra
  * packets on the stream). srtTakeStageTimes waits for them, writes the number of timed trace

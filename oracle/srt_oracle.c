@@ -235,3 +235,20 @@ size_t srto_render(const srto_scene* s, const float* offsets, size_t width, size
     free(edges);
     return (size_t)rows;
 }
+
+/* Stage 3 alone (deferred shading, the multi-GPU band path): shade rows [row_begin, row_begin +
+ * row_count) from hit ids (H x W, -1 = miss) and the offsets; same expressions as srto_render. */
+void srto_shade(const srto_scene* s, const float* offsets, const int* ids, size_t width, size_t height,
+                size_t row_begin, size_t row_count, float* rgba) {
+    float frame[12];
+    size_t y, x;
+    srto_frame(s->camera, width, height, frame);
+    for (y = row_begin; y < row_begin + row_count; ++y) {
+        for (x = 0; x < width; ++x) {
+            const float* o = offsets + 2 * (y * width + x);
+            float fx, fy;
+            srto_pixel_position(x, y, o[0], o[1], width, height, &fx, &fy);
+            shade(s, frame, (long)ids[y * width + x], fx, fy, rgba + 4 * (y * width + x));
+        }
+    }
+}

@@ -56,6 +56,9 @@ def lib():
         h.srto_render.argtypes = [ctypes.POINTER(Scene), _F, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t,
                                   ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int, _F]
         h.srto_render.restype = ctypes.c_size_t
+        h.srto_shade.argtypes = [ctypes.POINTER(Scene), _F, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t,
+                                 ctypes.c_size_t, ctypes.c_size_t, _F]
+        h.srto_shade.restype = None
         h.srto_threads.argtypes = [ctypes.c_int]
         h.srto_threads.restype = ctypes.c_int
         _lib = h
@@ -103,6 +106,18 @@ class OracleScene:
         out = np.full((height, width, 4), np.nan, np.float32)
         lib().srto_render(ctypes.byref(self._s), _fp(offsets), width, height, row_begin, row_count, row_step,
                           threads, _fp(out))
+        return out
+
+    def shade(self, width: int, height: int, ids: np.ndarray, offsets: np.ndarray | None = None) -> np.ndarray:
+        """Deferred shading of a whole frame from hit ids (H x W int32, -1 = miss)."""
+        if offsets is None:
+            offsets = np.full((height, width, 2), 0.5, np.float32)
+        offsets = np.ascontiguousarray(offsets, np.float32)
+        ids = np.ascontiguousarray(ids, np.int32)
+        assert offsets.shape == (height, width, 2) and ids.shape == (height, width)
+        out = np.full((height, width, 4), np.nan, np.float32)
+        lib().srto_shade(ctypes.byref(self._s), _fp(offsets), ids.ctypes.data_as(ctypes.c_void_p), width, height, 0,
+                         height, _fp(out))
         return out
 
     def close(self):

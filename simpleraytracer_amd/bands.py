@@ -1,11 +1,21 @@
-"""Row-band partition of a frame over ranks, and the band gather to one rank.
+"""Row-band partition of a frame over ranks, and the band gathers to one rank.
 
 Multi-GPU layout (DESIGN.md "Multi-GPU"): rank r of P renders frame rows
 [r*B, min(H, (r+1)*B)) with B = ceil(H / P); every rank holds a band buffer of exactly B rows
-(the last one padded) so the gather has equal counts; the destination concatenates the bands
-and keeps the first H rows. Inside one process, Renderer (csrc/renderer.cpp) does the same
-with ncclGather; across processes (one rank per GPU, torch.distributed over RCCL/xGMI, or
-gloo on CPU for tests) this module does it with ``dist.gather``.
+(the last one padded) so the gather has equal counts; the destination receives the bands in
+place into one (P*B)-row buffer and keeps the first H rows. Inside one process, Renderer
+(csrc/renderer.cpp) does the same with ncclGather; across processes (one rank per GPU,
+torch.distributed over RCCL/xGMI, or gloo on CPU for tests) this module does it with
+``dist.gather``.
+
+Two payloads:
+  * ``gather_bands``: the band's RGBA framebuffer rows (16 B per pixel);
+  * ``gather_band_ids``: the band's hit ids only (int32, 4 B per pixel), for deferred shading:
+    the compositing rank shades the whole frame from the ids (srtShadeAsync), bit-identical to
+    shading in the trace, with a quarter of the gather bytes.
+
+Frame k of a stream is composited on ``compositor(k, P)`` (rotating: every rank receives and
+shades 1/P of the frames, so every xGMI link carries traffic in both directions) or on rank 0.
 """
 from __future__ import annotations
 
@@ -22,12 +32,12 @@ def band_range(height: int, world: int, rank: int) -> tuple[int, int]:
     return begin, end - begin
 
 
-def gather_bands(band, height: int, dst: int = 0, group=None, out=None):
-    """Gather every rank's (B, W, C) band to ``dst``; returns the (H, W, C) frame on dst, else None.
+def compositor(frame: int, world: int, rotate: bool = True) -> int:
+    """Rank that gathers and shades frame ``frame``: frame % world when rotating, else 0."""
+    return frame % world if rotate else 0
 
-    ``out`` (dst only, optional): a (P * B, W, C) buffer the bands are received into in place
-    (its row slices are the gather list, so no concatenation copy); allocated when omitted.
-    """
+
+def _gather_into(band, height: int, dst: int, group, out, async_op: bool):
     import torch
     import torch.distributed as dist
 
@@ -36,13 +46,41 @@ def gather_bands(band, height: int, dst: int = 0, group=None, out=None):
     b = band_rows(height, world)
     if band.shape[0] != b:
         raise ValueError(f"band buffer must have {b} rows, got {band.shape[0]}")
+    # dst is a group rank; torch.distributed wants the global rank
+    dst_global = dst if group is None else dist.get_global_rank(group, dst)
     if rank == dst:
+        shape = (world * b,) + tuple(band.shape[1:])
         if out is None:
-            out = torch.empty((world * b,) + tuple(band.shape[1:]), dtype=band.dtype, device=band.device)
-        elif tuple(out.shape) != (world * b,) + tuple(band.shape[1:]) or not out.is_contiguous():
-            raise ValueError(f"out must be a contiguous {(world * b,) + tuple(band.shape[1:])} buffer")
+            out = torch.empty(shape, dtype=band.dtype, device=band.device)
+        elif tuple(out.shape) != shape or not out.is_contiguous() or out.dtype != band.dtype:
+            raise ValueError(f"out must be a contiguous {shape} {band.dtype} buffer")
         parts = [out[r * b:(r + 1) * b] for r in range(world)]
-        dist.gather(band, gather_list=parts, dst=dst, group=group)
-        return out[:height]
-    dist.gather(band, gather_list=None, dst=dst, group=group)
-    return None
+        work = dist.gather(band, gather_list=parts, dst=dst_global, group=group, async_op=async_op)
+        return out[:height], work
+    work = dist.gather(band, gather_list=None, dst=dst_global, group=group, async_op=async_op)
+    return None, work
+
+
+def gather_bands(band, height: int, dst: int = 0, group=None, out=None):
+    """Gather every rank's (B, W, C) band to ``dst``; returns the (H, W, C) frame on dst, else None.
+
+    ``out`` (dst only, optional): a (P * B, W, C) buffer the bands are received into in place
+    (its row slices are the gather list, so no concatenation copy); allocated when omitted.
+    """
+    frame, _ = _gather_into(band, height, dst, group, out, async_op=False)
+    return frame
+
+
+def gather_band_ids(band_ids, height: int, dst: int = 0, group=None, out=None, async_op: bool = False):
+    """Gather every rank's (B, W) int32 hit-id band to ``dst`` (deferred shading payload).
+
+    Returns (frame_ids or None, work): the (H, W) id frame on dst (a view of ``out``, received
+    in place), and the async work handle (None when synchronous). With ``async_op`` the caller
+    must ``work.wait()`` (on the stream that consumes the ids) before using them, and before
+    overwriting ``band_ids``.
+    """
+    import torch
+
+    if band_ids.dtype != torch.int32 or band_ids.dim() != 2:
+        raise ValueError("band_ids must be a (B, W) int32 tensor")
+    return _gather_into(band_ids, height, dst, group, out, async_op)

@@ -70,6 +70,7 @@ struct BandArgs {
     std::size_t height;     // full frame height (fy denominator)
     std::size_t row_begin;  // first frame row of the band
     std::size_t row_count;
+    int* ids = nullptr;     // device, row_count x width: non-null = store hit ids (-1 miss), not RGBA
 };
 
 // Launch the prepare kernel: writes PaddedTriangleCount(n) / kTileTriangles tiles into `edges`,
@@ -95,8 +96,11 @@ struct CullBins {
     unsigned* counts;      // tiles + 1: list lengths, then the large-list length
     unsigned* lists;       // tiles x capacity candidate ids (BinTrianglesKernel)
     unsigned* large_list;  // PaddedTriangleCount(n) ids binned to every tile
-    unsigned* tile_order;  // tiles x parts: trace launch order of (tile, part), most work first
-    unsigned* sync;        // self-resetting counter of finished bin blocks (SRT_ORDER_IN_BIN=1)
+    void* work;            // trace work list (TileOrderKernel): up to 2 x tiles x parts items, 8 B each
+    unsigned* work_count;  // its length
+    unsigned* slice_base;  // tiles: first key slice of a split tile
+    unsigned* arrive;      // tiles x parts: split items finished (self-resetting counters)
+    void* split_keys;      // key slices of split items: 8 KiB each, as many as work items
     void* bounds;          // (tiles_x + tiles_y) float2: monotone tile column / row bounds
     unsigned capacity;
     std::size_t tiles;
@@ -152,6 +156,11 @@ struct BvhLayout {
 };
 BvhLayout MakeBvhLayout(std::uint64_t n);
 std::size_t BvhBytes(std::uint64_t n);  // node boxes (16 B) + depth bounds (4 B), 256-B aligned
+
+// Deferred shading of a band from hit ids (band.ids) and sample offsets into band.rgba, with the
+// edge buffer's shading normals of the prepared frame: bit-identical to the fused trace.
+hipError_t LaunchShade(const float* d_vertices, const float* d_albedo, const float* d_edges, std::uint64_t n,
+                       const Frame& frame, const float background[3], const BandArgs& band, hipStream_t stream);
 
 // Element-wise IEEE binary16 <-> binary32 conversion on the device (ML_FLOAT16 images):
 // float -> half rounds to nearest even (overflow -> inf, NaN stays NaN); half -> float is exact.

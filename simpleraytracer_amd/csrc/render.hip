@@ -19,9 +19,12 @@ namespace srt {
 #ifdef SRT_DIAG
 // Diagnostic build only (make diag): per-block phase cycle counts of the cull kernel.
 // [block][0] stream cycles, [1] gather cycles, [2] filter+walk cycles, [3] block survivors,
-// [4] wave-0 survivors walked, [5] flush batches, [6] total cycles, [7] unused.
+// [4] packets (packet walk) / wave-0 survivors walked (stream walk), [5] batches, [6] walk
+// cycles in total, [7] mode bits; trace kernel: [8] start / [9] end (s_memrealtime, 100 MHz),
+// [10] work item, [11] chunk | chunks << 16 | last arriver << 32.
 constexpr int kDiagBlocks = 65536;
-__device__ unsigned long long g_srt_diag[kDiagBlocks][8];
+constexpr int kDiagCols = 16;
+__device__ unsigned long long g_srt_diag[kDiagBlocks][kDiagCols];
 #define SRT_STAMP(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
 #else
 #define SRT_STAMP(v)
@@ -57,6 +60,7 @@ struct TraceParams {
     const float4* __restrict__ normals;  // shading normals (PrepareRecord), by triangle id
     const float2* __restrict__ offsets;
     float4* __restrict__ out;
+    int* __restrict__ out_ids;  // non-null: store the hit id per pixel (-1 = miss) instead of RGBA
     unsigned n_pad;   // records in the edge buffer (multiple of kPadTriangles)
     unsigned n;       // records in the scene
     int tiles_x;         // cull tiles per tile row of the band
@@ -65,13 +69,16 @@ struct TraceParams {
     int width;
     int row_count;
     int row_begin;
-    int allow_raster;  // cull variant: raster walk for uniform-offset tiles (env SRT_CULL_RASTER=0 disables)
     // Cull variant with bins (render.h CullBins); tile_info == null: no bins, every tile
     // computes its own ray box and streams every record.
     const TileInfo* __restrict__ tile_info;   // per tile: ray box, uniform offset (TileInfoKernel)
     const CullRecord* __restrict__ cull;      // cull records in spatial order (the lists hold positions)
     const unsigned* __restrict__ order;       // spatial-order position -> record id
-    const unsigned* __restrict__ tile_order;  // block -> tile, most work first (TileOrderKernel)
+    const uint4* __restrict__ work;           // block -> work item (2 x uint4), most work first (TileOrderKernel)
+    const unsigned* __restrict__ work_count;  // [0]: work items (blocks past it exit)
+    const unsigned* __restrict__ slice_base;  // split tiles: first key slice
+    unsigned long long* __restrict__ split_keys;  // key slices of split work items (kBlockRows x 64 each)
+    unsigned* __restrict__ arrive;            // per (tile, part): split items finished (self-resetting)
     const unsigned* __restrict__ bin_lists;   // per tile: candidate ids (BinTrianglesKernel)
     const unsigned* __restrict__ bin_counts;  // per tile: list length; [tiles]: large-list length
     const unsigned* __restrict__ large_list;  // ids of records binned to every tile
@@ -411,8 +418,35 @@ __device__ __forceinline__ bool GenerateRays(const TraceParams& p, int x, int y0
     return same;
 }
 
-// Shade + store: rgb = albedo * |cos(N, d)| for a hit, background for a miss; alpha carries
+// Shade: rgb = albedo * |cos(N, d)| for a hit, background for a miss; alpha carries
 // float(tri_id) (exact for ids < 2^24), -1 for a miss.
+__device__ __forceinline__ float4 ShadePixel(const TraceParams& p, float fx, float fy, int id) {
+    if (id < 0) {
+        return make_float4(p.bg[0], p.bg[1], p.bg[2], -1.f);
+    }
+    const float dx = fmaf(fy, p.dv[0], fmaf(fx, p.du[0], p.base[0]));
+    const float dy = fmaf(fy, p.dv[1], fmaf(fx, p.du[1], p.base[1]));
+    const float dz = fmaf(fy, p.dv[2], fmaf(fx, p.du[2], p.base[2]));
+    const float4 nr = p.normals[id];  // (e1 x e2, |e1 x e2|) from the prepare kernel
+    const float nd = Dot3(nr.x, nr.y, nr.z, dx, dy, dz);
+    const float dd = Dot3(dx, dy, dz, dx, dy, dz);
+    const float cosv = fminf(fabsf(nd) / (nr.w * sqrtf(dd)), 1.f);
+    const float* a = p.albedo + 3ull * id;
+    return make_float4(a[0] * cosv, a[1] * cosv, a[2] * cosv, static_cast<float>(id));
+}
+
+// Store one pixel of the band: its shaded RGBA (one float4, 1 KiB contiguous per wave
+// instruction), or only its hit id (out_ids: deferred shading by ShadeIdsKernel, bit-identical).
+__device__ __forceinline__ void StorePixel(const TraceParams& p, int x, int y, float fx, float fy, int id) {
+    const size_t at = static_cast<size_t>(y) * p.width + x;
+    if (p.out_ids != nullptr) {
+        p.out_ids[at] = id;
+    } else {
+        p.out[at] = ShadePixel(p, fx, fy, id);
+    }
+}
+
+// Shade + store the lane's R rays.
 template <int R>
 __device__ __forceinline__ void ShadeAndStore(const TraceParams& p, int x, int y0, const Rays<R>& s) {
     if (x >= p.width) {
@@ -421,27 +455,27 @@ __device__ __forceinline__ void ShadeAndStore(const TraceParams& p, int x, int y
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const int y = y0 + r;
-        if (y >= p.row_count) {
-            continue;
+        if (y < p.row_count) {
+            StorePixel(p, x, y, s.fx[r], s.fy[r], s.bi[r]);
         }
-        float4 o;
-        const int id = s.bi[r];
-        if (id >= 0) {
-            const float fx = s.fx[r], fy = s.fy[r];
-            const float dx = fmaf(fy, p.dv[0], fmaf(fx, p.du[0], p.base[0]));
-            const float dy = fmaf(fy, p.dv[1], fmaf(fx, p.du[1], p.base[1]));
-            const float dz = fmaf(fy, p.dv[2], fmaf(fx, p.du[2], p.base[2]));
-            const float4 nr = p.normals[id];  // (e1 x e2, |e1 x e2|) from the prepare kernel
-            const float nd = Dot3(nr.x, nr.y, nr.z, dx, dy, dz);
-            const float dd = Dot3(dx, dy, dz, dx, dy, dz);
-            const float cosv = fminf(fabsf(nd) / (nr.w * sqrtf(dd)), 1.f);
-            const float* a = p.albedo + 3ull * id;
-            o = make_float4(a[0] * cosv, a[1] * cosv, a[2] * cosv, static_cast<float>(id));
-        } else {
-            o = make_float4(p.bg[0], p.bg[1], p.bg[2], -1.f);
-        }
-        p.out[static_cast<size_t>(y) * p.width + x] = o;
     }
+}
+
+// Deferred shading: one thread per pixel of a band, from its hit id and sample offset, with
+// GenerateRays' position expressions and ShadePixel: the frame equals the fused trace + shade
+// bit for bit.
+__global__ __launch_bounds__(256) void ShadeIdsKernel(TraceParams p, const int* __restrict__ ids) {
+    const size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= static_cast<size_t>(p.width) * p.row_count) {
+        return;
+    }
+    const int x = static_cast<int>(i % static_cast<unsigned>(p.width));
+    const int y = static_cast<int>(i / static_cast<unsigned>(p.width));
+    const float2 o = p.offsets[i];
+    const float fx = (static_cast<float>(x) + o.x) / p.wf;
+    const float fy = (static_cast<float>(p.row_begin + y) + o.y) / p.hf;
+    const int id = ids[i];
+    p.out[i] = ShadePixel(p, fx, fy, static_cast<unsigned>(id) < p.n ? id : -1);  // no id outside the scene
 }
 
 // ---------------------------------------------------------------------------------------
@@ -690,118 +724,53 @@ __device__ __forceinline__ void ExactTestAnyOrder(Rays<R>& s, const Record& q, f
     }
 }
 
-// Loads record `id`'s edge planes from the tile-planar buffer.
-__device__ __forceinline__ void LoadRecord(const float4* __restrict__ edges, unsigned id, float4& p0, float4& p1,
-                                           float& cyC, float& vol) {
-    const float4* tile = edges + static_cast<size_t>(id / kTileTriangles) * kTileFloat4;
-    const unsigned j = id % kTileTriangles;
-    p0 = tile[j];
-    p1 = tile[kTileTriangles + j];
-    cyC = Plane2(tile)[j];
-    vol = Plane3(tile)[j];
-}
-
-// Cull tile = one trace block: 64 columns x 32 rows of rays, W waves (4, 8 or 16) of 64 x R
-// rays, R = 32 / W rays per lane. Constants that depend on W live in CullShape<W>.
-constexpr int kTileRows = kCullTileRows;  // cull tile (bins): 64 columns x 32 rows
+// Cull tile = 64 columns x kTileRows rows of rays (the bins); trace block = one part of it,
+// 64 columns x kBlockRows rows: kCullWaves waves, each 64 columns x kCullR rows (lane =
+// column).
+constexpr int kTileRows = kCullTileRows;
 #ifndef SRT_BLOCK_ROWS
 #define SRT_BLOCK_ROWS 16
 #endif
-constexpr int kBlockRows = SRT_BLOCK_ROWS;  // trace block: one part of a cull tile
+constexpr int kBlockRows = SRT_BLOCK_ROWS;
 constexpr int kParts = kTileRows / kBlockRows;
-// Batch sizes of the cull walks (measured: these keep the trace block at 22 KB of LDS, up to
-// 7 blocks per CU; the earlier 2048 / 512 / 256 took 35 KB, 4 blocks per CU, and 1.7 % longer).
-#ifndef SRT_STREAM_STEP
-#define SRT_STREAM_STEP 1024
-#endif
+constexpr int kCullWaves = 4;
+constexpr int kCullThreads = kWave * kCullWaves;
+constexpr int kCullR = kBlockRows / kCullWaves;  // rays per lane
 #ifndef SRT_PACKET_BATCH
 #define SRT_PACKET_BATCH 256
-#endif
-#ifndef SRT_PACKET_FLAT
-// packet walk: 1 = a survivor's pixel range is cut row-major into packets of 64 pixels
-// (ceil(cols*rows/64) packets); 0 = power-of-two-wide packets (2^lg columns x 64>>lg rows)
-#define SRT_PACKET_FLAT 1
-#endif
-#ifndef SRT_PACKET_SPLIT
-// packet walk (row-major packets): a survivor's range may be cut into two row bands, each with
-// its own exact column range, when that takes fewer packets. Exact (GPU parity green) but
-// measured slower: the six column searches in the gather phase cost more than the packets
-// they save (trace 36.4 -> 43 us), so off by default.
-#define SRT_PACKET_SPLIT 0
-#endif
-#ifndef SRT_PACKET_WORD
-// packet walk (row-major packets, blocks of <= 16 rows): one packed word per packet
-#define SRT_PACKET_WORD (SRT_PACKET_FLAT && SRT_BLOCK_ROWS <= 16)
-#endif
-#ifndef SRT_FAST_DIV
-// packet walk (packed word path): t = vol / det by the IEEE sequence without its range
-// scaling / fixup steps when vol and every candidate lane's det are in range (see
-// EvalPacketFast). Exact (GPU parity green with it on) but measured slower: the per-packet
-// ballot + uniform branch and the per-lane vol flag cost more than the 3 VALU they save
-// (trace 36.5 -> 42.3 us), so off by default.
-#define SRT_FAST_DIV 0
-#endif
-#ifndef SRT_PIN_LOADS
-#define SRT_PIN_LOADS 1  // packet walk: pin loop-invariant lane values and keys (ISA scheduling)
 #endif
 #ifndef SRT_PACKET_ILP
 #define SRT_PACKET_ILP 2  // packet walk: packets evaluated together per wave (independent chains)
 #endif
-#ifndef SRT_FLUSH_BATCH
-#define SRT_FLUSH_BATCH 128
-#endif
-constexpr int kStreamStep = SRT_STREAM_STEP;  // FULL stream: records per block per step
-constexpr int kListG = 4;          // LIST stream: ids per lane per step
-constexpr int kPacketBatch = SRT_PACKET_BATCH;  // packet walk: survivors gathered per batch
+constexpr int kPacketBatch = SRT_PACKET_BATCH;  // candidates gathered per packet-walk batch
+constexpr int kSlices = kPacketBatch / kCullThreads;  // batch entries per thread
+constexpr int kStreamStep = kCullThreads;        // FULL stream: records per block per step
+static_assert(kPacketBatch % kCullThreads == 0 && kPacketBatch <= 256, "packet word: survivor slot < 256");
+static_assert(kBlockRows <= 16 && kBlockRows % kCullWaves == 0, "packet word: rows < 16");
 static_assert(kPadTriangles % kStreamStep == 0, "a stream step must cover whole pad units");
 
-// Block widths a build supports: at least one ray per lane and two streamed records per lane.
-constexpr bool CullWavesOk(int w) { return kBlockRows / w >= 1 && kStreamStep / (kWave * w) >= 2; }
-
-template <int W>
-struct CullShape {
-    static constexpr int kR = kBlockRows / W;             // rays per lane
-    static constexpr int kThreads = kWave * W;
-    static constexpr int kStreamG = kStreamStep / kThreads;  // FULL: records per lane per step
-    static constexpr int kBatch = SRT_FLUSH_BATCH;        // survivors gathered per flush batch
-    static constexpr int kShare = kBatch / W;             // raster walk: batch entries per wave
-    static constexpr int kListStep = kThreads * kListG;     // LIST stream: ids per block per step
-    static constexpr int kPBatch = kThreads > kPacketBatch ? kThreads : kPacketBatch;  // packet walk batch
-    static constexpr int kListCap = kBatch + (kListStep > kStreamStep ? kListStep : kStreamStep);  // < kBatch + one step
-};
-
-template <int W>
 struct CullShared {
+    float4 sv0[kPacketBatch];  // compacted survivors: plane 0
+    float4 sv1[kPacketBatch];  //                      plane 1
     union {
-        struct {  // stream walk (CullWalk)
-            unsigned ids[CullShape<W>::kListCap];
-            float4 st0[CullShape<W>::kBatch];  // gathered records: plane 0
-            float4 st1[CullShape<W>::kBatch];  //                   plane 1
-            float4 st2[CullShape<W>::kBatch];  //                   (cyC, vol, id, 0)
-            float4 st3[CullShape<W>::kBatch];  //                   screen box
-            unsigned hit[CullShape<W>::kBatch];  // raster walk: record may touch the tile (box + edge tests)
-            int counts[2][W];
-        } s;
-        struct {  // packet walk (PacketWalk): one batch of compacted survivors
-            float4 sv0[CullShape<W>::kPBatch];  // plane 0
-            float4 sv1[CullShape<W>::kPBatch];  // plane 1
-            float4 sv2[CullShape<W>::kPBatch];  // (cyC, vol, id, pixel range bits)
-#if SRT_PACKET_SPLIT
-            unsigned band2[CullShape<W>::kPBatch];  // second row band's range bits (split survivors)
-#endif
-            unsigned pre[CullShape<W>::kPBatch + 1];  // exclusive packet prefix, pre[S] = packets
-            unsigned wave_n[CullShape<W>::kPBatch / kWave];   // survivors per (slice, wave)
-            unsigned wave_pk[CullShape<W>::kPBatch / kWave];  // packets per (slice, wave)
-            float fxs[kWave];                // fx of the tile's columns
-            float fys[kBlockRows];           // fy of the block's rows
-        } k;
-    } u;
-    Box wave_box[W];
-    unsigned shared_fx;
-    unsigned regular;
-    // Raster walks: per-pixel lexicographic (t, id) keys of the tile's 32 x 64 rays.
-    unsigned long long keys[kBlockRows][kWave];
+        float4 sv2[kPacketBatch];  //                  (cyC, vol, id, packed pixel range)
+        unsigned ids[kPacketBatch + kStreamStep];  // FULL stream: surviving record ids (read
+                                                   // into registers before a batch writes sv2)
+    };
+    unsigned pre[kPacketBatch + 1];  // exclusive packet prefix, pre[S] = packets
+    unsigned wave_n[kSlices * kCullWaves];   // survivors per (slice, wave)
+    unsigned wave_pk[kSlices * kCullWaves];  // packets per (slice, wave)
+    float2 fxy[kBlockRows][kWave];  // ray position (fx, fy) of every pixel of the block
+    float clo[kWave], chi[kWave];    // monotone column bounds of fx (suffix min, prefix max)
+    float rlo[kBlockRows], rhi[kBlockRows];  // monotone row bounds of fy
+    unsigned counts[2][kCullWaves];            // FULL stream: survivors per wave and step
+    Box wave_box[kCullWaves];
+    unsigned last;  // split work item: this block arrived last
+    unsigned long long keys[kBlockRows][kWave];  // per-pixel lexicographic (t, id) keys
 };
+static_assert(sizeof(float2) * kWave * kCullWaves <= sizeof(float4) * kPacketBatch, "PacketTables scratch");
+static_assert((kPacketBatch + kStreamStep) * 4 <= sizeof(float4) * kPacketBatch, "stream ids alias sv2");
+constexpr int kFlushBatches = (kPacketBatch + kStreamStep - 1 + kPacketBatch - 1) / kPacketBatch;  // per flush
 
 // (t, id) packed so that unsigned order is lexicographic order: t >= 0 here (vol > 0,
 // det > 0), so its bit pattern orders like the value.
@@ -809,520 +778,95 @@ __device__ __forceinline__ unsigned long long HitKey(float t, int id) {
     return (static_cast<unsigned long long>(__float_as_uint(t)) << 32) | static_cast<unsigned>(id);
 }
 
-// Raster walk of one survivor over the whole tile (tiles whose rays all use the same sample
-// offset: fx depends only on the column = lane, fy only on the row). The screen box picks
-// the contiguous column range (lanes) and row range (of 32) it can touch; those pixels are
-// tested exactly, lane-parallel, 64 pixels per round (rows packed when the column range is
-// narrow), and each hit is merged into the pixel's key with an LDS atomic min. Same exact
-// test and the same lexicographic result as ExactTestAnyOrder; any wave may walk any
-// survivor, so a tile's survivors are shared evenly by its waves.
-__device__ __forceinline__ void RasterSurvivor(unsigned long long (*keys)[kWave], const Record& q, float vol, int id,
-                                               const float4& sb, bool use_sb, float fx_lane, float fy_lane,
-                                               int lane) {
-    unsigned long long cm = ~0ull;
-    unsigned rm = 0xFFFFFFFFu;
-    if (use_sb) {
-        cm = __ballot(fx_lane >= sb.x && fx_lane <= sb.y);
-        rm = static_cast<unsigned>(__ballot(fy_lane >= sb.z && fy_lane <= sb.w));  // lanes >= 32: NaN
-        if (cm == 0ull || rm == 0u) {
-            return;
-        }
-    }
-    const int c0 = __builtin_ctzll(cm), c1 = 63 - __builtin_clzll(cm);
-    const int r0 = __builtin_ctz(rm), r1 = 31 - __builtin_clz(rm);
-    const int ncols = c1 - c0 + 1;
-    const int lg = ncols <= 1 ? 0 : 32 - __builtin_clz(static_cast<unsigned>(ncols - 1));  // ceil(log2)
-    const int col = c0 + (lane & ((1 << lg) - 1));
-    const int step = kWave >> lg;
-#pragma unroll 1
-    for (int rr = r0; rr <= r1; rr += step) {
-        const int row = rr + (lane >> lg);
-        const float fx = __shfl(fx_lane, col);
-        const float fy = __shfl(fy_lane, row & (kBlockRows - 1));
-        if (col <= c1 && row <= r1) {
-            const float eA = fmaf(fy, q.cyA, fmaf(fx, q.cxA, q.c0A));
-            const float eB = fmaf(fy, q.cyB, fmaf(fx, q.cxB, q.c0B));
-            const float eC = fmaf(fy, q.cyC, fmaf(fx, q.cxC, q.c0C));
-            const float det = (eA + eB) + eC;
-            // all E >= 0 and det > 0 (NaN anywhere fails: det is then NaN)
-            if (fminf(fminf(eA, eB), eC) >= 0.f && det > 0.f) {
-                const float t = vol / det;
-                if (t < __builtin_inff()) {
-                    __hip_atomic_fetch_min(&keys[row][col], HitKey(t, id), __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_WORKGROUP);
-                }
-            }
-        }
-    }
-}
-
-// Per-tile source of candidate records for the cull stream: every record of the scene
-// (FULL), or (LIST) the tile's bin list followed by the large list (records binned to every
-// tile), as one virtual list of which this block takes positions [begin, end).
+// Candidate source of a block: LIST = positions [begin, end) of the tile's virtual list (its
+// bin list, then the large list of records binned to every tile); FULL = every record.
 struct CullSource {
-    const unsigned* list;   // LIST: the tile's ids (virtual positions < count1)
-    const unsigned* list2;  // LIST: large-list ids (virtual position v >= count1: list2[v - count1])
-    unsigned count1;        // LIST: ids in the tile's list
-    unsigned begin;         // LIST: this block's virtual positions [begin, end)
+    const unsigned* list;   // LIST: the tile's list (virtual positions < count1)
+    const unsigned* list2;  // LIST: large list (virtual position v >= count1: list2[v - count1])
+    unsigned count1;
+    unsigned begin;
     unsigned end;
-    unsigned step0;         // FULL: first record step of this block's chunk
-    unsigned steps;         // FULL: record steps of this block's chunk
+    bool full;
 };
 
-// Streams the tile's candidates, keeps those whose quantized screen box overlaps the tile's
-// (bq) in a block-wide LDS id list, and walks the survivors in flushes: gather their records
-// into LDS, then either the raster walk (RASTER: survivors shared by the waves) or, per wave,
-// the wave-box filter and ExactTestAnyOrder over every survivor (the wave's rays only).
-template <int W, bool SHARED, bool RASTER, bool LIST>
-__device__ __forceinline__ void CullWalk(const TraceParams& p, CullShared<W>& sh, Rays<CullShape<W>::kR>& s,
-                                         const Box& bb, const Box& wb, float fx_lane, float fy_lane,
-                                         CullSource src, unsigned tile) {
-    using S = CullShape<W>;
-    constexpr int R = S::kR;
-    constexpr int kThreads = S::kThreads;
-    constexpr int kBatch = S::kBatch;
-    constexpr int G = LIST ? kListG : S::kStreamG;
-    constexpr int kStep = kThreads * G;
-    static_assert(G <= 32, "pass bits of a step live in one 32-bit mask");
-    const int tid = threadIdx.x;
-    const int lane = tid & (kWave - 1);
-    const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);
-    const float4* __restrict__ sbox = p.screen_boxes;
-    const uint2* __restrict__ qbox = p.qboxes;
-    const bool block_sb = ScreenBoxUsable(bb);
-    const bool wave_sb = ScreenBoxUsable(wb);
-    const QBox bq = Quantize(bb);
-    const unsigned long long lt_mask = (1ull << lane) - 1ull;
-    const unsigned nsteps = LIST ? (src.end - src.begin + kStep - 1) / kStep : src.steps;
-
-    if constexpr (RASTER) {
-        for (int i = tid; i < kBlockRows * kWave; i += kThreads) {
-            (&sh.keys[0][0])[i] = ~0ull;
-        }  // visible to every wave after the first stream barrier
-    }
-#ifdef SRT_DIAG
-    unsigned long long d_stream = 0, d_gather = 0, d_walk = 0, d_surv = 0, d_wsurv = 0, d_batches = 0;
-    const unsigned long long d_t0 = __builtin_amdgcn_s_memtime();
-    unsigned long long d_mark = d_t0;
-#endif
-    // FULL: lane tid of step k reads records k * kStep + 2 * (l * kThreads + tid) + {0, 1}
-    //       (one 16-B load per record pair); LIST: virtual positions begin + k * kStep +
-    //       g * kThreads + tid (coalesced 4-B id loads) and their 8-B boxes. The whole step is
-    //       loaded one step ahead.
-    constexpr int L = LIST ? 1 : G / 2;
-    const uint4* __restrict__ qbox4 = reinterpret_cast<const uint4*>(qbox);
-    uint4 nb[L];
-    unsigned nid[LIST ? kListG : 1];
-    uint2 nq[LIST ? kListG : 1];
-    auto fetch = [&](unsigned k) {
-        if constexpr (LIST) {
-#pragma unroll
-            for (int g = 0; g < kListG; ++g) {
-                const unsigned v = src.begin + k * kStep + g * kThreads + tid;
-                const bool in = v < src.end;
-                nid[g] = in ? p.order[v < src.count1 ? src.list[v] : src.list2[v - src.count1]] : 0u;
-            }
-#pragma unroll
-            for (int g = 0; g < kListG; ++g) {
-                const unsigned v = src.begin + k * kStep + g * kThreads + tid;
-                nq[g] = v < src.end ? qbox[nid[g]] : make_uint2(0x80018001u, 0x80018001u);  // empty box
-            }
-        } else {
-#pragma unroll
-            for (int l = 0; l < L; ++l) {
-                nb[l] = qbox4[(src.step0 + k) * (kStep / 2) + l * kThreads + tid];
-            }
-        }
-    };
-    if (nsteps > 0) {
-        fetch(0);
-    }
-    int total = 0;  // ids in the block list (block-uniform)
-    for (unsigned k = 0; k < nsteps; ++k) {
-        uint4 cb[L];
-        uint2 cq[LIST ? kListG : 1];
-        unsigned cid[LIST ? kListG : 1];
-#pragma unroll
-        for (int l = 0; l < L; ++l) {
-            cb[l] = nb[l];
-        }
-#pragma unroll
-        for (int g = 0; g < (LIST ? kListG : 1); ++g) {
-            cq[g] = nq[g];
-            cid[g] = nid[g];
-        }
-        if (k + 1 < nsteps) {
-            fetch(k + 1);
-        }
-        auto record_id = [&](int g) -> unsigned {
-            if constexpr (LIST) {
-                return cid[g];
-            } else {
-                return (src.step0 + k) * kStep + 2 * ((g >> 1) * kThreads + tid) + (g & 1);
-            }
-        };
-        unsigned bits = 0u;
-        int wave_n = 0;
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-            unsigned qx, qy;
-            if constexpr (LIST) {
-                qx = cq[g].x;
-                qy = cq[g].y;
-            } else {
-                qx = (g & 1) ? cb[g >> 1].z : cb[g >> 1].x;
-                qy = (g & 1) ? cb[g >> 1].w : cb[g >> 1].y;
-            }
-            // Disabled records carry empty boxes; unbounded ones span the int16 range. LIST
-            // padding lanes carry an empty box too (and LIST implies a usable tile box).
-            const bool pass = !block_sb || QBoxOverlaps(bq, qx, qy);
-            bits |= pass ? (1u << g) : 0u;
-            wave_n += __popcll(__ballot(pass));
-        }
-        const unsigned ph = k & 1u;
-        if (lane == 0) {
-            sh.u.s.counts[ph][wave] = wave_n;
-        }
-        __syncthreads();
-        int off = total;
-        int step_n = 0;
-#pragma unroll
-        for (int w = 0; w < W; ++w) {
-            const int cw = sh.u.s.counts[ph][w];
-            off += w < wave ? cw : 0;
-            step_n += cw;
-        }
-        if (bits != 0u || step_n != 0) {
-#pragma unroll
-            for (int g = 0; g < G; ++g) {
-                const bool pass = (bits >> g) & 1u;
-                const unsigned long long m = __ballot(pass);
-                if (pass) {
-                    sh.u.s.ids[off + __popcll(m & lt_mask)] = record_id(g);
-                }
-                off += __popcll(m);
-            }
-        }
-        total += step_n;
-        if (total < kBatch && k + 1 < nsteps) {  // block-uniform
-            continue;
-        }
-        __syncthreads();  // every wave's ids are in the list
-#ifdef SRT_DIAG
-        {
-            const unsigned long long now = __builtin_amdgcn_s_memtime();
-            d_stream += now - d_mark;
-            d_mark = now;
-            d_surv += total;
-        }
-#endif
-        // Flush: gather every listed record in batches of kBatch, then walk.
-#pragma unroll 1
-        for (int b0 = 0; b0 < total; b0 += kBatch) {
-            const int e = b0 + tid;
-            if (tid >= kBatch) {
-                // not a gathering thread
-            } else if (e < total) {
-                const unsigned id = sh.u.s.ids[e];
-                float4 p0, p1;
-                float cyC, vol;
-                LoadRecord(p.edges, id, p0, p1, cyC, vol);
-                const float4 sb = sbox[id];
-                sh.u.s.st0[tid] = p0;
-                sh.u.s.st1[tid] = p1;
-                sh.u.s.st2[tid] = make_float4(cyC, vol, __uint_as_float(id), 0.f);
-                sh.u.s.st3[tid] = sb;
-                if constexpr (RASTER) {
-                    const Record r{p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w, cyC};
-                    sh.u.s.hit[tid] = ((!block_sb || ScreenBoxOverlaps(bb, sb)) && BoxMayHit(bb, r)) ? 1u : 0u;
-                }
-            } else if constexpr (RASTER) {
-                sh.u.s.hit[tid] = 0u;
-            }
-            __syncthreads();
-#ifdef SRT_DIAG
-            {
-                const unsigned long long now = __builtin_amdgcn_s_memtime();
-                d_gather += now - d_mark;
-                d_mark = now;
-                ++d_batches;
-            }
-#endif
-            const int nb_here = min(kBatch, total - b0);
-            if constexpr (RASTER) {
-                // This wave's share of the batch: entries wave * 64 .. wave * 64 + 63.
-                const int c0 = wave * S::kShare;
-                unsigned long long m = __ballot(lane < S::kShare && sh.u.s.hit[c0 + lane] != 0u);
-#ifdef SRT_DIAG
-                d_wsurv += __popcll(m);
-#endif
-                if (m != 0ull) {
-                    // Software-pipelined: the next survivor's LDS reads are issued before the
-                    // current one is walked, so their latency hides behind its work.
-                    int bit = __builtin_ctzll(m);
-                    float4 a = sh.u.s.st0[c0 + bit], b = sh.u.s.st1[c0 + bit], x = sh.u.s.st2[c0 + bit], sb = sh.u.s.st3[c0 + bit];
-                    for (;;) {
-                        m &= m - 1ull;
-                        const bool more = m != 0ull;
-                        const int nbit = more ? __builtin_ctzll(m) : bit;
-                        const float4 an = sh.u.s.st0[c0 + nbit], bn = sh.u.s.st1[c0 + nbit], xn = sh.u.s.st2[c0 + nbit],
-                                     sbn = sh.u.s.st3[c0 + nbit];
-                        const Record r{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, x.x};
-                        RasterSurvivor(sh.keys, r, x.y, __float_as_int(x.z), sb, block_sb, fx_lane, fy_lane, lane);
-                        if (!more) {
-                            break;
-                        }
-                        a = an;
-                        b = bn;
-                        x = xn;
-                        sb = sbn;
-                    }
-                }
-            } else {
-#pragma unroll 1
-                for (int c0 = 0; c0 < nb_here; c0 += kWave) {
-                    const int i = c0 + lane;
-                    bool pass = false;
-                    if (i < nb_here) {
-                        const float4 a = sh.u.s.st0[i], b = sh.u.s.st1[i], x = sh.u.s.st2[i];
-                        const Record r{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, x.x};
-                        pass = (!wave_sb || ScreenBoxOverlaps(wb, sh.u.s.st3[i])) && BoxMayHit(wb, r);
-                    }
-                    unsigned long long m = __ballot(pass);
-#ifdef SRT_DIAG
-                    d_wsurv += __popcll(m);
-#endif
-                    if (m != 0ull) {
-                        int bit = __builtin_ctzll(m);
-                        float4 a = sh.u.s.st0[c0 + bit], b = sh.u.s.st1[c0 + bit], x = sh.u.s.st2[c0 + bit];
-                        for (;;) {
-                            m &= m - 1ull;
-                            const bool more = m != 0ull;
-                            const int nbit = more ? __builtin_ctzll(m) : bit;
-                            const float4 an = sh.u.s.st0[c0 + nbit], bn = sh.u.s.st1[c0 + nbit], xn = sh.u.s.st2[c0 + nbit];
-                            const Record r{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, x.x};
-                            ExactTestAnyOrder<R, SHARED>(s, r, x.y, __float_as_int(x.z));
-                            if (!more) {
-                                break;
-                            }
-                            a = an;
-                            b = bn;
-                            x = xn;
-                        }
-                    }
-                }
-            }
-            __syncthreads();  // staging (and, after the last batch, the id list) reused next
-#ifdef SRT_DIAG
-            {
-                const unsigned long long now = __builtin_amdgcn_s_memtime();
-                d_walk += now - d_mark;
-                d_mark = now;
-            }
-#endif
-        }
-        total = 0;
-    }
-    if (nsteps == 0) {
-        __syncthreads();  // raster keys initialised by every wave before the read-back
-    }
-#ifdef SRT_DIAG
-    const unsigned blk = blockIdx.z * gridDim.y * gridDim.x + tile;
-    if (tid == 0 && blk < kDiagBlocks) {
-        unsigned long long* d = g_srt_diag[blk];
-        d[0] = d_stream;
-        d[1] = d_gather;
-        d[2] = d_walk;
-        d[3] = d_surv;
-        d[4] = d_wsurv;
-        d[5] = d_batches;
-        d[6] = __builtin_amdgcn_s_memtime() - d_t0;
-        d[7] = (RASTER ? 1 : 0) | (LIST ? 2 : 0) | 4 |
-               (p.bin_counts != nullptr ? (static_cast<unsigned long long>(p.bin_counts[tile]) << 16) |
-                                              (static_cast<unsigned long long>(p.bin_counts[p.tiles]) << 40)
-                                        : 0ull);
-    }
-#endif
-    if constexpr (RASTER) {
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const unsigned long long key = sh.keys[wave * R + r][lane];
-            if (key != ~0ull) {
-                s.bt[r] = __uint_as_float(static_cast<unsigned>(key >> 32));
-                s.bi[r] = static_cast<int>(static_cast<unsigned>(key));
-            }
-        }
-    }
+// Cull record of record `id` from the tile-planar edge buffer and the screen boxes (FULL).
+__device__ __forceinline__ CullRecord LoadCullById(const TraceParams& p, unsigned id) {
+    const float4* tile = p.edges + static_cast<size_t>(id / kTileTriangles) * kTileFloat4;
+    const unsigned j = id % kTileTriangles;
+    CullRecord r;
+    r.a = tile[j];
+    r.b = tile[kTileTriangles + j];
+    r.x = make_float4(Plane2(tile)[j], Plane3(tile)[j], __uint_as_float(id), 0.f);
+    r.sb = p.screen_boxes[id];
+    return r;
 }
 
 // ---------------------------------------------------------------------------------------
-// Packet walk: binned tiles (LIST) whose rays all share one sample offset, so fx depends on
-// the column only and fy on the row only, both monotone. Per batch of kPacketBatch list
-// entries:
-//   gather:  one thread per entry loads the record and its screen box, keeps it if it passes
-//            the tile-box tests (ScreenBoxOverlaps, BoxMayHit), and finds the exact column
-//            and row ranges of the tile whose ray positions lie inside the screen box (binary
-//            searches in the tile's fx / fy tables). Pixels outside those ranges cannot pass
-//            the exact test (screen-box guarantee), so skipping them is exact. The range is cut
-//            into packets of 64 pixels (2^lg columns x 64 >> lg rows, 2^lg >= the width).
+// Packet walk. The block's 64 x 16 ray positions sit in an LDS table; per column the
+// smallest and largest fx over the block's rows, per row the smallest and largest fy over
+// its columns, made monotone (lo' = suffix minimum, hi' = prefix maximum; a uniform-offset
+// tile's tables are single values, already monotone). Per batch of up to kPacketBatch
+// candidates:
+//   filter:  one thread per candidate keeps it if it passes the block-box tests
+//            (ScreenBoxOverlaps, BoxMayHit) and finds the columns whose fx interval can meet
+//            its screen box (hi'[c] >= xlo, lo'[c] <= xhi: searches in the monotone tables),
+//            and likewise the rows. A pixel outside those ranges has fx or fy outside the
+//            screen box, so it cannot pass the exact test (screen-box guarantee): skipping it
+//            is exact. (A block box outside the screen-box range: no screen-box tests, the
+//            whole block is the range.) The range is cut row-major into packets of 64 pixels;
 //   compact: survivors are compacted block-wide in any order, with an exclusive prefix of
 //            their packet counts;
 //   walk:    wave w takes the packets [w P / W, (w + 1) P / W) of the batch's P, two per
-//            iteration (independent dependency chains for the scheduler): each lane tests
-//            its pixel exactly and merges a hit into the pixel's key with an LDS atomic min.
+//            iteration (independent dependency chains for the scheduler): each lane reads its
+//            pixel's (fx, fy), tests it exactly and merges a hit into the pixel's key with an
+//            LDS atomic min.
 // Same exact test and lexicographic (t, id) result as ExactTestAnyOrder.
 // ---------------------------------------------------------------------------------------
-// One packet (64 pixels of one survivor's range) evaluated without branches: the pixel's
-// key and LDS address, and whether it is a hit (all E >= 0, det > 0, t finite; NaN anywhere
-// fails). `bits` = the survivor's packed pixel range (wave-uniform), `j` = packet index.
 struct PacketHit {
     unsigned long long key;
-    unsigned addr;  // byte offset of the pixel's 8-B key in the tile's keys
     bool hit;
 };
 
 struct PacketPixel {
-    unsigned colb, rowb;  // byte offsets of the pixel's column / row in the fx / fy tables
+    unsigned pixb;  // byte offset of the pixel in an 8-B-per-pixel block table (keys, positions)
     bool in;
 };
-
-[[maybe_unused]] __device__ __forceinline__ PacketPixel PacketLane(unsigned bits, unsigned j, int lane) {
-    const int c0 = bits & 63u, c1 = (bits >> 6) & 63u, r0 = (bits >> 12) & 31u, r1 = (bits >> 17) & 31u;
-    const int lg = (bits >> 22) & 7u;
-    const int col_u = c0 + (lane & ((1 << lg) - 1));
-    const int row_u = r0 + static_cast<int>(j << (6 - lg)) + (lane >> lg);
-    return PacketPixel{static_cast<unsigned>(min(col_u, c1)) * 4u, static_cast<unsigned>(min(row_u, r1)) * 4u,
-                       static_cast<bool>((col_u <= c1) & (row_u <= r1))};
-}
 
 // Row-major packing: packet j of a survivor with range [c0, c0 + nc) x [r0, r0 + nr) covers
 // range pixels p = 64 j + lane, p < nc * nr, at (c0 + p % nc, r0 + p / nc). p / nc is
 // (p * m) >> 17 with m = ceil(2^17 / nc): exact, because p < 1088 and nc <= 64 keep
 // p * (m - 2^17 / nc) / 2^17 < 1/nc (and p * m < 2^24 * 2^24 fits v_mul_u32_u24's low word,
-// p * m < 2^32). Lanes past the range read padding-free table entries but are not `in`.
-__device__ __forceinline__ unsigned PacketMagic(unsigned bits) {
-    const unsigned nc = ((bits >> 6) & 63u) + 1u;
+// p * m < 2^32). Lanes past the range address valid table entries but are not `in`.
+__device__ __forceinline__ unsigned PacketMagic(unsigned w) {
+    const unsigned nc = ((w >> 6) & 63u) + 1u;
     return (131071u + nc) / nc;
 }
-__device__ __forceinline__ PacketPixel PacketLaneFlat(unsigned bits, unsigned j, unsigned m, int lane) {
-    const unsigned c0 = bits & 63u, nc = ((bits >> 6) & 63u) + 1u, r0 = (bits >> 12) & 31u;
-    const unsigned nr = ((bits >> 17) & 31u) + 1u;
-    const unsigned pix = (j << 6) + static_cast<unsigned>(lane);
-    const unsigned row_in = __umul24(pix, m) >> 17;  // pix < 2^11, m <= 2^17
-    const unsigned col_in = pix - row_in * nc;
-    return PacketPixel{(c0 + col_in) * 4u, (r0 + row_in) * 4u, pix < nc * nr};
-}
 
-// Row band split (SRT_PACKET_SPLIT). For rows [ra, rb] of the range, an edge function
-// E = fma(fy, cy, fma(fx, cx, c0)) is monotone in fy (fma is monotone in each argument and the
-// fy table is nondecreasing in the row), so its largest value over the band at column c is at
-// fy* = fys[rb] (cy > 0) or fys[ra]; and at fixed fy* it is monotone in the column. The
-// columns where E(fx_c, fy*) >= 0 are therefore a prefix or suffix of [lo, hi], found by
-// binary search, and a column outside it fails that edge on every row of the band: dropping it
-// is exact. NaN coefficients: E is NaN everywhere (no pixel passes), any cut is exact.
-__device__ __forceinline__ void BandEdgeCut(const float* fxs, float fys_a, float fys_b, float cx, float cy, float c0,
-                                            int c_lo, int c_hi, int& lo, int& hi) {
-    // Branch-free lower bound over [c_lo, c_hi] (<= 64 columns, 7 fixed steps) of the first
-    // column that does not "advance": for cx > 0 advance while E < 0 (the passing columns are
-    // a suffix), for cx < 0 while E >= 0 (a prefix). cx == 0 (E constant in c) or NaN: one test.
-    const float fy = cy > 0.f ? fys_b : fys_a;
-    const bool inc = cx > 0.f;
-    int pos = c_lo;
-#pragma unroll
-    for (int step = 64; step >= 1; step >>= 1) {
-        const int c = pos + step - 1;
-        const float e = fmaf(fy, cy, fmaf(fxs[min(c, c_hi)], cx, c0));
-        pos += (c <= c_hi && ((e >= 0.f) != inc)) ? step : 0;
-    }
-    if (inc) {
-        lo = pos;
-        hi = c_hi;
-    } else if (cx < 0.f) {
-        lo = c_lo;
-        hi = pos - 1;
-    } else {
-        const bool pass = fmaf(fy, cy, fmaf(fxs[c_lo], cx, c0)) >= 0.f;
-        lo = c_lo;
-        hi = pass ? c_hi : c_lo - 1;
-    }
-}
-
-// Column range of rows [ra, rb] inside [c0, c1] (empty: c1 < c0 on return). The three edge
-// cuts are independent searches over [c0, c1] (their LDS reads overlap), then intersected.
-[[maybe_unused]] __device__ __forceinline__ void BandColumns(const float* fxs, const float* fys, const CullRecord& cr, int ra, int rb,
-                                            int& c0, int& c1) {
-    const float fa = fys[ra], fb = fys[rb];
-    int l0, h0, l1, h1, l2, h2;
-    BandEdgeCut(fxs, fa, fb, cr.a.y, cr.a.z, cr.a.x, c0, c1, l0, h0);
-    BandEdgeCut(fxs, fa, fb, cr.b.x, cr.b.y, cr.a.w, c0, c1, l1, h1);
-    BandEdgeCut(fxs, fa, fb, cr.b.w, cr.x.x, cr.b.z, c0, c1, l2, h2);
-    c0 = max(max(l0, l1), l2);
-    c1 = min(min(h0, h1), h2);
-}
-
-// One word per packet for the walk loop (one readlane instead of three): the range fields of
-// PacketLaneFlat's `bits` narrowed to 4-bit rows, the survivor slot and the packet index.
-// Needs rows < 16 (kBlockRows <= 16), slots < 256 and packets per survivor <= 16.
-__device__ __forceinline__ unsigned PacketWord(unsigned bits, unsigned slot, unsigned j) {
-    return (bits & 0xFFFu) | ((bits >> 12) & 15u) << 12 | ((bits >> 17) & 15u) << 16 | slot << 20 | j << 28;
+// One word per packet (one readlane in the walk loop): c0 (6 bits), nc - 1 (6), r0 (4),
+// nr - 1 (4), survivor slot (8), packet index (4).
+__device__ __forceinline__ unsigned PacketRange(int c0, int nc, int r0, int nr) {
+    return static_cast<unsigned>(c0) | static_cast<unsigned>(nc - 1) << 6 | static_cast<unsigned>(r0) << 12 |
+           static_cast<unsigned>(nr - 1) << 16;
 }
 __device__ __forceinline__ PacketPixel PacketLaneWord(unsigned w, unsigned m, int lane) {
-    // In byte units (4 pix): (4 pix m) >> 19 == (pix m) >> 17, 4 pix m < 2^32.
+    // In units of 4 pixels: (4 pix m) >> 19 == (pix m) >> 17, 4 pix m < 2^32.
     const unsigned c0 = w & 63u, nc = ((w >> 6) & 63u) + 1u, r0 = (w >> 12) & 15u, nr = ((w >> 16) & 15u) + 1u;
     const unsigned pix4 = (w >> 28 << 8) | (static_cast<unsigned>(lane) << 2);
     const unsigned row_in = __umul24(pix4, m) >> 19;
-    return PacketPixel{pix4 + c0 * 4u - row_in * (nc * 4u), row_in * 4u + r0 * 4u, pix4 < nc * nr * 4u};
+    const unsigned col4 = pix4 - row_in * (nc * 4u) + c0 * 4u;  // 4 * column
+    return PacketPixel{((row_in + r0) << 9) + col4 * 2u, pix4 < nc * nr * 4u};
 }
 
-__device__ __forceinline__ PacketHit EvalPacket(const float4& a, const float4& b, const float4& x, float fx, float fy,
-                                                const PacketPixel& px) {
-    const float eA = fmaf(fy, a.z, fmaf(fx, a.y, a.x));
-    const float eB = fmaf(fy, b.y, fmaf(fx, b.x, a.w));
-    const float eC = fmaf(fy, x.x, fmaf(fx, b.w, b.z));
+__device__ __forceinline__ PacketHit EvalPacket(const float4& a, const float4& b, const float4& x, float2 f,
+                                                bool in) {
+    const float eA = fmaf(f.y, a.z, fmaf(f.x, a.y, a.x));
+    const float eB = fmaf(f.y, b.y, fmaf(f.x, b.x, a.w));
+    const float eC = fmaf(f.y, x.x, fmaf(f.x, b.w, b.z));
     const float det = (eA + eB) + eC;
     const float t = x.y / det;
     PacketHit h;
-    h.hit = static_cast<bool>(px.in & (fminf(fminf(eA, eB), eC) >= 0.f) & (det > 0.f) & (t < __builtin_inff()));
+    h.hit = static_cast<bool>(in & (fminf(fminf(eA, eB), eC) >= 0.f) & (det > 0.f) & (t < __builtin_inff()));
     h.key = HitKey(t, __float_as_int(x.z));
-    h.addr = px.rowb * (kWave * 2u) + px.colb * 2u;
-    return h;
-}
-
-// EvalPacket with a cheaper exact division. The compiler's IEEE f32 division is
-//   s = div_scale(det), n = div_scale(vol) [vcc], y = rcp(s), y = fma(fma(-s, y, 1), y, y),
-//   q = n y, q = fma(fma(-s, q, n), y, q), q = div_fmas(fma(-s, q, n), y, q), div_fixup(q, det, vol)
-// and div_scale leaves its operand unchanged (vcc = 0), div_fmas is then a plain fma, and
-// div_fixup returns q, whenever vol and det are normal, nonzero, |exponent difference| < 96
-// and the quotient is normal: true for vol in [2^-48, 2^48) and det in [2^-47, 2^47). Then
-// the 8 instructions below give the same bits. vol is per survivor (vol_slow: outside its
-// range), det per lane: if any lane that passes the edge tests has det outside its range (or
-// vol_slow), the whole wave takes the IEEE division (a uniform branch) -- the fast path is an
-// evaluation shortcut, never a change of result. On the fast path every passing lane has
-// 0 < det and a finite t, so the hit is (edges pass) & (det in range).
-[[maybe_unused]] __device__ __forceinline__ PacketHit EvalPacketFast(const float4& a, const float4& b, const float4& x, float fx,
-                                                    float fy, const PacketPixel& px, bool vol_slow) {
-    const float eA = fmaf(fy, a.z, fmaf(fx, a.y, a.x));
-    const float eB = fmaf(fy, b.y, fmaf(fx, b.x, a.w));
-    const float eC = fmaf(fy, x.x, fmaf(fx, b.w, b.z));
-    const float det = (eA + eB) + eC;
-    const bool e_ok = static_cast<bool>(px.in & (fminf(fminf(eA, eB), eC) >= 0.f));
-    constexpr unsigned kLo = 0x28000000u, kHi = 0x57000000u;  // 2^-47, 2^47
-    const bool det_ok = __float_as_uint(det) - kLo < kHi - kLo;
-    PacketHit h;
-    float t;
-    if (vol_slow || __ballot(e_ok && !det_ok) != 0ull) {
-        t = x.y / det;
-        h.hit = static_cast<bool>(e_ok & (det > 0.f) & (t < __builtin_inff()));
-    } else {
-        const float y0 = __builtin_amdgcn_rcpf(det);
-        const float y1 = fmaf(fmaf(-det, y0, 1.f), y0, y0);
-        const float q0 = x.y * y1;
-        const float q1 = fmaf(fmaf(-det, q0, x.y), y1, q0);
-        t = fmaf(fmaf(-det, q1, x.y), y1, q1);
-        h.hit = e_ok & det_ok;
-    }
-    h.key = HitKey(t, __float_as_int(x.z));
-    h.addr = px.rowb * (kWave * 2u) + px.colb * 2u;
     return h;
 }
 
@@ -1355,379 +899,286 @@ __device__ __forceinline__ int LastAtMost(const float* t, int n, float v, int g)
     return g - 1;
 }
 
-template <int W>
-__device__ __forceinline__ void PacketWalk(const TraceParams& p, CullShared<W>& sh, Rays<CullShape<W>::kR>& s,
-                                           const Box& bb, float fx_lane, float fy_lane, const CullSource& src, int tx,
-                                           int row0) {
-    using S = CullShape<W>;
-    constexpr int R = S::kR;
-    constexpr int kThreads = S::kThreads;
-    constexpr int kBatchN = S::kPBatch;
-    constexpr int kSlices = kBatchN / kThreads;  // batch entries per thread
-    static_assert(kBatchN % kThreads == 0, "whole slices");
+// Inclusive scans over the 64 lanes of a wave: prefix maximum (up) / suffix minimum (down).
+__device__ __forceinline__ float WavePrefixMax(float v, int lane) {
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+        const float u = __shfl_up(v, o);
+        v = lane >= o ? fmaxf(v, u) : v;
+    }
+    return v;
+}
+__device__ __forceinline__ float WaveSuffixMin(float v, int lane) {
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+        const float u = __shfl_down(v, o);
+        v = lane + o < kWave ? fminf(v, u) : v;
+    }
+    return v;
+}
+__device__ __forceinline__ float WaveMin(float v) {
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+        v = fminf(v, __shfl_xor(v, o));
+    }
+    return v;
+}
+__device__ __forceinline__ float WaveMax(float v) {
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+        v = fmaxf(v, __shfl_xor(v, o));
+    }
+    return v;
+}
+
+// The block's position tables (see the section comment) from the lane's rays. `regular`:
+// every ray of the block has the same sample offset, so fx_lane (column `lane`) and fy_lane
+// (row `lane` < kBlockRows) already are the monotone tables. Ends with a barrier.
+__device__ __forceinline__ void PacketTables(CullShared& sh, const Rays<kCullR>& s, bool regular, float fx_lane,
+                                             float fy_lane, int nc, int nr) {
+    constexpr int R = kCullR;
+    const int tid = threadIdx.x;
+    const int lane = tid & (kWave - 1);
+    const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        sh.fxy[wave * R + r][lane] = make_float2(s.fx[r], s.fy[r]);
+    }
+    if (regular) {
+        if (tid < kWave) {
+            sh.clo[tid] = fx_lane;
+            sh.chi[tid] = fx_lane;
+        }
+        if (tid < kBlockRows) {
+            sh.rlo[tid] = fy_lane;
+            sh.rhi[tid] = fy_lane;
+        }
+        __syncthreads();
+        return;
+    }
+    // Per column: min / max of fx over this wave's rows (scratch in the survivor planes, which
+    // the first batch writes only after later barriers); per row: over the valid columns.
+    float2* part = reinterpret_cast<float2*>(sh.sv0);
+    float lo = __builtin_inff(), hi = -__builtin_inff();
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        lo = fminf(lo, s.fx[r]);
+        hi = fmaxf(hi, s.fx[r]);
+        const float fy = lane < nc ? s.fy[r] : __builtin_nanf("");  // NaN drops out of min / max
+        const float ylo = WaveMin(fy), yhi = WaveMax(fy);
+        if (lane == 0) {
+            sh.rlo[wave * R + r] = ylo;
+            sh.rhi[wave * R + r] = yhi;
+        }
+    }
+    part[wave * kWave + lane] = make_float2(lo, hi);
+    __syncthreads();
+    if (wave == 0) {
+        float clo = __builtin_inff(), chi = -__builtin_inff();
+#pragma unroll
+        for (int w = 0; w < kCullWaves; ++w) {
+            const float2 v = part[w * kWave + lane];
+            clo = fminf(clo, v.x);
+            chi = fmaxf(chi, v.y);
+        }
+        // Columns past the frame edge do not constrain the valid ones (searches stop at nc).
+        sh.clo[lane] = WaveSuffixMin(lane < nc ? clo : __builtin_inff(), lane);
+        sh.chi[lane] = WavePrefixMax(chi, lane);
+    } else if (wave == 1) {
+        const float rl = lane < nr ? sh.rlo[min(lane, kBlockRows - 1)] : __builtin_inff();
+        const float rh = lane < kBlockRows ? sh.rhi[lane] : -__builtin_inff();
+        const float rlo = WaveSuffixMin(rl, lane), rhi = WavePrefixMax(rh, lane);
+        if (lane < kBlockRows) {
+            sh.rlo[lane] = rlo;
+            sh.rhi[lane] = rhi;
+        }
+    }
+    __syncthreads();
+}
+
+// Per-block constants of the packet walk: valid columns / rows and the linear models of the
+// monotone tables for the range guesses; use_sb = the block box is inside the screen-box range.
+struct PacketFrame {
+    int nc, nr;
+    bool use_sb;
+    float fx_first, fx_scale, fy_first, fy_scale;
+};
+__device__ __forceinline__ PacketFrame MakePacketFrame(const CullShared& sh, int nc, int nr, bool use_sb) {
+    PacketFrame f;
+    f.nc = nc;
+    f.nr = nr;
+    f.use_sb = use_sb;
+    f.fx_first = sh.clo[0];
+    f.fy_first = sh.rlo[0];
+    const float fx_last = sh.chi[nc - 1], fy_last = sh.rhi[nr - 1];
+    f.fx_scale = nc > 1 && fx_last > f.fx_first ? static_cast<float>(nc - 1) / (fx_last - f.fx_first) : 0.f;
+    f.fy_scale = nr > 1 && fy_last > f.fy_first ? static_cast<float>(nr - 1) / (fy_last - f.fy_first) : 0.f;
+    return f;
+}
+
+// One packet-walk batch: candidate e * kCullThreads + tid is cr[e] when valid[e]. Filter,
+// compaction and the walk into sh.keys; `prefetch()` runs between the compaction and the walk
+// (the next batch's loads then hide behind the walk). Starts and ends with block-uniform
+// control flow; contains barriers; ends with one.
+template <class F>
+__device__ __forceinline__ void PacketBatch(CullShared& sh, const Box& bb, const PacketFrame& pf,
+                                            const CullRecord (&cr)[kSlices], const bool (&valid)[kSlices],
+                                            F&& prefetch) {
+    constexpr int W = kCullWaves;
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
     const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);
     const unsigned long long lt_mask = (1ull << lane) - 1ull;
-    auto& k = sh.u.k;
-#ifndef SRT_DIAG  // (the diag build records every block's counters)
-    if (src.end == src.begin) {
-        return;  // no candidates (block-uniform): every ray keeps its miss
+    bool pass[kSlices];
+    unsigned bits[kSlices], npk[kSlices];
+#pragma unroll
+    for (int e = 0; e < kSlices; ++e) {
+        bits[e] = 0u;
+        npk[e] = 0u;
+        const float4 sb = cr[e].sb;
+        const Record r{cr[e].a.x, cr[e].a.y, cr[e].a.z, cr[e].a.w, cr[e].b.x, cr[e].b.y, cr[e].b.z, cr[e].b.w,
+                       cr[e].x.x};
+        pass[e] = valid[e] && (!pf.use_sb || ScreenBoxOverlaps(bb, sb)) && BoxMayHit(bb, r);
+        if (pass[e]) {
+            int c0 = 0, c1 = pf.nc - 1, r0 = 0, r1 = pf.nr - 1;
+            if (pf.use_sb) {
+                // Columns whose fx interval can meet [sb.xlo, sb.xhi]; rows likewise.
+                c0 = FirstAtLeast(sh.chi, pf.nc, sb.x, GuessIndex(sb.x, pf.fx_first, pf.fx_scale, pf.nc));
+                c1 = LastAtMost(sh.clo, pf.nc, sb.y, GuessIndex(sb.y, pf.fx_first, pf.fx_scale, pf.nc) + 1);
+                r0 = FirstAtLeast(sh.rhi, pf.nr, sb.z, GuessIndex(sb.z, pf.fy_first, pf.fy_scale, pf.nr));
+                r1 = LastAtMost(sh.rlo, pf.nr, sb.w, GuessIndex(sb.w, pf.fy_first, pf.fy_scale, pf.nr) + 1);
+            }
+            pass[e] = c0 <= c1 && r0 <= r1;
+            if (pass[e]) {
+                npk[e] = static_cast<unsigned>(((c1 - c0 + 1) * (r1 - r0 + 1) + kWave - 1) / kWave);
+                bits[e] = PacketRange(c0, c1 - c0 + 1, r0, r1 - r0 + 1);
+            }
+        }
     }
-#endif
-    const int nc = min(kWave, p.width - tx * kWave);
-    const int nr = min(kBlockRows, p.row_count - row0);
-    if (tid < kWave) {
-        k.fxs[tid] = fx_lane;
+    // Compact the survivors block-wide ((slice, wave, lane) order); exclusive packet prefix
+    // in compacted order.
+    unsigned wpos[kSlices], incl[kSlices];
+#pragma unroll
+    for (int e = 0; e < kSlices; ++e) {
+        const unsigned long long m = __ballot(pass[e]);
+        wpos[e] = __popcll(m & lt_mask);
+        incl[e] = npk[e];
+#pragma unroll
+        for (int o = 1; o < kWave; o <<= 1) {
+            const unsigned t = __shfl_up(incl[e], o);
+            if (lane >= o) {
+                incl[e] += t;
+            }
+        }
+        if (lane == kWave - 1) {
+            sh.wave_n[e * W + wave] = __popcll(m);
+            sh.wave_pk[e * W + wave] = incl[e];
+        }
     }
-    if (tid < kBlockRows) {
-        k.fys[tid] = fy_lane;
-    }
-    for (int i = tid; i < kBlockRows * kWave; i += kThreads) {
-        (&sh.keys[0][0])[i] = ~0ull;
-    }
-    // Linear models of the (nondecreasing) column / row tables for the range guesses.
-    const float fx_first = __shfl(fx_lane, 0), fx_last = __shfl(fx_lane, nc - 1);
-    const float fy_first = __shfl(fy_lane, 0), fy_last = __shfl(fy_lane, nr - 1);
-    const float fx_scale = nc > 1 && fx_last > fx_first ? static_cast<float>(nc - 1) / (fx_last - fx_first) : 0.f;
-    const float fy_scale = nr > 1 && fy_last > fy_first ? static_cast<float>(nr - 1) / (fy_last - fy_first) : 0.f;
     __syncthreads();
-    const unsigned total = src.end - src.begin;
-#ifdef SRT_DIAG
-    unsigned long long d_gather = 0, d_walk = 0, d_surv = 0, d_pk = 0, d_batches = 0;
-    const unsigned long long d_t0 = __builtin_amdgcn_s_memtime();
-    unsigned long long d_mark = d_t0;
-#endif
-    // Gather loads are software-pipelined one batch ahead: batch b+1's records are requested
-    // before batch b's walk, so their latency hides behind it (heavy tiles take 2 batches).
-    CullRecord nxt[kSlices];
-    auto load_batch = [&](unsigned b0) {
+    // Bases of (slice e, this wave): the virtual waves (e', w') before it, in order.
+    unsigned n_surv = 0, n_pk = 0;
+    unsigned sbase[kSlices], pbase[kSlices];
+#pragma unroll
+    for (int e = 0; e < kSlices; ++e) {
+        sbase[e] = 0u;
+        pbase[e] = 0u;
+    }
+#pragma unroll
+    for (int vw = 0; vw < kSlices * W; ++vw) {
+        const unsigned wn = sh.wave_n[vw], wp = sh.wave_pk[vw];
 #pragma unroll
         for (int e = 0; e < kSlices; ++e) {
-            const unsigned v = b0 + e * kThreads + tid;
-            const unsigned vv = src.begin + (v < total ? v : 0u);
-#ifdef SRT_DIAG
-            if (p.exp & 256u) {  // timing experiment: coalesced loads (results wrong)
-                nxt[e] = p.cull[(vv & 0xFFFFu) % p.n];
-                continue;
-            }
-#endif
-            nxt[e] = p.cull[vv < src.count1 ? src.list[vv] : src.list2[vv - src.count1]];
+            const bool before = vw < e * W + wave;
+            sbase[e] += before ? wn : 0u;
+            pbase[e] += before ? wp : 0u;
         }
-    };
-    if (total != 0u) {
-        load_batch(0u);
+        n_surv += wn;
+        n_pk += wp;
     }
+#pragma unroll
+    for (int e = 0; e < kSlices; ++e) {
+        if (pass[e]) {
+            const unsigned slot = sbase[e] + wpos[e];
+            sh.sv0[slot] = cr[e].a;
+            sh.sv1[slot] = cr[e].b;
+            sh.sv2[slot] = make_float4(cr[e].x.x, cr[e].x.y, cr[e].x.z, __uint_as_float(bits[e]));
+            sh.pre[slot] = pbase[e] + incl[e] - npk[e];
+        }
+    }
+    if (tid == 0) {
+        sh.pre[n_surv] = n_pk;
+    }
+    __syncthreads();
+    prefetch();
+    // Walk this wave's packets [q_begin, q_end), 64 at a time: lane l finds packet q0 + l's
+    // survivor (binary search in pre) and packs its word, then the wave takes the packets
+    // kPacketIlp at a time (independent chains: all LDS reads issued together; a tail repeats
+    // the last packet, harmless under an atomic min) and applies the hits.
+    constexpr int kPacketIlp = SRT_PACKET_ILP;
+    const unsigned q_begin = wave * n_pk / W, q_end = (wave + 1) * n_pk / W;
+    const char* fxy = reinterpret_cast<const char*>(&sh.fxy[0][0]);
+    char* keys = reinterpret_cast<char*>(&sh.keys[0][0]);
 #pragma unroll 1
-    for (unsigned b0 = 0; b0 < total; b0 += kBatchN) {
-        // Gather: entries b0 + e * kThreads + tid of the block's virtual list.
-        CullRecord cr[kSlices];
-        bool pass[kSlices];
-#pragma unroll
-        for (int e = 0; e < kSlices; ++e) {
-            pass[e] = b0 + e * kThreads + tid < total;
-            cr[e] = nxt[e];
-        }
-        unsigned bits[kSlices], npk[kSlices], band2[kSlices];
-#pragma unroll
-        for (int e = 0; e < kSlices; ++e) {
-            bits[e] = 0u;
-            npk[e] = 0u;
-            band2[e] = 0u;
-            const float4 sb = cr[e].sb;
-            const Record r{cr[e].a.x, cr[e].a.y, cr[e].a.z, cr[e].a.w, cr[e].b.x, cr[e].b.y, cr[e].b.z, cr[e].b.w,
-                           cr[e].x.x};
-            pass[e] = pass[e] && ScreenBoxOverlaps(bb, sb) && BoxMayHit(bb, r);
-            if (pass[e]) {
-                // Columns c with sb.xlo <= fx[c] <= sb.xhi (fx nondecreasing in c); rows likewise.
-                // Interpolated guesses, then exact steps in the tables.
-                const int c0 = FirstAtLeast(k.fxs, nc, sb.x, GuessIndex(sb.x, fx_first, fx_scale, nc));
-                const int c1 = LastAtMost(k.fxs, nc, sb.y, GuessIndex(sb.y, fx_first, fx_scale, nc) + 1);
-                const int r0 = FirstAtLeast(k.fys, nr, sb.z, GuessIndex(sb.z, fy_first, fy_scale, nr));
-                const int r1 = LastAtMost(k.fys, nr, sb.w, GuessIndex(sb.w, fy_first, fy_scale, nr) + 1);
-                pass[e] = c0 <= c1 && r0 <= r1;
-                if (pass[e]) {
-                    const int ncols = c1 - c0 + 1;
-#if SRT_PACKET_FLAT
-                    npk[e] = static_cast<unsigned>((ncols * (r1 - r0 + 1) + kWave - 1) / kWave);
-                    bits[e] = static_cast<unsigned>(c0) | static_cast<unsigned>(ncols - 1) << 6 |
-                              static_cast<unsigned>(r0) << 12 | static_cast<unsigned>(r1 - r0) << 17;
-#if SRT_PACKET_SPLIT
-                    if (npk[e] > 1u) {  // a one-packet range cannot get cheaper
-                        const int rm = r0 + ((r1 - r0 + 1) >> 1);  // bands [r0, rm - 1], [rm, r1]
-                        int a0 = c0, a1 = c1, b0 = c0, b1 = c1;
-                        BandColumns(k.fxs, k.fys, cr[e], r0, rm - 1, a0, a1);
-                        BandColumns(k.fxs, k.fys, cr[e], rm, r1, b0, b1);
-                        const unsigned na = a0 <= a1 ? static_cast<unsigned>(((a1 - a0 + 1) * (rm - r0) + kWave - 1) / kWave) : 0u;
-                        const unsigned nb = b0 <= b1 ? static_cast<unsigned>(((b1 - b0 + 1) * (r1 - rm + 1) + kWave - 1) / kWave) : 0u;
-                        const unsigned bits_a = static_cast<unsigned>(a0) | static_cast<unsigned>(a1 - a0) << 6 |
-                                                static_cast<unsigned>(r0) << 12 | static_cast<unsigned>(rm - 1 - r0) << 17;
-                        const unsigned bits_b = static_cast<unsigned>(b0) | static_cast<unsigned>(b1 - b0) << 6 |
-                                                static_cast<unsigned>(rm) << 12 | static_cast<unsigned>(r1 - rm) << 17;
-                        if (na + nb < npk[e]) {
-                            npk[e] = na + nb;
-                            if (na == 0u) {
-                                bits[e] = bits_b;
-                            } else if (nb == 0u) {
-                                bits[e] = bits_a;
-                            } else {
-                                bits[e] = bits_a | 1u << 22;
-                                band2[e] = bits_b;
-                            }
-                            pass[e] = npk[e] != 0u;
-                        }
-                    }
-#endif
-#else
-                    const int lg = ncols <= 1 ? 0 : 32 - __builtin_clz(static_cast<unsigned>(ncols - 1));
-                    const int rpp = kWave >> lg;
-                    npk[e] = static_cast<unsigned>((r1 - r0 + rpp) / rpp);
-                    bits[e] = static_cast<unsigned>(c0) | static_cast<unsigned>(c1) << 6 |
-                              static_cast<unsigned>(r0) << 12 | static_cast<unsigned>(r1) << 17 |
-                              static_cast<unsigned>(lg) << 22;
-#endif
-                }
+    for (unsigned q0 = q_begin; q0 < q_end; q0 += kWave) {
+        const unsigned mine = min(q0 + static_cast<unsigned>(lane), q_end - 1u);
+        int lo = 0, hi = static_cast<int>(n_surv) - 1;  // last survivor with pre <= mine
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (sh.pre[mid] <= mine) {
+                lo = mid;
+            } else {
+                hi = mid - 1;
             }
         }
-        // Compact the survivors block-wide ((slice, wave, lane) order); exclusive packet
-        // prefix in compacted order.
-        unsigned wpos[kSlices], incl[kSlices];
-#pragma unroll
-        for (int e = 0; e < kSlices; ++e) {
-            const unsigned long long m = __ballot(pass[e]);
-            wpos[e] = __popcll(m & lt_mask);
-            incl[e] = npk[e];
-#pragma unroll
-            for (int o = 1; o < kWave; o <<= 1) {
-                const unsigned t = __shfl_up(incl[e], o);
-                if (lane >= o) {
-                    incl[e] += t;
-                }
-            }
-            if (lane == kWave - 1) {
-                k.wave_n[e * W + wave] = __popcll(m);
-                k.wave_pk[e * W + wave] = incl[e];
-            }
-        }
-        __syncthreads();
-        // Bases of (slice e, this wave): the virtual waves (e', w') before it, in order.
-        unsigned n_surv = 0, n_pk = 0;
-        unsigned sbase[kSlices], pbase[kSlices];
-#pragma unroll
-        for (int e = 0; e < kSlices; ++e) {
-            sbase[e] = 0u;
-            pbase[e] = 0u;
-        }
-#pragma unroll
-        for (int vw = 0; vw < kSlices * W; ++vw) {
-            const unsigned wn = k.wave_n[vw], wp = k.wave_pk[vw];
-#pragma unroll
-            for (int e = 0; e < kSlices; ++e) {
-                const bool before = vw < e * W + wave;
-                sbase[e] += before ? wn : 0u;
-                pbase[e] += before ? wp : 0u;
-            }
-            n_surv += wn;
-            n_pk += wp;
-        }
-#pragma unroll
-        for (int e = 0; e < kSlices; ++e) {
-            if (pass[e]) {
-                const unsigned slot = sbase[e] + wpos[e];
-                k.sv0[slot] = cr[e].a;
-                k.sv1[slot] = cr[e].b;
-                k.sv2[slot] = make_float4(cr[e].x.x, cr[e].x.y, cr[e].x.z, __uint_as_float(bits[e]));
-#if SRT_PACKET_SPLIT
-                k.band2[slot] = band2[e];
-#endif
-                k.pre[slot] = pbase[e] + incl[e] - npk[e];
-            }
-        }
-        if (tid == 0) {
-            k.pre[n_surv] = n_pk;
-        }
-        __syncthreads();
-#ifdef SRT_DIAG
-        {
-            const unsigned long long now = __builtin_amdgcn_s_memtime();
-            d_gather += now - d_mark;
-            d_mark = now;
-            d_surv += n_surv;
-            d_pk += n_pk;
-            ++d_batches;
-        }
-#endif
-        if (b0 + kBatchN < total) {
-            load_batch(b0 + kBatchN);
-        }
-        // Walk this wave's packets [q_begin, q_end), 64 at a time: lane l finds packet q0 + l's
-        // survivor (binary search in pre) and fetches its range bits, then the wave takes the
-        // packets kPacketIlp at a time (independent chains: all LDS reads issued together; a
-        // tail repeats the last packet, harmless under an atomic min) and applies the hits.
-        constexpr int kPacketIlp = SRT_PACKET_ILP;
-        unsigned q_begin = wave * n_pk / W, q_end = (wave + 1) * n_pk / W;
-#ifdef SRT_DIAG
-        if (p.exp & 64u) {
-            q_end = q_begin;
-        }
-#endif
-        unsigned long long* keys = &sh.keys[0][0];
+        const unsigned my_bits = __float_as_uint(sh.sv2[lo].w);
+        const unsigned my_w = my_bits | static_cast<unsigned>(lo) << 20 | (mine - sh.pre[lo]) << 28;
+        const unsigned my_m = PacketMagic(my_bits);
+        // Resolve the per-lane packet table before the loop, so the loop header does not wait
+        // for the previous iteration's LDS atomics (conservative waitcnt merge).
+        asm volatile("" ::"v"(my_w), "v"(my_m));
+        const unsigned n = min(static_cast<unsigned>(kWave), q_end - q0);
 #pragma unroll 1
-        for (unsigned q0 = q_begin; q0 < q_end; q0 += kWave) {
-            const unsigned mine = min(q0 + static_cast<unsigned>(lane), q_end - 1u);
-            int lo = 0, hi = static_cast<int>(n_surv) - 1;  // last survivor with pre <= mine
-            while (lo < hi) {
-                const int mid = (lo + hi + 1) >> 1;
-                if (k.pre[mid] <= mine) {
-                    lo = mid;
-                } else {
-                    hi = mid - 1;
-                }
+        for (unsigned i = 0; i < n; i += kPacketIlp) {
+            unsigned ps[kPacketIlp];
+            PacketPixel px[kPacketIlp];
+            float4 ra[kPacketIlp], rb[kPacketIlp], rx[kPacketIlp];
+            float2 f[kPacketIlp];
+#pragma unroll
+            for (int u = 0; u < kPacketIlp; ++u) {
+                const unsigned li = min(i + u, n - 1u);
+                const unsigned w = __builtin_amdgcn_readlane(my_w, li);
+                ps[u] = (w >> 20) & 255u;
+                px[u] = PacketLaneWord(w, __builtin_amdgcn_readlane(my_m, li), lane);
             }
-            const unsigned my_s = static_cast<unsigned>(lo);
-            unsigned my_j = mine - k.pre[lo];
-            unsigned my_bits = __float_as_uint(k.sv2[lo].w);
-#if SRT_PACKET_FLAT && SRT_PACKET_SPLIT
-            if (my_bits & (1u << 22)) {  // two row bands: the first band's packets come first
-                const unsigned na = ((((my_bits >> 6) & 63u) + 1u) * (((my_bits >> 17) & 31u) + 1u) + kWave - 1) / kWave;
-                if (my_j >= na) {
-                    my_bits = k.band2[lo];
-                    my_j -= na;
-                }
+#pragma unroll
+            for (int u = 0; u < kPacketIlp; ++u) {
+                ra[u] = sh.sv0[ps[u]];
+                rb[u] = sh.sv1[ps[u]];
+                rx[u] = sh.sv2[ps[u]];
+                f[u] = *reinterpret_cast<const float2*>(fxy + px[u].pixb);
             }
-#endif
-            const unsigned n = min(static_cast<unsigned>(kWave), q_end - q0);
-#if SRT_PACKET_FLAT
-            unsigned my_m = PacketMagic(my_bits);  // < 2^18; bit 31: vol outside the fast-division range
-#if SRT_FAST_DIV
-            {
-                const unsigned vb = __float_as_uint(k.sv2[my_s].y);
-                my_m |= vb - 0x27800000u < 0x57800000u - 0x27800000u ? 0u : 0x80000000u;  // [2^-48, 2^48)
+            PacketHit h[kPacketIlp];
+#pragma unroll
+            for (int u = 0; u < kPacketIlp; ++u) {
+                h[u] = EvalPacket(ra[u], rb[u], rx[u], f[u], px[u].in);
             }
-#endif
-#endif
-#if SRT_PACKET_WORD
-            constexpr bool kWord = kBlockRows <= 16 && S::kPBatch <= 256;  // field widths
-            const unsigned my_w = kWord ? PacketWord(my_bits, my_s, my_j) : 0u;
-            if constexpr (kWord) {
-                asm volatile("" ::"v"(my_w));
+            // Keys built before the hit branches: the record id is loaded with the rest of the
+            // record instead of by a separate LDS read (and full wait) inside the branch.
+#pragma unroll
+            for (int u = 0; u < kPacketIlp; ++u) {
+                asm volatile("" ::"v"(h[u].key));
             }
-#endif
-#if SRT_PIN_LOADS
-            // Resolve the per-lane packet table before the loop, so the loop header does not
-            // wait for the previous iteration's LDS atomics (conservative waitcnt merge).
-            asm volatile("" ::"v"(my_s), "v"(my_bits), "v"(my_j));
-#if SRT_PACKET_FLAT
-            asm volatile("" ::"v"(my_m));
-#endif
-#endif
-#pragma unroll 1
-            for (unsigned i = 0; i < n; i += kPacketIlp) {
-                unsigned ps[kPacketIlp];
-                PacketPixel px[kPacketIlp];
-                float4 ra[kPacketIlp], rb[kPacketIlp], rx[kPacketIlp];
-                float fx[kPacketIlp], fy[kPacketIlp];
-                bool vol_slow[kPacketIlp];
 #pragma unroll
-                for (int u = 0; u < kPacketIlp; ++u) {
-                    const unsigned li = min(i + u, n - 1u);
-                    vol_slow[u] = true;
-#if SRT_PACKET_WORD
-                    if constexpr (kWord) {
-                        const unsigned w = __builtin_amdgcn_readlane(my_w, li);
-                        const unsigned mm = __builtin_amdgcn_readlane(my_m, li);
-                        ps[u] = (w >> 20) & 255u;
-                        vol_slow[u] = (mm >> 31) != 0u;
-                        px[u] = PacketLaneWord(w, mm, lane);
-                    } else {
-                        ps[u] = __builtin_amdgcn_readlane(my_s, li);
-                        px[u] = PacketLaneFlat(__builtin_amdgcn_readlane(my_bits, li),
-                                               __builtin_amdgcn_readlane(my_j, li), __builtin_amdgcn_readlane(my_m, li),
-                                               lane);
-                    }
-#elif SRT_PACKET_FLAT
-                    ps[u] = __builtin_amdgcn_readlane(my_s, li);
-                    px[u] = PacketLaneFlat(__builtin_amdgcn_readlane(my_bits, li), __builtin_amdgcn_readlane(my_j, li),
-                                           __builtin_amdgcn_readlane(my_m, li), lane);
-#else
-                    ps[u] = __builtin_amdgcn_readlane(my_s, li);
-                    px[u] = PacketLane(__builtin_amdgcn_readlane(my_bits, li), __builtin_amdgcn_readlane(my_j, li), lane);
-#endif
-                }
-#pragma unroll
-                for (int u = 0; u < kPacketIlp; ++u) {
-                    ra[u] = k.sv0[ps[u]];
-                    rb[u] = k.sv1[ps[u]];
-                    rx[u] = k.sv2[ps[u]];
-                    fx[u] = *reinterpret_cast<const float*>(reinterpret_cast<const char*>(k.fxs) + px[u].colb);
-                    fy[u] = *reinterpret_cast<const float*>(reinterpret_cast<const char*>(k.fys) + px[u].rowb);
-                }
-                PacketHit h[kPacketIlp];
-#pragma unroll
-                for (int u = 0; u < kPacketIlp; ++u) {
-#if SRT_FAST_DIV && SRT_PACKET_FLAT
-                    h[u] = EvalPacketFast(ra[u], rb[u], rx[u], fx[u], fy[u], px[u], vol_slow[u]);
-#else
-                    (void)vol_slow[u];
-                    h[u] = EvalPacket(ra[u], rb[u], rx[u], fx[u], fy[u], px[u]);
-#endif
-                }
-#if SRT_PIN_LOADS
-                // Keys built before the hit branches: the record id is loaded with the rest of
-                // the record instead of by a separate LDS read (and full wait) inside the branch.
-#pragma unroll
-                for (int u = 0; u < kPacketIlp; ++u) {
-                    asm volatile("" ::"v"(h[u].key));
-                }
-#endif
-#pragma unroll
-                for (int u = 0; u < kPacketIlp; ++u) {
-#ifdef SRT_DIAG
-                    if (p.exp & 32u) {
-                        continue;
-                    }
-#endif
-                    if (h[u].hit) {
-                        __hip_atomic_fetch_min(reinterpret_cast<unsigned long long*>(
-                                                   reinterpret_cast<char*>(keys) + h[u].addr),
-                                               h[u].key, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_WORKGROUP);
-                    }
+            for (int u = 0; u < kPacketIlp; ++u) {
+                if (h[u].hit) {
+                    __hip_atomic_fetch_min(reinterpret_cast<unsigned long long*>(keys + px[u].pixb), h[u].key,
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
             }
         }
-        __syncthreads();  // batch storage reused; after the last batch: keys complete
-#ifdef SRT_DIAG
-        {
-            const unsigned long long now = __builtin_amdgcn_s_memtime();
-            d_walk += now - d_mark;
-            d_mark = now;
-        }
-#endif
     }
-#ifdef SRT_DIAG
-    const unsigned blk = blockIdx.y * gridDim.x + blockIdx.x;
-    if (tid == 0 && blk < kDiagBlocks) {
-        unsigned long long* d = g_srt_diag[blk];
-        d[0] = 0;
-        d[1] = d_gather;
-        d[2] = d_walk;
-        d[3] = d_surv;
-        d[4] = d_pk;
-        d[5] = d_batches;
-        d[6] = __builtin_amdgcn_s_memtime() - d_t0;
-        d[7] = 1 | 2 | 4 | 8 | (static_cast<unsigned long long>(src.count1) << 16) |
-               (static_cast<unsigned long long>(src.end - src.count1) << 40);
-    }
-#endif
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const unsigned long long key = sh.keys[wave * R + r][lane];
-        if (key != ~0ull) {
-            s.bt[r] = __uint_as_float(static_cast<unsigned>(key >> 32));
-            s.bi[r] = static_cast<int>(static_cast<unsigned>(key));
-        }
-    }
+    __syncthreads();  // batch storage reused
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1760,11 +1211,12 @@ struct BinParams {
     unsigned* __restrict__ counts;      // tiles + 1 (the last one: large list)
     unsigned* __restrict__ lists;       // tiles x capacity
     unsigned* __restrict__ large_list;  // n_pad
-    unsigned* __restrict__ tile_order;  // tiles: trace block -> tile (TileOrderKernel)
-    unsigned* __restrict__ sync;        // [0] bin blocks done (self-resetting)
+    uint4* __restrict__ work;           // trace work list (TileOrderKernel): 2 x uint4 per item
+    unsigned* __restrict__ work_count;  // [0]: work items
+    unsigned* __restrict__ slice_base;  // per split tile: first key slice (TileOrderKernel)
     float2* __restrict__ bounds;        // tiles_x + tiles_y monotone tile column / row bounds (TileBoundsKernel)
-    unsigned order_in_bin;              // the bin kernel's last block computes the tile order
     unsigned capacity;
+    unsigned chunk;                     // candidates per trace work item (at least; TileOrderKernel)
     unsigned n;
     unsigned exp;  // diagnostic build: experiment bits (env SRT_EXP), 0 in the product
     int tiles_x;
@@ -1933,76 +1385,154 @@ __device__ __forceinline__ int LastLoAtMost(const float2* b, int n, float v) {
 // the block counts its (tile, record) pairs in an LDS histogram, reserves each touched
 // tile's share of its list with ONE global atomic, then writes the ids. (Per-pair global
 // atomics serialise on the busy tiles' counters at the memory side.)
-// Longest-processing-time-first launch order of the trace blocks: tiles sorted by their work,
-// descending (FULL-stream tiles first, then by the log2 of their candidate count), so the
-// heavy tiles start first and the light ones fill in behind them. One block; a counting sort
-// over 64 buckets (order within a bucket arbitrary: the frame does not depend on it).
+// Trace work list: one block after the bin kernel. A tile's candidates (its list plus the
+// large list) are cut into chunks of at most C, C = chunk x ceil(mean candidates per tile /
+// chunk), so no trace block walks more than C of them: a heavy tile becomes several work
+// items over the same pixels (merged by the last to finish, TraceCullKernel), while the
+// number of items stays <= 2 x tiles x parts, the trace grid. Items are listed longest first
+// (counting sort by the log2 of candidates per item, FULL-stream tiles first), so the heavy
+// ones start first and the light ones fill in behind them. Split tiles get consecutive key
+// slices (slice_base, an exclusive scan over the tiles). Order within a bucket is arbitrary:
+// the frame does not depend on it.
+// Work item of the binned trace (TileOrderKernel), 32 B: w0 = (tile part, chunk | chunks << 16,
+// candidate range begin, end), w1 = (tile list length, sample offset x, y of the tile's first
+// ray, flags: 1 = every ray of the tile has that offset, 2 = FULL stream).
+constexpr unsigned kItemRegular = 1u;
+constexpr unsigned kItemFull = 2u;
 constexpr int kOrderThreads = 1024;
-// Counts written by device-scope atomics of the same kernel (the bin kernel's last block) need
-// device-scope loads; a later kernel (TileOrderKernel) reads them with plain loads.
-template <bool kSameKernel>
-__device__ __forceinline__ unsigned LoadCount(const unsigned* c) {
-    if constexpr (kSameKernel) {
-        return __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-        return *c;
-    }
-}
-template <bool kSameKernel>
-__device__ __forceinline__ unsigned TileWorkBucket(const BinParams& p, unsigned t, unsigned large) {
-    const unsigned cnt = LoadCount<kSameKernel>(&p.counts[t]);
-    if (p.tile_info[t].usable == 0u || cnt > p.capacity) {
-        return 63u;
-    }
-    const unsigned total = cnt + large;
-    return total == 0u ? 0u : 32u - __builtin_clz(total);
-}
-// One block of kThreads threads computes the whole order.
-template <bool kSameKernel, int kThreads>
-__device__ void TileOrderBlock(const BinParams& p) {
+constexpr int kOrderPer = kMaxBinTiles / kOrderThreads;  // tiles per thread
+__global__ __launch_bounds__(kOrderThreads) void TileOrderKernel(BinParams p) {
     __shared__ unsigned start[64];
+    __shared__ unsigned long long wsum[kOrderThreads / kWave];
+    __shared__ unsigned wscan[kOrderThreads / kWave];
     const int tid = threadIdx.x;
-    const unsigned nthreads = kThreads;  // == blockDim.x
+    const int lane = tid & (kWave - 1);
+    const int wave = tid / kWave;
     const unsigned tiles = static_cast<unsigned>(p.tiles_x * p.tiles_y);
-    const unsigned large = LoadCount<kSameKernel>(&p.counts[tiles]);
+    const unsigned large = p.counts[tiles];
     if (tid < 64) {
         start[tid] = 0u;
     }
-    // Buckets computed once (counts and tile info loaded once), kept in registers for the
-    // placement pass: kMaxBinTiles / blockDim.x tiles per thread at most.
-    constexpr int kPer = kMaxBinTiles / kThreads;
-    unsigned bucket[kPer];
+    // This thread's tiles t = tid + k * kOrderThreads: candidates (~0 = FULL stream); their
+    // sum in units of 64 candidates.
+    unsigned cand[kOrderPer], cnt[kOrderPer], ox[kOrderPer], oy[kOrderPer], reg[kOrderPer];
+    unsigned long long csum = 0ull;
 #pragma unroll
-    for (int k = 0; k < kPer; ++k) {
-        const unsigned t = tid + k * nthreads;
-        bucket[k] = t < tiles ? TileWorkBucket<kSameKernel>(p, t, large) : 0u;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < kPer; ++k) {
-        if (tid + k * nthreads < tiles) {
-            atomicAdd(&start[bucket[k]], static_cast<unsigned>(kParts));
-        }
-    }
-    __syncthreads();
-    unsigned first = 0u;  // tiles in heavier buckets
-    if (tid < 64) {
-        for (int b = 63; b > tid; --b) {
-            first += start[b];
-        }
-    }
-    __syncthreads();
-    if (tid < 64) {
-        start[tid] = first;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < kPer; ++k) {
-        const unsigned t = tid + k * nthreads;
+    for (int k = 0; k < kOrderPer; ++k) {
+        const unsigned t = tid + k * kOrderThreads;
+        cand[k] = 0u;
+        cnt[k] = 0u;
         if (t < tiles) {
-            const unsigned at = atomicAdd(&start[bucket[k]], static_cast<unsigned>(kParts));
-            for (int part = 0; part < kParts; ++part) {
-                p.tile_order[at + part] = t * kParts + part;  // trace work items (tile, part)
+            cnt[k] = p.counts[t];
+            const TileInfo ti = p.tile_info[t];
+            ox[k] = __float_as_uint(ti.ox);
+            oy[k] = __float_as_uint(ti.oy);
+            reg[k] = ti.regular;
+            const bool full = ti.usable == 0u || cnt[k] > p.capacity;
+            cand[k] = full ? ~0u : cnt[k] + large;
+            csum += full ? 0ull : (cnt[k] + large + 63u) / 64u;
+        }
+    }
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+        csum += __shfl_xor(csum, o);
+    }
+    if (lane == 0) {
+        wsum[wave] = csum;
+    }
+    __syncthreads();
+    // sum over tiles of ceil(candidates / 64): the 16 wave sums, one per lane, reduced
+    unsigned long long all = lane < kOrderThreads / kWave ? wsum[lane] : 0ull;
+#pragma unroll
+    for (int o = 1; o < kOrderThreads / kWave; o <<= 1) {
+        all += __shfl_xor(all, o);
+    }
+    // C = chunk x ceil(mean / chunk) >= mean candidates per tile, so sum_t ceil(c_t / C) <= 2 tiles.
+    const unsigned long long unit = static_cast<unsigned long long>(tiles) * (p.chunk / 64u);  // 64-candidate units
+    const unsigned long long per = (all + unit - 1ull) / unit;
+    const unsigned C = static_cast<unsigned>(min(p.chunk * (per < 1ull ? 1ull : per), 0x80000000ull));
+    // Chunks, bucket and items per tile; key slices for split tiles.
+    unsigned nch[kOrderPer], bucket[kOrderPer], items[kOrderPer];
+    unsigned slices = 0u;
+#pragma unroll
+    for (int k = 0; k < kOrderPer; ++k) {
+        const unsigned t = tid + k * kOrderThreads;
+        nch[k] = 1u;
+        bucket[k] = 0u;
+        items[k] = 0u;
+        if (t < tiles) {
+            const int rows_left = p.row_count - static_cast<int>(t / static_cast<unsigned>(p.tiles_x)) * kTileRows;
+            const unsigned parts = static_cast<unsigned>(min(kParts, (rows_left + kBlockRows - 1) / kBlockRows));
+            if (cand[k] == ~0u) {
+                bucket[k] = 63u;
+            } else if (cand[k] != 0u) {
+                nch[k] = cand[k] / C + (cand[k] % C != 0u ? 1u : 0u);
+                const unsigned w = cand[k] / nch[k] + (cand[k] % nch[k] != 0u ? 1u : 0u);
+                bucket[k] = 32u - __builtin_clz(w);
+            }
+            items[k] = nch[k] * parts;
+            slices += nch[k] > 1u ? nch[k] * kParts : 0u;
+        }
+    }
+    // Exclusive block scan of the slice counts (any order gives disjoint slices).
+    unsigned incl = slices;
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+        const unsigned u = __shfl_up(incl, o);
+        incl += lane >= o ? u : 0u;
+    }
+    if (lane == kWave - 1) {
+        wscan[wave] = incl;
+    }
+    __syncthreads();
+    unsigned wbase = lane < wave ? wscan[lane] : 0u;  // slices of the waves before this one
+#pragma unroll
+    for (int o = 1; o < kOrderThreads / kWave; o <<= 1) {
+        wbase += __shfl_xor(wbase, o);
+    }
+    unsigned base = wbase + incl - slices;
+#pragma unroll
+    for (int k = 0; k < kOrderPer; ++k) {
+        if (nch[k] > 1u) {
+            p.slice_base[tid + k * kOrderThreads] = base;
+            base += nch[k] * kParts;
+        }
+        if (items[k] != 0u) {
+            atomicAdd(&start[bucket[k]], items[k]);
+        }
+    }
+    __syncthreads();
+    if (wave == 0) {  // bucket b's first item: the items in heavier buckets (suffix sum, exclusive)
+        const unsigned c = start[lane];
+        unsigned suf = c;
+#pragma unroll
+        for (int o = 1; o < kWave; o <<= 1) {
+            const unsigned u = __shfl_down(suf, o);
+            suf += lane + o < kWave ? u : 0u;
+        }
+        start[lane] = suf - c;
+        if (lane == 0) {
+            p.work_count[0] = suf;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kOrderPer; ++k) {
+        if (items[k] != 0u) {
+            const unsigned t = tid + k * kOrderThreads;
+            const bool full = cand[k] == ~0u;
+            const unsigned flags = (full ? kItemFull : 0u) | (reg[k] != 0u ? kItemRegular : 0u);
+            const unsigned long long c_t = full ? 0ull : cand[k];
+            unsigned at = atomicAdd(&start[bucket[k]], items[k]);
+            const unsigned parts = items[k] / nch[k];
+            for (unsigned part = 0; part < parts; ++part) {
+                for (unsigned c = 0; c < nch[k]; ++c) {
+                    p.work[2 * at] = make_uint4(t * kParts + part, c | nch[k] << 16,
+                                                static_cast<unsigned>(c_t * c / nch[k]),
+                                                static_cast<unsigned>(c_t * (c + 1u) / nch[k]));
+                    p.work[2 * at + 1] = make_uint4(cnt[k], ox[k], oy[k], flags);
+                    ++at;
+                }
             }
         }
     }
@@ -2140,85 +1670,63 @@ __global__ __launch_bounds__(kBinThreads) void BinTrianglesKernel(BinParams p) {
             p.lists[static_cast<size_t>(t) * p.capacity + at] = i;
         }
     }
-    // The last block to finish computes the trace launch order from the final list counts.
-    // Every count update of a block is an atomic whose returned value the block consumed
-    // before this barrier, so it has been performed at the device coherence point; the last
-    // block reads the counts with device-scope atomic loads (no L2-wide fences needed).
-    __shared__ unsigned last;
-    if (p.order_in_bin == 0u) {
-        return;
-    }
-    __syncthreads();
-    if (tid == 0) {
-        last = atomicAdd(&p.sync[0], 1u) == gridDim.x - 1u ? 1u : 0u;
-    }
-    __syncthreads();
-    if (last != 0u) {
-        TileOrderBlock<true, kBinThreads>(p);
-        if (tid == 0) {
-            p.sync[0] = 0u;  // ready for the next frame (the kernel boundary orders it)
-        }
-    }
-}
-
-// Standalone order (a band with no records: the bin kernel, which normally computes the
-// order in its last block, is not launched).
-__global__ __launch_bounds__(kOrderThreads) void TileOrderKernel(BinParams p) {
-    TileOrderBlock<false, kOrderThreads>(p);
-}
-
-// Candidate source of a tile: LIST (binned, usable box, list complete): the tile's list then
-// the large list; FULL (no bins, an unusable tile box, or an overflowed list): every record.
-__device__ __forceinline__ CullSource TileSource(const TraceParams& p, const TileInfo& ti, unsigned tile) {
-    CullSource src{nullptr, nullptr, 0u, 0u, 0u, 0u, p.n_pad / kStreamStep};
-    if (p.tile_info == nullptr) {
-        return src;
-    }
-    const unsigned cnt = p.bin_counts[tile];
-    if (ti.usable != 0u && cnt <= p.bin_capacity) {
-        src.list = p.bin_lists + static_cast<size_t>(tile) * p.bin_capacity;
-        src.list2 = p.large_list;
-        src.count1 = cnt;
-        src.end = cnt + p.bin_counts[p.tiles];
-    }
-    return src;
-}
-
-// Rays of a regular tile (every offset equal to (ox, oy), bit for bit): GenerateRays'
-// expressions without reading the offsets.
-template <int R>
-__device__ __forceinline__ void UniformRays(const TraceParams& p, int x, int y_in_block, float ox, float fy_rows,
-                                            Rays<R>& s, Box& box) {
-    const int xc = min(x, p.width - 1);
-    const float fx = (static_cast<float>(xc) + ox) / p.wf;
-    box = Box{__builtin_inff(), -__builtin_inff(), __builtin_inff(), -__builtin_inff()};
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        s.fx[r] = fx;
-        // Row r's fy is wave-uniform: lane (y0 - row0) + r of fy_rows computed it (the same
-        // expression, (float(row_begin + yc) + oy) / hf), one division per lane instead of R.
-        s.fy[r] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(fy_rows), y_in_block + r));
-        s.bt[r] = __builtin_inff();
-        s.bi[r] = -1;
-        box.xlo = fminf(box.xlo, s.fx[r]);
-        box.xhi = fmaxf(box.xhi, s.fx[r]);
-        box.ylo = fminf(box.ylo, s.fy[r]);
-        box.yhi = fmaxf(box.yhi, s.fy[r]);
-    }
 }
 
 #ifndef SRT_TRACE_OCC
-#define SRT_TRACE_OCC 4
+#define SRT_TRACE_OCC 5
 #endif
-template <int W>
-__global__ __launch_bounds__(kWave * W, SRT_TRACE_OCC) void TraceCullKernel(TraceParams p) {
-    using S = CullShape<W>;
-    constexpr int R = S::kR;
-    __shared__ CullShared<W> sh;
-    // Block = one part (kBlockRows rows) of a cull tile (kTileRows rows); launched in the
-    // tile order's work order when the frame is binned.
-    const unsigned linear = blockIdx.y * gridDim.x + blockIdx.x;
-    const unsigned item = p.tile_order != nullptr ? p.tile_order[linear] : linear;
+
+__global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(TraceParams p) {
+    constexpr int R = kCullR;
+    __shared__ CullShared sh;
+#ifdef SRT_DIAG
+    const unsigned long long d_rt0 = __builtin_amdgcn_s_memrealtime();
+    const unsigned d_blk = blockIdx.y * gridDim.x + blockIdx.x;
+    unsigned long long d_gather = 0, d_walk = 0, d_batches = 0, d_cand = 0;
+    unsigned long long d_mark = __builtin_amdgcn_s_memtime();
+    auto diag_end = [&](unsigned it, unsigned ch, unsigned nch, unsigned last, unsigned full) {
+        if (threadIdx.x == 0 && d_blk < kDiagBlocks) {
+            unsigned long long* d = g_srt_diag[d_blk];
+            d[1] = d_gather;
+            d[2] = d_walk;
+            d[5] = d_batches;
+            d[7] = (full ? 0ull : 8ull) | d_cand << 40;
+            d[8] = d_rt0;
+            d[9] = __builtin_amdgcn_s_memrealtime();
+            d[10] = it;
+            d[11] = ch | nch << 16 | static_cast<unsigned long long>(last) << 32;
+        }
+    };
+#define SRT_DIAG_END(it, ch, nch, last, full) diag_end(it, ch, nch, last, full)
+#else
+#define SRT_DIAG_END(it, ch, nch, last, full)
+#endif
+    // Block = one part (kBlockRows rows) of a cull tile. Binned: work item blockIdx.x of the
+    // tile order's list (a part, or one candidate chunk of a split part; the grid is sized for
+    // the longest list and the blocks past its end exit). Unbinned: part (x, y), FULL stream.
+    unsigned item, chunk = 0u, nchunks = 1u, flags = kItemFull;
+    float ox = 0.f, oy = 0.f;
+    CullSource src{nullptr, nullptr, 0u, 0u, 0u, true};
+    if (p.work != nullptr) {
+        if (blockIdx.x >= p.work_count[0]) {
+            return;
+        }
+        const uint4 w0 = p.work[2 * blockIdx.x], w1 = p.work[2 * blockIdx.x + 1];
+        item = w0.x;
+        chunk = w0.y & 0xFFFFu;
+        nchunks = w0.y >> 16;
+        flags = w1.w;
+        ox = __uint_as_float(w1.y);
+        oy = __uint_as_float(w1.z);
+        src.list = p.bin_lists + static_cast<size_t>(item / kParts) * p.bin_capacity;
+        src.list2 = p.large_list;
+        src.count1 = w1.x;
+        src.begin = w0.z;
+        src.end = w0.w;
+        src.full = (flags & kItemFull) != 0u;
+    } else {
+        item = blockIdx.y * gridDim.x + blockIdx.x;
+    }
     const unsigned tile = item / kParts;
     const int tx = static_cast<int>(tile % static_cast<unsigned>(p.tiles_x));
     const int ty = static_cast<int>(tile / static_cast<unsigned>(p.tiles_x));
@@ -2226,103 +1734,236 @@ __global__ __launch_bounds__(kWave * W, SRT_TRACE_OCC) void TraceCullKernel(Trac
     if (row0 >= p.row_count) {
         return;  // the last tile row's empty part
     }
-    const bool binned = p.tile_info != nullptr;
-    TileInfo ti{};
-    if (binned) {
-        ti = p.tile_info[tile];
-    }
-    const CullSource src = TileSource(p, ti, tile);
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
     const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);
+    // LIST: the first batch's records are requested before the rays are set up (its loads
+    // are the block's longest dependency chain: list entry, then the 64-B record).
+    const unsigned total = src.end - src.begin;
+    CullRecord nxt[kSlices];
+    auto load_list = [&](unsigned b0) {
+#pragma unroll
+        for (int e = 0; e < kSlices; ++e) {
+            const unsigned v = b0 + e * kCullThreads + tid;
+            const unsigned vv = src.begin + (v < total ? v : 0u);
+            nxt[e] = p.cull[vv < src.count1 ? src.list[vv] : src.list2[vv - src.count1]];
+        }
+    };
+    if (!src.full && total != 0u) {
+        load_list(0u);
+    }
+    // Rays: lane = column x; rows y0 .. y0 + R - 1. A regular tile (every ray with the sample
+    // offset (ox, oy)) computes them without reading the offsets: fx per lane, and row r's fy
+    // from lane (wave R + r) of fy_lane (the GenerateRays expressions, bit for bit).
     const int x = tx * kWave + lane;
     const int y0 = row0 + wave * R;
+    const bool regular = (flags & kItemRegular) != 0u;
+    float fy_lane = __builtin_nanf("");
     Rays<R> s;
     Box lane_box;
-    bool same = true;
-    // Raster walks: lane = column (fx), lanes 0..kBlockRows-1 carry the block's rows' fy (the
-    // GenerateRays expression; bit-identical since every ray has the same offset).
-    float fy_lane = __builtin_nanf("");
-    const bool uniform_rays = binned && ti.regular != 0u;
-    if (uniform_rays) {
+    if (regular) {
         if (lane < kBlockRows) {
             const int yc = min(row0 + lane, p.row_count - 1);
-            fy_lane = (static_cast<float>(p.row_begin + yc) + ti.oy) / p.hf;
+            fy_lane = (static_cast<float>(p.row_begin + yc) + oy) / p.hf;
         }
-        UniformRays<R>(p, x, wave * R, ti.ox, fy_lane, s, lane_box);
-    } else {
-        same = GenerateRays<R>(p, x, y0, s, lane_box);
-    }
-    const Box wb = WaveReduceBox(lane_box);
-    // Raster walk eligibility: every ray of the block has the tile's first sample offset (bit
-    // pattern), so fx depends on the column only and fy on the row only.
-    bool regular = true;
-    float oy0;
-    if (binned) {
-        regular = ti.regular != 0u;
-        oy0 = ti.oy;
-    } else {
-        const int x0 = min(tx * kWave, p.width - 1);
-        const float2 o0 = p.offsets[static_cast<size_t>(row0) * p.width + x0];
-        oy0 = o0.y;
         const int xc = min(x, p.width - 1);
+        const float fx = (static_cast<float>(xc) + ox) / p.wf;
+        lane_box = Box{fx, fx, __builtin_inff(), -__builtin_inff()};
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            const int yc = min(y0 + r, p.row_count - 1);
-            const float2 o = p.offsets[static_cast<size_t>(yc) * p.width + xc];
-            regular = regular && __float_as_uint(o.x) == __float_as_uint(o0.x) &&
-                      __float_as_uint(o.y) == __float_as_uint(o0.y);
+            s.fx[r] = fx;
+            s.fy[r] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(fy_lane), wave * R + r));
+            lane_box.ylo = fminf(lane_box.ylo, s.fy[r]);
+            lane_box.yhi = fmaxf(lane_box.yhi, s.fy[r]);
         }
+        lane_box.xlo = fx != fx ? __builtin_inff() : fx;  // NaN positions drop out of the box
+        lane_box.xhi = fx != fx ? -__builtin_inff() : fx;
+    } else {
+        GenerateRays<R>(p, x, y0, s, lane_box);
     }
-    if (tid == 0) {
-        sh.shared_fx = 1u;
-        sh.regular = 1u;
-    }
-    __syncthreads();
+    const Box wb = WaveReduceBox(lane_box);
     if (lane == 0) {
         sh.wave_box[wave] = wb;
-    }
-    if (!__all(same) && lane == 0) {
-        sh.shared_fx = 0u;
-    }
-    if (!__all(regular) && lane == 0) {
-        sh.regular = 0u;
     }
     __syncthreads();
     Box bb = sh.wave_box[0];  // the block's ray box
 #pragma unroll
-    for (int w = 1; w < W; ++w) {
+    for (int w = 1; w < kCullWaves; ++w) {
         const Box o = sh.wave_box[w];
         bb = Box{fminf(bb.xlo, o.xlo), fmaxf(bb.xhi, o.xhi), fminf(bb.ylo, o.ylo), fmaxf(bb.yhi, o.yhi)};
     }
-    const bool list = src.list != nullptr;
-    const bool raster = sh.regular != 0u && p.allow_raster != 0;
-    const bool shared_fx = sh.shared_fx != 0u;
-    const float fx_lane = s.fx[0];
-    if (!uniform_rays && lane < kBlockRows) {
-        const int yc = min(row0 + lane, p.row_count - 1);
-        fy_lane = (static_cast<float>(p.row_begin + yc) + oy0) / p.hf;
+    const int nc = min(kWave, p.width - tx * kWave), nr = min(kBlockRows, p.row_count - row0);
+    PacketTables(sh, s, regular, s.fx[0], fy_lane, nc, nr);
+    for (int i = tid; i < kBlockRows * kWave; i += kCullThreads) {
+        (&sh.keys[0][0])[i] = ~0ull;
     }
-    if (raster) {
-        if (list) {
-            PacketWalk<W>(p, sh, s, bb, fx_lane, fy_lane, src, tx, row0);
-        } else {
-            CullWalk<W, true, true, false>(p, sh, s, bb, wb, fx_lane, fy_lane, src, tile);
+    const PacketFrame pf = MakePacketFrame(sh, nc, nr, ScreenBoxUsable(bb));
+    __syncthreads();  // keys initialised
+#ifdef SRT_DIAG
+    {
+        const unsigned long long now = __builtin_amdgcn_s_memtime();
+        d_gather += now - d_mark;
+        d_mark = now;
+    }
+#endif
+    if (!src.full) {
+        // LIST: candidates [begin, end) of the tile's virtual list, one batch ahead.
+#pragma unroll 1
+        for (unsigned b0 = 0; b0 < total; b0 += kPacketBatch) {
+            CullRecord cr[kSlices];
+            bool valid[kSlices];
+#pragma unroll
+            for (int e = 0; e < kSlices; ++e) {
+                cr[e] = nxt[e];
+                valid[e] = b0 + e * kCullThreads + tid < total;
+            }
+            PacketBatch(sh, bb, pf, cr, valid, [&] {
+                if (b0 + kPacketBatch < total) {
+                    load_list(b0 + kPacketBatch);
+                }
+            });
+#ifdef SRT_DIAG
+            ++d_batches;
+#endif
         }
-    } else if (shared_fx) {
-        if (list) {
-            CullWalk<W, true, false, true>(p, sh, s, bb, wb, fx_lane, fy_lane, src, tile);
-        } else {
-            CullWalk<W, true, false, false>(p, sh, s, bb, wb, fx_lane, fy_lane, src, tile);
-        }
+#ifdef SRT_DIAG
+        d_cand = total;
+#endif
     } else {
-        if (list) {
-            CullWalk<W, false, false, true>(p, sh, s, bb, wb, fx_lane, fy_lane, src, tile);
-        } else {
-            CullWalk<W, false, false, false>(p, sh, s, bb, wb, fx_lane, fy_lane, src, tile);
+        // FULL: stream every record's quantized screen box (one per thread per step, loaded one
+        // step ahead); the ones overlapping the block box join an LDS id list, which is walked
+        // in packet batches whenever it holds a batch (and at the end).
+        const bool block_sb = pf.use_sb;
+        const QBox bq = Quantize(bb);
+        const unsigned long long lt_mask = (1ull << lane) - 1ull;
+        const unsigned nsteps = p.n_pad / kStreamStep;
+        uint2 nq = p.qboxes[tid];
+        unsigned listed = 0u;  // ids in the list (block-uniform)
+#pragma unroll 1
+        for (unsigned k = 0; k < nsteps; ++k) {
+            const uint2 q = nq;
+            if (k + 1 < nsteps) {
+                nq = p.qboxes[(k + 1) * kStreamStep + tid];
+            }
+            // Disabled records carry empty boxes; unbounded ones span the int16 range.
+            const bool pass = !block_sb || QBoxOverlaps(bq, q.x, q.y);
+            const unsigned long long m = __ballot(pass);
+            const unsigned ph = k & 1u;
+            if (lane == 0) {
+                sh.counts[ph][wave] = __popcll(m);
+            }
+            __syncthreads();
+            unsigned off = listed, step_n = 0u;
+#pragma unroll
+            for (int w = 0; w < kCullWaves; ++w) {
+                const unsigned cw = sh.counts[ph][w];
+                off += w < wave ? cw : 0u;
+                step_n += cw;
+            }
+            if (pass) {
+                sh.ids[off + __popcll(m & lt_mask)] = k * kStreamStep + tid;
+            }
+            listed += step_n;
+            if (listed < kPacketBatch && k + 1 < nsteps) {  // block-uniform
+                continue;
+            }
+            __syncthreads();  // every wave's ids are in the list
+            // The list shares LDS with the survivor planes: every id this thread walks is read
+            // into registers before the first batch writes them.
+            unsigned my_ids[kFlushBatches][kSlices];
+#pragma unroll
+            for (int bi = 0; bi < kFlushBatches; ++bi) {
+#pragma unroll
+                for (int e = 0; e < kSlices; ++e) {
+                    const unsigned v = bi * kPacketBatch + e * kCullThreads + tid;
+                    my_ids[bi][e] = v < listed ? sh.ids[v] : 0u;
+                }
+            }
+#pragma unroll
+            for (int bi = 0; bi < kFlushBatches; ++bi) {
+                const unsigned b0 = bi * kPacketBatch;
+                if (b0 >= listed) {  // block-uniform
+                    break;
+                }
+                CullRecord cr[kSlices];
+                bool valid[kSlices];
+#pragma unroll
+                for (int e = 0; e < kSlices; ++e) {
+                    valid[e] = b0 + e * kCullThreads + tid < listed;
+                    cr[e] = LoadCullById(p, my_ids[bi][e]);
+                }
+                PacketBatch(sh, bb, pf, cr, valid, [] {});
+#ifdef SRT_DIAG
+                ++d_batches;
+                d_cand += min(listed - b0, static_cast<unsigned>(kPacketBatch));
+#endif
+            }
+            listed = 0u;
         }
     }
-    ShadeAndStore<R>(p, x, y0, s);
+#ifdef SRT_DIAG
+    d_walk = __builtin_amdgcn_s_memtime() - d_mark;
+#endif
+    unsigned long long key[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        key[r] = sh.keys[wave * R + r][lane];
+    }
+    if (nchunks > 1u) {
+        // Split part: publish this chunk's keys (write-through sc1 stores), count the arrival;
+        // the last of the part's chunks takes the minimum over every chunk's keys (sc1 loads)
+        // and shades. Hand-off form: MI355X_MICROARCH.md "Valid forms", table row 1 (sc1
+        // stores, every storing wave's vmcnt(0), barrier, one agent-scope add; the last
+        // adder's block loads sc1 after a barrier).
+        constexpr int kPix = kBlockRows * kWave;
+        unsigned long long* slices =
+            p.split_keys + static_cast<size_t>(p.slice_base[tile] + (item % kParts) * nchunks) * kPix;
+        const int pix = wave * R * kWave + lane;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            __hip_atomic_store(slices + static_cast<size_t>(chunk) * kPix + pix + r * kWave, key[r], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+            const unsigned before = __hip_atomic_fetch_add(&p.arrive[item], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned last = before == nchunks - 1u ? 1u : 0u;
+            if (last != 0u) {  // every chunk has arrived: reset for the next frame
+                __hip_atomic_store(&p.arrive[item], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            sh.last = last;
+        }
+        __syncthreads();
+        if (sh.last == 0u) {
+            SRT_DIAG_END(item, chunk, nchunks, 0u, src.full);
+            return;
+        }
+        for (unsigned c = 0; c < nchunks; ++c) {
+            if (c == chunk) {
+                continue;
+            }
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const unsigned long long o = __hip_atomic_load(slices + static_cast<size_t>(c) * kPix + pix + r * kWave,
+                                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                key[r] = o < key[r] ? o : key[r];
+            }
+        }
+    }
+    if (x < p.width) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int y = y0 + r;
+            if (y < p.row_count) {
+                const float2 f = sh.fxy[wave * R + r][lane];
+                const int id = key[r] != ~0ull ? static_cast<int>(static_cast<unsigned>(key[r])) : -1;
+                StorePixel(p, x, y, f.x, f.y, id);
+            }
+        }
+    }
+    SRT_DIAG_END(item, chunk, nchunks, 1u, src.full);
+#undef SRT_DIAG_END
 }
 
 // ---------------------------------------------------------------------------------------
@@ -2587,13 +2228,12 @@ bool EnvFlag(const char* name, bool dflt) {
     return v == nullptr || *v == '\0' ? dflt : std::strcmp(v, "0") != 0;
 }
 
-// Waves per trace block; env SRT_CULL_WAVES = 4, 8 or 16 (default 4), for measurement.
-int CullWavesFromEnv() {
-    const char* v = std::getenv("SRT_CULL_WAVES");
-    if (v != nullptr && (std::strcmp(v, "8") == 0 || std::strcmp(v, "16") == 0)) {
-        return std::atoi(v);
-    }
-    return 4;
+// Candidates per trace work item (TileOrderKernel's smallest chunk); env SRT_CULL_CHUNK, a
+// multiple of 64 (default 256: one packet-walk batch).
+unsigned CullChunkFromEnv() {
+    const char* v = std::getenv("SRT_CULL_CHUNK");
+    const long c = v == nullptr || *v == '\0' ? 256 : std::strtol(v, nullptr, 10);
+    return c < 64 ? 64u : static_cast<unsigned>((c + 63) / 64 * 64);
 }
 
 // ML_FLOAT16 images: 4 elements per thread (8-B half / 16-B float vectors), scalar tail.
@@ -2639,16 +2279,39 @@ hipError_t DiagRead(void* host, std::size_t bytes) {
 #endif
 
 namespace {
+// Carve-up of a scene's edge allocation (render.h kEdgeFloatsPerTriangle): tile-planar edge
+// records, screen boxes, quantized boxes, cull records, shading normals.
+struct EdgeLayout {
+    float4* tiles;
+    float4* screen_boxes;
+    uint2* qboxes;
+    CullRecord* cull;
+    float4* normals;
+};
+EdgeLayout EdgeBuffers(const float* d_edges, std::uint64_t n) {
+    EdgeLayout e;
+    const std::uint64_t n_pad = PaddedTriangleCount(n);
+    e.tiles = reinterpret_cast<float4*>(const_cast<float*>(d_edges));
+    e.screen_boxes = e.tiles + n_pad / kTileTriangles * kTileFloat4;
+    e.qboxes = reinterpret_cast<uint2*>(e.screen_boxes + n_pad);
+    e.cull = reinterpret_cast<CullRecord*>(e.qboxes + n_pad);
+    e.normals = reinterpret_cast<float4*>(e.cull + n_pad);
+    return e;
+}
+}  // namespace
+
+namespace {
 PrepareParams MakePrepareParams(const float* d_vertices, const unsigned* d_rank, std::uint64_t n, const Frame& frame,
                                 float* d_edges) {
     PrepareParams p{};
     p.vertices = d_vertices;
     p.rank = d_rank;
-    p.edges = reinterpret_cast<float4*>(d_edges);
-    p.screen_boxes = reinterpret_cast<float4*>(d_edges) + PaddedTriangleCount(n) / kTileTriangles * kTileFloat4;
-    p.qboxes = reinterpret_cast<uint2*>(p.screen_boxes + PaddedTriangleCount(n));
-    p.cull = reinterpret_cast<CullRecord*>(p.qboxes + PaddedTriangleCount(n));
-    p.normals = reinterpret_cast<float4*>(p.cull + PaddedTriangleCount(n));
+    const EdgeLayout e = EdgeBuffers(d_edges, n);
+    p.edges = e.tiles;
+    p.screen_boxes = e.screen_boxes;
+    p.qboxes = e.qboxes;
+    p.cull = e.cull;
+    p.normals = e.normals;
     p.n = static_cast<unsigned>(n);
     p.n_pad = static_cast<unsigned>(PaddedTriangleCount(n));
     for (int k = 0; k < 3; ++k) {
@@ -2746,8 +2409,11 @@ unsigned CullBinCapacity(std::uint64_t n, std::size_t tiles) {
 }
 
 namespace {
+// Trace work items of a band: at most 2 x (tiles x parts) (TileOrderKernel's chunk choice).
+std::size_t CullBudget(std::size_t tiles) { return 2 * tiles * kParts; }
+
 struct BinSizes {
-    std::size_t info, counts, lists, large, order, sync, bounds;
+    std::size_t info, counts, lists, large, work, work_count, slice_base, arrive, split_keys, bounds;
 };
 BinSizes CullBinSizes(std::uint64_t n, std::size_t width, std::size_t row_count) {
     const std::size_t tx = (width + kWave - 1) / kWave, ty = (row_count + kTileRows - 1) / kTileRows;
@@ -2758,8 +2424,11 @@ BinSizes CullBinSizes(std::uint64_t n, std::size_t width, std::size_t row_count)
     z.counts = al((tiles + 1) * 4);
     z.lists = al(tiles * static_cast<std::size_t>(CullBinCapacity(n, tiles)) * 4);
     z.large = al(PaddedTriangleCount(n) * 4);
-    z.order = al(tiles * kParts * 4);
-    z.sync = al(4);
+    z.work = al(CullBudget(tiles) * 2 * sizeof(uint4));
+    z.work_count = al(4);
+    z.slice_base = al(tiles * 4);
+    z.arrive = al(tiles * kParts * 4);
+    z.split_keys = al(CullBudget(tiles) * kBlockRows * kWave * 8);
     z.bounds = al((tx + ty) * 8);
     return z;
 }
@@ -2767,26 +2436,29 @@ BinSizes CullBinSizes(std::uint64_t n, std::size_t width, std::size_t row_count)
 
 std::size_t CullBinBytes(std::uint64_t n, std::size_t width, std::size_t row_count) {
     const BinSizes z = CullBinSizes(n, width, row_count);
-    return z.info + z.counts + z.lists + z.large + z.order + z.sync + z.bounds;
+    return z.info + z.counts + z.lists + z.large + z.work + z.work_count + z.slice_base + z.arrive + z.split_keys +
+           z.bounds;
 }
 
 CullBins CullBinLayout(void* base, std::uint64_t n, std::size_t width, std::size_t row_count) {
     const BinSizes z = CullBinSizes(n, width, row_count);
     unsigned char* w = static_cast<unsigned char*>(base);
     CullBins b{};
-    b.tile_info = w;
-    w += z.info;
-    b.counts = reinterpret_cast<unsigned*>(w);
-    w += z.counts;
-    b.lists = reinterpret_cast<unsigned*>(w);
-    w += z.lists;
-    b.large_list = reinterpret_cast<unsigned*>(w);
-    w += z.large;
-    b.tile_order = reinterpret_cast<unsigned*>(w);
-    w += z.order;
-    b.sync = reinterpret_cast<unsigned*>(w);
-    w += z.sync;
-    b.bounds = w;
+    auto take = [&w](std::size_t bytes) {
+        unsigned char* at = w;
+        w += bytes;
+        return at;
+    };
+    b.tile_info = take(z.info);
+    b.counts = reinterpret_cast<unsigned*>(take(z.counts));
+    b.lists = reinterpret_cast<unsigned*>(take(z.lists));
+    b.large_list = reinterpret_cast<unsigned*>(take(z.large));
+    b.work = take(z.work);
+    b.work_count = reinterpret_cast<unsigned*>(take(z.work_count));
+    b.slice_base = reinterpret_cast<unsigned*>(take(z.slice_base));
+    b.arrive = reinterpret_cast<unsigned*>(take(z.arrive));
+    b.split_keys = take(z.split_keys);
+    b.bounds = take(z.bounds);
     b.tiles = CullTiles(width, row_count);
     b.capacity = CullBinCapacity(n, b.tiles);
     return b;
@@ -2810,24 +2482,22 @@ hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_ver
         }
     }
     TraceParams p{};
-    p.edges = reinterpret_cast<const float4*>(d_edges);
-    p.screen_boxes = reinterpret_cast<const float4*>(d_edges) + PaddedTriangleCount(n) / kTileTriangles * kTileFloat4;
-    p.qboxes = reinterpret_cast<const uint2*>(p.screen_boxes + PaddedTriangleCount(n));
-    p.cull = reinterpret_cast<const CullRecord*>(p.qboxes + PaddedTriangleCount(n));
-    p.normals = reinterpret_cast<const float4*>(p.cull + PaddedTriangleCount(n));
+    const EdgeLayout e = EdgeBuffers(d_edges, n);
+    p.edges = e.tiles;
+    p.screen_boxes = e.screen_boxes;
+    p.qboxes = e.qboxes;
+    p.cull = e.cull;
+    p.normals = e.normals;
     p.vertices = d_vertices;
     p.albedo = d_albedo;
     p.offsets = reinterpret_cast<const float2*>(band.offsets);
     p.out = reinterpret_cast<float4*>(band.rgba);
+    p.out_ids = band.ids;
     p.n_pad = static_cast<unsigned>(PaddedTriangleCount(n));
     p.n_tiles = static_cast<unsigned>(n == 0 ? 1 : (n + kTileTriangles - 1) / kTileTriangles);
     p.width = static_cast<int>(band.width);
     p.row_count = static_cast<int>(band.row_count);
     p.row_begin = static_cast<int>(band.row_begin);
-    {
-        const char* r = std::getenv("SRT_CULL_RASTER");
-        p.allow_raster = (r != nullptr && std::strcmp(r, "0") == 0) ? 0 : 1;
-    }
     p.wf = static_cast<float>(band.width);
     p.hf = static_cast<float>(band.height);
     for (int k = 0; k < 3; ++k) {
@@ -2881,8 +2551,9 @@ hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_ver
             b.counts = bins->counts;
             b.lists = bins->lists;
             b.large_list = bins->large_list;
-            b.tile_order = bins->tile_order;
-            b.sync = bins->sync;
+            b.work = static_cast<uint4*>(bins->work);
+            b.work_count = bins->work_count;
+            b.slice_base = bins->slice_base;
             // Tile bounds once per frame (TileBoundsKernel) when the bin blocks' own reductions
             // would cost more: (bin blocks) x (tiles) tile-info reads above 200k (C5: 16M, bin
             // stage 164 -> 75 us; C3: 0.4M, where the extra launch adds ~1 % to one frame's
@@ -2895,6 +2566,7 @@ hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_ver
                 b.bounds = once ? static_cast<float2*>(bins->bounds) : nullptr;
             }
             b.capacity = bins->capacity;
+            b.chunk = CullChunkFromEnv();
             b.n = static_cast<unsigned>(n);
             b.tiles_x = static_cast<int>(gx);
             b.tiles_y = static_cast<int>(gy);
@@ -2919,23 +2591,23 @@ hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_ver
             } else {
                 Launch(TileInfoKernel, dim3(gx, gy), dim3(kBinThreads), stream, ev.prep_begin, ev.prep_end, b);
             }
-            b.order_in_bin = n != 0 && EnvFlag("SRT_ORDER_IN_BIN", false) ? 1u : 0u;
             if (n != 0 && b.bounds != nullptr) {
                 Launch(TileBoundsKernel, dim3(1), dim3(1024), stream, ev.bin_begin, nullptr, b);
             }
             if (n != 0) {
                 const unsigned blocks = static_cast<unsigned>((n + kBinThreads - 1) / kBinThreads);
                 Launch(BinTrianglesKernel, dim3(blocks), dim3(kBinThreads), stream,
-                       b.bounds != nullptr ? nullptr : ev.bin_begin,
-                       b.order_in_bin != 0u ? ev.bin_end : nullptr, b);
+                       b.bounds != nullptr ? nullptr : ev.bin_begin, nullptr, b);
             }
-            if (b.order_in_bin == 0u) {
-                Launch(TileOrderKernel, dim3(1), dim3(kOrderThreads), stream, n != 0 ? nullptr : ev.bin_begin,
-                       ev.bin_end, b);
-            }
+            Launch(TileOrderKernel, dim3(1), dim3(kOrderThreads), stream, n != 0 ? nullptr : ev.bin_begin,
+                   ev.bin_end, b);
             p.tile_info = b.tile_info;
             p.order = bins->order;
-            p.tile_order = bins->tile_order;
+            p.work = b.work;
+            p.work_count = b.work_count;
+            p.slice_base = b.slice_base;
+            p.split_keys = static_cast<unsigned long long*>(bins->split_keys);
+            p.arrive = bins->arrive;
             p.bin_lists = bins->lists;
             p.bin_counts = bins->counts;
             p.large_list = bins->large_list;
@@ -2943,27 +2615,52 @@ hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_ver
         }
         p.tiles_x = static_cast<int>(gx);
         p.tiles = gx * gy;
-        // One block per (tile, part): gridDim.x = tile columns, gridDim.y = tile rows x parts.
-        const dim3 grid(gx, gy * kParts);
-        const int waves = CullWavesFromEnv();
-        if constexpr (CullWavesOk(16)) {
-            if (waves == 16) {
-                Launch(TraceCullKernel<16>, grid, dim3(kWave * 16), stream, ev.begin, ev.end, p);
-                return hipGetLastError();
-            }
+        if (p.work != nullptr) {
+            // Binned: one block per work item of TileOrderKernel's list (at most the budget).
+            Launch(TraceCullKernel, dim3(static_cast<unsigned>(CullBudget(p.tiles))),
+                   dim3(kWave * kCullWaves), stream, ev.begin, ev.end, p);
+        } else {
+            // One block per (tile, part): gridDim.x = tile columns, gridDim.y = tile rows x parts.
+            Launch(TraceCullKernel, dim3(gx, gy * kParts), dim3(kWave * kCullWaves), stream, ev.begin,
+                   ev.end, p);
         }
-        if constexpr (CullWavesOk(8)) {
-            if (waves == 8) {
-                Launch(TraceCullKernel<8>, grid, dim3(kWave * 8), stream, ev.begin, ev.end, p);
-                return hipGetLastError();
-            }
-        }
-        Launch(TraceCullKernel<4>, grid, dim3(kWave * 4), stream, ev.begin, ev.end, p);
     } else {
         constexpr int kRowsPerBlock = kRowsPerLane * kLdsWaves;
         const unsigned gy = static_cast<unsigned>((band.row_count + kRowsPerBlock - 1) / kRowsPerBlock);
         Launch(TraceLdsKernel, dim3(gx, gy), dim3(kWave * kLdsWaves), stream, ev.begin, ev.end, p);
     }
+    return hipGetLastError();
+}
+
+hipError_t LaunchShade(const float* d_vertices, const float* d_albedo, const float* d_edges, std::uint64_t n,
+                       const Frame& frame, const float background[3], const BandArgs& band, hipStream_t stream) {
+    if (band.row_count == 0 || band.width == 0) {
+        return hipSuccess;
+    }
+    if (band.ids == nullptr || band.rgba == nullptr || band.offsets == nullptr) {
+        return hipErrorInvalidValue;
+    }
+    TraceParams p{};
+    p.normals = EdgeBuffers(d_edges, n).normals;
+    p.n = static_cast<unsigned>(n);
+    (void)d_vertices;
+    p.albedo = d_albedo;
+    p.offsets = reinterpret_cast<const float2*>(band.offsets);
+    p.out = reinterpret_cast<float4*>(band.rgba);
+    p.width = static_cast<int>(band.width);
+    p.row_count = static_cast<int>(band.row_count);
+    p.row_begin = static_cast<int>(band.row_begin);
+    p.wf = static_cast<float>(band.width);
+    p.hf = static_cast<float>(band.height);
+    for (int k = 0; k < 3; ++k) {
+        p.base[k] = frame.base[k];
+        p.du[k] = frame.du[k];
+        p.dv[k] = frame.dv[k];
+        p.bg[k] = background[k];
+    }
+    const std::size_t pixels = band.width * band.row_count;
+    hipLaunchKernelGGL(ShadeIdsKernel, dim3(static_cast<unsigned>((pixels + 255) / 256)), dim3(256), 0, stream, p,
+                       static_cast<const int*>(band.ids));
     return hipGetLastError();
 }
 

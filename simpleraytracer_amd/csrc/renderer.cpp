@@ -156,6 +156,9 @@ DeviceScene::~DeviceScene() {
     for (hipEvent_t e : m_prep_events) {
         (void)hipEventDestroy(e);
     }
+    if (m_order_event != nullptr) {
+        (void)hipEventDestroy(m_order_event);
+    }
     if (prev >= 0) {
         (void)hipSetDevice(prev);
     }
@@ -174,15 +177,54 @@ void DeviceScene::Prepare(std::size_t width, std::size_t height, hipStream_t str
     m_prepare_pending = true;
 }
 
+void DeviceScene::OrderAfterPrevious(hipStream_t stream) const {
+    if (m_used && stream != m_last_stream) {
+        if (m_order_event == nullptr) {
+            HipCheck(hipEventCreateWithFlags(&m_order_event, hipEventDisableTiming), "hipEventCreate(scene order)");
+        }
+        HipCheck(hipEventRecord(m_order_event, m_last_stream), "hipEventRecord(scene order)");
+        HipCheck(hipStreamWaitEvent(stream, m_order_event, 0), "hipStreamWaitEvent(scene order)");
+    }
+    m_used = true;
+    m_last_stream = stream;
+}
+
+// The edge records of the prepared frame, when no trace has enqueued them yet (a Shade first).
+void DeviceScene::PrepareIfPending(hipStream_t stream) const {
+    if (m_prepare_pending) {
+        HipCheck(LaunchPrepare(m_vertices, m_rank, m_n, m_frame, m_edges, stream), "prepare kernel launch");
+        m_prepare_pending = false;
+    }
+}
+
+void DeviceScene::Shade(const float* d_offsets, const int* d_ids, float* d_rgba, std::size_t row_begin,
+                        std::size_t row_count, hipStream_t stream) const {
+    if (m_width == 0) {
+        throw std::runtime_error("Shade: Prepare() has not been called");
+    }
+    if (row_begin + row_count > m_height) {
+        throw std::runtime_error("Shade: row band outside the frame");
+    }
+    if (row_count == 0) {
+        return;
+    }
+    OrderAfterPrevious(stream);
+    PrepareIfPending(stream);
+    BandArgs band{d_offsets, d_rgba, m_width, m_height, row_begin, row_count, const_cast<int*>(d_ids)};
+    HipCheck(LaunchShade(m_vertices, m_albedo, m_edges, m_n, m_frame, m_background, band, stream),
+             "shade kernel launch");
+}
+
 void DeviceScene::Trace(const float* d_offsets, float* d_rgba, std::size_t row_begin, std::size_t row_count,
-                        int variant, hipStream_t stream) const {
+                        int variant, hipStream_t stream, int* d_ids) const {
     if (m_width == 0) {
         throw std::runtime_error("Trace: Prepare() has not been called");
     }
     if (row_begin + row_count > m_height) {
         throw std::runtime_error("Trace: row band outside the frame");
     }
-    BandArgs band{d_offsets, d_rgba, m_width, m_height, row_begin, row_count};
+    OrderAfterPrevious(stream);
+    BandArgs band{d_offsets, d_rgba, m_width, m_height, row_begin, row_count, d_ids};
     CullBins bins{};
     const CullBins* use_bins = nullptr;
     if (variant == kTraceCull && row_count != 0 && CullBinningEnabled() && CullBinnable(m_width, row_count)) {

@@ -40,8 +40,13 @@ public:
     // Edge setup for a W x H frame. The records are computed by the next Trace, on its stream
     // (fused into its first kernel); they stay valid until the next Prepare.
     void Prepare(std::size_t width, std::size_t height, hipStream_t stream);
-    // Trace rows [row_begin, row_begin + row_count) of the prepared frame.
+    // Trace rows [row_begin, row_begin + row_count) of the prepared frame into RGBA, or (d_ids
+    // non-null, d_rgba ignored) into hit ids for deferred shading.
     void Trace(const float* d_offsets, float* d_rgba, std::size_t row_begin, std::size_t row_count, int variant,
+               hipStream_t stream, int* d_ids = nullptr) const;
+    // Deferred shading of rows [row_begin, row_begin + row_count) of the prepared frame from hit
+    // ids (as Trace writes them) and sample offsets: the RGBA the fused trace would store.
+    void Shade(const float* d_offsets, const int* d_ids, float* d_rgba, std::size_t row_begin, std::size_t row_count,
                hipStream_t stream) const;
 
     std::size_t width() const { return m_width; }
@@ -83,6 +88,13 @@ private:
     // bin end, begin, end); the first m_prep_timed / m_timed entries hold pending launches.
     hipEvent_t TimingEvent(std::vector<hipEvent_t>& pool, std::size_t i) const;
     bool m_timing = false;
+    // Calls on one scene are stream-ordered: the per-frame edge records and the cull work buffer
+    // are shared state, so a call on another stream than the previous one first waits for it.
+    void OrderAfterPrevious(hipStream_t stream) const;
+    void PrepareIfPending(hipStream_t stream) const;
+    mutable hipStream_t m_last_stream = nullptr;
+    mutable bool m_used = false;
+    mutable hipEvent_t m_order_event = nullptr;
     mutable std::vector<hipEvent_t> m_prep_events;
     mutable std::vector<hipEvent_t> m_events;
     mutable std::vector<bool> m_binned;

@@ -200,6 +200,40 @@ ML_API_ENTRY int srtTraceAsync(srt_device_scene scene, const float* d_offsets, f
     });
 }
 
+ML_API_ENTRY int srtTraceIdsAsync(srt_device_scene scene, const float* d_offsets, int* d_ids, size_t row_begin,
+                                  size_t row_count, int variant, void* stream) {
+    return Guarded([&] {
+        if (scene == nullptr) {
+            throw std::runtime_error("Bad scene handle");
+        }
+        if ((d_offsets == nullptr || d_ids == nullptr) && row_count != 0) {
+            throw std::runtime_error("Bad buffer argument");
+        }
+        if (variant != SRT_TRACE_LDS && variant != SRT_TRACE_SCALAR && variant != SRT_TRACE_CULL &&
+            variant != SRT_TRACE_BVH) {
+            throw std::runtime_error("Unknown trace variant " + std::to_string(variant));
+        }
+        srt::DeviceScene* s = FromHandle(scene);
+        Bind bind(s->device());
+        s->Trace(d_offsets, nullptr, row_begin, row_count, variant, static_cast<hipStream_t>(stream), d_ids);
+    });
+}
+
+ML_API_ENTRY int srtShadeAsync(srt_device_scene scene, const float* d_offsets, const int* d_ids, float* d_rgba,
+                               size_t row_begin, size_t row_count, void* stream) {
+    return Guarded([&] {
+        if (scene == nullptr) {
+            throw std::runtime_error("Bad scene handle");
+        }
+        if ((d_offsets == nullptr || d_ids == nullptr || d_rgba == nullptr) && row_count != 0) {
+            throw std::runtime_error("Bad buffer argument");
+        }
+        srt::DeviceScene* s = FromHandle(scene);
+        Bind bind(s->device());
+        s->Shade(d_offsets, d_ids, d_rgba, row_begin, row_count, static_cast<hipStream_t>(stream));
+    });
+}
+
 ML_API_ENTRY int srtSetStageTiming(srt_device_scene scene, int enable) {
     return Guarded([&] {
         if (scene == nullptr) {

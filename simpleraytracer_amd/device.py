@@ -112,18 +112,52 @@ class DeviceScene:
         _check(self._lib.srtPrepareAsync(self.handle, width, height, _stream(stream)))
         self.width, self.height = width, height
 
+    def _check_buffer(self, name, buf, rows, channels, dtype):
+        """Shape / contiguity, and for torch tensors dtype and device: the kernels read and write
+        raw pointers on self.device with these element types."""
+        want = (rows, self.width) + ((channels,) if channels else ())
+        if hasattr(buf, "shape") and tuple(buf.shape) != want:
+            raise ValueError(f"{name} must be {want}, got {tuple(buf.shape)}")
+        if hasattr(buf, "is_contiguous") and not buf.is_contiguous():
+            raise ValueError(f"{name} must be contiguous")
+        if hasattr(buf, "is_cuda"):
+            import torch
+
+            want_dtype = {"f32": torch.float32, "i32": torch.int32}[dtype]
+            if buf.dtype != want_dtype:
+                raise ValueError(f"{name} must be {want_dtype}, got {buf.dtype}")
+            if not buf.is_cuda or buf.device.index != self.device:
+                raise ValueError(f"{name} must live on cuda:{self.device}, got {buf.device}")
+
     def trace(self, offsets, rgba, row_begin: int = 0, row_count: int | None = None, variant: str = "cull",
               stream=None):
         """offsets: (rows, W, 2) float32 device buffer; rgba: (rows, W, 4) float32 device buffer."""
         if row_count is None:
             row_count = self.height - row_begin
-        for name, buf, ch in (("offsets", offsets, 2), ("rgba", rgba, 4)):
-            if hasattr(buf, "shape") and tuple(buf.shape) != (row_count, self.width, ch):
-                raise ValueError(f"{name} must be {(row_count, self.width, ch)}, got {tuple(buf.shape)}")
-            if hasattr(buf, "is_contiguous") and not buf.is_contiguous():
-                raise ValueError(f"{name} must be contiguous")
+        self._check_buffer("offsets", offsets, row_count, 2, "f32")
+        self._check_buffer("rgba", rgba, row_count, 4, "f32")
         _check(self._lib.srtTraceAsync(self.handle, _ptr(offsets), _ptr(rgba), row_begin, row_count,
                                        TRACE_VARIANTS[variant], _stream(stream)))
+
+    def trace_ids(self, offsets, ids, row_begin: int = 0, row_count: int | None = None, variant: str = "cull",
+                  stream=None):
+        """Hit ids only (deferred shading): offsets (rows, W, 2) float32, ids (rows, W) int32."""
+        if row_count is None:
+            row_count = self.height - row_begin
+        self._check_buffer("offsets", offsets, row_count, 2, "f32")
+        self._check_buffer("ids", ids, row_count, 0, "i32")
+        _check(self._lib.srtTraceIdsAsync(self.handle, _ptr(offsets), _ptr(ids), row_begin, row_count,
+                                          TRACE_VARIANTS[variant], _stream(stream)))
+
+    def shade(self, offsets, ids, rgba, row_begin: int = 0, row_count: int | None = None, stream=None):
+        """Deferred shading of the prepared frame's rows from hit ids: the RGBA trace() stores."""
+        if row_count is None:
+            row_count = self.height - row_begin
+        self._check_buffer("offsets", offsets, row_count, 2, "f32")
+        self._check_buffer("ids", ids, row_count, 0, "i32")
+        self._check_buffer("rgba", rgba, row_count, 4, "f32")
+        _check(self._lib.srtShadeAsync(self.handle, _ptr(offsets), _ptr(ids), _ptr(rgba), row_begin, row_count,
+                                       _stream(stream)))
 
     def set_stage_timing(self, enable: bool = True):
         """Bind HIP events to the prepare, bin and trace kernels' dispatches (no extra packets)."""

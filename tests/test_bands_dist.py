@@ -75,3 +75,69 @@ def test_gloo_band_gather_equals_single_process(scenes, tmp_path, world, wh):
     ref = OracleScene(scenes["soup300"]).render(w, h)
     assert got.shape == (h, w, 4)
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+
+
+def _ids_worker(rank, world, port, scene_path, w, h, frames, queues, out_dir):
+    """bench.py's multi-GPU band pipeline with CPU stand-ins for the device stages: rank r
+    traces band r of every frame (the oracle's ids), the id bands of frame k are gathered on
+    process group k % queues to the compositing rank k % world, which shades the frame from the
+    ids (the oracle's stage 3, as srtShadeAsync does on the GPU)."""
+    import torch
+    import torch.distributed as dist
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, repo)
+    from oracle.srt_oracle import OracleScene
+    from simpleraytracer_amd.bands import band_range, band_rows, compositor, gather_band_ids
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    groups = [dist.new_group(list(range(world))) for _ in range(queues)]
+    oracle = OracleScene(scene_path)
+    b0, cnt = band_range(h, world, rank)
+    outs = [torch.empty((world * band_rows(h, world), w), dtype=torch.int32) for _ in range(queues)]
+    for k in range(frames):
+        offs = np.random.default_rng(1000 + k).random((h, w, 2), dtype=np.float32)
+        band = torch.full((band_rows(h, world), w), -5, dtype=torch.int32)
+        if cnt:
+            img = oracle.render(w, h, offs, row_begin=b0, row_count=cnt, threads=1)
+            band[:cnt] = torch.from_numpy(img[b0:b0 + cnt, :, 3].astype(np.int32))
+        root = compositor(k, world)
+        ids, work = gather_band_ids(band, h, dst=root, group=groups[k % queues], out=outs[k % queues],
+                                    async_op=True)
+        work.wait()
+        if rank == root:
+            assert ids.shape == (h, w)
+            np.save(os.path.join(out_dir, f"frame{k}.npy"), oracle.shade(w, h, ids.numpy(), offs))
+        else:
+            assert ids is None
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,wh", [(2, (40, 37)), (3, (33, 29))])
+def test_gloo_id_gather_rotating_compositor(scenes, tmp_path, world, wh):
+    """Deferred-shading band pipeline (hit-id gather, rotating compositor, one process group per
+    frame queue): every frame, wherever it was composited, equals the single-process frame bit
+    for bit."""
+    import torch.multiprocessing as mp
+
+    from oracle.srt_oracle import OracleScene
+
+    w, h = wh
+    frames = 2 * world + 1
+    mp.start_processes(_ids_worker, args=(world, _free_port(), scenes["soup300"], w, h, frames, 2, str(tmp_path)),
+                       nprocs=world, join=True, start_method="spawn")
+    oracle = OracleScene(scenes["soup300"])
+    for k in range(frames):
+        offs = np.random.default_rng(1000 + k).random((h, w, 2), dtype=np.float32)
+        got = np.load(tmp_path / f"frame{k}.npy")
+        ref = oracle.render(w, h, offs)
+        assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), k
+
+
+def test_compositor_rotation():
+    from simpleraytracer_amd.bands import compositor
+
+    assert [compositor(k, 3) for k in range(7)] == [0, 1, 2, 0, 1, 2, 0]
+    assert [compositor(k, 3, rotate=False) for k in range(4)] == [0, 0, 0, 0]

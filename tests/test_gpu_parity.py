@@ -17,14 +17,15 @@ pytestmark = pytest.mark.gpu
 
 RGB_TOL = 1e-5
 VARIANTS = ("lds", "scalar", "cull", "bvh")
-# cull variant modes: (SRT_CULL_BIN, SRT_CULL_RASTER, SRT_CULL_BIN_CAP)
-CULL_MODES = (("1", "1", ""), ("1", "0", ""), ("0", "1", ""), ("0", "0", ""), ("1", "1", "8"), ("1", "0", "8"))
+# cull variant modes: (SRT_CULL_BIN, SRT_CULL_CHUNK, SRT_CULL_BIN_CAP): bin lists on / off,
+# candidates per trace work item (64: heavy tiles split into many items), forced list overflow
+CULL_MODES = (("1", "", ""), ("1", "64", ""), ("0", "", ""), ("1", "", "8"), ("1", "64", "8"), ("1", "128", ""))
 
 
 def set_cull_mode(monkeypatch, mode):
-    binning, raster, cap = mode
+    binning, chunk, cap = mode
     monkeypatch.setenv("SRT_CULL_BIN", binning)
-    monkeypatch.setenv("SRT_CULL_RASTER", raster)
+    monkeypatch.setenv("SRT_CULL_CHUNK", chunk)
     if cap:
         monkeypatch.setenv("SRT_CULL_BIN_CAP", cap)
     else:
@@ -163,7 +164,7 @@ def test_variants_bitwise_identical_1080p(gpu, scenes):
 
 @pytest.mark.parametrize("mode", CULL_MODES)
 def test_cull_modes(gpu, scenes, monkeypatch, mode):
-    """Every cull mode (bin lists on/off, raster walk on/off, forced bin-list overflow) against
+    """Every cull mode (bin lists on/off, split work items, forced bin-list overflow) against
     the oracle, with uniform and random offsets, on a frame that leaves partial tiles."""
     set_cull_mode(monkeypatch, mode)
     rng = np.random.default_rng(5)
@@ -534,3 +535,115 @@ def test_concurrent_frame_queues(gpu, scenes, variant):
     for (scene, _, _, out), ref in zip(qs, refs):
         assert np.array_equal(out.cpu().numpy().view(np.uint32), ref.view(np.uint32))
         scene.close()
+
+
+@pytest.mark.parametrize("chunk", ["64", ""])
+def test_split_items_across_frames(gpu, scenes, monkeypatch, chunk):
+    """Split work items (a heavy tile part cut into candidate chunks, merged by the last chunk
+    through global key slices): frames traced back to back on one scene and stream, each with
+    different per-pixel jitter, equal fresh single-frame renders bit for bit -- no key slice or
+    arrival counter state leaks from one frame into the next -- and the oracle on a row sample."""
+    import torch
+
+    import simpleraytracer_amd as srt
+
+    monkeypatch.setenv("SRT_CULL_CHUNK", chunk)
+    w, h = 640, 360
+    rng = np.random.default_rng(77)
+    offs = [rng.random((h, w, 2), dtype=np.float32) for _ in range(3)] + \
+           [np.full((h, w, 2), j, np.float32) for j in (0.5, 0.25, 0.75)]
+    refs = [torch_render(scenes["soup100k"], w, h, o) for o in offs]
+    scene = srt.DeviceScene(scenes["soup100k"], 0)
+    stream = torch.cuda.current_stream()
+    ins = [torch.from_numpy(o).cuda() for o in offs]
+    outs = [torch.empty((h, w, 4), dtype=torch.float32, device="cuda") for _ in offs]
+    for rep in range(2):
+        for o, out in zip(ins, outs):
+            scene.prepare(w, h, stream)
+            scene.trace(o, out, 0, h, stream=stream)
+    torch.cuda.synchronize()
+    for out, ref in zip(outs, refs):
+        assert np.array_equal(out.cpu().numpy().view(np.uint32), ref.view(np.uint32))
+    scene.close()
+    rows = np.arange(5, h, 60)
+    ref = oracle_render(scenes["soup100k"], w, h, offs[0], row_begin=5, row_count=h - 5, row_step=60)
+    assert_parity(refs[0], ref, rows=rows)
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_deferred_shading_bitwise(gpu, scenes, variant):
+    """srtTraceIdsAsync + srtShadeAsync (the multi-GPU band path: hit ids gathered, shaded by the
+    compositing GPU) equal the fused srtTraceAsync frame bit for bit, per band, with random
+    offsets; the ids are the frame's alpha channel."""
+    import torch
+
+    import simpleraytracer_amd as srt
+
+    w, h = 333, 170
+    rng = np.random.default_rng(41)
+    offs = rng.random((h, w, 2), dtype=np.float32)
+    ref = torch_render(scenes["soup2k"], w, h, offs, variant=variant)
+    scene = srt.DeviceScene(scenes["soup2k"], 0)
+    stream = torch.cuda.current_stream()
+    off = torch.from_numpy(offs).cuda()
+    ids = torch.full((h, w), -7, dtype=torch.int32, device="cuda")
+    rgba = torch.full((h, w, 4), float("nan"), dtype=torch.float32, device="cuda")
+    scene.prepare(w, h, stream)
+    for r0, rows in ((0, 61), (61, 1), (62, h - 62)):
+        scene.trace_ids(off[r0:r0 + rows], ids[r0:r0 + rows], r0, rows, variant=variant, stream=stream)
+    # shade the whole frame in two bands on a second scene (its prepare runs inside the shade)
+    scene2 = srt.DeviceScene(scenes["soup2k"], 0)
+    scene2.prepare(w, h, stream)
+    for r0, rows in ((0, 100), (100, h - 100)):
+        scene2.shade(off[r0:r0 + rows], ids[r0:r0 + rows], rgba[r0:r0 + rows], r0, rows, stream=stream)
+    torch.cuda.synchronize()
+    got_ids = ids.cpu().numpy()
+    assert np.array_equal(got_ids.astype(np.float32), ref[..., 3])
+    assert np.array_equal(rgba.cpu().numpy().view(np.uint32), ref.view(np.uint32))
+    scene.close()
+    scene2.close()
+
+
+def test_scene_calls_on_two_streams_are_ordered(gpu, scenes):
+    """One scene used from two streams (bands on alternating streams, a new prepare in between):
+    the library orders the calls, so every frame equals its single-stream render."""
+    import torch
+
+    import simpleraytracer_amd as srt
+
+    w, h = 256, 144
+    offs = [np.full((h, w, 2), j, np.float32) for j in (0.5, 0.3)]
+    refs = [torch_render(scenes["soup2k"], w, h, o) for o in offs]
+    scene = srt.DeviceScene(scenes["soup2k"], 0)
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    outs = [torch.empty((h, w, 4), dtype=torch.float32, device="cuda") for _ in offs]
+    torch.cuda.synchronize()
+    ins = [torch.from_numpy(o).cuda() for o in offs]  # alive until the end (used on side streams)
+    torch.cuda.synchronize()
+    for off, out in zip(ins, outs):
+        scene.prepare(w, h, streams[0])
+        for k, r0 in enumerate(range(0, h, 48)):
+            st = streams[k % 2]
+            scene.trace(off[r0:r0 + 48], out[r0:r0 + 48], r0, 48, stream=st)
+    torch.cuda.synchronize()
+    for out, ref in zip(outs, refs):
+        assert np.array_equal(out.cpu().numpy().view(np.uint32), ref.view(np.uint32))
+    scene.close()
+
+
+def test_device_buffers_are_validated(gpu, scenes):
+    """DeviceScene checks dtype and device of torch buffers before passing raw pointers."""
+    import torch
+
+    import simpleraytracer_amd as srt
+
+    scene = srt.DeviceScene(scenes["soup300"], 0)
+    scene.prepare(64, 32, torch.cuda.current_stream())
+    off = torch.full((32, 64, 2), 0.5, dtype=torch.float32, device="cuda")
+    with pytest.raises(ValueError, match="float32"):
+        scene.trace(off, torch.empty((32, 64, 4), dtype=torch.float16, device="cuda"))
+    with pytest.raises(ValueError, match="cuda:0"):
+        scene.trace(off, torch.empty((32, 64, 4), dtype=torch.float32))
+    with pytest.raises(ValueError, match="int32"):
+        scene.trace_ids(off, torch.empty((32, 64), dtype=torch.int64, device="cuda"))
+    scene.close()

@@ -1,11 +1,13 @@
 #!/usr/bin/env python3
-"""Per-block phase breakdown of the cull kernel (diagnostic build; run on the GPU box).
+"""Per-block timeline of the cull trace kernel (diagnostic build; run on the GPU box).
 
     make diag && SRT_LIB=simpleraytracer_amd/lib_diag/libModelRunner.so python tools/diag_cull.py
 
-Renders the headline frame with the `make diag` library (s_memtime stamps around the cull
-kernel's phases, render.hip SRT_DIAG) and prints the distribution of stream / gather /
-filter+walk cycles and survivor counts over the blocks, heaviest blocks first.
+Renders one frame (headline config by default; env W, H, TRI, OFFSETS=random) with the
+`make diag` library, whose trace kernel stamps every block's start and end (s_memrealtime,
+100 MHz), its work item (tile part, chunk of a split part, last arriver) and the packet-walk
+phase cycles (render.hip SRT_DIAG). Prints the kernel span, block durations, how many blocks
+run over time, the critical chains of split parts and the blocks that finish last.
 """
 from __future__ import annotations
 
@@ -19,6 +21,16 @@ import numpy as np
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
+COLS = 16  # render.hip kDiagCols
+
+
+def stats(col):
+    col = np.asarray(col, np.float64)
+    if col.size == 0:
+        return {}
+    return {"mean": round(float(col.mean()), 2), "p50": round(float(np.median(col)), 2),
+            "p90": round(float(np.percentile(col, 90)), 2), "max": round(float(col.max()), 2),
+            "sum": round(float(col.sum()), 1)}
 
 
 def main():
@@ -37,39 +49,62 @@ def main():
         path = srt.write_scene(os.path.join(d, "s.srt"), "soup", tri)
         scene = srt.DeviceScene(path, 0)
         stream = torch.cuda.current_stream()
-        off = torch.full((h, w, 2), 0.5, dtype=torch.float32, device="cuda")
+        if os.environ.get("OFFSETS") == "random":
+            g = torch.Generator().manual_seed(0x5EED)
+            off = torch.rand((h, w, 2), generator=g, dtype=torch.float32).cuda()
+        else:
+            off = torch.full((h, w, 2), 0.5, dtype=torch.float32, device="cuda")
         out = torch.empty((h, w, 4), dtype=torch.float32, device="cuda")
-        scene.prepare(w, h, stream)
         for _ in range(3):
+            scene.prepare(w, h, stream)
             scene.trace(off, out, 0, h, variant="cull", stream=stream)
         torch.cuda.synchronize()
-        buf = np.zeros((65536, 8), np.uint64)
+        buf = np.zeros((65536, COLS), np.uint64)
         assert lib.srtDiagRead(buf.ctypes.data, buf.nbytes) == 0, _native.last_error()
         scene.close()
-    shape = "8x4 tiles, bins " + os.environ.get("SRT_CULL_BIN", "1")
-    parts = int(os.environ.get("PARTS", 2))  # trace blocks per cull tile (render.hip kParts)
-    gx, gy = (w + 63) // 64, (h + 31) // 32
-    nb = gx * gy * parts
-    allb = buf[:nb].astype(np.float64)
-    ran = allb[:, 6] > 0
-    d = allb[ran]
-    # packet-walk blocks: [1] gather, [2] walk, [3] survivors, [4] packets, [5] batches, [6] total
-    names = ["stream", "gather", "walk", "surv", "packets", "batches", "total"]
-    summary = {"shape": f"{gx}x{gy} tiles x {parts} parts, bins " + os.environ.get("SRT_CULL_BIN", "1"),
-               "blocks": nb, "blocks_run": int(ran.sum())}
-    for i, n in enumerate(names):
-        col = d[:, i]
-        summary[n] = {"mean": float(col.mean()), "p50": float(np.median(col)), "p90": float(np.percentile(col, 90)),
-                      "max": float(col.max()), "sum": float(col.sum())}
-    mode = buf[:nb, 7].astype(np.int64)
-    cnt = (mode >> 16) & 0xFFFFFF
-    summary["tile_list"] = {"mean": float(cnt.mean()), "p50": float(np.median(cnt)), "p90": float(np.percentile(cnt, 90)),
-                            "max": int(cnt.max()), "sum": int(cnt.sum()) // parts, "large": int((mode >> 40).max())}
-    # Balance: total block-cycles spread over 256 CUs x 4 SIMDs vs the heaviest block.
-    summary["balance"] = {"sum_cycles_per_simd": float(d[:, 6].sum() / 1024), "max_block_cycles": float(d[:, 6].max())}
-    idx = np.nonzero(ran)[0]
-    heavy = idx[np.argsort(-allb[idx, 6])[:8]]
-    summary["heaviest"] = [{"block": int(b), **{n: int(allb[b, i]) for i, n in enumerate(names)}} for b in heavy]
+    ran = np.nonzero(buf[:, 9] > 0)[0]
+    b = buf[ran].astype(np.float64)
+    t0 = b[:, 8].min()
+    start = (b[:, 8] - t0) / 100.0  # us
+    end = (b[:, 9] - t0) / 100.0
+    dur = end - start
+    info = buf[ran, 11]
+    chunk, nch, last = info & 0xFFFF, (info >> 16) & 0xFFFF, (info >> 32) & 1
+    item = buf[ran, 10]
+    summary = {"frame": f"{w}x{h}, {tri} triangles, offsets {os.environ.get('OFFSETS', 'uniform')}",
+               "blocks": int(ran.size), "span_us": round(float(end.max()), 2),
+               "duration_us": stats(dur), "split_blocks": int((nch > 1).sum()),
+               "split_parts": int(len(set(item[nch > 1].tolist())))}
+    pk = buf[ran, 7] & 8 != 0  # packet-walk blocks
+    summary["packet_walk"] = {"blocks": int(pk.sum()), "gather_cycles": stats(b[pk, 1]), "walk_cycles": stats(b[pk, 2]),
+                              "survivors": stats(b[pk, 3]), "packets": stats(b[pk, 4]),
+                              "candidates": stats(buf[ran][pk, 7] >> 40)}
+    # blocks running over time (1 us bins)
+    nbins = int(np.ceil(end.max())) + 1
+    active = np.zeros(nbins)
+    for s0, e0 in zip(start, end):
+        active[int(s0):int(np.ceil(e0))] += 1
+    summary["active_blocks_per_us"] = [int(x) for x in active]
+    # split parts: start of the first chunk to the end of the last arriver
+    chains = {}
+    for i in np.nonzero(nch > 1)[0]:
+        c = chains.setdefault(int(item[i]), [1e9, 0.0, 0])
+        c[0] = min(c[0], start[i])
+        c[1] = max(c[1], end[i])
+        c[2] = int(nch[i])
+    top = sorted(chains.items(), key=lambda kv: -kv[1][1])[:8]
+    summary["split_chains_latest"] = [{"item": k, "first_start": round(v[0], 2), "end": round(v[1], 2), "chunks": v[2]}
+                                      for k, v in top]
+    order = np.argsort(-end)[:12]
+    summary["last_to_finish"] = [{"grid_block": int(ran[i]), "item": int(item[i]), "chunk": int(chunk[i]),
+                                  "chunks": int(nch[i]), "last": int(last[i]), "start": round(float(start[i]), 2),
+                                  "end": round(float(end[i]), 2), "candidates": int(buf[ran[i], 7] >> 40),
+                                  "packets": int(buf[ran[i], 4])} for i in order]
+    order = np.argsort(-dur)[:8]
+    summary["longest"] = [{"grid_block": int(ran[i]), "item": int(item[i]), "chunks": int(nch[i]),
+                           "start": round(float(start[i]), 2), "dur": round(float(dur[i]), 2),
+                           "candidates": int(buf[ran[i], 7] >> 40), "survivors": int(buf[ran[i], 3]),
+                           "packets": int(buf[ran[i], 4])} for i in order]
     print(json.dumps(summary, indent=1))
 
 

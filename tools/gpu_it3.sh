@@ -1,0 +1,16 @@
+#!/bin/bash
+# Parity tests, diag timelines (uniform + random offsets), bench lines and one-queue rocprof.
+source "$(dirname "$0")/gpu_lib.sh"
+Q=(--no-cpu-baseline --no-e2e --brute-steps 0)
+if [ "${SKIP_TESTS:-0}" != 1 ]; then
+    run pytest_gpu 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"}
+fi
+SRT_LIB=simpleraytracer_amd/lib_diag/libModelRunner.so run diag_uniform 120 python tools/diag_cull.py
+SRT_LIB=simpleraytracer_amd/lib_diag/libModelRunner.so OFFSETS=random run diag_random 120 python tools/diag_cull.py
+run bench_uniform 300 python bench.py --steps 3000 --warmup 20 "${Q[@]}"
+run bench_random 300 python bench.py --steps 1000 --warmup 20 --offsets random "${Q[@]}"
+run prof_uniform 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_uniform -o run --output-format csv -- \
+    python3 bench.py --steps 50 --warmup 5 --queues 1 "${Q[@]}"
+run prof_random 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_random -o run --output-format csv -- \
+    python3 bench.py --steps 50 --warmup 5 --offsets random --queues 1 "${Q[@]}"
+echo done
