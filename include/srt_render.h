@@ -91,6 +91,14 @@ ML_API_ENTRY int srtShadeAsync(srt_device_scene scene, const float* d_offsets, c
  * buffer are shared, so a call on a different stream than the previous call first waits (HIP
  * event) for the work enqueued before it. Use one scene per stream for concurrent frames. */
 
+/* Self-test of the multi-device band gather on host memory (no device): band i's padded buffer
+ * bands[i] (ceil(height / band_count) rows x width x 4 elements of element_bytes, 4 = float,
+ * 2 = half) lands where ncclGather puts it in the root's gather buffer, and the frame (height x
+ * width x 4) is that buffer's first rows -- the offsets and strides every gather path of mlInfer
+ * uses (Renderer: RCCL, device copies). */
+ML_API_ENTRY int srtGatherBandsHost(const void* const* bands, size_t band_count, size_t width, size_t height,
+                                    int element_bytes, void* frame);
+
 /* Stage timing (measurement): while enabled, srtPrepareAsync and srtTraceAsync bind HIP events
  * to their kernels' own dispatch packets (hipExtLaunchKernelGGL start/stop events: no extra
  * packets on the stream). srtTakeStageTimes waits for them, writes the number of timed trace

@@ -34,7 +34,10 @@ Image::Image(ml_image_info const* info) {
         return true;
     });
     m_info = *info;
-    m_bytes = m_info.width * m_info.height * m_info.channels * item;
+    if (!ImageBytes(m_info.width, m_info.height, m_info.channels, item, &m_bytes)) {
+        throw std::runtime_error("Image size overflows: " + std::to_string(m_info.width) + " x " +
+                                 std::to_string(m_info.height) + " x " + std::to_string(m_info.channels));
+    }
     if (HipDevicePresent() && hipHostMalloc(&m_data, m_bytes, hipHostMallocDefault) == hipSuccess) {
         m_pinned = true;
     } else {

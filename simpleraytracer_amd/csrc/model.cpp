@@ -70,6 +70,15 @@ ml_status Model::SetInputInfo(ml_image_info const* info) {
     if (!specified) {
         return ML_FAIL;
     }
+    // Sizes the kernels can index (32-bit pixel coordinates) and byte counts that fit size_t.
+    size_t in_bytes = 0, out_bytes = 0;
+    if (info->width > kMaxFrameSide || info->height > kMaxFrameSide ||
+        !ImageBytes(info->width, info->height, info->channels, DataTypeSize(info->dtype), &in_bytes) ||
+        !ImageBytes(info->width, info->height, 4, 4, &out_bytes)) {
+        m_error_cache << "Input image size " << info->width << " x " << info->height << " x " << info->channels
+                      << " exceeds the supported maximum (" << kMaxFrameSide << " per side)";
+        return ML_FAIL;
+    }
     const bool same = ForEachDim([this, info](auto dim, char const*) { return m_input_info.*dim == info->*dim; });
     if (same && m_renderer && m_renderer->configured()) {
         return ML_OK;  // nothing changed

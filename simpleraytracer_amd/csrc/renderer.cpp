@@ -50,9 +50,25 @@ bool CullBinningEnabled() {
     return v == nullptr || std::strcmp(v, "0") != 0;
 }
 
-bool GatherWithRccl() {
-    const char* mode = std::getenv("SRT_GATHER");
-    return mode == nullptr || std::strcmp(mode, "direct") != 0;
+GatherMode GatherModeFor(const std::vector<int>& devices) {
+    const char* v = std::getenv("SRT_GATHER");
+    if (v != nullptr && std::strcmp(v, "direct") == 0) {
+        return GatherMode::kDirect;
+    }
+    if (v != nullptr && std::strcmp(v, "copy") == 0) {
+        return GatherMode::kCopy;
+    }
+    if (v != nullptr && std::strcmp(v, "rccl") == 0) {
+        return GatherMode::kRccl;
+    }
+    for (std::size_t i = 0; i < devices.size(); ++i) {
+        for (std::size_t j = 0; j < i; ++j) {
+            if (devices[i] == devices[j]) {
+                return GatherMode::kCopy;  // one device twice: no RCCL communicator
+            }
+        }
+    }
+    return GatherMode::kRccl;
 }
 
 }  // namespace
@@ -92,6 +108,29 @@ std::vector<int> VisibleDevices() {
         devices.push_back(0);
     }
     return devices;
+}
+
+GatherPlan GatherPlan::Make(std::size_t width, std::size_t height, std::size_t bands, std::size_t elem) {
+    GatherPlan p;
+    p.width = width;
+    p.height = height;
+    p.bands = bands == 0 ? 1 : bands;
+    p.band_rows = (height + p.bands - 1) / p.bands;
+    p.elem = elem;
+    return p;
+}
+
+std::size_t GatherPlan::RowCount(std::size_t i) const {
+    const std::size_t end = (i + 1) * band_rows < height ? (i + 1) * band_rows : height;
+    return end - RowBegin(i);
+}
+
+void GatherOnHost(const GatherPlan& plan, const void* const* bands, void* gather_buf, void* frame) {
+    auto* g = static_cast<unsigned char*>(gather_buf);
+    for (std::size_t i = 0; i < plan.bands; ++i) {
+        std::memcpy(g + plan.RecvOffset(i), bands[i], plan.BandBytes());
+    }
+    std::memcpy(frame, g, plan.FrameBytes());
 }
 
 int TraceVariantFromEnv() {
@@ -360,11 +399,11 @@ Renderer::Renderer(const Scene& scene, std::vector<int> devices)
         m_slots.push_back(std::move(slot));
         m_slots.back()->scene = std::make_unique<DeviceScene>(scene, d);
     }
-    m_use_rccl = m_slots.size() > 1 && GatherWithRccl();
-    if (m_use_rccl) {
+    m_gather_mode = m_slots.size() > 1 ? GatherModeFor(devices) : GatherMode::kDirect;
+    if (m_gather_mode == GatherMode::kRccl) {
         std::vector<ncclComm_t> comms(m_slots.size());
         NcclCheck(ncclCommInitAll(comms.data(), static_cast<int>(devices.size()), devices.data()),
-                  "ncclCommInitAll (repeated devices need SRT_GATHER=direct)");
+                  "ncclCommInitAll (a repeated device needs SRT_GATHER=copy or direct)");
         m_comms.assign(comms.begin(), comms.end());
     }
 }
@@ -414,12 +453,12 @@ void Renderer::ReleaseBuffers() {
 
 void Renderer::Configure(std::size_t width, std::size_t height) {
     const std::size_t bands = m_slots.size();
-    const std::size_t band_rows = (height + bands - 1) / bands;
+    const GatherPlan plan = GatherPlan::Make(width, height, bands, m_out_half ? 2 : 4);
+    const std::size_t band_rows = plan.band_rows;
     // Allocate everything new before releasing the old buffers (strong guarantee).
     std::vector<float*> offs(bands, nullptr), outs(bands, nullptr);
     std::vector<std::uint16_t*> offs16(bands, nullptr), outs16(bands, nullptr);
     void* gather = nullptr;
-    const std::size_t out_elem = m_out_half ? 2 : 4;
     try {
         for (std::size_t i = 0; i < bands; ++i) {
             DeviceGuard guard(m_slots[i]->device);
@@ -432,9 +471,9 @@ void Renderer::Configure(std::size_t width, std::size_t height) {
                 outs16[i] = DeviceAlloc<std::uint16_t>(band_rows * width * 4, "hipMalloc(band framebuffer f16)");
             }
         }
-        if (m_use_rccl) {
+        if (m_gather_mode != GatherMode::kDirect) {
             DeviceGuard guard(m_slots.front()->device);
-            gather = DeviceAlloc<unsigned char>(bands * band_rows * width * 4 * out_elem, "hipMalloc(gather framebuffer)");
+            gather = DeviceAlloc<unsigned char>(bands * plan.BandBytes(), "hipMalloc(gather framebuffer)");
         }
     } catch (...) {
         for (std::size_t i = 0; i < bands; ++i) {
@@ -454,27 +493,61 @@ void Renderer::Configure(std::size_t width, std::size_t height) {
         s.rgba = outs[i];
         s.offsets16 = offs16[i];
         s.rgba16 = outs16[i];
-        s.row_begin = std::min(height, i * band_rows);
-        s.row_count = std::min(height, (i + 1) * band_rows) - s.row_begin;
+        s.row_begin = plan.RowBegin(i);
+        s.row_count = plan.RowCount(i);
     }
     m_gather = gather;
     m_width = width;
     m_height = height;
-    m_band_rows = band_rows;
+    m_plan = plan;
+}
+
+// On an exception mid-frame, copies already queued may still target the caller's host
+// buffers: wait for every stream used (ignoring their errors) before the error propagates.
+void Renderer::SyncAll() noexcept {
+    for (auto& sp : m_slots) {
+        (void)hipSetDevice(sp->device);
+        (void)hipStreamSynchronize(sp->stream);
+        if (sp->copy_in != nullptr) {
+            (void)hipStreamSynchronize(sp->copy_in);
+        }
+        if (sp->copy_out != nullptr) {
+            (void)hipStreamSynchronize(sp->copy_out);
+        }
+    }
 }
 
 void Renderer::Render(const void* host_offsets, void* host_rgba) {
     if (!configured()) {
         throw std::runtime_error("Renderer used before Configure()");
     }
-    if (m_slots.size() == 1 && E2eChunks() > 1 && m_height >= 2 * E2eChunks()) {
-        RenderPipelined(host_offsets, host_rgba, E2eChunks());
-        return;
+    int prev = -1;
+    (void)hipGetDevice(&prev);
+    try {
+        if (m_slots.size() == 1 && E2eChunks() > 1 && m_height >= 2 * E2eChunks()) {
+            RenderPipelined(host_offsets, host_rgba, E2eChunks());
+        } else {
+            RenderBands(host_offsets, host_rgba);
+        }
+    } catch (...) {
+        SyncAll();
+        if (prev >= 0) {
+            (void)hipSetDevice(prev);
+        }
+        throw;
     }
+}
+
+// One band per device: H2D of the band's offsets, prepare + trace, then the frame assembled on
+// the host image by the gather mode (GatherPlan: the same offsets for RCCL and device copies).
+void Renderer::RenderBands(const void* host_offsets, void* host_rgba) {
     const std::size_t w = m_width;
-    const std::size_t in_elem = m_in_half ? 2 : 4, out_elem = m_out_half ? 2 : 4;
+    const std::size_t in_elem = m_in_half ? 2 : 4, out_elem = m_plan.elem;
     const auto* in_bytes = static_cast<const unsigned char*>(host_offsets);
     auto* out_bytes = static_cast<unsigned char*>(host_rgba);
+    auto band_out = [this](const Slot& s) {
+        return m_out_half ? static_cast<void*>(s.rgba16) : static_cast<void*>(s.rgba);
+    };
     for (auto& sp : m_slots) {
         Slot& s = *sp;
         DeviceGuard guard(s.device);
@@ -492,25 +565,45 @@ void Renderer::Render(const void* host_offsets, void* host_rgba) {
         s.scene->Trace(s.offsets, s.rgba, s.row_begin, s.row_count, m_variant, s.stream);
         if (m_out_half) {
             // Whole padded band (rows past row_count are gathered but never copied out).
-            HipCheck(LaunchFloatToHalf(s.rgba, s.rgba16, m_band_rows * w * 4, s.stream), "framebuffer f32 -> f16");
+            HipCheck(LaunchFloatToHalf(s.rgba, s.rgba16, m_plan.BandElems(), s.stream), "framebuffer f32 -> f16");
         }
     }
-    if (m_use_rccl) {
-        // Equal-size bands (the last one padded) gathered to the first device over xGMI;
-        // frame rows 0..H-1 are then the first H rows of the gather buffer.
+    Slot& root = *m_slots.front();
+    if (m_gather_mode == GatherMode::kRccl) {
+        // Equal-size bands (the last one padded) gathered to the first device over xGMI.
         NcclCheck(ncclGroupStart(), "ncclGroupStart");
         for (std::size_t i = 0; i < m_slots.size(); ++i) {
             Slot& s = *m_slots[i];
-            const void* send = m_out_half ? static_cast<const void*>(s.rgba16) : static_cast<const void*>(s.rgba);
-            NcclCheck(ncclGather(send, i == 0 ? m_gather : nullptr, m_band_rows * w * 4,
+            NcclCheck(ncclGather(band_out(s), i == 0 ? m_gather : nullptr, m_plan.BandElems(),
                                  m_out_half ? ncclFloat16 : ncclFloat32, 0, static_cast<ncclComm_t>(m_comms[i]),
                                  s.stream),
                       "ncclGather");
         }
         NcclCheck(ncclGroupEnd(), "ncclGroupEnd");
-        Slot& root = *m_slots.front();
+    } else if (m_gather_mode == GatherMode::kCopy) {
+        // The same gather as device copies into the root's buffer at ncclGather's offsets; the
+        // root's stream then waits for every band's copy (an event per band).
+        for (std::size_t i = 0; i < m_slots.size(); ++i) {
+            Slot& s = *m_slots[i];
+            DeviceGuard guard(s.device);
+            HipCheck(hipMemcpyPeerAsync(static_cast<unsigned char*>(m_gather) + m_plan.RecvOffset(i), root.device,
+                                        band_out(s), s.device, m_plan.BandBytes(), s.stream),
+                     "hipMemcpyPeerAsync(band gather)");
+            if (i != 0) {
+                if (s.traced.empty()) {
+                    hipEvent_t e = nullptr;
+                    HipCheck(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate(band gather)");
+                    s.traced.push_back(e);
+                }
+                HipCheck(hipEventRecord(s.traced[0], s.stream), "hipEventRecord(band gather)");
+                DeviceGuard root_guard(root.device);
+                HipCheck(hipStreamWaitEvent(root.stream, s.traced[0], 0), "hipStreamWaitEvent(band gather)");
+            }
+        }
+    }
+    if (m_gather_mode != GatherMode::kDirect) {
         DeviceGuard guard(root.device);
-        HipCheck(hipMemcpyAsync(out_bytes, m_gather, m_height * w * 4 * out_elem, hipMemcpyDeviceToHost, root.stream),
+        HipCheck(hipMemcpyAsync(out_bytes, m_gather, m_plan.FrameBytes(), hipMemcpyDeviceToHost, root.stream),
                  "hipMemcpyAsync(frame D2H)");
     } else {
         for (auto& sp : m_slots) {
@@ -519,9 +612,8 @@ void Renderer::Render(const void* host_offsets, void* host_rgba) {
                 continue;
             }
             DeviceGuard guard(s.device);
-            const void* src = m_out_half ? static_cast<const void*>(s.rgba16) : static_cast<const void*>(s.rgba);
-            HipCheck(hipMemcpyAsync(out_bytes + s.row_begin * w * 4 * out_elem, src, s.row_count * w * 4 * out_elem,
-                                    hipMemcpyDeviceToHost, s.stream),
+            HipCheck(hipMemcpyAsync(out_bytes + s.row_begin * w * 4 * out_elem, band_out(s),
+                                    s.row_count * w * 4 * out_elem, hipMemcpyDeviceToHost, s.stream),
                      "hipMemcpyAsync(band D2H)");
         }
     }

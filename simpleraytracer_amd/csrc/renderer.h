@@ -106,6 +106,35 @@ private:
 // Trace kernel variant from env SRT_TRACE_VARIANT ("lds" | "scalar" | "cull", default cull).
 int TraceVariantFromEnv();
 
+// Row bands of a frame over `bands` devices and the layout of their gather:
+// equal bands of band_rows = ceil(H / bands) rows (the last padded), band i = frame rows
+// [RowBegin(i), RowBegin(i) + RowCount(i)); band i's padded buffer (BandBytes) lands at
+// RecvOffset(i) of the root's gather buffer, exactly where ncclGather puts it, so the frame is
+// the buffer's first FrameBytes. Every gather path (RCCL, device copies, the host self-test)
+// moves bytes with these numbers.
+struct GatherPlan {
+    std::size_t width = 0, height = 0, bands = 1, band_rows = 0;
+    std::size_t elem = 4;  // bytes per channel of the output image (4: float, 2: half)
+    static GatherPlan Make(std::size_t width, std::size_t height, std::size_t bands, std::size_t elem);
+    std::size_t RowBegin(std::size_t i) const { return i * band_rows < height ? i * band_rows : height; }
+    std::size_t RowCount(std::size_t i) const;
+    std::size_t BandElems() const { return band_rows * width * 4; }  // RGBA channels of one padded band
+    std::size_t BandBytes() const { return BandElems() * elem; }
+    std::size_t RecvOffset(std::size_t i) const { return i * BandBytes(); }
+    std::size_t FrameBytes() const { return height * width * 4 * elem; }
+};
+
+// The gather on host memory (self-test of the plan, no device): bands[i] = band i's padded
+// buffer, gathered into `gather_buf` (bands x BandBytes) as ncclGather would, then the frame
+// copied out to `frame`.
+void GatherOnHost(const GatherPlan& plan, const void* const* bands, void* gather_buf, void* frame);
+
+// How Renderer assembles a multi-device frame (env SRT_GATHER): "rccl" = ncclGather of the
+// bands to the first device, then one D2H (default for distinct devices); "copy" = the same
+// gather by device-to-device copies (default when a device repeats: RCCL needs distinct
+// devices); "direct" = per-device D2H into disjoint rows of the host image.
+enum class GatherMode { kRccl, kCopy, kDirect };
+
 class Renderer {
 public:
     Renderer(const Scene& scene, std::vector<int> devices);
@@ -127,19 +156,23 @@ public:
     bool output_half() const { return m_out_half; }
 
     std::size_t bands() const { return m_slots.size(); }
+    GatherMode gather_mode() const { return m_gather_mode; }
 
 private:
     struct Slot;
     void ReleaseBuffers();
     void RenderPipelined(const void* host_offsets, void* host_rgba, std::size_t chunks);
 
+    void RenderBands(const void* host_offsets, void* host_rgba);
+    void SyncAll() noexcept;
+
     std::vector<std::unique_ptr<Slot>> m_slots;
     std::vector<void*> m_comms;  // ncclComm_t per slot when gathering with RCCL
-    bool m_use_rccl = false;
+    GatherMode m_gather_mode = GatherMode::kDirect;
+    GatherPlan m_plan;
     int m_variant = 0;
     std::size_t m_width = 0;
     std::size_t m_height = 0;
-    std::size_t m_band_rows = 0;
     void* m_gather = nullptr;  // root device: bands x band_rows x W x 4 (float, or half)
     bool m_in_half = false;
     bool m_out_half = false;

@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <exception>
 #include <string>
+#include <vector>
 
 #include "render.h"
 #include "renderer.h"
@@ -231,6 +232,18 @@ ML_API_ENTRY int srtShadeAsync(srt_device_scene scene, const float* d_offsets, c
         srt::DeviceScene* s = FromHandle(scene);
         Bind bind(s->device());
         s->Shade(d_offsets, d_ids, d_rgba, row_begin, row_count, static_cast<hipStream_t>(stream));
+    });
+}
+
+ML_API_ENTRY int srtGatherBandsHost(const void* const* bands, size_t band_count, size_t width, size_t height,
+                                    int element_bytes, void* frame) {
+    return Guarded([&] {
+        if (bands == nullptr || frame == nullptr || band_count == 0 || (element_bytes != 2 && element_bytes != 4)) {
+            throw std::runtime_error("Bad argument");
+        }
+        const srt::GatherPlan plan = srt::GatherPlan::Make(width, height, band_count, element_bytes);
+        std::vector<unsigned char> gather(plan.bands * plan.BandBytes());
+        srt::GatherOnHost(plan, bands, gather.data(), frame);
     });
 }
 

@@ -31,4 +31,20 @@ inline char* FillBuffer(char* buffer, size_t buffer_size, const std::string& mes
     return buffer;
 }
 
+// width * height * channels * item in bytes, or false when the product overflows size_t.
+inline bool ImageBytes(size_t width, size_t height, size_t channels, size_t item, size_t* bytes) {
+    size_t b = item;
+    for (size_t f : {width, height, channels}) {
+        if (f != 0 && b > static_cast<size_t>(-1) / f) {
+            return false;
+        }
+        b *= f;
+    }
+    *bytes = b;
+    return true;
+}
+
+// Largest frame side the render kernels index with 32-bit pixel coordinates.
+constexpr size_t kMaxFrameSide = 1u << 30;
+
 }  // namespace ML

@@ -282,19 +282,42 @@ def test_repeat_render_deterministic(gpu, scenes):
     assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
 
 
-def test_ml_visible_devices_bands_direct(gpu, scenes, monkeypatch):
-    """Renderer with 3 row bands (all on device 0, direct D2H gather) == single band."""
+@pytest.mark.parametrize("devices", ["0,0", "0,0,0", "0,0,0,0,0,0,0,0"])
+@pytest.mark.parametrize("mode", ["copy", "direct"])
+def test_ml_gather_modes_bitwise(gpu, scenes, monkeypatch, devices, mode):
+    """mlInfer over P row bands on device 0 ("fake devices": one device listed P times), the
+    frame assembled by the band gather (device copies to ncclGather's receive offsets, then one
+    D2H) or by per-band D2H, equals the one-band frame bit for bit; 8 bands of 100 rows leave a
+    padded last band."""
     import simpleraytracer_amd as srt
 
+    monkeypatch.delenv("ML_VISIBLE_DEVICES", raising=False)
     ref = srt.render(scenes["soup2k"], 160, 100)
-    monkeypatch.setenv("ML_VISIBLE_DEVICES", "0,0,0")
-    monkeypatch.setenv("SRT_GATHER", "direct")
+    monkeypatch.setenv("ML_VISIBLE_DEVICES", devices)
+    monkeypatch.setenv("SRT_GATHER", mode)
     got = srt.render(scenes["soup2k"], 160, 100)
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
     for variant in ("scalar", "cull", "bvh"):
         monkeypatch.setenv("SRT_TRACE_VARIANT", variant)
         got2 = srt.render(scenes["soup2k"], 160, 100)
         assert np.array_equal(got2.view(np.uint32), ref.view(np.uint32))
+
+
+def test_ml_rccl_gather_two_devices(gpu, scenes, monkeypatch):
+    """The in-process ncclGather path (ML_VISIBLE_DEVICES=0,1: one RCCL communicator per device,
+    bands gathered to device 0 over xGMI) equals the one-device frame bit for bit."""
+    import torch
+
+    import simpleraytracer_amd as srt
+
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs 2 visible GPUs for an RCCL communicator (this box has "
+                    f"{torch.cuda.device_count()}); the same gather offsets run in test_ml_gather_modes_bitwise")
+    ref = srt.render(scenes["soup2k"], 160, 100)
+    monkeypatch.setenv("ML_VISIBLE_DEVICES", "0,1")
+    monkeypatch.setenv("SRT_GATHER", "rccl")
+    got = srt.render(scenes["soup2k"], 160, 100)
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
 
 
 def test_edge_cases_scene(gpu, tmp_path):
@@ -427,16 +450,19 @@ def test_obj_scene_renders_like_its_binary_conversion(gpu, tmp_path):
 def test_float16_images(gpu, scenes, tmp_path, monkeypatch, in_dtype, out_dtype):
     """ML_FLOAT16 images (scene flags): the frame equals the f32 oracle frame rounded to half
     (rgb within one half ulp of the f32 tolerance, tri_id channel bit-exact after rounding);
-    FLOAT16 offsets are the oracle's inputs exactly. Both gather modes."""
+    FLOAT16 offsets are the oracle's inputs exactly. One device (chunk pipeline), and two bands
+    on device 0 assembled by the band gather (device copies at ncclGather's offsets, padded half
+    bands) and by per-band D2H."""
     import simpleraytracer_amd as srt
 
     path = srt.convert_scene(scenes["soup300"], str(tmp_path / "h.srt"), input_dtype=in_dtype,
                              output_dtype=out_dtype)
-    w, h = 96, 64
+    w, h = 96, 63
     rng = np.random.default_rng(3)
     offs = rng.uniform(0, 1, (h, w, 2)).astype(np.float16 if in_dtype else np.float32)
     ref = oracle_render(path, w, h, offs.astype(np.float32))
-    for mode in ("rccl", "direct"):
+    for devices, mode in (("0", "direct"), ("0,0", "copy"), ("0,0", "direct")):
+        monkeypatch.setenv("ML_VISIBLE_DEVICES", devices)
         monkeypatch.setenv("SRT_GATHER", mode)
         got = srt.render(path, w, h, offs)
         assert got.dtype == (np.float16 if out_dtype else np.float32)
