@@ -400,6 +400,7 @@ def main():
     rotate = a.root == "rotate"
     main_run = Pipeline(ctx, path, a.mode, a.queues, a.variant, a.offsets, rotate)
     n_tri = main_run.triangles
+    _, order_build_ms = main_run.queues[0]["scene"].spatial_order()
     W, H = a.width, a.height
     extras = not a.no_extras
     # Secondary passes first (they also bring the clocks up before the timed value loop): one
@@ -497,6 +498,9 @@ def main():
                                   "trace_kernel = TraceCullKernel (rank 0's band at N > 1); frame = uninstrumented "
                                   "time per frame with config.frame_queues in flight"},
         }
+        line["scene_build"] = {"spatial_order_ms": round(order_build_ms, 4),
+                               "note": "once per scene at load, on the device (Morton codes + rocPRIM radix sort, "
+                                       "csrc/spatial.hip); not per frame"}
         if valu is not None:
             line["valu_issue"] = valu
         line["brute_force_equivalent"] = bfe

@@ -64,6 +64,12 @@ ML_API_ENTRY srt_device_scene srtDeviceSceneCreate(const char* path, int device)
 ML_API_ENTRY void srtDeviceSceneRelease(srt_device_scene scene);
 ML_API_ENTRY unsigned long long srtDeviceSceneTriangles(srt_device_scene scene);
 
+/* The scene's spatial order, built on the device at load (ids sorted by the Morton code of their
+ * centroid's image-plane position under the scene camera; rocPRIM radix sort): copied to
+ * `order` (capacity entries, NULL = skip) and the build's device time in ms (NULL = skip). */
+ML_API_ENTRY int srtDeviceSceneOrder(srt_device_scene scene, unsigned* order, unsigned long long capacity,
+                                     double* build_ms);
+
 /* Stage 1: edge-record setup for a W x H frame (one thread per triangle). The work is
  * enqueued by the next srtTraceAsync, on that call's stream, fused into its first kernel; the
  * records then serve every srtTraceAsync until the next srtPrepareAsync. */

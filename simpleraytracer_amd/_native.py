@@ -83,6 +83,8 @@ _SIGNATURES = {
     "srtDeviceSceneCreate": (ctypes.c_void_p, [ctypes.c_char_p, ctypes.c_int]),
     "srtDeviceSceneRelease": (None, [ctypes.c_void_p]),
     "srtDeviceSceneTriangles": (ctypes.c_ulonglong, [ctypes.c_void_p]),
+    "srtDeviceSceneOrder": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_ulonglong,
+                                           ctypes.POINTER(ctypes.c_double)]),
     "srtPrepareAsync": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_void_p]),
     "srtTraceAsync": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
                                      ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]),

@@ -162,6 +162,13 @@ std::size_t BvhBytes(std::uint64_t n);  // node boxes (16 B) + depth bounds (4 B
 hipError_t LaunchShade(const float* d_vertices, const float* d_albedo, const float* d_edges, std::uint64_t n,
                        const Frame& frame, const float background[3], const BandArgs& band, hipStream_t stream);
 
+// Spatial order of the records (spatial.hip): ids sorted by the Morton code of their centroid's
+// image-plane position under the scene camera, on the device (keys + rocPRIM radix sort), and
+// its inverse; synchronous on `stream`. Optional events bracket the build (timing).
+void BuildSpatialOrder(const float* d_vertices, std::uint64_t n, const Camera& camera, unsigned* d_order,
+                       unsigned* d_rank, hipStream_t stream, hipEvent_t ev_begin = nullptr,
+                       hipEvent_t ev_end = nullptr);
+
 // Element-wise IEEE binary16 <-> binary32 conversion on the device (ML_FLOAT16 images):
 // float -> half rounds to nearest even (overflow -> inf, NaN stays NaN); half -> float is exact.
 // `half` buffers are uint16 bit patterns on the host side.

@@ -836,7 +836,7 @@ struct PacketPixel {
 // range pixels p = 64 j + lane, p < nc * nr, at (c0 + p % nc, r0 + p / nc). p / nc is
 // (p * m) >> 17 with m = ceil(2^17 / nc): exact, because p < 1088 and nc <= 64 keep
 // p * (m - 2^17 / nc) / 2^17 < 1/nc (and p * m < 2^24 * 2^24 fits v_mul_u32_u24's low word,
-// p * m < 2^32). Lanes past the range address valid table entries but are not `in`.
+// p * m < 2^32). Lanes past the range are not `in` and address pixel 0.
 __device__ __forceinline__ unsigned PacketMagic(unsigned w) {
     const unsigned nc = ((w >> 6) & 63u) + 1u;
     return (131071u + nc) / nc;
@@ -854,7 +854,8 @@ __device__ __forceinline__ PacketPixel PacketLaneWord(unsigned w, unsigned m, in
     const unsigned pix4 = (w >> 28 << 8) | (static_cast<unsigned>(lane) << 2);
     const unsigned row_in = __umul24(pix4, m) >> 19;
     const unsigned col4 = pix4 - row_in * (nc * 4u) + c0 * 4u;  // 4 * column
-    return PacketPixel{((row_in + r0) << 9) + col4 * 2u, pix4 < nc * nr * 4u};
+    const bool in = pix4 < nc * nr * 4u;
+    return PacketPixel{in ? ((row_in + r0) << 9) + col4 * 2u : 0u, in};  // lanes past the range read pixel 0
 }
 
 __device__ __forceinline__ PacketHit EvalPacket(const float4& a, const float4& b, const float4& x, float2 f,
@@ -1401,10 +1402,29 @@ constexpr unsigned kItemRegular = 1u;
 constexpr unsigned kItemFull = 2u;
 constexpr int kOrderThreads = 1024;
 constexpr int kOrderPer = kMaxBinTiles / kOrderThreads;  // tiles per thread
+// Sum of v over the block (every thread gets it): a wave reduction, one word per wave in LDS.
+__device__ __forceinline__ unsigned long long BlockSum(unsigned long long v, unsigned long long* scratch) {
+    const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+        v += __shfl_xor(v, o);
+    }
+    if (lane == 0) {
+        scratch[wave] = v;
+    }
+    __syncthreads();
+    unsigned long long all = lane < kOrderThreads / kWave ? scratch[lane] : 0ull;
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+        all += __shfl_xor(all, o);
+    }
+    __syncthreads();  // scratch reusable
+    return all;
+}
+
 __global__ __launch_bounds__(kOrderThreads) void TileOrderKernel(BinParams p) {
     __shared__ unsigned start[64];
-    __shared__ unsigned long long wsum[kOrderThreads / kWave];
-    __shared__ unsigned wscan[kOrderThreads / kWave];
+    __shared__ unsigned long long scratch[kOrderThreads / kWave];
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
     const int wave = tid / kWave;
@@ -1413,15 +1433,15 @@ __global__ __launch_bounds__(kOrderThreads) void TileOrderKernel(BinParams p) {
     if (tid < 64) {
         start[tid] = 0u;
     }
-    // This thread's tiles t = tid + k * kOrderThreads: candidates (~0 = FULL stream); their
-    // sum in units of 64 candidates.
-    unsigned cand[kOrderPer], cnt[kOrderPer], ox[kOrderPer], oy[kOrderPer], reg[kOrderPer];
-    unsigned long long csum = 0ull;
+    // This thread's tiles t = tid + k * kOrderThreads: candidates (~0 = FULL stream) and facts.
+    unsigned cand[kOrderPer], cnt[kOrderPer], ox[kOrderPer], oy[kOrderPer], reg[kOrderPer], parts[kOrderPer];
+    unsigned long long csum = 0ull;  // in units of 64 candidates
 #pragma unroll
     for (int k = 0; k < kOrderPer; ++k) {
         const unsigned t = tid + k * kOrderThreads;
         cand[k] = 0u;
         cnt[k] = 0u;
+        parts[k] = 0u;
         if (t < tiles) {
             cnt[k] = p.counts[t];
             const TileInfo ti = p.tile_info[t];
@@ -1431,48 +1451,46 @@ __global__ __launch_bounds__(kOrderThreads) void TileOrderKernel(BinParams p) {
             const bool full = ti.usable == 0u || cnt[k] > p.capacity;
             cand[k] = full ? ~0u : cnt[k] + large;
             csum += full ? 0ull : (cnt[k] + large + 63u) / 64u;
+            const int rows_left = p.row_count - static_cast<int>(t / static_cast<unsigned>(p.tiles_x)) * kTileRows;
+            parts[k] = static_cast<unsigned>(min(kParts, (rows_left + kBlockRows - 1) / kBlockRows));
         }
     }
-#pragma unroll
-    for (int o = 1; o < kWave; o <<= 1) {
-        csum += __shfl_xor(csum, o);
-    }
-    if (lane == 0) {
-        wsum[wave] = csum;
-    }
-    __syncthreads();
-    // sum over tiles of ceil(candidates / 64): the 16 wave sums, one per lane, reduced
-    unsigned long long all = lane < kOrderThreads / kWave ? wsum[lane] : 0ull;
-#pragma unroll
-    for (int o = 1; o < kOrderThreads / kWave; o <<= 1) {
-        all += __shfl_xor(all, o);
-    }
-    // C = chunk x ceil(mean / chunk) >= mean candidates per tile, so sum_t ceil(c_t / C) <= 2 tiles.
-    const unsigned long long unit = static_cast<unsigned long long>(tiles) * (p.chunk / 64u);  // 64-candidate units
+    // C = chunk x ceil(mean / chunk) >= mean candidates per tile, so sum_t ceil(c_t / C) <= 2 tiles:
+    // at most CullBudget(tiles) = 2 x tiles x parts items and key slices.
+    const unsigned long long all = BlockSum(csum, scratch);
+    const unsigned long long unit = static_cast<unsigned long long>(tiles) * (p.chunk / 64u);
     const unsigned long long per = (all + unit - 1ull) / unit;
     const unsigned C = static_cast<unsigned>(min(p.chunk * (per < 1ull ? 1ull : per), 0x80000000ull));
-    // Chunks, bucket and items per tile; key slices for split tiles.
-    unsigned nch[kOrderPer], bucket[kOrderPer], items[kOrderPer];
+    unsigned nch[kOrderPer];
+    unsigned long long my_items = 0ull, my_slices = 0ull;
+#pragma unroll
+    for (int k = 0; k < kOrderPer; ++k) {
+        nch[k] = 1u;
+        if (cand[k] != ~0u && cand[k] != 0u) {
+            nch[k] = cand[k] / C + (cand[k] % C != 0u ? 1u : 0u);
+        }
+        my_items += static_cast<unsigned long long>(nch[k]) * parts[k];
+        my_slices += nch[k] > 1u ? static_cast<unsigned long long>(nch[k]) * kParts : 0ull;
+    }
+    // Guard (never expected to fire): a list past the trace grid or the key slices would lose
+    // work items; every tile part is then one unsplit item (<= tiles x parts, no slices).
+    const unsigned long long budget = 2ull * tiles * kParts;
+    const bool fits = BlockSum(my_items, scratch) <= budget && BlockSum(my_slices, scratch) <= budget;
+    unsigned bucket[kOrderPer];
     unsigned slices = 0u;
 #pragma unroll
     for (int k = 0; k < kOrderPer; ++k) {
-        const unsigned t = tid + k * kOrderThreads;
-        nch[k] = 1u;
-        bucket[k] = 0u;
-        items[k] = 0u;
-        if (t < tiles) {
-            const int rows_left = p.row_count - static_cast<int>(t / static_cast<unsigned>(p.tiles_x)) * kTileRows;
-            const unsigned parts = static_cast<unsigned>(min(kParts, (rows_left + kBlockRows - 1) / kBlockRows));
-            if (cand[k] == ~0u) {
-                bucket[k] = 63u;
-            } else if (cand[k] != 0u) {
-                nch[k] = cand[k] / C + (cand[k] % C != 0u ? 1u : 0u);
-                const unsigned w = cand[k] / nch[k] + (cand[k] % nch[k] != 0u ? 1u : 0u);
-                bucket[k] = 32u - __builtin_clz(w);
-            }
-            items[k] = nch[k] * parts;
-            slices += nch[k] > 1u ? nch[k] * kParts : 0u;
+        if (!fits) {
+            nch[k] = 1u;
         }
+        bucket[k] = 0u;
+        if (cand[k] == ~0u) {
+            bucket[k] = 63u;
+        } else if (cand[k] != 0u) {
+            const unsigned w = cand[k] / nch[k] + (cand[k] % nch[k] != 0u ? 1u : 0u);
+            bucket[k] = 32u - __builtin_clz(w);
+        }
+        slices += nch[k] > 1u ? nch[k] * kParts : 0u;
     }
     // Exclusive block scan of the slice counts (any order gives disjoint slices).
     unsigned incl = slices;
@@ -1482,12 +1500,12 @@ __global__ __launch_bounds__(kOrderThreads) void TileOrderKernel(BinParams p) {
         incl += lane >= o ? u : 0u;
     }
     if (lane == kWave - 1) {
-        wscan[wave] = incl;
+        scratch[wave] = incl;
     }
     __syncthreads();
-    unsigned wbase = lane < wave ? wscan[lane] : 0u;  // slices of the waves before this one
+    unsigned wbase = lane < wave ? static_cast<unsigned>(scratch[lane]) : 0u;  // slices of the waves before
 #pragma unroll
-    for (int o = 1; o < kOrderThreads / kWave; o <<= 1) {
+    for (int o = 1; o < kWave; o <<= 1) {
         wbase += __shfl_xor(wbase, o);
     }
     unsigned base = wbase + incl - slices;
@@ -1497,8 +1515,8 @@ __global__ __launch_bounds__(kOrderThreads) void TileOrderKernel(BinParams p) {
             p.slice_base[tid + k * kOrderThreads] = base;
             base += nch[k] * kParts;
         }
-        if (items[k] != 0u) {
-            atomicAdd(&start[bucket[k]], items[k]);
+        if (parts[k] != 0u) {
+            atomicAdd(&start[bucket[k]], nch[k] * parts[k]);
         }
     }
     __syncthreads();
@@ -1518,14 +1536,13 @@ __global__ __launch_bounds__(kOrderThreads) void TileOrderKernel(BinParams p) {
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < kOrderPer; ++k) {
-        if (items[k] != 0u) {
+        if (parts[k] != 0u) {
             const unsigned t = tid + k * kOrderThreads;
             const bool full = cand[k] == ~0u;
             const unsigned flags = (full ? kItemFull : 0u) | (reg[k] != 0u ? kItemRegular : 0u);
             const unsigned long long c_t = full ? 0ull : cand[k];
-            unsigned at = atomicAdd(&start[bucket[k]], items[k]);
-            const unsigned parts = items[k] / nch[k];
-            for (unsigned part = 0; part < parts; ++part) {
+            unsigned at = atomicAdd(&start[bucket[k]], nch[k] * parts[k]);
+            for (unsigned part = 0; part < parts[k]; ++part) {
                 for (unsigned c = 0; c < nch[k]; ++c) {
                     p.work[2 * at] = make_uint4(t * kParts + part, c | nch[k] << 16,
                                                 static_cast<unsigned>(c_t * c / nch[k]),

@@ -155,17 +155,30 @@ DeviceScene::DeviceScene(const Scene& scene, int device)
         m_vertices = DeviceAlloc<float>(m_n * 9, "hipMalloc(vertices)");
         m_albedo = DeviceAlloc<float>(m_n * 3, "hipMalloc(albedo)");
         m_edges = DeviceAlloc<float>(PaddedTriangleCount(m_n) * kEdgeFloatsPerTriangle, "hipMalloc(edges)");
-        const std::vector<std::uint32_t> order = SpatialOrder(scene);
-        std::vector<std::uint32_t> rank(order.size());
-        for (std::size_t i = 0; i < order.size(); ++i) {
-            rank[order[i]] = static_cast<std::uint32_t>(i);
-        }
         m_order = DeviceAlloc<unsigned>(m_n == 0 ? 1 : m_n, "hipMalloc(order)");
         m_rank = DeviceAlloc<unsigned>(m_n == 0 ? 1 : m_n, "hipMalloc(rank)");
-        HipCheck(hipMemcpy(m_order, order.data(), m_n * sizeof(unsigned), hipMemcpyHostToDevice), "hipMemcpy(order)");
-        HipCheck(hipMemcpy(m_rank, rank.data(), m_n * sizeof(unsigned), hipMemcpyHostToDevice), "hipMemcpy(rank)");
         HipCheck(hipMemcpy(m_vertices, scene.vertices.data(), m_n * 9 * sizeof(float), hipMemcpyHostToDevice),
                  "hipMemcpy(vertices)");
+        // The records' spatial order, built on the device (spatial.hip), timed.
+        hipEvent_t b0 = nullptr, b1 = nullptr;
+        HipCheck(hipEventCreate(&b0), "hipEventCreate(order build)");
+        if (hipEventCreate(&b1) != hipSuccess) {
+            (void)hipEventDestroy(b0);
+            throw std::runtime_error("HIP error: hipEventCreate(order build)");
+        }
+        try {
+            BuildSpatialOrder(m_vertices, m_n, m_camera, m_order, m_rank, nullptr, b0, b1);
+            float ms = 0.f;
+            if (m_n != 0 && hipEventElapsedTime(&ms, b0, b1) == hipSuccess) {
+                m_build_ms = ms;
+            }
+        } catch (...) {
+            (void)hipEventDestroy(b0);
+            (void)hipEventDestroy(b1);
+            throw;
+        }
+        (void)hipEventDestroy(b0);
+        (void)hipEventDestroy(b1);
         HipCheck(hipMemcpy(m_albedo, scene.albedo.data(), m_n * 3 * sizeof(float), hipMemcpyHostToDevice),
                  "hipMemcpy(albedo)");
     } catch (...) {

@@ -50,6 +50,9 @@ public:
                hipStream_t stream) const;
 
     std::size_t width() const { return m_width; }
+    // The spatial order (device, triangles entries) and the time its build took at load (ms).
+    const unsigned* order() const { return m_order; }
+    double build_ms() const { return m_build_ms; }
     std::size_t height() const { return m_height; }
 
     // Stage timing: while on, Prepare and Trace bind HIP events to their kernels' dispatch
@@ -72,8 +75,9 @@ private:
     float* m_vertices = nullptr;
     float* m_albedo = nullptr;
     float* m_edges = nullptr;
-    unsigned* m_order = nullptr;  // record ids in spatial order (SpatialOrder), for the cull bins
+    unsigned* m_order = nullptr;  // record ids in spatial order (BuildSpatialOrder), for the cull bins
     unsigned* m_rank = nullptr;   // its inverse: record id -> position
+    double m_build_ms = 0.0;      // spatial order build (BuildSpatialOrder) at load
     Frame m_frame{};
     std::size_t m_width = 0;
     std::size_t m_height = 0;

@@ -429,57 +429,6 @@ Scene MakeScene(int kind, std::uint64_t triangles, std::uint64_t seed, float siz
     }
 }
 
-std::vector<std::uint32_t> SpatialOrder(const Scene& scene) {
-    const Camera& c = scene.camera;
-    double f[3], r[3], u[3];
-    for (int k = 0; k < 3; ++k) {
-        f[k] = static_cast<double>(c.lookat[k]) - static_cast<double>(c.eye[k]);
-    }
-    const double up[3] = {c.up[0], c.up[1], c.up[2]};
-    r[0] = f[1] * up[2] - f[2] * up[1];
-    r[1] = f[2] * up[0] - f[0] * up[2];
-    r[2] = f[0] * up[1] - f[1] * up[0];
-    u[0] = r[1] * f[2] - r[2] * f[1];
-    u[1] = r[2] * f[0] - r[0] * f[2];
-    u[2] = r[0] * f[1] - r[1] * f[0];
-    const double fl = std::sqrt(f[0] * f[0] + f[1] * f[1] + f[2] * f[2]);
-    const double rl = std::sqrt(r[0] * r[0] + r[1] * r[1] + r[2] * r[2]);
-    const double ul = std::sqrt(u[0] * u[0] + u[1] * u[1] + u[2] * u[2]);
-    const double half_h = std::tan(static_cast<double>(c.vfov_deg) * 3.14159265358979323846 / 360.0);
-    const std::uint64_t n = scene.triangle_count();
-    std::vector<std::uint64_t> keyed(n);
-    for (std::uint64_t i = 0; i < n; ++i) {
-        const float* v = scene.vertices.data() + 9 * i;
-        double d[3];
-        for (int k = 0; k < 3; ++k) {
-            d[k] = (static_cast<double>(v[k]) + v[3 + k] + v[6 + k]) / 3.0 - c.eye[k];
-        }
-        const double z = (d[0] * f[0] + d[1] * f[1] + d[2] * f[2]) / fl;
-        std::uint64_t key = 0xFFFFFFFFull;
-        if (z > 0.0 && std::isfinite(z) && half_h > 0.0 && fl > 0.0 && rl > 0.0 && ul > 0.0) {
-            // image-plane coordinates in units of the half height, clamped to [-4, 4]
-            const double sx = (d[0] * r[0] + d[1] * r[1] + d[2] * r[2]) / rl / z / half_h;
-            const double sy = -(d[0] * u[0] + d[1] * u[1] + d[2] * u[2]) / ul / z / half_h;
-            const auto cell = [](double v) {
-                const double q = (std::fmin(std::fmax(v, -4.0), 4.0) + 4.0) / 8.0 * 65535.0;
-                return static_cast<std::uint32_t>(std::isfinite(q) ? q : 0.0);
-            };
-            const std::uint32_t qx = cell(sx), qy = cell(sy);
-            key = 0;
-            for (int b = 15; b >= 0; --b) {  // Morton interleave, y bit above x bit
-                key = (key << 2) | (((qy >> b) & 1u) << 1) | ((qx >> b) & 1u);
-            }
-        }
-        keyed[i] = (key << 32) | i;  // ties (and the behind-eye key) keep id order
-    }
-    std::sort(keyed.begin(), keyed.end());
-    std::vector<std::uint32_t> order(n);
-    for (std::uint64_t i = 0; i < n; ++i) {
-        order[i] = static_cast<std::uint32_t>(keyed[i] & 0xFFFFFFFFull);
-    }
-    return order;
-}
-
 Frame MakeFrame(const Camera& c, std::size_t width, std::size_t height) {
     double f[3], r[3], u[3];
     for (int k = 0; k < 3; ++k) {

@@ -58,12 +58,6 @@ void SaveScene(const Scene& scene, const std::string& path);
 // implementation-defined). `size` is the soup half-extent s (0 = kind default).
 Scene MakeScene(int kind, std::uint64_t triangles, std::uint64_t seed, float size);
 
-// Record ids sorted by the screen position of their centroids (Morton order of the view
-// direction's image-plane coordinates; triangles at or behind the eye plane last). The
-// binning pass walks records in this order so that neighbouring threads touch the same
-// tiles; any order gives the same frame.
-std::vector<std::uint32_t> SpatialOrder(const Scene& scene);
-
 // Camera -> affine frame for a W x H image. Computed in double, rounded once to float.
 Frame MakeFrame(const Camera& camera, std::size_t width, std::size_t height);
 

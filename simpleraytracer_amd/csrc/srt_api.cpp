@@ -171,6 +171,28 @@ ML_API_ENTRY unsigned long long srtDeviceSceneTriangles(srt_device_scene scene) 
     return scene == nullptr ? 0ULL : FromHandle(scene)->triangles();
 }
 
+ML_API_ENTRY int srtDeviceSceneOrder(srt_device_scene scene, unsigned* order, unsigned long long capacity,
+                                     double* build_ms) {
+    return Guarded([&] {
+        if (scene == nullptr) {
+            throw std::runtime_error("Bad scene handle");
+        }
+        srt::DeviceScene* s = FromHandle(scene);
+        if (order != nullptr) {
+            if (capacity < s->triangles()) {
+                throw std::runtime_error("Buffer too small: " + std::to_string(capacity) + " entries for " +
+                                         std::to_string(s->triangles()));
+            }
+            Bind bind(s->device());
+            srt::HipCheck(hipMemcpy(order, s->order(), s->triangles() * sizeof(unsigned), hipMemcpyDeviceToHost),
+                          "hipMemcpy(order)");
+        }
+        if (build_ms != nullptr) {
+            *build_ms = s->build_ms();
+        }
+    });
+}
+
 ML_API_ENTRY int srtPrepareAsync(srt_device_scene scene, size_t width, size_t height, void* stream) {
     return Guarded([&] {
         if (scene == nullptr) {

@@ -159,6 +159,16 @@ class DeviceScene:
         _check(self._lib.srtShadeAsync(self.handle, _ptr(offsets), _ptr(ids), _ptr(rgba), row_begin, row_count,
                                        _stream(stream)))
 
+    def spatial_order(self):
+        """(order, build_ms): the record ids in spatial order (numpy uint32), built on the device
+        at load, and the build's device time."""
+        import numpy as np
+
+        out = np.empty(max(1, self.triangles), np.uint32)
+        ms = ctypes.c_double()
+        _check(self._lib.srtDeviceSceneOrder(self.handle, out.ctypes.data, out.size, ctypes.byref(ms)))
+        return out[:self.triangles], ms.value
+
     def set_stage_timing(self, enable: bool = True):
         """Bind HIP events to the prepare, bin and trace kernels' dispatches (no extra packets)."""
         _check(self._lib.srtSetStageTiming(self.handle, 1 if enable else 0))
