@@ -96,11 +96,11 @@ struct CullBins {
     unsigned* counts;      // tiles + 1: list lengths, then the large-list length
     unsigned* lists;       // tiles x capacity candidate ids (BinTrianglesKernel)
     unsigned* large_list;  // PaddedTriangleCount(n) ids binned to every tile
-    void* work;            // trace work list (TileOrderKernel): up to 2 x tiles x parts items, 8 B each
+    void* work;            // trace work list (TileOrderKernel): tiles x parts descriptors, 32 B each
     unsigned* work_count;  // its length
-    unsigned* slice_base;  // tiles: first key slice of a split tile
-    unsigned* arrive;      // tiles x parts: split items finished (self-resetting counters)
-    void* split_keys;      // key slices of split items: 8 KiB each, as many as work items
+    unsigned* arrive;      // tiles x parts: split chunks finished (self-resetting counters)
+    void* split_keys;      // key slices of split parts: tiles x parts x max_chunks, 8 KiB each
+    unsigned max_chunks;   // M = CullMaxChunks(tiles)
     void* bounds;          // (tiles_x + tiles_y) float2: monotone tile column / row bounds
     unsigned capacity;
     std::size_t tiles;
@@ -115,6 +115,12 @@ bool CullBinnable(std::size_t width, std::size_t row_count);
 // Per-tile list capacity for n triangles (a list that overflows makes its tile stream every
 // record; results are unaffected). Env SRT_CULL_BIN_CAP overrides it (tests).
 unsigned CullBinCapacity(std::uint64_t n, std::size_t tiles);
+
+// Split width of a band's trace: a tile part's candidates go to at most M blocks (chunks), M =
+// ceil(resident trace blocks of the device / tile parts), 1 when the parts alone fill the chip,
+// at most kMaxChunks; env SRT_CULL_CHUNKS forces M (tests, measurement).
+constexpr int kMaxChunks = 16;
+unsigned CullMaxChunks(std::size_t tiles);
 
 // Bytes of the bin work buffer for n triangles and a band shape, and its carve-up.
 std::size_t CullBinBytes(std::uint64_t n, std::size_t width, std::size_t row_count);

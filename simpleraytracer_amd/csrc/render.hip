@@ -74,11 +74,12 @@ struct TraceParams {
     const TileInfo* __restrict__ tile_info;   // per tile: ray box, uniform offset (TileInfoKernel)
     const CullRecord* __restrict__ cull;      // cull records in spatial order (the lists hold positions)
     const unsigned* __restrict__ order;       // spatial-order position -> record id
-    const uint4* __restrict__ work;           // block -> work item (2 x uint4), most work first (TileOrderKernel)
-    const unsigned* __restrict__ work_count;  // [0]: work items (blocks past it exit)
-    const unsigned* __restrict__ slice_base;  // split tiles: first key slice
-    unsigned long long* __restrict__ split_keys;  // key slices of split work items (kBlockRows x 64 each)
-    unsigned* __restrict__ arrive;            // per (tile, part): split items finished (self-resetting)
+    const uint4* __restrict__ work;           // tile parts (2 x uint4 each), most work first (TileOrderKernel)
+    const unsigned* __restrict__ work_count;  // [0]: tile parts listed
+    unsigned long long* __restrict__ split_keys;  // key slices of split parts: (part, chunk), kBlockRows x 64 each
+    unsigned* __restrict__ arrive;            // per (tile, part): chunks finished (self-resetting)
+    unsigned max_chunks;                      // M: a part's candidates split into at most M chunks
+    unsigned chunk;                           // ... of at least this many candidates each
     const unsigned* __restrict__ bin_lists;   // per tile: candidate ids (BinTrianglesKernel)
     const unsigned* __restrict__ bin_counts;  // per tile: list length; [tiles]: large-list length
     const unsigned* __restrict__ large_list;  // ids of records binned to every tile
@@ -1212,12 +1213,10 @@ struct BinParams {
     unsigned* __restrict__ counts;      // tiles + 1 (the last one: large list)
     unsigned* __restrict__ lists;       // tiles x capacity
     unsigned* __restrict__ large_list;  // n_pad
-    uint4* __restrict__ work;           // trace work list (TileOrderKernel): 2 x uint4 per item
-    unsigned* __restrict__ work_count;  // [0]: work items
-    unsigned* __restrict__ slice_base;  // per split tile: first key slice (TileOrderKernel)
+    uint4* __restrict__ work;           // trace work list (TileOrderKernel): 2 x uint4 per tile part
+    unsigned* __restrict__ work_count;  // [0]: tile parts listed
     float2* __restrict__ bounds;        // tiles_x + tiles_y monotone tile column / row bounds (TileBoundsKernel)
     unsigned capacity;
-    unsigned chunk;                     // candidates per trace work item (at least; TileOrderKernel)
     unsigned n;
     unsigned exp;  // diagnostic build: experiment bits (env SRT_EXP), 0 in the product
     int tiles_x;
@@ -1386,45 +1385,20 @@ __device__ __forceinline__ int LastLoAtMost(const float2* b, int n, float v) {
 // the block counts its (tile, record) pairs in an LDS histogram, reserves each touched
 // tile's share of its list with ONE global atomic, then writes the ids. (Per-pair global
 // atomics serialise on the busy tiles' counters at the memory side.)
-// Trace work list: one block after the bin kernel. A tile's candidates (its list plus the
-// large list) are cut into chunks of at most C, C = chunk x ceil(mean candidates per tile /
-// chunk), so no trace block walks more than C of them: a heavy tile becomes several work
-// items over the same pixels (merged by the last to finish, TraceCullKernel), while the
-// number of items stays <= 2 x tiles x parts, the trace grid. Items are listed longest first
-// (counting sort by the log2 of candidates per item, FULL-stream tiles first), so the heavy
-// ones start first and the light ones fill in behind them. Split tiles get consecutive key
-// slices (slice_base, an exclusive scan over the tiles). Order within a bucket is arbitrary:
-// the frame does not depend on it.
-// Work item of the binned trace (TileOrderKernel), 32 B: w0 = (tile part, chunk | chunks << 16,
-// candidate range begin, end), w1 = (tile list length, sample offset x, y of the tile's first
-// ray, flags: 1 = every ray of the tile has that offset, 2 = FULL stream).
+// Trace work list: one block after the bin kernel. One 32-B descriptor per tile part, listed
+// longest first (counting sort by the log2 of the tile's candidates, FULL-stream tiles first),
+// so the heavy parts start first and the light ones fill in behind them; order within a bucket
+// is arbitrary (the frame does not depend on it). The trace grid is parts x M blocks: block b
+// runs chunk b % M of part b / M (TraceCullKernel splits a part's candidates into at most M
+// chunks of at least `chunk` candidates; the chunks past a part's count exit at once).
+// Descriptor: w0 = (tile part, candidates, tile list length, flags), w1 = (sample offset x, y of
+// the tile's first ray, 0, 0); flags: 1 = every ray of the tile has that offset, 2 = FULL.
 constexpr unsigned kItemRegular = 1u;
 constexpr unsigned kItemFull = 2u;
 constexpr int kOrderThreads = 1024;
 constexpr int kOrderPer = kMaxBinTiles / kOrderThreads;  // tiles per thread
-// Sum of v over the block (every thread gets it): a wave reduction, one word per wave in LDS.
-__device__ __forceinline__ unsigned long long BlockSum(unsigned long long v, unsigned long long* scratch) {
-    const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
-#pragma unroll
-    for (int o = 1; o < kWave; o <<= 1) {
-        v += __shfl_xor(v, o);
-    }
-    if (lane == 0) {
-        scratch[wave] = v;
-    }
-    __syncthreads();
-    unsigned long long all = lane < kOrderThreads / kWave ? scratch[lane] : 0ull;
-#pragma unroll
-    for (int o = 1; o < kWave; o <<= 1) {
-        all += __shfl_xor(all, o);
-    }
-    __syncthreads();  // scratch reusable
-    return all;
-}
-
 __global__ __launch_bounds__(kOrderThreads) void TileOrderKernel(BinParams p) {
     __shared__ unsigned start[64];
-    __shared__ unsigned long long scratch[kOrderThreads / kWave];
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
     const int wave = tid / kWave;
@@ -1433,94 +1407,35 @@ __global__ __launch_bounds__(kOrderThreads) void TileOrderKernel(BinParams p) {
     if (tid < 64) {
         start[tid] = 0u;
     }
-    // This thread's tiles t = tid + k * kOrderThreads: candidates (~0 = FULL stream) and facts.
-    unsigned cand[kOrderPer], cnt[kOrderPer], ox[kOrderPer], oy[kOrderPer], reg[kOrderPer], parts[kOrderPer];
-    unsigned long long csum = 0ull;  // in units of 64 candidates
+    // This thread's tiles t = tid + k * kOrderThreads.
+    unsigned cand[kOrderPer], cnt[kOrderPer], ox[kOrderPer], oy[kOrderPer], flags[kOrderPer], parts[kOrderPer],
+        bucket[kOrderPer];
 #pragma unroll
     for (int k = 0; k < kOrderPer; ++k) {
         const unsigned t = tid + k * kOrderThreads;
-        cand[k] = 0u;
-        cnt[k] = 0u;
         parts[k] = 0u;
         if (t < tiles) {
             cnt[k] = p.counts[t];
             const TileInfo ti = p.tile_info[t];
             ox[k] = __float_as_uint(ti.ox);
             oy[k] = __float_as_uint(ti.oy);
-            reg[k] = ti.regular;
             const bool full = ti.usable == 0u || cnt[k] > p.capacity;
-            cand[k] = full ? ~0u : cnt[k] + large;
-            csum += full ? 0ull : (cnt[k] + large + 63u) / 64u;
+            flags[k] = (full ? kItemFull : 0u) | (ti.regular != 0u ? kItemRegular : 0u);
+            cand[k] = full ? 0u : cnt[k] + large;
+            bucket[k] = full ? 63u : (cand[k] == 0u ? 0u : 32u - __builtin_clz(cand[k]));
             const int rows_left = p.row_count - static_cast<int>(t / static_cast<unsigned>(p.tiles_x)) * kTileRows;
             parts[k] = static_cast<unsigned>(min(kParts, (rows_left + kBlockRows - 1) / kBlockRows));
         }
     }
-    // C = chunk x ceil(mean / chunk) >= mean candidates per tile, so sum_t ceil(c_t / C) <= 2 tiles:
-    // at most CullBudget(tiles) = 2 x tiles x parts items and key slices.
-    const unsigned long long all = BlockSum(csum, scratch);
-    const unsigned long long unit = static_cast<unsigned long long>(tiles) * (p.chunk / 64u);
-    const unsigned long long per = (all + unit - 1ull) / unit;
-    const unsigned C = static_cast<unsigned>(min(p.chunk * (per < 1ull ? 1ull : per), 0x80000000ull));
-    unsigned nch[kOrderPer];
-    unsigned long long my_items = 0ull, my_slices = 0ull;
+    __syncthreads();  // start[] zeroed
 #pragma unroll
     for (int k = 0; k < kOrderPer; ++k) {
-        nch[k] = 1u;
-        if (cand[k] != ~0u && cand[k] != 0u) {
-            nch[k] = cand[k] / C + (cand[k] % C != 0u ? 1u : 0u);
-        }
-        my_items += static_cast<unsigned long long>(nch[k]) * parts[k];
-        my_slices += nch[k] > 1u ? static_cast<unsigned long long>(nch[k]) * kParts : 0ull;
-    }
-    // Guard (never expected to fire): a list past the trace grid or the key slices would lose
-    // work items; every tile part is then one unsplit item (<= tiles x parts, no slices).
-    const unsigned long long budget = 2ull * tiles * kParts;
-    const bool fits = BlockSum(my_items, scratch) <= budget && BlockSum(my_slices, scratch) <= budget;
-    unsigned bucket[kOrderPer];
-    unsigned slices = 0u;
-#pragma unroll
-    for (int k = 0; k < kOrderPer; ++k) {
-        if (!fits) {
-            nch[k] = 1u;
-        }
-        bucket[k] = 0u;
-        if (cand[k] == ~0u) {
-            bucket[k] = 63u;
-        } else if (cand[k] != 0u) {
-            const unsigned w = cand[k] / nch[k] + (cand[k] % nch[k] != 0u ? 1u : 0u);
-            bucket[k] = 32u - __builtin_clz(w);
-        }
-        slices += nch[k] > 1u ? nch[k] * kParts : 0u;
-    }
-    // Exclusive block scan of the slice counts (any order gives disjoint slices).
-    unsigned incl = slices;
-#pragma unroll
-    for (int o = 1; o < kWave; o <<= 1) {
-        const unsigned u = __shfl_up(incl, o);
-        incl += lane >= o ? u : 0u;
-    }
-    if (lane == kWave - 1) {
-        scratch[wave] = incl;
-    }
-    __syncthreads();
-    unsigned wbase = lane < wave ? static_cast<unsigned>(scratch[lane]) : 0u;  // slices of the waves before
-#pragma unroll
-    for (int o = 1; o < kWave; o <<= 1) {
-        wbase += __shfl_xor(wbase, o);
-    }
-    unsigned base = wbase + incl - slices;
-#pragma unroll
-    for (int k = 0; k < kOrderPer; ++k) {
-        if (nch[k] > 1u) {
-            p.slice_base[tid + k * kOrderThreads] = base;
-            base += nch[k] * kParts;
-        }
         if (parts[k] != 0u) {
-            atomicAdd(&start[bucket[k]], nch[k] * parts[k]);
+            atomicAdd(&start[bucket[k]], parts[k]);
         }
     }
     __syncthreads();
-    if (wave == 0) {  // bucket b's first item: the items in heavier buckets (suffix sum, exclusive)
+    if (wave == 0) {  // bucket b's first slot: the parts in heavier buckets (suffix sum, exclusive)
         const unsigned c = start[lane];
         unsigned suf = c;
 #pragma unroll
@@ -1538,18 +1453,10 @@ __global__ __launch_bounds__(kOrderThreads) void TileOrderKernel(BinParams p) {
     for (int k = 0; k < kOrderPer; ++k) {
         if (parts[k] != 0u) {
             const unsigned t = tid + k * kOrderThreads;
-            const bool full = cand[k] == ~0u;
-            const unsigned flags = (full ? kItemFull : 0u) | (reg[k] != 0u ? kItemRegular : 0u);
-            const unsigned long long c_t = full ? 0ull : cand[k];
-            unsigned at = atomicAdd(&start[bucket[k]], nch[k] * parts[k]);
+            const unsigned at = atomicAdd(&start[bucket[k]], parts[k]);
             for (unsigned part = 0; part < parts[k]; ++part) {
-                for (unsigned c = 0; c < nch[k]; ++c) {
-                    p.work[2 * at] = make_uint4(t * kParts + part, c | nch[k] << 16,
-                                                static_cast<unsigned>(c_t * c / nch[k]),
-                                                static_cast<unsigned>(c_t * (c + 1u) / nch[k]));
-                    p.work[2 * at + 1] = make_uint4(cnt[k], ox[k], oy[k], flags);
-                    ++at;
-                }
+                p.work[2 * (at + part)] = make_uint4(t * kParts + part, cand[k], cnt[k], flags[k]);
+                p.work[2 * (at + part) + 1] = make_uint4(ox[k], oy[k], 0u, 0u);
             }
         }
     }
@@ -1725,22 +1632,33 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(T
     float ox = 0.f, oy = 0.f;
     CullSource src{nullptr, nullptr, 0u, 0u, 0u, true};
     if (p.work != nullptr) {
-        if (blockIdx.x >= p.work_count[0]) {
+        const unsigned d = blockIdx.x / p.max_chunks;
+        chunk = blockIdx.x % p.max_chunks;
+        if (d >= p.work_count[0]) {
             return;
         }
-        const uint4 w0 = p.work[2 * blockIdx.x], w1 = p.work[2 * blockIdx.x + 1];
+        const uint4 w0 = p.work[2 * d], w1 = p.work[2 * d + 1];
         item = w0.x;
-        chunk = w0.y & 0xFFFFu;
-        nchunks = w0.y >> 16;
-        flags = w1.w;
-        ox = __uint_as_float(w1.y);
-        oy = __uint_as_float(w1.z);
-        src.list = p.bin_lists + static_cast<size_t>(item / kParts) * p.bin_capacity;
-        src.list2 = p.large_list;
-        src.count1 = w1.x;
-        src.begin = w0.z;
-        src.end = w0.w;
+        flags = w0.w;
+        ox = __uint_as_float(w1.x);
+        oy = __uint_as_float(w1.y);
         src.full = (flags & kItemFull) != 0u;
+        if (!src.full) {
+            // candidates cut into n <= M chunks of >= p.chunk: chunk c = [c q + c r / n, ...), q r = c_t / n, % n
+            const unsigned c_t = w0.y;
+            nchunks = min(p.max_chunks, max(1u, c_t / p.chunk + (c_t % p.chunk != 0u ? 1u : 0u)));
+            if (chunk >= nchunks) {
+                return;
+            }
+            const unsigned q = c_t / nchunks, r = c_t % nchunks;
+            src.list = p.bin_lists + static_cast<size_t>(item / kParts) * p.bin_capacity;
+            src.list2 = p.large_list;
+            src.count1 = w0.z;
+            src.begin = chunk * q + chunk * r / nchunks;
+            src.end = (chunk + 1u) * q + (chunk + 1u) * r / nchunks;
+        } else if (chunk != 0u) {
+            return;
+        }
     } else {
         item = blockIdx.y * gridDim.x + blockIdx.x;
     }
@@ -1933,8 +1851,7 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(T
         // stores, every storing wave's vmcnt(0), barrier, one agent-scope add; the last
         // adder's block loads sc1 after a barrier).
         constexpr int kPix = kBlockRows * kWave;
-        unsigned long long* slices =
-            p.split_keys + static_cast<size_t>(p.slice_base[tile] + (item % kParts) * nchunks) * kPix;
+        unsigned long long* slices = p.split_keys + static_cast<size_t>(item) * p.max_chunks * kPix;
         const int pix = wave * R * kWave + lane;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
@@ -2245,8 +2162,8 @@ bool EnvFlag(const char* name, bool dflt) {
     return v == nullptr || *v == '\0' ? dflt : std::strcmp(v, "0") != 0;
 }
 
-// Candidates per trace work item (TileOrderKernel's smallest chunk); env SRT_CULL_CHUNK, a
-// multiple of 64 (default 256: one packet-walk batch).
+// Smallest candidate chunk of a split tile part; env SRT_CULL_CHUNK, a multiple of 64 (default
+// 256: one packet-walk batch).
 unsigned CullChunkFromEnv() {
     const char* v = std::getenv("SRT_CULL_CHUNK");
     const long c = v == nullptr || *v == '\0' ? 256 : std::strtol(v, nullptr, 10);
@@ -2426,35 +2343,58 @@ unsigned CullBinCapacity(std::uint64_t n, std::size_t tiles) {
 }
 
 namespace {
-// Trace work items of a band: at most 2 x (tiles x parts) (TileOrderKernel's chunk choice).
-std::size_t CullBudget(std::size_t tiles) { return 2 * tiles * kParts; }
-
 struct BinSizes {
-    std::size_t info, counts, lists, large, work, work_count, slice_base, arrive, split_keys, bounds;
+    std::size_t info, counts, lists, large, work, work_count, arrive, split_keys, bounds;
 };
 BinSizes CullBinSizes(std::uint64_t n, std::size_t width, std::size_t row_count) {
     const std::size_t tx = (width + kWave - 1) / kWave, ty = (row_count + kTileRows - 1) / kTileRows;
     const std::size_t tiles = tx * ty;
     const auto al = [](std::size_t b) { return (b + 255) / 256 * 256; };
+    const unsigned m = CullMaxChunks(tiles);
     BinSizes z;
     z.info = al(tiles * sizeof(TileInfo));
     z.counts = al((tiles + 1) * 4);
     z.lists = al(tiles * static_cast<std::size_t>(CullBinCapacity(n, tiles)) * 4);
     z.large = al(PaddedTriangleCount(n) * 4);
-    z.work = al(CullBudget(tiles) * 2 * sizeof(uint4));
+    z.work = al(tiles * kParts * 2 * sizeof(uint4));
     z.work_count = al(4);
-    z.slice_base = al(tiles * 4);
     z.arrive = al(tiles * kParts * 4);
-    z.split_keys = al(CullBudget(tiles) * kBlockRows * kWave * 8);
+    z.split_keys = m > 1 ? al(tiles * kParts * m * kBlockRows * kWave * 8) : 0;
     z.bounds = al((tx + ty) * 8);
     return z;
 }
 }  // namespace
 
+unsigned CullMaxChunks(std::size_t tiles) {
+    if (const char* v = std::getenv("SRT_CULL_CHUNKS")) {  // measurement / tests: force the split width
+        const long m = std::strtol(v, nullptr, 10);
+        if (m > 0) {
+            return static_cast<unsigned>(m < kMaxChunks ? m : kMaxChunks);
+        }
+    }
+    // Resident trace blocks of the device (all CUs x blocks per CU), queried once per device.
+    static thread_local int cached_device = -1;
+    static thread_local unsigned slots = 0;
+    int dev = 0;
+    if (hipGetDevice(&dev) == hipSuccess && dev != cached_device) {
+        int per_cu = 0, cus = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, TraceCullKernel, kCullThreads, 0) == hipSuccess &&
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess) {
+            slots = static_cast<unsigned>(per_cu * cus);
+            cached_device = dev;
+        }
+    }
+    const std::size_t items = tiles * kParts;
+    if (items == 0 || slots <= items) {
+        return 1u;  // the parts alone fill the chip: no split
+    }
+    const std::size_t m = (slots + items - 1) / items;
+    return static_cast<unsigned>(m < static_cast<std::size_t>(kMaxChunks) ? m : kMaxChunks);
+}
+
 std::size_t CullBinBytes(std::uint64_t n, std::size_t width, std::size_t row_count) {
     const BinSizes z = CullBinSizes(n, width, row_count);
-    return z.info + z.counts + z.lists + z.large + z.work + z.work_count + z.slice_base + z.arrive + z.split_keys +
-           z.bounds;
+    return z.info + z.counts + z.lists + z.large + z.work + z.work_count + z.arrive + z.split_keys + z.bounds;
 }
 
 CullBins CullBinLayout(void* base, std::uint64_t n, std::size_t width, std::size_t row_count) {
@@ -2472,12 +2412,12 @@ CullBins CullBinLayout(void* base, std::uint64_t n, std::size_t width, std::size
     b.large_list = reinterpret_cast<unsigned*>(take(z.large));
     b.work = take(z.work);
     b.work_count = reinterpret_cast<unsigned*>(take(z.work_count));
-    b.slice_base = reinterpret_cast<unsigned*>(take(z.slice_base));
     b.arrive = reinterpret_cast<unsigned*>(take(z.arrive));
     b.split_keys = take(z.split_keys);
     b.bounds = take(z.bounds);
     b.tiles = CullTiles(width, row_count);
     b.capacity = CullBinCapacity(n, b.tiles);
+    b.max_chunks = z.split_keys != 0 ? CullMaxChunks(b.tiles) : 1u;
     return b;
 }
 
@@ -2570,7 +2510,6 @@ hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_ver
             b.large_list = bins->large_list;
             b.work = static_cast<uint4*>(bins->work);
             b.work_count = bins->work_count;
-            b.slice_base = bins->slice_base;
             // Tile bounds once per frame (TileBoundsKernel) when the bin blocks' own reductions
             // would cost more: (bin blocks) x (tiles) tile-info reads above 200k (C5: 16M, bin
             // stage 164 -> 75 us; C3: 0.4M, where the extra launch adds ~1 % to one frame's
@@ -2583,7 +2522,6 @@ hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_ver
                 b.bounds = once ? static_cast<float2*>(bins->bounds) : nullptr;
             }
             b.capacity = bins->capacity;
-            b.chunk = CullChunkFromEnv();
             b.n = static_cast<unsigned>(n);
             b.tiles_x = static_cast<int>(gx);
             b.tiles_y = static_cast<int>(gy);
@@ -2622,7 +2560,8 @@ hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_ver
             p.order = bins->order;
             p.work = b.work;
             p.work_count = b.work_count;
-            p.slice_base = b.slice_base;
+            p.max_chunks = bins->max_chunks;
+            p.chunk = CullChunkFromEnv();
             p.split_keys = static_cast<unsigned long long*>(bins->split_keys);
             p.arrive = bins->arrive;
             p.bin_lists = bins->lists;
@@ -2634,7 +2573,7 @@ hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_ver
         p.tiles = gx * gy;
         if (p.work != nullptr) {
             // Binned: one block per work item of TileOrderKernel's list (at most the budget).
-            Launch(TraceCullKernel, dim3(static_cast<unsigned>(CullBudget(p.tiles))),
+            Launch(TraceCullKernel, dim3(static_cast<unsigned>(p.tiles * kParts * p.max_chunks)),
                    dim3(kWave * kCullWaves), stream, ev.begin, ev.end, p);
         } else {
             // One block per (tile, part): gridDim.x = tile columns, gridDim.y = tile rows x parts.

@@ -291,11 +291,12 @@ void DeviceScene::Trace(const float* d_offsets, float* d_rgba, std::size_t row_b
             m_cull_bytes = bytes;
             m_cull_shape = 0;
         }
+        // A new carve-up (band shape, or the split width and so the layout): zero it.
         const std::uint64_t shape = (static_cast<std::uint64_t>(m_width) << 32) | row_count;
-        if (shape != m_cull_shape) {
-            // A new carve-up: zero it so the self-resetting counters start at 0.
+        if (shape != m_cull_shape || bytes != m_cull_layout) {
             HipCheck(hipMemsetAsync(m_cull_work, 0, bytes, stream), "hipMemsetAsync(cull work)");
             m_cull_shape = shape;
+            m_cull_layout = bytes;
         }
         bins = CullBinLayout(m_cull_work, m_n, m_width, row_count);
         bins.order = m_order;

@@ -563,8 +563,8 @@ def test_concurrent_frame_queues(gpu, scenes, variant):
         scene.close()
 
 
-@pytest.mark.parametrize("chunk", ["64", ""])
-def test_split_items_across_frames(gpu, scenes, monkeypatch, chunk):
+@pytest.mark.parametrize("chunk,chunks", [("64", ""), ("", ""), ("128", "16")])
+def test_split_items_across_frames(gpu, scenes, monkeypatch, chunk, chunks):
     """Split work items (a heavy tile part cut into candidate chunks, merged by the last chunk
     through global key slices): frames traced back to back on one scene and stream, each with
     different per-pixel jitter, equal fresh single-frame renders bit for bit -- no key slice or
@@ -574,6 +574,7 @@ def test_split_items_across_frames(gpu, scenes, monkeypatch, chunk):
     import simpleraytracer_amd as srt
 
     monkeypatch.setenv("SRT_CULL_CHUNK", chunk)
+    monkeypatch.setenv("SRT_CULL_CHUNKS", chunks)
     w, h = 640, 360
     rng = np.random.default_rng(77)
     offs = [rng.random((h, w, 2), dtype=np.float32) for _ in range(3)] + \
@@ -737,3 +738,17 @@ def test_device_spatial_order_edge_scene(gpu, tmp_path):
     order, _ = scene.spatial_order()
     scene.close()
     assert np.array_equal(order, morton_order_numpy(str(path)))
+
+
+@pytest.mark.parametrize("chunks", ["1", "4", "16"])
+def test_split_width_full_frame_bitwise(gpu, scenes, monkeypatch, chunks):
+    """The headline frame with every tile part split into up to M candidate chunks (forced M;
+    the default M is 1 at 1080p, where the parts alone fill the chip) equals brute force bit for
+    bit, uniform and jittered offsets."""
+    rng = np.random.default_rng(9)
+    for offs in (None, rng.random((1080, 1920, 2), dtype=np.float32)):
+        monkeypatch.delenv("SRT_CULL_CHUNKS", raising=False)
+        ref = torch_render(scenes["soup100k"], 1920, 1080, offs, variant="lds")
+        monkeypatch.setenv("SRT_CULL_CHUNKS", chunks)
+        got = torch_render(scenes["soup100k"], 1920, 1080, offs, variant="cull")
+        assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
