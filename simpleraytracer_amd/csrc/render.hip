@@ -744,14 +744,18 @@ constexpr int kCullR = kBlockRows / kCullWaves;  // rays per lane
 #define SRT_PACKET_ILP 2  // packet walk: packets evaluated together per wave (independent chains)
 #endif
 constexpr int kPacketBatch = SRT_PACKET_BATCH;  // candidates gathered per packet-walk batch
-constexpr int kSlices = kPacketBatch / kCullThreads;  // batch entries per thread
+constexpr int kSlices = (kPacketBatch + kCullThreads - 1) / kCullThreads;  // batch entries per thread
 constexpr int kStreamStep = kCullThreads;        // FULL stream: records per block per step
-static_assert(kPacketBatch % kCullThreads == 0 && kPacketBatch <= 256, "packet word: survivor slot < 256");
+static_assert((kPacketBatch % kCullThreads == 0 || kCullThreads % kPacketBatch == 0) && kPacketBatch <= 256,
+              "whole slices (or a part of the threads); packet word: survivor slot < 256");
 static_assert(kBlockRows <= 16 && kBlockRows % kCullWaves == 0, "packet word: rows < 16");
 static_assert(kPadTriangles % kStreamStep == 0, "a stream step must cover whole pad units");
 
+// Batch entry of thread tid's slice e (kPacketBatch < kCullThreads: the first threads only).
+__device__ __forceinline__ bool InBatch(int e, int tid) { return e * kCullThreads + tid < kPacketBatch; }
+
 struct CullShared {
-    float4 sv0[kPacketBatch];  // compacted survivors: plane 0
+    float4 sv0[kPacketBatch];  // compacted survivors: plane 0 (sv0, sv1 adjacent: PacketTables scratch)
     float4 sv1[kPacketBatch];  //                      plane 1
     union {
         float4 sv2[kPacketBatch];  //                  (cyC, vol, id, packed pixel range)
@@ -769,7 +773,7 @@ struct CullShared {
     unsigned last;  // split work item: this block arrived last
     unsigned long long keys[kBlockRows][kWave];  // per-pixel lexicographic (t, id) keys
 };
-static_assert(sizeof(float2) * kWave * kCullWaves <= sizeof(float4) * kPacketBatch, "PacketTables scratch");
+static_assert(sizeof(float2) * kWave * kCullWaves <= sizeof(float4) * 2 * kPacketBatch, "PacketTables scratch");
 static_assert((kPacketBatch + kStreamStep) * 4 <= sizeof(float4) * kPacketBatch, "stream ids alias sv2");
 constexpr int kFlushBatches = (kPacketBatch + kStreamStep - 1 + kPacketBatch - 1) / kPacketBatch;  // per flush
 
@@ -1519,12 +1523,20 @@ __global__ __launch_bounds__(1024) void TileBoundsKernel(BinParams p) {
     TileBounds(p, scratch, p.bounds);
 }
 
+// LDS of a bin block (dynamic, sized to the band so the bin blocks of one frame leave room for
+// other frames' trace blocks): the tile bounds, then the histogram (also TileBounds' scratch).
+std::size_t BinLdsBytes(int nx, int ny) {
+    const int hist = nx * ny > 2 * (nx + ny) ? nx * ny : 2 * (nx + ny);
+    return static_cast<std::size_t>(nx + ny) * sizeof(float2) + static_cast<std::size_t>(hist) * sizeof(unsigned);
+}
+
 __global__ __launch_bounds__(kBinThreads) void BinTrianglesKernel(BinParams p) {
-    __shared__ float2 b[kMaxBoundTiles];
-    __shared__ unsigned hist[kMaxBinTiles];
+    extern __shared__ float2 bin_lds[];
     const int tid = threadIdx.x;
     const int nx = p.tiles_x, ny = p.tiles_y;
     const int tiles = nx * ny;
+    float2* b = bin_lds;
+    unsigned* hist = reinterpret_cast<unsigned*>(bin_lds + nx + ny);
 
     // Prologue: the monotone tile-column and tile-row bounds -- precomputed once per frame by
     // TileBoundsKernel (p.bounds), or reduced here by every block (SRT_TILE_BOUNDS=0).
@@ -1562,6 +1574,7 @@ __global__ __launch_bounds__(kBinThreads) void BinTrianglesKernel(BinParams p) {
                     p.large_list[atomicAdd(&p.counts[tiles], 1u)] = i;
                 } else {
                     const Record rec{cr.a.x, cr.a.y, cr.a.z, cr.a.w, cr.b.x, cr.b.y, cr.b.z, cr.b.w, cr.x.x};
+#pragma unroll 1
                     for (int k = 0; k < w * h; ++k) {
                         const TileInfo ti = p.tile_info[(r0 + k / w) * nx + c0 + k % w];
                         const Box tb{ti.box.x, ti.box.y, ti.box.z, ti.box.w};
@@ -1680,8 +1693,10 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(T
 #pragma unroll
         for (int e = 0; e < kSlices; ++e) {
             const unsigned v = b0 + e * kCullThreads + tid;
-            const unsigned vv = src.begin + (v < total ? v : 0u);
-            nxt[e] = p.cull[vv < src.count1 ? src.list[vv] : src.list2[vv - src.count1]];
+            if (InBatch(e, tid)) {
+                const unsigned vv = src.begin + (v < total ? v : 0u);
+                nxt[e] = p.cull[vv < src.count1 ? src.list[vv] : src.list2[vv - src.count1]];
+            }
         }
     };
     if (!src.full && total != 0u) {
@@ -1750,7 +1765,7 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(T
 #pragma unroll
             for (int e = 0; e < kSlices; ++e) {
                 cr[e] = nxt[e];
-                valid[e] = b0 + e * kCullThreads + tid < total;
+                valid[e] = InBatch(e, tid) && b0 + e * kCullThreads + tid < total;
             }
             PacketBatch(sh, bb, pf, cr, valid, [&] {
                 if (b0 + kPacketBatch < total) {
@@ -1811,7 +1826,7 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(T
 #pragma unroll
                 for (int e = 0; e < kSlices; ++e) {
                     const unsigned v = bi * kPacketBatch + e * kCullThreads + tid;
-                    my_ids[bi][e] = v < listed ? sh.ids[v] : 0u;
+                    my_ids[bi][e] = InBatch(e, tid) && v < listed ? sh.ids[v] : 0u;
                 }
             }
 #pragma unroll
@@ -1824,7 +1839,7 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(T
                 bool valid[kSlices];
 #pragma unroll
                 for (int e = 0; e < kSlices; ++e) {
-                    valid[e] = b0 + e * kCullThreads + tid < listed;
+                    valid[e] = InBatch(e, tid) && b0 + e * kCullThreads + tid < listed;
                     cr[e] = LoadCullById(p, my_ids[bi][e]);
                 }
                 PacketBatch(sh, bb, pf, cr, valid, [] {});
@@ -2196,12 +2211,17 @@ __global__ __launch_bounds__(256) void HalfToFloatKernel(const _Float16* __restr
 // Launch on `stream`; with timing events, through hipExtLaunchKernelGGL so that the events
 // take the dispatch packet's own start / end timestamps (no extra stream packets).
 template <class K, class P>
-void Launch(K kernel, dim3 grid, dim3 block, hipStream_t stream, hipEvent_t start, hipEvent_t stop, const P& p) {
+void LaunchLds(K kernel, dim3 grid, dim3 block, std::size_t lds, hipStream_t stream, hipEvent_t start, hipEvent_t stop,
+               const P& p) {
     if (start != nullptr || stop != nullptr) {
-        hipExtLaunchKernelGGL(kernel, grid, block, 0, stream, start, stop, 0, p);
+        hipExtLaunchKernelGGL(kernel, grid, block, lds, stream, start, stop, 0, p);
     } else {
-        hipLaunchKernelGGL(kernel, grid, block, 0, stream, p);
+        hipLaunchKernelGGL(kernel, grid, block, lds, stream, p);
     }
+}
+template <class K, class P>
+void Launch(K kernel, dim3 grid, dim3 block, hipStream_t stream, hipEvent_t start, hipEvent_t stop, const P& p) {
+    LaunchLds(kernel, grid, block, 0, stream, start, stop, p);
 }
 
 }  // namespace
@@ -2551,8 +2571,8 @@ hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_ver
             }
             if (n != 0) {
                 const unsigned blocks = static_cast<unsigned>((n + kBinThreads - 1) / kBinThreads);
-                Launch(BinTrianglesKernel, dim3(blocks), dim3(kBinThreads), stream,
-                       b.bounds != nullptr ? nullptr : ev.bin_begin, nullptr, b);
+                LaunchLds(BinTrianglesKernel, dim3(blocks), dim3(kBinThreads), BinLdsBytes(b.tiles_x, b.tiles_y), stream,
+                          b.bounds != nullptr ? nullptr : ev.bin_begin, nullptr, b);
             }
             Launch(TileOrderKernel, dim3(1), dim3(kOrderThreads), stream, n != 0 ? nullptr : ev.bin_begin,
                    ev.bin_end, b);
