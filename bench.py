@@ -17,9 +17,12 @@ Multi-GPU, one rank per GPU over RCCL:
       (--root rotate, default) or rank 0 (--root fixed). Each rank keeps --queues frames in
       flight: queue q = its own DeviceScene (edge records, bins), HIP stream, band / frame
       buffers and RCCL process group, so one frame's setup, trace, gather and shading overlap
-      the others'. value = frames x W x H / the max-over-ranks time: "scaling": "strong".
-      After the timed loop every compositing rank compares its last frame with a one-GPU
-      render of the same frame bit for bit ("verified").
+      the others'. A queue gathers --batch frames' bands in ONE collective (a torch-RCCL gather
+      costs ~44 us of host time per call, more than a band's trace: tools/host_probe_bands.py)
+      and the compositor shades the batch in one launch (srtShadeBandsAsync); the compositor
+      rotates per batch. value = frames x W x H / the max-over-ranks time: "scaling": "strong".
+      After the timed loop every compositing rank compares its last batch's frames with a
+      one-GPU render of the same frame bit for bit ("verified").
   --mode frames: every rank renders whole frames of a temporal-jitter sequence (no collective);
       "scaling": "weak". Reported beside the bands line at N > 1 ("frames").
 At N = 1 the two modes coincide (one band = the frame, shaded in the trace).
@@ -68,6 +71,8 @@ def parse():
     p.add_argument("--root", default="rotate", choices=["rotate", "fixed"], help="bands: compositing rank")
     p.add_argument("--queues", type=int, default=int(os.environ.get("SRT_BENCH_QUEUES", "3")),
                    help="frames in flight per GPU (own scene buffers, HIP stream, process group each)")
+    p.add_argument("--batch", type=int, default=int(os.environ.get("SRT_BENCH_BATCH", "8")),
+                   help="bands, N > 1: frames per gather (one collective and one shading launch per batch)")
     p.add_argument("--offsets", default="uniform", choices=["uniform", "random"],
                    help="sample offsets: uniform 0.5 (headline) or seeded U[0,1) per-pixel jitter")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample length")
@@ -163,7 +168,7 @@ class Pipeline:
     band r of every frame (P > 1: hit ids, gathered to the compositor, which shades); mode
     "frames": whole frames, each rank its own jitter; P == 1: the two coincide."""
 
-    def __init__(self, ctx, path, mode="bands", queues=3, variant="cull", offsets="uniform", rotate=True):
+    def __init__(self, ctx, path, mode="bands", queues=3, variant="cull", offsets="uniform", rotate=True, batch=8):
         from simpleraytracer_amd.bands import band_range, band_rows
 
         torch, a = ctx.torch, ctx.a
@@ -171,6 +176,7 @@ class Pipeline:
         self.W, self.H = a.width, a.height
         P = ctx.world if mode == "bands" else 1
         self.P = P
+        self.G = max(1, batch) if P > 1 else 1  # frames per gather (one collective per G frames)
         self.row_begin, self.row_count = band_range(self.H, P, ctx.rank) if P > 1 else (0, self.H)
         self.B = band_rows(self.H, P)
         self.offsets = make_offsets(torch, a, ctx.dev, jitter(ctx.rank) if mode == "frames" else 0.5, offsets,
@@ -179,45 +185,77 @@ class Pipeline:
         self.queues = []
         for q in range(max(1, queues)):
             qd = {"scene": ctx.srt.DeviceScene(path, ctx.dev.index), "stream": torch.cuda.Stream(ctx.dev),
-                  "rgba": torch.zeros((self.H, self.W, 4), dtype=torch.float32, device=ctx.dev), "root": None}
+                  "root": None, "index": q, "fill": 0, "batches": 0, "shaded": 0}
             if P > 1:
-                qd["band_ids"] = torch.full((self.B, self.W), -1, dtype=torch.int32, device=ctx.dev)
-                qd["frame_ids"] = torch.empty((P * self.B, self.W), dtype=torch.int32, device=ctx.dev)
+                qd["rgba"] = torch.zeros((self.G, self.H, self.W, 4), dtype=torch.float32, device=ctx.dev)
+                qd["band_ids"] = torch.full((self.G, self.B, self.W), -1, dtype=torch.int32, device=ctx.dev)
+                qd["frame_ids"] = torch.empty(P * self.G * self.B * self.W, dtype=torch.int32, device=ctx.dev)
                 qd["group"] = ctx.groups[q % len(ctx.groups)]
+                qd["scene"].prepare(self.W, self.H)
+                # one validated launch closure per batch slot (the frame loop's host cost is HIP's)
+                qd["slots"] = [qd["scene"].bind_trace_ids(self.band_off, qd["band_ids"][j, :self.row_count],
+                                                          self.row_begin, self.row_count, variant=variant,
+                                                          stream=qd["stream"]) if self.row_count else None
+                               for j in range(self.G)]
+            else:
+                qd["rgba"] = torch.zeros((self.H, self.W, 4), dtype=torch.float32, device=ctx.dev)
             self.queues.append(qd)
         self.triangles = self.queues[0]["scene"].triangles
 
     def step(self, k, nq):
-        from simpleraytracer_amd.bands import compositor, gather_band_ids
-
-        ctx, torch = self.ctx, self.ctx.torch
         q = self.queues[k % nq]
         sc, st = q["scene"], q["stream"]
-        sc.prepare(self.W, self.H, st)
         if self.P == 1:
+            sc.prepare(self.W, self.H, st)
             sc.trace(self.offsets, q["rgba"], 0, self.H, variant=self.variant, stream=st)
             q["root"] = 0
             return
-        rows = self.row_count
-        if rows:
-            sc.trace_ids(self.band_off, q["band_ids"][:rows], self.row_begin, rows, variant=self.variant, stream=st)
-        root = compositor(k, self.P, self.rotate)
+        j = q["fill"]
+        if q["slots"][j] is not None:
+            q["slots"][j]()  # prepare + trace of this rank's band of the frame, ids into batch slot j
+        else:  # a rank with no rows (P > H) still prepares its frame
+            sc.prepare(self.W, self.H, st)
+        q["fill"] = j + 1
+        if q["fill"] == self.G:
+            self.flush(q, nq)
+
+    def flush(self, q, nq):
+        """Gather the queue's filled batch slots (one collective for all of them) to the batch's
+        compositor, which shades every frame of the batch in one launch."""
+        from simpleraytracer_amd.bands import compositor, gather_band_batch
+
+        ctx, torch = self.ctx, self.ctx.torch
+        f = q["fill"]
+        if f == 0:
+            return
+        sc, st = q["scene"], q["stream"]
+        root = compositor(q["batches"] * nq + q["index"], self.P, self.rotate)
+        batch = q["band_ids"][:f]
         if ctx.backend == "gloo":  # CPU rehearsal: gloo gathers host tensors, synchronously
             st.synchronize()
-            frame, _ = gather_band_ids(q["band_ids"].cpu(), self.H, dst=root, group=q["group"])
-            if frame is not None:
-                q["frame_ids"][:self.H].copy_(frame.to(ctx.dev))
+            host_out = torch.empty(self.P * f * self.B * self.W, dtype=torch.int32) if ctx.rank == root else None
+            ids, _ = gather_band_batch(batch.cpu(), self.H, dst=root, group=q["group"], out=host_out)
+            if ids is not None:
+                dev_ids = q["frame_ids"][:ids.numel()].view(ids.shape)
+                dev_ids.copy_(ids.to(ctx.dev))
                 torch.cuda.synchronize(ctx.dev)
+                ids = dev_ids
         else:
             with torch.cuda.stream(st):
-                _, work = gather_band_ids(q["band_ids"], self.H, dst=root, group=q["group"], out=q["frame_ids"],
-                                          async_op=True)
-                work.wait()  # the queue's stream waits for the gather (ids consumed / band reusable)
+                ids, work = gather_band_batch(batch, self.H, dst=root, group=q["group"], out=q["frame_ids"],
+                                              async_op=True)
+                work.wait()  # the queue's stream waits for the gather (ids consumed / slots reusable)
         if ctx.rank == root:
-            sc.shade(self.offsets, q["frame_ids"][:self.H], q["rgba"], 0, self.H, stream=st)
+            sc.shade_bands(self.offsets, ids, q["rgba"][:f], self.B, stream=st)
+            q["shaded"] = f
         q["root"] = root
+        q["batches"] += 1
+        q["fill"] = 0
 
-    def drain(self):
+    def drain(self, nq=None):
+        if self.P > 1:  # partial batches: every queue's filled slots are gathered and shaded
+            for q in self.queues[:nq or len(self.queues)]:
+                self.flush(q, nq or len(self.queues))
         for q in self.queues:
             q["stream"].synchronize()
 
@@ -228,7 +266,7 @@ class Pipeline:
         nq = min(queues or len(self.queues), len(self.queues))
         for k in range(warmup * nq):
             self.step(k, nq)
-        self.drain()
+        self.drain(nq)
         sc0 = self.queues[0]["scene"]
         sc0.take_stage_times()
         sc0.set_stage_timing(timing)
@@ -237,7 +275,7 @@ class Pipeline:
         t0 = time.perf_counter()
         for k in range(steps):
             self.step(warmup * nq + k, nq)
-        self.drain()
+        self.drain(nq)
         torch.cuda.synchronize(ctx.dev)
         ctx.barrier()
         elapsed = ctx.max_over_ranks(time.perf_counter() - t0)
@@ -248,19 +286,21 @@ class Pipeline:
                 "trace_ms": trace_ms, "launches": launches, "ms_per_step": elapsed / steps * 1e3, "queues": nq}
 
     def verify(self):
-        """Every rank that composited a frame compares its last one with a one-GPU render of the
+        """Every rank that composited a batch compares its frames with a one-GPU render of the
         same frame (fused trace, this device), bit for bit; True on every rank iff all agree."""
         ctx, torch = self.ctx, self.ctx.torch
         ok = True
         for q in self.queues:
             if q["root"] == ctx.rank:
                 ref_scene = ctx.srt.DeviceScene(q["scene"].path, ctx.dev.index)
-                ref = torch.empty_like(q["rgba"])
+                ref = torch.empty((self.H, self.W, 4), dtype=torch.float32, device=ctx.dev)
                 st = torch.cuda.current_stream(ctx.dev)
                 ref_scene.prepare(self.W, self.H, st)
                 ref_scene.trace(self.offsets, ref, 0, self.H, variant=self.variant, stream=st)
                 torch.cuda.synchronize(ctx.dev)
-                ok = ok and bool(torch.equal(ref.view(torch.int32), q["rgba"].view(torch.int32)))
+                frames = q["rgba"][:q["shaded"]] if self.P > 1 else q["rgba"][None]
+                for fr in frames:  # every frame of the queue's last composited batch
+                    ok = ok and bool(torch.equal(ref.view(torch.int32), fr.view(torch.int32)))
                 ref_scene.close()
                 break
         return ctx.max_over_ranks(0.0 if ok else 1.0) == 0.0
@@ -398,7 +438,7 @@ def main():
     path = ctx.scene_path(a.scene, a.triangles if a.scene == "soup" else None)
     wl = workload_name(a)
     rotate = a.root == "rotate"
-    main_run = Pipeline(ctx, path, a.mode, a.queues, a.variant, a.offsets, rotate)
+    main_run = Pipeline(ctx, path, a.mode, a.queues, a.variant, a.offsets, rotate, a.batch)
     n_tri = main_run.triangles
     _, order_build_ms = main_run.queues[0]["scene"].spatial_order()
     W, H = a.width, a.height
@@ -418,11 +458,11 @@ def main():
     if world > 1 and extras:  # the other split and the other compositor choice, same steps
         try:
             om = "frames" if a.mode == "bands" else "bands"
-            o = Pipeline(ctx, path, om, a.queues, a.variant, a.offsets, rotate)
+            o = Pipeline(ctx, path, om, a.queues, a.variant, a.offsets, rotate, a.batch)
             legs[om] = {**leg_summary(o.run(a.steps, a.warmup)), "scaling": "weak" if om == "frames" else "strong"}
             o.close()
             if a.mode == "bands":
-                o = Pipeline(ctx, path, "bands", a.queues, a.variant, a.offsets, not rotate)
+                o = Pipeline(ctx, path, "bands", a.queues, a.variant, a.offsets, not rotate, a.batch)
                 legs["fixed_root" if rotate else "rotating_root"] = leg_summary(o.run(a.steps, a.warmup))
                 o.close()
         except Exception as e:  # noqa: BLE001 -- the primary line must still be printed
@@ -487,6 +527,7 @@ def main():
                 "parallelism": par,
                 "trace_variant": a.variant,
                 "frame_queues": r["queues"],
+                "frames_per_gather": main_run.G,
                 "offsets": a.offsets,
             },
             "roofline": roof,
@@ -513,6 +554,7 @@ def main():
             line["verified"] = verified
             if band_ids:
                 line["gather"] = {"payload": "int32 hit id per pixel (deferred shading on the compositor)",
+                                  "frames_per_collective": main_run.G,
                                   "bytes_per_frame": (world - 1) * main_run.B * W * 4,
                                   "rgba_f32_equivalent": (world - 1) * main_run.B * W * 16}
         for k, v in legs.items():

@@ -93,6 +93,15 @@ ML_API_ENTRY int srtTraceIdsAsync(srt_device_scene scene, const float* d_offsets
 ML_API_ENTRY int srtShadeAsync(srt_device_scene scene, const float* d_offsets, const int* d_ids, float* d_rgba,
                                size_t row_begin, size_t row_count, void* stream);
 
+/* Stage 3 for a batch of `frames` frames of the prepared camera (the multi-process band path,
+ * where one gather carries several frames): the ids arrive band-major, as a gather of every
+ * rank's (frames x band_rows x width) band buffer leaves them,
+ *   d_ids[band][frame][band_rows][width], band = 0 .. ceil(height / band_rows) - 1,
+ * d_offsets is the frame's (height x width x 2), d_rgba receives frames x height x width x 4.
+ * One launch; each frame is bit-identical to srtTraceAsync's RGBA. */
+ML_API_ENTRY int srtShadeBandsAsync(srt_device_scene scene, const float* d_offsets, const int* d_ids, float* d_rgba,
+                                    size_t frames, size_t band_rows, void* stream);
+
 /* Calls on one srt_device_scene are ordered: the per-frame edge records and the cull work
  * buffer are shared, so a call on a different stream than the previous call first waits (HIP
  * event) for the work enqueued before it. Use one scene per stream for concurrent frames. */

@@ -92,6 +92,8 @@ _SIGNATURES = {
                                         ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]),
     "srtShadeAsync": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                      ctypes.c_size_t, ctypes.c_size_t, ctypes.c_void_p]),
+    "srtShadeBandsAsync": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                          ctypes.c_size_t, ctypes.c_size_t, ctypes.c_void_p]),
     "srtGatherBandsHost": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_size_t,
                                           ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]),
     "srtSetStageTiming": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),

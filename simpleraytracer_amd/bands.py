@@ -84,3 +84,35 @@ def gather_band_ids(band_ids, height: int, dst: int = 0, group=None, out=None, a
     if band_ids.dtype != torch.int32 or band_ids.dim() != 2:
         raise ValueError("band_ids must be a (B, W) int32 tensor")
     return _gather_into(band_ids, height, dst, group, out, async_op)
+
+
+def gather_band_batch(batch, height: int, dst: int = 0, group=None, out=None, async_op: bool = False):
+    """Gather F frames' bands in ONE collective: every rank's (F, B, W) int32 hit-id batch
+    (frame f's band in batch[f]) to ``dst``, received band-major into (P, F, B, W) — the layout
+    srtShadeBandsAsync (DeviceScene.shade_bands) shades in one launch.
+
+    One collective per F frames: a torch-RCCL gather costs ~44 us of host time per call
+    (tools/host_probe_bands.py), more than a band's trace, so the band path gathers batches.
+    ``out`` (dst only): a buffer of at least P*F*B*W int32 elements (viewed, not copied).
+    Returns (ids (P, F, B, W) on dst else None, work)."""
+    import torch
+    import torch.distributed as dist
+
+    if batch.dtype != torch.int32 or batch.dim() != 3 or not batch.is_contiguous():
+        raise ValueError("batch must be a contiguous (F, B, W) int32 tensor")
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    frames, b, width = batch.shape
+    if b != band_rows(height, world):
+        raise ValueError(f"batch bands must have {band_rows(height, world)} rows, got {b}")
+    dst_global = dst if group is None else dist.get_global_rank(group, dst)
+    if rank != dst:
+        return None, dist.gather(batch, gather_list=None, dst=dst_global, group=group, async_op=async_op)
+    need = world * frames * b * width
+    if out is None:
+        out = torch.empty(need, dtype=batch.dtype, device=batch.device)
+    elif out.dtype != batch.dtype or not out.is_contiguous() or out.numel() < need:
+        raise ValueError(f"out must be a contiguous int32 buffer of at least {need} elements")
+    ids = out.view(-1)[:need].view(world, frames, b, width)
+    work = dist.gather(batch, gather_list=list(ids.unbind(0)), dst=dst_global, group=group, async_op=async_op)
+    return ids, work

@@ -165,8 +165,12 @@ std::size_t BvhBytes(std::uint64_t n);  // node boxes (16 B) + depth bounds (4 B
 
 // Deferred shading of a band from hit ids (band.ids) and sample offsets into band.rgba, with the
 // edge buffer's shading normals of the prepared frame: bit-identical to the fused trace.
+// frames > 1 shades a batch whose ids are band-major, ids[band][frame][band_rows][width] (a
+// gather of `frames` frames of band_rows-row bands; band_rows 0 = one band of row_count rows),
+// into band.rgba[frame][row_count][width].
 hipError_t LaunchShade(const float* d_vertices, const float* d_albedo, const float* d_edges, std::uint64_t n,
-                       const Frame& frame, const float background[3], const BandArgs& band, hipStream_t stream);
+                       const Frame& frame, const float background[3], const BandArgs& band, hipStream_t stream,
+                       std::size_t frames = 1, std::size_t band_rows = 0);
 
 // Spatial order of the records (spatial.hip): ids sorted by the Morton code of their centroid's
 // image-plane position under the scene camera, on the device (keys + rocPRIM radix sort), and

@@ -464,19 +464,26 @@ __device__ __forceinline__ void ShadeAndStore(const TraceParams& p, int x, int y
 
 // Deferred shading: one thread per pixel of a band, from its hit id and sample offset, with
 // GenerateRays' position expressions and ShadePixel: the frame equals the fused trace + shade
-// bit for bit.
-__global__ __launch_bounds__(256) void ShadeIdsKernel(TraceParams p, const int* __restrict__ ids) {
+// bit for bit. blockIdx.y = frame g of a batch whose ids arrive band-major, as a gather of
+// `frames` frames of row bands leaves them: ids[band][g][band_rows][width] (one frame and one
+// band of row_count rows: the plain (row_count, width) layout); out[g][row_count][width].
+__global__ __launch_bounds__(256) void ShadeIdsKernel(TraceParams p, const int* __restrict__ ids,
+                                                      unsigned band_rows, unsigned frames) {
     const size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (i >= static_cast<size_t>(p.width) * p.row_count) {
+    const size_t pixels = static_cast<size_t>(p.width) * p.row_count;
+    if (i >= pixels) {
         return;
     }
+    const unsigned g = blockIdx.y;
     const int x = static_cast<int>(i % static_cast<unsigned>(p.width));
     const int y = static_cast<int>(i / static_cast<unsigned>(p.width));
+    const unsigned band = static_cast<unsigned>(y) / band_rows;
+    const size_t at = ((static_cast<size_t>(band) * frames + g) * band_rows + (y - band * band_rows)) * p.width + x;
     const float2 o = p.offsets[i];
     const float fx = (static_cast<float>(x) + o.x) / p.wf;
     const float fy = (static_cast<float>(p.row_begin + y) + o.y) / p.hf;
-    const int id = ids[i];
-    p.out[i] = ShadePixel(p, fx, fy, static_cast<unsigned>(id) < p.n ? id : -1);  // no id outside the scene
+    const int id = ids[at];
+    p.out[g * pixels + i] = ShadePixel(p, fx, fy, static_cast<unsigned>(id) < p.n ? id : -1);  // no id outside the scene
 }
 
 // ---------------------------------------------------------------------------------------
@@ -2609,11 +2616,16 @@ hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_ver
 }
 
 hipError_t LaunchShade(const float* d_vertices, const float* d_albedo, const float* d_edges, std::uint64_t n,
-                       const Frame& frame, const float background[3], const BandArgs& band, hipStream_t stream) {
-    if (band.row_count == 0 || band.width == 0) {
+                       const Frame& frame, const float background[3], const BandArgs& band, hipStream_t stream,
+                       std::size_t frames, std::size_t band_rows) {
+    if (band.row_count == 0 || band.width == 0 || frames == 0) {
         return hipSuccess;
     }
-    if (band.ids == nullptr || band.rgba == nullptr || band.offsets == nullptr) {
+    if (band_rows == 0) {
+        band_rows = band.row_count;
+    }
+    if (band.ids == nullptr || band.rgba == nullptr || band.offsets == nullptr || frames > 65535 ||
+        band_rows > band.row_count) {
         return hipErrorInvalidValue;
     }
     TraceParams p{};
@@ -2635,8 +2647,9 @@ hipError_t LaunchShade(const float* d_vertices, const float* d_albedo, const flo
         p.bg[k] = background[k];
     }
     const std::size_t pixels = band.width * band.row_count;
-    hipLaunchKernelGGL(ShadeIdsKernel, dim3(static_cast<unsigned>((pixels + 255) / 256)), dim3(256), 0, stream, p,
-                       static_cast<const int*>(band.ids));
+    hipLaunchKernelGGL(ShadeIdsKernel, dim3(static_cast<unsigned>((pixels + 255) / 256), static_cast<unsigned>(frames)),
+                       dim3(256), 0, stream, p, static_cast<const int*>(band.ids), static_cast<unsigned>(band_rows),
+                       static_cast<unsigned>(frames));
     return hipGetLastError();
 }
 

@@ -250,20 +250,23 @@ void DeviceScene::PrepareIfPending(hipStream_t stream) const {
 }
 
 void DeviceScene::Shade(const float* d_offsets, const int* d_ids, float* d_rgba, std::size_t row_begin,
-                        std::size_t row_count, hipStream_t stream) const {
+                        std::size_t row_count, hipStream_t stream, std::size_t frames, std::size_t band_rows) const {
     if (m_width == 0) {
         throw std::runtime_error("Shade: Prepare() has not been called");
     }
     if (row_begin + row_count > m_height) {
         throw std::runtime_error("Shade: row band outside the frame");
     }
-    if (row_count == 0) {
+    if (band_rows > row_count || frames > 65535) {
+        throw std::runtime_error("Shade: band_rows exceeds the rows shaded, or more than 65535 frames");
+    }
+    if (row_count == 0 || frames == 0) {
         return;
     }
     OrderAfterPrevious(stream);
     PrepareIfPending(stream);
     BandArgs band{d_offsets, d_rgba, m_width, m_height, row_begin, row_count, const_cast<int*>(d_ids)};
-    HipCheck(LaunchShade(m_vertices, m_albedo, m_edges, m_n, m_frame, m_background, band, stream),
+    HipCheck(LaunchShade(m_vertices, m_albedo, m_edges, m_n, m_frame, m_background, band, stream, frames, band_rows),
              "shade kernel launch");
 }
 

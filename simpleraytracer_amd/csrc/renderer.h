@@ -46,8 +46,10 @@ public:
                hipStream_t stream, int* d_ids = nullptr) const;
     // Deferred shading of rows [row_begin, row_begin + row_count) of the prepared frame from hit
     // ids (as Trace writes them) and sample offsets: the RGBA the fused trace would store.
+    // frames > 1: a batch of that many frames of this camera, ids band-major as a gather of
+    // band_rows-row bands leaves them (render.h LaunchShade), rgba [frames][row_count][width].
     void Shade(const float* d_offsets, const int* d_ids, float* d_rgba, std::size_t row_begin, std::size_t row_count,
-               hipStream_t stream) const;
+               hipStream_t stream, std::size_t frames = 1, std::size_t band_rows = 0) const;
 
     std::size_t width() const { return m_width; }
     // The spatial order (device, triangles entries) and the time its build took at load (ms).

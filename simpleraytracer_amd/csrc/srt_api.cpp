@@ -257,6 +257,24 @@ ML_API_ENTRY int srtShadeAsync(srt_device_scene scene, const float* d_offsets, c
     });
 }
 
+ML_API_ENTRY int srtShadeBandsAsync(srt_device_scene scene, const float* d_offsets, const int* d_ids, float* d_rgba,
+                                    size_t frames, size_t band_rows, void* stream) {
+    return Guarded([&] {
+        if (scene == nullptr) {
+            throw std::runtime_error("Bad scene handle");
+        }
+        if ((d_offsets == nullptr || d_ids == nullptr || d_rgba == nullptr) && frames != 0) {
+            throw std::runtime_error("Bad buffer argument");
+        }
+        if (band_rows == 0) {
+            throw std::runtime_error("band_rows must be positive");
+        }
+        srt::DeviceScene* s = FromHandle(scene);
+        Bind bind(s->device());
+        s->Shade(d_offsets, d_ids, d_rgba, 0, s->height(), static_cast<hipStream_t>(stream), frames, band_rows);
+    });
+}
+
 ML_API_ENTRY int srtGatherBandsHost(const void* const* bands, size_t band_count, size_t width, size_t height,
                                     int element_bytes, void* frame) {
     return Guarded([&] {

@@ -118,6 +118,9 @@ class DeviceScene:
         want = (rows, self.width) + ((channels,) if channels else ())
         if hasattr(buf, "shape") and tuple(buf.shape) != want:
             raise ValueError(f"{name} must be {want}, got {tuple(buf.shape)}")
+        self._check_tensor(name, buf, dtype)
+
+    def _check_tensor(self, name, buf, dtype):
         if hasattr(buf, "is_contiguous") and not buf.is_contiguous():
             raise ValueError(f"{name} must be contiguous")
         if hasattr(buf, "is_cuda"):
@@ -149,6 +152,24 @@ class DeviceScene:
         _check(self._lib.srtTraceIdsAsync(self.handle, _ptr(offsets), _ptr(ids), row_begin, row_count,
                                           TRACE_VARIANTS[variant], _stream(stream)))
 
+    def bind_trace_ids(self, offsets, ids, row_begin: int = 0, row_count: int | None = None, variant: str = "cull",
+                       stream=None):
+        """prepare + trace_ids of this band as a zero-argument callable: the buffers are checked
+        once here, each call is then just the two C-ABI calls (a frame loop's host cost is the
+        HIP launches, not Python checks). The buffers must stay alive while it is used."""
+        if row_count is None:
+            row_count = self.height - row_begin
+        self._check_buffer("offsets", offsets, row_count, 2, "f32")
+        self._check_buffer("ids", ids, row_count, 0, "i32")
+        lib, h, w, hh = self._lib, self.handle, self.width, self.height
+        op, ip, s, v = _ptr(offsets), _ptr(ids), _stream(stream), TRACE_VARIANTS[variant]
+
+        def run():
+            _check(lib.srtPrepareAsync(h, w, hh, s))
+            _check(lib.srtTraceIdsAsync(h, op, ip, row_begin, row_count, v, s))
+
+        return run
+
     def shade(self, offsets, ids, rgba, row_begin: int = 0, row_count: int | None = None, stream=None):
         """Deferred shading of the prepared frame's rows from hit ids: the RGBA trace() stores."""
         if row_count is None:
@@ -158,6 +179,24 @@ class DeviceScene:
         self._check_buffer("rgba", rgba, row_count, 4, "f32")
         _check(self._lib.srtShadeAsync(self.handle, _ptr(offsets), _ptr(ids), _ptr(rgba), row_begin, row_count,
                                        _stream(stream)))
+
+    def shade_bands(self, offsets, ids, rgba, band_rows: int, stream=None):
+        """Deferred shading of a batch of frames whose ids were gathered band-major:
+        ids (bands, frames, band_rows, W) int32 (bands = ceil(H / band_rows)), offsets (H, W, 2),
+        rgba (frames, H, W, 4); one launch (srtShadeBandsAsync)."""
+        if band_rows <= 0:
+            raise ValueError("band_rows must be positive")
+        bands = (self.height + band_rows - 1) // band_rows
+        frames = ids.shape[1] if hasattr(ids, "shape") and len(ids.shape) == 4 else 0
+        self._check_buffer("offsets", offsets, self.height, 2, "f32")
+        if hasattr(ids, "shape") and tuple(ids.shape) != (bands, frames, band_rows, self.width):
+            raise ValueError(f"ids must be {(bands, 'frames', band_rows, self.width)}, got {tuple(ids.shape)}")
+        if hasattr(rgba, "shape") and tuple(rgba.shape) != (frames, self.height, self.width, 4):
+            raise ValueError(f"rgba must be {(frames, self.height, self.width, 4)}, got {tuple(rgba.shape)}")
+        for name, buf, dtype in (("ids", ids, "i32"), ("rgba", rgba, "f32")):
+            self._check_tensor(name, buf, dtype)
+        _check(self._lib.srtShadeBandsAsync(self.handle, _ptr(offsets), _ptr(ids), _ptr(rgba), frames, band_rows,
+                                            _stream(stream)))
 
     def spatial_order(self):
         """(order, build_ms): the record ids in spatial order (numpy uint32), built on the device

@@ -136,6 +136,89 @@ def test_gloo_id_gather_rotating_compositor(scenes, tmp_path, world, wh):
         assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), k
 
 
+def band_major_frame(ids, g, height):
+    """Frame g of a band-major batch ids[band][frame][band_rows][width], by ShadeIdsKernel's
+    index expression (render.hip): at = ((band * frames + g) * band_rows + y % band_rows) * W + x."""
+    bands, frames, b, w = ids.shape
+    flat = np.asarray(ids).reshape(-1)
+    y = np.arange(height)[:, None]
+    x = np.arange(w)[None, :]
+    band = y // b
+    at = ((band * frames + g) * b + (y - band * b)) * w + x
+    return flat[at]
+
+
+def _batch_worker(rank, world, port, scene_path, w, h, batches, out_dir):
+    """bench.py's batched band path with CPU stand-ins: rank r traces band r of F frames into an
+    (F, B, W) batch, ONE gather per batch (gather_band_batch) to the rotating compositor, which
+    shades every frame of the batch from the band-major ids."""
+    import torch
+    import torch.distributed as dist
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, repo)
+    from oracle.srt_oracle import OracleScene
+    from simpleraytracer_amd.bands import band_range, band_rows, compositor, gather_band_batch
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    oracle = OracleScene(scene_path)
+    b0, cnt = band_range(h, world, rank)
+    B = band_rows(h, world)
+    out = torch.empty(world * max(batches) * B * w, dtype=torch.int32)
+    k = 0
+    for bi, frames in enumerate(batches):
+        batch = torch.full((frames, B, w), -5, dtype=torch.int32)
+        offs = [np.random.default_rng(2000 + k + f).random((h, w, 2), dtype=np.float32) for f in range(frames)]
+        for f in range(frames):
+            if cnt:
+                img = oracle.render(w, h, offs[f], row_begin=b0, row_count=cnt, threads=1)
+                batch[f, :cnt] = torch.from_numpy(img[b0:b0 + cnt, :, 3].astype(np.int32))
+        root = compositor(bi, world)
+        ids, work = gather_band_batch(batch, h, dst=root, out=out, async_op=True)
+        work.wait()
+        if rank == root:
+            assert ids.shape == (world, frames, B, w)
+            for f in range(frames):
+                np.save(os.path.join(out_dir, f"frame{k + f}.npy"),
+                        oracle.shade(w, h, band_major_frame(ids.numpy(), f, h), offs[f]))
+        else:
+            assert ids is None
+        k += frames
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,wh", [(2, (40, 37)), (3, (33, 29))])
+def test_gloo_batched_id_gather(scenes, tmp_path, world, wh):
+    """One collective per batch of frames (full and partial batches): every frame shaded from the
+    band-major gather layout equals the single-process frame bit for bit."""
+    import torch.multiprocessing as mp
+
+    from oracle.srt_oracle import OracleScene
+
+    w, h = wh
+    batches = [3, 1, 2]
+    mp.start_processes(_batch_worker, args=(world, _free_port(), scenes["soup300"], w, h, batches, str(tmp_path)),
+                       nprocs=world, join=True, start_method="spawn")
+    oracle = OracleScene(scenes["soup300"])
+    k = 0
+    for frames in batches:
+        for f in range(frames):
+            offs = np.random.default_rng(2000 + k + f).random((h, w, 2), dtype=np.float32)
+            got = np.load(tmp_path / f"frame{k + f}.npy")
+            ref = oracle.render(w, h, offs)
+            assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), (k, f)
+        k += frames
+
+
+def test_band_major_layout_matches_concatenation():
+    ids = np.arange(3 * 4 * 5 * 6).reshape(3, 4, 5, 6)  # 3 bands x 4 frames x 5 rows x 6 cols
+    for g in range(4):
+        want = np.concatenate([ids[p, g] for p in range(3)])[:13]
+        assert np.array_equal(band_major_frame(ids, g, 13), want)
+
+
 def test_compositor_rotation():
     from simpleraytracer_amd.bands import compositor
 

@@ -631,6 +631,42 @@ def test_deferred_shading_bitwise(gpu, scenes, variant):
     scene2.close()
 
 
+@pytest.mark.parametrize("bands", [1, 3, 4])
+def test_batched_band_shading_bitwise(gpu, scenes, bands):
+    """srtShadeBandsAsync (bench.py's batched band gather): the ids of F frames arrive band-major
+    ids[band][frame][band_rows][W], the last band padded (170 rows in 3 / 4 bands); one launch
+    shades all F frames, each equal to the fused trace bit for bit. Frame f of the batch holds
+    the ids of a different frame's band order (the padded rows hold garbage, never read)."""
+    import torch
+
+    import simpleraytracer_amd as srt
+
+    w, h, frames = 333, 170, 3
+    rng = np.random.default_rng(43)
+    offs = rng.random((h, w, 2), dtype=np.float32)
+    ref = torch_render(scenes["soup2k"], w, h, offs)
+    scene = srt.DeviceScene(scenes["soup2k"], 0)
+    stream = torch.cuda.current_stream()
+    off = torch.from_numpy(offs).cuda()
+    b = (h + bands - 1) // bands
+    ids = torch.full((bands, frames, b, w), -7, dtype=torch.int32, device="cuda")
+    scene.prepare(w, h, stream)
+    for p in range(bands):
+        r0, rows = p * b, min(h, (p + 1) * b) - p * b
+        for f in range(frames):
+            scene.trace_ids(off[r0:r0 + rows], ids[p, f, :rows], r0, rows, stream=stream)
+        ids[p, :, rows:] = 2 ** 30  # padding: an id outside the scene, never read
+    rgba = torch.full((frames, h, w, 4), float("nan"), dtype=torch.float32, device="cuda")
+    scene.shade_bands(off, ids, rgba, b, stream=stream)
+    torch.cuda.synchronize()
+    got = rgba.cpu().numpy()
+    for f in range(frames):
+        assert np.array_equal(got[f].view(np.uint32), ref.view(np.uint32)), f
+    with pytest.raises(ValueError):
+        scene.shade_bands(off, ids, rgba[:2], b, stream=stream)
+    scene.close()
+
+
 def test_scene_calls_on_two_streams_are_ordered(gpu, scenes):
     """One scene used from two streams (bands on alternating streams, a new prepare in between):
     the library orders the calls, so every frame equals its single-stream render."""
