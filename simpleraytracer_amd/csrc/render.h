@@ -96,12 +96,13 @@ struct CullBins {
     unsigned* counts;      // tiles + 1: list lengths, then the large-list length
     unsigned* lists;       // tiles x capacity candidate ids (BinTrianglesKernel)
     unsigned* large_list;  // PaddedTriangleCount(n) ids binned to every tile
-    void* work;            // trace work list (TileOrderKernel): tiles x parts descriptors, 32 B each
+    void* work;            // trace work list (the last bin block): tiles x parts descriptors, 32 B each
     unsigned* work_count;  // its length
     unsigned* arrive;      // tiles x parts: split chunks finished (self-resetting counters)
     void* split_keys;      // key slices of split parts: tiles x parts x max_chunks, 8 KiB each
     unsigned max_chunks;   // M = CullMaxChunks(tiles)
-    void* bounds;          // (tiles_x + tiles_y) float2: monotone tile column / row bounds
+    unsigned* range_tag;   // = gen when some sample offset of the frame lies outside [0, 1] (tile blocks)
+    unsigned gen;          // the scene's frame number (never 0): tags are compared with it, not reset
     unsigned capacity;
     std::size_t tiles;
 };

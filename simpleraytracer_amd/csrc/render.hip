@@ -74,7 +74,7 @@ struct TraceParams {
     const TileInfo* __restrict__ tile_info;   // per tile: ray box, uniform offset (TileInfoKernel)
     const CullRecord* __restrict__ cull;      // cull records in spatial order (the lists hold positions)
     const unsigned* __restrict__ order;       // spatial-order position -> record id
-    const uint4* __restrict__ work;           // tile parts (2 x uint4 each), most work first (TileOrderKernel)
+    const uint4* __restrict__ work;           // tile parts (2 x uint4 each), most work first (BuildWorkOrder)
     const unsigned* __restrict__ work_count;  // [0]: tile parts listed
     unsigned long long* __restrict__ split_keys;  // key slices of split parts: (part, chunk), kBlockRows x 64 each
     unsigned* __restrict__ arrive;            // per (tile, part): chunks finished (self-resetting)
@@ -1195,20 +1195,22 @@ __device__ __forceinline__ void PacketBatch(CullShared& sh, const Box& bb, const
 }
 
 // ---------------------------------------------------------------------------------------
-// Cull bins: the first cull level, built per band before the trace. A tile is 64 x 32 rays
-// (one trace block).
+// Cull bins: the first cull level, built per band before the trace, in three launches (the
+// record setup rides in the first). A tile is 64 x 32 rays.
 //   TileInfoKernel:     one block per tile reads the tile's sample offsets once: the ray
-//                       box, "regular" (every offset equal to the first, bit for bit) and the
-//                       first offset; it clears the tile's bin count.
-//   BinTrianglesKernel: every block first reduces the tile boxes to per tile-column and per
-//                       tile-row bounds, made monotone (suffix minimum of lo, prefix maximum
-//                       of hi). Then one thread per record: binary searches in them give
-//                       the contiguous range of tile columns and rows whose boxes can overlap
-//                       the record's screen box; every tile of the range whose own box passes
-//                       the screen-box overlap and the edge-function corner test (BoxMayHit)
-//                       gets the id appended to its list. A record whose range spans more than
+//   (PrepareInfoKernel) box, "regular" (every offset equal to the first, bit for bit) and the
+//                       first offset; it clears the tile's bin count and tags the frame if an
+//                       offset lies outside [0, 1].
+//   BinTrianglesKernel: per tile column and row, monotone bounds of the tile boxes (analytic
+//                       for offsets in [0, 1], else reduced from the tile boxes: BinTileBounds).
+//                       Then one thread per record: binary searches in the bounds give the
+//                       contiguous range of tile columns and rows whose boxes can overlap the
+//                       record's screen box; every tile of the range whose own box passes the
+//                       screen-box overlap and the edge-function corner test (BoxMayHit) gets
+//                       the id appended to its list. A record whose range spans more than
 //                       kLargeTiles tiles (big, or an unbounded screen box) goes to the large
 //                       list, which every binned tile walks after its own list.
+//   WorkOrderKernel:    one block lists the trace work (BuildWorkOrder).
 // Both steps drop only (record, tile) pairs that provably fail the exact test for every ray
 // of the tile, so the frame stays bit-identical to brute force. A tile whose box is outside
 // the screen-box range, or whose list overflowed, streams every record instead.
@@ -1224,9 +1226,10 @@ struct BinParams {
     unsigned* __restrict__ counts;      // tiles + 1 (the last one: large list)
     unsigned* __restrict__ lists;       // tiles x capacity
     unsigned* __restrict__ large_list;  // n_pad
-    uint4* __restrict__ work;           // trace work list (TileOrderKernel): 2 x uint4 per tile part
+    uint4* __restrict__ work;           // trace work list (BuildWorkOrder): 2 x uint4 per tile part
     unsigned* __restrict__ work_count;  // [0]: tile parts listed
-    float2* __restrict__ bounds;        // tiles_x + tiles_y monotone tile column / row bounds (TileBoundsKernel)
+    unsigned* __restrict__ range_tag;   // = gen: some sample offset of this frame lies outside [0, 1]
+    unsigned gen;                       // frame number of the scene (never 0)
     unsigned capacity;
     unsigned n;
     unsigned exp;  // diagnostic build: experiment bits (env SRT_EXP), 0 in the product
@@ -1278,6 +1281,7 @@ __device__ __forceinline__ void TileInfoBlock(const BinParams& p, int bx, int by
     constexpr int kPer = kWave * kTileRows / kBinThreads;  // offsets per thread (8)
     __shared__ Box boxes[kWaves];
     __shared__ unsigned irregular;
+    __shared__ unsigned out_of_range;
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
     const int wave = tid / kWave;
@@ -1285,6 +1289,7 @@ __device__ __forceinline__ void TileInfoBlock(const BinParams& p, int bx, int by
     const int y0 = by * kTileRows;
     if (tid == 0) {
         irregular = 0u;
+        out_of_range = 0u;
     }
     // All loads first (clamped addresses: duplicates of real pixels), then the box. Same
     // expressions as GenerateRays; NaN positions drop out of the box (fminf / fmaxf).
@@ -1297,7 +1302,7 @@ __device__ __forceinline__ void TileInfoBlock(const BinParams& p, int bx, int by
         o[k] = p.offsets[static_cast<size_t>(yy) * p.width + xx];
     }
     Box box{__builtin_inff(), -__builtin_inff(), __builtin_inff(), -__builtin_inff()};
-    bool regular = true;
+    bool regular = true, in_range = true;
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
         const int yy = min(y0 + wave + k * kWaves, p.row_count - 1);
@@ -1306,14 +1311,19 @@ __device__ __forceinline__ void TileInfoBlock(const BinParams& p, int bx, int by
         box = Box{fminf(box.xlo, fx), fmaxf(box.xhi, fx), fminf(box.ylo, fy), fmaxf(box.yhi, fy)};
         regular = regular && __float_as_uint(o[k].x) == __float_as_uint(o0.x) &&
                   __float_as_uint(o[k].y) == __float_as_uint(o0.y);
+        in_range = in_range && o[k].x >= 0.f && o[k].x <= 1.f && o[k].y >= 0.f && o[k].y <= 1.f;  // NaN: false
     }
     box = WaveReduceBox(box);
     const bool wave_regular = __all(regular);
-    __syncthreads();  // `irregular` initialised
+    const bool wave_in_range = __all(in_range);
+    __syncthreads();  // `irregular`, `out_of_range` initialised
     if (lane == 0) {
         boxes[wave] = box;
         if (!wave_regular) {
             irregular = 1u;
+        }
+        if (!wave_in_range) {
+            out_of_range = 1u;
         }
     }
     __syncthreads();
@@ -1335,6 +1345,9 @@ __device__ __forceinline__ void TileInfoBlock(const BinParams& p, int bx, int by
         p.counts[tile] = 0u;  // the bin kernel runs after this one (stream order)
         if (tile == 0) {
             p.counts[p.tiles_x * p.tiles_y] = 0u;  // large list
+        }
+        if (out_of_range != 0u) {
+            *p.range_tag = p.gen;  // this frame's bin blocks reduce the tile boxes (BinTileBounds)
         }
     }
 }
@@ -1396,57 +1409,67 @@ __device__ __forceinline__ int LastLoAtMost(const float2* b, int n, float v) {
 // the block counts its (tile, record) pairs in an LDS histogram, reserves each touched
 // tile's share of its list with ONE global atomic, then writes the ids. (Per-pair global
 // atomics serialise on the busy tiles' counters at the memory side.)
-// Trace work list: one block after the bin kernel. One 32-B descriptor per tile part, listed
-// longest first (counting sort by the log2 of the tile's candidates, FULL-stream tiles first),
-// so the heavy parts start first and the light ones fill in behind them; order within a bucket
-// is arbitrary (the frame does not depend on it). The trace grid is parts x M blocks: block b
-// runs chunk b % M of part b / M (TraceCullKernel splits a part's candidates into at most M
-// chunks of at least `chunk` candidates; the chunks past a part's count exit at once).
+// Trace work list (WorkOrderKernel, after the bin kernel). One 32-B descriptor per
+// tile part, listed longest first (counting sort by the log2 of the tile's candidates, FULL-stream
+// tiles first), so the heavy parts start first and the light ones fill in behind them; order
+// within a bucket is arbitrary (the frame does not depend on it). The trace grid is parts x M
+// blocks: block b runs chunk b % M of part b / M (TraceCullKernel splits a part's candidates into
+// at most M chunks of at least `chunk` candidates; the chunks past a part's count exit at once).
 // Descriptor: w0 = (tile part, candidates, tile list length, flags), w1 = (sample offset x, y of
 // the tile's first ray, 0, 0); flags: 1 = every ray of the tile has that offset, 2 = FULL.
 constexpr unsigned kItemRegular = 1u;
 constexpr unsigned kItemFull = 2u;
-constexpr int kOrderThreads = 1024;
-constexpr int kOrderPer = kMaxBinTiles / kOrderThreads;  // tiles per thread
-__global__ __launch_bounds__(kOrderThreads) void TileOrderKernel(BinParams p) {
-    __shared__ unsigned start[64];
+struct OrderItem {
+    unsigned cand, flags, bucket, parts;
+};
+__device__ __forceinline__ OrderItem MakeOrderItem(const BinParams& p, unsigned t, unsigned cnt, unsigned large,
+                                                   const TileInfo& ti) {
+    OrderItem it;
+    const bool full = ti.usable == 0u || cnt > p.capacity;
+    it.flags = (full ? kItemFull : 0u) | (ti.regular != 0u ? kItemRegular : 0u);
+    it.cand = full ? 0u : cnt + large;
+    it.bucket = full ? 63u : (it.cand == 0u ? 0u : 32u - __builtin_clz(it.cand));
+    const int rows_left = p.row_count - static_cast<int>(t / static_cast<unsigned>(p.tiles_x)) * kTileRows;
+    it.parts = static_cast<unsigned>(min(kParts, (rows_left + kBlockRows - 1) / kBlockRows));
+    return it;
+}
+// Called by every thread of the order block; start = 64 LDS words, cnt = tiles LDS words. Two passes,
+// each issuing all of a thread's loads together (kOrderUnroll tiles): (1) lengths + tile flags
+// -> bucket histogram, lengths kept in LDS; (2) tile info again -> descriptors.
+constexpr int kOrderUnroll = 4;
+__device__ void BuildWorkOrder(const BinParams& p, unsigned* start, unsigned* cnt) {
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
-    const int wave = tid / kWave;
+    const unsigned nthreads = blockDim.x;
     const unsigned tiles = static_cast<unsigned>(p.tiles_x * p.tiles_y);
-    const unsigned large = p.counts[tiles];
     if (tid < 64) {
         start[tid] = 0u;
     }
-    // This thread's tiles t = tid + k * kOrderThreads.
-    unsigned cand[kOrderPer], cnt[kOrderPer], ox[kOrderPer], oy[kOrderPer], flags[kOrderPer], parts[kOrderPer],
-        bucket[kOrderPer];
-#pragma unroll
-    for (int k = 0; k < kOrderPer; ++k) {
-        const unsigned t = tid + k * kOrderThreads;
-        parts[k] = 0u;
-        if (t < tiles) {
-            cnt[k] = p.counts[t];
-            const TileInfo ti = p.tile_info[t];
-            ox[k] = __float_as_uint(ti.ox);
-            oy[k] = __float_as_uint(ti.oy);
-            const bool full = ti.usable == 0u || cnt[k] > p.capacity;
-            flags[k] = (full ? kItemFull : 0u) | (ti.regular != 0u ? kItemRegular : 0u);
-            cand[k] = full ? 0u : cnt[k] + large;
-            bucket[k] = full ? 63u : (cand[k] == 0u ? 0u : 32u - __builtin_clz(cand[k]));
-            const int rows_left = p.row_count - static_cast<int>(t / static_cast<unsigned>(p.tiles_x)) * kTileRows;
-            parts[k] = static_cast<unsigned>(min(kParts, (rows_left + kBlockRows - 1) / kBlockRows));
-        }
-    }
+    const unsigned large = p.counts[tiles];
     __syncthreads();  // start[] zeroed
+    for (unsigned t0 = tid; t0 < tiles; t0 += kOrderUnroll * nthreads) {
+        unsigned c[kOrderUnroll];
+        TileInfo ti[kOrderUnroll];
 #pragma unroll
-    for (int k = 0; k < kOrderPer; ++k) {
-        if (parts[k] != 0u) {
-            atomicAdd(&start[bucket[k]], parts[k]);
+        for (int u = 0; u < kOrderUnroll; ++u) {
+            const unsigned t = min(t0 + u * nthreads, tiles - 1u);
+            c[u] = p.counts[t];
+            ti[u] = p.tile_info[t];
+        }
+#pragma unroll
+        for (int u = 0; u < kOrderUnroll; ++u) {
+            const unsigned t = t0 + u * nthreads;
+            if (t < tiles) {
+                cnt[t] = c[u];
+                const OrderItem it = MakeOrderItem(p, t, c[u], large, ti[u]);
+                if (it.parts != 0u) {
+                    atomicAdd(&start[it.bucket], it.parts);
+                }
+            }
         }
     }
     __syncthreads();
-    if (wave == 0) {  // bucket b's first slot: the parts in heavier buckets (suffix sum, exclusive)
+    if (tid < kWave) {  // bucket b's first slot: the parts in heavier buckets (suffix sum, exclusive)
         const unsigned c = start[lane];
         unsigned suf = c;
 #pragma unroll
@@ -1460,28 +1483,59 @@ __global__ __launch_bounds__(kOrderThreads) void TileOrderKernel(BinParams p) {
         }
     }
     __syncthreads();
+    for (unsigned t0 = tid; t0 < tiles; t0 += kOrderUnroll * nthreads) {
+        TileInfo ti[kOrderUnroll];
 #pragma unroll
-    for (int k = 0; k < kOrderPer; ++k) {
-        if (parts[k] != 0u) {
-            const unsigned t = tid + k * kOrderThreads;
-            const unsigned at = atomicAdd(&start[bucket[k]], parts[k]);
-            for (unsigned part = 0; part < parts[k]; ++part) {
-                p.work[2 * (at + part)] = make_uint4(t * kParts + part, cand[k], cnt[k], flags[k]);
-                p.work[2 * (at + part) + 1] = make_uint4(ox[k], oy[k], 0u, 0u);
+        for (int u = 0; u < kOrderUnroll; ++u) {
+            ti[u] = p.tile_info[min(t0 + u * nthreads, tiles - 1u)];
+        }
+#pragma unroll
+        for (int u = 0; u < kOrderUnroll; ++u) {
+            const unsigned t = t0 + u * nthreads;
+            if (t >= tiles) {
+                continue;
+            }
+            const OrderItem it = MakeOrderItem(p, t, cnt[t], large, ti[u]);
+            if (it.parts != 0u) {
+                const unsigned at = atomicAdd(&start[it.bucket], it.parts);
+                for (unsigned part = 0; part < it.parts; ++part) {
+                    p.work[2 * (at + part)] = make_uint4(t * kParts + part, it.cand, cnt[t], it.flags);
+                    p.work[2 * (at + part) + 1] = make_uint4(__float_as_uint(ti[u].ox), __float_as_uint(ti[u].oy), 0u, 0u);
+                }
             }
         }
     }
 }
 
-// Monotone tile-column and tile-row bounds of the usable tiles' boxes (lo' = suffix minimum,
-// hi' = prefix maximum; both nondecreasing) into out[0 .. nx + ny) (LDS or global). One block
-// of >= 4 waves; `scratch` = 2 (nx + ny) LDS words. Ends with a barrier.
-__device__ void TileBounds(const BinParams& p, unsigned* scratch, float2* out) {
+// A bin block's monotone tile-column and tile-row bounds (lo' nondecreasing, hi' nondecreasing)
+// into out[0 .. nx + ny) in LDS; `scratch` = 2 (nx + ny) LDS words; ends with a barrier.
+//  * Every sample offset of the frame in [0, 1] (no tile block tagged the frame): tile column c
+//    holds x in [64c, 64c + 63], so fl(x + o) lies in [64c, 64c + 64] and, the rounded division
+//    being monotone, every fx of the tile in [fl(64c / W), fl((64c + 64) / W)]; rows likewise.
+//    These analytic bounds contain every tile box and are already monotone: no reduction.
+//  * Otherwise (offsets outside [0, 1], NaN): the usable tiles' boxes reduced per column and row
+//    with LDS atomics on order-preserving bits, then made monotone (lo' = suffix minimum,
+//    hi' = prefix maximum) by wave scans.
+// Either way a tile outside a record's searched range cannot overlap its screen box; the tiles
+// inside are tested against their own boxes, so the bins do not depend on which path ran.
+__device__ void BinTileBounds(const BinParams& p, unsigned* scratch, float2* out) {
     const int tid = threadIdx.x;
     const int nthreads = blockDim.x;
     const int lane = tid & (kWave - 1);
     const int wave = tid / kWave;
     const int nx = p.tiles_x, ny = p.tiles_y;
+    if (*p.range_tag != p.gen) {  // written by the previous launch's tile blocks
+        for (int i = tid; i < nx + ny; i += nthreads) {
+            const bool col = i < nx;
+            const float v0 = col ? static_cast<float>(i * kWave) : static_cast<float>(p.row_begin + (i - nx) * kTileRows);
+            const float v1 = col ? static_cast<float>((i + 1) * kWave)
+                                 : static_cast<float>(p.row_begin + (i - nx + 1) * kTileRows);
+            const float d = col ? p.wf : p.hf;
+            out[i] = make_float2(v0 / d, v1 / d);
+        }
+        __syncthreads();
+        return;
+    }
     const int tiles = nx * ny;
     unsigned* col_lo = scratch;
     unsigned* col_hi = scratch + nx;
@@ -1523,17 +1577,10 @@ __device__ void TileBounds(const BinParams& p, unsigned* scratch, float2* out) {
     __syncthreads();
 }
 
-// One block: the frame's tile bounds, once, for every bin block (a bin block reducing all
-// tile infos itself costs O(tiles) L2 reads per block: 0.5 GB per frame at C5).
-__global__ __launch_bounds__(1024) void TileBoundsKernel(BinParams p) {
-    __shared__ unsigned scratch[2 * kMaxBoundTiles];
-    TileBounds(p, scratch, p.bounds);
-}
-
 // LDS of a bin block (dynamic, sized to the band so the bin blocks of one frame leave room for
-// other frames' trace blocks): the tile bounds, then the histogram (also TileBounds' scratch).
+// other frames' trace blocks): the tile bounds, then the histogram.
 std::size_t BinLdsBytes(int nx, int ny) {
-    const int hist = nx * ny > 2 * (nx + ny) ? nx * ny : 2 * (nx + ny);
+    const int hist = nx * ny > 2 * (nx + ny) ? nx * ny : 2 * (nx + ny);  // also BinTileBounds' scratch
     return static_cast<std::size_t>(nx + ny) * sizeof(float2) + static_cast<std::size_t>(hist) * sizeof(unsigned);
 }
 
@@ -1545,19 +1592,13 @@ __global__ __launch_bounds__(kBinThreads) void BinTrianglesKernel(BinParams p) {
     float2* b = bin_lds;
     unsigned* hist = reinterpret_cast<unsigned*>(bin_lds + nx + ny);
 
-    // Prologue: the monotone tile-column and tile-row bounds -- precomputed once per frame by
-    // TileBoundsKernel (p.bounds), or reduced here by every block (SRT_TILE_BOUNDS=0).
-    if (p.bounds != nullptr) {
-        for (int i = tid; i < nx + ny; i += kBinThreads) {
-            b[i] = p.bounds[i];
-        }
-    } else {
-        TileBounds(p, hist, b);
-    }
-    __syncthreads();
+    // Prologue: the monotone tile-column and tile-row bounds (the histogram's LDS is the
+    // reduction's scratch), then the histogram zeroed.
+    BinTileBounds(p, hist, b);
     for (int t = tid; t < tiles; t += kBinThreads) {
         hist[t] = 0u;
     }
+    __syncthreads();  // bounds in LDS, histogram zeroed
 
     // This thread's record: its tile range and the tiles of it that pass (bit k = tile
     // (r0 + k / w, c0 + k % w) of the range, at most kLargeTiles of them).
@@ -1593,7 +1634,6 @@ __global__ __launch_bounds__(kBinThreads) void BinTrianglesKernel(BinParams p) {
             }
         }
     }
-    __syncthreads();  // histogram zeroed
     for (unsigned m = mask; m != 0u; m &= m - 1u) {
         const int k = __builtin_ctz(m);
         atomicAdd(&hist[(r0 + k / w) * nx + c0 + k % w], 1u);
@@ -1614,6 +1654,19 @@ __global__ __launch_bounds__(kBinThreads) void BinTrianglesKernel(BinParams p) {
             p.lists[static_cast<size_t>(t) * p.capacity + at] = i;
         }
     }
+    // Every block's list lengths are final (its count atomics returned): the last block to
+    // finish lists the trace work (one launch fewer than a separate ordering kernel).
+}
+
+// The trace work list: one 1024-thread block after the bin kernel. Built instead by the bin
+// kernel's last block (self-resetting arrival counter, sc1 count loads) the frame has one
+// launch fewer but the ~5 us single-block tail inside the bin launch cost 10 % of the
+// three-queue throughput at C3 (60.9 vs 67.3 Grays/s; plain, no-wait and two-level arrivals
+// alike: profiles/r02/ab_order/).
+__global__ __launch_bounds__(1024) void WorkOrderKernel(BinParams p) {
+    __shared__ unsigned start[64];
+    __shared__ unsigned cnt[kMaxBinTiles];
+    BuildWorkOrder(p, start, cnt);
 }
 
 #ifndef SRT_TRACE_OCC
@@ -2371,7 +2424,7 @@ unsigned CullBinCapacity(std::uint64_t n, std::size_t tiles) {
 
 namespace {
 struct BinSizes {
-    std::size_t info, counts, lists, large, work, work_count, arrive, split_keys, bounds;
+    std::size_t info, counts, lists, large, work, work_count, arrive, split_keys, range_tag;
 };
 BinSizes CullBinSizes(std::uint64_t n, std::size_t width, std::size_t row_count) {
     const std::size_t tx = (width + kWave - 1) / kWave, ty = (row_count + kTileRows - 1) / kTileRows;
@@ -2387,7 +2440,7 @@ BinSizes CullBinSizes(std::uint64_t n, std::size_t width, std::size_t row_count)
     z.work_count = al(4);
     z.arrive = al(tiles * kParts * 4);
     z.split_keys = m > 1 ? al(tiles * kParts * m * kBlockRows * kWave * 8) : 0;
-    z.bounds = al((tx + ty) * 8);
+    z.range_tag = al(4);
     return z;
 }
 }  // namespace
@@ -2421,7 +2474,7 @@ unsigned CullMaxChunks(std::size_t tiles) {
 
 std::size_t CullBinBytes(std::uint64_t n, std::size_t width, std::size_t row_count) {
     const BinSizes z = CullBinSizes(n, width, row_count);
-    return z.info + z.counts + z.lists + z.large + z.work + z.work_count + z.arrive + z.split_keys + z.bounds;
+    return z.info + z.counts + z.lists + z.large + z.work + z.work_count + z.arrive + z.split_keys + z.range_tag;
 }
 
 CullBins CullBinLayout(void* base, std::uint64_t n, std::size_t width, std::size_t row_count) {
@@ -2441,7 +2494,7 @@ CullBins CullBinLayout(void* base, std::uint64_t n, std::size_t width, std::size
     b.work_count = reinterpret_cast<unsigned*>(take(z.work_count));
     b.arrive = reinterpret_cast<unsigned*>(take(z.arrive));
     b.split_keys = take(z.split_keys);
-    b.bounds = take(z.bounds);
+    b.range_tag = reinterpret_cast<unsigned*>(take(z.range_tag));
     b.tiles = CullTiles(width, row_count);
     b.capacity = CullBinCapacity(n, b.tiles);
     b.max_chunks = z.split_keys != 0 ? CullMaxChunks(b.tiles) : 1u;
@@ -2537,17 +2590,8 @@ hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_ver
             b.large_list = bins->large_list;
             b.work = static_cast<uint4*>(bins->work);
             b.work_count = bins->work_count;
-            // Tile bounds once per frame (TileBoundsKernel) when the bin blocks' own reductions
-            // would cost more: (bin blocks) x (tiles) tile-info reads above 200k (C5: 16M, bin
-            // stage 164 -> 75 us; C3: 0.4M, where the extra launch adds ~1 % to one frame's
-            // latency but the chip time it saves gives +3 % with frame queues in flight; C2 and
-            // small frames: 1k, no extra launch). Env SRT_TILE_BOUNDS=0/1 forces either way.
-            {
-                const std::uint64_t reads = (n + kBinThreads - 1) / kBinThreads * static_cast<std::uint64_t>(gx) * gy;
-                const char* v = std::getenv("SRT_TILE_BOUNDS");
-                const bool once = v != nullptr && *v != '\0' ? std::strcmp(v, "0") != 0 : reads > 200000ull;
-                b.bounds = once ? static_cast<float2*>(bins->bounds) : nullptr;
-            }
+            b.range_tag = bins->range_tag;
+            b.gen = bins->gen;
             b.capacity = bins->capacity;
             b.n = static_cast<unsigned>(n);
             b.tiles_x = static_cast<int>(gx);
@@ -2573,16 +2617,11 @@ hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_ver
             } else {
                 Launch(TileInfoKernel, dim3(gx, gy), dim3(kBinThreads), stream, ev.prep_begin, ev.prep_end, b);
             }
-            if (n != 0 && b.bounds != nullptr) {
-                Launch(TileBoundsKernel, dim3(1), dim3(1024), stream, ev.bin_begin, nullptr, b);
-            }
-            if (n != 0) {
-                const unsigned blocks = static_cast<unsigned>((n + kBinThreads - 1) / kBinThreads);
-                LaunchLds(BinTrianglesKernel, dim3(blocks), dim3(kBinThreads), BinLdsBytes(b.tiles_x, b.tiles_y), stream,
-                          b.bounds != nullptr ? nullptr : ev.bin_begin, nullptr, b);
-            }
-            Launch(TileOrderKernel, dim3(1), dim3(kOrderThreads), stream, n != 0 ? nullptr : ev.bin_begin,
-                   ev.bin_end, b);
+            // Bins (at least one block), then the trace work list.
+            const unsigned blocks = static_cast<unsigned>(n == 0 ? 1 : (n + kBinThreads - 1) / kBinThreads);
+            LaunchLds(BinTrianglesKernel, dim3(blocks), dim3(kBinThreads), BinLdsBytes(b.tiles_x, b.tiles_y), stream,
+                      ev.bin_begin, nullptr, b);
+            Launch(WorkOrderKernel, dim3(1), dim3(1024), stream, nullptr, ev.bin_end, b);
             p.tile_info = b.tile_info;
             p.order = bins->order;
             p.work = b.work;
@@ -2599,7 +2638,7 @@ hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_ver
         p.tiles_x = static_cast<int>(gx);
         p.tiles = gx * gy;
         if (p.work != nullptr) {
-            // Binned: one block per work item of TileOrderKernel's list (at most the budget).
+            // Binned: M blocks per work item of the bin kernel's list (BuildWorkOrder).
             Launch(TraceCullKernel, dim3(static_cast<unsigned>(p.tiles * kParts * p.max_chunks)),
                    dim3(kWave * kCullWaves), stream, ev.begin, ev.end, p);
         } else {

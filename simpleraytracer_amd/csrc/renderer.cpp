@@ -303,6 +303,8 @@ void DeviceScene::Trace(const float* d_offsets, float* d_rgba, std::size_t row_b
         }
         bins = CullBinLayout(m_cull_work, m_n, m_width, row_count);
         bins.order = m_order;
+        m_cull_gen = m_cull_gen + 1u == 0u ? 1u : m_cull_gen + 1u;
+        bins.gen = m_cull_gen;
         use_bins = &bins;
     }
     if (variant == kTraceBvh && m_bvh == nullptr && row_count != 0) {

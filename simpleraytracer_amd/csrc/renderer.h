@@ -89,6 +89,7 @@ private:
     mutable std::size_t m_cull_bytes = 0;
     mutable std::uint64_t m_cull_shape = 0;  // (width << 32) | rows of the current carve-up
     mutable std::size_t m_cull_layout = 0;   // its bytes (they change with the split width too)
+    mutable unsigned m_cull_gen = 0;         // frames binned (render.h CullBins::gen)
     // BVH variant: node boxes + depth bounds (render.h BvhLayout), allocated by the first bvh Trace.
     mutable unsigned char* m_bvh = nullptr;
     // Stage-timing events, reused: per timed Prepare (begin, end), per timed Trace (bin begin,

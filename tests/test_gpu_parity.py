@@ -174,20 +174,36 @@ def test_cull_modes(gpu, scenes, monkeypatch, mode):
         assert_parity(got, oracle_render(scenes["soup2k"], w, h, offsets))
 
 
-@pytest.mark.parametrize("bounds", ["0", "1"])
-def test_cull_tile_bounds_paths(gpu, scenes, monkeypatch, bounds):
-    """Tile column/row bounds reduced by every bin block (SRT_TILE_BOUNDS=0) or once per frame
-    by TileBoundsKernel (=1): the same frame, bit for bit, and oracle parity on a row sample."""
-    monkeypatch.delenv("SRT_TILE_BOUNDS", raising=False)
-    ref = torch_render(scenes["soup100k"], 1920, 1080, variant="lds")
-    monkeypatch.setenv("SRT_TILE_BOUNDS", bounds)
-    got = torch_render(scenes["soup100k"], 1920, 1080, variant="cull")
-    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
-    rng = np.random.default_rng(23)
-    w, h = 257, 131
-    offsets = rng.random((h, w, 2), dtype=np.float32)
-    assert_parity(torch_render(scenes["soup2k"], w, h, offsets, variant="cull"),
-                  oracle_render(scenes["soup2k"], w, h, offsets))
+def test_cull_setup_state_across_frames(gpu, scenes):
+    """The per-frame setup hands off between blocks through self-resetting state (tile-box
+    accumulators and the last tile block's bounds, the bin blocks' arrival count and the last
+    bin block's work list): one scene over frames whose band shape (the layout is re-zeroed)
+    and offsets (uniform, random, far outside the frame, NaN) change, each frame bit-identical
+    to a fresh brute-force render, twice in a row."""
+    import torch
+
+    import simpleraytracer_amd as srt
+
+    w, h = 333, 170
+    rng = np.random.default_rng(29)
+    far = np.full((h, w, 2), -3.25, np.float32)
+    nan = rng.random((h, w, 2), dtype=np.float32)
+    nan[5:40, 70:90] = np.nan
+    cases = [(0, h, None), (40, 77, rng.random((h, w, 2), dtype=np.float32)), (0, h, far), (17, 1, None),
+             (0, h, nan), (0, h, None)]
+    scene = srt.DeviceScene(scenes["soup2k"], 0)
+    stream = torch.cuda.current_stream()
+    for rep in range(2):
+        for k, (r0, rows, offs) in enumerate(cases):
+            o = np.full((h, w, 2), 0.5, np.float32) if offs is None else offs
+            ref = torch_render(scenes["soup2k"], w, h, o, variant="lds")[r0:r0 + rows]
+            off = torch.from_numpy(np.ascontiguousarray(o[r0:r0 + rows])).cuda()
+            out = torch.full((rows, w, 4), float("nan"), dtype=torch.float32, device="cuda")
+            scene.prepare(w, h, stream)
+            scene.trace(off, out, r0, rows, variant="cull", stream=stream)
+            torch.cuda.synchronize()
+            assert np.array_equal(out.cpu().numpy().view(np.uint32), ref.view(np.uint32)), (rep, k)
+    scene.close()
 
 
 @pytest.mark.parametrize("mode", CULL_MODES[:4])
