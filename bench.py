@@ -71,8 +71,9 @@ def parse():
     p.add_argument("--root", default="rotate", choices=["rotate", "fixed"], help="bands: compositing rank")
     p.add_argument("--queues", type=int, default=int(os.environ.get("SRT_BENCH_QUEUES", "3")),
                    help="frames in flight per GPU (own scene buffers, HIP stream, process group each)")
-    p.add_argument("--batch", type=int, default=int(os.environ.get("SRT_BENCH_BATCH", "8")),
-                   help="bands, N > 1: frames per gather (one collective and one shading launch per batch)")
+    p.add_argument("--batch", type=int, default=int(os.environ.get("SRT_BENCH_BATCH", "0")),
+                   help="frames per launch (srtTraceBatchAsync, <= 8) and, bands at N > 1, per gather and "
+                        "shading launch; 0 = 8 at N > 1, 1 at N = 1")
     p.add_argument("--offsets", default="uniform", choices=["uniform", "random"],
                    help="sample offsets: uniform 0.5 (headline) or seeded U[0,1) per-pixel jitter")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample length")
@@ -168,7 +169,7 @@ class Pipeline:
     band r of every frame (P > 1: hit ids, gathered to the compositor, which shades); mode
     "frames": whole frames, each rank its own jitter; P == 1: the two coincide."""
 
-    def __init__(self, ctx, path, mode="bands", queues=3, variant="cull", offsets="uniform", rotate=True, batch=8):
+    def __init__(self, ctx, path, mode="bands", queues=3, variant="cull", offsets="uniform", rotate=True, batch=1):
         from simpleraytracer_amd.bands import band_range, band_rows
 
         torch, a = ctx.torch, ctx.a
@@ -176,52 +177,61 @@ class Pipeline:
         self.W, self.H = a.width, a.height
         P = ctx.world if mode == "bands" else 1
         self.P = P
-        self.G = max(1, batch) if P > 1 else 1  # frames per gather (one collective per G frames)
+        self.G = max(1, min(batch, ctx.srt.MAX_BATCH))  # frames per launch (and per gather at P > 1)
         self.row_begin, self.row_count = band_range(self.H, P, ctx.rank) if P > 1 else (0, self.H)
         self.B = band_rows(self.H, P)
         self.offsets = make_offsets(torch, a, ctx.dev, jitter(ctx.rank) if mode == "frames" else 0.5, offsets,
                                     seed=0x5EED + (ctx.rank if mode == "frames" else 0))
         self.band_off = self.offsets[self.row_begin:self.row_begin + self.row_count]
+        self.timing = False
         self.queues = []
         for q in range(max(1, queues)):
             qd = {"scene": ctx.srt.DeviceScene(path, ctx.dev.index), "stream": torch.cuda.Stream(ctx.dev),
-                  "root": None, "index": q, "fill": 0, "batches": 0, "shaded": 0}
+                  "root": None, "index": q, "fill": 0, "traced": 0, "batches": 0, "shaded": 0, "runs": {}}
+            qd["scene"].prepare(self.W, self.H)
+            qd["rgba"] = torch.zeros((self.G, self.H, self.W, 4), dtype=torch.float32, device=ctx.dev)
             if P > 1:
-                qd["rgba"] = torch.zeros((self.G, self.H, self.W, 4), dtype=torch.float32, device=ctx.dev)
                 qd["band_ids"] = torch.full((self.G, self.B, self.W), -1, dtype=torch.int32, device=ctx.dev)
                 qd["frame_ids"] = torch.empty(P * self.G * self.B * self.W, dtype=torch.int32, device=ctx.dev)
                 qd["group"] = ctx.groups[q % len(ctx.groups)]
-                qd["scene"].prepare(self.W, self.H)
-                # one validated launch closure per batch slot (the frame loop's host cost is HIP's)
-                qd["slots"] = [qd["scene"].bind_trace_ids(self.band_off, qd["band_ids"][j, :self.row_count],
-                                                          self.row_begin, self.row_count, variant=variant,
-                                                          stream=qd["stream"]) if self.row_count else None
-                               for j in range(self.G)]
-            else:
-                qd["rgba"] = torch.zeros((self.H, self.W, 4), dtype=torch.float32, device=ctx.dev)
             self.queues.append(qd)
         self.triangles = self.queues[0]["scene"].triangles
 
+    def _batch_run(self, q, f):
+        """The queue's batched trace of its first f slots (one srtTraceBatchAsync call), bound once."""
+        if f not in q["runs"]:
+            sc, st = q["scene"], q["stream"]
+            if self.P > 1:
+                q["runs"][f] = sc.bind_trace_batch([self.band_off] * f, [q["band_ids"][j, :self.row_count]
+                                                                         for j in range(f)],
+                                                   self.row_begin, self.row_count, self.variant, st, ids=True)
+            else:
+                q["runs"][f] = sc.bind_trace_batch([self.offsets] * f, [q["rgba"][j] for j in range(f)], 0, self.H,
+                                                   self.variant, st)
+        return q["runs"][f]
+
     def step(self, k, nq):
+        """Frame k on queue k % nq: into the queue's next batch slot; a full batch is traced
+        (one call for all its frames), then at P > 1 gathered and shaded. With stage timing
+        on, each frame is traced on its own (the single-frame calls bind the HIP events)."""
         q = self.queues[k % nq]
         sc, st = q["scene"], q["stream"]
-        if self.P == 1:
-            sc.prepare(self.W, self.H, st)
-            sc.trace(self.offsets, q["rgba"], 0, self.H, variant=self.variant, stream=st)
-            q["root"] = 0
-            return
         j = q["fill"]
-        if q["slots"][j] is not None:
-            q["slots"][j]()  # prepare + trace of this rank's band of the frame, ids into batch slot j
-        else:  # a rank with no rows (P > H) still prepares its frame
+        if self.timing and self.row_count:
             sc.prepare(self.W, self.H, st)
+            if self.P > 1:
+                sc.trace_ids(self.band_off, q["band_ids"][j, :self.row_count], self.row_begin, self.row_count,
+                             variant=self.variant, stream=st)
+            else:
+                sc.trace(self.offsets, q["rgba"][j], 0, self.H, variant=self.variant, stream=st)
+            q["traced"] = j + 1
         q["fill"] = j + 1
         if q["fill"] == self.G:
             self.flush(q, nq)
 
     def flush(self, q, nq):
-        """Gather the queue's filled batch slots (one collective for all of them) to the batch's
-        compositor, which shades every frame of the batch in one launch."""
+        """Trace the queue's filled slots (if not yet), then at P > 1 gather them (one collective
+        for all of them) to the batch's compositor, which shades every frame in one launch."""
         from simpleraytracer_amd.bands import compositor, gather_band_batch
 
         ctx, torch = self.ctx, self.ctx.torch
@@ -229,6 +239,12 @@ class Pipeline:
         if f == 0:
             return
         sc, st = q["scene"], q["stream"]
+        if q["traced"] < f and self.row_count:
+            self._batch_run(q, f)()
+        q["fill"] = q["traced"] = 0
+        if self.P == 1:
+            q["root"], q["shaded"] = 0, f
+            return
         root = compositor(q["batches"] * nq + q["index"], self.P, self.rotate)
         batch = q["band_ids"][:f]
         if ctx.backend == "gloo":  # CPU rehearsal: gloo gathers host tensors, synchronously
@@ -250,12 +266,10 @@ class Pipeline:
             q["shaded"] = f
         q["root"] = root
         q["batches"] += 1
-        q["fill"] = 0
 
     def drain(self, nq=None):
-        if self.P > 1:  # partial batches: every queue's filled slots are gathered and shaded
-            for q in self.queues[:nq or len(self.queues)]:
-                self.flush(q, nq or len(self.queues))
+        for q in self.queues[:nq or len(self.queues)]:  # partial batches
+            self.flush(q, nq or len(self.queues))
         for q in self.queues:
             q["stream"].synchronize()
 
@@ -270,6 +284,7 @@ class Pipeline:
         sc0 = self.queues[0]["scene"]
         sc0.take_stage_times()
         sc0.set_stage_timing(timing)
+        self.timing = timing
         ctx.barrier()
         torch.cuda.synchronize(ctx.dev)
         t0 = time.perf_counter()
@@ -280,6 +295,7 @@ class Pipeline:
         ctx.barrier()
         elapsed = ctx.max_over_ranks(time.perf_counter() - t0)
         sc0.set_stage_timing(False)
+        self.timing = False
         launches, prep_ms, bin_ms, trace_ms = sc0.take_stage_times()
         units = self.W * self.H * steps * (ctx.world if self.mode == "frames" else 1)
         return {"elapsed": elapsed, "mrays": units / elapsed / 1e6, "prepare_ms": prep_ms, "bin_ms": bin_ms,
@@ -298,8 +314,7 @@ class Pipeline:
                 ref_scene.prepare(self.W, self.H, st)
                 ref_scene.trace(self.offsets, ref, 0, self.H, variant=self.variant, stream=st)
                 torch.cuda.synchronize(ctx.dev)
-                frames = q["rgba"][:q["shaded"]] if self.P > 1 else q["rgba"][None]
-                for fr in frames:  # every frame of the queue's last composited batch
+                for fr in q["rgba"][:q["shaded"]]:  # every frame of the queue's last composited batch
                     ok = ok and bool(torch.equal(ref.view(torch.int32), fr.view(torch.int32)))
                 ref_scene.close()
                 break
@@ -433,6 +448,8 @@ def leg_summary(r):
 
 def main():
     a = parse()
+    if a.batch <= 0:
+        a.batch = 8 if a.gpus > 1 else 1
     ctx = Ctx(a)
     world, rank = ctx.world, ctx.rank
     path = ctx.scene_path(a.scene, a.triangles if a.scene == "soup" else None)
@@ -469,14 +486,14 @@ def main():
             legs["secondary_error"] = f"{type(e).__name__}: {e}"
     if world == 1 and extras:
         if a.offsets == "uniform":  # per-pixel jitter: the irregular-offset path
-            o = Pipeline(ctx, path, "bands", a.queues, a.variant, "random")
+            o = Pipeline(ctx, path, "bands", a.queues, a.variant, "random", batch=a.batch)
             rr = o.run(min(a.steps, 1000), a.warmup)
             rt2 = o.run(min(a.steps, 300), 2, queues=1, timing=True)
             o.close()
             legs["offsets_random"] = {**leg_summary(rr), "trace_kernel_ms": round(rt2["trace_ms"], 5),
                                       "note": "seeded U[0,1) per-pixel sample offsets (every tile irregular)"}
         if a.scene == "soup":  # C2: the Cornell box at the same resolution
-            o = Pipeline(ctx, ctx.scene_path("cornell"), "bands", a.queues, a.variant, a.offsets)
+            o = Pipeline(ctx, ctx.scene_path("cornell"), "bands", a.queues, a.variant, a.offsets, batch=a.batch)
             legs["c2_cornell"] = {**leg_summary(o.run(min(a.steps, 1000), a.warmup)),
                                   "workload": workload_name(a, "cornell")}
             o.close()
@@ -527,7 +544,7 @@ def main():
                 "parallelism": par,
                 "trace_variant": a.variant,
                 "frame_queues": r["queues"],
-                "frames_per_gather": main_run.G,
+                "frames_per_launch": main_run.G,
                 "offsets": a.offsets,
             },
             "roofline": roof,

@@ -87,6 +87,17 @@ ML_API_ENTRY int srtTraceAsync(srt_device_scene scene, const float* d_offsets, f
 ML_API_ENTRY int srtTraceIdsAsync(srt_device_scene scene, const float* d_offsets, int* d_ids,
                                   size_t row_begin, size_t row_count, int variant, void* stream);
 
+/* Stages 1-2 for a batch of up to SRT_MAX_BATCH frames of the prepared camera (same band of
+ * each): frame f's sample offsets d_offsets[f] (row_count x width x 2, band-local) and either its
+ * RGBA d_rgba[f] (row_count x width x 4) or, with d_rgba NULL, its hit ids d_ids[f]
+ * (row_count x width). Every frame gets the whole per-frame work of srtPrepareAsync +
+ * srtTraceAsync (record setup, bins, trace): the same pixels, bit for bit; the cull variant runs
+ * the batch with one launch per stage, so a frame costs a quarter of the host launches. */
+#define SRT_MAX_BATCH 8
+ML_API_ENTRY int srtTraceBatchAsync(srt_device_scene scene, const float* const* d_offsets, float* const* d_rgba,
+                                    int* const* d_ids, size_t frames, size_t row_begin, size_t row_count, int variant,
+                                    void* stream);
+
 /* Stage 3 (deferred shading): rows [row_begin, row_begin + row_count) of the prepared frame
  * shaded from hit ids (as srtTraceIdsAsync writes them) and sample offsets (both band-local,
  * row_count x width) into d_rgba: bit-identical to srtTraceAsync's RGBA. */

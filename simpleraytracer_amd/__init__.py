@@ -8,11 +8,11 @@ Layers:
   device.py    scene files + device-level stages on caller buffers (DeviceScene)
   bands.py     row-band partition and the one-process-per-GPU band gather
 """
-from .device import (DeviceScene, SrtError, convert_scene, read_scene, scene_frame, scene_triangles,  # noqa: F401
-                     write_scene)
+from .device import (MAX_BATCH, DeviceScene, SrtError, convert_scene, read_scene, scene_frame,  # noqa: F401
+                     scene_triangles, write_scene)
 from .runner import Context, Image, MLError, Model, default_offsets, render  # noqa: F401
 
 __all__ = [
     "Context", "Image", "Model", "MLError", "render", "default_offsets",
-    "DeviceScene", "SrtError", "write_scene", "scene_triangles", "scene_frame", "read_scene", "convert_scene",
+    "DeviceScene", "SrtError", "MAX_BATCH", "write_scene", "scene_triangles", "scene_frame", "read_scene", "convert_scene",
 ]

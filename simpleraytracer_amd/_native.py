@@ -28,6 +28,7 @@ SRT_TRACE_LDS = 0
 SRT_TRACE_SCALAR = 1
 SRT_TRACE_CULL = 2
 SRT_TRACE_BVH = 3
+SRT_MAX_BATCH = 8  # include/srt_render.h: frames per srtTraceBatchAsync call
 
 
 class ImageInfo(ctypes.Structure):
@@ -90,6 +91,9 @@ _SIGNATURES = {
                                      ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]),
     "srtTraceIdsAsync": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
                                         ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]),
+    "srtTraceBatchAsync": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p),
+                                          ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_size_t,
+                                          ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]),
     "srtShadeAsync": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                      ctypes.c_size_t, ctypes.c_size_t, ctypes.c_void_p]),
     "srtShadeBandsAsync": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,

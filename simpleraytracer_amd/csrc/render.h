@@ -85,6 +85,7 @@ constexpr int kCullTileCols = 64;
 #define SRT_TILE_ROWS 32
 #endif
 constexpr int kCullTileRows = SRT_TILE_ROWS;
+constexpr int kMaxBatch = 8;          // frames of one batched cull launch (LaunchCullFrames)
 constexpr int kMaxBoundTiles = 2048;  // binning needs tiles_x + tiles_y <= this
 constexpr int kMaxBinTiles = 8192;    // and tiles_x * tiles_y <= this (bin kernel LDS histogram)
 
@@ -163,6 +164,21 @@ struct BvhLayout {
 };
 BvhLayout MakeBvhLayout(std::uint64_t n);
 std::size_t BvhBytes(std::uint64_t n);  // node boxes (16 B) + depth bounds (4 B), 256-B aligned
+
+// One frame of a batched cull launch: its edge-record slot, its bins (one band shape for the
+// whole batch) and its band buffers.
+struct CullFrame {
+    const float* edges;
+    const CullBins* bins;
+    BandArgs band;
+};
+// The cull pipeline for `count` (<= kMaxBatch) frames of one camera in four launches (record
+// setup + tile info when prepare_rank is set, else tile info; bins; work lists; trace), block z
+// of each working on frame z: the same per-frame work as `count` LaunchTrace calls, with a
+// quarter of the launches per frame. Events (optional) bracket the batch.
+hipError_t LaunchCullFrames(const CullFrame* frames, std::size_t count, std::uint64_t n, const float* d_vertices,
+                            const float* d_albedo, const Frame& frame, const float background[3],
+                            const unsigned* prepare_rank, hipStream_t stream, const StageEvents* events);
 
 // Deferred shading of a band from hit ids (band.ids) and sample offsets into band.rgba, with the
 // edge buffer's shading normals of the prepared frame: bit-identical to the fused trace.

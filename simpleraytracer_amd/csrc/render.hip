@@ -93,6 +93,12 @@ struct TraceParams {
     float bg[3];
 };
 
+// Frames of one batched launch (render.h kMaxBatch): block (x, y, z) works on frame z, reading
+// its parameters from the kernel-argument segment (uniform loads).
+struct TraceBatch {
+    TraceParams f[kMaxBatch];
+};
+
 struct PrepareParams {
     const float* __restrict__ vertices;
     const unsigned* __restrict__ rank;  // record id -> position in the spatial order
@@ -1352,8 +1358,12 @@ __device__ __forceinline__ void TileInfoBlock(const BinParams& p, int bx, int by
     }
 }
 
-__global__ __launch_bounds__(kBinThreads) void TileInfoKernel(BinParams p) {
-    TileInfoBlock(p, blockIdx.x, blockIdx.y);
+struct BinBatch {
+    BinParams f[kMaxBatch];
+};
+
+__global__ __launch_bounds__(kBinThreads) void TileInfoKernel(const BinBatch batch) {
+    TileInfoBlock(batch.f[blockIdx.z], blockIdx.x, blockIdx.y);
 }
 
 // Prepare (one thread per record) and tile info (one block per tile) in one launch: block
@@ -1365,8 +1375,12 @@ struct PrepareInfoParams {
     BinParams bin;
     unsigned prep_blocks;
 };
-__global__ __launch_bounds__(kBinThreads) void PrepareInfoKernel(PrepareInfoParams p) {
+struct PrepareInfoBatch {
+    PrepareInfoParams f[kMaxBatch];
+};
+__global__ __launch_bounds__(kBinThreads) void PrepareInfoKernel(const PrepareInfoBatch batch) {
     static_assert(kBinThreads == 256, "prepare blocks are 256 threads");
+    const PrepareInfoParams& p = batch.f[blockIdx.z];
     const unsigned b = blockIdx.x;
     if (b < p.prep_blocks) {
         PrepareRecord(p.prep, b * kBinThreads + threadIdx.x);
@@ -1584,8 +1598,9 @@ std::size_t BinLdsBytes(int nx, int ny) {
     return static_cast<std::size_t>(nx + ny) * sizeof(float2) + static_cast<std::size_t>(hist) * sizeof(unsigned);
 }
 
-__global__ __launch_bounds__(kBinThreads) void BinTrianglesKernel(BinParams p) {
+__global__ __launch_bounds__(kBinThreads) void BinTrianglesKernel(const BinBatch batch) {
     extern __shared__ float2 bin_lds[];
+    const BinParams& p = batch.f[blockIdx.z];
     const int tid = threadIdx.x;
     const int nx = p.tiles_x, ny = p.tiles_y;
     const int tiles = nx * ny;
@@ -1663,17 +1678,18 @@ __global__ __launch_bounds__(kBinThreads) void BinTrianglesKernel(BinParams p) {
 // launch fewer but the ~5 us single-block tail inside the bin launch cost 10 % of the
 // three-queue throughput at C3 (60.9 vs 67.3 Grays/s; plain, no-wait and two-level arrivals
 // alike: profiles/r02/ab_order/).
-__global__ __launch_bounds__(1024) void WorkOrderKernel(BinParams p) {
+__global__ __launch_bounds__(1024) void WorkOrderKernel(const BinBatch batch) {
     __shared__ unsigned start[64];
     __shared__ unsigned cnt[kMaxBinTiles];
-    BuildWorkOrder(p, start, cnt);
+    BuildWorkOrder(batch.f[blockIdx.z], start, cnt);
 }
 
 #ifndef SRT_TRACE_OCC
 #define SRT_TRACE_OCC 5
 #endif
 
-__global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(TraceParams p) {
+__global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(const TraceBatch batch) {
+    const TraceParams& p = batch.f[blockIdx.z];
     constexpr int R = kCullR;
     __shared__ CullShared sh;
 #ifdef SRT_DIAG
@@ -2231,12 +2247,6 @@ __global__ __launch_bounds__(kWave * kBvhWaves) void TraceBvhKernel(BvhTraceArgs
     ShadeAndStore<R>(p, x, y0, s);
 }
 
-// Boolean env switch ("0" = off), for measurement of alternatives.
-bool EnvFlag(const char* name, bool dflt) {
-    const char* v = std::getenv(name);
-    return v == nullptr || *v == '\0' ? dflt : std::strcmp(v, "0") != 0;
-}
-
 // Smallest candidate chunk of a split tile part; env SRT_CULL_CHUNK, a multiple of 64 (default
 // 256: one packet-walk batch).
 unsigned CullChunkFromEnv() {
@@ -2501,23 +2511,9 @@ CullBins CullBinLayout(void* base, std::uint64_t n, std::size_t width, std::size
     return b;
 }
 
-hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_vertices, const float* d_albedo,
-                       const Frame& frame, const float background[3], const BandArgs& band, int variant,
-                       const CullBins* bins, hipStream_t stream, const StageEvents* events,
-                       const unsigned* prepare_rank, void* bvh) {
-    if (band.row_count == 0 || band.width == 0) {
-        return hipSuccess;
-    }
-    const StageEvents ev = events != nullptr ? *events : StageEvents{};
-    const bool fuse_prepare =
-        prepare_rank != nullptr && variant == kTraceCull && bins != nullptr && EnvFlag("SRT_FUSE_PREPARE", true);
-    if (prepare_rank != nullptr && !fuse_prepare) {
-        const hipError_t e = LaunchPrepare(d_vertices, prepare_rank, n, frame, const_cast<float*>(d_edges), stream,
-                                           ev.prep_begin, ev.prep_end);
-        if (e != hipSuccess) {
-            return e;
-        }
-    }
+namespace {
+TraceParams MakeTraceParams(const float* d_edges, std::uint64_t n, const float* d_vertices, const float* d_albedo,
+                            const Frame& frame, const float background[3], const BandArgs& band) {
     TraceParams p{};
     const EdgeLayout e = EdgeBuffers(d_edges, n);
     p.edges = e.tiles;
@@ -2544,7 +2540,130 @@ hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_ver
         p.bg[k] = background[k];
     }
     p.n = static_cast<unsigned>(n);
-    const unsigned gx = static_cast<unsigned>((band.width + kWave - 1) / kWave);
+    p.tiles_x = static_cast<int>((band.width + kWave - 1) / kWave);
+    p.tiles = static_cast<unsigned>(p.tiles_x) * static_cast<unsigned>((band.row_count + kTileRows - 1) / kTileRows);
+#ifdef SRT_DIAG
+    if (const char* x = std::getenv("SRT_EXP")) {
+        p.exp = static_cast<unsigned>(std::strtoul(x, nullptr, 0));
+    }
+#endif
+    return p;
+}
+
+// The bin stage's parameters for trace parameters `p` and its bins; binds the bins to `p`.
+BinParams BindBins(TraceParams& p, const CullBins& bins, std::uint64_t n) {
+    BinParams b{};
+    b.offsets = p.offsets;
+    b.cull = p.cull;
+    b.tile_info = static_cast<TileInfo*>(bins.tile_info);
+    b.counts = bins.counts;
+    b.lists = bins.lists;
+    b.large_list = bins.large_list;
+    b.work = static_cast<uint4*>(bins.work);
+    b.work_count = bins.work_count;
+    b.range_tag = bins.range_tag;
+    b.gen = bins.gen;
+    b.capacity = bins.capacity;
+    b.n = static_cast<unsigned>(n);
+    b.tiles_x = p.tiles_x;
+    b.tiles_y = static_cast<int>(p.tiles / static_cast<unsigned>(p.tiles_x));
+    b.width = p.width;
+    b.row_count = p.row_count;
+    b.row_begin = p.row_begin;
+    b.wf = p.wf;
+    b.hf = p.hf;
+    b.exp = p.exp;
+    p.tile_info = b.tile_info;
+    p.order = bins.order;
+    p.work = b.work;
+    p.work_count = b.work_count;
+    p.max_chunks = bins.max_chunks;
+    p.chunk = CullChunkFromEnv();
+    p.split_keys = static_cast<unsigned long long*>(bins.split_keys);
+    p.arrive = bins.arrive;
+    p.bin_lists = bins.lists;
+    p.bin_counts = bins.counts;
+    p.large_list = bins.large_list;
+    p.bin_capacity = bins.capacity;
+    return b;
+}
+}  // namespace
+
+hipError_t LaunchCullFrames(const CullFrame* frames, std::size_t count, std::uint64_t n, const float* d_vertices,
+                            const float* d_albedo, const Frame& frame, const float background[3],
+                            const unsigned* prepare_rank, hipStream_t stream, const StageEvents* events) {
+    if (frames == nullptr || count == 0 || count > static_cast<std::size_t>(kMaxBatch)) {
+        return hipErrorInvalidValue;
+    }
+    const BandArgs& band0 = frames[0].band;
+    if (band0.row_count == 0 || band0.width == 0) {
+        return hipSuccess;
+    }
+    if (!CullBinnable(band0.width, band0.row_count)) {
+        return hipErrorInvalidValue;
+    }
+    const StageEvents ev = events != nullptr ? *events : StageEvents{};
+    TraceBatch tb{};
+    BinBatch bb{};
+    PrepareInfoBatch pb{};
+    for (std::size_t i = 0; i < count; ++i) {
+        const CullFrame& f = frames[i];
+        if (f.bins == nullptr || f.edges == nullptr || f.band.width != band0.width ||
+            f.band.row_count != band0.row_count || f.band.row_begin != band0.row_begin ||
+            f.band.height != band0.height || f.bins->max_chunks != frames[0].bins->max_chunks) {
+            return hipErrorInvalidValue;  // one band shape per batch
+        }
+        tb.f[i] = MakeTraceParams(f.edges, n, d_vertices, d_albedo, frame, background, f.band);
+        if (f.bins->tiles != tb.f[i].tiles) {
+            return hipErrorInvalidValue;  // bins sized for another band shape
+        }
+        bb.f[i] = BindBins(tb.f[i], *f.bins, n);
+        if (prepare_rank != nullptr) {
+            pb.f[i].prep = MakePrepareParams(d_vertices, prepare_rank, n, frame, const_cast<float*>(f.edges));
+            pb.f[i].bin = bb.f[i];
+            pb.f[i].prep_blocks = (pb.f[i].prep.n_pad + kBinThreads - 1) / kBinThreads;
+        }
+    }
+    const unsigned z = static_cast<unsigned>(count);
+    const unsigned gx = static_cast<unsigned>(tb.f[0].tiles_x), gy = tb.f[0].tiles / gx;
+    // Record setup (when the frame's records are pending) and tile info in one launch; bins (at
+    // least one block); the trace work list; the trace: M blocks per work item.
+    if (prepare_rank != nullptr) {
+        Launch(PrepareInfoKernel, dim3(pb.f[0].prep_blocks + gx * gy, 1, z), dim3(kBinThreads), stream, ev.prep_begin,
+               ev.prep_end, pb);
+    } else {
+        Launch(TileInfoKernel, dim3(gx, gy, z), dim3(kBinThreads), stream, ev.prep_begin, ev.prep_end, bb);
+    }
+    const unsigned blocks = static_cast<unsigned>(n == 0 ? 1 : (n + kBinThreads - 1) / kBinThreads);
+    LaunchLds(BinTrianglesKernel, dim3(blocks, 1, z), dim3(kBinThreads), BinLdsBytes(static_cast<int>(gx), static_cast<int>(gy)),
+              stream, ev.bin_begin, nullptr, bb);
+    Launch(WorkOrderKernel, dim3(1, 1, z), dim3(1024), stream, nullptr, ev.bin_end, bb);
+    Launch(TraceCullKernel, dim3(tb.f[0].tiles * kParts * tb.f[0].max_chunks, 1, z), dim3(kWave * kCullWaves), stream,
+           ev.begin, ev.end, tb);
+    return hipGetLastError();
+}
+
+hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_vertices, const float* d_albedo,
+                       const Frame& frame, const float background[3], const BandArgs& band, int variant,
+                       const CullBins* bins, hipStream_t stream, const StageEvents* events,
+                       const unsigned* prepare_rank, void* bvh) {
+    if (band.row_count == 0 || band.width == 0) {
+        return hipSuccess;
+    }
+    if (variant == kTraceCull && bins != nullptr) {
+        const CullFrame f{d_edges, bins, band};
+        return LaunchCullFrames(&f, 1, n, d_vertices, d_albedo, frame, background, prepare_rank, stream, events);
+    }
+    const StageEvents ev = events != nullptr ? *events : StageEvents{};
+    if (prepare_rank != nullptr) {
+        const hipError_t e = LaunchPrepare(d_vertices, prepare_rank, n, frame, const_cast<float*>(d_edges), stream,
+                                           ev.prep_begin, ev.prep_end);
+        if (e != hipSuccess) {
+            return e;
+        }
+    }
+    const TraceParams p = MakeTraceParams(d_edges, n, d_vertices, d_albedo, frame, background, band);
+    const unsigned gx = static_cast<unsigned>(p.tiles_x);
     if (variant == kTraceBvh) {
         if (bvh == nullptr) {
             return hipErrorInvalidValue;
@@ -2570,82 +2689,16 @@ hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_ver
         constexpr int kRowsPerBlock = kBvhRows * 4;
         const unsigned gy = static_cast<unsigned>((band.row_count + kRowsPerBlock - 1) / kRowsPerBlock);
         Launch(TraceBvhKernel, dim3(gx, gy), dim3(kWave * kBvhWaves), stream, ev.begin, ev.end, a);
-        return hipGetLastError();
-    }
-    if (variant == kTraceScalar) {
+    } else if (variant == kTraceScalar) {
         const unsigned gy = static_cast<unsigned>((band.row_count + kRowsPerLane - 1) / kRowsPerLane);
         Launch(TraceScalarKernel, dim3(gx, gy), dim3(kWave), stream, ev.begin, ev.end, p);
     } else if (variant == kTraceCull) {
-        const unsigned gy = static_cast<unsigned>((band.row_count + kTileRows - 1) / kTileRows);
-        if (bins != nullptr) {
-            if (bins->tiles != static_cast<std::size_t>(gx) * gy || !CullBinnable(band.width, band.row_count)) {
-                return hipErrorInvalidValue;  // bins sized for another band shape
-            }
-            BinParams b{};
-            b.offsets = p.offsets;
-            b.cull = p.cull;
-            b.tile_info = static_cast<TileInfo*>(bins->tile_info);
-            b.counts = bins->counts;
-            b.lists = bins->lists;
-            b.large_list = bins->large_list;
-            b.work = static_cast<uint4*>(bins->work);
-            b.work_count = bins->work_count;
-            b.range_tag = bins->range_tag;
-            b.gen = bins->gen;
-            b.capacity = bins->capacity;
-            b.n = static_cast<unsigned>(n);
-            b.tiles_x = static_cast<int>(gx);
-            b.tiles_y = static_cast<int>(gy);
-            b.width = p.width;
-            b.row_count = p.row_count;
-            b.row_begin = p.row_begin;
-            b.wf = p.wf;
-            b.hf = p.hf;
-#ifdef SRT_DIAG
-            if (const char* e = std::getenv("SRT_EXP")) {
-                b.exp = static_cast<unsigned>(std::strtoul(e, nullptr, 0));
-                p.exp = b.exp;
-            }
-#endif
-            if (fuse_prepare) {
-                PrepareInfoParams f{};
-                f.prep = MakePrepareParams(d_vertices, prepare_rank, n, frame, const_cast<float*>(d_edges));
-                f.bin = b;
-                f.prep_blocks = (f.prep.n_pad + kBinThreads - 1) / kBinThreads;
-                Launch(PrepareInfoKernel, dim3(f.prep_blocks + gx * gy), dim3(kBinThreads), stream, ev.prep_begin,
-                       ev.prep_end, f);
-            } else {
-                Launch(TileInfoKernel, dim3(gx, gy), dim3(kBinThreads), stream, ev.prep_begin, ev.prep_end, b);
-            }
-            // Bins (at least one block), then the trace work list.
-            const unsigned blocks = static_cast<unsigned>(n == 0 ? 1 : (n + kBinThreads - 1) / kBinThreads);
-            LaunchLds(BinTrianglesKernel, dim3(blocks), dim3(kBinThreads), BinLdsBytes(b.tiles_x, b.tiles_y), stream,
-                      ev.bin_begin, nullptr, b);
-            Launch(WorkOrderKernel, dim3(1), dim3(1024), stream, nullptr, ev.bin_end, b);
-            p.tile_info = b.tile_info;
-            p.order = bins->order;
-            p.work = b.work;
-            p.work_count = b.work_count;
-            p.max_chunks = bins->max_chunks;
-            p.chunk = CullChunkFromEnv();
-            p.split_keys = static_cast<unsigned long long*>(bins->split_keys);
-            p.arrive = bins->arrive;
-            p.bin_lists = bins->lists;
-            p.bin_counts = bins->counts;
-            p.large_list = bins->large_list;
-            p.bin_capacity = bins->capacity;
-        }
-        p.tiles_x = static_cast<int>(gx);
-        p.tiles = gx * gy;
-        if (p.work != nullptr) {
-            // Binned: M blocks per work item of the bin kernel's list (BuildWorkOrder).
-            Launch(TraceCullKernel, dim3(static_cast<unsigned>(p.tiles * kParts * p.max_chunks)),
-                   dim3(kWave * kCullWaves), stream, ev.begin, ev.end, p);
-        } else {
-            // One block per (tile, part): gridDim.x = tile columns, gridDim.y = tile rows x parts.
-            Launch(TraceCullKernel, dim3(gx, gy * kParts), dim3(kWave * kCullWaves), stream, ev.begin,
-                   ev.end, p);
-        }
+        // Unbinned: one block per (tile, part), gridDim.x = tile columns, gridDim.y = tile rows x
+        // parts; every block streams every record.
+        TraceBatch tb{};
+        tb.f[0] = p;
+        Launch(TraceCullKernel, dim3(gx, p.tiles / gx * kParts), dim3(kWave * kCullWaves), stream, ev.begin, ev.end,
+               tb);
     } else {
         constexpr int kRowsPerBlock = kRowsPerLane * kLdsWaves;
         const unsigned gy = static_cast<unsigned>((band.row_count + kRowsPerBlock - 1) / kRowsPerBlock);

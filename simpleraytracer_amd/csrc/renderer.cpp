@@ -270,6 +270,96 @@ void DeviceScene::Shade(const float* d_offsets, const int* d_ids, float* d_rgba,
              "shade kernel launch");
 }
 
+// Grow-only cull work for `slots` frame slots of one carve-up (render.h CullBins; counters reset
+// themselves, so a slot is zero-filled only on its first use with this carve-up).
+void DeviceScene::EnsureCullWork(std::size_t slots, std::size_t row_count, hipStream_t stream) const {
+    const std::size_t bytes = CullBinBytes(m_n, m_width, row_count);
+    if (slots * bytes > m_cull_bytes) {
+        HipCheck(hipStreamSynchronize(stream), "hipStreamSynchronize(cull work)");
+        (void)hipFree(m_cull_work);
+        m_cull_work = nullptr;
+        m_cull_bytes = 0;
+        m_cull_work = DeviceAlloc<unsigned char>(slots * bytes, "hipMalloc(cull work)");
+        m_cull_bytes = slots * bytes;
+        m_cull_shape = 0;
+    }
+    // A new carve-up (band shape, or the split width and so the layout): zero every slot again.
+    const std::uint64_t shape = (static_cast<std::uint64_t>(m_width) << 32) | row_count;
+    if (shape != m_cull_shape || bytes != m_cull_layout) {
+        m_cull_shape = shape;
+        m_cull_layout = bytes;
+        m_cull_zeroed = 0;
+    }
+    if (slots > m_cull_zeroed) {
+        HipCheck(hipMemsetAsync(m_cull_work + m_cull_zeroed * bytes, 0, (slots - m_cull_zeroed) * bytes, stream),
+                 "hipMemsetAsync(cull work)");
+        m_cull_zeroed = slots;
+    }
+}
+
+CullBins DeviceScene::CullSlot(std::size_t slot, std::size_t row_count) const {
+    CullBins bins = CullBinLayout(m_cull_work + slot * m_cull_layout, m_n, m_width, row_count);
+    bins.order = m_order;
+    m_cull_gen = m_cull_gen + 1u == 0u ? 1u : m_cull_gen + 1u;
+    bins.gen = m_cull_gen;
+    return bins;
+}
+
+// Edge records for `slots` frame slots (slot 0 is the one Prepare / Trace / Shade use). Growing
+// drops the prepared records, so the next trace recomputes them.
+void DeviceScene::EnsureEdgeSlots(std::size_t slots, hipStream_t stream) const {
+    if (slots <= m_edge_slots) {
+        return;
+    }
+    HipCheck(hipStreamSynchronize(stream), "hipStreamSynchronize(edges)");
+    const std::size_t floats = PaddedTriangleCount(m_n) * kEdgeFloatsPerTriangle;
+    float* grown = DeviceAlloc<float>(slots * floats, "hipMalloc(edges)");
+    (void)hipFree(m_edges);
+    m_edges = grown;
+    m_edge_slots = slots;
+    m_prepare_pending = true;
+}
+
+void DeviceScene::TraceBatch(const float* const* d_offsets, float* const* d_rgba, int* const* d_ids, std::size_t frames,
+                             std::size_t row_begin, std::size_t row_count, int variant, hipStream_t stream) const {
+    if (m_width == 0) {
+        throw std::runtime_error("TraceBatch: Prepare() has not been called");
+    }
+    if (row_begin + row_count > m_height) {
+        throw std::runtime_error("TraceBatch: row band outside the frame");
+    }
+    if (frames > static_cast<std::size_t>(kMaxBatch)) {
+        throw std::runtime_error("TraceBatch: at most " + std::to_string(kMaxBatch) + " frames per batch");
+    }
+    if (frames == 0 || row_count == 0) {
+        return;
+    }
+    if (variant != kTraceCull || !CullBinningEnabled() || !CullBinnable(m_width, row_count)) {
+        for (std::size_t f = 0; f < frames; ++f) {  // frame by frame, each with its own record setup
+            m_prepare_pending = true;
+            Trace(d_offsets[f], d_rgba != nullptr ? d_rgba[f] : nullptr, row_begin, row_count, variant, stream,
+                  d_ids != nullptr ? d_ids[f] : nullptr);
+        }
+        return;
+    }
+    OrderAfterPrevious(stream);
+    EnsureEdgeSlots(frames, stream);
+    EnsureCullWork(frames, row_count, stream);
+    CullBins bins[kMaxBatch];
+    CullFrame cf[kMaxBatch];
+    const std::size_t floats = PaddedTriangleCount(m_n) * kEdgeFloatsPerTriangle;
+    for (std::size_t f = 0; f < frames; ++f) {
+        bins[f] = CullSlot(f, row_count);
+        cf[f].edges = m_edges + f * floats;
+        cf[f].bins = &bins[f];
+        cf[f].band = BandArgs{d_offsets[f], d_rgba != nullptr ? d_rgba[f] : nullptr, m_width, m_height, row_begin,
+                              row_count, d_ids != nullptr ? d_ids[f] : nullptr};
+    }
+    HipCheck(LaunchCullFrames(cf, frames, m_n, m_vertices, m_albedo, m_frame, m_background, m_rank, stream, nullptr),
+             "batched trace launch");
+    m_prepare_pending = false;  // slot 0 holds the prepared frame's records
+}
+
 void DeviceScene::Trace(const float* d_offsets, float* d_rgba, std::size_t row_begin, std::size_t row_count,
                         int variant, hipStream_t stream, int* d_ids) const {
     if (m_width == 0) {
@@ -283,28 +373,8 @@ void DeviceScene::Trace(const float* d_offsets, float* d_rgba, std::size_t row_b
     CullBins bins{};
     const CullBins* use_bins = nullptr;
     if (variant == kTraceCull && row_count != 0 && CullBinningEnabled() && CullBinnable(m_width, row_count)) {
-        // One grow-only, zero-filled allocation (render.h CullBins); its counters reset themselves.
-        const std::size_t bytes = CullBinBytes(m_n, m_width, row_count);
-        if (bytes > m_cull_bytes) {
-            HipCheck(hipStreamSynchronize(stream), "hipStreamSynchronize(cull work)");
-            (void)hipFree(m_cull_work);
-            m_cull_work = nullptr;
-            m_cull_bytes = 0;
-            m_cull_work = DeviceAlloc<unsigned char>(bytes, "hipMalloc(cull work)");
-            m_cull_bytes = bytes;
-            m_cull_shape = 0;
-        }
-        // A new carve-up (band shape, or the split width and so the layout): zero it.
-        const std::uint64_t shape = (static_cast<std::uint64_t>(m_width) << 32) | row_count;
-        if (shape != m_cull_shape || bytes != m_cull_layout) {
-            HipCheck(hipMemsetAsync(m_cull_work, 0, bytes, stream), "hipMemsetAsync(cull work)");
-            m_cull_shape = shape;
-            m_cull_layout = bytes;
-        }
-        bins = CullBinLayout(m_cull_work, m_n, m_width, row_count);
-        bins.order = m_order;
-        m_cull_gen = m_cull_gen + 1u == 0u ? 1u : m_cull_gen + 1u;
-        bins.gen = m_cull_gen;
+        EnsureCullWork(1, row_count, stream);
+        bins = CullSlot(0, row_count);
         use_bins = &bins;
     }
     if (variant == kTraceBvh && m_bvh == nullptr && row_count != 0) {

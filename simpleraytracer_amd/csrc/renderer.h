@@ -17,6 +17,8 @@
 
 namespace srt {
 
+struct CullBins;  // render.h
+
 // Throws std::runtime_error("HIP error: <what>: <reason>") on failure.
 void HipCheck(hipError_t err, const char* what);
 
@@ -50,6 +52,13 @@ public:
     // band_rows-row bands leaves them (render.h LaunchShade), rgba [frames][row_count][width].
     void Shade(const float* d_offsets, const int* d_ids, float* d_rgba, std::size_t row_begin, std::size_t row_count,
                hipStream_t stream, std::size_t frames = 1, std::size_t band_rows = 0) const;
+    // `frames` (<= kMaxBatch) frames of the prepared camera, rows [row_begin, row_begin +
+    // row_count) each: frame f's offsets d_offsets[f], its RGBA d_rgba[f] or (d_ids non-null) its
+    // hit ids d_ids[f]. Each frame gets the whole per-frame pipeline (record setup, bins, work
+    // list, trace), as `frames` Prepare + Trace calls would; the cull variant runs all frames in
+    // one launch per stage (render.h LaunchCullFrames), the others frame by frame.
+    void TraceBatch(const float* const* d_offsets, float* const* d_rgba, int* const* d_ids, std::size_t frames,
+                    std::size_t row_begin, std::size_t row_count, int variant, hipStream_t stream) const;
 
     std::size_t width() const { return m_width; }
     // The spatial order (device, triangles entries) and the time its build took at load (ms).
@@ -76,7 +85,8 @@ private:
     float m_background[3];
     float* m_vertices = nullptr;
     float* m_albedo = nullptr;
-    float* m_edges = nullptr;
+    mutable float* m_edges = nullptr;        // kEdgeFloatsPerTriangle per padded record, per frame slot
+    mutable std::size_t m_edge_slots = 1;    // frame slots of m_edges (TraceBatch grows it; slot 0 = Trace's)
     unsigned* m_order = nullptr;  // record ids in spatial order (BuildSpatialOrder), for the cull bins
     unsigned* m_rank = nullptr;   // its inverse: record id -> position
     double m_build_ms = 0.0;      // spatial order build (BuildSpatialOrder) at load
@@ -90,6 +100,12 @@ private:
     mutable std::uint64_t m_cull_shape = 0;  // (width << 32) | rows of the current carve-up
     mutable std::size_t m_cull_layout = 0;   // its bytes (they change with the split width too)
     mutable unsigned m_cull_gen = 0;         // frames binned (render.h CullBins::gen)
+    mutable std::size_t m_cull_zeroed = 0;   // frame slots of the current carve-up zero-filled
+    // The cull work of frame slots [0, slots) for a row_count-row band (grown, zeroed on first use
+    // of a slot with this carve-up), and slot `slot`'s carve-up with a fresh frame number.
+    void EnsureCullWork(std::size_t slots, std::size_t row_count, hipStream_t stream) const;
+    CullBins CullSlot(std::size_t slot, std::size_t row_count) const;
+    void EnsureEdgeSlots(std::size_t slots, hipStream_t stream) const;
     // BVH variant: node boxes + depth bounds (render.h BvhLayout), allocated by the first bvh Trace.
     mutable unsigned char* m_bvh = nullptr;
     // Stage-timing events, reused: per timed Prepare (begin, end), per timed Trace (bin begin,

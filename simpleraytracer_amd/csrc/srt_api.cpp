@@ -242,6 +242,38 @@ ML_API_ENTRY int srtTraceIdsAsync(srt_device_scene scene, const float* d_offsets
     });
 }
 
+static_assert(SRT_MAX_BATCH == srt::kMaxBatch, "include/srt_render.h SRT_MAX_BATCH");
+
+ML_API_ENTRY int srtTraceBatchAsync(srt_device_scene scene, const float* const* d_offsets, float* const* d_rgba,
+                                    int* const* d_ids, size_t frames, size_t row_begin, size_t row_count, int variant,
+                                    void* stream) {
+    return Guarded([&] {
+        if (scene == nullptr) {
+            throw std::runtime_error("Bad scene handle");
+        }
+        if (frames > SRT_MAX_BATCH) {
+            throw std::runtime_error("At most " + std::to_string(SRT_MAX_BATCH) + " frames per batch");
+        }
+        if (frames != 0 && row_count != 0) {
+            if (d_offsets == nullptr || (d_rgba == nullptr) == (d_ids == nullptr)) {
+                throw std::runtime_error("Bad buffer argument");
+            }
+            for (size_t f = 0; f < frames; ++f) {
+                if (d_offsets[f] == nullptr || (d_rgba != nullptr ? d_rgba[f] == nullptr : d_ids[f] == nullptr)) {
+                    throw std::runtime_error("Bad buffer argument");
+                }
+            }
+        }
+        if (variant != SRT_TRACE_LDS && variant != SRT_TRACE_SCALAR && variant != SRT_TRACE_CULL &&
+            variant != SRT_TRACE_BVH) {
+            throw std::runtime_error("Unknown trace variant " + std::to_string(variant));
+        }
+        srt::DeviceScene* s = FromHandle(scene);
+        Bind bind(s->device());
+        s->TraceBatch(d_offsets, d_rgba, d_ids, frames, row_begin, row_count, variant, static_cast<hipStream_t>(stream));
+    });
+}
+
 ML_API_ENTRY int srtShadeAsync(srt_device_scene scene, const float* d_offsets, const int* d_ids, float* d_rgba,
                                size_t row_begin, size_t row_count, void* stream) {
     return Guarded([&] {

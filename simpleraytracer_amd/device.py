@@ -16,11 +16,12 @@ import ctypes
 import os
 
 from . import _native
-from ._native import (SRT_SCENE_CORNELL, SRT_SCENE_SOUP, SRT_SCENE_TRIANGLE, SRT_TRACE_BVH, SRT_TRACE_CULL,
-                      SRT_TRACE_LDS, SRT_TRACE_SCALAR)
+from ._native import (SRT_MAX_BATCH, SRT_SCENE_CORNELL, SRT_SCENE_SOUP, SRT_SCENE_TRIANGLE, SRT_TRACE_BVH,
+                      SRT_TRACE_CULL, SRT_TRACE_LDS, SRT_TRACE_SCALAR)
 
 SCENE_KINDS = {"triangle": SRT_SCENE_TRIANGLE, "cornell": SRT_SCENE_CORNELL, "soup": SRT_SCENE_SOUP}
 TRACE_VARIANTS = {"lds": SRT_TRACE_LDS, "scalar": SRT_TRACE_SCALAR, "cull": SRT_TRACE_CULL, "bvh": SRT_TRACE_BVH}
+MAX_BATCH = SRT_MAX_BATCH
 SOUP_SEED = 0x5EED  # 100k soup seed; the 1M soup uses SOUP_SEED + 1
 
 
@@ -169,6 +170,40 @@ class DeviceScene:
             _check(lib.srtTraceIdsAsync(h, op, ip, row_begin, row_count, v, s))
 
         return run
+
+    def bind_trace_batch(self, offsets, outs, row_begin: int = 0, row_count: int | None = None, variant: str = "cull",
+                         stream=None, ids: bool = False):
+        """prepare + trace of len(outs) (<= MAX_BATCH) frames of this band as a zero-argument
+        callable (srtTraceBatchAsync): frame f's sample offsets offsets[f] ((rows, W, 2) float32)
+        and its output outs[f] ((rows, W) int32 hit ids with ids=True, else (rows, W, 4) float32
+        RGBA). Every frame gets the whole per-frame work; the cull variant launches each stage
+        once for the batch. Checked once here; the buffers must stay alive while it is used."""
+        if row_count is None:
+            row_count = self.height - row_begin
+        frames = len(outs)
+        if frames > MAX_BATCH or len(offsets) != frames:
+            raise ValueError(f"1 to {MAX_BATCH} frames, one offsets buffer per output")
+        for f in range(frames):
+            self._check_buffer(f"offsets[{f}]", offsets[f], row_count, 2, "f32")
+            self._check_buffer(f"outs[{f}]", outs[f], row_count, 0 if ids else 4, "i32" if ids else "f32")
+        arr = ctypes.c_void_p * max(1, frames)
+        offs = arr(*[_ptr(o) for o in offsets])
+        out = arr(*[_ptr(o) for o in outs])
+        rgba, idp = (None, out) if ids else (out, None)
+        lib, h, w, hh = self._lib, self.handle, self.width, self.height
+        s, v = _stream(stream), TRACE_VARIANTS[variant]
+
+        def run():
+            _check(lib.srtPrepareAsync(h, w, hh, s))
+            _check(lib.srtTraceBatchAsync(h, offs, rgba, idp, frames, row_begin, row_count, v, s))
+
+        run.keep = (offsets, outs, offs, out)  # the pointer arrays live as long as the callable
+        return run
+
+    def trace_batch(self, offsets, outs, row_begin: int = 0, row_count: int | None = None, variant: str = "cull",
+                    stream=None, ids: bool = False):
+        """One batched call (bind_trace_batch) run once."""
+        self.bind_trace_batch(offsets, outs, row_begin, row_count, variant, stream, ids)()
 
     def shade(self, offsets, ids, rgba, row_begin: int = 0, row_count: int | None = None, stream=None):
         """Deferred shading of the prepared frame's rows from hit ids: the RGBA trace() stores."""

@@ -51,7 +51,7 @@ def header_symbols():
 
 def test_every_header_symbol_is_exported(L):
     syms = header_symbols()
-    assert len(syms) == 14 + 18  # the reference ABI + the srt* extension (include/srt_render.h)
+    assert len(syms) == 14 + 19  # the reference ABI + the srt* extension (include/srt_render.h)
     out = subprocess.run(["nm", "-D", "--defined-only", str(_native.LIB_PATH)], capture_output=True, text=True,
                          check=True).stdout
     exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
@@ -60,6 +60,15 @@ def test_every_header_symbol_is_exported(L):
         assert getattr(L, s) is not None
     # nothing else leaks out of the hidden-visibility build
     assert {s for s in exported if s.startswith(("ml", "srt"))} == set(syms)
+
+
+def test_batch_limit_matches_header():
+    import re
+
+    import simpleraytracer_amd as srt
+
+    hdr = (REPO / "include" / "srt_render.h").read_text()
+    assert int(re.search(r"#define SRT_MAX_BATCH (\d+)", hdr).group(1)) == srt.MAX_BATCH == 8
 
 
 def test_reference_entry_points_are_the_ml_family():

@@ -683,6 +683,74 @@ def test_batched_band_shading_bitwise(gpu, scenes, bands):
     scene.close()
 
 
+@pytest.mark.parametrize("variant", ["cull", "lds"])
+def test_trace_batch_bitwise(gpu, scenes, variant):
+    """srtTraceBatchAsync: F frames (each with its own random offsets) in one call, RGBA for the
+    whole frame and hit ids for a band, equal the frames traced one at a time bit for bit (cull:
+    one launch per stage for the batch; other variants: frame by frame). Afterwards the scene's
+    single-frame calls (trace, shade from slot 0's records) are still exact."""
+    import torch
+
+    import simpleraytracer_amd as srt
+
+    w, h, frames = 333, 170, 3
+    rng = np.random.default_rng(47)
+    offs = [rng.random((h, w, 2), dtype=np.float32) for _ in range(frames)]
+    refs = [torch_render(scenes["soup2k"], w, h, o, variant="lds") for o in offs]
+    scene = srt.DeviceScene(scenes["soup2k"], 0)
+    stream = torch.cuda.current_stream()
+    scene.prepare(w, h, stream)
+    off = [torch.from_numpy(o).cuda() for o in offs]
+    rgba = [torch.full((h, w, 4), float("nan"), dtype=torch.float32, device="cuda") for _ in range(frames)]
+    scene.trace_batch(off, rgba, 0, h, variant=variant, stream=stream)
+    r0, rows = 40, 77
+    band_off = [o[r0:r0 + rows].contiguous() for o in off] * 3  # 9 > MAX_BATCH: checked below
+    ids = [torch.full((rows, w), -7, dtype=torch.int32, device="cuda") for _ in range(srt.MAX_BATCH)]
+    scene.trace_batch(band_off[:srt.MAX_BATCH], ids, r0, rows, variant=variant, stream=stream, ids=True)
+    torch.cuda.synchronize()
+    for f in range(frames):
+        assert np.array_equal(rgba[f].cpu().numpy().view(np.uint32), refs[f].view(np.uint32)), f
+    for f in range(srt.MAX_BATCH):
+        want = refs[f % frames][r0:r0 + rows, :, 3]
+        assert np.array_equal(ids[f].cpu().numpy().astype(np.float32), want), f
+    # single-frame calls after a batch: a band trace and the deferred shading of ids
+    one = torch.empty((rows, w, 4), dtype=torch.float32, device="cuda")
+    scene.prepare(w, h, stream)
+    scene.trace(band_off[1], one, r0, rows, variant=variant, stream=stream)
+    shaded = torch.empty((rows, w, 4), dtype=torch.float32, device="cuda")
+    scene.shade(band_off[1], ids[1], shaded, r0, rows, stream=stream)
+    torch.cuda.synchronize()
+    assert np.array_equal(one.cpu().numpy().view(np.uint32), refs[1][r0:r0 + rows].view(np.uint32))
+    assert np.array_equal(shaded.cpu().numpy().view(np.uint32), refs[1][r0:r0 + rows].view(np.uint32))
+    with pytest.raises(ValueError):
+        scene.trace_batch(band_off, ids + ids[:1], r0, rows, stream=stream, ids=True)
+    scene.close()
+
+
+def test_trace_batch_c3_band_of_8(gpu, scenes):
+    """The bench's N = 8 band (135 rows of 1080p, C3) batched 8 frames at a time: every frame's
+    ids equal a single srtTraceIdsAsync of the band, bit for bit."""
+    import torch
+
+    import simpleraytracer_amd as srt
+
+    w, h, r0, rows = 1920, 1080, 405, 135
+    scene = srt.DeviceScene(scenes["soup100k"], 0)
+    stream = torch.cuda.current_stream()
+    scene.prepare(w, h, stream)
+    off = torch.full((rows, w, 2), 0.5, dtype=torch.float32, device="cuda")
+    ref = torch.empty((rows, w), dtype=torch.int32, device="cuda")
+    scene.trace_ids(off, ref, r0, rows, stream=stream)
+    ids = [torch.full((rows, w), -7, dtype=torch.int32, device="cuda") for _ in range(srt.MAX_BATCH)]
+    run = scene.bind_trace_batch([off] * srt.MAX_BATCH, ids, r0, rows, stream=stream, ids=True)
+    for _ in range(3):
+        run()
+    torch.cuda.synchronize()
+    for f in range(srt.MAX_BATCH):
+        assert torch.equal(ids[f], ref), f
+    scene.close()
+
+
 def test_scene_calls_on_two_streams_are_ordered(gpu, scenes):
     """One scene used from two streams (bands on alternating streams, a new prepare in between):
     the library orders the calls, so every frame equals its single-stream render."""

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-rank work of the multi-GPU band pipeline, measured on one GPU (no interconnect).
 
-    python tools/band_sim.py [--ranks 2,4,8] [--queues 3] [--steps 2000]
+    python tools/band_sim.py [--ranks 2,4,8] [--queues 3] [--steps 2000] [--batch 8]
 
 For P ranks, rank r's per-frame work in bench.py --mode bands is: the edge-record setup and
 bins for the whole frame's records, the trace of band r (hit ids), and -- on every P-th frame,
@@ -33,47 +33,68 @@ def main():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--triangles", type=int, default=100_000)
+    ap.add_argument("--batch", type=int, default=8, help="frames per launch / per gather (bench.py --batch)")
     a = ap.parse_args()
     import torch
 
     import simpleraytracer_amd as srt
     from simpleraytracer_amd.bands import band_range, band_rows
 
-    W, H = a.width, a.height
+    W, H, G = a.width, a.height, max(1, min(a.batch, srt.MAX_BATCH))
     dev = torch.device("cuda", 0)
     tmp = tempfile.TemporaryDirectory()
     path = srt.write_scene(os.path.join(tmp.name, "soup.srt"), "soup", a.triangles)
     off = torch.full((H, W, 2), 0.5, dtype=torch.float32, device=dev)
+    # the frame's real ids, for realistic compositor shading work
+    ref_scene = srt.DeviceScene(path, 0)
+    ref_scene.prepare(W, H)
+    frame_ids = torch.empty((H, W), dtype=torch.int32, device=dev)
+    ref_scene.trace_ids(off, frame_ids, 0, H)
+    torch.cuda.synchronize()
+    ref_scene.close()
     qs = [{"scene": srt.DeviceScene(path, 0), "stream": torch.cuda.Stream(dev),
-           "ids": torch.full((H, W), -1, dtype=torch.int32, device=dev),
-           "rgba": torch.empty((H, W, 4), dtype=torch.float32, device=dev)} for _ in range(a.queues)]
-    out = {"workload": f"soup-{a.triangles} {W}x{H}", "queues": a.queues, "ranks": {}}
+           "ids": torch.full((G, H, W), -1, dtype=torch.int32, device=dev),
+           "rgba": torch.empty((G, H, W, 4), dtype=torch.float32, device=dev)} for _ in range(a.queues)]
+    for q in qs:
+        q["scene"].prepare(W, H)
+    out = {"workload": f"soup-{a.triangles} {W}x{H}", "queues": a.queues, "batch": G, "ranks": {}}
     for P in [int(x) for x in a.ranks.split(",")]:
         per = []
+        B = band_rows(H, P)
+        gathered = torch.full((P, G, B, W), -1, dtype=torch.int32, device=dev)  # band-major, as gathered
+        for p in range(P):
+            b0, c = band_range(H, P, p)
+            gathered[p, :, :c] = frame_ids[b0:b0 + c]
         for r in range(P):
             r0, rows = band_range(H, P, r)
-
-            def step(k):
-                q = qs[k % a.queues]
-                q["scene"].prepare(W, H, q["stream"])
+            for q in qs:
                 if P == 1:
-                    q["scene"].trace(off, q["rgba"], 0, H, stream=q["stream"])
-                    return
-                if rows:
-                    q["scene"].trace_ids(off[r0:r0 + rows], q["ids"][:rows], r0, rows, stream=q["stream"])
-                if k % P == r:  # this rank composites frame k
-                    q["scene"].shade(off, q["ids"], q["rgba"], 0, H, stream=q["stream"])
+                    q["run"] = q["scene"].bind_trace_batch([off] * G, [q["rgba"][j] for j in range(G)], 0, H,
+                                                           stream=q["stream"])
+                else:
+                    q["run"] = q["scene"].bind_trace_batch([off[r0:r0 + rows]] * G,
+                                                           [q["ids"][j, :rows] for j in range(G)], r0, rows,
+                                                           stream=q["stream"], ids=True) if rows else None
 
-            for k in range(a.warmup * a.queues):
+            def step(k):  # batch k: G frames
+                q = qs[k % a.queues]
+                if q["run"] is not None:
+                    q["run"]()
+                if P > 1 and k % P == r:  # this rank composites batch k
+                    q["scene"].shade_bands(off, gathered, q["rgba"], B, stream=q["stream"])
+
+            batches = max(1, a.steps // G)
+            for k in range(max(2, a.warmup // G) * a.queues):
                 step(k)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            for k in range(a.steps):
+            for k in range(batches):
                 step(k)
             torch.cuda.synchronize()
             dt = time.perf_counter() - t0
-            per.append({"rank": r, "rows": rows, "us_per_frame": round(dt / a.steps * 1e6, 2),
-                        "frame_mrays_per_s": round(W * H * a.steps / dt / 1e6, 1)})
+            frames = batches * G
+            per.append({"rank": r, "rows": rows, "us_per_frame": round(dt / frames * 1e6, 2),
+                        "frame_mrays_per_s": round(W * H * frames / dt / 1e6, 1)})
         worst = min(p["frame_mrays_per_s"] for p in per)
         out["ranks"][P] = {"per_rank": per, "ceiling_mrays_per_s": worst, "band_rows": band_rows(H, P)}
         print(json.dumps({"P": P, "ceiling_mrays_per_s": worst, "per_rank": per}), flush=True)
