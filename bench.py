@@ -552,9 +552,9 @@ def main():
                           "trace_kernel": round(rt["trace_ms"], 5), "frame": round(r["ms_per_step"], 5),
                           "frame_instrumented": round(rt["ms_per_step"], 5), "timed_launches": rt["launches"],
                           "note": "one frame in flight, HIP events bound to the kernels' dispatches: prepare = "
-                                  "PrepareInfoKernel, bin = TileBounds + BinTriangles + TileOrder (work list), "
-                                  "trace_kernel = TraceCullKernel (rank 0's band at N > 1); frame = uninstrumented "
-                                  "time per frame with config.frame_queues in flight"},
+                                  "PrepareInfoKernel (record setup + tile info), bin = BinTrianglesKernel + "
+                                  "WorkOrderKernel, trace_kernel = TraceCullKernel (rank 0's band at N > 1); frame = "
+                                  "uninstrumented time per frame with config.frame_queues in flight"},
         }
         line["scene_build"] = {"spatial_order_ms": round(order_build_ms, 4),
                                "note": "once per scene at load, on the device (Morton codes + rocPRIM radix sort, "

@@ -72,7 +72,7 @@ public:
     struct StageTimes {
         unsigned launches = 0;     // timed Trace calls
         double prepare_ms = 0.0;   // PrepareKernel (mean over timed Prepare calls)
-        double bin_ms = 0.0;       // bin stage (cull: TileInfo start .. TileOrder end); 0 otherwise
+        double bin_ms = 0.0;       // bin stage (cull: BinTriangles start .. WorkOrder end); 0 otherwise
         double kernel_ms = 0.0;    // the trace kernel alone
     };
     void SetTiming(bool on);

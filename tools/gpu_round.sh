@@ -1,11 +1,12 @@
 #!/bin/bash
 # Full GPU-box session for a round's evidence: parity tests, smoke, the default bench line
-# (with cpu_baseline + e2e), rocprofv3 kernel stats of the bench (frame queues and one queue),
-# and the PMC passes of the trace kernel (FETCH_SIZE, WRITE_SIZE and 8 SQ counters, each a
-# run of its own). Every GPU step has its own time limit; a crash-type exit ends the script
+# (with cpu_baseline + e2e), 2- and 4-rank gloo rehearsals of the N > 1 band path and the band
+# simulation, rocprofv3 kernel stats of the bench (frame queues and one queue), the PMC passes
+# of the trace kernel (FETCH_SIZE, WRITE_SIZE and 8 SQ counters, each a run of its own) and the
+# host-cost probe of the band step (one-rank RCCL). Every GPU step has its own time limit; a crash-type exit ends the script
 # (tests/lib.sh run). Output under gpurun_out/; copy what is judged into profiles/.
 source "$(dirname "$0")/gpu_lib.sh"
-STEPS=${STEPS:-tests,smoke,bench,prof,pmc}
+STEPS=${STEPS:-tests,smoke,bench,rehearse,prof,pmc,host}
 KERNEL_RE=${KERNEL_RE:-TraceCullKernel}
 KEY=${KEY:-"soup-100k 1920x1080 1spp|cull"}
 Q=(--steps 50 --warmup 5 --queues 1 --no-extras --no-cpu-baseline)
@@ -26,6 +27,11 @@ if [[ $STEPS == *rehearse* ]]; then
             --warmup 2 --no-extras
     done
     run band_sim 300 python tools/band_sim.py
+    run band_sim_b1 300 python tools/band_sim.py --batch 1
+fi
+if [[ $STEPS == *host* ]]; then
+    run host_bands 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
+        --master-port 29541 tools/host_probe_bands.py
 fi
 if [[ $STEPS == *prof* ]]; then
     run prof_stats 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
