@@ -172,13 +172,14 @@ struct CullFrame {
     const CullBins* bins;
     BandArgs band;
 };
-// The cull pipeline for `count` (<= kMaxBatch) frames of one camera in four launches (record
-// setup + tile info when prepare_rank is set, else tile info; bins; work lists; trace), block z
-// of each working on frame z: the same per-frame work as `count` LaunchTrace calls, with a
-// quarter of the launches per frame. Events (optional) bracket the batch.
+// The cull pipeline for `count` (<= kMaxBatch) frames of one camera in four launches (tile info;
+// record setup + bins; work lists; trace), block z of each working on frame z: the same per-frame
+// work as `count` single-frame calls, with a quarter of the launches per frame. The records are
+// computed in the bin launch every call (bins->order: position -> id; d_rank unused). Events
+// (optional): prep = tile info, bin = record setup + bins + work list, trace.
 hipError_t LaunchCullFrames(const CullFrame* frames, std::size_t count, std::uint64_t n, const float* d_vertices,
-                            const float* d_albedo, const Frame& frame, const float background[3],
-                            const unsigned* prepare_rank, hipStream_t stream, const StageEvents* events);
+                            const float* d_albedo, const Frame& frame, const float background[3], const unsigned* d_rank,
+                            hipStream_t stream, const StageEvents* events);
 
 // Deferred shading of a band from hit ids (band.ids) and sample offsets into band.rgba, with the
 // edge buffer's shading normals of the prepared frame: bit-identical to the fused trace.

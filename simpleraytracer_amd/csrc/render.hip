@@ -80,7 +80,7 @@ struct TraceParams {
     unsigned* __restrict__ arrive;            // per (tile, part): chunks finished (self-resetting)
     unsigned max_chunks;                      // M: a part's candidates split into at most M chunks
     unsigned chunk;                           // ... of at least this many candidates each
-    const unsigned* __restrict__ bin_lists;   // per tile: candidate ids (BinTrianglesKernel)
+    const unsigned* __restrict__ bin_lists;   // per tile: candidate positions (PrepareBinKernel)
     const unsigned* __restrict__ bin_counts;  // per tile: list length; [tiles]: large-list length
     const unsigned* __restrict__ large_list;  // ids of records binned to every tile
     unsigned bin_capacity;
@@ -102,6 +102,7 @@ struct TraceBatch {
 struct PrepareParams {
     const float* __restrict__ vertices;
     const unsigned* __restrict__ rank;  // record id -> position in the spatial order
+    const unsigned* __restrict__ order; // position -> record id (the fused bin pass)
     float4* __restrict__ edges;
     float4* __restrict__ screen_boxes;
     uint2* __restrict__ qboxes;
@@ -212,23 +213,18 @@ __device__ __forceinline__ unsigned PackI16(int low, int high) {
     return (static_cast<unsigned>(low) & 0xFFFFu) | (static_cast<unsigned>(high) << 16);
 }
 
-// One thread per triangle: origin-relative edge normals nA = B x C, nB = C x A, nC = A x B
-// (A, B, C = vertices - eye), signed volume vol = A . nA, orientation normalised so vol > 0,
-// then each normal projected onto the affine ray frame: E(fx, fy) = n . (base + fx du + fy dv).
-__device__ __forceinline__ void PrepareRecord(const PrepareParams& p, unsigned i) {
-    if (i >= p.n_pad) {
-        return;
-    }
-    float4* tile = p.edges + static_cast<size_t>(i / kTileTriangles) * kTileFloat4;
-    const unsigned j = i % kTileTriangles;
-    float* p2 = reinterpret_cast<float*>(tile + 2 * kTileTriangles);
-    float* p3 = p2 + kTileTriangles;
+// Record of triangle `id` (real = a scene triangle, else padding): origin-relative edge normals
+// nA = B x C, nB = C x A, nC = A x B (A, B, C = vertices - eye), signed volume vol = A . nA,
+// orientation normalised so vol > 0, then each normal projected onto the affine ray frame:
+// E(fx, fy) = n . (base + fx du + fy dv): c = (c0A, cxA, cyA, c0B, cxB, cyB, c0C, cxC, cyC).
+// Disabled (padding, degenerate, plane through the eye): NaN record, empty screen box.
+__device__ __forceinline__ void ComputeRecord(const PrepareParams& p, unsigned id, bool real, float c[9], float& vol,
+                                              float4& sb) {
     const float qnan = __builtin_nanf("");
-    bool disabled = i >= p.n;
-    float c[9];
-    float vol = qnan;
+    bool disabled = !real;
+    vol = qnan;
     if (!disabled) {
-        const float* v = p.vertices + 9ull * i;
+        const float* v = p.vertices + 9ull * id;
         const float ax = v[0] - p.origin[0], ay = v[1] - p.origin[1], az = v[2] - p.origin[2];
         const float bx = v[3] - p.origin[0], by = v[4] - p.origin[1], bz = v[5] - p.origin[2];
         const float cx = v[6] - p.origin[0], cy = v[7] - p.origin[1], cz = v[8] - p.origin[2];
@@ -262,13 +258,9 @@ __device__ __forceinline__ void PrepareRecord(const PrepareParams& p, unsigned i
         }
         vol = qnan;
     }
-    tile[j] = make_float4(c[0], c[1], c[2], c[3]);
-    tile[kTileTriangles + j] = make_float4(c[4], c[5], c[6], c[7]);
-    p2[j] = c[8];
-    p3[j] = vol;
     // Disabled records: an empty box (culled by every ray box the screen boxes apply to).
-    float4 sb = disabled ? make_float4(__builtin_inff(), -__builtin_inff(), __builtin_inff(), -__builtin_inff())
-                         : make_float4(0.f, 0.f, 0.f, 0.f);
+    sb = disabled ? make_float4(__builtin_inff(), -__builtin_inff(), __builtin_inff(), -__builtin_inff())
+                  : make_float4(0.f, 0.f, 0.f, 0.f);
 #ifdef SRT_DIAG
     if ((p.exp & 512u) == 0u && !disabled) {  // timing experiment: 512 skips the screen box
         sb = ScreenBox(c);
@@ -278,29 +270,54 @@ __device__ __forceinline__ void PrepareRecord(const PrepareParams& p, unsigned i
         sb = ScreenBox(c);
     }
 #endif
+}
+
+// Stored as (hi, -lo) pairs so the cull test is one saturating packed add per axis.
+__device__ __forceinline__ uint2 QuantizeBox(const float4& sb) {
+    return make_uint2(PackI16(QuantHi(sb.y), -QuantLo(sb.x)), PackI16(QuantHi(sb.w), -QuantLo(sb.z)));
+}
+
+// Shading normal: the exact expressions the shading epilogue used to evaluate per hit.
+__device__ __forceinline__ float4 ShadingNormal(const float* __restrict__ vertices, unsigned id) {
+    const float* v = vertices + 9ull * id;
+    const float e1x = v[3] - v[0], e1y = v[4] - v[1], e1z = v[5] - v[2];
+    const float e2x = v[6] - v[0], e2y = v[7] - v[1], e2z = v[8] - v[2];
+    float nx, ny, nz;
+    Cross3(e1x, e1y, e1z, e2x, e2y, e2z, nx, ny, nz);
+    return make_float4(nx, ny, nz, sqrtf(Dot3(nx, ny, nz, nx, ny, nz)));
+}
+
+// The full record pass (every variant but the binned cull path, which fuses it into its bin
+// kernel): one thread per record id i, writing the tile-planar edge record, the screen box, and
+// at the record's spatial position (rank[i]; padding ids are their own position) its quantized
+// box and cull record; the shading normal by id.
+__device__ __forceinline__ void PrepareRecord(const PrepareParams& p, unsigned i) {
+    if (i >= p.n_pad) {
+        return;
+    }
+    float4* tile = p.edges + static_cast<size_t>(i / kTileTriangles) * kTileFloat4;
+    const unsigned j = i % kTileTriangles;
+    float* p2 = reinterpret_cast<float*>(tile + 2 * kTileTriangles);
+    float* p3 = p2 + kTileTriangles;
+    const bool real = i < p.n;
+    float c[9], vol;
+    float4 sb;
+    ComputeRecord(p, i, real, c, vol, sb);
+    tile[j] = make_float4(c[0], c[1], c[2], c[3]);
+    tile[kTileTriangles + j] = make_float4(c[4], c[5], c[6], c[7]);
+    p2[j] = c[8];
+    p3[j] = vol;
     p.screen_boxes[i] = sb;
-    // Stored as (hi, -lo) pairs so the cull test is one saturating packed add per axis.
-    p.qboxes[i] = make_uint2(PackI16(QuantHi(sb.y), -QuantLo(sb.x)), PackI16(QuantHi(sb.w), -QuantLo(sb.z)));
-    if (i < p.n) {
-        // Shading normal, the exact expressions ShadeAndStore used to evaluate per hit.
-        const float* v = p.vertices + 9ull * i;
-        const float e1x = v[3] - v[0], e1y = v[4] - v[1], e1z = v[5] - v[2];
-        const float e2x = v[6] - v[0], e2y = v[7] - v[1], e2z = v[8] - v[2];
-        float nx, ny, nz;
-        Cross3(e1x, e1y, e1z, e2x, e2y, e2z, nx, ny, nz);
-        p.normals[i] = make_float4(nx, ny, nz, sqrtf(Dot3(nx, ny, nz, nx, ny, nz)));
-        CullRecord r;
-        r.a = make_float4(c[0], c[1], c[2], c[3]);
-        r.b = make_float4(c[4], c[5], c[6], c[7]);
-        r.x = make_float4(c[8], vol, __uint_as_float(i), 0.f);
-        r.sb = sb;
-#ifdef SRT_DIAG
-        if (p.exp & 1024u) {  // timing experiment: coalesced record writes (wrong order)
-            p.cull[i] = r;
-            return;
-        }
-#endif
-        p.cull[p.rank[i]] = r;
+    const unsigned pos = real ? p.rank[i] : i;
+    p.qboxes[pos] = QuantizeBox(sb);
+    CullRecord r;
+    r.a = make_float4(c[0], c[1], c[2], c[3]);
+    r.b = make_float4(c[4], c[5], c[6], c[7]);
+    r.x = make_float4(c[8], vol, __uint_as_float(i), 0.f);
+    r.sb = sb;
+    p.cull[pos] = r;
+    if (real) {
+        p.normals[i] = ShadingNormal(p.vertices, i);
     }
 }
 
@@ -807,18 +824,6 @@ struct CullSource {
     bool full;
 };
 
-// Cull record of record `id` from the tile-planar edge buffer and the screen boxes (FULL).
-__device__ __forceinline__ CullRecord LoadCullById(const TraceParams& p, unsigned id) {
-    const float4* tile = p.edges + static_cast<size_t>(id / kTileTriangles) * kTileFloat4;
-    const unsigned j = id % kTileTriangles;
-    CullRecord r;
-    r.a = tile[j];
-    r.b = tile[kTileTriangles + j];
-    r.x = make_float4(Plane2(tile)[j], Plane3(tile)[j], __uint_as_float(id), 0.f);
-    r.sb = p.screen_boxes[id];
-    return r;
-}
-
 // ---------------------------------------------------------------------------------------
 // Packet walk. The block's 64 x 16 ray positions sit in an LDS table; per column the
 // smallest and largest fx over the block's rows, per row the smallest and largest fy over
@@ -1202,20 +1207,14 @@ __device__ __forceinline__ void PacketBatch(CullShared& sh, const Box& bb, const
 
 // ---------------------------------------------------------------------------------------
 // Cull bins: the first cull level, built per band before the trace, in three launches (the
-// record setup rides in the first). A tile is 64 x 32 rays.
-//   TileInfoKernel:     one block per tile reads the tile's sample offsets once: the ray
-//   (PrepareInfoKernel) box, "regular" (every offset equal to the first, bit for bit) and the
-//                       first offset; it clears the tile's bin count and tags the frame if an
-//                       offset lies outside [0, 1].
-//   BinTrianglesKernel: per tile column and row, monotone bounds of the tile boxes (analytic
-//                       for offsets in [0, 1], else reduced from the tile boxes: BinTileBounds).
-//                       Then one thread per record: binary searches in the bounds give the
-//                       contiguous range of tile columns and rows whose boxes can overlap the
-//                       record's screen box; every tile of the range whose own box passes the
-//                       screen-box overlap and the edge-function corner test (BoxMayHit) gets
-//                       the id appended to its list. A record whose range spans more than
-//                       kLargeTiles tiles (big, or an unbounded screen box) goes to the large
-//                       list, which every binned tile walks after its own list.
+// frame's record setup rides in the second). A tile is 64 x 32 rays.
+//   TileInfoKernel:     one block per tile reads the tile's sample offsets once: the ray box,
+//                       "regular" (every offset equal to the first, bit for bit) and the first
+//                       offset; it clears the tile's bin count and tags the frame if an offset
+//                       lies outside [0, 1].
+//   PrepareBinKernel:   per tile column and row, monotone bounds of the tile boxes (analytic for
+//                       offsets in [0, 1], else reduced from the tile boxes: BinTileBounds); one
+//                       thread per record (spatial order) computes the record and bins it.
 //   WorkOrderKernel:    one block lists the trace work (BuildWorkOrder).
 // Both steps drop only (record, tile) pairs that provably fail the exact test for every ray
 // of the tile, so the frame stays bit-identical to brute force. A tile whose box is outside
@@ -1366,31 +1365,6 @@ __global__ __launch_bounds__(kBinThreads) void TileInfoKernel(const BinBatch bat
     TileInfoBlock(batch.f[blockIdx.z], blockIdx.x, blockIdx.y);
 }
 
-// Prepare (one thread per record) and tile info (one block per tile) in one launch: block
-// b < prep_blocks prepares records, the others are tile blocks. The two are independent
-// (records vs sample offsets), so the latency-bound prepare blocks overlap the
-// bandwidth-bound tile blocks.
-struct PrepareInfoParams {
-    PrepareParams prep;
-    BinParams bin;
-    unsigned prep_blocks;
-};
-struct PrepareInfoBatch {
-    PrepareInfoParams f[kMaxBatch];
-};
-__global__ __launch_bounds__(kBinThreads) void PrepareInfoKernel(const PrepareInfoBatch batch) {
-    static_assert(kBinThreads == 256, "prepare blocks are 256 threads");
-    const PrepareInfoParams& p = batch.f[blockIdx.z];
-    const unsigned b = blockIdx.x;
-    if (b < p.prep_blocks) {
-        PrepareRecord(p.prep, b * kBinThreads + threadIdx.x);
-        return;
-    }
-    const unsigned t = b - p.prep_blocks;
-    TileInfoBlock(p.bin, static_cast<int>(t % static_cast<unsigned>(p.bin.tiles_x)),
-                  static_cast<int>(t / static_cast<unsigned>(p.bin.tiles_x)));
-}
-
 // First index i of the nondecreasing hi'[0..n) with hi'[i] >= v (n if none).
 __device__ __forceinline__ int FirstHiAtLeast(const float2* b, int n, float v) {
     int lo = 0, hi = n;
@@ -1418,11 +1392,6 @@ __device__ __forceinline__ int LastLoAtMost(const float2* b, int n, float v) {
     return lo - 1;
 }
 
-// One thread per record, records taken in the scene's spatial order (p.order: sorted by the
-// screen position of their centroid at scene load), so a block's records fall in few tiles:
-// the block counts its (tile, record) pairs in an LDS histogram, reserves each touched
-// tile's share of its list with ONE global atomic, then writes the ids. (Per-pair global
-// atomics serialise on the busy tiles' counters at the memory side.)
 // Trace work list (WorkOrderKernel, after the bin kernel). One 32-B descriptor per
 // tile part, listed longest first (counting sort by the log2 of the tile's candidates, FULL-stream
 // tiles first), so the heavy parts start first and the light ones fill in behind them; order
@@ -1598,52 +1567,98 @@ std::size_t BinLdsBytes(int nx, int ny) {
     return static_cast<std::size_t>(nx + ny) * sizeof(float2) + static_cast<std::size_t>(hist) * sizeof(unsigned);
 }
 
-__global__ __launch_bounds__(kBinThreads) void BinTrianglesKernel(const BinBatch batch) {
+// Records and bins of a frame in one launch (the binned cull path). Block b owns spatial
+// positions [256 b, 256 b + 256) (the scene's Morton order, so a block's records fall in few
+// tiles). Each thread computes the record of its position (triangle order[i]) in registers and
+// writes, by position, its quantized box (the FULL stream's input) and its 64-B cull record (the
+// trace's only record reads), and its shading normal by id. The cull record is skipped when no
+// trace of this band can read it: with every offset of the frame in [0, 1] (no tile block tagged
+// it), every ray of the band lies in its analytic row bounds [lo' of the first tile row, hi' of
+// the last]; a record whose quantized screen box misses those rows is never listed (its row
+// range is empty) and never passes a FULL block's box test (a block box lies inside the rows and
+// quantisation is monotone). Padding and tagged frames write every record. The block then bins
+// the records it holds: binary searches in the bounds give each record the range of tiles its
+// screen box can overlap, every tile of the range passing ScreenBoxOverlaps + BoxMayHit against
+// its own box gets the position appended (records spanning more than kLargeTiles tiles go to the
+// large list); an LDS histogram of (tile, record) pairs reserves each touched tile's share of
+// its list with ONE global atomic (per-pair global atomics serialise on the busy tiles).
+struct PrepareBinParams {
+    PrepareParams prep;
+    BinParams bin;
+};
+struct PrepareBinBatch {
+    PrepareBinParams f[kMaxBatch];
+};
+__global__ __launch_bounds__(kBinThreads) void PrepareBinKernel(const PrepareBinBatch batch) {
     extern __shared__ float2 bin_lds[];
-    const BinParams& p = batch.f[blockIdx.z];
+    const PrepareBinParams& pb = batch.f[blockIdx.z];
+    const BinParams& p = pb.bin;
+    const PrepareParams& pp = pb.prep;
     const int tid = threadIdx.x;
     const int nx = p.tiles_x, ny = p.tiles_y;
     const int tiles = nx * ny;
     float2* b = bin_lds;
     unsigned* hist = reinterpret_cast<unsigned*>(bin_lds + nx + ny);
 
-    // Prologue: the monotone tile-column and tile-row bounds (the histogram's LDS is the
-    // reduction's scratch), then the histogram zeroed.
+    // This thread's record (its loads in flight while the block builds the tile bounds).
+    const unsigned i = blockIdx.x * kBinThreads + tid;  // spatial-order position (list entry)
+    const bool real = i < pp.n;
+    float c[9], vol = 0.f;
+    float4 sb = make_float4(__builtin_inff(), -__builtin_inff(), __builtin_inff(), -__builtin_inff());
+    const unsigned id = real ? pp.order[i] : i;
+    if (i < pp.n_pad) {
+        ComputeRecord(pp, id, real, c, vol, sb);
+    }
+    // The monotone tile-column and tile-row bounds (the histogram's LDS is the reduction's
+    // scratch), then the histogram zeroed.
     BinTileBounds(p, hist, b);
     for (int t = tid; t < tiles; t += kBinThreads) {
         hist[t] = 0u;
     }
-    __syncthreads();  // bounds in LDS, histogram zeroed
+    if (i < pp.n_pad) {
+        pp.qboxes[i] = QuantizeBox(sb);
+        if (real) {
+            pp.normals[id] = ShadingNormal(pp.vertices, id);
+        }
+        bool needed = !real || *p.range_tag == p.gen;
+        if (!needed) {  // analytic bounds: b[nx] is the first tile row, b[nx + ny - 1] the last
+            needed = QuantLo(sb.z) <= QuantHi(b[nx + ny - 1].y) && QuantHi(sb.w) >= QuantLo(b[nx].x);
+        }
+        if (needed) {
+            CullRecord r;
+            r.a = make_float4(c[0], c[1], c[2], c[3]);
+            r.b = make_float4(c[4], c[5], c[6], c[7]);
+            r.x = make_float4(c[8], vol, __uint_as_float(id), 0.f);
+            r.sb = sb;
+            pp.cull[i] = r;
+        }
+    }
+    __syncthreads();  // histogram zeroed
 
-    // This thread's record: its tile range and the tiles of it that pass (bit k = tile
-    // (r0 + k / w, c0 + k % w) of the range, at most kLargeTiles of them).
-    const unsigned i = blockIdx.x * kBinThreads + tid;  // spatial-order position (list entry)
+    // The record's tile range and the tiles of it that pass (bit k = tile (r0 + k / w, c0 + k % w)
+    // of the range, at most kLargeTiles of them).
     unsigned mask = 0u;
     int c0 = 0, r0 = 0, w = 1;
-    if (i < p.n) {
-        const CullRecord cr = p.cull[i];
-        const float4 sb = cr.sb;
-        if (sb.x <= sb.y && sb.z <= sb.w && (p.exp & 1u) == 0u) {  // else disabled: empty box
-            // Any tile (c, r) whose box overlaps sb has hi'[c] >= hi[c] >= sb.xlo and
-            // lo'[c] <= lo[c] <= sb.xhi, so c lies in [c0, c1]; rows likewise.
-            c0 = FirstHiAtLeast(b, nx, sb.x);
-            const int c1 = LastLoAtMost(b, nx, sb.y);
-            r0 = FirstHiAtLeast(b + nx, ny, sb.z);
-            const int r1 = LastLoAtMost(b + nx, ny, sb.w);
-            w = c1 - c0 + 1;
-            const int h = r1 - r0 + 1;
-            if (w > 0 && h > 0 && (p.exp & 2u) == 0u) {
-                if (w * h > kLargeTiles) {
-                    p.large_list[atomicAdd(&p.counts[tiles], 1u)] = i;
-                } else {
-                    const Record rec{cr.a.x, cr.a.y, cr.a.z, cr.a.w, cr.b.x, cr.b.y, cr.b.z, cr.b.w, cr.x.x};
+    if (real && sb.x <= sb.y && sb.z <= sb.w && (p.exp & 1u) == 0u) {  // else disabled: empty box
+        // Any tile (c, r) whose box overlaps sb has hi'[c] >= hi[c] >= sb.xlo and
+        // lo'[c] <= lo[c] <= sb.xhi, so c lies in [c0, c1]; rows likewise.
+        c0 = FirstHiAtLeast(b, nx, sb.x);
+        const int c1 = LastLoAtMost(b, nx, sb.y);
+        r0 = FirstHiAtLeast(b + nx, ny, sb.z);
+        const int r1 = LastLoAtMost(b + nx, ny, sb.w);
+        w = c1 - c0 + 1;
+        const int h = r1 - r0 + 1;
+        if (w > 0 && h > 0 && (p.exp & 2u) == 0u) {
+            if (w * h > kLargeTiles) {
+                p.large_list[atomicAdd(&p.counts[tiles], 1u)] = i;
+            } else {
+                const Record rec{c[0], c[1], c[2], c[3], c[4], c[5], c[6], c[7], c[8]};
 #pragma unroll 1
-                    for (int k = 0; k < w * h; ++k) {
-                        const TileInfo ti = p.tile_info[(r0 + k / w) * nx + c0 + k % w];
-                        const Box tb{ti.box.x, ti.box.y, ti.box.z, ti.box.w};
-                        if (ti.usable != 0u && ScreenBoxOverlaps(tb, sb) && BoxMayHit(tb, rec)) {
-                            mask |= 1u << k;
-                        }
+                for (int k = 0; k < w * h; ++k) {
+                    const TileInfo ti = p.tile_info[(r0 + k / w) * nx + c0 + k % w];
+                    const Box tb{ti.box.x, ti.box.y, ti.box.z, ti.box.w};
+                    if (ti.usable != 0u && ScreenBoxOverlaps(tb, sb) && BoxMayHit(tb, rec)) {
+                        mask |= 1u << k;
                     }
                 }
             }
@@ -1669,8 +1684,6 @@ __global__ __launch_bounds__(kBinThreads) void BinTrianglesKernel(const BinBatch
             p.lists[static_cast<size_t>(t) * p.capacity + at] = i;
         }
     }
-    // Every block's list lengths are final (its count atomics returned): the last block to
-    // finish lists the trace work (one launch fewer than a separate ordering kernel).
 }
 
 // The trace work list: one 1024-thread block after the bin kernel. Built instead by the bin
@@ -1856,9 +1869,10 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(c
         d_cand = total;
 #endif
     } else {
-        // FULL: stream every record's quantized screen box (one per thread per step, loaded one
-        // step ahead); the ones overlapping the block box join an LDS id list, which is walked
-        // in packet batches whenever it holds a batch (and at the end).
+        // FULL: stream every record's quantized screen box in spatial order (one per thread per
+        // step, loaded one step ahead); the positions overlapping the block box join an LDS list,
+        // walked in packet batches (cull records by position) whenever it holds a batch (and at
+        // the end).
         const bool block_sb = pf.use_sb;
         const QBox bq = Quantize(bb);
         const unsigned long long lt_mask = (1ull << lane) - 1ull;
@@ -1916,7 +1930,7 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(c
 #pragma unroll
                 for (int e = 0; e < kSlices; ++e) {
                     valid[e] = InBatch(e, tid) && b0 + e * kCullThreads + tid < listed;
-                    cr[e] = LoadCullById(p, my_ids[bi][e]);
+                    cr[e] = p.cull[my_ids[bi][e]];
                 }
                 PacketBatch(sh, bb, pf, cr, valid, [] {});
 #ifdef SRT_DIAG
@@ -2590,8 +2604,8 @@ BinParams BindBins(TraceParams& p, const CullBins& bins, std::uint64_t n) {
 }  // namespace
 
 hipError_t LaunchCullFrames(const CullFrame* frames, std::size_t count, std::uint64_t n, const float* d_vertices,
-                            const float* d_albedo, const Frame& frame, const float background[3],
-                            const unsigned* prepare_rank, hipStream_t stream, const StageEvents* events) {
+                            const float* d_albedo, const Frame& frame, const float background[3], const unsigned* d_rank,
+                            hipStream_t stream, const StageEvents* events) {
     if (frames == nullptr || count == 0 || count > static_cast<std::size_t>(kMaxBatch)) {
         return hipErrorInvalidValue;
     }
@@ -2605,10 +2619,10 @@ hipError_t LaunchCullFrames(const CullFrame* frames, std::size_t count, std::uin
     const StageEvents ev = events != nullptr ? *events : StageEvents{};
     TraceBatch tb{};
     BinBatch bb{};
-    PrepareInfoBatch pb{};
+    PrepareBinBatch pb{};
     for (std::size_t i = 0; i < count; ++i) {
         const CullFrame& f = frames[i];
-        if (f.bins == nullptr || f.edges == nullptr || f.band.width != band0.width ||
+        if (f.bins == nullptr || f.edges == nullptr || f.bins->order == nullptr || f.band.width != band0.width ||
             f.band.row_count != band0.row_count || f.band.row_begin != band0.row_begin ||
             f.band.height != band0.height || f.bins->max_chunks != frames[0].bins->max_chunks) {
             return hipErrorInvalidValue;  // one band shape per batch
@@ -2618,25 +2632,18 @@ hipError_t LaunchCullFrames(const CullFrame* frames, std::size_t count, std::uin
             return hipErrorInvalidValue;  // bins sized for another band shape
         }
         bb.f[i] = BindBins(tb.f[i], *f.bins, n);
-        if (prepare_rank != nullptr) {
-            pb.f[i].prep = MakePrepareParams(d_vertices, prepare_rank, n, frame, const_cast<float*>(f.edges));
-            pb.f[i].bin = bb.f[i];
-            pb.f[i].prep_blocks = (pb.f[i].prep.n_pad + kBinThreads - 1) / kBinThreads;
-        }
+        pb.f[i].prep = MakePrepareParams(d_vertices, d_rank, n, frame, const_cast<float*>(f.edges));
+        pb.f[i].prep.order = f.bins->order;
+        pb.f[i].bin = bb.f[i];
     }
     const unsigned z = static_cast<unsigned>(count);
     const unsigned gx = static_cast<unsigned>(tb.f[0].tiles_x), gy = tb.f[0].tiles / gx;
-    // Record setup (when the frame's records are pending) and tile info in one launch; bins (at
-    // least one block); the trace work list; the trace: M blocks per work item.
-    if (prepare_rank != nullptr) {
-        Launch(PrepareInfoKernel, dim3(pb.f[0].prep_blocks + gx * gy, 1, z), dim3(kBinThreads), stream, ev.prep_begin,
-               ev.prep_end, pb);
-    } else {
-        Launch(TileInfoKernel, dim3(gx, gy, z), dim3(kBinThreads), stream, ev.prep_begin, ev.prep_end, bb);
-    }
-    const unsigned blocks = static_cast<unsigned>(n == 0 ? 1 : (n + kBinThreads - 1) / kBinThreads);
-    LaunchLds(BinTrianglesKernel, dim3(blocks, 1, z), dim3(kBinThreads), BinLdsBytes(static_cast<int>(gx), static_cast<int>(gy)),
-              stream, ev.bin_begin, nullptr, bb);
+    // Tile info; records + bins (every padded position: the FULL stream reads them all); the
+    // trace work list; the trace: M blocks per work item.
+    Launch(TileInfoKernel, dim3(gx, gy, z), dim3(kBinThreads), stream, ev.prep_begin, ev.prep_end, bb);
+    const unsigned blocks = (pb.f[0].prep.n_pad + kBinThreads - 1) / kBinThreads;
+    LaunchLds(PrepareBinKernel, dim3(blocks, 1, z), dim3(kBinThreads),
+              BinLdsBytes(static_cast<int>(gx), static_cast<int>(gy)), stream, ev.bin_begin, nullptr, pb);
     Launch(WorkOrderKernel, dim3(1, 1, z), dim3(1024), stream, nullptr, ev.bin_end, bb);
     Launch(TraceCullKernel, dim3(tb.f[0].tiles * kParts * tb.f[0].max_chunks, 1, z), dim3(kWave * kCullWaves), stream,
            ev.begin, ev.end, tb);
@@ -2650,9 +2657,9 @@ hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_ver
     if (band.row_count == 0 || band.width == 0) {
         return hipSuccess;
     }
-    if (variant == kTraceCull && bins != nullptr) {
+    if (variant == kTraceCull && bins != nullptr) {  // computes the records itself, every call
         const CullFrame f{d_edges, bins, band};
-        return LaunchCullFrames(&f, 1, n, d_vertices, d_albedo, frame, background, prepare_rank, stream, events);
+        return LaunchCullFrames(&f, 1, n, d_vertices, d_albedo, frame, background, nullptr, stream, events);
     }
     const StageEvents ev = events != nullptr ? *events : StageEvents{};
     if (prepare_rank != nullptr) {

@@ -223,10 +223,11 @@ void DeviceScene::Prepare(std::size_t width, std::size_t height, hipStream_t str
     m_frame = MakeFrame(m_camera, width, height);
     m_width = width;
     m_height = height;
-    // Deferred: the next Trace enqueues the record setup on its stream, fused with its first
-    // bin kernel when it bins (render.hip PrepareInfoKernel).
+    // Deferred: the next Trace enqueues the record setup on its stream (the binned cull path
+    // computes the records inside its bin kernel on every call, render.hip PrepareBinKernel).
     (void)stream;
     m_prepare_pending = true;
+    m_normals_current = false;
 }
 
 void DeviceScene::OrderAfterPrevious(hipStream_t stream) const {
@@ -241,11 +242,13 @@ void DeviceScene::OrderAfterPrevious(hipStream_t stream) const {
     m_last_stream = stream;
 }
 
-// The edge records of the prepared frame, when no trace has enqueued them yet (a Shade first).
-void DeviceScene::PrepareIfPending(hipStream_t stream) const {
-    if (m_prepare_pending) {
+// The shading normals of the prepared frame, when no trace has written them yet (a Shade first):
+// the full record pass.
+void DeviceScene::NormalsIfStale(hipStream_t stream) const {
+    if (!m_normals_current) {
         HipCheck(LaunchPrepare(m_vertices, m_rank, m_n, m_frame, m_edges, stream), "prepare kernel launch");
         m_prepare_pending = false;
+        m_normals_current = true;
     }
 }
 
@@ -264,7 +267,7 @@ void DeviceScene::Shade(const float* d_offsets, const int* d_ids, float* d_rgba,
         return;
     }
     OrderAfterPrevious(stream);
-    PrepareIfPending(stream);
+    NormalsIfStale(stream);
     BandArgs band{d_offsets, d_rgba, m_width, m_height, row_begin, row_count, const_cast<int*>(d_ids)};
     HipCheck(LaunchShade(m_vertices, m_albedo, m_edges, m_n, m_frame, m_background, band, stream, frames, band_rows),
              "shade kernel launch");
@@ -318,6 +321,7 @@ void DeviceScene::EnsureEdgeSlots(std::size_t slots, hipStream_t stream) const {
     m_edges = grown;
     m_edge_slots = slots;
     m_prepare_pending = true;
+    m_normals_current = false;
 }
 
 void DeviceScene::TraceBatch(const float* const* d_offsets, float* const* d_rgba, int* const* d_ids, std::size_t frames,
@@ -361,7 +365,7 @@ void DeviceScene::TraceBatch(const float* const* d_offsets, float* const* d_rgba
     }
     HipCheck(LaunchCullFrames(cf, frames, m_n, m_vertices, m_albedo, m_frame, m_background, m_rank, stream, nullptr),
              "batched trace launch");
-    m_prepare_pending = false;  // slot 0 holds the prepared frame's records
+    m_normals_current = true;  // slot 0's normals (the tile-planar records are the full pass's)
 }
 
 void DeviceScene::Trace(const float* d_offsets, float* d_rgba, std::size_t row_begin, std::size_t row_count,
@@ -384,9 +388,11 @@ void DeviceScene::Trace(const float* d_offsets, float* d_rgba, std::size_t row_b
     if (variant == kTraceBvh && m_bvh == nullptr && row_count != 0) {
         m_bvh = DeviceAlloc<unsigned char>(BvhBytes(m_n), "hipMalloc(bvh)");
     }
-    const bool prepare = m_prepare_pending && row_count != 0;
+    // The full record pass for every path but the binned cull one, which computes its records in
+    // its bin kernel (its "prepare" stage is the tile-info kernel).
+    const bool prepare = use_bins == nullptr && m_prepare_pending && row_count != 0;
     StageEvents ev{};
-    if (m_timing && prepare) {
+    if (m_timing && (prepare || (use_bins != nullptr && row_count != 0))) {
         ev.prep_begin = TimingEvent(m_prep_events, 2 * m_prep_timed);
         ev.prep_end = TimingEvent(m_prep_events, 2 * m_prep_timed + 1);
         ++m_prep_timed;
@@ -409,6 +415,10 @@ void DeviceScene::Trace(const float* d_offsets, float* d_rgba, std::size_t row_b
              "trace kernel launch");
     if (prepare) {
         m_prepare_pending = false;
+        m_normals_current = true;
+    }
+    if (use_bins != nullptr && row_count != 0) {
+        m_normals_current = true;
     }
 }
 

@@ -115,7 +115,7 @@ private:
     // Calls on one scene are stream-ordered: the per-frame edge records and the cull work buffer
     // are shared state, so a call on another stream than the previous one first waits for it.
     void OrderAfterPrevious(hipStream_t stream) const;
-    void PrepareIfPending(hipStream_t stream) const;
+    void NormalsIfStale(hipStream_t stream) const;
     mutable hipStream_t m_last_stream = nullptr;
     mutable bool m_used = false;
     mutable hipEvent_t m_order_event = nullptr;
@@ -123,7 +123,8 @@ private:
     mutable std::vector<hipEvent_t> m_events;
     mutable std::vector<bool> m_binned;
     mutable std::size_t m_prep_timed = 0;
-    mutable bool m_prepare_pending = false;
+    mutable bool m_prepare_pending = false;  // the full record pass has not run for the prepared frame
+    mutable bool m_normals_current = false;  // slot 0's shading normals written since the last Prepare
     mutable std::size_t m_timed = 0;
 };
 
