@@ -165,13 +165,17 @@ def test_variants_bitwise_identical_1080p(gpu, scenes):
 @pytest.mark.parametrize("mode", CULL_MODES)
 def test_cull_modes(gpu, scenes, monkeypatch, mode):
     """Every cull mode (bin lists on/off, split work items, forced bin-list overflow) against
-    the oracle, with uniform and random offsets, on a frame that leaves partial tiles."""
+    the oracle, with uniform and random offsets, on a frame that leaves partial tiles; and the
+    same frame traced as uneven row bands (a band's bin pass writes only the cull records that
+    can reach its rows; with forced overflow its tiles stream every record) bit for bit."""
     set_cull_mode(monkeypatch, mode)
     rng = np.random.default_rng(5)
     w, h = 200, 150
     for offsets in (None, rng.random((h, w, 2), dtype=np.float32)):
         got = torch_render(scenes["soup2k"], w, h, offsets, variant="cull")
         assert_parity(got, oracle_render(scenes["soup2k"], w, h, offsets))
+        banded = torch_render(scenes["soup2k"], w, h, offsets, variant="cull", bands=[37, 1, 50, 62])
+        assert np.array_equal(banded.view(np.uint32), got.view(np.uint32))
 
 
 def test_cull_setup_state_across_frames(gpu, scenes):
