@@ -69,6 +69,8 @@ def parse():
     p.add_argument("--variant", default=os.environ.get("SRT_BENCH_VARIANT", "cull"), choices=list(KERNEL_NAMES))
     p.add_argument("--mode", default="bands", choices=["bands", "frames"], help="multi-GPU split (module doc)")
     p.add_argument("--root", default="rotate", choices=["rotate", "fixed"], help="bands: compositing rank")
+    p.add_argument("--rows", default="interleaved", choices=["interleaved", "contiguous"],
+                   help="bands: each rank's rows, the frame's 32-row tile rows dealt round-robin or one block")
     p.add_argument("--queues", type=int, default=int(os.environ.get("SRT_BENCH_QUEUES", "3")),
                    help="frames in flight per GPU (own scene buffers, HIP stream, process group each)")
     p.add_argument("--batch", type=int, default=int(os.environ.get("SRT_BENCH_BATCH", "0")),
@@ -169,8 +171,10 @@ class Pipeline:
     band r of every frame (P > 1: hit ids, gathered to the compositor, which shades); mode
     "frames": whole frames, each rank its own jitter; P == 1: the two coincide."""
 
-    def __init__(self, ctx, path, mode="bands", queues=3, variant="cull", offsets="uniform", rotate=True, batch=1):
-        from simpleraytracer_amd.bands import band_range, band_rows
+    def __init__(self, ctx, path, mode="bands", queues=3, variant="cull", offsets="uniform", rotate=True, batch=1,
+                 rows="interleaved"):
+        from simpleraytracer_amd.bands import (band_range, band_rows, interleaved_band_rows, interleaved_frame_rows,
+                                               interleaved_range)
 
         torch, a = ctx.torch, ctx.a
         self.ctx, self.mode, self.variant, self.rotate = ctx, mode, variant, rotate
@@ -178,11 +182,20 @@ class Pipeline:
         P = ctx.world if mode == "bands" else 1
         self.P = P
         self.G = max(1, min(batch, ctx.srt.MAX_BATCH))  # frames per launch (and per gather at P > 1)
-        self.row_begin, self.row_count = band_range(self.H, P, ctx.rank) if P > 1 else (0, self.H)
-        self.B = band_rows(self.H, P)
+        self.interleave = P if (P > 1 and rows == "interleaved") else 1
+        if self.interleave > 1:
+            self.row_begin, self.row_count = interleaved_range(self.H, P, ctx.rank)
+            self.B = interleaved_band_rows(self.H, P)
+        else:
+            self.row_begin, self.row_count = band_range(self.H, P, ctx.rank) if P > 1 else (0, self.H)
+            self.B = band_rows(self.H, P)
         self.offsets = make_offsets(torch, a, ctx.dev, jitter(ctx.rank) if mode == "frames" else 0.5, offsets,
                                     seed=0x5EED + (ctx.rank if mode == "frames" else 0))
-        self.band_off = self.offsets[self.row_begin:self.row_begin + self.row_count]
+        if self.interleave > 1:  # the band's rows of the frame's offsets, in band order (one copy)
+            rows_t = torch.from_numpy(interleaved_frame_rows(self.H, P, ctx.rank)).to(ctx.dev)
+            self.band_off = self.offsets.index_select(0, rows_t).contiguous()
+        else:
+            self.band_off = self.offsets[self.row_begin:self.row_begin + self.row_count]
         self.timing = False
         self.queues = []
         for q in range(max(1, queues)):
@@ -197,18 +210,20 @@ class Pipeline:
             self.queues.append(qd)
         self.triangles = self.queues[0]["scene"].triangles
 
-    def _batch_run(self, q, f):
-        """The queue's batched trace of its first f slots (one srtTraceBatchAsync call), bound once."""
-        if f not in q["runs"]:
+    def _batch_run(self, q, f, slot=0):
+        """The queue's batched trace of f slots from `slot` (one srtTraceBatchAsync call), bound once."""
+        key = (f, slot)
+        if key not in q["runs"]:
             sc, st = q["scene"], q["stream"]
             if self.P > 1:
-                q["runs"][f] = sc.bind_trace_batch([self.band_off] * f, [q["band_ids"][j, :self.row_count]
-                                                                         for j in range(f)],
-                                                   self.row_begin, self.row_count, self.variant, st, ids=True)
+                q["runs"][key] = sc.bind_trace_batch([self.band_off] * f, [q["band_ids"][j, :self.row_count]
+                                                                           for j in range(slot, slot + f)],
+                                                     self.row_begin, self.row_count, self.variant, st, ids=True,
+                                                     row_interleave=self.interleave)
             else:
-                q["runs"][f] = sc.bind_trace_batch([self.offsets] * f, [q["rgba"][j] for j in range(f)], 0, self.H,
-                                                   self.variant, st)
-        return q["runs"][f]
+                q["runs"][key] = sc.bind_trace_batch([self.offsets] * f, [q["rgba"][j] for j in range(slot, slot + f)],
+                                                     0, self.H, self.variant, st)
+        return q["runs"][key]
 
     def step(self, k, nq):
         """Frame k on queue k % nq: into the queue's next batch slot; a full batch is traced
@@ -217,13 +232,8 @@ class Pipeline:
         q = self.queues[k % nq]
         sc, st = q["scene"], q["stream"]
         j = q["fill"]
-        if self.timing and self.row_count:
-            sc.prepare(self.W, self.H, st)
-            if self.P > 1:
-                sc.trace_ids(self.band_off, q["band_ids"][j, :self.row_count], self.row_begin, self.row_count,
-                             variant=self.variant, stream=st)
-            else:
-                sc.trace(self.offsets, q["rgba"][j], 0, self.H, variant=self.variant, stream=st)
+        if self.timing and self.row_count:  # one frame per call: the stage events time one frame
+            self._batch_run(q, 1, j)()
             q["traced"] = j + 1
         q["fill"] = j + 1
         if q["fill"] == self.G:
@@ -250,7 +260,8 @@ class Pipeline:
         if ctx.backend == "gloo":  # CPU rehearsal: gloo gathers host tensors, synchronously
             st.synchronize()
             host_out = torch.empty(self.P * f * self.B * self.W, dtype=torch.int32) if ctx.rank == root else None
-            ids, _ = gather_band_batch(batch.cpu(), self.H, dst=root, group=q["group"], out=host_out)
+            ids, _ = gather_band_batch(batch.cpu(), self.H, dst=root, group=q["group"], out=host_out,
+                                       interleaved=self.interleave > 1)
             if ids is not None:
                 dev_ids = q["frame_ids"][:ids.numel()].view(ids.shape)
                 dev_ids.copy_(ids.to(ctx.dev))
@@ -259,10 +270,11 @@ class Pipeline:
         else:
             with torch.cuda.stream(st):
                 ids, work = gather_band_batch(batch, self.H, dst=root, group=q["group"], out=q["frame_ids"],
-                                              async_op=True)
+                                              async_op=True, interleaved=self.interleave > 1)
                 work.wait()  # the queue's stream waits for the gather (ids consumed / slots reusable)
         if ctx.rank == root:
-            sc.shade_bands(self.offsets, ids, q["rgba"][:f], self.B, stream=st)
+            sc.shade_bands(self.offsets, ids, q["rgba"][:f], self.B, stream=st,
+                           interleaved=self.interleave if self.interleave > 1 else 0)
             q["shaded"] = f
         q["root"] = root
         q["batches"] += 1
@@ -455,7 +467,7 @@ def main():
     path = ctx.scene_path(a.scene, a.triangles if a.scene == "soup" else None)
     wl = workload_name(a)
     rotate = a.root == "rotate"
-    main_run = Pipeline(ctx, path, a.mode, a.queues, a.variant, a.offsets, rotate, a.batch)
+    main_run = Pipeline(ctx, path, a.mode, a.queues, a.variant, a.offsets, rotate, a.batch, a.rows)
     n_tri = main_run.triangles
     _, order_build_ms = main_run.queues[0]["scene"].spatial_order()
     W, H = a.width, a.height
@@ -475,12 +487,16 @@ def main():
     if world > 1 and extras:  # the other split and the other compositor choice, same steps
         try:
             om = "frames" if a.mode == "bands" else "bands"
-            o = Pipeline(ctx, path, om, a.queues, a.variant, a.offsets, rotate, a.batch)
+            o = Pipeline(ctx, path, om, a.queues, a.variant, a.offsets, rotate, a.batch, a.rows)
             legs[om] = {**leg_summary(o.run(a.steps, a.warmup)), "scaling": "weak" if om == "frames" else "strong"}
             o.close()
             if a.mode == "bands":
-                o = Pipeline(ctx, path, "bands", a.queues, a.variant, a.offsets, not rotate, a.batch)
+                o = Pipeline(ctx, path, "bands", a.queues, a.variant, a.offsets, not rotate, a.batch, a.rows)
                 legs["fixed_root" if rotate else "rotating_root"] = leg_summary(o.run(a.steps, a.warmup))
+                o.close()
+                other = "contiguous" if a.rows == "interleaved" else "interleaved"
+                o = Pipeline(ctx, path, "bands", a.queues, a.variant, a.offsets, rotate, a.batch, other)
+                legs[f"{other}_rows"] = leg_summary(o.run(a.steps, a.warmup))
                 o.close()
         except Exception as e:  # noqa: BLE001 -- the primary line must still be printed
             legs["secondary_error"] = f"{type(e).__name__}: {e}"
@@ -519,7 +535,8 @@ def main():
         launch_rays = main_run.row_count * W
         roof, valu, bfe = roofline_fields(wl, a.variant, launch_rays, n_tri, rt["trace_ms"], band_ids)
         if band_ids:
-            par = f"bands x{world} + RCCL gather of hit ids to the {'rotating' if rotate else 'rank-0'} compositor"
+            par = (f"bands x{world} ({a.rows} rows) + RCCL gather of hit ids to the "
+                   f"{'rotating' if rotate else 'rank-0'} compositor")
         else:
             par = f"{a.mode} x{world}"
         line = {

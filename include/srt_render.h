@@ -92,11 +92,16 @@ ML_API_ENTRY int srtTraceIdsAsync(srt_device_scene scene, const float* d_offsets
  * RGBA d_rgba[f] (row_count x width x 4) or, with d_rgba NULL, its hit ids d_ids[f]
  * (row_count x width). Every frame gets the whole per-frame work of srtPrepareAsync +
  * srtTraceAsync (record setup, bins, trace): the same pixels, bit for bit; the cull variant runs
- * the batch with one launch per stage, so a frame costs a quarter of the host launches. */
+ * the batch with one launch per stage, so a frame costs a quarter of the host launches.
+ * row_interleave 1: the band is frame rows [row_begin, row_begin + row_count). P > 1: the frame's
+ * 32-row tile rows are dealt round-robin to P bands and this band holds tile rows
+ * row_begin / 32 + k P, k = 0, 1, ..., concatenated (row_begin a multiple of 32, row_count =
+ * those rows' total; SRT_TILE_ROWS = 32). */
 #define SRT_MAX_BATCH 8
+#define SRT_TILE_ROWS 32
 ML_API_ENTRY int srtTraceBatchAsync(srt_device_scene scene, const float* const* d_offsets, float* const* d_rgba,
-                                    int* const* d_ids, size_t frames, size_t row_begin, size_t row_count, int variant,
-                                    void* stream);
+                                    int* const* d_ids, size_t frames, size_t row_begin, size_t row_count,
+                                    size_t row_interleave, int variant, void* stream);
 
 /* Stage 3 (deferred shading): rows [row_begin, row_begin + row_count) of the prepared frame
  * shaded from hit ids (as srtTraceIdsAsync writes them) and sample offsets (both band-local,
@@ -107,11 +112,14 @@ ML_API_ENTRY int srtShadeAsync(srt_device_scene scene, const float* d_offsets, c
 /* Stage 3 for a batch of `frames` frames of the prepared camera (the multi-process band path,
  * where one gather carries several frames): the ids arrive band-major, as a gather of every
  * rank's (frames x band_rows x width) band buffer leaves them,
- *   d_ids[band][frame][band_rows][width], band = 0 .. ceil(height / band_rows) - 1,
- * d_offsets is the frame's (height x width x 2), d_rgba receives frames x height x width x 4.
- * One launch; each frame is bit-identical to srtTraceAsync's RGBA. */
+ *   d_ids[band][frame][band_rows][width],
+ * with bands = ceil(height / band_rows) contiguous bands (interleaved = 0), or `interleaved`
+ * bands that took the frame's 32-row tile rows round-robin (srtTraceBatchAsync row_interleave;
+ * band_rows >= the largest band's rows). d_offsets is the frame's (height x width x 2), d_rgba
+ * receives frames x height x width x 4. One launch; each frame is bit-identical to
+ * srtTraceAsync's RGBA. */
 ML_API_ENTRY int srtShadeBandsAsync(srt_device_scene scene, const float* d_offsets, const int* d_ids, float* d_rgba,
-                                    size_t frames, size_t band_rows, void* stream);
+                                    size_t frames, size_t band_rows, size_t interleaved, void* stream);
 
 /* Calls on one srt_device_scene are ordered: the per-frame edge records and the cull work
  * buffer are shared, so a call on a different stream than the previous call first waits (HIP

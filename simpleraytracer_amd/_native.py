@@ -29,6 +29,7 @@ SRT_TRACE_SCALAR = 1
 SRT_TRACE_CULL = 2
 SRT_TRACE_BVH = 3
 SRT_MAX_BATCH = 8  # include/srt_render.h: frames per srtTraceBatchAsync call
+SRT_TILE_ROWS = 32  # include/srt_render.h: rows per tile row (interleaved bands deal these)
 
 
 class ImageInfo(ctypes.Structure):
@@ -93,11 +94,11 @@ _SIGNATURES = {
                                         ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]),
     "srtTraceBatchAsync": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p),
                                           ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_size_t,
-                                          ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]),
+                                          ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]),
     "srtShadeAsync": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                      ctypes.c_size_t, ctypes.c_size_t, ctypes.c_void_p]),
     "srtShadeBandsAsync": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
-                                          ctypes.c_size_t, ctypes.c_size_t, ctypes.c_void_p]),
+                                          ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_void_p]),
     "srtGatherBandsHost": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_size_t,
                                           ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]),
     "srtSetStageTiming": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),

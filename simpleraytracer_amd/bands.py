@@ -3,7 +3,9 @@
 Multi-GPU layout (DESIGN.md "Multi-GPU"): rank r of P renders frame rows
 [r*B, min(H, (r+1)*B)) with B = ceil(H / P); every rank holds a band buffer of exactly B rows
 (the last one padded) so the gather has equal counts; the destination receives the bands in
-place into one (P*B)-row buffer and keeps the first H rows. Inside one process, Renderer
+place into one (P*B)-row buffer and keeps the first H rows. Interleaved bands
+(``interleaved_range``) deal the frame's 32-row tile rows round-robin instead, so every rank gets
+a share of the dense centre; the gathered layout is then unscrambled by the shading kernel. Inside one process, Renderer
 (csrc/renderer.cpp) does the same with ncclGather; across processes (one rank per GPU,
 torch.distributed over RCCL/xGMI, or gloo on CPU for tests) this module does it with
 ``dist.gather``.
@@ -30,6 +32,33 @@ def band_range(height: int, world: int, rank: int) -> tuple[int, int]:
     begin = min(height, rank * b)
     end = min(height, (rank + 1) * b)
     return begin, end - begin
+
+
+TILE_ROWS = 32  # include/srt_render.h SRT_TILE_ROWS: interleaved bands deal whole tile rows
+
+
+def interleaved_range(height: int, world: int, rank: int) -> tuple[int, int]:
+    """(row_begin, row_count) of ``rank``'s interleaved band: the frame's 32-row tile rows dealt
+    round-robin, rank r holding tile rows r, r + P, r + 2P, ... (srtTraceBatchAsync
+    row_interleave = P); row_count may be 0. Balances the work of a frame whose centre is denser
+    than its edges, which contiguous bands do not."""
+    tiles = (height + TILE_ROWS - 1) // TILE_ROWS
+    rows = sum(min(TILE_ROWS, height - t * TILE_ROWS) for t in range(rank, tiles, world))
+    return min(height, rank * TILE_ROWS), rows
+
+
+def interleaved_band_rows(height: int, world: int) -> int:
+    """Rows of the largest interleaved band (rank 0's): the gather's per-rank buffer height."""
+    return interleaved_range(height, world, 0)[1]
+
+
+def interleaved_frame_rows(height: int, world: int, rank: int):
+    """The frame rows of ``rank``'s interleaved band, in band order (numpy int64)."""
+    import numpy as np
+
+    tiles = (height + TILE_ROWS - 1) // TILE_ROWS
+    return np.concatenate([np.arange(t * TILE_ROWS, min(height, (t + 1) * TILE_ROWS))
+                           for t in range(rank, tiles, world)] or [np.zeros(0, np.int64)]).astype(np.int64)
 
 
 def compositor(frame: int, world: int, rotate: bool = True) -> int:
@@ -86,10 +115,12 @@ def gather_band_ids(band_ids, height: int, dst: int = 0, group=None, out=None, a
     return _gather_into(band_ids, height, dst, group, out, async_op)
 
 
-def gather_band_batch(batch, height: int, dst: int = 0, group=None, out=None, async_op: bool = False):
+def gather_band_batch(batch, height: int, dst: int = 0, group=None, out=None, async_op: bool = False,
+                      interleaved: bool = False):
     """Gather F frames' bands in ONE collective: every rank's (F, B, W) int32 hit-id batch
     (frame f's band in batch[f]) to ``dst``, received band-major into (P, F, B, W) — the layout
-    srtShadeBandsAsync (DeviceScene.shade_bands) shades in one launch.
+    srtShadeBandsAsync (DeviceScene.shade_bands) shades in one launch. ``interleaved``: the bands
+    are interleaved (interleaved_range), each batch band interleaved_band_rows rows.
 
     One collective per F frames: a torch-RCCL gather costs ~44 us of host time per call
     (tools/host_probe_bands.py), more than a band's trace, so the band path gathers batches.
@@ -103,8 +134,9 @@ def gather_band_batch(batch, height: int, dst: int = 0, group=None, out=None, as
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     frames, b, width = batch.shape
-    if b != band_rows(height, world):
-        raise ValueError(f"batch bands must have {band_rows(height, world)} rows, got {b}")
+    want = interleaved_band_rows(height, world) if interleaved else band_rows(height, world)
+    if b != want:
+        raise ValueError(f"batch bands must have {want} rows, got {b}")
     dst_global = dst if group is None else dist.get_global_rank(group, dst)
     if rank != dst:
         return None, dist.gather(batch, gather_list=None, dst=dst_global, group=group, async_op=async_op)

@@ -71,7 +71,19 @@ struct BandArgs {
     std::size_t row_begin;  // first frame row of the band
     std::size_t row_count;
     int* ids = nullptr;     // device, row_count x width: non-null = store hit ids (-1 miss), not RGBA
+    // 1: frame rows [row_begin, row_begin + row_count). P > 1: the band deals the frame's tile rows
+    // (kCullTileRows each) round-robin over P bands: frame tile rows row_begin / kCullTileRows + k P,
+    // k = 0, 1, ..., concatenated (row_begin a multiple of kCullTileRows; only the band's last tile
+    // row may be partial, and then it is the frame's last).
+    std::size_t row_interleave = 1;
 };
+
+// Frame row of band-local row `local` (BandArgs::row_interleave).
+inline std::size_t BandFrameRow(std::size_t row_begin, std::size_t interleave, std::size_t local);
+// Whether a band fits a frame of `height` rows (row_count may be 0).
+bool BandFits(std::size_t row_begin, std::size_t row_count, std::size_t interleave, std::size_t height);
+// Rows of band `band` of `bands` interleaved bands of a `height`-row frame.
+std::size_t InterleavedBandRows(std::size_t height, std::size_t bands, std::size_t band);
 
 // Launch the prepare kernel: writes PaddedTriangleCount(n) / kTileTriangles tiles into `edges`,
 // then the screen boxes, quantized boxes and cull records (d_rank: id -> spatial-order rank).
@@ -85,6 +97,10 @@ constexpr int kCullTileCols = 64;
 #define SRT_TILE_ROWS 32
 #endif
 constexpr int kCullTileRows = SRT_TILE_ROWS;
+
+inline std::size_t BandFrameRow(std::size_t row_begin, std::size_t interleave, std::size_t local) {
+    return row_begin + local + local / kCullTileRows * kCullTileRows * (interleave - 1);
+}
 constexpr int kMaxBatch = 8;          // frames of one batched cull launch (LaunchCullFrames)
 constexpr int kMaxBoundTiles = 2048;  // binning needs tiles_x + tiles_y <= this
 constexpr int kMaxBinTiles = 8192;    // and tiles_x * tiles_y <= this (bin kernel LDS histogram)
@@ -186,9 +202,10 @@ hipError_t LaunchCullFrames(const CullFrame* frames, std::size_t count, std::uin
 // frames > 1 shades a batch whose ids are band-major, ids[band][frame][band_rows][width] (a
 // gather of `frames` frames of band_rows-row bands; band_rows 0 = one band of row_count rows),
 // into band.rgba[frame][row_count][width].
+// interleaved > 0: the ids' bands are that many interleaved bands (BandArgs::row_interleave).
 hipError_t LaunchShade(const float* d_vertices, const float* d_albedo, const float* d_edges, std::uint64_t n,
                        const Frame& frame, const float background[3], const BandArgs& band, hipStream_t stream,
-                       std::size_t frames = 1, std::size_t band_rows = 0);
+                       std::size_t frames = 1, std::size_t band_rows = 0, std::size_t interleaved = 0);
 
 // Spatial order of the records (spatial.hip): ids sorted by the Morton code of their centroid's
 // image-plane position under the scene camera, on the device (keys + rocPRIM radix sort), and

@@ -69,6 +69,7 @@ struct TraceParams {
     int width;
     int row_count;
     int row_begin;
+    int row_interleave;  // band = frame tile rows row_begin / kTileRows + k * row_interleave (1: contiguous rows)
     // Cull variant with bins (render.h CullBins); tile_info == null: no bins, every tile
     // computes its own ray box and streams every record.
     const TileInfo* __restrict__ tile_info;   // per tile: ray box, uniform offset (TileInfoKernel)
@@ -419,6 +420,12 @@ __device__ __forceinline__ void TestTriangle(Rays<R>& s, const Record& q, unsign
 // Ray generation: lane owns column x, rows y0..y0+R-1 of the band (clamped for edge lanes;
 // clamped lanes compute but never store). Returns whether all R rays share fx's bit
 // pattern; `box` receives the rays' (fx, fy) bounding box (NaN positions drop out: a ray
+// Frame row of band-local row `local`: the band holds frame tile rows row_begin / kCullTileRows
+// + k * interleave, k = 0, 1, ... (interleave 1: the contiguous rows row_begin + local).
+__device__ __forceinline__ int FrameRow(int row_begin, int interleave, int local) {
+    return row_begin + local + local / kCullTileRows * kCullTileRows * (interleave - 1);
+}
+
 // with a NaN position fails every test).
 template <int R>
 __device__ __forceinline__ bool GenerateRays(const TraceParams& p, int x, int y0, Rays<R>& s, Box& box) {
@@ -430,7 +437,7 @@ __device__ __forceinline__ bool GenerateRays(const TraceParams& p, int x, int y0
         const int yc = min(y0 + r, p.row_count - 1);
         const float2 o = p.offsets[static_cast<size_t>(yc) * p.width + xc];
         s.fx[r] = (static_cast<float>(xc) + o.x) / p.wf;
-        s.fy[r] = (static_cast<float>(p.row_begin + yc) + o.y) / p.hf;
+        s.fy[r] = (static_cast<float>(FrameRow(p.row_begin, p.row_interleave, yc)) + o.y) / p.hf;
         s.bt[r] = __builtin_inff();
         s.bi[r] = -1;
         same = same && (__float_as_uint(s.fx[r]) == __float_as_uint(s.fx[0]));
@@ -489,9 +496,11 @@ __device__ __forceinline__ void ShadeAndStore(const TraceParams& p, int x, int y
 // GenerateRays' position expressions and ShadePixel: the frame equals the fused trace + shade
 // bit for bit. blockIdx.y = frame g of a batch whose ids arrive band-major, as a gather of
 // `frames` frames of row bands leaves them: ids[band][g][band_rows][width] (one frame and one
-// band of row_count rows: the plain (row_count, width) layout); out[g][row_count][width].
+// band of row_count rows: the plain (row_count, width) layout); out[g][row_count][width]. With
+// `interleaved` bands the bands took the frame's tile rows round-robin: row y is row
+// (t / bands) * kCullTileRows + y % kCullTileRows of band t % bands, t = y / kCullTileRows.
 __global__ __launch_bounds__(256) void ShadeIdsKernel(TraceParams p, const int* __restrict__ ids,
-                                                      unsigned band_rows, unsigned frames) {
+                                                      unsigned band_rows, unsigned frames, unsigned interleaved) {
     const size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     const size_t pixels = static_cast<size_t>(p.width) * p.row_count;
     if (i >= pixels) {
@@ -500,11 +509,19 @@ __global__ __launch_bounds__(256) void ShadeIdsKernel(TraceParams p, const int* 
     const unsigned g = blockIdx.y;
     const int x = static_cast<int>(i % static_cast<unsigned>(p.width));
     const int y = static_cast<int>(i / static_cast<unsigned>(p.width));
-    const unsigned band = static_cast<unsigned>(y) / band_rows;
-    const size_t at = ((static_cast<size_t>(band) * frames + g) * band_rows + (y - band * band_rows)) * p.width + x;
+    unsigned band, local;
+    if (interleaved != 0u) {
+        const unsigned t = static_cast<unsigned>(y) / kCullTileRows;
+        band = t % interleaved;
+        local = t / interleaved * kCullTileRows + static_cast<unsigned>(y) % kCullTileRows;
+    } else {
+        band = static_cast<unsigned>(y) / band_rows;
+        local = static_cast<unsigned>(y) - band * band_rows;
+    }
+    const size_t at = ((static_cast<size_t>(band) * frames + g) * band_rows + local) * p.width + x;
     const float2 o = p.offsets[i];
     const float fx = (static_cast<float>(x) + o.x) / p.wf;
-    const float fy = (static_cast<float>(p.row_begin + y) + o.y) / p.hf;
+    const float fy = (static_cast<float>(FrameRow(p.row_begin, p.row_interleave, y)) + o.y) / p.hf;
     const int id = ids[at];
     p.out[g * pixels + i] = ShadePixel(p, fx, fy, static_cast<unsigned>(id) < p.n ? id : -1);  // no id outside the scene
 }
@@ -1243,6 +1260,7 @@ struct BinParams {
     int width;
     int row_count;
     int row_begin;
+    int row_interleave;
     float wf;
     float hf;
 };
@@ -1312,7 +1330,7 @@ __device__ __forceinline__ void TileInfoBlock(const BinParams& p, int bx, int by
     for (int k = 0; k < kPer; ++k) {
         const int yy = min(y0 + wave + k * kWaves, p.row_count - 1);
         const float fx = (static_cast<float>(xx) + o[k].x) / p.wf;
-        const float fy = (static_cast<float>(p.row_begin + yy) + o[k].y) / p.hf;
+        const float fy = (static_cast<float>(FrameRow(p.row_begin, p.row_interleave, yy)) + o[k].y) / p.hf;
         box = Box{fminf(box.xlo, fx), fmaxf(box.xhi, fx), fminf(box.ylo, fy), fmaxf(box.yhi, fy)};
         regular = regular && __float_as_uint(o[k].x) == __float_as_uint(o0.x) &&
                   __float_as_uint(o[k].y) == __float_as_uint(o0.y);
@@ -1510,9 +1528,9 @@ __device__ void BinTileBounds(const BinParams& p, unsigned* scratch, float2* out
     if (*p.range_tag != p.gen) {  // written by the previous launch's tile blocks
         for (int i = tid; i < nx + ny; i += nthreads) {
             const bool col = i < nx;
-            const float v0 = col ? static_cast<float>(i * kWave) : static_cast<float>(p.row_begin + (i - nx) * kTileRows);
-            const float v1 = col ? static_cast<float>((i + 1) * kWave)
-                                 : static_cast<float>(p.row_begin + (i - nx + 1) * kTileRows);
+            const int r0 = FrameRow(p.row_begin, p.row_interleave, (i - nx) * kTileRows);  // the tile row's first
+            const float v0 = col ? static_cast<float>(i * kWave) : static_cast<float>(r0);
+            const float v1 = col ? static_cast<float>((i + 1) * kWave) : static_cast<float>(r0 + kTileRows);
             const float d = col ? p.wf : p.hf;
             out[i] = make_float2(v0 / d, v1 / d);
         }
@@ -1573,10 +1591,10 @@ std::size_t BinLdsBytes(int nx, int ny) {
 // writes, by position, its quantized box (the FULL stream's input) and its 64-B cull record (the
 // trace's only record reads), and its shading normal by id. The cull record is skipped when no
 // trace of this band can read it: with every offset of the frame in [0, 1] (no tile block tagged
-// it), every ray of the band lies in its analytic row bounds [lo' of the first tile row, hi' of
-// the last]; a record whose quantized screen box misses those rows is never listed (its row
-// range is empty) and never passes a FULL block's box test (a block box lies inside the rows and
-// quantisation is monotone). Padding and tagged frames write every record. The block then bins
+// it), every ray of a tile row of the band lies in that row's analytic bounds; a record whose
+// quantized screen box meets none of the band's quantized tile-row bounds is never listed (its
+// row range is empty) and never passes a FULL block's box test (a block box lies inside its tile
+// row and quantisation is monotone). Padding and tagged frames write every record. The block then bins
 // the records it holds: binary searches in the bounds give each record the range of tiles its
 // screen box can overlap, every tile of the range passing ScreenBoxOverlaps + BoxMayHit against
 // its own box gets the position appended (records spanning more than kLargeTiles tiles go to the
@@ -1621,8 +1639,20 @@ __global__ __launch_bounds__(kBinThreads) void PrepareBinKernel(const PrepareBin
             pp.normals[id] = ShadingNormal(pp.vertices, id);
         }
         bool needed = !real || *p.range_tag == p.gen;
-        if (!needed) {  // analytic bounds: b[nx] is the first tile row, b[nx + ny - 1] the last
-            needed = QuantLo(sb.z) <= QuantHi(b[nx + ny - 1].y) && QuantHi(sb.w) >= QuantLo(b[nx].x);
+        if (!needed) {  // does the quantized box meet a tile row of the band (analytic row bounds)?
+            // Quantisation keeps both bound sequences nondecreasing: the first row whose quantized
+            // hi reaches the box's lo has the smallest lo of the rows that can meet it.
+            const int qlo = QuantLo(sb.z), qhi = QuantHi(sb.w);
+            int lo = 0, hi = ny;
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (QuantHi(b[nx + mid].y) >= qlo) {
+                    hi = mid;
+                } else {
+                    lo = mid + 1;
+                }
+            }
+            needed = lo < ny && QuantLo(b[nx + lo].x) <= qhi;
         }
         if (needed) {
             CullRecord r;
@@ -1803,7 +1833,7 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(c
     if (regular) {
         if (lane < kBlockRows) {
             const int yc = min(row0 + lane, p.row_count - 1);
-            fy_lane = (static_cast<float>(p.row_begin + yc) + oy) / p.hf;
+            fy_lane = (static_cast<float>(FrameRow(p.row_begin, p.row_interleave, yc)) + oy) / p.hf;
         }
         const int xc = min(x, p.width - 1);
         const float fx = (static_cast<float>(xc) + ox) / p.wf;
@@ -2545,6 +2575,7 @@ TraceParams MakeTraceParams(const float* d_edges, std::uint64_t n, const float* 
     p.width = static_cast<int>(band.width);
     p.row_count = static_cast<int>(band.row_count);
     p.row_begin = static_cast<int>(band.row_begin);
+    p.row_interleave = static_cast<int>(band.row_interleave);
     p.wf = static_cast<float>(band.width);
     p.hf = static_cast<float>(band.height);
     for (int k = 0; k < 3; ++k) {
@@ -2584,6 +2615,7 @@ BinParams BindBins(TraceParams& p, const CullBins& bins, std::uint64_t n) {
     b.width = p.width;
     b.row_count = p.row_count;
     b.row_begin = p.row_begin;
+    b.row_interleave = p.row_interleave;
     b.wf = p.wf;
     b.hf = p.hf;
     b.exp = p.exp;
@@ -2624,6 +2656,7 @@ hipError_t LaunchCullFrames(const CullFrame* frames, std::size_t count, std::uin
         const CullFrame& f = frames[i];
         if (f.bins == nullptr || f.edges == nullptr || f.bins->order == nullptr || f.band.width != band0.width ||
             f.band.row_count != band0.row_count || f.band.row_begin != band0.row_begin ||
+            f.band.row_interleave != band0.row_interleave ||
             f.band.height != band0.height || f.bins->max_chunks != frames[0].bins->max_chunks) {
             return hipErrorInvalidValue;  // one band shape per batch
         }
@@ -2714,9 +2747,31 @@ hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_ver
     return hipGetLastError();
 }
 
+bool BandFits(std::size_t row_begin, std::size_t row_count, std::size_t interleave, std::size_t height) {
+    if (interleave == 0 || row_begin > height) {
+        return false;
+    }
+    if (row_count == 0) {
+        return true;
+    }
+    if (interleave > 1 && row_begin % kCullTileRows != 0) {
+        return false;
+    }
+    return BandFrameRow(row_begin, interleave, row_count - 1) < height;  // earlier tile rows are full
+}
+
+std::size_t InterleavedBandRows(std::size_t height, std::size_t bands, std::size_t band) {
+    const std::size_t tiles = (height + kCullTileRows - 1) / kCullTileRows;
+    std::size_t rows = 0;
+    for (std::size_t t = band; t < tiles; t += bands) {
+        rows += std::min<std::size_t>(kCullTileRows, height - t * kCullTileRows);
+    }
+    return rows;
+}
+
 hipError_t LaunchShade(const float* d_vertices, const float* d_albedo, const float* d_edges, std::uint64_t n,
                        const Frame& frame, const float background[3], const BandArgs& band, hipStream_t stream,
-                       std::size_t frames, std::size_t band_rows) {
+                       std::size_t frames, std::size_t band_rows, std::size_t interleaved) {
     if (band.row_count == 0 || band.width == 0 || frames == 0) {
         return hipSuccess;
     }
@@ -2737,6 +2792,7 @@ hipError_t LaunchShade(const float* d_vertices, const float* d_albedo, const flo
     p.width = static_cast<int>(band.width);
     p.row_count = static_cast<int>(band.row_count);
     p.row_begin = static_cast<int>(band.row_begin);
+    p.row_interleave = static_cast<int>(band.row_interleave);
     p.wf = static_cast<float>(band.width);
     p.hf = static_cast<float>(band.height);
     for (int k = 0; k < 3; ++k) {
@@ -2748,7 +2804,7 @@ hipError_t LaunchShade(const float* d_vertices, const float* d_albedo, const flo
     const std::size_t pixels = band.width * band.row_count;
     hipLaunchKernelGGL(ShadeIdsKernel, dim3(static_cast<unsigned>((pixels + 255) / 256), static_cast<unsigned>(frames)),
                        dim3(256), 0, stream, p, static_cast<const int*>(band.ids), static_cast<unsigned>(band_rows),
-                       static_cast<unsigned>(frames));
+                       static_cast<unsigned>(frames), static_cast<unsigned>(interleaved));
     return hipGetLastError();
 }
 

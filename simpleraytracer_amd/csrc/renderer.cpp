@@ -253,9 +253,13 @@ void DeviceScene::NormalsIfStale(hipStream_t stream) const {
 }
 
 void DeviceScene::Shade(const float* d_offsets, const int* d_ids, float* d_rgba, std::size_t row_begin,
-                        std::size_t row_count, hipStream_t stream, std::size_t frames, std::size_t band_rows) const {
+                        std::size_t row_count, hipStream_t stream, std::size_t frames, std::size_t band_rows,
+                        std::size_t interleaved) const {
     if (m_width == 0) {
         throw std::runtime_error("Shade: Prepare() has not been called");
+    }
+    if (interleaved > 0 && (row_begin != 0 || band_rows < InterleavedBandRows(m_height, interleaved, 0))) {
+        throw std::runtime_error("Shade: interleaved bands cover the whole frame in band_rows-row buffers");
     }
     if (row_begin + row_count > m_height) {
         throw std::runtime_error("Shade: row band outside the frame");
@@ -269,7 +273,8 @@ void DeviceScene::Shade(const float* d_offsets, const int* d_ids, float* d_rgba,
     OrderAfterPrevious(stream);
     NormalsIfStale(stream);
     BandArgs band{d_offsets, d_rgba, m_width, m_height, row_begin, row_count, const_cast<int*>(d_ids)};
-    HipCheck(LaunchShade(m_vertices, m_albedo, m_edges, m_n, m_frame, m_background, band, stream, frames, band_rows),
+    HipCheck(LaunchShade(m_vertices, m_albedo, m_edges, m_n, m_frame, m_background, band, stream, frames, band_rows,
+                         interleaved),
              "shade kernel launch");
 }
 
@@ -325,11 +330,12 @@ void DeviceScene::EnsureEdgeSlots(std::size_t slots, hipStream_t stream) const {
 }
 
 void DeviceScene::TraceBatch(const float* const* d_offsets, float* const* d_rgba, int* const* d_ids, std::size_t frames,
-                             std::size_t row_begin, std::size_t row_count, int variant, hipStream_t stream) const {
+                             std::size_t row_begin, std::size_t row_count, int variant, hipStream_t stream,
+                             std::size_t row_interleave) const {
     if (m_width == 0) {
         throw std::runtime_error("TraceBatch: Prepare() has not been called");
     }
-    if (row_begin + row_count > m_height) {
+    if (!BandFits(row_begin, row_count, row_interleave, m_height)) {
         throw std::runtime_error("TraceBatch: row band outside the frame");
     }
     if (frames > static_cast<std::size_t>(kMaxBatch)) {
@@ -342,7 +348,7 @@ void DeviceScene::TraceBatch(const float* const* d_offsets, float* const* d_rgba
         for (std::size_t f = 0; f < frames; ++f) {  // frame by frame, each with its own record setup
             m_prepare_pending = true;
             Trace(d_offsets[f], d_rgba != nullptr ? d_rgba[f] : nullptr, row_begin, row_count, variant, stream,
-                  d_ids != nullptr ? d_ids[f] : nullptr);
+                  d_ids != nullptr ? d_ids[f] : nullptr, row_interleave);
         }
         return;
     }
@@ -361,23 +367,25 @@ void DeviceScene::TraceBatch(const float* const* d_offsets, float* const* d_rgba
         cf[f].edges = m_edges + f * floats;
         cf[f].bins = &bins[f];
         cf[f].band = BandArgs{d_offsets[f], d_rgba != nullptr ? d_rgba[f] : nullptr, m_width, m_height, row_begin,
-                              row_count, d_ids != nullptr ? d_ids[f] : nullptr};
+                              row_count, d_ids != nullptr ? d_ids[f] : nullptr, row_interleave};
     }
-    HipCheck(LaunchCullFrames(cf, frames, m_n, m_vertices, m_albedo, m_frame, m_background, m_rank, stream, nullptr),
+    const StageEvents ev = BindStageEvents(true, true);
+    HipCheck(LaunchCullFrames(cf, frames, m_n, m_vertices, m_albedo, m_frame, m_background, m_rank, stream,
+                              m_timing ? &ev : nullptr),
              "batched trace launch");
     m_normals_current = true;  // slot 0's normals (the tile-planar records are the full pass's)
 }
 
 void DeviceScene::Trace(const float* d_offsets, float* d_rgba, std::size_t row_begin, std::size_t row_count,
-                        int variant, hipStream_t stream, int* d_ids) const {
+                        int variant, hipStream_t stream, int* d_ids, std::size_t row_interleave) const {
     if (m_width == 0) {
         throw std::runtime_error("Trace: Prepare() has not been called");
     }
-    if (row_begin + row_count > m_height) {
+    if (!BandFits(row_begin, row_count, row_interleave, m_height)) {
         throw std::runtime_error("Trace: row band outside the frame");
     }
     OrderAfterPrevious(stream);
-    BandArgs band{d_offsets, d_rgba, m_width, m_height, row_begin, row_count, d_ids};
+    BandArgs band{d_offsets, d_rgba, m_width, m_height, row_begin, row_count, d_ids, row_interleave};
     CullBins bins{};
     const CullBins* use_bins = nullptr;
     if (variant == kTraceCull && row_count != 0 && CullBinningEnabled() && CullBinnable(m_width, row_count)) {
@@ -391,25 +399,8 @@ void DeviceScene::Trace(const float* d_offsets, float* d_rgba, std::size_t row_b
     // The full record pass for every path but the binned cull one, which computes its records in
     // its bin kernel (its "prepare" stage is the tile-info kernel).
     const bool prepare = use_bins == nullptr && m_prepare_pending && row_count != 0;
-    StageEvents ev{};
-    if (m_timing && (prepare || (use_bins != nullptr && row_count != 0))) {
-        ev.prep_begin = TimingEvent(m_prep_events, 2 * m_prep_timed);
-        ev.prep_end = TimingEvent(m_prep_events, 2 * m_prep_timed + 1);
-        ++m_prep_timed;
-    }
-    if (m_timing) {
-        const std::size_t k = 4 * m_timed;
-        const bool staged = use_bins != nullptr || (variant == kTraceBvh && m_n != 0);
-        ev.bin_begin = staged ? TimingEvent(m_events, k) : nullptr;
-        ev.bin_end = staged ? TimingEvent(m_events, k + 1) : nullptr;
-        ev.begin = TimingEvent(m_events, k + 2);
-        ev.end = TimingEvent(m_events, k + 3);
-        if (m_binned.size() <= m_timed) {
-            m_binned.resize(m_timed + 1);
-        }
-        m_binned[m_timed] = staged;
-        ++m_timed;
-    }
+    const StageEvents ev = BindStageEvents(prepare || (use_bins != nullptr && row_count != 0),
+                                           use_bins != nullptr || (variant == kTraceBvh && m_n != 0));
     HipCheck(LaunchTrace(m_edges, m_n, m_vertices, m_albedo, m_frame, m_background, band, variant, use_bins, stream,
                          m_timing ? &ev : nullptr, prepare ? m_rank : nullptr, m_bvh),
              "trace kernel launch");
@@ -420,6 +411,30 @@ void DeviceScene::Trace(const float* d_offsets, float* d_rgba, std::size_t row_b
     if (use_bins != nullptr && row_count != 0) {
         m_normals_current = true;
     }
+}
+
+// With stage timing on: events for one traced call (a batch counts as one call).
+StageEvents DeviceScene::BindStageEvents(bool prep, bool staged) const {
+    StageEvents ev{};
+    if (!m_timing) {
+        return ev;
+    }
+    if (prep) {
+        ev.prep_begin = TimingEvent(m_prep_events, 2 * m_prep_timed);
+        ev.prep_end = TimingEvent(m_prep_events, 2 * m_prep_timed + 1);
+        ++m_prep_timed;
+    }
+    const std::size_t k = 4 * m_timed;
+    ev.bin_begin = staged ? TimingEvent(m_events, k) : nullptr;
+    ev.bin_end = staged ? TimingEvent(m_events, k + 1) : nullptr;
+    ev.begin = TimingEvent(m_events, k + 2);
+    ev.end = TimingEvent(m_events, k + 3);
+    if (m_binned.size() <= m_timed) {
+        m_binned.resize(m_timed + 1);
+    }
+    m_binned[m_timed] = staged;
+    ++m_timed;
+    return ev;
 }
 
 hipEvent_t DeviceScene::TimingEvent(std::vector<hipEvent_t>& pool, std::size_t i) const {

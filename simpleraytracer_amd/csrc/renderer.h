@@ -17,7 +17,8 @@
 
 namespace srt {
 
-struct CullBins;  // render.h
+struct CullBins;     // render.h
+struct StageEvents;  // render.h
 
 // Throws std::runtime_error("HIP error: <what>: <reason>") on failure.
 void HipCheck(hipError_t err, const char* what);
@@ -44,21 +45,25 @@ public:
     void Prepare(std::size_t width, std::size_t height, hipStream_t stream);
     // Trace rows [row_begin, row_begin + row_count) of the prepared frame into RGBA, or (d_ids
     // non-null, d_rgba ignored) into hit ids for deferred shading.
+    // row_interleave > 1: the band deals the frame's tile rows round-robin (render.h BandArgs).
     void Trace(const float* d_offsets, float* d_rgba, std::size_t row_begin, std::size_t row_count, int variant,
-               hipStream_t stream, int* d_ids = nullptr) const;
+               hipStream_t stream, int* d_ids = nullptr, std::size_t row_interleave = 1) const;
     // Deferred shading of rows [row_begin, row_begin + row_count) of the prepared frame from hit
     // ids (as Trace writes them) and sample offsets: the RGBA the fused trace would store.
     // frames > 1: a batch of that many frames of this camera, ids band-major as a gather of
     // band_rows-row bands leaves them (render.h LaunchShade), rgba [frames][row_count][width].
+    // interleaved > 0: the gathered bands are that many interleaved bands.
     void Shade(const float* d_offsets, const int* d_ids, float* d_rgba, std::size_t row_begin, std::size_t row_count,
-               hipStream_t stream, std::size_t frames = 1, std::size_t band_rows = 0) const;
+               hipStream_t stream, std::size_t frames = 1, std::size_t band_rows = 0,
+               std::size_t interleaved = 0) const;
     // `frames` (<= kMaxBatch) frames of the prepared camera, rows [row_begin, row_begin +
     // row_count) each: frame f's offsets d_offsets[f], its RGBA d_rgba[f] or (d_ids non-null) its
     // hit ids d_ids[f]. Each frame gets the whole per-frame pipeline (record setup, bins, work
     // list, trace), as `frames` Prepare + Trace calls would; the cull variant runs all frames in
     // one launch per stage (render.h LaunchCullFrames), the others frame by frame.
     void TraceBatch(const float* const* d_offsets, float* const* d_rgba, int* const* d_ids, std::size_t frames,
-                    std::size_t row_begin, std::size_t row_count, int variant, hipStream_t stream) const;
+                    std::size_t row_begin, std::size_t row_count, int variant, hipStream_t stream,
+                    std::size_t row_interleave = 1) const;
 
     std::size_t width() const { return m_width; }
     // The spatial order (device, triangles entries) and the time its build took at load (ms).
@@ -111,6 +116,7 @@ private:
     // Stage-timing events, reused: per timed Prepare (begin, end), per timed Trace (bin begin,
     // bin end, begin, end); the first m_prep_timed / m_timed entries hold pending launches.
     hipEvent_t TimingEvent(std::vector<hipEvent_t>& pool, std::size_t i) const;
+    StageEvents BindStageEvents(bool prep, bool staged) const;
     bool m_timing = false;
     // Calls on one scene are stream-ordered: the per-frame edge records and the cull work buffer
     // are shared state, so a call on another stream than the previous one first waits for it.

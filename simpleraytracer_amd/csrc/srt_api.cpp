@@ -243,10 +243,11 @@ ML_API_ENTRY int srtTraceIdsAsync(srt_device_scene scene, const float* d_offsets
 }
 
 static_assert(SRT_MAX_BATCH == srt::kMaxBatch, "include/srt_render.h SRT_MAX_BATCH");
+static_assert(SRT_TILE_ROWS == srt::kCullTileRows, "include/srt_render.h SRT_TILE_ROWS");
 
 ML_API_ENTRY int srtTraceBatchAsync(srt_device_scene scene, const float* const* d_offsets, float* const* d_rgba,
-                                    int* const* d_ids, size_t frames, size_t row_begin, size_t row_count, int variant,
-                                    void* stream) {
+                                    int* const* d_ids, size_t frames, size_t row_begin, size_t row_count,
+                                    size_t row_interleave, int variant, void* stream) {
     return Guarded([&] {
         if (scene == nullptr) {
             throw std::runtime_error("Bad scene handle");
@@ -270,7 +271,8 @@ ML_API_ENTRY int srtTraceBatchAsync(srt_device_scene scene, const float* const* 
         }
         srt::DeviceScene* s = FromHandle(scene);
         Bind bind(s->device());
-        s->TraceBatch(d_offsets, d_rgba, d_ids, frames, row_begin, row_count, variant, static_cast<hipStream_t>(stream));
+        s->TraceBatch(d_offsets, d_rgba, d_ids, frames, row_begin, row_count, variant, static_cast<hipStream_t>(stream),
+                      row_interleave);
     });
 }
 
@@ -290,7 +292,7 @@ ML_API_ENTRY int srtShadeAsync(srt_device_scene scene, const float* d_offsets, c
 }
 
 ML_API_ENTRY int srtShadeBandsAsync(srt_device_scene scene, const float* d_offsets, const int* d_ids, float* d_rgba,
-                                    size_t frames, size_t band_rows, void* stream) {
+                                    size_t frames, size_t band_rows, size_t interleaved, void* stream) {
     return Guarded([&] {
         if (scene == nullptr) {
             throw std::runtime_error("Bad scene handle");
@@ -303,7 +305,8 @@ ML_API_ENTRY int srtShadeBandsAsync(srt_device_scene scene, const float* d_offse
         }
         srt::DeviceScene* s = FromHandle(scene);
         Bind bind(s->device());
-        s->Shade(d_offsets, d_ids, d_rgba, 0, s->height(), static_cast<hipStream_t>(stream), frames, band_rows);
+        s->Shade(d_offsets, d_ids, d_rgba, 0, s->height(), static_cast<hipStream_t>(stream), frames, band_rows,
+                 interleaved);
     });
 }
 

@@ -172,12 +172,14 @@ class DeviceScene:
         return run
 
     def bind_trace_batch(self, offsets, outs, row_begin: int = 0, row_count: int | None = None, variant: str = "cull",
-                         stream=None, ids: bool = False):
+                         stream=None, ids: bool = False, row_interleave: int = 1):
         """prepare + trace of len(outs) (<= MAX_BATCH) frames of this band as a zero-argument
         callable (srtTraceBatchAsync): frame f's sample offsets offsets[f] ((rows, W, 2) float32)
         and its output outs[f] ((rows, W) int32 hit ids with ids=True, else (rows, W, 4) float32
         RGBA). Every frame gets the whole per-frame work; the cull variant launches each stage
-        once for the batch. Checked once here; the buffers must stay alive while it is used."""
+        once for the batch. row_interleave P > 1: the band is tile rows row_begin / 32 + k P of
+        the frame (bands.interleaved_range). Checked once here; the buffers must stay alive
+        while it is used."""
         if row_count is None:
             row_count = self.height - row_begin
         frames = len(outs)
@@ -195,15 +197,15 @@ class DeviceScene:
 
         def run():
             _check(lib.srtPrepareAsync(h, w, hh, s))
-            _check(lib.srtTraceBatchAsync(h, offs, rgba, idp, frames, row_begin, row_count, v, s))
+            _check(lib.srtTraceBatchAsync(h, offs, rgba, idp, frames, row_begin, row_count, row_interleave, v, s))
 
         run.keep = (offsets, outs, offs, out)  # the pointer arrays live as long as the callable
         return run
 
     def trace_batch(self, offsets, outs, row_begin: int = 0, row_count: int | None = None, variant: str = "cull",
-                    stream=None, ids: bool = False):
+                    stream=None, ids: bool = False, row_interleave: int = 1):
         """One batched call (bind_trace_batch) run once."""
-        self.bind_trace_batch(offsets, outs, row_begin, row_count, variant, stream, ids)()
+        self.bind_trace_batch(offsets, outs, row_begin, row_count, variant, stream, ids, row_interleave)()
 
     def shade(self, offsets, ids, rgba, row_begin: int = 0, row_count: int | None = None, stream=None):
         """Deferred shading of the prepared frame's rows from hit ids: the RGBA trace() stores."""
@@ -215,13 +217,14 @@ class DeviceScene:
         _check(self._lib.srtShadeAsync(self.handle, _ptr(offsets), _ptr(ids), _ptr(rgba), row_begin, row_count,
                                        _stream(stream)))
 
-    def shade_bands(self, offsets, ids, rgba, band_rows: int, stream=None):
+    def shade_bands(self, offsets, ids, rgba, band_rows: int, stream=None, interleaved: int = 0):
         """Deferred shading of a batch of frames whose ids were gathered band-major:
-        ids (bands, frames, band_rows, W) int32 (bands = ceil(H / band_rows)), offsets (H, W, 2),
+        ids (bands, frames, band_rows, W) int32 (bands = ceil(H / band_rows) contiguous bands, or
+        `interleaved` bands dealt the frame's tile rows round-robin), offsets (H, W, 2),
         rgba (frames, H, W, 4); one launch (srtShadeBandsAsync)."""
         if band_rows <= 0:
             raise ValueError("band_rows must be positive")
-        bands = (self.height + band_rows - 1) // band_rows
+        bands = interleaved if interleaved else (self.height + band_rows - 1) // band_rows
         frames = ids.shape[1] if hasattr(ids, "shape") and len(ids.shape) == 4 else 0
         self._check_buffer("offsets", offsets, self.height, 2, "f32")
         if hasattr(ids, "shape") and tuple(ids.shape) != (bands, frames, band_rows, self.width):
@@ -231,7 +234,7 @@ class DeviceScene:
         for name, buf, dtype in (("ids", ids, "i32"), ("rgba", rgba, "f32")):
             self._check_tensor(name, buf, dtype)
         _check(self._lib.srtShadeBandsAsync(self.handle, _ptr(offsets), _ptr(ids), _ptr(rgba), frames, band_rows,
-                                            _stream(stream)))
+                                            interleaved, _stream(stream)))
 
     def spatial_order(self):
         """(order, build_ms): the record ids in spatial order (numpy uint32), built on the device

@@ -219,6 +219,99 @@ def test_band_major_layout_matches_concatenation():
         assert np.array_equal(band_major_frame(ids, g, 13), want)
 
 
+@pytest.mark.parametrize("h", [1, 31, 32, 33, 170, 1080, 2160])
+@pytest.mark.parametrize("p", [1, 2, 3, 4, 8, 40])
+def test_interleaved_partition_covers_frame_once(h, p):
+    from simpleraytracer_amd.bands import interleaved_band_rows, interleaved_frame_rows, interleaved_range
+
+    rows = np.concatenate([interleaved_frame_rows(h, p, r) for r in range(p)])
+    assert np.array_equal(np.sort(rows), np.arange(h))
+    for r in range(p):
+        begin, count = interleaved_range(h, p, r)
+        fr = interleaved_frame_rows(h, p, r)
+        assert count == len(fr) <= interleaved_band_rows(h, p)
+        if count:
+            assert begin == r * 32 == fr[0]
+            local = np.arange(count)  # the kernels' FrameRow(row_begin, P, local)
+            assert np.array_equal(begin + local + local // 32 * 32 * (p - 1), fr)
+
+
+def interleaved_frame(ids, g, height):
+    """Frame g of a band-major batch of interleaved bands, by ShadeIdsKernel's interleaved index
+    expression (render.hip): t = y / 32, band = t % P, local = (t / P) * 32 + y % 32."""
+    bands, frames, b, w = ids.shape
+    y = np.arange(height)
+    t = y // 32
+    band, local = t % bands, t // bands * 32 + y % 32
+    return np.asarray(ids)[band, g, local]
+
+
+def test_interleaved_layout_matches_partition():
+    from simpleraytracer_amd.bands import interleaved_band_rows, interleaved_frame_rows
+
+    h, w, p, frames = 170, 5, 3, 2
+    frame = np.arange(frames * h * w).reshape(frames, h, w)
+    b = interleaved_band_rows(h, p)
+    ids = np.full((p, frames, b, w), -1)
+    for r in range(p):
+        fr = interleaved_frame_rows(h, p, r)
+        ids[r, :, :len(fr)] = frame[:, fr]
+    for g in range(frames):
+        assert np.array_equal(interleaved_frame(ids, g, h), frame[g])
+
+
+def _interleaved_worker(rank, world, port, scene_path, w, h, frames, out_dir):
+    """Interleaved bands over gloo: rank r renders its tile rows (oracle, tile row by tile row)
+    of `frames` frames into an (F, B, W) id batch; one gather; rank 0 shades every frame from the
+    band-major interleaved layout."""
+    import torch
+    import torch.distributed as dist
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, repo)
+    from oracle.srt_oracle import OracleScene
+    from simpleraytracer_amd.bands import gather_band_batch, interleaved_band_rows, interleaved_frame_rows
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    oracle = OracleScene(scene_path)
+    fr = interleaved_frame_rows(h, world, rank)
+    B = interleaved_band_rows(h, world)
+    batch = torch.full((frames, B, w), -5, dtype=torch.int32)
+    offs = [np.random.default_rng(3000 + f).random((h, w, 2), dtype=np.float32) for f in range(frames)]
+    for f in range(frames):
+        for k in range(0, len(fr), 32):  # one tile row (contiguous frame rows) at a time
+            r0, n = int(fr[k]), min(32, len(fr) - k)
+            img = oracle.render(w, h, offs[f], row_begin=r0, row_count=n, threads=1)
+            batch[f, k:k + n] = torch.from_numpy(img[r0:r0 + n, :, 3].astype(np.int32))
+    ids, work = gather_band_batch(batch, h, dst=0, async_op=True, interleaved=True)
+    work.wait()
+    if rank == 0:
+        for f in range(frames):
+            np.save(os.path.join(out_dir, f"frame{f}.npy"),
+                    oracle.shade(w, h, interleaved_frame(ids.numpy(), f, h).astype(np.int32), offs[f]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,wh", [(2, (40, 70)), (3, (33, 100))])
+def test_gloo_interleaved_batch(scenes, tmp_path, world, wh):
+    """Interleaved bands (tile rows dealt round-robin), one gather per batch: every frame shaded
+    from the gathered layout equals the single-process frame bit for bit."""
+    import torch.multiprocessing as mp
+
+    from oracle.srt_oracle import OracleScene
+
+    w, h = wh
+    mp.start_processes(_interleaved_worker, args=(world, _free_port(), scenes["soup300"], w, h, 2, str(tmp_path)),
+                       nprocs=world, join=True, start_method="spawn")
+    oracle = OracleScene(scenes["soup300"])
+    for f in range(2):
+        offs = np.random.default_rng(3000 + f).random((h, w, 2), dtype=np.float32)
+        got = np.load(tmp_path / f"frame{f}.npy")
+        assert np.array_equal(got.view(np.uint32), oracle.render(w, h, offs).view(np.uint32)), f
+
+
 def test_compositor_rotation():
     from simpleraytracer_amd.bands import compositor
 

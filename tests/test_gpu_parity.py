@@ -755,6 +755,50 @@ def test_trace_batch_c3_band_of_8(gpu, scenes):
     scene.close()
 
 
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
+@pytest.mark.parametrize("mode", [CULL_MODES[0], CULL_MODES[3]])
+def test_interleaved_bands_bitwise(gpu, scenes, monkeypatch, world, mode):
+    """Interleaved bands (the frame's 32-row tile rows dealt round-robin, row_interleave = P):
+    every rank's batched trace of its rows (hit ids and RGBA), then the gathered band-major ids
+    shaded with the interleaved layout (srtShadeBandsAsync), equal the brute-force frame bit for
+    bit; 170 rows leave a partial last tile row; forced list overflow streams records in a band."""
+    import torch
+
+    import simpleraytracer_amd as srt
+    from simpleraytracer_amd.bands import interleaved_band_rows, interleaved_frame_rows, interleaved_range
+
+    set_cull_mode(monkeypatch, mode)
+    w, h, frames = 333, 170, 2
+    offs = np.random.default_rng(53).random((h, w, 2), dtype=np.float32)
+    ref = torch_render(scenes["soup2k"], w, h, offs, variant="lds")
+    off = torch.from_numpy(offs).cuda()
+    stream = torch.cuda.current_stream()
+    b = interleaved_band_rows(h, world)
+    gathered = torch.full((world, frames, b, w), 2 ** 30, dtype=torch.int32, device="cuda")
+    scene = srt.DeviceScene(scenes["soup2k"], 0)
+    scene.prepare(w, h, stream)
+    for r in range(world):
+        r0, rows = interleaved_range(h, world, r)
+        fr = interleaved_frame_rows(h, world, r)
+        if rows == 0:
+            continue
+        band_off = off.index_select(0, torch.from_numpy(fr).cuda()).contiguous()
+        scene.trace_batch([band_off] * frames, [gathered[r, f, :rows] for f in range(frames)], r0, rows,
+                          stream=stream, ids=True, row_interleave=world)
+        rgba = torch.empty((rows, w, 4), dtype=torch.float32, device="cuda")
+        scene.trace_batch([band_off], [rgba], r0, rows, stream=stream, row_interleave=world)
+        torch.cuda.synchronize()
+        assert np.array_equal(rgba.cpu().numpy().view(np.uint32), ref[fr].view(np.uint32)), r
+    out = torch.full((frames, h, w, 4), float("nan"), dtype=torch.float32, device="cuda")
+    scene.shade_bands(off, gathered, out, b, stream=stream, interleaved=world)
+    torch.cuda.synchronize()
+    for f in range(frames):
+        assert np.array_equal(out[f].cpu().numpy().view(np.uint32), ref.view(np.uint32)), f
+    with pytest.raises(srt.SrtError):  # an interleaved band must start on a tile row
+        scene.trace_batch([off[:1]], [out[0, :1]], 1, 1, stream=stream, row_interleave=2)
+    scene.close()
+
+
 def test_scene_calls_on_two_streams_are_ordered(gpu, scenes):
     """One scene used from two streams (bands on alternating streams, a new prepare in between):
     the library orders the calls, so every frame equals its single-stream render."""

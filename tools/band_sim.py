@@ -34,11 +34,13 @@ def main():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--triangles", type=int, default=100_000)
     ap.add_argument("--batch", type=int, default=8, help="frames per launch / per gather (bench.py --batch)")
+    ap.add_argument("--rows", default="interleaved", choices=["interleaved", "contiguous"], help="bench.py --rows")
     a = ap.parse_args()
     import torch
 
     import simpleraytracer_amd as srt
-    from simpleraytracer_amd.bands import band_range, band_rows
+    from simpleraytracer_amd.bands import (band_range, band_rows, interleaved_band_rows, interleaved_frame_rows,
+                                           interleaved_range)
 
     W, H, G = a.width, a.height, max(1, min(a.batch, srt.MAX_BATCH))
     dev = torch.device("cuda", 0)
@@ -57,31 +59,35 @@ def main():
            "rgba": torch.empty((G, H, W, 4), dtype=torch.float32, device=dev)} for _ in range(a.queues)]
     for q in qs:
         q["scene"].prepare(W, H)
-    out = {"workload": f"soup-{a.triangles} {W}x{H}", "queues": a.queues, "batch": G, "ranks": {}}
+    out = {"workload": f"soup-{a.triangles} {W}x{H}", "queues": a.queues, "batch": G, "rows": a.rows, "ranks": {}}
     for P in [int(x) for x in a.ranks.split(",")]:
         per = []
-        B = band_rows(H, P)
+        inter = P if (P > 1 and a.rows == "interleaved") else 0
+        B = interleaved_band_rows(H, P) if inter else band_rows(H, P)
         gathered = torch.full((P, G, B, W), -1, dtype=torch.int32, device=dev)  # band-major, as gathered
+        band_rows_of = []
         for p in range(P):
-            b0, c = band_range(H, P, p)
-            gathered[p, :, :c] = frame_ids[b0:b0 + c]
+            fr = torch.from_numpy(interleaved_frame_rows(H, P, p)).to(dev) if inter else None
+            b0, c = interleaved_range(H, P, p) if inter else band_range(H, P, p)
+            gathered[p, :, :c] = frame_ids.index_select(0, fr) if inter else frame_ids[b0:b0 + c]
+            band_rows_of.append((b0, c, off.index_select(0, fr).contiguous() if inter else off[b0:b0 + c]))
         for r in range(P):
-            r0, rows = band_range(H, P, r)
+            r0, rows, band_off = band_rows_of[r]
             for q in qs:
                 if P == 1:
                     q["run"] = q["scene"].bind_trace_batch([off] * G, [q["rgba"][j] for j in range(G)], 0, H,
                                                            stream=q["stream"])
                 else:
-                    q["run"] = q["scene"].bind_trace_batch([off[r0:r0 + rows]] * G,
-                                                           [q["ids"][j, :rows] for j in range(G)], r0, rows,
-                                                           stream=q["stream"], ids=True) if rows else None
+                    q["run"] = q["scene"].bind_trace_batch([band_off] * G, [q["ids"][j, :rows] for j in range(G)],
+                                                           r0, rows, stream=q["stream"], ids=True,
+                                                           row_interleave=max(1, inter)) if rows else None
 
             def step(k):  # batch k: G frames
                 q = qs[k % a.queues]
                 if q["run"] is not None:
                     q["run"]()
                 if P > 1 and k % P == r:  # this rank composites batch k
-                    q["scene"].shade_bands(off, gathered, q["rgba"], B, stream=q["stream"])
+                    q["scene"].shade_bands(off, gathered, q["rgba"], B, stream=q["stream"], interleaved=inter)
 
             batches = max(1, a.steps // G)
             for k in range(max(2, a.warmup // G) * a.queues):
