@@ -74,8 +74,8 @@ def parse():
     p.add_argument("--queues", type=int, default=int(os.environ.get("SRT_BENCH_QUEUES", "3")),
                    help="frames in flight per GPU (own scene buffers, HIP stream, process group each)")
     p.add_argument("--batch", type=int, default=int(os.environ.get("SRT_BENCH_BATCH", "0")),
-                   help="frames per launch (srtTraceBatchAsync, <= 8) and, bands at N > 1, per gather and "
-                        "shading launch; 0 = 8 at N > 1, 1 at N = 1")
+                   help="frames per batch: traced in srtTraceBatchAsync calls of <= 8 frames and, bands at "
+                        "N > 1, gathered in one collective and shaded in one launch; 0 = 16 at N > 1, 1 at N = 1")
     p.add_argument("--offsets", default="uniform", choices=["uniform", "random"],
                    help="sample offsets: uniform 0.5 (headline) or seeded U[0,1) per-pixel jitter")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample length")
@@ -181,7 +181,8 @@ class Pipeline:
         self.W, self.H = a.width, a.height
         P = ctx.world if mode == "bands" else 1
         self.P = P
-        self.G = max(1, min(batch, ctx.srt.MAX_BATCH))  # frames per launch (and per gather at P > 1)
+        self.G = max(1, batch)  # frames per batch: per gather + shading launch at P > 1
+        self.L = min(self.G, ctx.srt.MAX_BATCH)  # frames per batched trace call
         self.interleave = P if (P > 1 and rows == "interleaved") else 1
         if self.interleave > 1:
             self.row_begin, self.row_count = interleaved_range(self.H, P, ctx.rank)
@@ -250,7 +251,8 @@ class Pipeline:
             return
         sc, st = q["scene"], q["stream"]
         if q["traced"] < f and self.row_count:
-            self._batch_run(q, f)()
+            for slot in range(0, f, self.L):
+                self._batch_run(q, min(self.L, f - slot), slot)()
         q["fill"] = q["traced"] = 0
         if self.P == 1:
             q["root"], q["shaded"] = 0, f
@@ -461,7 +463,7 @@ def leg_summary(r):
 def main():
     a = parse()
     if a.batch <= 0:
-        a.batch = 8 if a.gpus > 1 else 1
+        a.batch = 16 if a.gpus > 1 else 1
     ctx = Ctx(a)
     world, rank = ctx.world, ctx.rank
     path = ctx.scene_path(a.scene, a.triangles if a.scene == "soup" else None)
@@ -561,7 +563,8 @@ def main():
                 "parallelism": par,
                 "trace_variant": a.variant,
                 "frame_queues": r["queues"],
-                "frames_per_launch": main_run.G,
+                "frames_per_launch": main_run.L,
+                "frames_per_batch": main_run.G,
                 "offsets": a.offsets,
             },
             "roofline": roof,

@@ -33,7 +33,7 @@ def main():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--triangles", type=int, default=100_000)
-    ap.add_argument("--batch", type=int, default=8, help="frames per launch / per gather (bench.py --batch)")
+    ap.add_argument("--batch", type=int, default=16, help="frames per gather / shading launch (bench.py --batch)")
     ap.add_argument("--rows", default="interleaved", choices=["interleaved", "contiguous"], help="bench.py --rows")
     a = ap.parse_args()
     import torch
@@ -42,7 +42,8 @@ def main():
     from simpleraytracer_amd.bands import (band_range, band_rows, interleaved_band_rows, interleaved_frame_rows,
                                            interleaved_range)
 
-    W, H, G = a.width, a.height, max(1, min(a.batch, srt.MAX_BATCH))
+    W, H, G = a.width, a.height, max(1, a.batch)
+    L = min(G, srt.MAX_BATCH)  # frames per batched trace call
     dev = torch.device("cuda", 0)
     tmp = tempfile.TemporaryDirectory()
     path = srt.write_scene(os.path.join(tmp.name, "soup.srt"), "soup", a.triangles)
@@ -74,18 +75,22 @@ def main():
         for r in range(P):
             r0, rows, band_off = band_rows_of[r]
             for q in qs:
-                if P == 1:
-                    q["run"] = q["scene"].bind_trace_batch([off] * G, [q["rgba"][j] for j in range(G)], 0, H,
-                                                           stream=q["stream"])
-                else:
-                    q["run"] = q["scene"].bind_trace_batch([band_off] * G, [q["ids"][j, :rows] for j in range(G)],
-                                                           r0, rows, stream=q["stream"], ids=True,
-                                                           row_interleave=max(1, inter)) if rows else None
+                q["runs"] = []
+                for s0 in range(0, G, L):
+                    n = min(L, G - s0)
+                    if P == 1:
+                        q["runs"].append(q["scene"].bind_trace_batch([off] * n, [q["rgba"][j] for j in range(s0, s0 + n)],
+                                                                     0, H, stream=q["stream"]))
+                    elif rows:
+                        q["runs"].append(q["scene"].bind_trace_batch([band_off] * n,
+                                                                     [q["ids"][j, :rows] for j in range(s0, s0 + n)],
+                                                                     r0, rows, stream=q["stream"], ids=True,
+                                                                     row_interleave=max(1, inter)))
 
             def step(k):  # batch k: G frames
                 q = qs[k % a.queues]
-                if q["run"] is not None:
-                    q["run"]()
+                for run in q["runs"]:
+                    run()
                 if P > 1 and k % P == r:  # this rank composites batch k
                     q["scene"].shade_bands(off, gathered, q["rgba"], B, stream=q["stream"], interleaved=inter)
 

@@ -27,7 +27,7 @@ if [[ $STEPS == *rehearse* ]]; then
             --warmup 2 --no-extras
     done
     run band_sim 300 python tools/band_sim.py
-    run band_sim_b1 300 python tools/band_sim.py --batch 1
+    run band_sim_b8 300 python tools/band_sim.py --batch 8
 fi
 if [[ $STEPS == *host* ]]; then
     run host_bands 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
