@@ -4,25 +4,26 @@
     python bench.py [--gpus N --steps K --warmup W]        (N > 1: launched by torch.distributed.run)
 
 One step = one complete frame of the hot path on device-resident inputs (SURVEY.md section 8
-rows a9-a13): edge-record setup (prepare kernel), the cull bins (tile bounds / bin / work-list
-kernels), the closest-hit trace (TraceCullKernel; its frame is bit-identical to brute force,
-DESIGN.md section 5, tests/test_gpu_parity.py), shading and the framebuffer store. Nothing is
-cached across frames.
+rows a9-a13): tile info, record setup and bins, the trace work list, the closest-hit trace
+(TraceCullKernel; its frame is bit-identical to brute force, DESIGN.md section 5,
+tests/test_gpu_parity.py), shading and the framebuffer store. Nothing is cached across frames.
+
+Each GPU keeps --queues (3) frame queues, each its own DeviceScene, HIP stream and buffers, and a
+queue takes --batch frames at a time: up to 8 of them go through one srtTraceBatchAsync call (the
+same per-frame work, one launch per stage for the batch). N = 1: batches of 8 frames, each frame
+shaded into its own RGBA framebuffer; the single_queue pass runs one frame per launch on one
+queue (the per-frame latency).
 
 Multi-GPU, one rank per GPU over RCCL:
-  --mode bands (default; BASELINE config C4): every frame is tiled into P row bands, rank r
-      traces band r, the bands are gathered over RCCL to the frame's compositing rank, which
-      shades and stores the whole frame. The gather moves each band's hit ids (int32, 4 B per
-      pixel; deferred shading, bit-identical); the compositor is rank k % P for frame k
-      (--root rotate, default) or rank 0 (--root fixed). Each rank keeps --queues frames in
-      flight: queue q = its own DeviceScene (edge records, bins), HIP stream, band / frame
-      buffers and RCCL process group, so one frame's setup, trace, gather and shading overlap
-      the others'. A queue gathers --batch frames' bands in ONE collective (a torch-RCCL gather
-      costs ~44 us of host time per call, more than a band's trace: tools/host_probe_bands.py)
-      and the compositor shades the batch in one launch (srtShadeBandsAsync); the compositor
-      rotates per batch. value = frames x W x H / the max-over-ranks time: "scaling": "strong".
-      After the timed loop every compositing rank compares its last batch's frames with a
-      one-GPU render of the same frame bit for bit ("verified").
+  --mode bands (default; BASELINE config C4): every frame is split into P bands -- the frame's
+      32-row tile rows dealt round-robin (--rows interleaved, default) or contiguous blocks --,
+      rank r traces its band (hit ids, 4 B per pixel; deferred shading, bit-identical), a batch
+      of 16 frames' bands is gathered over RCCL in ONE collective (a torch-RCCL gather costs
+      ~40 us of host time per call, more than a band's trace: tools/host_probe_bands.py) to
+      the batch's compositor, rank (batch index) % P (--root rotate, default) or rank 0 (--root
+      fixed), which shades the 16 frames in one launch (srtShadeBandsAsync). value = frames x W x
+      H / the max-over-ranks time: "scaling": "strong". After the timed loop every compositing
+      rank compares its last batch's frames with a one-GPU render bit for bit ("verified").
   --mode frames: every rank renders whole frames of a temporal-jitter sequence (no collective);
       "scaling": "weak". Reported beside the bands line at N > 1 ("frames").
 At N = 1 the two modes coincide (one band = the frame, shaded in the trace).
@@ -75,7 +76,7 @@ def parse():
                    help="frames in flight per GPU (own scene buffers, HIP stream, process group each)")
     p.add_argument("--batch", type=int, default=int(os.environ.get("SRT_BENCH_BATCH", "0")),
                    help="frames per batch: traced in srtTraceBatchAsync calls of <= 8 frames and, bands at "
-                        "N > 1, gathered in one collective and shaded in one launch; 0 = 16 at N > 1, 1 at N = 1")
+                        "N > 1, gathered in one collective and shaded in one launch; 0 = 16 at N > 1, 8 at N = 1")
     p.add_argument("--offsets", default="uniform", choices=["uniform", "random"],
                    help="sample offsets: uniform 0.5 (headline) or seeded U[0,1) per-pixel jitter")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample length")
@@ -287,9 +288,19 @@ class Pipeline:
         for q in self.queues:
             q["stream"].synchronize()
 
-    def run(self, steps, warmup, queues=None, timing=False):
+    def run(self, steps, warmup, queues=None, timing=False, batch=None):
         """`steps` timed frames after `warmup` per queue; stage timing binds events on queue 0's
-        scene (use queues=1 then)."""
+        scene (use queues=1 then); `batch` (<= the pipeline's) overrides the frames per batch."""
+        G, L = self.G, self.L
+        if batch:
+            self.G = min(batch, G)
+            self.L = min(self.G, L)
+        try:
+            return self._run(steps, warmup, queues, timing)
+        finally:
+            self.G, self.L = G, L
+
+    def _run(self, steps, warmup, queues, timing):
         torch, ctx = self.ctx.torch, self.ctx
         nq = min(queues or len(self.queues), len(self.queues))
         for k in range(warmup * nq):
@@ -463,7 +474,7 @@ def leg_summary(r):
 def main():
     a = parse()
     if a.batch <= 0:
-        a.batch = 16 if a.gpus > 1 else 1
+        a.batch = 16 if a.gpus > 1 else 8
     ctx = Ctx(a)
     world, rank = ctx.world, ctx.rank
     path = ctx.scene_path(a.scene, a.triangles if a.scene == "soup" else None)
@@ -478,7 +489,8 @@ def main():
     # frame in flight (per-frame latency), then the same with HIP events bound to the kernels'
     # dispatch packets for the stage times (each event-bound dispatch leaves a 5-10 us bubble,
     # so that pass is slower; its kernel durations are not inflated by frame overlap).
-    r1 = main_run.run(a.steps, a.warmup, queues=1) if len(main_run.queues) > 1 else None
+    # (one frame per launch at N = 1: this pass is the per-frame latency)
+    r1 = main_run.run(a.steps, a.warmup, queues=1, batch=1 if world == 1 else None) if len(main_run.queues) > 1 else None
     rt = main_run.run(min(a.steps, 1000), 2, queues=1, timing=True)
     ranks_stages = stage_times_all_ranks(ctx, rt)
     # value: uninstrumented frames over the frame queues
@@ -584,7 +596,8 @@ def main():
         line["brute_force_equivalent"] = bfe
         if r1 is not None:
             line["single_queue"] = {"mrays_per_s": round(r1["mrays"], 4), "ms_per_step": round(r1["ms_per_step"], 5),
-                                    "note": "the same frames with one frame in flight (per-frame latency)"}
+                                    "note": "the same frames with one frame in flight (N = 1: one frame per launch, "
+                                            "the per-frame latency)"}
         if world > 1:
             line["ranks_stages_ms"] = [{"rank": i, "prepare": round(s[0], 5), "bin": round(s[1], 5),
                                         "trace_kernel": round(s[2], 5)} for i, s in enumerate(ranks_stages)]
