@@ -474,7 +474,10 @@ def leg_summary(r):
 def main():
     a = parse()
     if a.batch <= 0:
-        a.batch = 16 if a.gpus > 1 else 8
+        # 16 frames per gather at N > 1, 8 per launch at N = 1; fewer when the run is short, so
+        # that every queue still fills several batches (a run of 20 steps over 3 queues would
+        # otherwise time nothing but the final partial batches)
+        a.batch = max(1, min(16 if a.gpus > 1 else 8, a.steps // (4 * max(1, a.queues))))
     ctx = Ctx(a)
     world, rank = ctx.world, ctx.rank
     path = ctx.scene_path(a.scene, a.triangles if a.scene == "soup" else None)
@@ -583,10 +586,10 @@ def main():
             "stages_ms": {"prepare": round(rt["prepare_ms"], 5), "bin": round(rt["bin_ms"], 5),
                           "trace_kernel": round(rt["trace_ms"], 5), "frame": round(r["ms_per_step"], 5),
                           "frame_instrumented": round(rt["ms_per_step"], 5), "timed_launches": rt["launches"],
-                          "note": "one frame in flight, HIP events bound to the kernels' dispatches: prepare = "
-                                  "PrepareInfoKernel (record setup + tile info), bin = BinTrianglesKernel + "
-                                  "WorkOrderKernel, trace_kernel = TraceCullKernel (rank 0's band at N > 1); frame = "
-                                  "uninstrumented time per frame with config.frame_queues in flight"},
+                          "note": "one frame per launch in flight, HIP events bound to the kernels' dispatches: "
+                                  "prepare = TileInfoKernel (tile ray boxes), bin = PrepareBinKernel (record setup + "
+                                  "bins) + WorkOrderKernel, trace_kernel = TraceCullKernel (rank 0's band at N > 1); "
+                                  "frame = uninstrumented time per frame with config.frame_queues in flight"},
         }
         line["scene_build"] = {"spatial_order_ms": round(order_build_ms, 4),
                                "note": "once per scene at load, on the device (Morton codes + rocPRIM radix sort, "

@@ -9,7 +9,7 @@ source "$(dirname "$0")/gpu_lib.sh"
 STEPS=${STEPS:-tests,smoke,bench,rehearse,prof,pmc,host}
 KERNEL_RE=${KERNEL_RE:-TraceCullKernel}
 KEY=${KEY:-"soup-100k 1920x1080 1spp|cull"}
-Q=(--steps 50 --warmup 5 --queues 1 --no-extras --no-cpu-baseline)
+Q=(--steps 50 --warmup 5 --queues 1 --batch 1 --no-extras --no-cpu-baseline)  # one frame per dispatch
 if [[ $STEPS == *tests* ]]; then
     run pytest_gpu 900 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread
 fi
