@@ -211,6 +211,12 @@ class Pipeline:
                 qd["group"] = ctx.groups[q % len(ctx.groups)]
             self.queues.append(qd)
         self.triangles = self.queues[0]["scene"].triangles
+        # Grow every queue's frame slots to the largest batched call now (allocation, zero fill):
+        # a batch larger than the warm-up's partial ones must not allocate inside a timed loop.
+        if self.row_count:
+            for q in self.queues:
+                self._batch_run(q, self.L)()
+            torch.cuda.synchronize(ctx.dev)
 
     def _batch_run(self, q, f, slot=0):
         """The queue's batched trace of f slots from `slot` (one srtTraceBatchAsync call), bound once."""
@@ -474,10 +480,11 @@ def leg_summary(r):
 def main():
     a = parse()
     if a.batch <= 0:
-        # 16 frames per gather at N > 1, 8 per launch at N = 1; fewer when the run is short, so
-        # that every queue still fills several batches (a run of 20 steps over 3 queues would
-        # otherwise time nothing but the final partial batches)
-        a.batch = max(1, min(16 if a.gpus > 1 else 8, a.steps // (4 * max(1, a.queues))))
+        # 16 frames per gather at N > 1, 8 per launch at N = 1, at most one batch per queue's
+        # share of the run: a short run (the driver's 20 steps over 3 queues) then traces, gathers
+        # and shades its frames in ~one batch per queue instead of per-frame collectives (~45 us
+        # of host time each) or a tail of partial batches
+        a.batch = max(1, min(16 if a.gpus > 1 else 8, -(-a.steps // max(1, a.queues))))
     ctx = Ctx(a)
     world, rank = ctx.world, ctx.rank
     path = ctx.scene_path(a.scene, a.triangles if a.scene == "soup" else None)
