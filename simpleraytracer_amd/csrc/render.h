@@ -113,11 +113,11 @@ struct CullBins {
     unsigned* counts;      // tiles + 1: list lengths, then the large-list length
     unsigned* lists;       // tiles x capacity candidate ids (BinTrianglesKernel)
     unsigned* large_list;  // PaddedTriangleCount(n) ids binned to every tile
-    void* work;            // trace work list (the last bin block): tiles x parts descriptors, 32 B each
+    void* work;            // trace work list (WorkOrderKernel): descs descriptors, 32 B each
     unsigned* work_count;  // its length
-    unsigned* arrive;      // tiles x parts: split chunks finished (self-resetting counters)
-    void* split_keys;      // key slices of split parts: tiles x parts x max_chunks, 8 KiB each
-    unsigned max_chunks;   // M = CullMaxChunks(tiles)
+    unsigned* arrive;      // per split slot: split chunks finished (self-resetting counters)
+    void* split_keys;      // key slices of split parts: one per split slot (<= descs), 8 KiB each
+    unsigned descs;        // trace grid = work descriptors per frame (<= CullDescriptors(tiles, 1))
     unsigned* range_tag;   // = gen when some sample offset of the frame lies outside [0, 1] (tile blocks)
     unsigned gen;          // the scene's frame number (never 0): tags are compared with it, not reset
     unsigned capacity;
@@ -134,11 +134,14 @@ bool CullBinnable(std::size_t width, std::size_t row_count);
 // record; results are unaffected). Env SRT_CULL_BIN_CAP overrides it (tests).
 unsigned CullBinCapacity(std::uint64_t n, std::size_t tiles);
 
-// Split width of a band's trace: a tile part's candidates go to at most M blocks (chunks), M =
-// ceil(resident trace blocks of the device / tile parts), 1 when the parts alone fill the chip,
-// at most kMaxChunks; env SRT_CULL_CHUNKS forces M (tests, measurement).
+// Trace grid of a band shape in a launch of `frames` frames: work descriptors per frame. A tile
+// part's candidates may be cut into up to kMaxChunks chunks (blocks); WorkOrderKernel picks the
+// chunk size so that a frame's descriptors fit. Room = max(parts x M, parts + E / frames): M =
+// ceil(resident trace blocks / the launch's parts) (small bands: > 1), E = env SRT_CULL_SPLIT
+// (default: the resident trace blocks) for cutting the heavy parts. Env SRT_CULL_CHUNKS = m
+// forces parts x m (tests, measurement).
 constexpr int kMaxChunks = 16;
-unsigned CullMaxChunks(std::size_t tiles);
+unsigned CullDescriptors(std::size_t tiles, std::size_t frames);
 
 // Bytes of the bin work buffer for n triangles and a band shape, and its carve-up.
 std::size_t CullBinBytes(std::uint64_t n, std::size_t width, std::size_t row_count);

@@ -77,10 +77,8 @@ struct TraceParams {
     const unsigned* __restrict__ order;       // spatial-order position -> record id
     const uint4* __restrict__ work;           // tile parts (2 x uint4 each), most work first (BuildWorkOrder)
     const unsigned* __restrict__ work_count;  // [0]: tile parts listed
-    unsigned long long* __restrict__ split_keys;  // key slices of split parts: (part, chunk), kBlockRows x 64 each
-    unsigned* __restrict__ arrive;            // per (tile, part): chunks finished (self-resetting)
-    unsigned max_chunks;                      // M: a part's candidates split into at most M chunks
-    unsigned chunk;                           // ... of at least this many candidates each
+    unsigned long long* __restrict__ split_keys;  // key slices of split parts: one per split slot, kBlockRows x 64 each
+    unsigned* __restrict__ arrive;            // per split part (its first slot): chunks finished (self-resetting)
     const unsigned* __restrict__ bin_lists;   // per tile: candidate positions (PrepareBinKernel)
     const unsigned* __restrict__ bin_counts;  // per tile: list length; [tiles]: large-list length
     const unsigned* __restrict__ large_list;  // ids of records binned to every tile
@@ -1253,6 +1251,8 @@ struct BinParams {
     unsigned* __restrict__ range_tag;   // = gen: some sample offset of this frame lies outside [0, 1]
     unsigned gen;                       // frame number of the scene (never 0)
     unsigned capacity;
+    unsigned descs;      // trace work descriptors the trace grid has room for (CullDescriptors)
+    unsigned min_chunk;  // smallest candidate chunk of a split part
     unsigned n;
     unsigned exp;  // diagnostic build: experiment bits (env SRT_EXP), 0 in the product
     int tiles_x;
@@ -1410,18 +1410,23 @@ __device__ __forceinline__ int LastLoAtMost(const float2* b, int n, float v) {
     return lo - 1;
 }
 
-// Trace work list (WorkOrderKernel, after the bin kernel). One 32-B descriptor per
-// tile part, listed longest first (counting sort by the log2 of the tile's candidates, FULL-stream
-// tiles first), so the heavy parts start first and the light ones fill in behind them; order
-// within a bucket is arbitrary (the frame does not depend on it). The trace grid is parts x M
-// blocks: block b runs chunk b % M of part b / M (TraceCullKernel splits a part's candidates into
-// at most M chunks of at least `chunk` candidates; the chunks past a part's count exit at once).
-// Descriptor: w0 = (tile part, candidates, tile list length, flags), w1 = (sample offset x, y of
-// the tile's first ray, 0, 0); flags: 1 = every ray of the tile has that offset, 2 = FULL.
+// Trace work list (WorkOrderKernel, after the bin kernel). One 32-B descriptor per trace block:
+// a tile part, or one candidate chunk of a split part. The grid has room for p.descs
+// descriptors D; with P parts holding C candidates in all (each part counted with its tile's
+// candidates), chunks of S = the power of two >= max(p.min_chunk, C / (D - P)) candidates fit,
+// since sum ceil(c / S) <= P + C / S <= D. So the heavy parts -- which bound a frame's trace
+// time -- are cut into several blocks and the light ones stay whole. The list is longest first
+// (counting sort by the log2 of the candidates per descriptor, FULL-stream tiles first), so the
+// heavy work starts first and the light work fills in behind it; order within a bucket is
+// arbitrary (the frame does not depend on it). Descriptor: w0 = (tile part, its candidates, tile
+// list length, flags), w1 = (sample offset x, y of the tile's first ray, chunk | chunks << 16,
+// first split slot of the part); flags: 1 = every ray of the tile has that offset, 2 = FULL. A
+// split part's chunks own consecutive split slots (key slices; the arrival counter at the first).
+// One block on one CU: every per-tile instruction costs the whole chip's wait, hence shifts.
 constexpr unsigned kItemRegular = 1u;
 constexpr unsigned kItemFull = 2u;
 struct OrderItem {
-    unsigned cand, flags, bucket, parts;
+    unsigned cand, flags, parts;
 };
 __device__ __forceinline__ OrderItem MakeOrderItem(const BinParams& p, unsigned t, unsigned cnt, unsigned large,
                                                    const TileInfo& ti) {
@@ -1429,16 +1434,24 @@ __device__ __forceinline__ OrderItem MakeOrderItem(const BinParams& p, unsigned 
     const bool full = ti.usable == 0u || cnt > p.capacity;
     it.flags = (full ? kItemFull : 0u) | (ti.regular != 0u ? kItemRegular : 0u);
     it.cand = full ? 0u : cnt + large;
-    it.bucket = full ? 63u : (it.cand == 0u ? 0u : 32u - __builtin_clz(it.cand));
     const int rows_left = p.row_count - static_cast<int>(t / static_cast<unsigned>(p.tiles_x)) * kTileRows;
     it.parts = static_cast<unsigned>(min(kParts, (rows_left + kBlockRows - 1) / kBlockRows));
     return it;
 }
-// Called by every thread of the order block; start = 64 LDS words, cnt = tiles LDS words. Two passes,
-// each issuing all of a thread's loads together (kOrderUnroll tiles): (1) lengths + tile flags
-// -> bucket histogram, lengths kept in LDS; (2) tile info again -> descriptors.
+// Chunks per part (chunk size 2^shift, at most kMaxChunks) and LPT bucket of a tile.
+__device__ __forceinline__ void ItemChunks(unsigned cand, unsigned flags, unsigned shift, unsigned& nch,
+                                           unsigned& bucket) {
+    const bool full = (flags & kItemFull) != 0u;
+    nch = full ? 1u : min(static_cast<unsigned>(kMaxChunks), max(1u, (cand + (1u << shift) - 1u) >> shift));
+    const unsigned per = cand >> (31u - __builtin_clz(nch));  // ~ candidates per chunk
+    bucket = full ? 63u : (per == 0u ? 0u : 32u - __builtin_clz(per));
+}
+// Called by every thread of the order block; start = 64 LDS words, cnt / meta = tiles LDS
+// words / bytes, sum = 2 LDS words. (1) lengths + tile flags into LDS, the candidate total;
+// (2) the chunk size, the bucket histogram (LDS only); (3) tile info again -> descriptors.
 constexpr int kOrderUnroll = 4;
-__device__ void BuildWorkOrder(const BinParams& p, unsigned* start, unsigned* cnt) {
+__device__ void BuildWorkOrder(const BinParams& p, unsigned* start, unsigned* cnt, unsigned char* meta,
+                               unsigned* sum) {
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
     const unsigned nthreads = blockDim.x;
@@ -1446,8 +1459,12 @@ __device__ void BuildWorkOrder(const BinParams& p, unsigned* start, unsigned* cn
     if (tid < 64) {
         start[tid] = 0u;
     }
+    if (tid < 2) {
+        sum[tid] = 0u;
+    }
     const unsigned large = p.counts[tiles];
-    __syncthreads();  // start[] zeroed
+    unsigned long long my_cand = 0ull;
+    unsigned my_parts = 0u;
     for (unsigned t0 = tid; t0 < tiles; t0 += kOrderUnroll * nthreads) {
         unsigned c[kOrderUnroll];
         TileInfo ti[kOrderUnroll];
@@ -1461,16 +1478,45 @@ __device__ void BuildWorkOrder(const BinParams& p, unsigned* start, unsigned* cn
         for (int u = 0; u < kOrderUnroll; ++u) {
             const unsigned t = t0 + u * nthreads;
             if (t < tiles) {
-                cnt[t] = c[u];
                 const OrderItem it = MakeOrderItem(p, t, c[u], large, ti[u]);
-                if (it.parts != 0u) {
-                    atomicAdd(&start[it.bucket], it.parts);
-                }
+                cnt[t] = it.cand;
+                meta[t] = static_cast<unsigned char>(it.flags | it.parts << 2);
+                my_cand += static_cast<unsigned long long>(it.parts) * it.cand;
+                my_parts += it.parts;
             }
         }
     }
+    // Candidates in units of 16 (a 32-bit total up to 2^36), rounded up; parts.
+    unsigned v16 = static_cast<unsigned>((my_cand + 15ull) >> 4), vp = my_parts;
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+        v16 += __shfl_xor(v16, o);
+        vp += __shfl_xor(vp, o);
+    }
+    __syncthreads();  // start[], sum[] zeroed
+    if (lane == 0) {
+        atomicAdd(&sum[0], v16);
+        atomicAdd(&sum[1], vp);
+    }
     __syncthreads();
-    if (tid < kWave) {  // bucket b's first slot: the parts in heavier buckets (suffix sum, exclusive)
+    unsigned shift = 31u;  // chunk size 2^31: no split
+    if (p.descs > sum[1]) {
+        const unsigned room = p.descs - sum[1];
+        const unsigned long long want = (16ull * sum[0] + room - 1ull) / room;  // C / (D - P), rounded up
+        const unsigned long long size = want > p.min_chunk ? want : p.min_chunk;
+        shift = size >= (1ull << 31) ? 31u : 64u - static_cast<unsigned>(__builtin_clzll(size - 1ull));
+        shift = size <= 1ull ? 0u : shift;
+    }
+    for (unsigned t = tid; t < tiles; t += nthreads) {
+        const unsigned parts = meta[t] >> 2;
+        if (parts != 0u) {
+            unsigned nch, bucket;
+            ItemChunks(cnt[t], meta[t] & 3u, shift, nch, bucket);
+            atomicAdd(&start[bucket], parts * nch);
+        }
+    }
+    __syncthreads();
+    if (tid < kWave) {  // bucket b's first slot: the descriptors in heavier buckets (suffix sum, exclusive)
         const unsigned c = start[lane];
         unsigned suf = c;
 #pragma unroll
@@ -1481,6 +1527,7 @@ __device__ void BuildWorkOrder(const BinParams& p, unsigned* start, unsigned* cn
         start[lane] = suf - c;
         if (lane == 0) {
             p.work_count[0] = suf;
+            sum[0] = 0u;  // split slots handed out (sum[] read by every thread before the barrier above)
         }
     }
     __syncthreads();
@@ -1496,12 +1543,21 @@ __device__ void BuildWorkOrder(const BinParams& p, unsigned* start, unsigned* cn
             if (t >= tiles) {
                 continue;
             }
-            const OrderItem it = MakeOrderItem(p, t, cnt[t], large, ti[u]);
-            if (it.parts != 0u) {
-                const unsigned at = atomicAdd(&start[it.bucket], it.parts);
-                for (unsigned part = 0; part < it.parts; ++part) {
-                    p.work[2 * (at + part)] = make_uint4(t * kParts + part, it.cand, cnt[t], it.flags);
-                    p.work[2 * (at + part) + 1] = make_uint4(__float_as_uint(ti[u].ox), __float_as_uint(ti[u].oy), 0u, 0u);
+            const unsigned parts = meta[t] >> 2, flags = meta[t] & 3u, cand = cnt[t];
+            if (parts == 0u) {
+                continue;
+            }
+            unsigned nch, bucket;
+            ItemChunks(cand, flags, shift, nch, bucket);
+            const unsigned at = atomicAdd(&start[bucket], parts * nch);
+            const unsigned slot = nch > 1u ? atomicAdd(&sum[0], parts * nch) : 0u;
+            const unsigned list_len = (flags & kItemFull) ? 0u : cand - large;
+            for (unsigned part = 0; part < parts; ++part) {
+                for (unsigned ch = 0; ch < nch; ++ch) {
+                    const unsigned d = at + part * nch + ch;
+                    p.work[2 * d] = make_uint4(t * kParts + part, cand, list_len, flags);
+                    p.work[2 * d + 1] = make_uint4(__float_as_uint(ti[u].ox), __float_as_uint(ti[u].oy),
+                                                   ch | nch << 16, slot + part * nch);
                 }
             }
         }
@@ -1723,8 +1779,10 @@ __global__ __launch_bounds__(kBinThreads) void PrepareBinKernel(const PrepareBin
 // alike: profiles/r02/ab_order/).
 __global__ __launch_bounds__(1024) void WorkOrderKernel(const BinBatch batch) {
     __shared__ unsigned start[64];
+    __shared__ unsigned sum[2];
     __shared__ unsigned cnt[kMaxBinTiles];
-    BuildWorkOrder(batch.f[blockIdx.z], start, cnt);
+    __shared__ unsigned char meta[kMaxBinTiles];
+    BuildWorkOrder(batch.f[blockIdx.z], start, cnt, meta, sum);
 }
 
 #ifndef SRT_TRACE_OCC
@@ -1760,12 +1818,11 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(c
     // Block = one part (kBlockRows rows) of a cull tile. Binned: work item blockIdx.x of the
     // tile order's list (a part, or one candidate chunk of a split part; the grid is sized for
     // the longest list and the blocks past its end exit). Unbinned: part (x, y), FULL stream.
-    unsigned item, chunk = 0u, nchunks = 1u, flags = kItemFull;
+    unsigned item, chunk = 0u, nchunks = 1u, slot = 0u, flags = kItemFull;
     float ox = 0.f, oy = 0.f;
     CullSource src{nullptr, nullptr, 0u, 0u, 0u, true};
     if (p.work != nullptr) {
-        const unsigned d = blockIdx.x / p.max_chunks;
-        chunk = blockIdx.x % p.max_chunks;
+        const unsigned d = blockIdx.x;
         if (d >= p.work_count[0]) {
             return;
         }
@@ -1774,22 +1831,19 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(c
         flags = w0.w;
         ox = __uint_as_float(w1.x);
         oy = __uint_as_float(w1.y);
+        chunk = w1.z & 0xFFFFu;
+        nchunks = w1.z >> 16;
+        slot = w1.w;
         src.full = (flags & kItemFull) != 0u;
         if (!src.full) {
-            // candidates cut into n <= M chunks of >= p.chunk: chunk c = [c q + c r / n, ...), q r = c_t / n, % n
+            // candidates cut into n chunks: chunk c = [c q + c r / n, (c + 1) q + (c + 1) r / n), q r = c_t / n, % n
             const unsigned c_t = w0.y;
-            nchunks = min(p.max_chunks, max(1u, c_t / p.chunk + (c_t % p.chunk != 0u ? 1u : 0u)));
-            if (chunk >= nchunks) {
-                return;
-            }
             const unsigned q = c_t / nchunks, r = c_t % nchunks;
             src.list = p.bin_lists + static_cast<size_t>(item / kParts) * p.bin_capacity;
             src.list2 = p.large_list;
             src.count1 = w0.z;
             src.begin = chunk * q + chunk * r / nchunks;
             src.end = (chunk + 1u) * q + (chunk + 1u) * r / nchunks;
-        } else if (chunk != 0u) {
-            return;
         }
     } else {
         item = blockIdx.y * gridDim.x + blockIdx.x;
@@ -1986,7 +2040,7 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(c
         // stores, every storing wave's vmcnt(0), barrier, one agent-scope add; the last
         // adder's block loads sc1 after a barrier).
         constexpr int kPix = kBlockRows * kWave;
-        unsigned long long* slices = p.split_keys + static_cast<size_t>(item) * p.max_chunks * kPix;
+        unsigned long long* slices = p.split_keys + static_cast<size_t>(slot) * kPix;
         const int pix = wave * R * kWave + lane;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
@@ -1996,10 +2050,10 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(c
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (tid == 0) {
-            const unsigned before = __hip_atomic_fetch_add(&p.arrive[item], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned before = __hip_atomic_fetch_add(&p.arrive[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const unsigned last = before == nchunks - 1u ? 1u : 0u;
             if (last != 0u) {  // every chunk has arrived: reset for the next frame
-                __hip_atomic_store(&p.arrive[item], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&p.arrive[slot], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             sh.last = last;
         }
@@ -2477,36 +2531,8 @@ unsigned CullBinCapacity(std::uint64_t n, std::size_t tiles) {
 }
 
 namespace {
-struct BinSizes {
-    std::size_t info, counts, lists, large, work, work_count, arrive, split_keys, range_tag;
-};
-BinSizes CullBinSizes(std::uint64_t n, std::size_t width, std::size_t row_count) {
-    const std::size_t tx = (width + kWave - 1) / kWave, ty = (row_count + kTileRows - 1) / kTileRows;
-    const std::size_t tiles = tx * ty;
-    const auto al = [](std::size_t b) { return (b + 255) / 256 * 256; };
-    const unsigned m = CullMaxChunks(tiles);
-    BinSizes z;
-    z.info = al(tiles * sizeof(TileInfo));
-    z.counts = al((tiles + 1) * 4);
-    z.lists = al(tiles * static_cast<std::size_t>(CullBinCapacity(n, tiles)) * 4);
-    z.large = al(PaddedTriangleCount(n) * 4);
-    z.work = al(tiles * kParts * 2 * sizeof(uint4));
-    z.work_count = al(4);
-    z.arrive = al(tiles * kParts * 4);
-    z.split_keys = m > 1 ? al(tiles * kParts * m * kBlockRows * kWave * 8) : 0;
-    z.range_tag = al(4);
-    return z;
-}
-}  // namespace
-
-unsigned CullMaxChunks(std::size_t tiles) {
-    if (const char* v = std::getenv("SRT_CULL_CHUNKS")) {  // measurement / tests: force the split width
-        const long m = std::strtol(v, nullptr, 10);
-        if (m > 0) {
-            return static_cast<unsigned>(m < kMaxChunks ? m : kMaxChunks);
-        }
-    }
-    // Resident trace blocks of the device (all CUs x blocks per CU), queried once per device.
+// Resident trace blocks of the current device (all CUs x blocks per CU), queried once per device.
+unsigned TraceSlots() {
     static thread_local int cached_device = -1;
     static thread_local unsigned slots = 0;
     int dev = 0;
@@ -2518,12 +2544,54 @@ unsigned CullMaxChunks(std::size_t tiles) {
             cached_device = dev;
         }
     }
-    const std::size_t items = tiles * kParts;
-    if (items == 0 || slots <= items) {
-        return 1u;  // the parts alone fill the chip: no split
+    return slots;
+}
+
+long EnvLong(const char* name, long fallback) {
+    const char* v = std::getenv(name);
+    return v == nullptr || *v == '\0' ? fallback : std::strtol(v, nullptr, 10);
+}
+
+struct BinSizes {
+    std::size_t info, counts, lists, large, work, work_count, arrive, split_keys, range_tag;
+};
+BinSizes CullBinSizes(std::uint64_t n, std::size_t width, std::size_t row_count) {
+    const std::size_t tx = (width + kWave - 1) / kWave, ty = (row_count + kTileRows - 1) / kTileRows;
+    const std::size_t tiles = tx * ty;
+    const auto al = [](std::size_t b) { return (b + 255) / 256 * 256; };
+    const std::size_t descs = CullDescriptors(tiles, 1);  // the most a launch of this shape lists
+    const bool split = descs > tiles * kParts;
+    BinSizes z;
+    z.info = al(tiles * sizeof(TileInfo));
+    z.counts = al((tiles + 1) * 4);
+    z.lists = al(tiles * static_cast<std::size_t>(CullBinCapacity(n, tiles)) * 4);
+    z.large = al(PaddedTriangleCount(n) * 4);
+    z.work = al(descs * 2 * sizeof(uint4));
+    z.work_count = al(4);
+    z.arrive = split ? al(descs * 4) : 0;
+    z.split_keys = split ? al(descs * kBlockRows * kWave * 8) : 0;
+    z.range_tag = al(4);
+    return z;
+}
+}  // namespace
+
+unsigned CullDescriptors(std::size_t tiles, std::size_t frames) {
+    const std::size_t parts = tiles * kParts;
+    frames = frames == 0 ? 1 : frames;
+    const long forced = EnvLong("SRT_CULL_CHUNKS", 0);
+    if (forced > 0) {  // measurement / tests: room for `forced` descriptors per part
+        return static_cast<unsigned>(parts * static_cast<std::size_t>(forced < kMaxChunks ? forced : kMaxChunks));
     }
-    const std::size_t m = (slots + items - 1) / items;
-    return static_cast<unsigned>(m < static_cast<std::size_t>(kMaxChunks) ? m : kMaxChunks);
+    const std::size_t slots = TraceSlots();
+    // Parts that leave the chip partly idle (small bands): M = ceil(slots / all parts) each.
+    std::size_t m = parts * frames >= slots || parts == 0 ? 1 : (slots + parts * frames - 1) / (parts * frames);
+    m = m < static_cast<std::size_t>(kMaxChunks) ? m : kMaxChunks;
+    // Room to cut the heavy parts: SRT_CULL_SPLIT extra descriptors per launch (default: one per
+    // resident block), shared by the launch's frames.
+    const long extra = EnvLong("SRT_CULL_SPLIT", static_cast<long>(slots));
+    const std::size_t e = extra > 0 ? static_cast<std::size_t>(extra) / frames : 0;
+    const std::size_t d = parts * m > parts + e ? parts * m : parts + e;
+    return static_cast<unsigned>(d);
 }
 
 std::size_t CullBinBytes(std::uint64_t n, std::size_t width, std::size_t row_count) {
@@ -2551,7 +2619,7 @@ CullBins CullBinLayout(void* base, std::uint64_t n, std::size_t width, std::size
     b.range_tag = reinterpret_cast<unsigned*>(take(z.range_tag));
     b.tiles = CullTiles(width, row_count);
     b.capacity = CullBinCapacity(n, b.tiles);
-    b.max_chunks = z.split_keys != 0 ? CullMaxChunks(b.tiles) : 1u;
+    b.descs = z.split_keys != 0 ? CullDescriptors(b.tiles, 1) : static_cast<unsigned>(b.tiles * kParts);
     return b;
 }
 
@@ -2609,6 +2677,8 @@ BinParams BindBins(TraceParams& p, const CullBins& bins, std::uint64_t n) {
     b.range_tag = bins.range_tag;
     b.gen = bins.gen;
     b.capacity = bins.capacity;
+    b.descs = bins.descs;
+    b.min_chunk = CullChunkFromEnv();
     b.n = static_cast<unsigned>(n);
     b.tiles_x = p.tiles_x;
     b.tiles_y = static_cast<int>(p.tiles / static_cast<unsigned>(p.tiles_x));
@@ -2623,8 +2693,6 @@ BinParams BindBins(TraceParams& p, const CullBins& bins, std::uint64_t n) {
     p.order = bins.order;
     p.work = b.work;
     p.work_count = b.work_count;
-    p.max_chunks = bins.max_chunks;
-    p.chunk = CullChunkFromEnv();
     p.split_keys = static_cast<unsigned long long*>(bins.split_keys);
     p.arrive = bins.arrive;
     p.bin_lists = bins.lists;
@@ -2657,7 +2725,7 @@ hipError_t LaunchCullFrames(const CullFrame* frames, std::size_t count, std::uin
         if (f.bins == nullptr || f.edges == nullptr || f.bins->order == nullptr || f.band.width != band0.width ||
             f.band.row_count != band0.row_count || f.band.row_begin != band0.row_begin ||
             f.band.row_interleave != band0.row_interleave ||
-            f.band.height != band0.height || f.bins->max_chunks != frames[0].bins->max_chunks) {
+            f.band.height != band0.height || f.bins->descs != frames[0].bins->descs) {
             return hipErrorInvalidValue;  // one band shape per batch
         }
         tb.f[i] = MakeTraceParams(f.edges, n, d_vertices, d_albedo, frame, background, f.band);
@@ -2672,13 +2740,13 @@ hipError_t LaunchCullFrames(const CullFrame* frames, std::size_t count, std::uin
     const unsigned z = static_cast<unsigned>(count);
     const unsigned gx = static_cast<unsigned>(tb.f[0].tiles_x), gy = tb.f[0].tiles / gx;
     // Tile info; records + bins (every padded position: the FULL stream reads them all); the
-    // trace work list; the trace: M blocks per work item.
+    // trace work list; the trace: one block per work descriptor.
     Launch(TileInfoKernel, dim3(gx, gy, z), dim3(kBinThreads), stream, ev.prep_begin, ev.prep_end, bb);
     const unsigned blocks = (pb.f[0].prep.n_pad + kBinThreads - 1) / kBinThreads;
     LaunchLds(PrepareBinKernel, dim3(blocks, 1, z), dim3(kBinThreads),
               BinLdsBytes(static_cast<int>(gx), static_cast<int>(gy)), stream, ev.bin_begin, nullptr, pb);
     Launch(WorkOrderKernel, dim3(1, 1, z), dim3(1024), stream, nullptr, ev.bin_end, bb);
-    Launch(TraceCullKernel, dim3(tb.f[0].tiles * kParts * tb.f[0].max_chunks, 1, z), dim3(kWave * kCullWaves), stream,
+    Launch(TraceCullKernel, dim3(frames[0].bins->descs, 1, z), dim3(kWave * kCullWaves), stream,
            ev.begin, ev.end, tb);
     return hipGetLastError();
 }

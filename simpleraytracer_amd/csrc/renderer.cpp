@@ -358,12 +358,12 @@ void DeviceScene::TraceBatch(const float* const* d_offsets, float* const* d_rgba
     CullBins bins[kMaxBatch];
     CullFrame cf[kMaxBatch];
     const std::size_t floats = PaddedTriangleCount(m_n) * kEdgeFloatsPerTriangle;
-    // The split width for the whole batch: its frames' parts together fill the chip sooner
-    // (a 135-row band alone splits 5 ways; eight of them do not need to).
-    const unsigned batch_chunks = CullMaxChunks(CullTiles(m_width, row_count) * frames);
+    // The trace grid for the whole batch: its frames' parts together fill the chip sooner (a
+    // 135-row band alone splits 5 ways; eight of them do not need to).
+    const unsigned batch_descs = CullDescriptors(CullTiles(m_width, row_count), frames);
     for (std::size_t f = 0; f < frames; ++f) {
         bins[f] = CullSlot(f, row_count);
-        bins[f].max_chunks = std::min(bins[f].max_chunks, batch_chunks);
+        bins[f].descs = std::min(bins[f].descs, batch_descs);
         cf[f].edges = m_edges + f * floats;
         cf[f].bins = &bins[f];
         cf[f].band = BandArgs{d_offsets[f], d_rgba != nullptr ? d_rgba[f] : nullptr, m_width, m_height, row_begin,
