@@ -1425,6 +1425,7 @@ __device__ __forceinline__ int LastLoAtMost(const float2* b, int n, float v) {
 // One block on one CU: every per-tile instruction costs the whole chip's wait, hence shifts.
 constexpr unsigned kItemRegular = 1u;
 constexpr unsigned kItemFull = 2u;
+constexpr unsigned kWorkEnd = 0xFFFFFFFFu;  // w0.x of a descriptor past the end of the list
 struct OrderItem {
     unsigned cand, flags, parts;
 };
@@ -1528,9 +1529,14 @@ __device__ void BuildWorkOrder(const BinParams& p, unsigned* start, unsigned* cn
         if (lane == 0) {
             p.work_count[0] = suf;
             sum[0] = 0u;  // split slots handed out (sum[] read by every thread before the barrier above)
+            sum[1] = suf;
         }
     }
     __syncthreads();
+    // Descriptors past the list end: an end mark, so a trace block needs no count load first.
+    for (unsigned d = sum[1] + tid; d < p.descs; d += nthreads) {
+        p.work[2 * d] = make_uint4(kWorkEnd, 0u, 0u, 0u);
+    }
     for (unsigned t0 = tid; t0 < tiles; t0 += kOrderUnroll * nthreads) {
         TileInfo ti[kOrderUnroll];
 #pragma unroll
@@ -1822,11 +1828,11 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(c
     float ox = 0.f, oy = 0.f;
     CullSource src{nullptr, nullptr, 0u, 0u, 0u, true};
     if (p.work != nullptr) {
-        const unsigned d = blockIdx.x;
-        if (d >= p.work_count[0]) {
+        const unsigned d = blockIdx.x;  // < descs: the list, then end marks
+        const uint4 w0 = p.work[2 * d], w1 = p.work[2 * d + 1];
+        if (w0.x == kWorkEnd) {
             return;
         }
-        const uint4 w0 = p.work[2 * d], w1 = p.work[2 * d + 1];
         item = w0.x;
         flags = w0.w;
         ox = __uint_as_float(w1.x);

@@ -63,6 +63,8 @@ def main():
         assert lib.srtDiagRead(buf.ctypes.data, buf.nbytes) == 0, _native.last_error()
         scene.close()
     ran = np.nonzero(buf[:, 9] > 0)[0]
+    if os.environ.get("DIAG_RAW"):  # every stamped block's row, for offline analysis
+        np.save(os.environ["DIAG_RAW"], buf[ran])
     b = buf[ran].astype(np.float64)
     t0 = b[:, 8].min()
     start = (b[:, 8] - t0) / 100.0  # us
