@@ -1425,7 +1425,9 @@ __device__ __forceinline__ int LastLoAtMost(const float2* b, int n, float v) {
 // One block on one CU: every per-tile instruction costs the whole chip's wait, hence shifts.
 constexpr unsigned kItemRegular = 1u;
 constexpr unsigned kItemFull = 2u;
+constexpr unsigned kItemEmpty = 4u;  // no candidate can hit a ray of the tile: every pixel misses
 constexpr unsigned kWorkEnd = 0xFFFFFFFFu;  // w0.x of a descriptor past the end of the list
+constexpr int kEmptyTest = 4;  // a tile with an empty bin list is tested against up to this many large-list records
 struct OrderItem {
     unsigned cand, flags, parts;
 };
@@ -1452,7 +1454,7 @@ __device__ __forceinline__ void ItemChunks(unsigned cand, unsigned flags, unsign
 // (2) the chunk size, the bucket histogram (LDS only); (3) tile info again -> descriptors.
 constexpr int kOrderUnroll = 4;
 __device__ void BuildWorkOrder(const BinParams& p, unsigned* start, unsigned* cnt, unsigned char* meta,
-                               unsigned* sum) {
+                               unsigned* sum, CullRecord* lrec) {
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
     const unsigned nthreads = blockDim.x;
@@ -1464,6 +1466,9 @@ __device__ void BuildWorkOrder(const BinParams& p, unsigned* start, unsigned* cn
         sum[tid] = 0u;
     }
     const unsigned large = p.counts[tiles];
+    if (tid < kEmptyTest && static_cast<unsigned>(tid) < large && large <= static_cast<unsigned>(kEmptyTest)) {
+        lrec[tid] = p.cull[p.large_list[tid]];  // read after the barriers below
+    }
     unsigned long long my_cand = 0ull;
     unsigned my_parts = 0u;
     for (unsigned t0 = tid; t0 < tiles; t0 += kOrderUnroll * nthreads) {
@@ -1558,10 +1563,24 @@ __device__ void BuildWorkOrder(const BinParams& p, unsigned* start, unsigned* cn
             const unsigned at = atomicAdd(&start[bucket], parts * nch);
             const unsigned slot = nch > 1u ? atomicAdd(&sum[0], parts * nch) : 0u;
             const unsigned list_len = (flags & kItemFull) ? 0u : cand - large;
+            // Empty bin list and few large-list records: if none of those can hit a ray of the
+            // tile box (the tests the trace blocks run against their part boxes, which lie inside
+            // it), every pixel misses (a ray outside the box has a NaN position and misses too).
+            unsigned out_flags = flags;
+            if ((flags & kItemFull) == 0u && list_len == 0u && large <= static_cast<unsigned>(kEmptyTest)) {
+                const Box tb{ti[u].box.x, ti[u].box.y, ti[u].box.z, ti[u].box.w};
+                bool may = false;
+                for (unsigned k = 0; k < large; ++k) {
+                    const CullRecord& r = lrec[k];
+                    const Record q{r.a.x, r.a.y, r.a.z, r.a.w, r.b.x, r.b.y, r.b.z, r.b.w, r.x.x};
+                    may = may || (ScreenBoxOverlaps(tb, r.sb) && BoxMayHit(tb, q));
+                }
+                out_flags |= may ? 0u : kItemEmpty;
+            }
             for (unsigned part = 0; part < parts; ++part) {
                 for (unsigned ch = 0; ch < nch; ++ch) {
                     const unsigned d = at + part * nch + ch;
-                    p.work[2 * d] = make_uint4(t * kParts + part, cand, list_len, flags);
+                    p.work[2 * d] = make_uint4(t * kParts + part, cand, list_len, out_flags);
                     p.work[2 * d + 1] = make_uint4(__float_as_uint(ti[u].ox), __float_as_uint(ti[u].oy),
                                                    ch | nch << 16, slot + part * nch);
                 }
@@ -1788,7 +1807,8 @@ __global__ __launch_bounds__(1024) void WorkOrderKernel(const BinBatch batch) {
     __shared__ unsigned sum[2];
     __shared__ unsigned cnt[kMaxBinTiles];
     __shared__ unsigned char meta[kMaxBinTiles];
-    BuildWorkOrder(batch.f[blockIdx.z], start, cnt, meta, sum);
+    __shared__ CullRecord lrec[kEmptyTest];
+    BuildWorkOrder(batch.f[blockIdx.z], start, cnt, meta, sum, lrec);
 }
 
 #ifndef SRT_TRACE_OCC
@@ -1864,6 +1884,20 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(c
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
     const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);
+    if (flags & kItemEmpty) {  // every pixel misses (BuildWorkOrder): the miss value, no rays
+        const int xe = tx * kWave + lane;
+        if (xe < p.width) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int y = row0 + wave * R + r;
+                if (y < p.row_count) {
+                    StorePixel(p, xe, y, 0.f, 0.f, -1);
+                }
+            }
+        }
+        SRT_DIAG_END(item, chunk, nchunks, 1u, src.full);
+        return;
+    }
     // LIST: the first batch's records are requested before the rays are set up (its loads
     // are the block's longest dependency chain: list entry, then the 64-B record).
     const unsigned total = src.end - src.begin;
