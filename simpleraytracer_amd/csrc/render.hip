@@ -796,6 +796,9 @@ static_assert((kPacketBatch % kCullThreads == 0 || kCullThreads % kPacketBatch =
 static_assert(kBlockRows <= 16 && kBlockRows % kCullWaves == 0, "packet word: rows < 16");
 static_assert(kPadTriangles % kStreamStep == 0, "a stream step must cover whole pad units");
 
+constexpr int kWindowPackets = 128;  // packet walk: packets per window of the batch's pixel stream
+constexpr unsigned kWindowPixels = kWindowPackets * kWave;
+
 // Batch entry of thread tid's slice e (kPacketBatch < kCullThreads: the first threads only).
 __device__ __forceinline__ bool InBatch(int e, int tid) { return e * kCullThreads + tid < kPacketBatch; }
 
@@ -807,9 +810,10 @@ struct CullShared {
         unsigned ids[kPacketBatch + kStreamStep];  // FULL stream: surviving record ids (read
                                                    // into registers before a batch writes sv2)
     };
-    unsigned pre[kPacketBatch + 1];  // exclusive packet prefix, pre[S] = packets
+    unsigned pre[kPacketBatch + 1];  // exclusive pixel prefix, pre[S] = pixels of the batch
     unsigned wave_n[kSlices * kCullWaves];   // survivors per (slice, wave)
-    unsigned wave_pk[kSlices * kCullWaves];  // packets per (slice, wave)
+    unsigned wave_pk[kSlices * kCullWaves];  // pixels per (slice, wave)
+    uint4 pk[kWindowPackets];  // window packet k: (last-pixel bits lo, hi, survivors ending before, 0)
     float2 fxy[kBlockRows][kWave];  // ray position (fx, fy) of every pixel of the block
     float clo[kWave], chi[kWave];    // monotone column bounds of fx (suffix min, prefix max)
     float rlo[kBlockRows], rhi[kBlockRows];  // monotone row bounds of fy
@@ -851,13 +855,15 @@ struct CullSource {
 //            and likewise the rows. A pixel outside those ranges has fx or fy outside the
 //            screen box, so it cannot pass the exact test (screen-box guarantee): skipping it
 //            is exact. (A block box outside the screen-box range: no screen-box tests, the
-//            whole block is the range.) The range is cut row-major into packets of 64 pixels;
+//            whole block is the range.);
 //   compact: survivors are compacted block-wide in any order, with an exclusive prefix of
-//            their packet counts;
-//   walk:    wave w takes the packets [w P / W, (w + 1) P / W) of the batch's P, two per
-//            iteration (independent dependency chains for the scheduler): each lane reads its
-//            pixel's (fx, fy), tests it exactly and merges a hit into the pixel's key with an
-//            LDS atomic min.
+//            their pixel counts: the batch's pixel stream, every range row-major, back to back;
+//   walk:    the stream is cut into packets of 64 consecutive pixels, which may span several
+//            survivors (dense: round 1 padded every range to whole packets, 56 % of the lanes
+//            busy at C3); wave w takes the packets [w P / W, (w + 1) P / W) of a window's P, two
+//            per iteration (independent dependency chains for the scheduler): each lane finds
+//            its survivor from the window's range-end bitmap, reads its pixel's (fx, fy), tests
+//            it exactly and merges a hit into the pixel's key with an LDS atomic min.
 // Same exact test and lexicographic (t, id) result as ExactTestAnyOrder.
 // ---------------------------------------------------------------------------------------
 struct PacketHit {
@@ -867,33 +873,14 @@ struct PacketHit {
 
 struct PacketPixel {
     unsigned pixb;  // byte offset of the pixel in an 8-B-per-pixel block table (keys, positions)
-    bool in;
+    bool in;        // a pixel of the stream (lanes past its end address pixel 0)
 };
 
-// Row-major packing: packet j of a survivor with range [c0, c0 + nc) x [r0, r0 + nr) covers
-// range pixels p = 64 j + lane, p < nc * nr, at (c0 + p % nc, r0 + p / nc). p / nc is
-// (p * m) >> 17 with m = ceil(2^17 / nc): exact, because p < 1088 and nc <= 64 keep
-// p * (m - 2^17 / nc) / 2^17 < 1/nc (and p * m < 2^24 * 2^24 fits v_mul_u32_u24's low word,
-// p * m < 2^32). Lanes past the range are not `in` and address pixel 0.
-__device__ __forceinline__ unsigned PacketMagic(unsigned w) {
-    const unsigned nc = ((w >> 6) & 63u) + 1u;
-    return (131071u + nc) / nc;
-}
-
-// One word per packet (one readlane in the walk loop): c0 (6 bits), nc - 1 (6), r0 (4),
-// nr - 1 (4), survivor slot (8), packet index (4).
+// A survivor's range [c0, c0 + nc) x [r0, r0 + nr) inside the part, one word (sv2.w):
+// c0 (6 bits), nc - 1 (6), r0 (4), nr - 1 (4).
 __device__ __forceinline__ unsigned PacketRange(int c0, int nc, int r0, int nr) {
     return static_cast<unsigned>(c0) | static_cast<unsigned>(nc - 1) << 6 | static_cast<unsigned>(r0) << 12 |
            static_cast<unsigned>(nr - 1) << 16;
-}
-__device__ __forceinline__ PacketPixel PacketLaneWord(unsigned w, unsigned m, int lane) {
-    // In units of 4 pixels: (4 pix m) >> 19 == (pix m) >> 17, 4 pix m < 2^32.
-    const unsigned c0 = w & 63u, nc = ((w >> 6) & 63u) + 1u, r0 = (w >> 12) & 15u, nr = ((w >> 16) & 15u) + 1u;
-    const unsigned pix4 = (w >> 28 << 8) | (static_cast<unsigned>(lane) << 2);
-    const unsigned row_in = __umul24(pix4, m) >> 19;
-    const unsigned col4 = pix4 - row_in * (nc * 4u) + c0 * 4u;  // 4 * column
-    const bool in = pix4 < nc * nr * 4u;
-    return PacketPixel{in ? ((row_in + r0) << 9) + col4 * 2u : 0u, in};  // lanes past the range read pixel 0
 }
 
 __device__ __forceinline__ PacketHit EvalPacket(const float4& a, const float4& b, const float4& x, float2 f,
@@ -1089,7 +1076,7 @@ __device__ __forceinline__ void PacketBatch(CullShared& sh, const Box& bb, const
             }
             pass[e] = c0 <= c1 && r0 <= r1;
             if (pass[e]) {
-                npk[e] = static_cast<unsigned>(((c1 - c0 + 1) * (r1 - r0 + 1) + kWave - 1) / kWave);
+                npk[e] = static_cast<unsigned>((c1 - c0 + 1) * (r1 - r0 + 1));  // pixels of the range
                 bits[e] = PacketRange(c0, c1 - c0 + 1, r0, r1 - r0 + 1);
             }
         }
@@ -1150,51 +1137,80 @@ __device__ __forceinline__ void PacketBatch(CullShared& sh, const Box& bb, const
     }
     __syncthreads();
     prefetch();
-    // Walk this wave's packets [q_begin, q_end), 64 at a time: lane l finds packet q0 + l's
-    // survivor (binary search in pre) and packs its word, then the wave takes the packets
-    // kPacketIlp at a time (independent chains: all LDS reads issued together; a tail repeats
-    // the last packet, harmless under an atomic min) and applies the hits.
+    // Walk the batch's pixel stream -- the survivors' ranges back to back in slot order, each
+    // row-major -- in windows of kWindowPixels. Per window: a bitmap of the pixels that end a
+    // survivor's range and, per 64-pixel packet, the number of ranges that end before it, so
+    // that lane l of packet k (pixel g = 64 k + l) finds its survivor as that number plus the
+    // range ends below it in the packet (mbcnt), and its pixel as position g - pre[s] of the
+    // range. The waves split each window's packets evenly, kPacketIlp at a time (independent
+    // chains; a tail repeats the last packet, harmless under the atomic min).
     constexpr int kPacketIlp = SRT_PACKET_ILP;
-    const unsigned q_begin = wave * n_pk / W, q_end = (wave + 1) * n_pk / W;
     const char* fxy = reinterpret_cast<const char*>(&sh.fxy[0][0]);
     char* keys = reinterpret_cast<char*>(&sh.keys[0][0]);
+    const unsigned last_slot = n_surv == 0u ? 0u : n_surv - 1u;
+    unsigned ended = 0u;  // ranges that end before the window (block-uniform)
 #pragma unroll 1
-    for (unsigned q0 = q_begin; q0 < q_end; q0 += kWave) {
-        const unsigned mine = min(q0 + static_cast<unsigned>(lane), q_end - 1u);
-        int lo = 0, hi = static_cast<int>(n_surv) - 1;  // last survivor with pre <= mine
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (sh.pre[mid] <= mine) {
-                lo = mid;
-            } else {
-                hi = mid - 1;
+    for (unsigned w0 = 0; w0 < n_pk; w0 += kWindowPixels) {
+        const unsigned wn = min(kWindowPixels, n_pk - w0);
+        const unsigned npk_w = (wn + kWave - 1u) / kWave;
+        for (int k = tid; k < kWindowPackets; k += kCullThreads) {
+            sh.pk[k] = make_uint4(0u, 0u, 0u, 0u);
+        }
+        __syncthreads();
+        for (unsigned slot = tid; slot < n_surv; slot += kCullThreads) {
+            const unsigned o = sh.pre[slot + 1] - 1u - w0;  // the range's last pixel, in the window
+            if (o < wn) {
+                atomicOr((o & 32u) ? &sh.pk[o >> 6].y : &sh.pk[o >> 6].x, 1u << (o & 31u));
             }
         }
-        const unsigned my_bits = __float_as_uint(sh.sv2[lo].w);
-        const unsigned my_w = my_bits | static_cast<unsigned>(lo) << 20 | (mine - sh.pre[lo]) << 28;
-        const unsigned my_m = PacketMagic(my_bits);
-        // Resolve the per-lane packet table before the loop, so the loop header does not wait
-        // for the previous iteration's LDS atomics (conservative waitcnt merge).
-        asm volatile("" ::"v"(my_w), "v"(my_m));
-        const unsigned n = min(static_cast<unsigned>(kWave), q_end - q0);
+        __syncthreads();
+        if (wave == 0) {  // exclusive prefix of the range ends over the window's packets, 2 per lane
+            const uint4 pa = sh.pk[2 * lane], pb = sh.pk[2 * lane + 1];
+            const unsigned ca = __popc(pa.x) + __popc(pa.y), cb = __popc(pb.x) + __popc(pb.y);
+            unsigned incl = ca + cb;
+#pragma unroll
+            for (int o = 1; o < kWave; o <<= 1) {
+                const unsigned t = __shfl_up(incl, o);
+                if (lane >= o) {
+                    incl += t;
+                }
+            }
+            sh.pk[2 * lane].z = ended + incl - ca - cb;
+            sh.pk[2 * lane + 1].z = ended + incl - cb;
+        }
+        __syncthreads();
+        {
+            const uint4 pl = sh.pk[kWindowPackets - 1];  // entries past the window are empty
+            ended = pl.z + __popc(pl.x) + __popc(pl.y);
+        }
+        const unsigned k_begin = wave * npk_w / W, k_end = (wave + 1) * npk_w / W;
 #pragma unroll 1
-        for (unsigned i = 0; i < n; i += kPacketIlp) {
-            unsigned ps[kPacketIlp];
+        for (unsigned k = k_begin; k < k_end; k += kPacketIlp) {
             PacketPixel px[kPacketIlp];
             float4 ra[kPacketIlp], rb[kPacketIlp], rx[kPacketIlp];
             float2 f[kPacketIlp];
 #pragma unroll
             for (int u = 0; u < kPacketIlp; ++u) {
-                const unsigned li = min(i + u, n - 1u);
-                const unsigned w = __builtin_amdgcn_readlane(my_w, li);
-                ps[u] = (w >> 20) & 255u;
-                px[u] = PacketLaneWord(w, __builtin_amdgcn_readlane(my_m, li), lane);
+                const unsigned kk = min(k + u, k_end - 1u);
+                const uint4 e = sh.pk[kk];  // one address: a broadcast read
+                const unsigned g = w0 + kk * kWave + static_cast<unsigned>(lane);
+                const unsigned sl = min(__builtin_amdgcn_mbcnt_hi(e.y, __builtin_amdgcn_mbcnt_lo(e.x, 0u)) + e.z,
+                                        last_slot);
+                const bool in = g < n_pk;
+                ra[u] = sh.sv0[sl];
+                rb[u] = sh.sv1[sl];
+                rx[u] = sh.sv2[sl];
+                const unsigned q = g - sh.pre[sl];  // pixel of the range, row-major
+                const unsigned w = __float_as_uint(rx[u].w);
+                const unsigned c0 = w & 63u, nc = ((w >> 6) & 63u) + 1u, r0 = (w >> 12) & 15u;
+                // row = q / nc, exact: q < 1024, so (q + 1/2) / nc is >= 1/128 from an integer
+                const unsigned row = static_cast<unsigned>((static_cast<float>(q) + 0.5f) *
+                                                           __builtin_amdgcn_rcpf(static_cast<float>(nc)));
+                const unsigned col = q - row * nc;
+                px[u] = PacketPixel{in ? ((row + r0) << 9) + ((col + c0) << 3) : 0u, in};
             }
 #pragma unroll
             for (int u = 0; u < kPacketIlp; ++u) {
-                ra[u] = sh.sv0[ps[u]];
-                rb[u] = sh.sv1[ps[u]];
-                rx[u] = sh.sv2[ps[u]];
                 f[u] = *reinterpret_cast<const float2*>(fxy + px[u].pixb);
             }
             PacketHit h[kPacketIlp];
@@ -1202,8 +1218,6 @@ __device__ __forceinline__ void PacketBatch(CullShared& sh, const Box& bb, const
             for (int u = 0; u < kPacketIlp; ++u) {
                 h[u] = EvalPacket(ra[u], rb[u], rx[u], f[u], px[u].in);
             }
-            // Keys built before the hit branches: the record id is loaded with the rest of the
-            // record instead of by a separate LDS read (and full wait) inside the branch.
 #pragma unroll
             for (int u = 0; u < kPacketIlp; ++u) {
                 asm volatile("" ::"v"(h[u].key));
@@ -1216,8 +1230,8 @@ __device__ __forceinline__ void PacketBatch(CullShared& sh, const Box& bb, const
                 }
             }
         }
+        __syncthreads();  // window table reused
     }
-    __syncthreads();  // batch storage reused
 }
 
 // ---------------------------------------------------------------------------------------
