@@ -783,7 +783,7 @@ constexpr int kCullWaves = 4;
 constexpr int kCullThreads = kWave * kCullWaves;
 constexpr int kCullR = kBlockRows / kCullWaves;  // rays per lane
 #ifndef SRT_PACKET_BATCH
-#define SRT_PACKET_BATCH 256
+#define SRT_PACKET_BATCH 128
 #endif
 #ifndef SRT_PACKET_ILP
 #define SRT_PACKET_ILP 2  // packet walk: packets evaluated together per wave (independent chains)
@@ -1826,7 +1826,7 @@ __global__ __launch_bounds__(1024) void WorkOrderKernel(const BinBatch batch) {
 }
 
 #ifndef SRT_TRACE_OCC
-#define SRT_TRACE_OCC 5
+#define SRT_TRACE_OCC 6
 #endif
 
 __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(const TraceBatch batch) {
