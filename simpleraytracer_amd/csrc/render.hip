@@ -796,21 +796,27 @@ static_assert((kPacketBatch % kCullThreads == 0 || kCullThreads % kPacketBatch =
 static_assert(kBlockRows <= 16 && kBlockRows % kCullWaves == 0, "packet word: rows < 16");
 static_assert(kPadTriangles % kStreamStep == 0, "a stream step must cover whole pad units");
 
-constexpr int kWindowPackets = 128;  // packet walk: packets per window of the batch's pixel stream
+#ifndef SRT_WINDOW_PACKETS
+#define SRT_WINDOW_PACKETS 128
+#endif
+constexpr int kWindowPackets = SRT_WINDOW_PACKETS;  // packet walk: packets per window of the pixel stream
 constexpr unsigned kWindowPixels = kWindowPackets * kWave;
 
 // Batch entry of thread tid's slice e (kPacketBatch < kCullThreads: the first threads only).
 __device__ __forceinline__ bool InBatch(int e, int tid) { return e * kCullThreads + tid < kPacketBatch; }
 
 struct CullShared {
-    float4 sv0[kPacketBatch];  // compacted survivors: plane 0 (sv0, sv1 adjacent: PacketTables scratch)
-    float4 sv1[kPacketBatch];  //                      plane 1
     union {
-        float4 sv2[kPacketBatch];  //                  (cyC, vol, id, packed pixel range)
-        unsigned ids[kPacketBatch + kStreamStep];  // FULL stream: surviving record ids (read
-                                                   // into registers before a batch writes sv2)
+        struct {
+            float4 sv0[kPacketBatch];  // compacted survivors: plane 0 (sv0, sv1 adjacent: PacketTables scratch)
+            float4 sv1[kPacketBatch];  //                      plane 1
+            float4 sv2[kPacketBatch];  //                      (cyC, vol, id, 1 / nc)
+        };
+        unsigned ids[kPacketBatch + kStreamStep];  // FULL stream: surviving record ids (read into
+                                                   // registers before a batch writes the planes)
     };
-    unsigned pre[kPacketBatch + 1];  // exclusive pixel prefix, pre[S] = pixels of the batch
+    uint2 aux[kPacketBatch + 1];  // per survivor: (exclusive pixel prefix, range base pixel byte offset | nc << 16);
+                                  // aux[S].x = pixels of the batch
     unsigned wave_n[kSlices * kCullWaves];   // survivors per (slice, wave)
     unsigned wave_pk[kSlices * kCullWaves];  // pixels per (slice, wave)
     uint4 pk[kWindowPackets];  // window packet k: (last-pixel bits lo, hi, survivors ending before, 0)
@@ -823,7 +829,7 @@ struct CullShared {
     unsigned long long keys[kBlockRows][kWave];  // per-pixel lexicographic (t, id) keys
 };
 static_assert(sizeof(float2) * kWave * kCullWaves <= sizeof(float4) * 2 * kPacketBatch, "PacketTables scratch");
-static_assert((kPacketBatch + kStreamStep) * 4 <= sizeof(float4) * kPacketBatch, "stream ids alias sv2");
+static_assert((kPacketBatch + kStreamStep) * 4 <= sizeof(float4) * 3 * kPacketBatch, "stream ids alias the planes");
 constexpr int kFlushBatches = (kPacketBatch + kStreamStep - 1 + kPacketBatch - 1) / kPacketBatch;  // per flush
 
 // (t, id) packed so that unsigned order is lexicographic order: t >= 0 here (vol > 0,
@@ -875,13 +881,6 @@ struct PacketPixel {
     unsigned pixb;  // byte offset of the pixel in an 8-B-per-pixel block table (keys, positions)
     bool in;        // a pixel of the stream (lanes past its end address pixel 0)
 };
-
-// A survivor's range [c0, c0 + nc) x [r0, r0 + nr) inside the part, one word (sv2.w):
-// c0 (6 bits), nc - 1 (6), r0 (4), nr - 1 (4).
-__device__ __forceinline__ unsigned PacketRange(int c0, int nc, int r0, int nr) {
-    return static_cast<unsigned>(c0) | static_cast<unsigned>(nc - 1) << 6 | static_cast<unsigned>(r0) << 12 |
-           static_cast<unsigned>(nr - 1) << 16;
-}
 
 __device__ __forceinline__ PacketHit EvalPacket(const float4& a, const float4& b, const float4& x, float2 f,
                                                 bool in) {
@@ -1056,7 +1055,7 @@ __device__ __forceinline__ void PacketBatch(CullShared& sh, const Box& bb, const
     const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);
     const unsigned long long lt_mask = (1ull << lane) - 1ull;
     bool pass[kSlices];
-    unsigned bits[kSlices], npk[kSlices];
+    unsigned bits[kSlices], npk[kSlices];  // bits: range base pixel byte offset | range width << 16
 #pragma unroll
     for (int e = 0; e < kSlices; ++e) {
         bits[e] = 0u;
@@ -1077,7 +1076,8 @@ __device__ __forceinline__ void PacketBatch(CullShared& sh, const Box& bb, const
             pass[e] = c0 <= c1 && r0 <= r1;
             if (pass[e]) {
                 npk[e] = static_cast<unsigned>((c1 - c0 + 1) * (r1 - r0 + 1));  // pixels of the range
-                bits[e] = PacketRange(c0, c1 - c0 + 1, r0, r1 - r0 + 1);
+                bits[e] = (static_cast<unsigned>(r0) << 9) + (static_cast<unsigned>(c0) << 3) |
+                          static_cast<unsigned>(c1 - c0 + 1) << 16;
             }
         }
     }
@@ -1128,12 +1128,13 @@ __device__ __forceinline__ void PacketBatch(CullShared& sh, const Box& bb, const
             const unsigned slot = sbase[e] + wpos[e];
             sh.sv0[slot] = cr[e].a;
             sh.sv1[slot] = cr[e].b;
-            sh.sv2[slot] = make_float4(cr[e].x.x, cr[e].x.y, cr[e].x.z, __uint_as_float(bits[e]));
-            sh.pre[slot] = pbase[e] + incl[e] - npk[e];
+            const float rnc = __builtin_amdgcn_rcpf(static_cast<float>(bits[e] >> 16));
+            sh.sv2[slot] = make_float4(cr[e].x.x, cr[e].x.y, cr[e].x.z, rnc);
+            sh.aux[slot] = make_uint2(pbase[e] + incl[e] - npk[e], bits[e]);
         }
     }
     if (tid == 0) {
-        sh.pre[n_surv] = n_pk;
+        sh.aux[n_surv] = make_uint2(n_pk, 0u);
     }
     __syncthreads();
     prefetch();
@@ -1158,7 +1159,7 @@ __device__ __forceinline__ void PacketBatch(CullShared& sh, const Box& bb, const
         }
         __syncthreads();
         for (unsigned slot = tid; slot < n_surv; slot += kCullThreads) {
-            const unsigned o = sh.pre[slot + 1] - 1u - w0;  // the range's last pixel, in the window
+            const unsigned o = sh.aux[slot + 1].x - 1u - w0;  // the range's last pixel, in the window
             if (o < wn) {
                 atomicOr((o & 32u) ? &sh.pk[o >> 6].y : &sh.pk[o >> 6].x, 1u << (o & 31u));
             }
@@ -1200,14 +1201,13 @@ __device__ __forceinline__ void PacketBatch(CullShared& sh, const Box& bb, const
                 ra[u] = sh.sv0[sl];
                 rb[u] = sh.sv1[sl];
                 rx[u] = sh.sv2[sl];
-                const unsigned q = g - sh.pre[sl];  // pixel of the range, row-major
-                const unsigned w = __float_as_uint(rx[u].w);
-                const unsigned c0 = w & 63u, nc = ((w >> 6) & 63u) + 1u, r0 = (w >> 12) & 15u;
-                // row = q / nc, exact: q < 1024, so (q + 1/2) / nc is >= 1/128 from an integer
-                const unsigned row = static_cast<unsigned>((static_cast<float>(q) + 0.5f) *
-                                                           __builtin_amdgcn_rcpf(static_cast<float>(nc)));
-                const unsigned col = q - row * nc;
-                px[u] = PacketPixel{in ? ((row + r0) << 9) + ((col + c0) << 3) : 0u, in};
+                const uint2 ax = sh.aux[sl];
+                const unsigned q = g - ax.x;  // pixel of the range, row-major
+                // row = q / nc, exact: q < 1024 and 1 / nc within 1 ulp, so (q + 1/2) / nc is
+                // >= 1/128 from an integer and the product is within 2^-10 of it
+                const unsigned row = static_cast<unsigned>((static_cast<float>(q) + 0.5f) * rx[u].w);
+                const unsigned col = q - __umul24(row, ax.y >> 16);
+                px[u] = PacketPixel{in ? (ax.y & 0xFFFFu) + (row << 9) + (col << 3) : 0u, in};
             }
 #pragma unroll
             for (int u = 0; u < kPacketIlp; ++u) {
@@ -1462,6 +1462,9 @@ __device__ __forceinline__ void ItemChunks(unsigned cand, unsigned flags, unsign
     nch = full ? 1u : min(static_cast<unsigned>(kMaxChunks), max(1u, (cand + (1u << shift) - 1u) >> shift));
     const unsigned per = cand >> (31u - __builtin_clz(nch));  // ~ candidates per chunk
     bucket = full ? 63u : (per == 0u ? 0u : 32u - __builtin_clz(per));
+#ifdef SRT_EXP_SPATIAL  // measurement builds only: one bucket (list ~ in tile order)
+    bucket = 0u;
+#endif
 }
 // Called by every thread of the order block; start = 64 LDS words, cnt / meta = tiles LDS
 // words / bytes, sum = 2 LDS words. (1) lengths + tile flags into LDS, the candidate total;
@@ -1833,6 +1836,9 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(c
     const TraceParams& p = batch.f[blockIdx.z];
     constexpr int R = kCullR;
     __shared__ CullShared sh;
+#ifdef SRT_EXP_SETUP_ONLY  // measurement builds only (make exp): the frame's setup without its trace
+    return;
+#endif
 #ifdef SRT_DIAG
     const unsigned long long d_rt0 = __builtin_amdgcn_s_memrealtime();
     const unsigned d_blk = blockIdx.y * gridDim.x + blockIdx.x;
@@ -1862,7 +1868,14 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(c
     float ox = 0.f, oy = 0.f;
     CullSource src{nullptr, nullptr, 0u, 0u, 0u, true};
     if (p.work != nullptr) {
+#ifdef SRT_EXP_SPATIAL  // measurement builds only: XCD (b % 8) takes a contiguous eighth of the list
+        const unsigned d = (blockIdx.x % 8u) * ((gridDim.x + 7u) / 8u) + blockIdx.x / 8u;
+        if (d >= gridDim.x) {
+            return;
+        }
+#else
         const unsigned d = blockIdx.x;  // < descs: the list, then end marks
+#endif
         const uint4 w0 = p.work[2 * d], w1 = p.work[2 * d + 1];
         if (w0.x == kWorkEnd) {
             return;
