@@ -16,7 +16,7 @@ queue (the per-frame latency).
 
 Multi-GPU, one rank per GPU over RCCL:
   --mode bands (default; BASELINE config C4): every frame is split into P bands -- the frame's
-      32-row tile rows dealt round-robin (--rows interleaved, default) or contiguous blocks --,
+      16-row tile rows dealt round-robin (--rows interleaved, default) or contiguous blocks --,
       rank r traces its band (hit ids, 4 B per pixel; deferred shading, bit-identical), a batch
       of 16 frames' bands is gathered over RCCL in ONE collective (a torch-RCCL gather costs
       ~40 us of host time per call, more than a band's trace: tools/host_probe_bands.py) to
@@ -71,7 +71,7 @@ def parse():
     p.add_argument("--mode", default="bands", choices=["bands", "frames"], help="multi-GPU split (module doc)")
     p.add_argument("--root", default="rotate", choices=["rotate", "fixed"], help="bands: compositing rank")
     p.add_argument("--rows", default="interleaved", choices=["interleaved", "contiguous"],
-                   help="bands: each rank's rows, the frame's 32-row tile rows dealt round-robin or one block")
+                   help="bands: each rank's rows, the frame's 16-row tile rows dealt round-robin or one block")
     p.add_argument("--queues", type=int, default=int(os.environ.get("SRT_BENCH_QUEUES", "3")),
                    help="frames in flight per GPU (own scene buffers, HIP stream, process group each)")
     p.add_argument("--batch", type=int, default=int(os.environ.get("SRT_BENCH_BATCH", "0")),

@@ -94,11 +94,11 @@ ML_API_ENTRY int srtTraceIdsAsync(srt_device_scene scene, const float* d_offsets
  * srtTraceAsync (record setup, bins, trace): the same pixels, bit for bit; the cull variant runs
  * the batch with one launch per stage, so a frame costs a quarter of the host launches.
  * row_interleave 1: the band is frame rows [row_begin, row_begin + row_count). P > 1: the frame's
- * 32-row tile rows are dealt round-robin to P bands and this band holds tile rows
- * row_begin / 32 + k P, k = 0, 1, ..., concatenated (row_begin a multiple of 32, row_count =
- * those rows' total; SRT_TILE_ROWS = 32). */
+ * 16-row tile rows are dealt round-robin to P bands and this band holds tile rows
+ * row_begin / 16 + k P, k = 0, 1, ..., concatenated (row_begin a multiple of 16, row_count =
+ * those rows' total; SRT_TILE_ROWS = 16). */
 #define SRT_MAX_BATCH 8
-#define SRT_TILE_ROWS 32
+#define SRT_TILE_ROWS 16
 ML_API_ENTRY int srtTraceBatchAsync(srt_device_scene scene, const float* const* d_offsets, float* const* d_rgba,
                                     int* const* d_ids, size_t frames, size_t row_begin, size_t row_count,
                                     size_t row_interleave, int variant, void* stream);
@@ -114,7 +114,7 @@ ML_API_ENTRY int srtShadeAsync(srt_device_scene scene, const float* d_offsets, c
  * rank's (frames x band_rows x width) band buffer leaves them,
  *   d_ids[band][frame][band_rows][width],
  * with bands = ceil(height / band_rows) contiguous bands (interleaved = 0), or `interleaved`
- * bands that took the frame's 32-row tile rows round-robin (srtTraceBatchAsync row_interleave;
+ * bands that took the frame's 16-row tile rows round-robin (srtTraceBatchAsync row_interleave;
  * band_rows >= the largest band's rows). d_offsets is the frame's (height x width x 2), d_rgba
  * receives frames x height x width x 4. One launch; each frame is bit-identical to
  * srtTraceAsync's RGBA. */

@@ -29,7 +29,7 @@ SRT_TRACE_SCALAR = 1
 SRT_TRACE_CULL = 2
 SRT_TRACE_BVH = 3
 SRT_MAX_BATCH = 8  # include/srt_render.h: frames per srtTraceBatchAsync call
-SRT_TILE_ROWS = 32  # include/srt_render.h: rows per tile row (interleaved bands deal these)
+SRT_TILE_ROWS = 16  # include/srt_render.h: rows per tile row (interleaved bands deal these)
 
 
 class ImageInfo(ctypes.Structure):

@@ -4,7 +4,7 @@ Multi-GPU layout (DESIGN.md "Multi-GPU"): rank r of P renders frame rows
 [r*B, min(H, (r+1)*B)) with B = ceil(H / P); every rank holds a band buffer of exactly B rows
 (the last one padded) so the gather has equal counts; the destination receives the bands in
 place into one (P*B)-row buffer and keeps the first H rows. Interleaved bands
-(``interleaved_range``) deal the frame's 32-row tile rows round-robin instead, so every rank gets
+(``interleaved_range``) deal the frame's 16-row tile rows round-robin instead, so every rank gets
 a share of the dense centre; the gathered layout is then unscrambled by the shading kernel. Inside one process, Renderer
 (csrc/renderer.cpp) does the same with ncclGather; across processes (one rank per GPU,
 torch.distributed over RCCL/xGMI, or gloo on CPU for tests) this module does it with
@@ -34,11 +34,11 @@ def band_range(height: int, world: int, rank: int) -> tuple[int, int]:
     return begin, end - begin
 
 
-TILE_ROWS = 32  # include/srt_render.h SRT_TILE_ROWS: interleaved bands deal whole tile rows
+TILE_ROWS = 16  # include/srt_render.h SRT_TILE_ROWS: interleaved bands deal whole tile rows
 
 
 def interleaved_range(height: int, world: int, rank: int) -> tuple[int, int]:
-    """(row_begin, row_count) of ``rank``'s interleaved band: the frame's 32-row tile rows dealt
+    """(row_begin, row_count) of ``rank``'s interleaved band: the frame's 16-row tile rows dealt
     round-robin, rank r holding tile rows r, r + P, r + 2P, ... (srtTraceBatchAsync
     row_interleave = P); row_count may be 0. Balances the work of a frame whose centre is denser
     than its edges, which contiguous bands do not."""

@@ -91,10 +91,12 @@ hipError_t LaunchPrepare(const float* d_vertices, const unsigned* d_rank, std::u
                          float* d_edges, hipStream_t stream, hipEvent_t ev_begin = nullptr,
                          hipEvent_t ev_end = nullptr);
 
-// Cull tiles: 64 columns x 32 rows of rays, one trace block each (render.hip "Cull bins").
+// Cull tiles: 64 columns x 16 rows of rays, one trace block each (render.hip "Cull bins"; 32-row
+// tiles of two 16-row trace blocks measured 3 % slower at C3: each block filtered the candidates of
+// both halves).
 constexpr int kCullTileCols = 64;
 #ifndef SRT_TILE_ROWS
-#define SRT_TILE_ROWS 32
+#define SRT_TILE_ROWS 16
 #endif
 constexpr int kCullTileRows = SRT_TILE_ROWS;
 
@@ -109,6 +111,7 @@ constexpr int kMaxBinTiles = 8192;    // and tiles_x * tiles_y <= this (bin kern
 // CullBinLayout; it must be zero-filled when allocated: the counters reset themselves).
 struct CullBins {
     const unsigned* order; // the scene's record ids in spatial order (DeviceScene; not in the buffer)
+    const float* svertices;  // the scene's vertices in that order (DeviceScene; not in the buffer)
     void* tile_info;       // tiles x 32 B: ray box, uniform offset (TileInfoKernel)
     unsigned* counts;      // tiles + 1: list lengths, then the large-list length
     unsigned* lists;       // tiles x capacity candidate ids (BinTrianglesKernel)
@@ -214,7 +217,7 @@ hipError_t LaunchShade(const float* d_vertices, const float* d_albedo, const flo
 // image-plane position under the scene camera, on the device (keys + rocPRIM radix sort), and
 // its inverse; synchronous on `stream`. Optional events bracket the build (timing).
 void BuildSpatialOrder(const float* d_vertices, std::uint64_t n, const Camera& camera, unsigned* d_order,
-                       unsigned* d_rank, hipStream_t stream, hipEvent_t ev_begin = nullptr,
+                       unsigned* d_rank, float* d_svertices, hipStream_t stream, hipEvent_t ev_begin = nullptr,
                        hipEvent_t ev_end = nullptr);
 
 // Element-wise IEEE binary16 <-> binary32 conversion on the device (ML_FLOAT16 images):

@@ -102,6 +102,7 @@ struct PrepareParams {
     const float* __restrict__ vertices;
     const unsigned* __restrict__ rank;  // record id -> position in the spatial order
     const unsigned* __restrict__ order; // position -> record id (the fused bin pass)
+    const float* __restrict__ svertices;  // vertices by position (the fused bin pass)
     float4* __restrict__ edges;
     float4* __restrict__ screen_boxes;
     uint2* __restrict__ qboxes;
@@ -217,13 +218,13 @@ __device__ __forceinline__ unsigned PackI16(int low, int high) {
 // orientation normalised so vol > 0, then each normal projected onto the affine ray frame:
 // E(fx, fy) = n . (base + fx du + fy dv): c = (c0A, cxA, cyA, c0B, cxB, cyB, c0C, cxC, cyC).
 // Disabled (padding, degenerate, plane through the eye): NaN record, empty screen box.
-__device__ __forceinline__ void ComputeRecord(const PrepareParams& p, unsigned id, bool real, float c[9], float& vol,
-                                              float4& sb) {
+// v = the triangle's 9 vertex coordinates.
+__device__ __forceinline__ void ComputeRecord(const PrepareParams& p, const float* __restrict__ v, bool real, float c[9],
+                                              float& vol, float4& sb) {
     const float qnan = __builtin_nanf("");
     bool disabled = !real;
     vol = qnan;
     if (!disabled) {
-        const float* v = p.vertices + 9ull * id;
         const float ax = v[0] - p.origin[0], ay = v[1] - p.origin[1], az = v[2] - p.origin[2];
         const float bx = v[3] - p.origin[0], by = v[4] - p.origin[1], bz = v[5] - p.origin[2];
         const float cx = v[6] - p.origin[0], cy = v[7] - p.origin[1], cz = v[8] - p.origin[2];
@@ -276,9 +277,9 @@ __device__ __forceinline__ uint2 QuantizeBox(const float4& sb) {
     return make_uint2(PackI16(QuantHi(sb.y), -QuantLo(sb.x)), PackI16(QuantHi(sb.w), -QuantLo(sb.z)));
 }
 
-// Shading normal: the exact expressions the shading epilogue used to evaluate per hit.
-__device__ __forceinline__ float4 ShadingNormal(const float* __restrict__ vertices, unsigned id) {
-    const float* v = vertices + 9ull * id;
+// Shading normal of the triangle with vertex coordinates v[0..9): the exact expressions the
+// shading epilogue used to evaluate per hit.
+__device__ __forceinline__ float4 ShadingNormal(const float* __restrict__ v) {
     const float e1x = v[3] - v[0], e1y = v[4] - v[1], e1z = v[5] - v[2];
     const float e2x = v[6] - v[0], e2y = v[7] - v[1], e2z = v[8] - v[2];
     float nx, ny, nz;
@@ -301,7 +302,7 @@ __device__ __forceinline__ void PrepareRecord(const PrepareParams& p, unsigned i
     const bool real = i < p.n;
     float c[9], vol;
     float4 sb;
-    ComputeRecord(p, i, real, c, vol, sb);
+    ComputeRecord(p, p.vertices + 9ull * i, real, c, vol, sb);
     tile[j] = make_float4(c[0], c[1], c[2], c[3]);
     tile[kTileTriangles + j] = make_float4(c[4], c[5], c[6], c[7]);
     p2[j] = c[8];
@@ -316,7 +317,7 @@ __device__ __forceinline__ void PrepareRecord(const PrepareParams& p, unsigned i
     r.sb = sb;
     p.cull[pos] = r;
     if (real) {
-        p.normals[i] = ShadingNormal(p.vertices, i);
+        p.normals[i] = ShadingNormal(p.vertices + 9ull * i);
     }
 }
 
@@ -801,6 +802,7 @@ static_assert(kPadTriangles % kStreamStep == 0, "a stream step must cover whole 
 #endif
 constexpr int kWindowPackets = SRT_WINDOW_PACKETS;  // packet walk: packets per window of the pixel stream
 constexpr unsigned kWindowPixels = kWindowPackets * kWave;
+static_assert(kWindowPackets == 2 * kWave, "window prefix: two packets per lane");
 
 // Batch entry of thread tid's slice e (kPacketBatch < kCullThreads: the first threads only).
 __device__ __forceinline__ bool InBatch(int e, int tid) { return e * kCullThreads + tid < kPacketBatch; }
@@ -819,7 +821,7 @@ struct CullShared {
                                   // aux[S].x = pixels of the batch
     unsigned wave_n[kSlices * kCullWaves];   // survivors per (slice, wave)
     unsigned wave_pk[kSlices * kCullWaves];  // pixels per (slice, wave)
-    uint4 pk[kWindowPackets];  // window packet k: (last-pixel bits lo, hi, survivors ending before, 0)
+    uint2 pk[2][kWindowPackets];  // window packet k: last-pixel bits (lo, hi); two buffers, alternate batches
     float2 fxy[kBlockRows][kWave];  // ray position (fx, fy) of every pixel of the block
     float clo[kWave], chi[kWave];    // monotone column bounds of fx (suffix min, prefix max)
     float rlo[kBlockRows], rhi[kBlockRows];  // monotone row bounds of fy
@@ -1044,16 +1046,20 @@ __device__ __forceinline__ PacketFrame MakePacketFrame(const CullShared& sh, int
 // One packet-walk batch: candidate e * kCullThreads + tid is cr[e] when valid[e]. Filter,
 // compaction and the walk into sh.keys; `prefetch()` runs between the compaction and the walk
 // (the next batch's loads then hide behind the walk). Starts and ends with block-uniform
-// control flow; contains barriers; ends with one.
+// control flow. Two barriers for a batch of <= kWindowPixels pixels, none at the end: the next
+// batch's first barrier separates this walk from its plane writes, the range-end bitmap
+// alternates between two buffers (`buf` = batch parity; this batch clears the other one), and
+// the caller puts a barrier between the last batch and its reads of sh.keys.
 template <class F>
 __device__ __forceinline__ void PacketBatch(CullShared& sh, const Box& bb, const PacketFrame& pf,
                                             const CullRecord (&cr)[kSlices], const bool (&valid)[kSlices],
-                                            F&& prefetch) {
+                                            unsigned buf, F&& prefetch) {
     constexpr int W = kCullWaves;
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
     const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);
     const unsigned long long lt_mask = (1ull << lane) - 1ull;
+    uint2* pkb = sh.pk[buf];
     bool pass[kSlices];
     unsigned bits[kSlices], npk[kSlices];  // bits: range base pixel byte offset | range width << 16
 #pragma unroll
@@ -1131,12 +1137,21 @@ __device__ __forceinline__ void PacketBatch(CullShared& sh, const Box& bb, const
             const float rnc = __builtin_amdgcn_rcpf(static_cast<float>(bits[e] >> 16));
             sh.sv2[slot] = make_float4(cr[e].x.x, cr[e].x.y, cr[e].x.z, rnc);
             sh.aux[slot] = make_uint2(pbase[e] + incl[e] - npk[e], bits[e]);
+            const unsigned o = pbase[e] + incl[e] - 1u;  // the range's last pixel in the stream
+            if (o < kWindowPixels) {                      // first window: its end bit
+                atomicOr((o & 32u) ? &pkb[o >> 6].y : &pkb[o >> 6].x, 1u << (o & 31u));
+            }
         }
     }
     if (tid == 0) {
         sh.aux[n_surv] = make_uint2(n_pk, 0u);
     }
     __syncthreads();
+    // The other buffer (last read by the previous batch's walk, which every wave finished before
+    // this batch's first barrier) is cleared for the next batch.
+    if (tid < kWindowPackets) {
+        sh.pk[buf ^ 1u][tid] = make_uint2(0u, 0u);
+    }
     prefetch();
     // Walk the batch's pixel stream -- the survivors' ranges back to back in slot order, each
     // row-major -- in windows of kWindowPixels. Per window: a bitmap of the pixels that end a
@@ -1154,36 +1169,34 @@ __device__ __forceinline__ void PacketBatch(CullShared& sh, const Box& bb, const
     for (unsigned w0 = 0; w0 < n_pk; w0 += kWindowPixels) {
         const unsigned wn = min(kWindowPixels, n_pk - w0);
         const unsigned npk_w = (wn + kWave - 1u) / kWave;
-        for (int k = tid; k < kWindowPackets; k += kCullThreads) {
-            sh.pk[k] = make_uint4(0u, 0u, 0u, 0u);
-        }
-        __syncthreads();
-        for (unsigned slot = tid; slot < n_surv; slot += kCullThreads) {
-            const unsigned o = sh.aux[slot + 1].x - 1u - w0;  // the range's last pixel, in the window
-            if (o < wn) {
-                atomicOr((o & 32u) ? &sh.pk[o >> 6].y : &sh.pk[o >> 6].x, 1u << (o & 31u));
+        if (w0 != 0u) {  // a later window (rare: > kWindowPixels pixels in the batch): rebuild its bitmap
+            __syncthreads();  // every wave done with the previous window
+            if (tid < kWindowPackets) {
+                pkb[tid] = make_uint2(0u, 0u);
             }
-        }
-        __syncthreads();
-        if (wave == 0) {  // exclusive prefix of the range ends over the window's packets, 2 per lane
-            const uint4 pa = sh.pk[2 * lane], pb = sh.pk[2 * lane + 1];
-            const unsigned ca = __popc(pa.x) + __popc(pa.y), cb = __popc(pb.x) + __popc(pb.y);
-            unsigned incl = ca + cb;
-#pragma unroll
-            for (int o = 1; o < kWave; o <<= 1) {
-                const unsigned t = __shfl_up(incl, o);
-                if (lane >= o) {
-                    incl += t;
+            __syncthreads();
+            for (unsigned slot = tid; slot < n_surv; slot += kCullThreads) {
+                const unsigned o = sh.aux[slot + 1].x - 1u - w0;  // the range's last pixel, in the window
+                if (o < wn) {
+                    atomicOr((o & 32u) ? &pkb[o >> 6].y : &pkb[o >> 6].x, 1u << (o & 31u));
                 }
             }
-            sh.pk[2 * lane].z = ended + incl - ca - cb;
-            sh.pk[2 * lane + 1].z = ended + incl - cb;
+            __syncthreads();
         }
-        __syncthreads();
-        {
-            const uint4 pl = sh.pk[kWindowPackets - 1];  // entries past the window are empty
-            ended = pl.z + __popc(pl.x) + __popc(pl.y);
+        // Every wave: exclusive prefix of the range ends over the window's packets (2 per lane,
+        // packets 2l and 2l + 1 in lane l), kept in registers -- no barrier to publish it.
+        const uint2 pa = pkb[2 * lane], pb = pkb[2 * lane + 1];
+        const unsigned ca = __popc(pa.x) + __popc(pa.y), cb = __popc(pb.x) + __popc(pb.y);
+        unsigned incl = ca + cb;
+#pragma unroll
+        for (int o = 1; o < kWave; o <<= 1) {
+            const unsigned t = __shfl_up(incl, o);
+            if (lane >= o) {
+                incl += t;
+            }
         }
+        const unsigned za = ended + incl - ca - cb;  // ranges ending before packet 2 lane
+        ended += static_cast<unsigned>(__builtin_amdgcn_readlane(static_cast<int>(incl), kWave - 1));
         const unsigned k_begin = wave * npk_w / W, k_end = (wave + 1) * npk_w / W;
 #pragma unroll 1
         for (unsigned k = k_begin; k < k_end; k += kPacketIlp) {
@@ -1193,9 +1206,15 @@ __device__ __forceinline__ void PacketBatch(CullShared& sh, const Box& bb, const
 #pragma unroll
             for (int u = 0; u < kPacketIlp; ++u) {
                 const unsigned kk = min(k + u, k_end - 1u);
-                const uint4 e = sh.pk[kk];  // one address: a broadcast read
+                const uint2 e = pkb[kk];  // one address: a broadcast read
+                // ranges ending before packet kk: lane kk / 2's prefix, plus its first packet's ends
+                const int src = static_cast<int>(kk >> 1);
+                unsigned z = static_cast<unsigned>(__builtin_amdgcn_readlane(static_cast<int>(za), src));
+                if (kk & 1u) {
+                    z += static_cast<unsigned>(__builtin_amdgcn_readlane(static_cast<int>(ca), src));
+                }
                 const unsigned g = w0 + kk * kWave + static_cast<unsigned>(lane);
-                const unsigned sl = min(__builtin_amdgcn_mbcnt_hi(e.y, __builtin_amdgcn_mbcnt_lo(e.x, 0u)) + e.z,
+                const unsigned sl = min(__builtin_amdgcn_mbcnt_hi(e.y, __builtin_amdgcn_mbcnt_lo(e.x, 0u)) + z,
                                         last_slot);
                 const bool in = g < n_pk;
                 ra[u] = sh.sv0[sl];
@@ -1230,7 +1249,6 @@ __device__ __forceinline__ void PacketBatch(CullShared& sh, const Box& bb, const
                 }
             }
         }
-        __syncthreads();  // window table reused
     }
 }
 
@@ -1250,7 +1268,11 @@ __device__ __forceinline__ void PacketBatch(CullShared& sh, const Box& bb, const
 // the screen-box range, or whose list overflowed, streams every record instead.
 // ---------------------------------------------------------------------------------------
 constexpr int kBinThreads = 256;
-constexpr int kLargeTiles = 16;  // records spanning more tiles go to the large list
+#ifndef SRT_LARGE_TILES
+#define SRT_LARGE_TILES 16
+#endif
+constexpr int kLargeTiles = SRT_LARGE_TILES;  // records spanning more tiles go to the large list
+static_assert(kLargeTiles <= 32, "a record's tile mask is 32 bits");
 static_assert(kTileRows == kCullTileRows && kWave == kCullTileCols, "render.h tile shape");
 
 struct BinParams {
@@ -1436,6 +1458,8 @@ __device__ __forceinline__ int LastLoAtMost(const float2* b, int n, float v) {
 // list length, flags), w1 = (sample offset x, y of the tile's first ray, chunk | chunks << 16,
 // first split slot of the part); flags: 1 = every ray of the tile has that offset, 2 = FULL. A
 // split part's chunks own consecutive split slots (key slices; the arrival counter at the first).
+// (Gathering whole empty tiles four to a descriptor, one block storing all their misses, cut the
+// trace grid by ~950 blocks at C3 and measured no faster: an empty part's block is cheap.)
 // One block on one CU: every per-tile instruction costs the whole chip's wait, hence shifts.
 constexpr unsigned kItemRegular = 1u;
 constexpr unsigned kItemFull = 2u;
@@ -1696,7 +1720,9 @@ std::size_t BinLdsBytes(int nx, int ny) {
 // the records it holds: binary searches in the bounds give each record the range of tiles its
 // screen box can overlap, every tile of the range passing ScreenBoxOverlaps + BoxMayHit against
 // its own box gets the position appended (records spanning more than kLargeTiles tiles go to the
-// large list); an LDS histogram of (tile, record) pairs reserves each touched tile's share of
+// large list). (Staging the block's window of tile boxes in LDS first, instead of each thread
+// loading its tiles' boxes one after another, measured 1.4 us slower: two more barriers and a
+// reduction for loads that hit the L2.) An LDS histogram of (tile, record) pairs reserves each touched tile's share of
 // its list with ONE global atomic (per-pair global atomics serialise on the busy tiles).
 struct PrepareBinParams {
     PrepareParams prep;
@@ -1722,8 +1748,9 @@ __global__ __launch_bounds__(kBinThreads) void PrepareBinKernel(const PrepareBin
     float c[9], vol = 0.f;
     float4 sb = make_float4(__builtin_inff(), -__builtin_inff(), __builtin_inff(), -__builtin_inff());
     const unsigned id = real ? pp.order[i] : i;
+    const float* v = pp.svertices + 9ull * (real ? i : 0u);  // by position: no order -> vertex chain
     if (i < pp.n_pad) {
-        ComputeRecord(pp, id, real, c, vol, sb);
+        ComputeRecord(pp, v, real, c, vol, sb);
     }
     // The monotone tile-column and tile-row bounds (the histogram's LDS is the reduction's
     // scratch), then the histogram zeroed.
@@ -1734,7 +1761,7 @@ __global__ __launch_bounds__(kBinThreads) void PrepareBinKernel(const PrepareBin
     if (i < pp.n_pad) {
         pp.qboxes[i] = QuantizeBox(sb);
         if (real) {
-            pp.normals[id] = ShadingNormal(pp.vertices, id);
+            pp.normals[id] = ShadingNormal(v);
         }
         bool needed = !real || *p.range_tag == p.gen;
         if (!needed) {  // does the quantized box meet a tile row of the band (analytic row bounds)?
@@ -1763,10 +1790,9 @@ __global__ __launch_bounds__(kBinThreads) void PrepareBinKernel(const PrepareBin
     }
     __syncthreads();  // histogram zeroed
 
-    // The record's tile range and the tiles of it that pass (bit k = tile (r0 + k / w, c0 + k % w)
-    // of the range, at most kLargeTiles of them).
-    unsigned mask = 0u;
-    int c0 = 0, r0 = 0, w = 1;
+    // The record's tile range (bit k of the mask below = tile (r0 + k / w, c0 + k % w) of the
+    // range, at most kLargeTiles of them).
+    int c0 = 0, r0 = 0, w = 0, h = 0;
     if (real && sb.x <= sb.y && sb.z <= sb.w && (p.exp & 1u) == 0u) {  // else disabled: empty box
         // Any tile (c, r) whose box overlaps sb has hi'[c] >= hi[c] >= sb.xlo and
         // lo'[c] <= lo[c] <= sb.xhi, so c lies in [c0, c1]; rows likewise.
@@ -1774,21 +1800,22 @@ __global__ __launch_bounds__(kBinThreads) void PrepareBinKernel(const PrepareBin
         const int c1 = LastLoAtMost(b, nx, sb.y);
         r0 = FirstHiAtLeast(b + nx, ny, sb.z);
         const int r1 = LastLoAtMost(b + nx, ny, sb.w);
-        w = c1 - c0 + 1;
-        const int h = r1 - r0 + 1;
-        if (w > 0 && h > 0 && (p.exp & 2u) == 0u) {
-            if (w * h > kLargeTiles) {
-                p.large_list[atomicAdd(&p.counts[tiles], 1u)] = i;
-            } else {
-                const Record rec{c[0], c[1], c[2], c[3], c[4], c[5], c[6], c[7], c[8]};
+        w = max(c1 - c0 + 1, 0);
+        h = max(r1 - r0 + 1, 0);
+        if (w * h > kLargeTiles && (p.exp & 2u) == 0u) {
+            p.large_list[atomicAdd(&p.counts[tiles], 1u)] = i;
+        }
+    }
+    const bool listed = w * h > 0 && w * h <= kLargeTiles && (p.exp & 2u) == 0u;
+    unsigned mask = 0u;
+    if (listed) {
+        const Record rec{c[0], c[1], c[2], c[3], c[4], c[5], c[6], c[7], c[8]};
 #pragma unroll 1
-                for (int k = 0; k < w * h; ++k) {
-                    const TileInfo ti = p.tile_info[(r0 + k / w) * nx + c0 + k % w];
-                    const Box tb{ti.box.x, ti.box.y, ti.box.z, ti.box.w};
-                    if (ti.usable != 0u && ScreenBoxOverlaps(tb, sb) && BoxMayHit(tb, rec)) {
-                        mask |= 1u << k;
-                    }
-                }
+        for (int k = 0; k < w * h; ++k) {
+            const TileInfo ti = p.tile_info[(r0 + k / w) * nx + c0 + k % w];
+            const Box tb{ti.box.x, ti.box.y, ti.box.z, ti.box.w};
+            if (ti.usable != 0u && ScreenBoxOverlaps(tb, sb) && BoxMayHit(tb, rec)) {
+                mask |= 1u << k;
             }
         }
     }
@@ -1987,6 +2014,10 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(c
     for (int i = tid; i < kBlockRows * kWave; i += kCullThreads) {
         (&sh.keys[0][0])[i] = ~0ull;
     }
+    for (int i = tid; i < 2 * kWindowPackets; i += kCullThreads) {
+        (&sh.pk[0][0])[i] = make_uint2(0u, 0u);
+    }
+    unsigned pk_buf = 0u;  // range-end bitmap buffer of the next batch
     const PacketFrame pf = MakePacketFrame(sh, nc, nr, ScreenBoxUsable(bb));
     __syncthreads();  // keys initialised
 #ifdef SRT_DIAG
@@ -2007,11 +2038,12 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(c
                 cr[e] = nxt[e];
                 valid[e] = InBatch(e, tid) && b0 + e * kCullThreads + tid < total;
             }
-            PacketBatch(sh, bb, pf, cr, valid, [&] {
+            PacketBatch(sh, bb, pf, cr, valid, pk_buf, [&] {
                 if (b0 + kPacketBatch < total) {
                     load_list(b0 + kPacketBatch);
                 }
             });
+            pk_buf ^= 1u;
 #ifdef SRT_DIAG
             ++d_batches;
 #endif
@@ -2083,7 +2115,8 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(c
                     valid[e] = InBatch(e, tid) && b0 + e * kCullThreads + tid < listed;
                     cr[e] = p.cull[my_ids[bi][e]];
                 }
-                PacketBatch(sh, bb, pf, cr, valid, [] {});
+                PacketBatch(sh, bb, pf, cr, valid, pk_buf, [] {});
+                pk_buf ^= 1u;
 #ifdef SRT_DIAG
                 ++d_batches;
                 d_cand += min(listed - b0, static_cast<unsigned>(kPacketBatch));
@@ -2092,6 +2125,7 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(c
             listed = 0u;
         }
     }
+    __syncthreads();  // every wave's walk has merged its hits into sh.keys
 #ifdef SRT_DIAG
     d_walk = __builtin_amdgcn_s_memtime() - d_mark;
 #endif
@@ -2789,7 +2823,8 @@ hipError_t LaunchCullFrames(const CullFrame* frames, std::size_t count, std::uin
     PrepareBinBatch pb{};
     for (std::size_t i = 0; i < count; ++i) {
         const CullFrame& f = frames[i];
-        if (f.bins == nullptr || f.edges == nullptr || f.bins->order == nullptr || f.band.width != band0.width ||
+        if (f.bins == nullptr || f.edges == nullptr || f.bins->order == nullptr || f.bins->svertices == nullptr ||
+            f.band.width != band0.width ||
             f.band.row_count != band0.row_count || f.band.row_begin != band0.row_begin ||
             f.band.row_interleave != band0.row_interleave ||
             f.band.height != band0.height || f.bins->descs != frames[0].bins->descs) {
@@ -2802,6 +2837,7 @@ hipError_t LaunchCullFrames(const CullFrame* frames, std::size_t count, std::uin
         bb.f[i] = BindBins(tb.f[i], *f.bins, n);
         pb.f[i].prep = MakePrepareParams(d_vertices, d_rank, n, frame, const_cast<float*>(f.edges));
         pb.f[i].prep.order = f.bins->order;
+        pb.f[i].prep.svertices = f.bins->svertices;
         pb.f[i].bin = bb.f[i];
     }
     const unsigned z = static_cast<unsigned>(count);

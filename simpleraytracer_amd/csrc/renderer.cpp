@@ -157,6 +157,7 @@ DeviceScene::DeviceScene(const Scene& scene, int device)
         m_edges = DeviceAlloc<float>(PaddedTriangleCount(m_n) * kEdgeFloatsPerTriangle, "hipMalloc(edges)");
         m_order = DeviceAlloc<unsigned>(m_n == 0 ? 1 : m_n, "hipMalloc(order)");
         m_rank = DeviceAlloc<unsigned>(m_n == 0 ? 1 : m_n, "hipMalloc(rank)");
+        m_svertices = DeviceAlloc<float>(m_n == 0 ? 9 : m_n * 9, "hipMalloc(spatial vertices)");
         HipCheck(hipMemcpy(m_vertices, scene.vertices.data(), m_n * 9 * sizeof(float), hipMemcpyHostToDevice),
                  "hipMemcpy(vertices)");
         // The records' spatial order, built on the device (spatial.hip), timed.
@@ -167,7 +168,7 @@ DeviceScene::DeviceScene(const Scene& scene, int device)
             throw std::runtime_error("HIP error: hipEventCreate(order build)");
         }
         try {
-            BuildSpatialOrder(m_vertices, m_n, m_camera, m_order, m_rank, nullptr, b0, b1);
+            BuildSpatialOrder(m_vertices, m_n, m_camera, m_order, m_rank, m_svertices, nullptr, b0, b1);
             float ms = 0.f;
             if (m_n != 0 && hipEventElapsedTime(&ms, b0, b1) == hipSuccess) {
                 m_build_ms = ms;
@@ -187,6 +188,7 @@ DeviceScene::DeviceScene(const Scene& scene, int device)
         (void)hipFree(m_edges);
         (void)hipFree(m_order);
         (void)hipFree(m_rank);
+        (void)hipFree(m_svertices);
         throw;
     }
 }
@@ -200,6 +202,7 @@ DeviceScene::~DeviceScene() {
     (void)hipFree(m_edges);
     (void)hipFree(m_order);
     (void)hipFree(m_rank);
+    (void)hipFree(m_svertices);
     (void)hipFree(m_cull_work);
     (void)hipFree(m_bvh);
     for (hipEvent_t e : m_events) {
@@ -308,6 +311,7 @@ void DeviceScene::EnsureCullWork(std::size_t slots, std::size_t row_count, hipSt
 CullBins DeviceScene::CullSlot(std::size_t slot, std::size_t row_count) const {
     CullBins bins = CullBinLayout(m_cull_work + slot * m_cull_layout, m_n, m_width, row_count);
     bins.order = m_order;
+    bins.svertices = m_svertices;
     m_cull_gen = m_cull_gen + 1u == 0u ? 1u : m_cull_gen + 1u;
     bins.gen = m_cull_gen;
     return bins;

@@ -94,6 +94,7 @@ private:
     mutable std::size_t m_edge_slots = 1;    // frame slots of m_edges (TraceBatch grows it; slot 0 = Trace's)
     unsigned* m_order = nullptr;  // record ids in spatial order (BuildSpatialOrder), for the cull bins
     unsigned* m_rank = nullptr;   // its inverse: record id -> position
+    float* m_svertices = nullptr; // vertices in spatial order (svertices[i] = vertices[order[i]])
     double m_build_ms = 0.0;      // spatial order build (BuildSpatialOrder) at load
     Frame m_frame{};
     std::size_t m_width = 0;

@@ -57,12 +57,19 @@ __global__ __launch_bounds__(256) void MortonKeysKernel(const float* __restrict_
     }
 }
 
-// rank[order[i]] = i
+// rank[order[i]] = i; svertices[i] = vertices[order[i]] (the bin kernel's record pass reads
+// the vertices by spatial position: coalesced, and no order -> vertex load chain per frame).
 __global__ __launch_bounds__(256) void RankKernel(const unsigned* __restrict__ order, unsigned n,
-                                                  unsigned* __restrict__ rank) {
+                                                  const float* __restrict__ vertices, unsigned* __restrict__ rank,
+                                                  float* __restrict__ svertices) {
     const unsigned i = blockIdx.x * 256 + threadIdx.x;
     if (i < n) {
-        rank[order[i]] = i;
+        const unsigned id = order[i];
+        rank[id] = i;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            svertices[9ull * i + k] = vertices[9ull * id + k];
+        }
     }
 }
 
@@ -96,7 +103,8 @@ void Check(hipError_t e, const char* what) {
 }  // namespace
 
 void BuildSpatialOrder(const float* d_vertices, std::uint64_t n, const Camera& camera, unsigned* d_order,
-                       unsigned* d_rank, hipStream_t stream, hipEvent_t ev_begin, hipEvent_t ev_end) {
+                       unsigned* d_rank, float* d_svertices, hipStream_t stream, hipEvent_t ev_begin,
+                       hipEvent_t ev_end) {
     if (n == 0) {
         return;
     }
@@ -127,7 +135,8 @@ void BuildSpatialOrder(const float* d_vertices, std::uint64_t n, const Camera& c
         // stable LSD radix sort: equal codes keep id order, so the order is unique
         Check(rocprim::radix_sort_pairs(temp, temp_bytes, keys, keys_sorted, ids, d_order, un, 0, 32, stream),
               "rocprim::radix_sort_pairs");
-        hipLaunchKernelGGL(RankKernel, dim3(blocks), dim3(256), 0, stream, d_order, un, d_rank);
+        hipLaunchKernelGGL(RankKernel, dim3(blocks), dim3(256), 0, stream, d_order, un, d_vertices, d_rank,
+                           d_svertices);
         Check(hipGetLastError(), "RankKernel launch");
         if (ev_end != nullptr) {
             Check(hipEventRecord(ev_end, stream), "hipEventRecord(order build)");

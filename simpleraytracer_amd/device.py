@@ -177,7 +177,7 @@ class DeviceScene:
         callable (srtTraceBatchAsync): frame f's sample offsets offsets[f] ((rows, W, 2) float32)
         and its output outs[f] ((rows, W) int32 hit ids with ids=True, else (rows, W, 4) float32
         RGBA). Every frame gets the whole per-frame work; the cull variant launches each stage
-        once for the batch. row_interleave P > 1: the band is tile rows row_begin / 32 + k P of
+        once for the batch. row_interleave P > 1: the band is tile rows row_begin / 16 + k P of
         the frame (bands.interleaved_range). Checked once here; the buffers must stay alive
         while it is used."""
         if row_count is None:

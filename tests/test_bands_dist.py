@@ -14,7 +14,7 @@ import sys
 import numpy as np
 import pytest
 
-from simpleraytracer_amd.bands import band_range, band_rows
+from simpleraytracer_amd.bands import TILE_ROWS, band_range, band_rows
 
 
 @pytest.mark.parametrize("h", [1, 2, 7, 37, 135, 1080, 2160])
@@ -231,18 +231,18 @@ def test_interleaved_partition_covers_frame_once(h, p):
         fr = interleaved_frame_rows(h, p, r)
         assert count == len(fr) <= interleaved_band_rows(h, p)
         if count:
-            assert begin == r * 32 == fr[0]
+            assert begin == r * TILE_ROWS == fr[0]
             local = np.arange(count)  # the kernels' FrameRow(row_begin, P, local)
-            assert np.array_equal(begin + local + local // 32 * 32 * (p - 1), fr)
+            assert np.array_equal(begin + local + local // TILE_ROWS * TILE_ROWS * (p - 1), fr)
 
 
 def interleaved_frame(ids, g, height):
     """Frame g of a band-major batch of interleaved bands, by ShadeIdsKernel's interleaved index
-    expression (render.hip): t = y / 32, band = t % P, local = (t / P) * 32 + y % 32."""
+    expression (render.hip): t = y / T, band = t % P, local = (t / P) * T + y % T (T = TILE_ROWS)."""
     bands, frames, b, w = ids.shape
     y = np.arange(height)
-    t = y // 32
-    band, local = t % bands, t // bands * 32 + y % 32
+    t = y // TILE_ROWS
+    band, local = t % bands, t // bands * TILE_ROWS + y % TILE_ROWS
     return np.asarray(ids)[band, g, local]
 
 
@@ -280,8 +280,8 @@ def _interleaved_worker(rank, world, port, scene_path, w, h, frames, out_dir):
     batch = torch.full((frames, B, w), -5, dtype=torch.int32)
     offs = [np.random.default_rng(3000 + f).random((h, w, 2), dtype=np.float32) for f in range(frames)]
     for f in range(frames):
-        for k in range(0, len(fr), 32):  # one tile row (contiguous frame rows) at a time
-            r0, n = int(fr[k]), min(32, len(fr) - k)
+        for k in range(0, len(fr), TILE_ROWS):  # one tile row (contiguous frame rows) at a time
+            r0, n = int(fr[k]), min(TILE_ROWS, len(fr) - k)
             img = oracle.render(w, h, offs[f], row_begin=r0, row_count=n, threads=1)
             batch[f, k:k + n] = torch.from_numpy(img[r0:r0 + n, :, 3].astype(np.int32))
     ids, work = gather_band_batch(batch, h, dst=0, async_op=True, interleaved=True)

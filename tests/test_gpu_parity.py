@@ -758,7 +758,7 @@ def test_trace_batch_c3_band_of_8(gpu, scenes):
 @pytest.mark.parametrize("world", [2, 3, 4, 8])
 @pytest.mark.parametrize("mode", [CULL_MODES[0], CULL_MODES[3]])
 def test_interleaved_bands_bitwise(gpu, scenes, monkeypatch, world, mode):
-    """Interleaved bands (the frame's 32-row tile rows dealt round-robin, row_interleave = P):
+    """Interleaved bands (the frame's 16-row tile rows dealt round-robin, row_interleave = P):
     every rank's batched trace of its rows (hit ids and RGBA), then the gathered band-major ids
     shaded with the interleaved layout (srtShadeBandsAsync), equal the brute-force frame bit for
     bit; 170 rows leave a partial last tile row; forced list overflow streams records in a band."""
