@@ -177,15 +177,23 @@ __device__ float4 ScreenBox(const float c[9]) {
         return unbounded;
     }
     double xlo = 1e300, xhi = -1e300, ylo = 1e300, yhi = -1e300;
+    const double dv[3] = {dBC, dCA, dAB};  // corner v's determinant: lines (v + 1) % 3, (v + 2) % 3
     for (int v = 0; v < 3; ++v) {
         const int i = (v + 1) % 3, j = (v + 2) % 3;  // corner opposite edge v: lines i and j
-        const double d = gx[i] * gy[j] - gy[i] * gx[j];
+        // One division per corner: x, y and the pads multiply by 1 / d, which adds ~2 ulp (4e-16)
+        // of relative error to x and y, far inside the 1e-12 pads (four divisions per corner
+        // before). d is a nonzero difference of exact products of floats, so |d| >= 2^-298 and
+        // 1 / d is finite; the guard keeps a NaN corner (0 x inf), which fmin / fmax would drop,
+        // from ever shrinking the box.
+        const double inv = 1.0 / dv[v], ainv = fabs(inv);
+        if (!(ainv < 1e300)) {
+            return unbounded;
+        }
         const double tx1 = -k[i] * gy[j], tx2 = k[j] * gy[i];
         const double ty1 = -gx[i] * k[j], ty2 = gx[j] * k[i];
-        const double x = (tx1 + tx2) / d, y = (ty1 + ty2) / d;
-        const double ad = fabs(d);
-        const double px = 1e-12 * ((fabs(tx1) + fabs(tx2)) / ad + fabs(x)) + 1e-300;
-        const double py = 1e-12 * ((fabs(ty1) + fabs(ty2)) / ad + fabs(y)) + 1e-300;
+        const double x = (tx1 + tx2) * inv, y = (ty1 + ty2) * inv;
+        const double px = 1e-12 * ((fabs(tx1) + fabs(tx2)) * ainv + fabs(x)) + 1e-300;
+        const double py = 1e-12 * ((fabs(ty1) + fabs(ty2)) * ainv + fabs(y)) + 1e-300;
         xlo = fmin(xlo, x - px);
         xhi = fmax(xhi, x + px);
         ylo = fmin(ylo, y - py);
@@ -1206,13 +1214,14 @@ __device__ __forceinline__ void PacketBatch(CullShared& sh, const Box& bb, const
 #pragma unroll
             for (int u = 0; u < kPacketIlp; ++u) {
                 const unsigned kk = min(k + u, k_end - 1u);
-                const uint2 e = pkb[kk];  // one address: a broadcast read
                 // ranges ending before packet kk: lane kk / 2's prefix, plus its first packet's ends
                 const int src = static_cast<int>(kk >> 1);
                 unsigned z = static_cast<unsigned>(__builtin_amdgcn_readlane(static_cast<int>(za), src));
                 if (kk & 1u) {
                     z += static_cast<unsigned>(__builtin_amdgcn_readlane(static_cast<int>(ca), src));
                 }
+                const uint2 e = pkb[kk];  // one address: a broadcast read (from the scan's registers by
+                                          // readlane: 2 VGPR spills, measured 3 % slower)
                 const unsigned g = w0 + kk * kWave + static_cast<unsigned>(lane);
                 const unsigned sl = min(__builtin_amdgcn_mbcnt_hi(e.y, __builtin_amdgcn_mbcnt_lo(e.x, 0u)) + z,
                                         last_slot);
@@ -1334,20 +1343,28 @@ __device__ void WaveScanOrdered(unsigned* a, int n, bool reverse, int lane) {
     }
 }
 
-// One block per tile (bx, by).
+// One block per kInfoTiles vertically adjacent tiles: tiles (bx, kInfoTiles by + k), k = wave /
+// kInfoWaves (a 64 x 16 tile alone is too little work for a 256-thread block: 4 loads per thread).
+constexpr int kInfoTiles = 2;
 __device__ __forceinline__ void TileInfoBlock(const BinParams& p, int bx, int by) {
     constexpr int kWaves = kBinThreads / kWave;
-    constexpr int kPer = kWave * kTileRows / kBinThreads;  // offsets per thread (8)
+    constexpr int kInfoWaves = kWaves / kInfoTiles;             // waves per tile
+    constexpr int kPer = kTileRows / kInfoWaves;                 // offsets per thread (8)
+    static_assert(kWaves % kInfoTiles == 0 && kTileRows % kInfoWaves == 0, "tile info block shape");
     __shared__ Box boxes[kWaves];
-    __shared__ unsigned irregular;
+    __shared__ unsigned irregular[kInfoTiles];
     __shared__ unsigned out_of_range;
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
     const int wave = tid / kWave;
+    const int sub = wave / kInfoWaves, w2 = wave % kInfoWaves;
+    const int ty = by * kInfoTiles + sub;  // this wave's tile row (may be past the band: no write)
     const int x0 = bx * kWave;
-    const int y0 = by * kTileRows;
+    const int y0 = min(ty * kTileRows, p.row_count - 1);
+    if (tid < kInfoTiles) {
+        irregular[tid] = 0u;
+    }
     if (tid == 0) {
-        irregular = 0u;
         out_of_range = 0u;
     }
     // All loads first (clamped addresses: duplicates of real pixels), then the box. Same
@@ -1357,14 +1374,14 @@ __device__ __forceinline__ void TileInfoBlock(const BinParams& p, int bx, int by
     float2 o[kPer];
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
-        const int yy = min(y0 + wave + k * kWaves, p.row_count - 1);
+        const int yy = min(y0 + w2 + k * kInfoWaves, p.row_count - 1);
         o[k] = p.offsets[static_cast<size_t>(yy) * p.width + xx];
     }
     Box box{__builtin_inff(), -__builtin_inff(), __builtin_inff(), -__builtin_inff()};
     bool regular = true, in_range = true;
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
-        const int yy = min(y0 + wave + k * kWaves, p.row_count - 1);
+        const int yy = min(y0 + w2 + k * kInfoWaves, p.row_count - 1);
         const float fx = (static_cast<float>(xx) + o[k].x) / p.wf;
         const float fy = (static_cast<float>(FrameRow(p.row_begin, p.row_interleave, yy)) + o[k].y) / p.hf;
         box = Box{fminf(box.xlo, fx), fmaxf(box.xhi, fx), fminf(box.ylo, fy), fmaxf(box.yhi, fy)};
@@ -1374,40 +1391,40 @@ __device__ __forceinline__ void TileInfoBlock(const BinParams& p, int bx, int by
     }
     box = WaveReduceBox(box);
     const bool wave_regular = __all(regular);
-    const bool wave_in_range = __all(in_range);
+    const bool wave_in_range = __all(in_range) || ty >= p.tiles_y;  // a tile past the band: no tag
     __syncthreads();  // `irregular`, `out_of_range` initialised
     if (lane == 0) {
         boxes[wave] = box;
         if (!wave_regular) {
-            irregular = 1u;
+            irregular[sub] = 1u;
         }
         if (!wave_in_range) {
             out_of_range = 1u;
         }
     }
     __syncthreads();
-    if (tid == 0) {
-        box = boxes[0];
+    if (lane == 0 && w2 == 0 && ty < p.tiles_y) {  // the tile's first wave
+        box = boxes[wave];
 #pragma unroll
-        for (int w = 1; w < kWaves; ++w) {
-            const Box b = boxes[w];
+        for (int w = 1; w < kInfoWaves; ++w) {
+            const Box b = boxes[wave + w];
             box = Box{fminf(box.xlo, b.xlo), fmaxf(box.xhi, b.xhi), fminf(box.ylo, b.ylo), fmaxf(box.yhi, b.yhi)};
         }
         TileInfo ti;
         ti.box = make_float4(box.xlo, box.xhi, box.ylo, box.yhi);
         ti.ox = o0.x;
         ti.oy = o0.y;
-        ti.regular = irregular == 0u ? 1u : 0u;
+        ti.regular = irregular[sub] == 0u ? 1u : 0u;
         ti.usable = ScreenBoxUsable(box) ? 1u : 0u;
-        const unsigned tile = by * p.tiles_x + bx;
+        const unsigned tile = ty * p.tiles_x + bx;
         p.tile_info[tile] = ti;
         p.counts[tile] = 0u;  // the bin kernel runs after this one (stream order)
         if (tile == 0) {
             p.counts[p.tiles_x * p.tiles_y] = 0u;  // large list
         }
-        if (out_of_range != 0u) {
-            *p.range_tag = p.gen;  // this frame's bin blocks reduce the tile boxes (BinTileBounds)
-        }
+    }
+    if (tid == 0 && out_of_range != 0u) {
+        *p.range_tag = p.gen;  // this frame's bin blocks reduce the tile boxes (BinTileBounds)
     }
 }
 
@@ -1486,9 +1503,6 @@ __device__ __forceinline__ void ItemChunks(unsigned cand, unsigned flags, unsign
     nch = full ? 1u : min(static_cast<unsigned>(kMaxChunks), max(1u, (cand + (1u << shift) - 1u) >> shift));
     const unsigned per = cand >> (31u - __builtin_clz(nch));  // ~ candidates per chunk
     bucket = full ? 63u : (per == 0u ? 0u : 32u - __builtin_clz(per));
-#ifdef SRT_EXP_SPATIAL  // measurement builds only: one bucket (list ~ in tile order)
-    bucket = 0u;
-#endif
 }
 // Called by every thread of the order block; start = 64 LDS words, cnt / meta = tiles LDS
 // words / bytes, sum = 2 LDS words. (1) lengths + tile flags into LDS, the candidate total;
@@ -1709,7 +1723,7 @@ std::size_t BinLdsBytes(int nx, int ny) {
 
 // Records and bins of a frame in one launch (the binned cull path). Block b owns spatial
 // positions [256 b, 256 b + 256) (the scene's Morton order, so a block's records fall in few
-// tiles). Each thread computes the record of its position (triangle order[i]) in registers and
+// tiles; two records per thread, 98 VGPRs, measured 5 us slower). Each thread computes the record of its position (triangle order[i]) in registers and
 // writes, by position, its quantized box (the FULL stream's input) and its 64-B cull record (the
 // trace's only record reads), and its shading normal by id. The cull record is skipped when no
 // trace of this band can read it: with every offset of the frame in [0, 1] (no tile block tagged
@@ -1895,14 +1909,7 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(c
     float ox = 0.f, oy = 0.f;
     CullSource src{nullptr, nullptr, 0u, 0u, 0u, true};
     if (p.work != nullptr) {
-#ifdef SRT_EXP_SPATIAL  // measurement builds only: XCD (b % 8) takes a contiguous eighth of the list
-        const unsigned d = (blockIdx.x % 8u) * ((gridDim.x + 7u) / 8u) + blockIdx.x / 8u;
-        if (d >= gridDim.x) {
-            return;
-        }
-#else
         const unsigned d = blockIdx.x;  // < descs: the list, then end marks
-#endif
         const uint4 w0 = p.work[2 * d], w1 = p.work[2 * d + 1];
         if (w0.x == kWorkEnd) {
             return;
@@ -2843,14 +2850,15 @@ hipError_t LaunchCullFrames(const CullFrame* frames, std::size_t count, std::uin
     const unsigned z = static_cast<unsigned>(count);
     const unsigned gx = static_cast<unsigned>(tb.f[0].tiles_x), gy = tb.f[0].tiles / gx;
     // Tile info; records + bins (every padded position: the FULL stream reads them all); the
-    // trace work list; the trace: one block per work descriptor.
-    Launch(TileInfoKernel, dim3(gx, gy, z), dim3(kBinThreads), stream, ev.prep_begin, ev.prep_end, bb);
+    // trace work list; the trace: one block per work descriptor (grid z = frame; interleaving the
+    // frames' descriptors so every frame's heaviest work starts first measured no faster).
+    Launch(TileInfoKernel, dim3(gx, (gy + kInfoTiles - 1) / kInfoTiles, z), dim3(kBinThreads), stream, ev.prep_begin,
+           ev.prep_end, bb);
     const unsigned blocks = (pb.f[0].prep.n_pad + kBinThreads - 1) / kBinThreads;
     LaunchLds(PrepareBinKernel, dim3(blocks, 1, z), dim3(kBinThreads),
               BinLdsBytes(static_cast<int>(gx), static_cast<int>(gy)), stream, ev.bin_begin, nullptr, pb);
     Launch(WorkOrderKernel, dim3(1, 1, z), dim3(1024), stream, nullptr, ev.bin_end, bb);
-    Launch(TraceCullKernel, dim3(frames[0].bins->descs, 1, z), dim3(kWave * kCullWaves), stream,
-           ev.begin, ev.end, tb);
+    Launch(TraceCullKernel, dim3(frames[0].bins->descs, 1, z), dim3(kWave * kCullWaves), stream, ev.begin, ev.end, tb);
     return hipGetLastError();
 }
 
