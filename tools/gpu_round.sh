@@ -6,7 +6,7 @@
 # host-cost probe of the band step (one-rank RCCL). Every GPU step has its own time limit; a crash-type exit ends the script
 # (tests/lib.sh run). Output under gpurun_out/; copy what is judged into profiles/.
 source "$(dirname "$0")/gpu_lib.sh"
-STEPS=${STEPS:-tests,smoke,bench,rehearse,prof,pmc,host}
+STEPS=${STEPS:-tests,smoke,bench,c5,rehearse,prof,pmc,host}
 KERNEL_RE=${KERNEL_RE:-TraceCullKernel}
 KEY=${KEY:-"soup-100k 1920x1080 1spp|cull"}
 Q=(--steps 50 --warmup 5 --queues 1 --batch 1 --no-extras --no-cpu-baseline)  # one frame per dispatch
@@ -19,6 +19,10 @@ fi
 if [[ $STEPS == *bench* ]]; then
     run bench 600 python bench.py
     run bench_driver_shape 300 python bench.py --steps 20 --warmup 5
+fi
+if [[ $STEPS == *c5* ]]; then
+    run bench_c5 600 python bench.py --width 3840 --height 2160 --triangles 1000000 --steps 300 --warmup 5 \
+        --no-extras --no-cpu-baseline
 fi
 if [[ $STEPS == *rehearse* ]]; then
     for n in 2 4; do
