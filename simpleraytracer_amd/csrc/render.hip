@@ -794,10 +794,14 @@ constexpr int kCullR = kBlockRows / kCullWaves;  // rays per lane
 #ifndef SRT_PACKET_BATCH
 #define SRT_PACKET_BATCH 128
 #endif
+#ifndef SRT_LANE_PIXELS
+#define SRT_LANE_PIXELS 2  // packet walk: consecutive range pixels per lane (one record read for them)
+#endif
 #ifndef SRT_PACKET_ILP
-#define SRT_PACKET_ILP 2  // packet walk: packets evaluated together per wave (independent chains)
+#define SRT_PACKET_ILP 1  // packet walk: packets evaluated together per wave (independent chains)
 #endif
 constexpr int kPacketBatch = SRT_PACKET_BATCH;  // candidates gathered per packet-walk batch
+constexpr unsigned kLanePixels = SRT_LANE_PIXELS;
 constexpr int kSlices = (kPacketBatch + kCullThreads - 1) / kCullThreads;  // batch entries per thread
 constexpr int kStreamStep = kCullThreads;        // FULL stream: records per block per step
 static_assert((kPacketBatch % kCullThreads == 0 || kCullThreads % kPacketBatch == 0) && kPacketBatch <= 256,
@@ -1091,8 +1095,9 @@ __device__ __forceinline__ void PacketBatch(CullShared& sh, const Box& bb, const
             pass[e] = c0 <= c1 && r0 <= r1;
             if (pass[e]) {
                 npk[e] = static_cast<unsigned>((c1 - c0 + 1) * (r1 - r0 + 1));  // pixels of the range
+                npk[e] = (npk[e] + kLanePixels - 1u) / kLanePixels;  // stream units: one lane's pixels
                 bits[e] = (static_cast<unsigned>(r0) << 9) + (static_cast<unsigned>(c0) << 3) |
-                          static_cast<unsigned>(c1 - c0 + 1) << 16;
+                          static_cast<unsigned>(c1 - c0 + 1) << 16 | static_cast<unsigned>(r1 - r0 + 1) << 24;
             }
         }
     }
@@ -1143,7 +1148,7 @@ __device__ __forceinline__ void PacketBatch(CullShared& sh, const Box& bb, const
             const unsigned slot = sbase[e] + wpos[e];
             sh.sv0[slot] = cr[e].a;
             sh.sv1[slot] = cr[e].b;
-            const float rnc = __builtin_amdgcn_rcpf(static_cast<float>(bits[e] >> 16));
+            const float rnc = __builtin_amdgcn_rcpf(static_cast<float>((bits[e] >> 16) & 0xFFu));
             sh.sv2[slot] = make_float4(cr[e].x.x, cr[e].x.y, cr[e].x.z, rnc);
             sh.aux[slot] = make_uint2(pbase[e] + incl[e] - npk[e], bits[e]);
             const unsigned o = pbase[e] + incl[e] - 1u;  // the range's last pixel in the stream
@@ -1209,9 +1214,9 @@ __device__ __forceinline__ void PacketBatch(CullShared& sh, const Box& bb, const
         const unsigned k_begin = wave * npk_w / W, k_end = (wave + 1) * npk_w / W;
 #pragma unroll 1
         for (unsigned k = k_begin; k < k_end; k += kPacketIlp) {
-            PacketPixel px[kPacketIlp];
+            PacketPixel px[kPacketIlp][kLanePixels];
             float4 ra[kPacketIlp], rb[kPacketIlp], rx[kPacketIlp];
-            float2 f[kPacketIlp];
+            float2 f[kPacketIlp][kLanePixels];
 #pragma unroll
             for (int u = 0; u < kPacketIlp; ++u) {
                 const unsigned kk = min(k + u, k_end - 1u);
@@ -1231,31 +1236,58 @@ __device__ __forceinline__ void PacketBatch(CullShared& sh, const Box& bb, const
                 rb[u] = sh.sv1[sl];
                 rx[u] = sh.sv2[sl];
                 const uint2 ax = sh.aux[sl];
-                const unsigned q = g - ax.x;  // pixel of the range, row-major
+                const unsigned nc = (ax.y >> 16) & 0xFFu, nr = ax.y >> 24, base = ax.y & 0xFFFFu;
+                const unsigned q = (g - ax.x) * kLanePixels;  // the lane's first pixel of the range, row-major
                 // row = q / nc, exact: q < 1024 and 1 / nc within 1 ulp, so (q + 1/2) / nc is
                 // >= 1/128 from an integer and the product is within 2^-10 of it
                 const unsigned row = static_cast<unsigned>((static_cast<float>(q) + 0.5f) * rx[u].w);
-                const unsigned col = q - __umul24(row, ax.y >> 16);
-                px[u] = PacketPixel{in ? (ax.y & 0xFFFFu) + (row << 9) + (col << 3) : 0u, in};
+                const unsigned col = q - __umul24(row, nc);
+                // pixel q + j: j columns on, wrapping into the next rows (j < kLanePixels, so it
+                // wraps at most j times); past the range's last row when the range's pixel count is
+                // not a multiple of kLanePixels
+#pragma unroll
+                for (int j = 0; j < kLanePixels; ++j) {
+                    unsigned c = col + j, r = row;
+#pragma unroll
+                    for (int w = 0; w < j; ++w) {
+                        const bool wrap = c >= nc;
+                        c = wrap ? c - nc : c;
+                        r = wrap ? r + 1u : r;
+                    }
+                    const bool ok = in && r < nr;
+                    px[u][j] = PacketPixel{ok ? base + (r << 9) + (c << 3) : 0u, ok};
+                }
+            }
+            PacketHit h[kPacketIlp][kLanePixels];
+#pragma unroll
+            for (int u = 0; u < kPacketIlp; ++u) {
+#pragma unroll
+                for (int j = 0; j < kLanePixels; ++j) {
+                    f[u][j] = *reinterpret_cast<const float2*>(fxy + px[u][j].pixb);
+                }
             }
 #pragma unroll
             for (int u = 0; u < kPacketIlp; ++u) {
-                f[u] = *reinterpret_cast<const float2*>(fxy + px[u].pixb);
-            }
-            PacketHit h[kPacketIlp];
 #pragma unroll
-            for (int u = 0; u < kPacketIlp; ++u) {
-                h[u] = EvalPacket(ra[u], rb[u], rx[u], f[u], px[u].in);
+                for (int j = 0; j < kLanePixels; ++j) {
+                    h[u][j] = EvalPacket(ra[u], rb[u], rx[u], f[u][j], px[u][j].in);
+                }
             }
 #pragma unroll
             for (int u = 0; u < kPacketIlp; ++u) {
-                asm volatile("" ::"v"(h[u].key));
+#pragma unroll
+                for (int j = 0; j < kLanePixels; ++j) {
+                    asm volatile("" ::"v"(h[u][j].key));
+                }
             }
 #pragma unroll
             for (int u = 0; u < kPacketIlp; ++u) {
-                if (h[u].hit) {
-                    __hip_atomic_fetch_min(reinterpret_cast<unsigned long long*>(keys + px[u].pixb), h[u].key,
-                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#pragma unroll
+                for (int j = 0; j < kLanePixels; ++j) {
+                    if (h[u][j].hit) {
+                        __hip_atomic_fetch_min(reinterpret_cast<unsigned long long*>(keys + px[u][j].pixb), h[u][j].key,
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
                 }
             }
         }
