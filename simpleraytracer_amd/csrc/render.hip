@@ -1419,7 +1419,7 @@ __device__ __forceinline__ void TileInfoBlock(const BinParams& p, int bx, int by
     };
     if (x0 + kWave <= p.width && (p.width & 1) == 0 && (reinterpret_cast<uintptr_t>(p.offsets) & 15u) == 0) {
         // Whole-width tile, 16-B aligned rows: lane = a column pair of one of two rows, 16 B per
-        // load (1 KB per wave instruction).
+        // load (1 KB per wave instruction). (Nontemporal loads here measured 2.6 % slower.)
         const int xa = x0 + 2 * (lane & (kWave / 2 - 1)), half = lane / (kWave / 2);
         float4 o[kPer / 2];
 #pragma unroll
