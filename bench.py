@@ -8,7 +8,7 @@ rows a9-a13): tile info, record setup and bins, the trace work list, the closest
 (TraceCullKernel; its frame is bit-identical to brute force, DESIGN.md section 5,
 tests/test_gpu_parity.py), shading and the framebuffer store. Nothing is cached across frames.
 
-Each GPU keeps --queues (3) frame queues, each its own DeviceScene, HIP stream and buffers, and a
+Each GPU keeps --queues frame queues (default: 3 at N > 1 and for runs of at most 24 frames, else 2), each its own DeviceScene, HIP stream and buffers, and a
 queue takes --batch frames at a time: up to 8 of them go through one srtTraceBatchAsync call (the
 same per-frame work, one launch per stage for the batch). N = 1: batches of 8 frames, each frame
 shaded into its own RGBA framebuffer; the single_queue pass runs one frame per launch on one
@@ -72,8 +72,9 @@ def parse():
     p.add_argument("--root", default="rotate", choices=["rotate", "fixed"], help="bands: compositing rank")
     p.add_argument("--rows", default="interleaved", choices=["interleaved", "contiguous"],
                    help="bands: each rank's rows, the frame's 16-row tile rows dealt round-robin or one block")
-    p.add_argument("--queues", type=int, default=int(os.environ.get("SRT_BENCH_QUEUES", "3")),
-                   help="frames in flight per GPU (own scene buffers, HIP stream, process group each)")
+    p.add_argument("--queues", type=int, default=int(os.environ.get("SRT_BENCH_QUEUES", "0")),
+                   help="frames in flight per GPU (own scene buffers, HIP stream, process group each); 0 = 3 at "
+                        "N > 1 or when the run is at most one 8-frame batch per queue, else 2")
     p.add_argument("--batch", type=int, default=int(os.environ.get("SRT_BENCH_BATCH", "0")),
                    help="frames per batch: traced in srtTraceBatchAsync calls of <= 8 frames and, bands at "
                         "N > 1, gathered in one collective and shaded in one launch; 0 = 16 at N > 1, 8 at N = 1")
@@ -479,6 +480,12 @@ def leg_summary(r):
 
 def main():
     a = parse()
+    if a.queues <= 0:
+        # Measured at C3 (profiles/r02/queues): long runs 2 / 3 / 1 queues 112.3 / 106.6 / 95.8
+        # Grays/s (with 8-frame launches two queues already fill the chip, a third adds L2
+        # contention); the driver's 20-step runs 91.8 / 96.9 / 83.6 (3 queues take one batch each,
+        # 2 queues leave a 2-frame tail batch each).
+        a.queues = 3 if a.gpus > 1 or -(-a.steps // 3) <= 8 else 2
     if a.batch <= 0:
         # 16 frames per gather at N > 1, 8 per launch at N = 1, at most one batch per queue's
         # share of the run: a short run (the driver's 20 steps over 3 queues) then traces, gathers
