@@ -480,11 +480,13 @@ def leg_summary(r):
 
 def main():
     a = parse()
+    leg_queues = a.queues if a.queues > 0 else 3  # the secondary legs (random offsets, Cornell, variants)
     if a.queues <= 0:
         # Measured at C3 (profiles/r02/queues): long runs 2 / 3 / 1 queues 112.3 / 106.6 / 95.8
         # Grays/s (with 8-frame launches two queues already fill the chip, a third adds L2
         # contention); the driver's 20-step runs 91.8 / 96.9 / 83.6 (3 queues take one batch each,
-        # 2 queues leave a 2-frame tail batch each).
+        # 2 queues leave a 2-frame tail batch each). The secondary legs keep 3: random offsets
+        # 78.1 vs 87.7, Cornell 143 vs 154, the BVH 15.1 vs 20.8 Grays/s with 2 vs 3.
         a.queues = 3 if a.gpus > 1 or -(-a.steps // 3) <= 8 else 2
     if a.batch <= 0:
         # 16 frames per gather at N > 1, 8 per launch at N = 1, at most one batch per queue's
@@ -533,14 +535,14 @@ def main():
             legs["secondary_error"] = f"{type(e).__name__}: {e}"
     if world == 1 and extras:
         if a.offsets == "uniform":  # per-pixel jitter: the irregular-offset path
-            o = Pipeline(ctx, path, "bands", a.queues, a.variant, "random", batch=a.batch)
+            o = Pipeline(ctx, path, "bands", leg_queues, a.variant, "random", batch=a.batch)
             rr = o.run(min(a.steps, 1000), a.warmup)
             rt2 = o.run(min(a.steps, 300), 2, queues=1, timing=True)
             o.close()
             legs["offsets_random"] = {**leg_summary(rr), "trace_kernel_ms": round(rt2["trace_ms"], 5),
                                       "note": "seeded U[0,1) per-pixel sample offsets (every tile irregular)"}
         if a.scene == "soup":  # C2: the Cornell box at the same resolution
-            o = Pipeline(ctx, ctx.scene_path("cornell"), "bands", a.queues, a.variant, a.offsets, batch=a.batch)
+            o = Pipeline(ctx, ctx.scene_path("cornell"), "bands", leg_queues, a.variant, a.offsets, batch=a.batch)
             legs["c2_cornell"] = {**leg_summary(o.run(min(a.steps, 1000), a.warmup)),
                                   "workload": workload_name(a, "cornell")}
             o.close()
@@ -551,7 +553,7 @@ def main():
         if a.brute_steps > 0:  # the other exact accelerator, same frame
             for v in ("cull", "bvh"):
                 if v != a.variant:
-                    o = Pipeline(ctx, path, "bands", a.queues, v, a.offsets)
+                    o = Pipeline(ctx, path, "bands", leg_queues, v, a.offsets)
                     vr = o.run(min(a.steps, 1000), a.warmup)
                     vt = o.run(min(a.steps, 300), 2, queues=1, timing=True)
                     o.close()
