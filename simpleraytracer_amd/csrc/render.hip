@@ -1383,7 +1383,10 @@ __device__ void WaveScanOrdered(unsigned* a, int n, bool reverse, int lane) {
 
 // One block per kInfoTiles vertically adjacent tiles: tiles (bx, kInfoTiles by + k), k = wave /
 // kInfoWaves (a 64 x 16 tile alone is too little work for a 256-thread block: 4 loads per thread).
-constexpr int kInfoTiles = 2;
+#ifndef SRT_INFO_TILES
+#define SRT_INFO_TILES 2  // 4: one wave per tile, 510 blocks: tile info 5.2 -> 5.6 us, throughput +1 % (noise)
+#endif
+constexpr int kInfoTiles = SRT_INFO_TILES;
 __device__ __forceinline__ void TileInfoBlock(const BinParams& p, int bx, int by) {
     constexpr int kWaves = kBinThreads / kWave;
     constexpr int kInfoWaves = kWaves / kInfoTiles;             // waves per tile
@@ -1947,7 +1950,12 @@ __global__ __launch_bounds__(kBinThreads) void PrepareBinKernel(const PrepareBin
 // launch fewer but the ~5 us single-block tail inside the bin launch cost 10 % of the
 // three-queue throughput at C3 (60.9 vs 67.3 Grays/s; plain, no-wait and two-level arrivals
 // alike: profiles/r02/ab_order/).
-__global__ __launch_bounds__(1024) void WorkOrderKernel(const BinBatch batch) {
+#ifndef SRT_ORDER_THREADS
+#define SRT_ORDER_THREADS 1024
+#endif
+constexpr int kOrderThreads = SRT_ORDER_THREADS;  // the work-order block (kOrderUnroll tiles per thread per
+                                                  // pass; 512 / 256 threads: 9.0 / 12.2 instead of 8.1 us)
+__global__ __launch_bounds__(kOrderThreads) void WorkOrderKernel(const BinBatch batch) {
     __shared__ unsigned start[64];
     __shared__ unsigned sum[2];
     __shared__ unsigned cnt[kMaxBinTiles];
@@ -2944,7 +2952,7 @@ hipError_t LaunchCullFrames(const CullFrame* frames, std::size_t count, std::uin
     const unsigned blocks = (pb.f[0].prep.n_pad + kBinThreads - 1) / kBinThreads;
     LaunchLds(PrepareBinKernel, dim3(blocks, 1, z), dim3(kBinThreads),
               BinLdsBytes(static_cast<int>(gx), static_cast<int>(gy)), stream, ev.bin_begin, nullptr, pb);
-    Launch(WorkOrderKernel, dim3(1, 1, z), dim3(1024), stream, nullptr, ev.bin_end, bb);
+    Launch(WorkOrderKernel, dim3(1, 1, z), dim3(kOrderThreads), stream, nullptr, ev.bin_end, bb);
     Launch(TraceCullKernel, dim3(frames[0].bins->descs, 1, z), dim3(kWave * kCullWaves), stream, ev.begin, ev.end, tb);
     return hipGetLastError();
 }
