@@ -1,32 +1,33 @@
 #!/usr/bin/env python3
 """Headline benchmark: Mrays/s rendering the 100k-triangle synthetic soup at 1920x1080, 1 spp.
 
-    python bench.py [--gpus N --steps K --warmup W]        (N > 1: launched by torch.distributed.run)
+    python bench.py [--gpus N --steps K --warmup W]
 
-One step = one complete frame of the hot path on device-resident inputs (SURVEY.md section 8
-rows a9-a13): tile info, record setup and bins, the trace work list, the closest-hit trace
-(TraceCullKernel; its frame is bit-identical to brute force, DESIGN.md section 5,
-tests/test_gpu_parity.py), shading and the framebuffer store. Nothing is cached across frames.
+Runs with or without a launcher:
+  * no WORLD_SIZE (or WORLD_SIZE=1): one process drives all N GPUs (devices 0..N-1) through the
+    library's frame engine, one C++ worker thread per GPU, RCCL communicators from ncclCommInitAll;
+  * python -m torch.distributed.run --nproc-per-node N bench.py --gpus N: one rank per GPU; the
+    ranks share an RCCL unique id over torch.distributed (gloo: control plane only -- barriers, the
+    id, max-over-ranks) and the engine's native communicator carries the data.
+SRT_BENCH_ONE_DEVICE=1 puts every "device" on GPU 0 (single process: the bands are then exchanged
+by device copies -- the multi-GPU rehearsal on a one-GPU box).
 
-Each GPU keeps --queues frame queues (default: 3 at N > 1 and for runs of at most 24 frames, else 2), each its own DeviceScene, HIP stream and buffers, and a
-queue takes --batch frames at a time: up to 8 of them go through one srtTraceBatchAsync call (the
-same per-frame work, one launch per stage for the batch). N = 1: batches of 8 frames, each frame
-shaded into its own RGBA framebuffer; the single_queue pass runs one frame per launch on one
-queue (the per-frame latency).
+One step = one batch of --frames-per-step frames (default 16: a 16-frame jitter sequence of the
+same view), each frame a complete pass of the hot path on device-resident inputs (SURVEY.md
+section 8 rows a9-a13): tile info, record setup and bins, the trace work list, the closest-hit
+trace (TraceCullKernel; bit-identical to brute force), shading and the
+framebuffer store. Nothing is cached across frames. Each GPU keeps --queues batches in flight.
 
-Multi-GPU, one rank per GPU over RCCL:
-  --mode bands (default; BASELINE config C4): every frame is split into P bands -- the frame's
-      16-row tile rows dealt round-robin (--rows interleaved, default) or contiguous blocks --,
-      rank r traces its band (hit ids, 4 B per pixel; deferred shading, bit-identical), a batch
-      of 16 frames' bands is gathered over RCCL in ONE collective (a torch-RCCL gather costs
-      ~40 us of host time per call, more than a band's trace: tools/host_probe_bands.py) to
-      the batch's compositor, rank (batch index) % P (--root rotate, default) or rank 0 (--root
-      fixed), which shades the 16 frames in one launch (srtShadeBandsAsync). value = frames x W x
-      H / the max-over-ranks time: "scaling": "strong". After the timed loop every compositing
-      rank compares its last batch's frames with a one-GPU render bit for bit ("verified").
-  --mode frames: every rank renders whole frames of a temporal-jitter sequence (no collective);
-      "scaling": "weak". Reported beside the bands line at N > 1 ("frames").
-At N = 1 the two modes coincide (one band = the frame, shaded in the trace).
+Multi-GPU (BASELINE config C4), --mode bands (default): every frame is split
+into N row bands (the frame's 16-row tile rows dealt round-robin, --rows interleaved), GPU d traces
+band d of every frame of the batch (hit ids, 4 B per pixel), the bands go to the frames'
+compositors over RCCL -- --exchange alltoall (default): frame f of a batch to GPU f % N, the
+batch's N gathers fused into one ncclSend/ncclRecv group --, and each compositor shades its frames
+in one launch (deferred shading, bit-identical). value = frames x W x H / the max-over-ranks time
+of the timed steps: "scaling": "strong". --mode frames: every GPU renders whole frames of its own
+(no exchange): "scaling": "weak" (a leg of the N > 1 line). After the timed steps every compositor
+compares its last batches' frames with a single-GPU render by another kernel, bit for bit
+("verified").
 
 Prints ONE JSON line on rank 0 (fields in DESIGN.md section 6).
 """
@@ -48,9 +49,9 @@ FP32_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md chip table (spec, vector fp32
 SIMDS, CLOCK_GHZ = 1024, 2.4  # 256 CUs x 4 SIMD-32; wave64 VALU issue = 2 cycles per instruction
 EDGE_BYTES_PER_TRI = 36      # 9 fp32 edge coefficients per ray-triangle test
 CULL_RECORD_BYTES = 64       # one cull record per triangle (render.hip CullRecord)
+VERTEX_BYTES = 36            # 9 fp32 per triangle, read by the record pass
 PIXEL_IO_BYTES = 8 + 16      # sample offsets in + RGBA out per ray
 FLOPS_PER_TEST = 12          # 3 edge functions x 2 FMA
-GOLDEN = 0.6180339887498949  # temporal jitter sequence step
 KERNEL_NAMES = {"lds": "TraceLdsKernel", "scalar": "TraceScalarKernel", "cull": "TraceCullKernel",
                 "bvh": "TraceBvhKernel"}
 PROFILES = REPO / "profiles"
@@ -59,27 +60,25 @@ PROFILES = REPO / "profiles"
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    # 3000 frames = ~0.1 s timed at C3: 1000 frames (36 ms) read ~2.5 % low, the clocks still
-    # settling (profiles/r01/ab/README.md)
-    p.add_argument("--steps", type=int, default=3000)
-    p.add_argument("--warmup", type=int, default=20)
+    # 200 steps x 16 frames = 3200 frames, ~60 ms timed at C3 on one GPU
+    p.add_argument("--steps", type=int, default=200, help="timed steps (batches of --frames-per-step frames)")
+    p.add_argument("--warmup", type=int, default=4, help="untimed steps first")
+    p.add_argument("--frames-per-step", type=int, default=16, help="frames per step = per batch")
     p.add_argument("--width", type=int, default=1920)
     p.add_argument("--height", type=int, default=1080)
     p.add_argument("--scene", default="soup", choices=["soup", "cornell", "triangle"])
     p.add_argument("--triangles", type=int, default=100_000)
     p.add_argument("--variant", default=os.environ.get("SRT_BENCH_VARIANT", "cull"), choices=list(KERNEL_NAMES))
     p.add_argument("--mode", default="bands", choices=["bands", "frames"], help="multi-GPU split (module doc)")
-    p.add_argument("--root", default="rotate", choices=["rotate", "fixed"], help="bands: compositing rank")
+    p.add_argument("--exchange", default="alltoall", choices=["alltoall", "rotating", "root"],
+                   help="bands: where frames are composited (module doc)")
     p.add_argument("--rows", default="interleaved", choices=["interleaved", "contiguous"],
-                   help="bands: each rank's rows, the frame's 16-row tile rows dealt round-robin or one block")
-    p.add_argument("--queues", type=int, default=int(os.environ.get("SRT_BENCH_QUEUES", "0")),
-                   help="frames in flight per GPU (own scene buffers, HIP stream, process group each); 0 = 3 at "
-                        "N > 1 or when the run is at most one 8-frame batch per queue, else 2")
-    p.add_argument("--batch", type=int, default=int(os.environ.get("SRT_BENCH_BATCH", "0")),
-                   help="frames per batch: traced in srtTraceBatchAsync calls of <= 8 frames and, bands at "
-                        "N > 1, gathered in one collective and shaded in one launch; 0 = 16 at N > 1, 8 at N = 1")
+                   help="bands: each GPU's rows, the frame's 16-row tile rows dealt round-robin or one block")
+    p.add_argument("--queues", type=int, default=int(os.environ.get("SRT_BENCH_QUEUES", "2")),
+                   help="batches in flight per GPU (own scene buffers and HIP stream each)")
     p.add_argument("--offsets", default="uniform", choices=["uniform", "random"],
                    help="sample offsets: uniform 0.5 (headline) or seeded U[0,1) per-pixel jitter")
+    p.add_argument("--inputs", type=int, default=1, help="distinct resident input images frames cycle through")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample length")
     p.add_argument("--brute-steps", type=int, default=5, help="timed frames of the brute-force LDS kernel (0 = skip)")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -88,293 +87,151 @@ def parse():
     return p.parse_args()
 
 
-def workload_name(a, scene=None, triangles=None):
+def workload_name(a, scene=None, triangles=None, width=None, height=None):
     scene = scene or a.scene
     triangles = triangles or a.triangles
+    w, h = width or a.width, height or a.height
     if scene == "soup":
         tri = f"{triangles // 1000}k" if triangles % 1000 == 0 else str(triangles)
-        return f"soup-{tri} {a.width}x{a.height} 1spp"
-    return f"{scene} {a.width}x{a.height} 1spp"
+        return f"soup-{tri} {w}x{h} 1spp"
+    return f"{scene} {w}x{h} 1spp"
 
 
-def jitter(rank: int) -> float:
-    """Uniform sub-pixel offset of rank r's frames in frames mode (r = 0: 0.5, the headline frame)."""
+def make_offsets(a, kind="uniform", count=1, seed=0x5EED):
+    """(count, H, W, 2) float32 host offsets: uniform 0.5, or seeded U[0, 1) per-pixel jitter."""
     import numpy as np
 
-    return float(np.float32((0.5 + rank * GOLDEN) % 1.0))
+    if kind == "random":
+        rng = np.random.default_rng(seed)
+        return rng.random((count, a.height, a.width, 2), dtype=np.float32)
+    return np.full((count, a.height, a.width, 2), 0.5, dtype=np.float32)
 
 
-def make_offsets(torch, a, dev, value=0.5, kind="uniform", seed=0x5EED):
-    if kind == "random":  # seeded per-pixel jitter, U[0, 1)
-        g = torch.Generator(device="cpu").manual_seed(seed)
-        return torch.rand((a.height, a.width, 2), generator=g, dtype=torch.float32).to(dev)
-    return torch.full((a.height, a.width, 2), value, dtype=torch.float32, device=dev)
-
-
-class Ctx:
-    """This rank's process-wide state: torch, the process groups, the device, the scene files."""
+class Job:
+    """How this process takes part: one process for all GPUs, or one rank of a torchrun job."""
 
     def __init__(self, a):
         import torch
-        import torch.distributed as dist
 
-        import simpleraytracer_amd as srt
+        self.torch = torch
+        env_world = int(os.environ.get("WORLD_SIZE", "1") or 1)
+        self.one_device = bool(os.environ.get("SRT_BENCH_ONE_DEVICE"))
+        self.dist = None
+        if env_world > 1:
+            if env_world != a.gpus:
+                raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={env_world}")
+            import torch.distributed as dist
 
-        self.torch, self.dist, self.srt, self.a = torch, dist, srt, a
-        self.world = int(os.environ.get("WORLD_SIZE", "1"))
-        self.rank = int(os.environ.get("RANK", "0"))
-        local = int(os.environ.get("LOCAL_RANK", "0"))
-        if os.environ.get("SRT_BENCH_ONE_DEVICE"):  # rehearsal of N > 1 ranks on a one-GPU box (with gloo)
-            local = 0
-        if self.world != a.gpus:
-            raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={self.world}")
-        torch.cuda.set_device(local)
-        self.dev = torch.device("cuda", local)
-        self.backend = None
-        self.groups = []
-        if self.world > 1:
-            self.backend = os.environ.get("SRT_BENCH_BACKEND", "nccl")  # gloo: CPU-side rehearsal on one GPU
-            if self.backend == "nccl":
-                dist.init_process_group("nccl", device_id=self.dev)
-            else:
-                dist.init_process_group(self.backend)
-            # one process group (RCCL communicator, NCCL stream) per frame queue: the gathers of
-            # different frames in flight run concurrently
-            self.groups = [dist.new_group(list(range(self.world))) for _ in range(max(1, a.queues))]
+            self.dist = dist
+            self.rank = int(os.environ.get("RANK", "0"))
+            local = 0 if self.one_device else int(os.environ.get("LOCAL_RANK", "0"))
+            dist.init_process_group("gloo")  # control plane; the engine's RCCL communicator moves the data
+            self.world = env_world
+            self.devices = [local]
+        else:
+            self.rank = 0
+            self.world = a.gpus
+            self.devices = [0] * a.gpus if self.one_device else list(range(a.gpus))
+        self.launch = "torchrun" if self.dist is not None else "single-process"
         self.tmp = tempfile.TemporaryDirectory()
         self.paths = {}
 
+    @property
+    def ranked(self):
+        return self.dist is not None
+
     def scene_path(self, kind, triangles=None):
+        import simpleraytracer_amd as srt
+
         key = (kind, triangles)
         if key not in self.paths:
             path = os.path.join(self.tmp.name, f"{kind}_{triangles}_rank{self.rank}.srt")
             if kind == "soup":
-                self.srt.write_scene(path, "soup", triangles)
+                srt.write_scene(path, "soup", triangles)
             else:
-                self.srt.write_scene(path, kind)
+                srt.write_scene(path, kind)
             self.paths[key] = path
         return self.paths[key]
 
+    def engine(self, path, a, mode=None, exchange=None, rows=None, queues=None, batch=None, variant=None,
+               width=None, height=None):
+        from simpleraytracer_amd.engine import FrameEngine, unique_id
+
+        kw = dict(variant=variant or a.variant, queues=queues or a.queues, batch=batch or a.frames_per_step,
+                  rows=rows or a.rows, exchange=exchange or a.exchange, split=mode or a.mode)
+        w, h = width or a.width, height or a.height
+        if not self.ranked:
+            return FrameEngine(path, w, h, devices=self.devices, **kw)
+        return FrameEngine.rank(path, w, h, self.devices[0], self.rank, self.world, self.share_uid(unique_id), **kw)
+
+    def share_uid(self, make):
+        """Rank 0's make() (the RCCL unique id), on every rank."""
+        uid = [make() if self.rank == 0 else None]
+        self.dist.broadcast_object_list(uid, src=0)
+        return uid[0]
+
+    def sync(self):
+        for d in sorted(set(self.devices)):
+            self.torch.cuda.synchronize(d)
+
+    def barrier(self):
+        if self.ranked:
+            self.dist.barrier()
+
     def max_over_ranks(self, x):
-        if self.world == 1:
+        if not self.ranked:
             return x
-        t = self.torch.tensor([x], dtype=self.torch.float64,
-                              device=self.dev if self.backend != "gloo" else "cpu")
+        t = self.torch.tensor([x], dtype=self.torch.float64)
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t.item())
 
-    def barrier(self):
-        if self.world > 1:
-            self.dist.barrier()
-
-
-class Pipeline:
-    """Frames over `queues` frame queues on this rank (module doc). mode "bands": rank r traces
-    band r of every frame (P > 1: hit ids, gathered to the compositor, which shades); mode
-    "frames": whole frames, each rank its own jitter; P == 1: the two coincide."""
-
-    def __init__(self, ctx, path, mode="bands", queues=3, variant="cull", offsets="uniform", rotate=True, batch=1,
-                 rows="interleaved"):
-        from simpleraytracer_amd.bands import (band_range, band_rows, interleaved_band_rows, interleaved_frame_rows,
-                                               interleaved_range)
-
-        torch, a = ctx.torch, ctx.a
-        self.ctx, self.mode, self.variant, self.rotate = ctx, mode, variant, rotate
-        self.W, self.H = a.width, a.height
-        P = ctx.world if mode == "bands" else 1
-        self.P = P
-        self.G = max(1, batch)  # frames per batch: per gather + shading launch at P > 1
-        self.L = min(self.G, ctx.srt.MAX_BATCH)  # frames per batched trace call
-        self.interleave = P if (P > 1 and rows == "interleaved") else 1
-        if self.interleave > 1:
-            self.row_begin, self.row_count = interleaved_range(self.H, P, ctx.rank)
-            self.B = interleaved_band_rows(self.H, P)
-        else:
-            self.row_begin, self.row_count = band_range(self.H, P, ctx.rank) if P > 1 else (0, self.H)
-            self.B = band_rows(self.H, P)
-        self.offsets = make_offsets(torch, a, ctx.dev, jitter(ctx.rank) if mode == "frames" else 0.5, offsets,
-                                    seed=0x5EED + (ctx.rank if mode == "frames" else 0))
-        if self.interleave > 1:  # the band's rows of the frame's offsets, in band order (one copy)
-            rows_t = torch.from_numpy(interleaved_frame_rows(self.H, P, ctx.rank)).to(ctx.dev)
-            self.band_off = self.offsets.index_select(0, rows_t).contiguous()
-        else:
-            self.band_off = self.offsets[self.row_begin:self.row_begin + self.row_count]
-        self.timing = False
-        self.queues = []
-        for q in range(max(1, queues)):
-            qd = {"scene": ctx.srt.DeviceScene(path, ctx.dev.index), "stream": torch.cuda.Stream(ctx.dev),
-                  "root": None, "index": q, "fill": 0, "traced": 0, "batches": 0, "shaded": 0, "runs": {}}
-            qd["scene"].prepare(self.W, self.H)
-            qd["rgba"] = torch.zeros((self.G, self.H, self.W, 4), dtype=torch.float32, device=ctx.dev)
-            if P > 1:
-                qd["band_ids"] = torch.full((self.G, self.B, self.W), -1, dtype=torch.int32, device=ctx.dev)
-                qd["frame_ids"] = torch.empty(P * self.G * self.B * self.W, dtype=torch.int32, device=ctx.dev)
-                qd["group"] = ctx.groups[q % len(ctx.groups)]
-            self.queues.append(qd)
-        self.triangles = self.queues[0]["scene"].triangles
-        # Grow every queue's frame slots to the largest batched call now (allocation, zero fill):
-        # a batch larger than the warm-up's partial ones must not allocate inside a timed loop.
-        if self.row_count:
-            for q in self.queues:
-                self._batch_run(q, self.L)()
-            torch.cuda.synchronize(ctx.dev)
-
-    def _batch_run(self, q, f, slot=0):
-        """The queue's batched trace of f slots from `slot` (one srtTraceBatchAsync call), bound once."""
-        key = (f, slot)
-        if key not in q["runs"]:
-            sc, st = q["scene"], q["stream"]
-            if self.P > 1:
-                q["runs"][key] = sc.bind_trace_batch([self.band_off] * f, [q["band_ids"][j, :self.row_count]
-                                                                           for j in range(slot, slot + f)],
-                                                     self.row_begin, self.row_count, self.variant, st, ids=True,
-                                                     row_interleave=self.interleave)
-            else:
-                q["runs"][key] = sc.bind_trace_batch([self.offsets] * f, [q["rgba"][j] for j in range(slot, slot + f)],
-                                                     0, self.H, self.variant, st)
-        return q["runs"][key]
-
-    def step(self, k, nq):
-        """Frame k on queue k % nq: into the queue's next batch slot; a full batch is traced
-        (one call for all its frames), then at P > 1 gathered and shaded. With stage timing
-        on, each frame is traced on its own (the single-frame calls bind the HIP events)."""
-        q = self.queues[k % nq]
-        sc, st = q["scene"], q["stream"]
-        j = q["fill"]
-        if self.timing and self.row_count:  # one frame per call: the stage events time one frame
-            self._batch_run(q, 1, j)()
-            q["traced"] = j + 1
-        q["fill"] = j + 1
-        if q["fill"] == self.G:
-            self.flush(q, nq)
-
-    def flush(self, q, nq):
-        """Trace the queue's filled slots (if not yet), then at P > 1 gather them (one collective
-        for all of them) to the batch's compositor, which shades every frame in one launch."""
-        from simpleraytracer_amd.bands import compositor, gather_band_batch
-
-        ctx, torch = self.ctx, self.ctx.torch
-        f = q["fill"]
-        if f == 0:
-            return
-        sc, st = q["scene"], q["stream"]
-        if q["traced"] < f and self.row_count:
-            for slot in range(0, f, self.L):
-                self._batch_run(q, min(self.L, f - slot), slot)()
-        q["fill"] = q["traced"] = 0
-        if self.P == 1:
-            q["root"], q["shaded"] = 0, f
-            return
-        root = compositor(q["batches"] * nq + q["index"], self.P, self.rotate)
-        batch = q["band_ids"][:f]
-        if ctx.backend == "gloo":  # CPU rehearsal: gloo gathers host tensors, synchronously
-            st.synchronize()
-            host_out = torch.empty(self.P * f * self.B * self.W, dtype=torch.int32) if ctx.rank == root else None
-            ids, _ = gather_band_batch(batch.cpu(), self.H, dst=root, group=q["group"], out=host_out,
-                                       interleaved=self.interleave > 1)
-            if ids is not None:
-                dev_ids = q["frame_ids"][:ids.numel()].view(ids.shape)
-                dev_ids.copy_(ids.to(ctx.dev))
-                torch.cuda.synchronize(ctx.dev)
-                ids = dev_ids
-        else:
-            with torch.cuda.stream(st):
-                ids, work = gather_band_batch(batch, self.H, dst=root, group=q["group"], out=q["frame_ids"],
-                                              async_op=True, interleaved=self.interleave > 1)
-                work.wait()  # the queue's stream waits for the gather (ids consumed / slots reusable)
-        if ctx.rank == root:
-            sc.shade_bands(self.offsets, ids, q["rgba"][:f], self.B, stream=st,
-                           interleaved=self.interleave if self.interleave > 1 else 0)
-            q["shaded"] = f
-        q["root"] = root
-        q["batches"] += 1
-
-    def drain(self, nq=None):
-        for q in self.queues[:nq or len(self.queues)]:  # partial batches
-            self.flush(q, nq or len(self.queues))
-        for q in self.queues:
-            q["stream"].synchronize()
-
-    def run(self, steps, warmup, queues=None, timing=False, batch=None):
-        """`steps` timed frames after `warmup` per queue; stage timing binds events on queue 0's
-        scene (use queues=1 then); `batch` (<= the pipeline's) overrides the frames per batch."""
-        G, L = self.G, self.L
-        if batch:
-            self.G = min(batch, G)
-            self.L = min(self.G, L)
-        try:
-            return self._run(steps, warmup, queues, timing)
-        finally:
-            self.G, self.L = G, L
-
-    def _run(self, steps, warmup, queues, timing):
-        torch, ctx = self.ctx.torch, self.ctx
-        nq = min(queues or len(self.queues), len(self.queues))
-        for k in range(warmup * nq):
-            self.step(k, nq)
-        self.drain(nq)
-        sc0 = self.queues[0]["scene"]
-        sc0.take_stage_times()
-        sc0.set_stage_timing(timing)
-        self.timing = timing
-        ctx.barrier()
-        torch.cuda.synchronize(ctx.dev)
-        t0 = time.perf_counter()
-        for k in range(steps):
-            self.step(warmup * nq + k, nq)
-        self.drain(nq)
-        torch.cuda.synchronize(ctx.dev)
-        ctx.barrier()
-        elapsed = ctx.max_over_ranks(time.perf_counter() - t0)
-        sc0.set_stage_timing(False)
-        self.timing = False
-        launches, prep_ms, bin_ms, trace_ms = sc0.take_stage_times()
-        units = self.W * self.H * steps * (ctx.world if self.mode == "frames" else 1)
-        return {"elapsed": elapsed, "mrays": units / elapsed / 1e6, "prepare_ms": prep_ms, "bin_ms": bin_ms,
-                "trace_ms": trace_ms, "launches": launches, "ms_per_step": elapsed / steps * 1e3, "queues": nq}
-
-    def verify(self):
-        """Every rank that composited a batch compares its frames with a one-GPU render of the
-        same frame (fused trace, this device), bit for bit; True on every rank iff all agree."""
-        ctx, torch = self.ctx, self.ctx.torch
-        ok = True
-        for q in self.queues:
-            if q["root"] == ctx.rank:
-                ref_scene = ctx.srt.DeviceScene(q["scene"].path, ctx.dev.index)
-                ref = torch.empty((self.H, self.W, 4), dtype=torch.float32, device=ctx.dev)
-                st = torch.cuda.current_stream(ctx.dev)
-                ref_scene.prepare(self.W, self.H, st)
-                ref_scene.trace(self.offsets, ref, 0, self.H, variant=self.variant, stream=st)
-                torch.cuda.synchronize(ctx.dev)
-                for fr in q["rgba"][:q["shaded"]]:  # every frame of the queue's last composited batch
-                    ok = ok and bool(torch.equal(ref.view(torch.int32), fr.view(torch.int32)))
-                ref_scene.close()
-                break
-        return ctx.max_over_ranks(0.0 if ok else 1.0) == 0.0
+    def gather(self, values):
+        """Every rank's list of floats (rank order)."""
+        if not self.ranked:
+            return [values]
+        out = [None] * self.world
+        self.dist.all_gather_object(out, values)
+        return out
 
     def close(self):
-        for q in self.queues:
-            q["scene"].close()
+        if self.ranked:
+            self.dist.destroy_process_group()
+        self.tmp.cleanup()
 
 
-def stage_times_all_ranks(ctx, r):
-    """[prepare, bin, trace] ms of every rank (instrumented single-queue pass)."""
-    torch = ctx.torch
-    mine = torch.tensor([r["prepare_ms"], r["bin_ms"], r["trace_ms"]], dtype=torch.float64,
-                        device=ctx.dev if ctx.backend != "gloo" else "cpu")
-    if ctx.world == 1:
-        return [mine.tolist()]
-    out = [torch.zeros_like(mine) for _ in range(ctx.world)]
-    ctx.dist.all_gather(out, mine)
-    return [t.tolist() for t in out]
+def timed(job, eng, steps, warmup):
+    """`warmup` untimed batches, then exactly `steps` batches bracketed by a barrier + device
+    synchronisation on both sides; elapsed = max over ranks. Returns (elapsed s, Mrays/s)."""
+    eng.run(warmup)
+    job.sync()
+    job.barrier()
+    t0 = time.perf_counter()
+    eng.run(steps)  # returns once every local device has finished
+    job.sync()
+    elapsed = job.max_over_ranks(time.perf_counter() - t0)
+    job.barrier()
+    frames = steps * eng.batch * (job.world if eng.options["split"] == "frames" else 1)
+    return elapsed, frames * eng.width * eng.height / elapsed / 1e6
+
+
+def run_leg(job, a, path, inputs, steps, warmup, **kw):
+    eng = job.engine(path, a, **kw)
+    try:
+        eng.set_inputs(inputs)
+        el, mr = timed(job, eng, steps, warmup)
+        return {"mrays_per_s": round(mr, 3), "ms_per_step": round(el / steps * 1e3, 5),
+                "ms_per_frame": round(el / (steps * eng.batch) * 1e3, 6), "queues": eng.options["queues"],
+                "frames_per_step": eng.batch}
+    finally:
+        eng.close()
 
 
 def cpu_baseline(scene_path, a):
     """The oracle ('port') on this host's cores over a bounded, evenly spaced row sample."""
     from oracle import srt_oracle
 
-    # OMP_NUM_THREADS is the GPU box's CPU share for one GPU (16 of its 256 host CPUs; gpurun
-    # and the driver set it); os.cpu_count() reports the whole machine.
+    # OMP_NUM_THREADS is the GPU box's CPU share for one GPU (16 of its 256 host CPUs; gpurun and
+    # the driver set it); os.cpu_count() reports the whole machine.
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
     sc = srt_oracle.OracleScene(scene_path)
     h = a.height
@@ -415,8 +272,9 @@ def cpu_baseline(scene_path, a):
         "kind": "port",
         "sample": f"{rows} of {h} rows (every {step}th, all {a.width} columns) of {workload_name(a)}; "
                   f"{dt:.1f} s; OpenMP scalar C oracle (oracle/srt_oracle.c), brute force",
-        "cores_note": "OMP_NUM_THREADS = this GPU's share of the box's host CPUs (host_cpus counts the "
-                      "whole machine)",
+        "cores_note": "threads = OMP_NUM_THREADS, the CPU share the GPU box gives one GPU (16 of the machine's "
+                      "host_cpus); BASELINE.md's 'all host cores' is not available to one GPU's job, so the "
+                      "all-core rate would be about host_cpus / cores times this (scalar, linear in threads)",
     }
 
 
@@ -431,15 +289,22 @@ def committed_profile(name, key):
         return None
 
 
-def roofline_fields(wl, variant, launch_rays, n_tri, kernel_ms, band_ids):
-    """The trace kernel's roofline (algorithmic bytes: each ray's offsets in + its output, each
-    triangle's cull record once), the measured VALU issue from the committed PMC summary, and
-    the section 8(d) brute-force-equivalent figures, clearly separated."""
+def profile_key(wl, variant, world, rows_mode):
+    """PMC summaries are keyed by the exact launch shape: the full frame at N = 1, the band at N > 1."""
+    return f"{wl}|{variant}" if world == 1 else f"{wl}|{variant}|bands{world}|{rows_mode}"
+
+
+def roofline_fields(wl, variant, launch_rays, n_tri, kernel_ms, band_ids, height_frac, key):
+    """The trace kernel's roofline from the latency pass (one frame per launch, one in flight):
+    algorithmic bytes = each ray's offsets in + its output + the cull records it can read (all N at
+    N = 1; the band's pro-rata share at N > 1), over the kernel's HIP-event time; the measured HBM
+    traffic and VALU issue from committed rocprofv3 summaries of the same launch shape, else null."""
     kernel_s = kernel_ms * 1e-3
     out_bytes = 4 if band_ids else 16
-    alg = launch_rays * (8 + out_bytes) + n_tri * CULL_RECORD_BYTES
+    rec_bytes = int(round(n_tri * CULL_RECORD_BYTES * height_frac))
+    alg = launch_rays * (8 + out_bytes) + rec_bytes
     achieved = alg / kernel_s / 1e9
-    pmc = committed_profile("pmc_traffic.json", f"{wl}|{variant}") or {}
+    pmc = committed_profile("pmc_traffic.json", key) or {}
     roof = {
         "bound": "hbm",
         "achieved": round(achieved, 1),
@@ -450,11 +315,15 @@ def roofline_fields(wl, variant, launch_rays, n_tri, kernel_ms, band_ids):
         "kernel": KERNEL_NAMES[variant],
         "kernel_ms": round(kernel_ms, 5),
         "bytes_per_launch": alg,
-        "note": f"algorithmic bytes = launch rays x (8 B offsets in + {out_bytes} B out) + triangles x 64 B "
-                "(each cull record once), over the trace kernel's HIP-event time; traffic = measured HBM "
-                "bytes per launch (rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE, profiles/pmc_traffic.json)",
+        "measured_in": "latency pass: one frame per launch, one frame in flight, HIP events bound to the "
+                       "kernel's dispatch (the overlapped `value` run is timed as a whole: whole_frame below)",
+        "profile_key": key,
+        "note": f"algorithmic bytes = launch rays x (8 B offsets in + {out_bytes} B out) + cull records x 64 B"
+                f"{'' if height_frac == 1 else ' x the band share of the rows'}; traffic = measured HBM bytes per "
+                "launch of this launch shape (rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE, profiles/pmc_traffic.json), "
+                "null when no committed pass matches it",
     }
-    sq = committed_profile("pmc_sq.json", f"{wl}|{variant}")
+    sq = committed_profile("pmc_sq.json", key)
     valu = None
     if sq and sq.get("sq_insts_valu_per_launch"):
         issue_s = sq["sq_insts_valu_per_launch"] * 2 / (SIMDS * CLOCK_GHZ * 1e9)
@@ -474,112 +343,167 @@ def roofline_fields(wl, variant, launch_rays, n_tri, kernel_ms, band_ids):
     return roof, valu, bfe
 
 
-def leg_summary(r):
-    return {"mrays_per_s": round(r["mrays"], 3), "ms_per_step": round(r["ms_per_step"], 5), "queues": r["queues"]}
+def whole_frame_fields(W, H, n_tri, ms_per_frame, world):
+    """The overlapped run as a whole: a frame's compulsory bytes (offsets in, RGBA framebuffer out,
+    vertices read by the record pass) per frame time, against the HBM peak of the GPUs used."""
+    bytes_frame = W * H * PIXEL_IO_BYTES + n_tri * VERTEX_BYTES
+    gbs = bytes_frame / (ms_per_frame * 1e-3) / 1e9
+    return {"bytes_per_frame": bytes_frame, "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS * world,
+            "unit": "GB/s", "frac": round(gbs / (HBM_PEAK_GBS * world), 4),
+            "note": "per frame: W x H x (8 B offsets + 16 B RGBA) + triangles x 36 B vertices, over ms_per_frame of "
+                    "the timed (overlapped) run; peak = 8 TB/s x GPUs"}
+
+
+def e2e_ml_api(scene_path, W, H, reps=10, warmup=3, devices=None):
+    """PCIe-inclusive rate through the ml* API (host images in, host framebuffer out): median of
+    `reps` frames after `warmup`. devices: ML_VISIBLE_DEVICES for a multi-GPU mlInfer."""
+    import numpy as np
+
+    import simpleraytracer_amd as srt
+
+    old = os.environ.get("ML_VISIBLE_DEVICES")
+    if devices is not None:
+        os.environ["ML_VISIBLE_DEVICES"] = ",".join(str(d) for d in devices)
+    try:
+        ctx = srt.Context()
+        model = ctx.create_model(scene_path)
+        model.set_input_info(W, H)
+        (idt, iw, ih, ic), (odt, ow, oh, oc) = model.info()
+        inp = ctx.create_image(idt, iw, ih, ic)
+        out = ctx.create_image(odt, ow, oh, oc)
+        inp.array()[...] = np.float32(0.5)
+        for _ in range(warmup):
+            model.infer(inp, out)
+        times = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            model.infer(inp, out)
+            times.append(time.perf_counter() - t0)
+        frame = out.array().copy()
+        inp.close()
+        out.close()
+        model.close()
+        ctx.close()
+    finally:
+        if devices is not None:
+            if old is None:
+                os.environ.pop("ML_VISIBLE_DEVICES", None)
+            else:
+                os.environ["ML_VISIBLE_DEVICES"] = old
+    dt = sorted(times)[len(times) // 2]
+    return {"mrays_per_s": round(W * H / dt / 1e6, 4), "ms_per_frame": round(dt * 1e3, 3)}, frame
 
 
 def main():
     a = parse()
-    leg_queues = a.queues if a.queues > 0 else 3  # the secondary legs (random offsets, Cornell, variants)
-    if a.queues <= 0:
-        # Measured at C3 (profiles/r02/queues): long runs 2 / 3 / 1 queues 112.3 / 106.6 / 95.8
-        # Grays/s (with 8-frame launches two queues already fill the chip, a third adds L2
-        # contention); the driver's 20-step runs 91.8 / 96.9 / 83.6 (3 queues take one batch each,
-        # 2 queues leave a 2-frame tail batch each). The secondary legs keep 3: random offsets
-        # 78.1 vs 87.7, Cornell 143 vs 154, the BVH 15.1 vs 20.8 Grays/s with 2 vs 3.
-        a.queues = 3 if a.gpus > 1 or -(-a.steps // 3) <= 8 else 2
-    if a.batch <= 0:
-        # 16 frames per gather at N > 1, 8 per launch at N = 1, at most one batch per queue's
-        # share of the run: a short run (the driver's 20 steps over 3 queues) then traces, gathers
-        # and shades its frames in ~one batch per queue instead of per-frame collectives (~45 us
-        # of host time each) or a tail of partial batches
-        a.batch = max(1, min(16 if a.gpus > 1 else 8, -(-a.steps // max(1, a.queues))))
-    ctx = Ctx(a)
-    world, rank = ctx.world, ctx.rank
-    path = ctx.scene_path(a.scene, a.triangles if a.scene == "soup" else None)
+    if a.frames_per_step < 1 or a.queues < 1:
+        raise SystemExit("--frames-per-step and --queues must be positive")
+    job = Job(a)
+    world, rank = job.world, job.rank
+    path = job.scene_path(a.scene, a.triangles if a.scene == "soup" else None)
     wl = workload_name(a)
-    rotate = a.root == "rotate"
-    main_run = Pipeline(ctx, path, a.mode, a.queues, a.variant, a.offsets, rotate, a.batch, a.rows)
-    n_tri = main_run.triangles
-    _, order_build_ms = main_run.queues[0]["scene"].spatial_order()
     W, H = a.width, a.height
     extras = not a.no_extras
-    # Secondary passes first (they also bring the clocks up before the timed value loop): one
-    # frame in flight (per-frame latency), then the same with HIP events bound to the kernels'
-    # dispatch packets for the stage times (each event-bound dispatch leaves a 5-10 us bubble,
-    # so that pass is slower; its kernel durations are not inflated by frame overlap).
-    # (one frame per launch at N = 1: this pass is the per-frame latency)
-    r1 = main_run.run(a.steps, a.warmup, queues=1, batch=1 if world == 1 else None) if len(main_run.queues) > 1 else None
-    rt = main_run.run(min(a.steps, 1000), 2, queues=1, timing=True)
-    ranks_stages = stage_times_all_ranks(ctx, rt)
-    # value: uninstrumented frames over the frame queues
-    r = main_run.run(a.steps, a.warmup)
-    verified = main_run.verify() if (world > 1 and a.mode == "bands") else None
-    main_run.close()
+    inputs = make_offsets(a, a.offsets, max(1, a.inputs))
+
+    # value: the timed steps on the main engine
+    eng = job.engine(path, a)
+    info = eng.info()
+    n_tri = None
+    eng.set_inputs(inputs)
+    elapsed, mrays = timed(job, eng, a.steps, a.warmup)
+    frames = a.steps * a.frames_per_step
+    bad, checked = eng.verify()
+    verified = job.gather([bad, checked])
+    # stage times of every rank's band (single-frame launches, events on the dispatches)
+    n_stage = min(1000, max(20, frames))
+    st = eng.stage_times(0, n_stage)
+    if job.ranked:
+        ranks_stages = job.gather(list(st))
+    else:  # every device of this process, in band order
+        ranks_stages = [list(st)] + [list(eng.stage_times(i, n_stage)) for i in range(1, info["local_devices"])]
+    eng.close()
+    import simpleraytracer_amd as srt
+
+    n_tri = srt.scene_triangles(path)
+
     legs = {}
-    if world > 1 and extras:  # the other split and the other compositor choice, same steps
-        try:
-            om = "frames" if a.mode == "bands" else "bands"
-            o = Pipeline(ctx, path, om, a.queues, a.variant, a.offsets, rotate, a.batch, a.rows)
-            legs[om] = {**leg_summary(o.run(a.steps, a.warmup)), "scaling": "weak" if om == "frames" else "strong"}
-            o.close()
-            if a.mode == "bands":
-                o = Pipeline(ctx, path, "bands", a.queues, a.variant, a.offsets, not rotate, a.batch, a.rows)
-                legs["fixed_root" if rotate else "rotating_root"] = leg_summary(o.run(a.steps, a.warmup))
-                o.close()
-                other = "contiguous" if a.rows == "interleaved" else "interleaved"
-                o = Pipeline(ctx, path, "bands", a.queues, a.variant, a.offsets, rotate, a.batch, other)
-                legs[f"{other}_rows"] = leg_summary(o.run(a.steps, a.warmup))
-                o.close()
-        except Exception as e:  # noqa: BLE001 -- the primary line must still be printed
-            legs["secondary_error"] = f"{type(e).__name__}: {e}"
     if world == 1 and extras:
-        if a.offsets == "uniform":  # per-pixel jitter: the irregular-offset path
-            o = Pipeline(ctx, path, "bands", leg_queues, a.variant, "random", batch=a.batch)
-            rr = o.run(min(a.steps, 1000), a.warmup)
-            rt2 = o.run(min(a.steps, 300), 2, queues=1, timing=True)
-            o.close()
-            legs["offsets_random"] = {**leg_summary(rr), "trace_kernel_ms": round(rt2["trace_ms"], 5),
+        # one frame per launch, one in flight: the per-frame latency
+        legs["single_queue"] = run_leg(job, a, path, inputs, min(a.steps * a.frames_per_step, 2000), 20,
+                                       queues=1, batch=1)
+        legs["single_queue"]["note"] = "one frame per launch and in flight (the per-frame latency)"
+        if a.inputs == 1:  # inputs that cannot stay in the 256 MB Infinity Cache
+            ring = make_offsets(a, a.offsets, 16)
+            legs["rotating_inputs"] = {**run_leg(job, a, path, ring, a.steps, a.warmup), "inputs": 16,
+                                       "input_bytes": int(ring.nbytes),
+                                       "note": "frames cycle through 16 distinct resident input images (265 MB > the "
+                                               "256 MB MALL), same values as the headline's"}
+        if a.offsets == "uniform":
+            legs["offsets_random"] = {**run_leg(job, a, path, make_offsets(a, "random"), min(a.steps, 60), a.warmup),
                                       "note": "seeded U[0,1) per-pixel sample offsets (every tile irregular)"}
-        if a.scene == "soup":  # C2: the Cornell box at the same resolution
-            o = Pipeline(ctx, ctx.scene_path("cornell"), "bands", leg_queues, a.variant, a.offsets, batch=a.batch)
-            legs["c2_cornell"] = {**leg_summary(o.run(min(a.steps, 1000), a.warmup)),
+        if a.scene == "soup":
+            legs["c2_cornell"] = {**run_leg(job, a, job.scene_path("cornell"), inputs, min(a.steps, 60), a.warmup),
                                   "workload": workload_name(a, "cornell")}
-            o.close()
         if a.brute_steps > 0 and a.variant != "lds":
-            o = Pipeline(ctx, path, "bands", 1, "lds", a.offsets)
-            legs["brute_force"] = o.run(a.brute_steps, 1, queues=1, timing=True)
-            o.close()
-        if a.brute_steps > 0:  # the other exact accelerator, same frame
+            e = job.engine(path, a, variant="lds", queues=1, batch=1)
+            e.set_inputs(inputs)
+            el, mr = timed(job, e, a.brute_steps, 1)
+            n, _, _, kt = e.stage_times(0, a.brute_steps)
+            e.close()
+            tf = W * H * n_tri * FLOPS_PER_TEST / (kt * 1e-3) / 1e12
+            legs["brute_force"] = {
+                "variant": "lds", "kernel": "TraceLdsKernel", "mrays_per_s": round(mr, 3), "kernel_ms": round(kt, 4),
+                "steps": a.brute_steps, "valu_equivalent_tflops": round(tf, 2),
+                "valu_equivalent_frac": round(tf / FP32_PEAK_TFLOPS, 4),
+                "note": "north_star design taken literally: every ray tests every triangle, records tiled through "
+                        "LDS; valu_equivalent counts 12 flops per test (DESIGN.md 5: ~5.25 VALU instructions per "
+                        "test are issued)"}
+        if a.brute_steps > 0:
             for v in ("cull", "bvh"):
                 if v != a.variant:
-                    o = Pipeline(ctx, path, "bands", leg_queues, v, a.offsets)
-                    vr = o.run(min(a.steps, 1000), a.warmup)
-                    vt = o.run(min(a.steps, 300), 2, queues=1, timing=True)
-                    o.close()
-                    legs[f"variant_{v}"] = {**leg_summary(vr), "kernel": KERNEL_NAMES[v],
-                                            "stages_ms": {"prepare": round(vt["prepare_ms"], 5),
-                                                          "bin": round(vt["bin_ms"], 5),
-                                                          "trace_kernel": round(vt["trace_ms"], 5)},
+                    e = job.engine(path, a, variant=v, queues=3)
+                    e.set_inputs(inputs)
+                    _, mr = timed(job, e, min(a.steps, 30), 2)
+                    n, pm, bm, tm = e.stage_times(0, 100)
+                    e.close()
+                    legs[f"variant_{v}"] = {"mrays_per_s": round(mr, 3), "kernel": KERNEL_NAMES[v],
+                                            "stages_ms": {"prepare": round(pm, 5), "bin": round(bm, 5),
+                                                          "trace_kernel": round(tm, 5)},
                                             "note": "bit-identical frame (tests/test_gpu_parity.py)"}
+    if world > 1 and extras:
+        for name, kw in (("frames", {"mode": "frames"}),
+                         ("rotating_gather", {"exchange": "rotating"}),
+                         ("contiguous_rows", {"rows": "contiguous"})):
+            if (name == "frames" and a.mode == "frames") or (name == "rotating_gather" and a.exchange != "alltoall") \
+                    or (name == "contiguous_rows" and a.rows == "contiguous"):
+                continue
+            try:
+                legs[name] = run_leg(job, a, path, inputs, a.steps, a.warmup, **kw)
+                legs[name]["scaling"] = "weak" if name == "frames" else "strong"
+            except Exception as e:  # noqa: BLE001 -- the primary line must still be printed
+                legs[name] = {"error": f"{type(e).__name__}: {e}"}
 
     if rank == 0:
-        band_ids = world > 1 and a.mode == "bands"
-        launch_rays = main_run.row_count * W
-        roof, valu, bfe = roofline_fields(wl, a.variant, launch_rays, n_tri, rt["trace_ms"], band_ids)
-        if band_ids:
-            par = (f"bands x{world} ({a.rows} rows) + RCCL gather of hit ids to the "
-                   f"{'rotating' if rotate else 'rank-0'} compositor")
+        band = world > 1 and a.mode == "bands"
+        rows0 = info["band_rows"] if band else H
+        launch_rays = rows0 * W
+        key = profile_key(wl, a.variant, world if band else 1, a.rows)
+        roof, valu, bfe = roofline_fields(wl, a.variant, launch_rays, n_tri, st[3], band, rows0 / H, key)
+        ms_frame = elapsed / frames * 1e3
+        if band:
+            par = (f"bands x{world} ({a.rows} rows) + {'RCCL' if info['rccl'] else 'device-copy'} "
+                   f"{a.exchange} exchange of hit ids to the compositors")
         else:
             par = f"{a.mode} x{world}"
         line = {
             "metric": "Mrays/s at 1920x1080 on 100k-tri synthetic mesh",
-            "value": round(r["mrays"], 4),
+            "value": round(mrays, 4),
             "unit": "Mrays/s",
             "n_gpus": world,
             "steps": a.steps,
             "warmup": a.warmup,
-            "ms_per_step": round(r["ms_per_step"], 5),
+            "ms_per_step": round(elapsed / a.steps * 1e3, 5),
             "higher_is_better": True,
             "scaling": "strong" if a.mode == "bands" else "weak",
             "vs_baseline": None,
@@ -592,92 +516,57 @@ def main():
                 "height": H,
                 "spp": 1,
                 "parallelism": par,
+                "launch": job.launch,
+                "devices": job.devices if not job.ranked else f"rank {rank} of {world}",
                 "trace_variant": a.variant,
-                "frame_queues": r["queues"],
-                "frames_per_launch": main_run.L,
-                "frames_per_batch": main_run.G,
+                "frames_per_step": a.frames_per_step,
+                "frame_queues": a.queues,
+                "inputs": max(1, a.inputs),
                 "offsets": a.offsets,
             },
+            "ms_per_frame": round(ms_frame, 6),
             "roofline": roof,
-            "stages_ms": {"prepare": round(rt["prepare_ms"], 5), "bin": round(rt["bin_ms"], 5),
-                          "trace_kernel": round(rt["trace_ms"], 5), "frame": round(r["ms_per_step"], 5),
-                          "frame_instrumented": round(rt["ms_per_step"], 5), "timed_launches": rt["launches"],
-                          "note": "one frame per launch in flight, HIP events bound to the kernels' dispatches: "
-                                  "prepare = TileInfoKernel (tile ray boxes), bin = PrepareBinKernel (record setup + "
-                                  "bins) + WorkOrderKernel, trace_kernel = TraceCullKernel (rank 0's band at N > 1); "
-                                  "frame = uninstrumented time per frame with config.frame_queues in flight"},
+            "whole_frame": whole_frame_fields(W, H, n_tri, ms_frame, world if a.mode == "bands" else 1),
+            "stages_ms": {"prepare": round(st[1], 5), "bin": round(st[2], 5), "trace_kernel": round(st[3], 5),
+                          "timed_launches": st[0],
+                          "note": "single-frame launches of rank 0's band, HIP events bound to the kernels' dispatches: "
+                                  "prepare = TileInfoKernel, bin = PrepareBinKernel (record setup + bins) + "
+                                  "WorkOrderKernel, trace_kernel = TraceCullKernel"},
         }
-        line["scene_build"] = {"spatial_order_ms": round(order_build_ms, 4),
-                               "note": "once per scene at load, on the device (Morton codes + rocPRIM radix sort, "
-                                       "csrc/spatial.hip); not per frame"}
         if valu is not None:
             line["valu_issue"] = valu
         line["brute_force_equivalent"] = bfe
-        if r1 is not None:
-            line["single_queue"] = {"mrays_per_s": round(r1["mrays"], 4), "ms_per_step": round(r1["ms_per_step"], 5),
-                                    "note": "the same frames with one frame in flight (N = 1: one frame per launch, "
-                                            "the per-frame latency)"}
+        line["verified"] = all(v[0] == 0 and v[1] > 0 for v in verified)
+        line["verify"] = {"frames_checked": sum(v[1] for v in verified), "mismatches": sum(v[0] for v in verified),
+                          "note": "every frame composited in each queue's last batch vs a single-GPU full-frame render "
+                                  "of its input by another trace kernel (lds for cull), bit for bit"}
         if world > 1:
-            line["ranks_stages_ms"] = [{"rank": i, "prepare": round(s[0], 5), "bin": round(s[1], 5),
-                                        "trace_kernel": round(s[2], 5)} for i, s in enumerate(ranks_stages)]
-            line["verified"] = verified
-            if band_ids:
-                line["gather"] = {"payload": "int32 hit id per pixel (deferred shading on the compositor)",
-                                  "frames_per_collective": main_run.G,
-                                  "bytes_per_frame": (world - 1) * main_run.B * W * 4,
-                                  "rgba_f32_equivalent": (world - 1) * main_run.B * W * 16}
+            line["ranks_stages_ms"] = [{"rank": i, "prepare": round(s[1], 5), "bin": round(s[2], 5),
+                                        "trace_kernel": round(s[3], 5)} for i, s in enumerate(ranks_stages)]
+            if band:
+                line["exchange"] = {"pattern": a.exchange, "transport": "RCCL" if info["rccl"] else "device copies",
+                                    "payload": "int32 hit id per pixel (deferred shading on the compositor)",
+                                    "bytes_per_frame": int(info["exchange_bytes_per_frame"]),
+                                    "rgba_f32_equivalent": int(info["exchange_bytes_per_frame"] * 4)}
         for k, v in legs.items():
-            if k == "brute_force":
-                bs = v["trace_ms"] * 1e-3
-                tf = launch_rays * n_tri * FLOPS_PER_TEST / bs / 1e12
-                line["brute_force"] = {
-                    "variant": "lds", "kernel": "TraceLdsKernel", "mrays_per_s": round(v["mrays"], 3),
-                    "kernel_ms": round(v["trace_ms"], 4), "steps": a.brute_steps,
-                    "valu_equivalent_tflops": round(tf, 2), "valu_equivalent_frac": round(tf / FP32_PEAK_TFLOPS, 4),
-                    "note": "north_star design taken literally: every ray tests every triangle, records tiled "
-                            "through LDS; valu_equivalent counts 12 flops per test (DESIGN.md 5: ~5.25 VALU "
-                            "instructions per test are issued)"}
-            else:
-                line[k] = v
+            line[k] = v
         if world == 1 and not a.no_e2e and extras:
-            line["e2e_ml_api"] = e2e_ml_api(path, W, H)
+            e2e, _ = e2e_ml_api(path, W, H)
+            line["e2e_ml_api"] = {**e2e, "path": "mlInfer: H2D offsets + trace + D2H framebuffer (pinned host images), "
+                                                 "4 row chunks pipelined over three streams"}
+        if world > 1 and not job.ranked and not a.no_e2e and extras:
+            try:
+                e2e, _ = e2e_ml_api(path, W, H, devices=job.devices)
+                line["ml_multi"] = {**e2e, "devices": job.devices,
+                                    "path": "mlInfer over ML_VISIBLE_DEVICES: H2D band offsets + interleaved band traces "
+                                            "(hit ids) + gather to device 0 + shading + D2H"}
+            except Exception as e:  # noqa: BLE001
+                line["ml_multi"] = {"error": f"{type(e).__name__}: {e}"}
         if world == 1 and not a.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(path, a)
         print(json.dumps(line), flush=True)
-    if world > 1:
-        ctx.dist.destroy_process_group()
-    ctx.tmp.cleanup()
-
-
-def e2e_ml_api(scene_path, W, H, reps=10, warmup=3):
-    """PCIe-inclusive rate through the ml* API (host images in, host framebuffer out): median
-    of `reps` frames after `warmup` (first frames pay one-time allocations)."""
-    import numpy as np
-
-    import simpleraytracer_amd as srt
-
-    ctx = srt.Context()
-    model = ctx.create_model(scene_path)
-    model.set_input_info(W, H)
-    (idt, iw, ih, ic), (odt, ow, oh, oc) = model.info()
-    inp = ctx.create_image(idt, iw, ih, ic)
-    out = ctx.create_image(odt, ow, oh, oc)
-    inp.array()[...] = np.float32(0.5)
-    for _ in range(warmup):
-        model.infer(inp, out)
-    times = []
-    for _ in range(reps):
-        t0 = time.perf_counter()
-        model.infer(inp, out)
-        times.append(time.perf_counter() - t0)
-    dt = sorted(times)[len(times) // 2]
-    inp.close()
-    out.close()
-    model.close()
-    ctx.close()
-    return {"mrays_per_s": round(W * H / dt / 1e6, 4), "ms_per_frame": round(dt * 1e3, 3),
-            "path": "mlInfer: H2D offsets + prepare + trace + D2H framebuffer (pinned host images), "
-                    "single device: 4 row chunks pipelined over three streams (SRT_E2E_CHUNKS)"}
+    job.barrier()
+    job.close()
 
 
 if __name__ == "__main__":

@@ -125,14 +125,6 @@ ML_API_ENTRY int srtShadeBandsAsync(srt_device_scene scene, const float* d_offse
  * buffer are shared, so a call on a different stream than the previous call first waits (HIP
  * event) for the work enqueued before it. Use one scene per stream for concurrent frames. */
 
-/* Self-test of the multi-device band gather on host memory (no device): band i's padded buffer
- * bands[i] (ceil(height / band_count) rows x width x 4 elements of element_bytes, 4 = float,
- * 2 = half) lands where ncclGather puts it in the root's gather buffer, and the frame (height x
- * width x 4) is that buffer's first rows -- the offsets and strides every gather path of mlInfer
- * uses (Renderer: RCCL, device copies). */
-ML_API_ENTRY int srtGatherBandsHost(const void* const* bands, size_t band_count, size_t width, size_t height,
-                                    int element_bytes, void* frame);
-
 /* Stage timing (measurement): while enabled, srtPrepareAsync and srtTraceAsync bind HIP events
  * to their kernels' own dispatch packets (hipExtLaunchKernelGGL start/stop events: no extra
  * packets on the stream). srtTakeStageTimes waits for them, writes the number of timed trace
@@ -141,6 +133,73 @@ ML_API_ENTRY int srtGatherBandsHost(const void* const* bands, size_t band_count,
 ML_API_ENTRY int srtSetStageTiming(srt_device_scene scene, int enable);
 ML_API_ENTRY int srtTakeStageTimes(srt_device_scene scene, unsigned* launches, double* prepare_ms, double* bin_ms,
                                    double* trace_ms);
+
+/* ---------------------------------------------------------------------------------------------
+ * Frame engine (csrc/engine.h): a stream of frames over one or more GPUs, the native multi-GPU
+ * path of BASELINE config C4 (and C3 / C5 on one GPU). A run is a sequence of batches of `batch`
+ * frames; every device keeps `queues` batches in flight (own scene buffers and HIP stream each).
+ * Split SRT_SPLIT_BANDS over P devices: each frame is cut into P row bands (the frame's 16-row tile
+ * rows dealt round-robin, or contiguous blocks), device d traces band d (hit ids, 4 B per pixel),
+ * the bands move over RCCL to the frame's compositor, which shades the frame from the ids (one
+ * launch per batch, bit-identical to the fused trace). Exchanges: SRT_EXCHANGE_ALLTOALL (frame f of
+ * a batch composited on device f % P; the batch's P gathers fused into one ncclSend / ncclRecv
+ * group), SRT_EXCHANGE_ROTATING (the batch gathered to device b % P), SRT_EXCHANGE_ROOT (device 0).
+ * P == 1: trace + shade fused (RGBA). SRT_SPLIT_FRAMES: every device renders whole frames of its
+ * own (no exchange). Devices: all in this process (srtEngineCreate; one worker thread per device,
+ * ncclCommInitAll; a repeated device exchanges by device copies -- the one-GPU rehearsal), or one
+ * per process (srtEngineCreateRank; ncclCommInitRank with a unique id from srtEngineUniqueId). */
+typedef struct srt_engine_t* srt_engine;
+#define SRT_ROWS_INTERLEAVED 0
+#define SRT_ROWS_CONTIGUOUS 1
+#define SRT_EXCHANGE_ALLTOALL 0
+#define SRT_EXCHANGE_ROTATING 1
+#define SRT_EXCHANGE_ROOT 2
+#define SRT_SPLIT_BANDS 0
+#define SRT_SPLIT_FRAMES 1
+typedef struct srt_engine_options {
+    int variant;    /* SRT_TRACE_* */
+    size_t queues;  /* batches in flight per device (0 = 2) */
+    size_t batch;   /* frames per batch (0 = 16) */
+    int rows;       /* SRT_ROWS_* */
+    int exchange;   /* SRT_EXCHANGE_* */
+    int split;      /* SRT_SPLIT_* */
+} srt_engine_options;
+
+/* 128-byte RCCL unique id for srtEngineCreateRank (call on one rank, share with the others). */
+ML_API_ENTRY int srtEngineUniqueId(void* id128);
+ML_API_ENTRY srt_engine srtEngineCreate(const char* scene_path, const int* devices, size_t device_count, size_t width,
+                                        size_t height, const srt_engine_options* options);
+/* Every rank calls this concurrently (RCCL communicator setup synchronises them). */
+ML_API_ENTRY srt_engine srtEngineCreateRank(const char* scene_path, int device, int rank, int world,
+                                            const void* unique_id128, size_t width, size_t height,
+                                            const srt_engine_options* options);
+ML_API_ENTRY void srtEngineRelease(srt_engine engine);
+/* `count` full-frame sample-offset images (count x height x width x 2 floats, host), kept resident on
+ * every device; frame k reads input k % count. */
+ML_API_ENTRY int srtEngineSetInputs(srt_engine engine, const float* host_offsets, size_t count);
+/* Render `batches` x batch frames, continuing the frame sequence; synchronous. */
+ML_API_ENTRY int srtEngineRun(srt_engine engine, size_t batches);
+/* Every locally composited frame of each queue's last batch vs a single-device full-frame render of
+ * its input (another trace variant), bit for bit: mismatching and checked frame counts. */
+ML_API_ENTRY int srtEngineVerify(srt_engine engine, size_t* mismatches, size_t* checked);
+/* Frame k of the last `queues` batches into host RGBA (height x width x 4 floats); fails when another
+ * rank composited it (bands) or it is no longer resident. */
+ML_API_ENTRY int srtEngineReadFrame(srt_engine engine, size_t frame, float* host_rgba);
+/* Stage times of `launches` single-frame traces of local device `local`'s band (see
+ * srtTakeStageTimes). */
+ML_API_ENTRY int srtEngineStageTimes(srt_engine engine, size_t local, size_t launches, unsigned* launched,
+                                     double* prepare_ms, double* bin_ms, double* trace_ms);
+/* Shape of the run: devices in the job, local devices, rows of local device 0's band, rows of every
+ * band buffer, whether the exchange uses RCCL, exchanged bytes per frame (bands, all devices). */
+ML_API_ENTRY int srtEngineInfo(srt_engine engine, size_t* devices, size_t* local_devices, size_t* band_rows,
+                               size_t* buffer_rows, int* rccl, double* exchange_bytes_per_frame);
+/* Host self-test of the engine's exchange layout (no device): band_ids[d] = band d's hit ids of a
+ * batch's frames (batch x buffer rows x width int32, buffer rows = srtEngineInfo's); recv[c]
+ * receives compositor c's buffer as the device path lays it out, [bands][frames of c][buffer rows]
+ * [width] (frames of c: recv_frames[c]; pass NULL recv to only query recv_frames). */
+ML_API_ENTRY int srtExchangeHost(const int* const* band_ids, size_t bands, size_t width, size_t height, int rows,
+                                 int exchange, size_t batch, size_t batch_index, int* const* recv,
+                                 size_t* recv_frames, size_t* buffer_rows);
 
 #ifdef __cplusplus
 }

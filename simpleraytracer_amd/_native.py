@@ -29,6 +29,13 @@ SRT_TRACE_SCALAR = 1
 SRT_TRACE_CULL = 2
 SRT_TRACE_BVH = 3
 SRT_MAX_BATCH = 8  # include/srt_render.h: frames per srtTraceBatchAsync call
+SRT_ROWS_INTERLEAVED = 0
+SRT_ROWS_CONTIGUOUS = 1
+SRT_EXCHANGE_ALLTOALL = 0
+SRT_EXCHANGE_ROTATING = 1
+SRT_EXCHANGE_ROOT = 2
+SRT_SPLIT_BANDS = 0
+SRT_SPLIT_FRAMES = 1
 SRT_TILE_ROWS = 16  # include/srt_render.h: rows per tile row (interleaved bands deal these)
 
 
@@ -55,6 +62,23 @@ class ModelParams(ctypes.Structure):
         ("output_node", ctypes.c_char_p),
     ]
 
+
+class EngineOptions(ctypes.Structure):
+    """``srt_engine_options`` (include/srt_render.h)."""
+
+    _fields_ = [
+        ("variant", ctypes.c_int),
+        ("queues", ctypes.c_size_t),
+        ("batch", ctypes.c_size_t),
+        ("rows", ctypes.c_int),
+        ("exchange", ctypes.c_int),
+        ("split", ctypes.c_int),
+    ]
+
+
+_SZ = ctypes.c_size_t
+_PSZ = ctypes.POINTER(ctypes.c_size_t)
+_PD = ctypes.POINTER(ctypes.c_double)
 
 # name -> (restype, argtypes)
 _SIGNATURES = {
@@ -99,11 +123,23 @@ _SIGNATURES = {
                                      ctypes.c_size_t, ctypes.c_size_t, ctypes.c_void_p]),
     "srtShadeBandsAsync": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                           ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_void_p]),
-    "srtGatherBandsHost": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_size_t,
-                                          ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]),
     "srtSetStageTiming": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "srtTakeStageTimes": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint), ctypes.POINTER(ctypes.c_double),
                                          ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
+    "srtEngineUniqueId": (ctypes.c_int, [ctypes.c_void_p]),
+    "srtEngineCreate": (ctypes.c_void_p, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int), _SZ, _SZ, _SZ,
+                                          ctypes.POINTER(EngineOptions)]),
+    "srtEngineCreateRank": (ctypes.c_void_p, [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                              _SZ, _SZ, ctypes.POINTER(EngineOptions)]),
+    "srtEngineRelease": (None, [ctypes.c_void_p]),
+    "srtEngineSetInputs": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, _SZ]),
+    "srtEngineRun": (ctypes.c_int, [ctypes.c_void_p, _SZ]),
+    "srtEngineVerify": (ctypes.c_int, [ctypes.c_void_p, _PSZ, _PSZ]),
+    "srtEngineReadFrame": (ctypes.c_int, [ctypes.c_void_p, _SZ, ctypes.c_void_p]),
+    "srtEngineStageTimes": (ctypes.c_int, [ctypes.c_void_p, _SZ, _SZ, ctypes.POINTER(ctypes.c_uint), _PD, _PD, _PD]),
+    "srtEngineInfo": (ctypes.c_int, [ctypes.c_void_p, _PSZ, _PSZ, _PSZ, _PSZ, ctypes.POINTER(ctypes.c_int), _PD]),
+    "srtExchangeHost": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), _SZ, _SZ, _SZ, ctypes.c_int, ctypes.c_int, _SZ,
+                                       _SZ, ctypes.POINTER(ctypes.c_void_p), _PSZ, _PSZ]),
 }
 
 _lib = None

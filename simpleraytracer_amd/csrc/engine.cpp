@@ -1,0 +1,845 @@
+#include "engine.h"
+
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <condition_variable>
+#include <cstdlib>
+#include <cstring>
+#include <exception>
+#include <functional>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <thread>
+
+#include "render.h"
+
+namespace srt {
+namespace {
+
+void NcclCheck(ncclResult_t res, const char* what) {
+    if (res != ncclSuccess) {
+        throw std::runtime_error(std::string("RCCL error: ") + what + ": " + ncclGetErrorString(res));
+    }
+}
+
+template <class T>
+T* DeviceAlloc(std::size_t count, const char* what) {
+    void* p = nullptr;
+    HipCheck(hipMalloc(&p, (count == 0 ? 1 : count) * sizeof(T)), what);
+    return static_cast<T*>(p);
+}
+
+bool GatherByCopies(const std::vector<int>& devices) {
+    const char* v = std::getenv("SRT_GATHER");
+    if (v != nullptr && std::strcmp(v, "copy") == 0) {
+        return true;
+    }
+    for (std::size_t i = 0; i < devices.size(); ++i) {
+        for (std::size_t j = 0; j < i; ++j) {
+            if (devices[i] == devices[j]) {
+                return true;  // one device twice: no RCCL communicator (the "fake devices" rehearsal)
+            }
+        }
+    }
+    return false;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------------------
+// Band split and exchange plan (pure index math; shared with the host self-test).
+
+BandSplit BandSplit::Make(std::size_t height, std::size_t bands, bool interleaved) {
+    BandSplit s;
+    s.height = height;
+    s.bands = bands == 0 ? 1 : bands;
+    s.interleaved = interleaved;
+    return s;
+}
+
+std::size_t BandSplit::RowBegin(std::size_t band) const {
+    if (bands == 1) {
+        return 0;
+    }
+    const std::size_t step = interleaved ? static_cast<std::size_t>(kCullTileRows) : (height + bands - 1) / bands;
+    return std::min(height, band * step);
+}
+
+std::size_t BandSplit::RowCount(std::size_t band) const {
+    if (bands == 1) {
+        return height;
+    }
+    if (interleaved) {
+        return InterleavedBandRows(height, bands, band);
+    }
+    const std::size_t b = (height + bands - 1) / bands;
+    return std::min(height, (band + 1) * b) - RowBegin(band);
+}
+
+std::size_t BandSplit::BufferRows() const {
+    if (bands == 1) {
+        return height;
+    }
+    return interleaved ? InterleavedBandRows(height, bands, 0) : (height + bands - 1) / bands;
+}
+
+std::size_t BandSplit::FrameRow(std::size_t band, std::size_t local) const {
+    return BandFrameRow(RowBegin(band), Interleave(), local);
+}
+
+std::size_t ExchangePlan::Compositor(std::size_t batch_index, std::size_t f) const {
+    switch (exchange) {
+        case EngineOptions::kRotatingGather:
+            return batch_index % bands;
+        case EngineOptions::kRootGather:
+            return 0;
+        default:
+            return f % bands;
+    }
+}
+
+std::size_t ExchangePlan::Slot(std::size_t f) const {
+    return exchange == EngineOptions::kAllToAll ? f / bands : f;
+}
+
+std::size_t ExchangePlan::FramesFor(std::size_t batch_index, std::size_t compositor) const {
+    switch (exchange) {
+        case EngineOptions::kRotatingGather:
+            return compositor == batch_index % bands ? batch : 0;
+        case EngineOptions::kRootGather:
+            return compositor == 0 ? batch : 0;
+        default:
+            return compositor < batch ? (batch - compositor + bands - 1) / bands : 0;
+    }
+}
+
+std::size_t ExchangePlan::MaxFramesPerCompositor() const {
+    return exchange == EngineOptions::kAllToAll ? (batch + bands - 1) / bands : batch;
+}
+
+namespace {
+// Offset (in pixels) of compositor c's slot j in a device's send buffer: all-to-all keeps one
+// region of MaxFramesPerCompositor frames per compositor; the gathers send everything to one.
+std::size_t SendPixels(const ExchangePlan& plan, std::size_t c, std::size_t j, std::size_t band_pixels) {
+    const std::size_t region = plan.exchange == EngineOptions::kAllToAll ? c * plan.MaxFramesPerCompositor() : 0;
+    return (region + j) * band_pixels;
+}
+}  // namespace
+
+std::vector<std::vector<int>> ExchangeOnHost(const BandSplit& split, const ExchangePlan& plan, std::size_t width,
+                                             std::size_t batch_index, const std::vector<std::vector<int>>& band_ids) {
+    const std::size_t P = split.bands, B = split.BufferRows(), F = plan.batch;
+    const std::size_t band_pixels = B * width;
+    if (band_ids.size() != P) {
+        throw std::runtime_error("ExchangeOnHost: one id buffer per band");
+    }
+    for (const auto& ids : band_ids) {
+        if (ids.size() != F * band_pixels) {
+            throw std::runtime_error("ExchangeOnHost: id buffers must be frames x buffer rows x width");
+        }
+    }
+    std::vector<std::vector<int>> recv(P);
+    for (std::size_t c = 0; c < P; ++c) {
+        const std::size_t n = plan.FramesFor(batch_index, c);
+        recv[c].assign(P * n * band_pixels, -1);
+        // What device d sends to c (its send buffer region in SendPixels order), landing at region
+        // d of c's receive buffer: the device path's ncclSend / ncclRecv pairs, as copies.
+        for (std::size_t d = 0; d < P; ++d) {
+            const std::size_t send_frames =
+                plan.exchange == EngineOptions::kAllToAll ? P * plan.MaxFramesPerCompositor() : F;
+            std::vector<int> send(send_frames * band_pixels, -1);
+            for (std::size_t f = 0; f < F; ++f) {
+                const std::size_t cf = plan.Compositor(batch_index, f);
+                std::copy_n(band_ids[d].begin() + f * band_pixels, band_pixels,
+                            send.begin() + SendPixels(plan, cf, plan.Slot(f), band_pixels));
+            }
+            std::copy_n(send.begin() + SendPixels(plan, c, 0, band_pixels), n * band_pixels,
+                        recv[c].begin() + d * n * band_pixels);
+        }
+    }
+    return recv;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Worker threads: one per local device; a job runs on every worker, the caller waits. The
+// device-copy exchange synchronises the workers at a host barrier (abortable: a worker that fails
+// releases the others with an error).
+
+struct FrameEngine::Pool {
+    explicit Pool(std::size_t n) : m_n(n) {
+        for (std::size_t i = 0; i < n; ++i) {
+            m_threads.emplace_back([this, i] { Loop(i); });
+        }
+    }
+    ~Pool() {
+        {
+            std::lock_guard<std::mutex> lk(m_mu);
+            m_stop = true;
+        }
+        m_cv.notify_all();
+        for (auto& t : m_threads) {
+            t.join();
+        }
+    }
+    void Run(const std::function<void(std::size_t)>& job) {
+        std::unique_lock<std::mutex> lk(m_mu);
+        m_job = &job;
+        m_pending = m_n;
+        m_error = nullptr;
+        m_aborted = false;
+        m_bar_count = 0;
+        ++m_gen;
+        m_cv.notify_all();
+        m_done.wait(lk, [this] { return m_pending == 0; });
+        m_job = nullptr;
+        if (m_error) {
+            std::rethrow_exception(m_error);
+        }
+    }
+    void Barrier() {
+        std::unique_lock<std::mutex> lk(m_mu);
+        if (m_aborted) {
+            throw std::runtime_error("another device's worker failed");
+        }
+        const std::size_t gen = m_bar_gen;
+        if (++m_bar_count == m_n) {
+            m_bar_count = 0;
+            ++m_bar_gen;
+            m_bar_cv.notify_all();
+            return;
+        }
+        m_bar_cv.wait(lk, [&] { return m_bar_gen != gen || m_aborted; });
+        if (m_bar_gen == gen) {
+            throw std::runtime_error("another device's worker failed");
+        }
+    }
+
+private:
+    void Loop(std::size_t i) {
+        std::size_t seen = 0;
+        for (;;) {
+            const std::function<void(std::size_t)>* job = nullptr;
+            {
+                std::unique_lock<std::mutex> lk(m_mu);
+                m_cv.wait(lk, [&] { return m_stop || m_gen != seen; });
+                if (m_stop) {
+                    return;
+                }
+                seen = m_gen;
+                job = m_job;
+            }
+            try {
+                (*job)(i);
+            } catch (...) {
+                std::lock_guard<std::mutex> lk(m_mu);
+                if (!m_error) {
+                    m_error = std::current_exception();
+                }
+                m_aborted = true;
+                m_bar_cv.notify_all();
+            }
+            std::lock_guard<std::mutex> lk(m_mu);
+            if (--m_pending == 0) {
+                m_done.notify_all();
+            }
+        }
+    }
+
+    std::size_t m_n;
+    std::vector<std::thread> m_threads;
+    std::mutex m_mu;
+    std::condition_variable m_cv, m_done, m_bar_cv;
+    const std::function<void(std::size_t)>* m_job = nullptr;
+    std::size_t m_gen = 0, m_pending = 0, m_bar_count = 0, m_bar_gen = 0;
+    bool m_stop = false, m_aborted = false;
+    std::exception_ptr m_error;
+};
+
+// ---------------------------------------------------------------------------------------------
+
+struct FrameEngine::Queue {
+    std::unique_ptr<DeviceScene> scene;
+    hipStream_t stream = nullptr;
+    hipEvent_t traced = nullptr;     // the batch's trace done (queue stream)
+    hipEvent_t exchanged = nullptr;  // the batch's exchange done (comm stream)
+    int* send = nullptr;             // bands: ids for the other compositors
+    int* recv = nullptr;             // bands: [P][frames composited here][buffer rows][W] ids
+    float* rgba = nullptr;           // frames rendered / composited here per batch, H x W x 4 each
+    std::size_t rgba_frames = 0;
+    std::size_t last_batch = 0;
+    bool used = false;
+};
+
+struct FrameEngine::Device {
+    int device = 0;
+    std::size_t band = 0;  // global band / rank index
+    hipStream_t comm = nullptr;
+    std::vector<Queue> queues;
+    float* full = nullptr;  // inputs x H x W x 2
+    float* band_in = nullptr;  // inputs x band rows x W x 2
+    std::size_t row_begin = 0, rows = 0;
+};
+
+FrameEngine::FrameEngine(const Scene& scene, const std::vector<int>& devices, std::size_t width,
+                         std::size_t height, const EngineOptions& options)
+    : m_opt(options), m_width(width), m_height(height), m_world(devices.size()) {
+    if (devices.empty()) {
+        throw std::runtime_error("FrameEngine: no devices");
+    }
+    Init(scene, devices);
+    m_copy = m_bands && m_world > 1 && GatherByCopies(devices);
+    try {
+        if (m_bands && m_world > 1 && !m_copy) {
+            std::vector<ncclComm_t> comms(m_world);
+            std::vector<int> devs(devices);
+            NcclCheck(ncclCommInitAll(comms.data(), static_cast<int>(m_world), devs.data()), "ncclCommInitAll");
+            m_comms.assign(comms.begin(), comms.end());
+        }
+        AllocateQueues();
+        if (m_dev.size() > 1) {
+            m_pool = std::make_unique<Pool>(m_dev.size());
+        }
+    } catch (...) {
+        Release();
+        throw;
+    }
+}
+
+FrameEngine::FrameEngine(const Scene& scene, int device, int rank, int world, const void* unique_id,
+                         std::size_t width, std::size_t height, const EngineOptions& options)
+    : m_opt(options), m_width(width), m_height(height), m_world(world < 1 ? 1 : static_cast<std::size_t>(world)),
+      m_rank0(rank < 0 ? 0 : static_cast<std::size_t>(rank)) {
+    if (rank < 0 || rank >= world) {
+        throw std::runtime_error("FrameEngine: rank " + std::to_string(rank) + " outside world " +
+                                 std::to_string(world));
+    }
+    Init(scene, std::vector<int>{device});
+    try {
+        if (m_bands && m_world > 1) {
+            if (unique_id == nullptr) {
+                throw std::runtime_error("FrameEngine: a multi-rank band split needs the RCCL unique id");
+            }
+            DeviceGuard guard(device);
+            ncclUniqueId id;
+            std::memcpy(&id, unique_id, sizeof(id));
+            ncclComm_t comm = nullptr;
+            NcclCheck(ncclCommInitRank(&comm, world, id, rank), "ncclCommInitRank");
+            m_comms.push_back(comm);
+        }
+        AllocateQueues();
+    } catch (...) {
+        Release();
+        throw;
+    }
+}
+
+void FrameEngine::UniqueId(void* out128) {
+    ncclUniqueId id;
+    NcclCheck(ncclGetUniqueId(&id), "ncclGetUniqueId");
+    static_assert(sizeof(id) == 128, "ncclUniqueId is 128 bytes");
+    std::memcpy(out128, &id, sizeof(id));
+}
+
+void FrameEngine::Init(const Scene& scene, const std::vector<int>& devices) {
+    if (m_width == 0 || m_height == 0) {
+        throw std::runtime_error("FrameEngine: frame dimensions must be non-zero");
+    }
+    if (m_opt.batch == 0 || m_opt.batch > 4096 || m_opt.queues == 0 || m_opt.queues > 16) {
+        throw std::runtime_error("FrameEngine: batch must be 1..4096 frames and queues 1..16");
+    }
+    if (m_opt.variant < kTraceLds || m_opt.variant > kTraceBvh) {
+        throw std::runtime_error("FrameEngine: unknown trace variant " + std::to_string(m_opt.variant));
+    }
+    if (m_opt.exchange < EngineOptions::kAllToAll || m_opt.exchange > EngineOptions::kRootGather ||
+        (m_opt.split != EngineOptions::kBands && m_opt.split != EngineOptions::kFrames)) {
+        throw std::runtime_error("FrameEngine: unknown exchange or split");
+    }
+    m_bands = m_opt.split == EngineOptions::kBands;
+    m_split = BandSplit::Make(m_height, m_bands ? m_world : 1, m_opt.interleaved);
+    m_plan.bands = m_split.bands;
+    m_plan.batch = m_opt.batch;
+    m_plan.exchange = m_opt.exchange;
+    m_scene = std::make_unique<Scene>(scene);
+    m_n = scene.triangle_count();
+    for (std::size_t i = 0; i < devices.size(); ++i) {
+        auto d = std::make_unique<Device>();
+        d->device = devices[i];
+        d->band = m_rank0 + i;
+        d->row_begin = m_split.RowBegin(m_bands ? d->band : 0);
+        d->rows = m_split.RowCount(m_bands ? d->band : 0);
+        m_dev.push_back(std::move(d));
+    }
+}
+
+void FrameEngine::AllocateQueues() {
+    const bool exchange = m_bands && m_world > 1;
+    const std::size_t band_pixels = m_split.BufferRows() * m_width;
+    const std::size_t frame_floats4 = m_width * m_height * 4;
+    for (auto& dp : m_dev) {
+        Device& d = *dp;
+        DeviceGuard guard(d.device);
+        HipCheck(hipStreamCreateWithFlags(&d.comm, hipStreamNonBlocking), "hipStreamCreate(comm)");
+        d.queues.resize(m_opt.queues);
+        for (Queue& q : d.queues) {
+            HipCheck(hipStreamCreateWithFlags(&q.stream, hipStreamNonBlocking), "hipStreamCreate(queue)");
+            HipCheck(hipEventCreateWithFlags(&q.traced, hipEventDisableTiming), "hipEventCreate(traced)");
+            HipCheck(hipEventCreateWithFlags(&q.exchanged, hipEventDisableTiming), "hipEventCreate(exchanged)");
+            q.scene = std::make_unique<DeviceScene>(*m_scene, d.device);
+            q.scene->Prepare(m_width, m_height, q.stream);
+            if (exchange) {
+                const std::size_t send_frames = m_plan.exchange == EngineOptions::kAllToAll
+                                                    ? m_world * m_plan.MaxFramesPerCompositor()
+                                                    : m_plan.batch;
+                q.send = DeviceAlloc<int>(send_frames * band_pixels, "hipMalloc(send ids)");
+                q.recv = DeviceAlloc<int>(m_world * m_plan.MaxFramesPerCompositor() * band_pixels,
+                                          "hipMalloc(receive ids)");
+                q.rgba_frames = m_plan.MaxFramesPerCompositor();
+            } else {
+                q.rgba_frames = m_opt.batch;
+            }
+            q.rgba = DeviceAlloc<float>(q.rgba_frames * frame_floats4, "hipMalloc(frames)");
+        }
+    }
+}
+
+FrameEngine::~FrameEngine() { Release(); }
+
+void FrameEngine::Release() noexcept {
+    m_pool.reset();
+    for (auto& dp : m_dev) {
+        if (!dp) {
+            continue;
+        }
+        (void)hipSetDevice(dp->device);
+        for (Queue& q : dp->queues) {
+            if (q.stream != nullptr) {
+                (void)hipStreamSynchronize(q.stream);
+            }
+        }
+        if (dp->comm != nullptr) {
+            (void)hipStreamSynchronize(dp->comm);
+        }
+    }
+    for (void* c : m_comms) {
+        (void)ncclCommDestroy(static_cast<ncclComm_t>(c));
+    }
+    m_comms.clear();
+    for (auto& dp : m_dev) {
+        if (!dp) {
+            continue;
+        }
+        (void)hipSetDevice(dp->device);
+        for (Queue& q : dp->queues) {
+            q.scene.reset();
+            (void)hipFree(q.send);
+            (void)hipFree(q.recv);
+            (void)hipFree(q.rgba);
+            q.send = q.recv = nullptr;
+            q.rgba = nullptr;
+            if (q.traced != nullptr) {
+                (void)hipEventDestroy(q.traced);
+            }
+            if (q.exchanged != nullptr) {
+                (void)hipEventDestroy(q.exchanged);
+            }
+            if (q.stream != nullptr) {
+                (void)hipStreamDestroy(q.stream);
+            }
+            q.traced = q.exchanged = nullptr;
+            q.stream = nullptr;
+        }
+        dp->queues.clear();
+        (void)hipFree(dp->full);
+        (void)hipFree(dp->band_in);
+        dp->full = dp->band_in = nullptr;
+        if (dp->comm != nullptr) {
+            (void)hipStreamDestroy(dp->comm);
+            dp->comm = nullptr;
+        }
+    }
+    m_dev.clear();
+}
+
+std::size_t FrameEngine::band_rows(std::size_t local) const { return local < m_dev.size() ? m_dev[local]->rows : 0; }
+
+std::size_t FrameEngine::frames_rendered() const {
+    return m_run_batches * m_opt.batch * (m_bands ? 1 : m_world);
+}
+
+double FrameEngine::exchange_bytes_per_frame() const {
+    if (!m_bands || m_world == 1) {
+        return 0.0;
+    }
+    return static_cast<double>(m_world - 1) * static_cast<double>(m_split.BufferRows() * m_width) * 4.0;
+}
+
+void FrameEngine::SetInputs(const float* host_offsets, std::size_t count) {
+    if (host_offsets == nullptr || count == 0) {
+        throw std::runtime_error("SetInputs: no input frames");
+    }
+    const bool exchange = m_bands && m_world > 1;
+    if (exchange && count > 1 &&
+        (count % m_opt.batch != 0 || (m_plan.exchange == EngineOptions::kAllToAll && m_opt.batch % m_world != 0))) {
+        throw std::runtime_error("SetInputs: with bands over " + std::to_string(m_world) + " devices, " +
+                                 std::to_string(count) + " inputs need a multiple of the batch (" +
+                                 std::to_string(m_opt.batch) + ") and a batch divisible by the devices");
+    }
+    const std::size_t ff = FrameFloats();
+    for (auto& dp : m_dev) {
+        Device& d = *dp;
+        DeviceGuard guard(d.device);
+        for (Queue& q : d.queues) {
+            HipCheck(hipStreamSynchronize(q.stream), "hipStreamSynchronize(inputs)");
+            q.used = false;  // frames of the previous inputs are no longer verifiable / readable
+        }
+        (void)hipFree(d.full);
+        (void)hipFree(d.band_in);
+        d.full = d.band_in = nullptr;
+        d.full = DeviceAlloc<float>(count * ff, "hipMalloc(inputs)");
+        HipCheck(hipMemcpy(d.full, host_offsets, count * ff * sizeof(float), hipMemcpyHostToDevice),
+                 "hipMemcpy(inputs)");
+        if (exchange) {  // the band's rows of every input, band-local and contiguous
+            const std::size_t row_floats = m_width * 2;
+            std::vector<float> band(count * d.rows * row_floats);
+            for (std::size_t r = 0; r < count; ++r) {
+                for (std::size_t y = 0; y < d.rows; ++y) {
+                    const std::size_t fy = m_split.FrameRow(d.band, y);
+                    std::memcpy(band.data() + (r * d.rows + y) * row_floats, host_offsets + r * ff + fy * row_floats,
+                                row_floats * sizeof(float));
+                }
+            }
+            d.band_in = DeviceAlloc<float>(band.size(), "hipMalloc(band inputs)");
+            HipCheck(hipMemcpy(d.band_in, band.data(), band.size() * sizeof(float), hipMemcpyHostToDevice),
+                     "hipMemcpy(band inputs)");
+        }
+    }
+    m_inputs = count;
+}
+
+const float* FrameEngine::FullInput(std::size_t local, std::size_t k) const {
+    return m_dev[local]->full + (k % m_inputs) * FrameFloats();
+}
+
+const float* FrameEngine::BandInput(std::size_t local, std::size_t k) const {
+    const Device& d = *m_dev[local];
+    return d.band_in + (k % m_inputs) * d.rows * m_width * 2;
+}
+
+void FrameEngine::TracePhase(std::size_t local, std::size_t b) {
+    Device& d = *m_dev[local];
+    const std::size_t qi = b % m_opt.queues;
+    Queue& q = d.queues[qi];
+    const std::size_t F = m_opt.batch, k0 = b * F;
+    const bool exchange = m_bands && m_world > 1;
+    if (exchange && q.used) {
+        // This queue's send / receive buffers are free once its previous batch's exchange is done
+        // (RCCL: on this device's comm stream; copies: every peer read our send buffer on its own).
+        HipCheck(hipStreamWaitEvent(q.stream, q.exchanged, 0), "hipStreamWaitEvent(exchanged)");
+        if (m_copy) {
+            for (std::size_t p = 0; p < m_dev.size(); ++p) {
+                if (p != local) {
+                    HipCheck(hipStreamWaitEvent(q.stream, m_dev[p]->queues[qi].exchanged, 0),
+                             "hipStreamWaitEvent(peer exchanged)");
+                }
+            }
+        }
+    }
+    q.used = true;
+    q.last_batch = b;
+    const float* offs[kMaxBatch];
+    float* rgba[kMaxBatch];
+    int* ids[kMaxBatch];
+    const std::size_t frame_floats4 = m_width * m_height * 4;
+    if (!exchange) {  // whole frames, traced and shaded in one kernel
+        for (std::size_t f0 = 0; f0 < F; f0 += kMaxBatch) {
+            const std::size_t n = std::min<std::size_t>(kMaxBatch, F - f0);
+            for (std::size_t j = 0; j < n; ++j) {
+                offs[j] = FullInput(local, k0 + f0 + j);
+                rgba[j] = q.rgba + (f0 + j) * frame_floats4;
+            }
+            q.scene->TraceBatch(offs, rgba, nullptr, n, 0, m_height, m_opt.variant, q.stream, 1);
+        }
+        return;
+    }
+    const std::size_t band_pixels = m_split.BufferRows() * m_width;
+    const std::size_t self = d.band;
+    const std::size_t n_self = m_plan.FramesFor(b, self);
+    if (d.rows != 0) {
+        for (std::size_t f0 = 0; f0 < F; f0 += kMaxBatch) {
+            const std::size_t n = std::min<std::size_t>(kMaxBatch, F - f0);
+            for (std::size_t j = 0; j < n; ++j) {
+                const std::size_t f = f0 + j;
+                const std::size_t c = m_plan.Compositor(b, f), slot = m_plan.Slot(f);
+                offs[j] = BandInput(local, k0 + f);
+                ids[j] = c == self ? q.recv + (self * n_self + slot) * band_pixels
+                                   : q.send + SendPixels(m_plan, c, slot, band_pixels);
+            }
+            q.scene->TraceBatch(offs, nullptr, ids, n, d.row_begin, d.rows, m_opt.variant, q.stream,
+                                m_split.Interleave());
+        }
+    }
+    HipCheck(hipEventRecord(q.traced, q.stream), "hipEventRecord(traced)");
+}
+
+void FrameEngine::ExchangePhase(std::size_t local, std::size_t b) {
+    Device& d = *m_dev[local];
+    Queue& q = d.queues[b % m_opt.queues];
+    const std::size_t band_pixels = m_split.BufferRows() * m_width;
+    const std::size_t self = d.band, n_self = m_plan.FramesFor(b, self);
+    auto comm = static_cast<ncclComm_t>(m_comms[local]);
+    HipCheck(hipStreamWaitEvent(d.comm, q.traced, 0), "hipStreamWaitEvent(traced)");
+    for (std::size_t p = 0; p < m_world; ++p) {
+        if (p == self) {
+            continue;
+        }
+        const std::size_t n_p = m_plan.FramesFor(b, p);
+        if (n_p != 0) {
+            NcclCheck(ncclSend(q.send + SendPixels(m_plan, p, 0, band_pixels), n_p * band_pixels, ncclInt32,
+                               static_cast<int>(p), comm, d.comm),
+                      "ncclSend(band ids)");
+        }
+        if (n_self != 0) {
+            NcclCheck(ncclRecv(q.recv + p * n_self * band_pixels, n_self * band_pixels, ncclInt32, static_cast<int>(p),
+                               comm, d.comm),
+                      "ncclRecv(band ids)");
+        }
+    }
+}
+
+void FrameEngine::CopyPhase(std::size_t local, std::size_t b) {
+    Device& d = *m_dev[local];
+    const std::size_t qi = b % m_opt.queues;
+    Queue& q = d.queues[qi];
+    const std::size_t band_pixels = m_split.BufferRows() * m_width;
+    const std::size_t self = d.band, n_self = m_plan.FramesFor(b, self);
+    HipCheck(hipStreamWaitEvent(d.comm, q.traced, 0), "hipStreamWaitEvent(traced)");
+    if (n_self != 0) {
+        for (std::size_t p = 0; p < m_dev.size(); ++p) {
+            if (p == local) {
+                continue;
+            }
+            Device& peer = *m_dev[p];
+            Queue& pq = peer.queues[qi];
+            HipCheck(hipStreamWaitEvent(d.comm, pq.traced, 0), "hipStreamWaitEvent(peer traced)");
+            HipCheck(hipMemcpyPeerAsync(q.recv + peer.band * n_self * band_pixels, d.device,
+                                        pq.send + SendPixels(m_plan, self, 0, band_pixels), peer.device,
+                                        n_self * band_pixels * sizeof(int), d.comm),
+                     "hipMemcpyPeerAsync(band ids)");
+        }
+    }
+    HipCheck(hipEventRecord(q.exchanged, d.comm), "hipEventRecord(exchanged)");
+}
+
+void FrameEngine::ShadePhase(std::size_t local, std::size_t b) {
+    Device& d = *m_dev[local];
+    Queue& q = d.queues[b % m_opt.queues];
+    const std::size_t self = d.band, n_self = m_plan.FramesFor(b, self);
+    if (n_self == 0) {
+        return;
+    }
+    HipCheck(hipStreamWaitEvent(q.stream, q.exchanged, 0), "hipStreamWaitEvent(exchanged)");
+    // The compositor's frames in slot order read evenly strided inputs (SetInputs' condition).
+    const std::size_t F = m_opt.batch, k0 = b * F;
+    const bool a2a = m_plan.exchange == EngineOptions::kAllToAll;
+    const std::size_t first = k0 + (a2a ? self : 0);
+    const std::size_t stride = m_inputs == 1 ? 0 : (a2a ? m_world : 1) * FrameFloats();
+    q.scene->Shade(FullInput(local, first), q.recv, q.rgba, 0, m_height, q.stream, n_self, m_split.BufferRows(),
+                   m_split.interleaved ? m_world : 0, stride);
+}
+
+void FrameEngine::RunWorker(std::size_t local, std::size_t b0, std::size_t batches) {
+    Device& d = *m_dev[local];
+    DeviceGuard guard(d.device);
+    const bool exchange = m_bands && m_world > 1;
+    for (std::size_t b = b0; b < b0 + batches; ++b) {
+        TracePhase(local, b);
+        if (!exchange) {
+            continue;
+        }
+        Queue& q = d.queues[b % m_opt.queues];
+        if (m_copy) {
+            Barrier();  // every device's trace of batch b is enqueued (its `traced` recorded)
+            CopyPhase(local, b);
+            Barrier();  // every `exchanged` recorded before any device reuses a send buffer
+        } else {
+            NcclCheck(ncclGroupStart(), "ncclGroupStart");
+            try {
+                ExchangePhase(local, b);
+            } catch (...) {
+                (void)ncclGroupEnd();
+                throw;
+            }
+            NcclCheck(ncclGroupEnd(), "ncclGroupEnd");
+            HipCheck(hipEventRecord(q.exchanged, d.comm), "hipEventRecord(exchanged)");
+        }
+        ShadePhase(local, b);
+    }
+    for (Queue& q : d.queues) {
+        HipCheck(hipStreamSynchronize(q.stream), "render (queue)");
+    }
+    HipCheck(hipStreamSynchronize(d.comm), "render (exchange)");
+}
+
+void FrameEngine::Barrier() {
+    if (m_pool) {
+        m_pool->Barrier();
+    }
+}
+
+void FrameEngine::Run(std::size_t batches) {
+    if (m_inputs == 0) {
+        throw std::runtime_error("Run: SetInputs() has not been called");
+    }
+    const std::size_t b0 = m_next_batch;
+    m_run_batches = batches;
+    if (batches == 0) {
+        return;
+    }
+    m_next_batch += batches;
+    if (m_pool) {
+        const std::function<void(std::size_t)> job = [this, b0, batches](std::size_t i) { RunWorker(i, b0, batches); };
+        m_pool->Run(job);
+    } else {
+        RunWorker(0, b0, batches);
+    }
+}
+
+bool FrameEngine::ReadFrame(std::size_t k, float* host_rgba) {
+    const std::size_t F = m_opt.batch, b = k / F, f = k % F;
+    if (b >= m_next_batch || b + m_opt.queues < m_next_batch) {
+        return false;
+    }
+    const bool exchange = m_bands && m_world > 1;
+    std::size_t local = 0, slot = f;
+    if (exchange) {
+        const std::size_t c = m_plan.Compositor(b, f);
+        if (c < m_rank0 || c >= m_rank0 + m_dev.size()) {
+            return false;
+        }
+        local = c - m_rank0;
+        slot = m_plan.Slot(f);
+    }
+    Device& d = *m_dev[local];
+    Queue& q = d.queues[b % m_opt.queues];
+    if (!q.used || q.last_batch != b) {
+        return false;
+    }
+    DeviceGuard guard(d.device);
+    HipCheck(hipStreamSynchronize(q.stream), "hipStreamSynchronize(read frame)");
+    const std::size_t frame_floats4 = m_width * m_height * 4;
+    HipCheck(hipMemcpy(host_rgba, q.rgba + slot * frame_floats4, frame_floats4 * sizeof(float), hipMemcpyDeviceToHost),
+             "hipMemcpy(read frame)");
+    return true;
+}
+
+std::size_t FrameEngine::Verify(std::size_t* checked) {
+    const std::size_t F = m_opt.batch;
+    const std::size_t frame_floats4 = m_width * m_height * 4;
+    const bool exchange = m_bands && m_world > 1;
+    std::size_t bad = 0, count = 0;
+    std::vector<float> got(frame_floats4);
+    for (std::size_t local = 0; local < m_dev.size(); ++local) {
+        Device& d = *m_dev[local];
+        DeviceGuard guard(d.device);
+        // Reference: one full-frame fused trace per input on a fresh scene of this device.
+        DeviceScene ref_scene(*m_scene, d.device);
+        hipStream_t st = nullptr;
+        HipCheck(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate(verify)");
+        float* ref_dev = nullptr;
+        std::vector<std::vector<float>> refs(m_inputs);
+        try {
+            ref_dev = DeviceAlloc<float>(frame_floats4, "hipMalloc(verify)");
+            ref_scene.Prepare(m_width, m_height, st);
+            for (Queue& q : d.queues) {
+                if (!q.used) {
+                    continue;
+                }
+                HipCheck(hipStreamSynchronize(q.stream), "hipStreamSynchronize(verify)");
+                const std::size_t b = q.last_batch;
+                for (std::size_t f = 0; f < F; ++f) {
+                    std::size_t slot = f;
+                    if (exchange) {
+                        if (m_plan.Compositor(b, f) != d.band) {
+                            continue;
+                        }
+                        slot = m_plan.Slot(f);
+                    }
+                    const std::size_t r = (b * F + f) % m_inputs;
+                    if (refs[r].empty()) {
+                        ref_scene.Trace(FullInput(local, r), ref_dev, 0, m_height, m_opt.variant == kTraceCull ? kTraceLds
+                                                                                                              : kTraceCull,
+                                        st);
+                        HipCheck(hipStreamSynchronize(st), "verify render");
+                        refs[r].resize(frame_floats4);
+                        HipCheck(hipMemcpy(refs[r].data(), ref_dev, frame_floats4 * sizeof(float),
+                                           hipMemcpyDeviceToHost),
+                                 "hipMemcpy(verify reference)");
+                    }
+                    HipCheck(hipMemcpy(got.data(), q.rgba + slot * frame_floats4, frame_floats4 * sizeof(float),
+                                       hipMemcpyDeviceToHost),
+                             "hipMemcpy(verify frame)");
+                    ++count;
+                    if (std::memcmp(got.data(), refs[r].data(), frame_floats4 * sizeof(float)) != 0) {
+                        ++bad;
+                    }
+                }
+            }
+        } catch (...) {
+            (void)hipFree(ref_dev);
+            (void)hipStreamDestroy(st);
+            throw;
+        }
+        (void)hipFree(ref_dev);
+        (void)hipStreamDestroy(st);
+    }
+    if (checked != nullptr) {
+        *checked = count;
+    }
+    return bad;
+}
+
+DeviceScene::StageTimes FrameEngine::MeasureStages(std::size_t local, std::size_t launches) {
+    if (local >= m_dev.size()) {
+        throw std::runtime_error("MeasureStages: no local device " + std::to_string(local));
+    }
+    if (m_inputs == 0) {
+        throw std::runtime_error("MeasureStages: SetInputs() has not been called");
+    }
+    Device& d = *m_dev[local];
+    DeviceGuard guard(d.device);
+    Queue& q = d.queues[0];
+    for (Queue& qq : d.queues) {
+        HipCheck(hipStreamSynchronize(qq.stream), "hipStreamSynchronize(stages)");
+    }
+    HipCheck(hipStreamSynchronize(d.comm), "hipStreamSynchronize(stages)");
+    const bool exchange = m_bands && m_world > 1;
+    q.scene->TakeTimes();
+    q.scene->SetTiming(true);
+    try {
+        for (std::size_t i = 0; i < launches; ++i) {
+            if (exchange) {
+                const float* offs[1] = {BandInput(local, i)};
+                int* ids[1] = {q.send};
+                if (d.rows != 0) {
+                    q.scene->TraceBatch(offs, nullptr, ids, 1, d.row_begin, d.rows, m_opt.variant, q.stream,
+                                        m_split.Interleave());
+                }
+            } else {
+                const float* offs[1] = {FullInput(local, i)};
+                float* rgba[1] = {q.rgba};
+                q.scene->TraceBatch(offs, rgba, nullptr, 1, 0, m_height, m_opt.variant, q.stream, 1);
+            }
+        }
+    } catch (...) {
+        q.scene->SetTiming(false);
+        throw;
+    }
+    q.scene->SetTiming(false);
+    const DeviceScene::StageTimes t = q.scene->TakeTimes();
+    q.used = false;  // its buffers now hold measurement frames, not a batch (Verify / ReadFrame skip it)
+    return t;
+}
+
+}  // namespace srt

@@ -1,0 +1,157 @@
+// Frame engine: a stream of frames rendered over one or more GPUs (SURVEY.md section 8 rows a9-a13,
+// (e)), the native counterpart of what bench.py and a multi-GPU host renderer drive.
+//
+// A run is a sequence of *batches* of F frames. Each local device keeps Q frame queues (its own
+// DeviceScene, HIP stream and buffers each); batch b runs on queue b % Q of every device, so Q
+// batches are in flight per device.
+//
+// Split "bands" over P devices (BASELINE config C4): every frame is cut into P row bands -- the
+// frame's 16-row tile rows dealt round-robin (interleaved, default) or P contiguous blocks --,
+// device d traces band d of the batch's F frames (hit ids only, 4 B per pixel), the bands move to
+// the frames' compositors over RCCL, and each compositor shades its frames from the gathered ids
+// (deferred shading, bit-identical to the fused trace). Exchange patterns:
+//   kAllToAll       frame f of a batch is composited on device f % P: the batch's P gathers
+//                   (one per compositor) are fused into one group of ncclSend / ncclRecv, so every
+//                   directed xGMI link carries 1/P of the payload;
+//   kRotatingGather the whole batch is gathered to device b % P (one gather per batch);
+//   kRootGather     everything to device 0.
+// P == 1 traces and shades in one kernel (RGBA), no exchange.
+// Split "frames": every device renders whole frames of its own (no exchange; weak scaling).
+//
+// Devices are either all in this process (one worker thread per device, communicators from
+// ncclCommInitAll; a repeated device -- "fake devices" on a one-GPU box -- or SRT_GATHER=copy
+// exchanges by device copies instead), or one per process (rank mode: ncclCommInitRank with a
+// unique id the ranks share, one rank per GPU as torch.distributed.run launches them).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <memory>
+#include <vector>
+
+#include "renderer.h"
+#include "scene.h"
+
+namespace srt {
+
+struct EngineOptions {
+    enum Split { kBands = 0, kFrames = 1 };
+    enum Exchange { kAllToAll = 0, kRotatingGather = 1, kRootGather = 2 };
+    int variant = 2;           // render.h TraceVariant (kTraceCull)
+    std::size_t queues = 2;    // batches in flight per device
+    std::size_t batch = 16;    // frames per batch
+    bool interleaved = true;   // bands: tile rows dealt round-robin (else contiguous blocks)
+    int exchange = kAllToAll;  // bands at P > 1
+    int split = kBands;
+};
+
+// Row bands of an H-row frame over P devices (interleaved or contiguous), the layout every
+// exchange path and the shading kernel agree on.
+struct BandSplit {
+    std::size_t height = 0, bands = 1;
+    bool interleaved = true;
+    static BandSplit Make(std::size_t height, std::size_t bands, bool interleaved);
+    std::size_t RowBegin(std::size_t band) const;  // first frame row (interleaved: band * 16)
+    std::size_t RowCount(std::size_t band) const;  // rows of the band
+    std::size_t BufferRows() const;                // rows of every band's (padded) buffer
+    std::size_t Interleave() const { return interleaved && bands > 1 ? bands : 1; }
+    std::size_t FrameRow(std::size_t band, std::size_t local) const;
+};
+
+// Which device composites frame f of batch b, and that frame's slot among the device's frames.
+struct ExchangePlan {
+    std::size_t bands = 1, batch = 1;
+    int exchange = EngineOptions::kAllToAll;
+    std::size_t Compositor(std::size_t batch_index, std::size_t f) const;
+    std::size_t Slot(std::size_t f) const;                                      // index among its compositor's frames
+    std::size_t FramesFor(std::size_t batch_index, std::size_t compositor) const;  // frames composited there
+    std::size_t MaxFramesPerCompositor() const;
+};
+
+// Host self-test of the exchange (no device): band_ids[d] = device d's traced ids of the batch's F
+// frames, frame-major (F x buffer rows x width int32, its own band). Returns, for compositor c,
+// its receive buffer exactly as the device path lays it out: [P][FramesFor(b, c)][buffer rows][W].
+std::vector<std::vector<int>> ExchangeOnHost(const BandSplit& split, const ExchangePlan& plan, std::size_t width,
+                                             std::size_t batch_index, const std::vector<std::vector<int>>& band_ids);
+
+class FrameEngine {
+public:
+    // All devices in this process.
+    FrameEngine(const Scene& scene, const std::vector<int>& devices, std::size_t width, std::size_t height,
+                const EngineOptions& options);
+    // One device of a `world`-device job, this process being `rank` (unique_id: 128 bytes from
+    // UniqueId() on rank 0, shared by every rank; every rank constructs concurrently).
+    FrameEngine(const Scene& scene, int device, int rank, int world, const void* unique_id, std::size_t width,
+                std::size_t height, const EngineOptions& options);
+    ~FrameEngine();
+    FrameEngine(const FrameEngine&) = delete;
+    FrameEngine& operator=(const FrameEngine&) = delete;
+
+    static void UniqueId(void* out128);
+
+    // `count` full-frame sample-offset images (count x H x W x 2 floats, host), resident on every
+    // local device from now on (each device keeps the frames and its band's rows of each); frame k
+    // of a run reads input k % count. Bands at P > 1 with count > 1 need count % batch == 0 and
+    // (all-to-all) batch % P == 0, so a compositor's frames read evenly strided inputs.
+    void SetInputs(const float* host_offsets, std::size_t count);
+    // Render `batches` batches (batch x frames each), continuing the frame sequence; returns when
+    // every local device has finished.
+    void Run(std::size_t batches);
+    // Every frame composited locally in each queue's last batch, compared bit for bit with a
+    // single-device full-frame render of its input. Returns the number of mismatching frames;
+    // `checked` receives the number compared.
+    std::size_t Verify(std::size_t* checked);
+    // Frame k (of the last Q batches) into host RGBA (H x W x 4 floats); false when frame k is not
+    // resident on a local device (another rank composited it, or it is older).
+    bool ReadFrame(std::size_t k, float* host_rgba);
+    // Stage times of `launches` single-frame traces of local device `local`'s band (HIP events bound
+    // to the kernels' dispatches): mean ms of tile info, record setup + bins + work list, trace.
+    DeviceScene::StageTimes MeasureStages(std::size_t local, std::size_t launches);
+
+    std::size_t devices() const { return m_world; }
+    std::size_t local_devices() const { return m_dev.size(); }
+    std::size_t frames_per_batch() const { return m_opt.batch; }
+    std::size_t frames_rendered() const;  // this run's frames over all devices (frames split: x P)
+    std::size_t band_rows(std::size_t local) const;
+    std::size_t buffer_rows() const { return m_split.BufferRows(); }
+    bool uses_rccl() const { return !m_comms.empty(); }
+    std::uint64_t triangles() const { return m_n; }
+    // Bytes each device sends per batch on average (bands at P > 1), for the report.
+    double exchange_bytes_per_frame() const;
+
+private:
+    struct Queue;
+    struct Device;
+    struct Pool;
+    void Init(const Scene& scene, const std::vector<int>& devices);
+    void Release() noexcept;
+    void AllocateQueues();
+    void TracePhase(std::size_t local, std::size_t b);
+    void ExchangePhase(std::size_t local, std::size_t b);  // RCCL: inside a group
+    void CopyPhase(std::size_t local, std::size_t b);      // device-copy exchange
+    void ShadePhase(std::size_t local, std::size_t b);
+    void RunWorker(std::size_t local, std::size_t b0, std::size_t batches);
+    void Barrier();
+    const float* BandInput(std::size_t local, std::size_t k) const;
+    const float* FullInput(std::size_t local, std::size_t k) const;
+    std::size_t FrameFloats() const { return m_width * m_height * 2; }
+
+    EngineOptions m_opt;
+    std::size_t m_width = 0, m_height = 0, m_world = 1, m_rank0 = 0;  // m_rank0: global index of local 0
+    std::uint64_t m_n = 0;
+    bool m_bands = true;       // bands split at P > 1 (exchange + shading)
+    bool m_copy = false;       // exchange by device copies (repeated device / SRT_GATHER=copy)
+    BandSplit m_split;
+    ExchangePlan m_plan;
+    std::vector<std::unique_ptr<Device>> m_dev;
+    std::vector<void*> m_comms;  // ncclComm_t per local device
+    std::unique_ptr<Pool> m_pool;
+    std::size_t m_inputs = 0;
+    std::size_t m_next_batch = 0;  // batches issued so far (the frame sequence continues across runs)
+    std::size_t m_run_batches = 0;
+    std::unique_ptr<Scene> m_scene;  // for Verify's reference renders
+};
+
+}  // namespace srt

@@ -209,9 +209,12 @@ hipError_t LaunchCullFrames(const CullFrame* frames, std::size_t count, std::uin
 // gather of `frames` frames of band_rows-row bands; band_rows 0 = one band of row_count rows),
 // into band.rgba[frame][row_count][width].
 // interleaved > 0: the ids' bands are that many interleaved bands (BandArgs::row_interleave).
+// offsets_stride: floats between consecutive frames' sample offsets (0: every frame of the batch
+// shares band.offsets; a multiple of 2).
 hipError_t LaunchShade(const float* d_vertices, const float* d_albedo, const float* d_edges, std::uint64_t n,
                        const Frame& frame, const float background[3], const BandArgs& band, hipStream_t stream,
-                       std::size_t frames = 1, std::size_t band_rows = 0, std::size_t interleaved = 0);
+                       std::size_t frames = 1, std::size_t band_rows = 0, std::size_t interleaved = 0,
+                       std::size_t offsets_stride = 0);
 
 // Spatial order of the records (spatial.hip): ids sorted by the Morton code of their centroid's
 // image-plane position under the scene camera, on the device (keys + rocPRIM radix sort), and

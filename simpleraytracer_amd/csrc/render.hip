@@ -511,7 +511,8 @@ __device__ __forceinline__ void ShadeAndStore(const TraceParams& p, int x, int y
 // `interleaved` bands the bands took the frame's tile rows round-robin: row y is row
 // (t / bands) * kCullTileRows + y % kCullTileRows of band t % bands, t = y / kCullTileRows.
 __global__ __launch_bounds__(256) void ShadeIdsKernel(TraceParams p, const int* __restrict__ ids,
-                                                      unsigned band_rows, unsigned frames, unsigned interleaved) {
+                                                      unsigned band_rows, unsigned frames, unsigned interleaved,
+                                                      size_t offsets_stride) {
     const size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     const size_t pixels = static_cast<size_t>(p.width) * p.row_count;
     if (i >= pixels) {
@@ -530,7 +531,7 @@ __global__ __launch_bounds__(256) void ShadeIdsKernel(TraceParams p, const int* 
         local = static_cast<unsigned>(y) - band * band_rows;
     }
     const size_t at = ((static_cast<size_t>(band) * frames + g) * band_rows + local) * p.width + x;
-    const float2 o = p.offsets[i];
+    const float2 o = p.offsets[i + g * offsets_stride];  // frame g's sample offsets (stride 0: shared)
     const float fx = (static_cast<float>(x) + o.x) / p.wf;
     const float fy = (static_cast<float>(FrameRow(p.row_begin, p.row_interleave, y)) + o.y) / p.hf;
     const int id = ids[at];
@@ -3045,7 +3046,8 @@ std::size_t InterleavedBandRows(std::size_t height, std::size_t bands, std::size
 
 hipError_t LaunchShade(const float* d_vertices, const float* d_albedo, const float* d_edges, std::uint64_t n,
                        const Frame& frame, const float background[3], const BandArgs& band, hipStream_t stream,
-                       std::size_t frames, std::size_t band_rows, std::size_t interleaved) {
+                       std::size_t frames, std::size_t band_rows, std::size_t interleaved,
+                       std::size_t offsets_stride) {
     if (band.row_count == 0 || band.width == 0 || frames == 0) {
         return hipSuccess;
     }
@@ -3078,7 +3080,7 @@ hipError_t LaunchShade(const float* d_vertices, const float* d_albedo, const flo
     const std::size_t pixels = band.width * band.row_count;
     hipLaunchKernelGGL(ShadeIdsKernel, dim3(static_cast<unsigned>((pixels + 255) / 256), static_cast<unsigned>(frames)),
                        dim3(256), 0, stream, p, static_cast<const int*>(band.ids), static_cast<unsigned>(band_rows),
-                       static_cast<unsigned>(frames), static_cast<unsigned>(interleaved));
+                       static_cast<unsigned>(frames), static_cast<unsigned>(interleaved), offsets_stride / 2);
     return hipGetLastError();
 }
 

@@ -6,31 +6,13 @@
 #include <cstdlib>
 #include <cstring>
 #include <sstream>
+#include <type_traits>
 
+#include "engine.h"
 #include "render.h"
 
 namespace srt {
 namespace {
-
-// Restores the caller's current HIP device on scope exit (the C ABI must not leak a
-// hipSetDevice into the host application).
-class DeviceGuard {
-public:
-    explicit DeviceGuard(int device) {
-        if (hipGetDevice(&m_prev) != hipSuccess) {
-            m_prev = -1;
-        }
-        HipCheck(hipSetDevice(device), "hipSetDevice");
-    }
-    ~DeviceGuard() {
-        if (m_prev >= 0) {
-            (void)hipSetDevice(m_prev);
-        }
-    }
-
-private:
-    int m_prev = -1;
-};
 
 void NcclCheck(ncclResult_t res, const char* what) {
     if (res != ncclSuccess) {
@@ -108,29 +90,6 @@ std::vector<int> VisibleDevices() {
         devices.push_back(0);
     }
     return devices;
-}
-
-GatherPlan GatherPlan::Make(std::size_t width, std::size_t height, std::size_t bands, std::size_t elem) {
-    GatherPlan p;
-    p.width = width;
-    p.height = height;
-    p.bands = bands == 0 ? 1 : bands;
-    p.band_rows = (height + p.bands - 1) / p.bands;
-    p.elem = elem;
-    return p;
-}
-
-std::size_t GatherPlan::RowCount(std::size_t i) const {
-    const std::size_t end = (i + 1) * band_rows < height ? (i + 1) * band_rows : height;
-    return end - RowBegin(i);
-}
-
-void GatherOnHost(const GatherPlan& plan, const void* const* bands, void* gather_buf, void* frame) {
-    auto* g = static_cast<unsigned char*>(gather_buf);
-    for (std::size_t i = 0; i < plan.bands; ++i) {
-        std::memcpy(g + plan.RecvOffset(i), bands[i], plan.BandBytes());
-    }
-    std::memcpy(frame, g, plan.FrameBytes());
 }
 
 int TraceVariantFromEnv() {
@@ -235,12 +194,18 @@ void DeviceScene::Prepare(std::size_t width, std::size_t height, hipStream_t str
 
 void DeviceScene::OrderAfterPrevious(hipStream_t stream) const {
     if (m_used && stream != m_last_stream) {
-        if (m_order_event == nullptr) {
-            HipCheck(hipEventCreateWithFlags(&m_order_event, hipEventDisableTiming), "hipEventCreate(scene order)");
-        }
-        HipCheck(hipEventRecord(m_order_event, m_last_stream), "hipEventRecord(scene order)");
         HipCheck(hipStreamWaitEvent(stream, m_order_event, 0), "hipStreamWaitEvent(scene order)");
     }
+}
+
+// Marks the end of this call's work on `stream`: the next call on another stream waits for it. The
+// event is recorded on the call's own stream, so the library never touches a stream after the call
+// that was given it has returned (the caller may destroy it).
+void DeviceScene::RecordOrder(hipStream_t stream) const {
+    if (m_order_event == nullptr) {
+        HipCheck(hipEventCreateWithFlags(&m_order_event, hipEventDisableTiming), "hipEventCreate(scene order)");
+    }
+    HipCheck(hipEventRecord(m_order_event, stream), "hipEventRecord(scene order)");
     m_used = true;
     m_last_stream = stream;
 }
@@ -257,7 +222,7 @@ void DeviceScene::NormalsIfStale(hipStream_t stream) const {
 
 void DeviceScene::Shade(const float* d_offsets, const int* d_ids, float* d_rgba, std::size_t row_begin,
                         std::size_t row_count, hipStream_t stream, std::size_t frames, std::size_t band_rows,
-                        std::size_t interleaved) const {
+                        std::size_t interleaved, std::size_t offsets_stride) const {
     if (m_width == 0) {
         throw std::runtime_error("Shade: Prepare() has not been called");
     }
@@ -277,8 +242,9 @@ void DeviceScene::Shade(const float* d_offsets, const int* d_ids, float* d_rgba,
     NormalsIfStale(stream);
     BandArgs band{d_offsets, d_rgba, m_width, m_height, row_begin, row_count, const_cast<int*>(d_ids)};
     HipCheck(LaunchShade(m_vertices, m_albedo, m_edges, m_n, m_frame, m_background, band, stream, frames, band_rows,
-                         interleaved),
+                         interleaved, offsets_stride),
              "shade kernel launch");
+    RecordOrder(stream);
 }
 
 // Grow-only cull work for `slots` frame slots of one carve-up (render.h CullBins; counters reset
@@ -378,6 +344,7 @@ void DeviceScene::TraceBatch(const float* const* d_offsets, float* const* d_rgba
                               m_timing ? &ev : nullptr),
              "batched trace launch");
     m_normals_current = true;  // slot 0's normals (the tile-planar records are the full pass's)
+    RecordOrder(stream);
 }
 
 void DeviceScene::Trace(const float* d_offsets, float* d_rgba, std::size_t row_begin, std::size_t row_count,
@@ -415,6 +382,7 @@ void DeviceScene::Trace(const float* d_offsets, float* d_rgba, std::size_t row_b
     if (use_bins != nullptr && row_count != 0) {
         m_normals_current = true;
     }
+    RecordOrder(stream);
 }
 
 // With stage timing on: events for one traced call (a batch counts as one call).
@@ -486,18 +454,31 @@ struct Renderer::Slot {
     int device = 0;
     hipStream_t stream = nullptr;
     std::unique_ptr<DeviceScene> scene;
-    float* offsets = nullptr;  // band_rows x W x 2
-    float* rgba = nullptr;     // band_rows x W x 4
-    std::uint16_t* offsets16 = nullptr;  // FLOAT16 input: band_rows x W x 2 halves (H2D staging)
-    std::uint16_t* rgba16 = nullptr;     // FLOAT16 output: band_rows x W x 4 halves
+    std::size_t band = 0;  // band index (= slot index)
     std::size_t row_begin = 0;
     std::size_t row_count = 0;
     // Pipelined single-device render (Renderer::RenderPipelined): copy streams and per-chunk
-    // events (H2D done, chunk traced).
+    // events (H2D done, chunk traced); `traced[0]` also orders the device-copy gather.
     hipStream_t copy_in = nullptr;
     hipStream_t copy_out = nullptr;
     std::vector<hipEvent_t> in_done;
     std::vector<hipEvent_t> traced;
+};
+
+// The buffers of one frame size (Configure builds a new set before releasing the old one).
+struct Renderer::Buffers {
+    std::vector<int> devices;
+    std::vector<float*> offsets;           // band rows x W x 2 per slot (one device: the frame)
+    std::vector<std::uint16_t*> offsets16;  // FLOAT16 input: H2D staging
+    std::vector<float*> rgba;              // band rows x W x 4 (direct mode, one device)
+    std::vector<std::uint16_t*> rgba16;    // FLOAT16 output staging of rgba
+    std::vector<int*> ids;                 // band rows x W hit ids (gather modes)
+    int root = 0;
+    float* full = nullptr;                 // root: the frame's offsets (shading), H x W x 2
+    std::uint16_t* full16 = nullptr;
+    int* gather = nullptr;                 // root: bands x band rows x W gathered ids
+    float* frame = nullptr;                // root: H x W x 4 shaded frame
+    std::uint16_t* frame16 = nullptr;
 };
 
 namespace {
@@ -507,19 +488,35 @@ std::size_t E2eChunks() {
     const long c = v == nullptr || *v == '\0' ? 4 : std::strtol(v, nullptr, 10);
     return c < 1 ? 1 : (c > 16 ? 16 : static_cast<std::size_t>(c));
 }
+
+bool InterleavedFromEnv() {
+    const char* v = std::getenv("SRT_BAND_ROWS");
+    return v == nullptr || std::strcmp(v, "contiguous") != 0;
+}
+
+template <class T>
+void FreeOn(int device, T*& p) noexcept {
+    if (p != nullptr) {
+        (void)hipSetDevice(device);
+        (void)hipFree(p);
+        p = nullptr;
+    }
+}
 }  // namespace
 
 Renderer::Renderer(const Scene& scene, std::vector<int> devices)
-    : m_variant(TraceVariantFromEnv()),
+    : m_interleaved(InterleavedFromEnv()),
+      m_variant(TraceVariantFromEnv()),
       m_in_half((scene.flags & kFlagInputFloat16) != 0u),
       m_out_half((scene.flags & kFlagOutputFloat16) != 0u) {
-    for (int d : devices) {
+    for (std::size_t i = 0; i < devices.size(); ++i) {
         auto slot = std::make_unique<Slot>();
-        slot->device = d;
-        DeviceGuard guard(d);
+        slot->device = devices[i];
+        slot->band = i;
+        DeviceGuard guard(devices[i]);
         HipCheck(hipStreamCreateWithFlags(&slot->stream, hipStreamNonBlocking), "hipStreamCreate");
         m_slots.push_back(std::move(slot));
-        m_slots.back()->scene = std::make_unique<DeviceScene>(scene, d);
+        m_slots.back()->scene = std::make_unique<DeviceScene>(scene, devices[i]);
     }
     m_gather_mode = m_slots.size() > 1 ? GatherModeFor(devices) : GatherMode::kDirect;
     if (m_gather_mode == GatherMode::kRccl) {
@@ -531,7 +528,10 @@ Renderer::Renderer(const Scene& scene, std::vector<int> devices)
 }
 
 Renderer::~Renderer() {
-    ReleaseBuffers();
+    SyncAll();
+    if (m_buf) {
+        ReleaseBuffers(*m_buf);
+    }
     for (void* c : m_comms) {
         (void)ncclCommDestroy(static_cast<ncclComm_t>(c));
     }
@@ -554,74 +554,87 @@ Renderer::~Renderer() {
     }
 }
 
-void Renderer::ReleaseBuffers() {
-    for (auto& slot : m_slots) {
-        (void)hipSetDevice(slot->device);
-        (void)hipFree(slot->offsets);
-        (void)hipFree(slot->rgba);
-        (void)hipFree(slot->offsets16);
-        (void)hipFree(slot->rgba16);
-        slot->offsets = nullptr;
-        slot->rgba = nullptr;
-        slot->offsets16 = nullptr;
-        slot->rgba16 = nullptr;
+void Renderer::ReleaseBuffers(Buffers& b) noexcept {
+    for (std::size_t i = 0; i < b.devices.size(); ++i) {
+        FreeOn(b.devices[i], b.offsets[i]);
+        FreeOn(b.devices[i], b.offsets16[i]);
+        FreeOn(b.devices[i], b.rgba[i]);
+        FreeOn(b.devices[i], b.rgba16[i]);
+        FreeOn(b.devices[i], b.ids[i]);
     }
-    if (m_gather != nullptr) {
-        (void)hipSetDevice(m_slots.front()->device);
-        (void)hipFree(m_gather);
-        m_gather = nullptr;
-    }
+    FreeOn(b.root, b.full);
+    FreeOn(b.root, b.full16);
+    FreeOn(b.root, b.gather);
+    FreeOn(b.root, b.frame);
+    FreeOn(b.root, b.frame16);
 }
 
 void Renderer::Configure(std::size_t width, std::size_t height) {
     const std::size_t bands = m_slots.size();
-    const GatherPlan plan = GatherPlan::Make(width, height, bands, m_out_half ? 2 : 4);
-    const std::size_t band_rows = plan.band_rows;
+    const bool multi = bands > 1;
+    const bool gather = multi && m_gather_mode != GatherMode::kDirect;
+    const BandSplit split = BandSplit::Make(height, bands, m_interleaved);
+    const std::size_t band_rows = split.BufferRows();
     // Allocate everything new before releasing the old buffers (strong guarantee).
-    std::vector<float*> offs(bands, nullptr), outs(bands, nullptr);
-    std::vector<std::uint16_t*> offs16(bands, nullptr), outs16(bands, nullptr);
-    void* gather = nullptr;
+    auto nb = std::make_unique<Buffers>();
+    nb->offsets.assign(bands, nullptr);
+    nb->offsets16.assign(bands, nullptr);
+    nb->rgba.assign(bands, nullptr);
+    nb->rgba16.assign(bands, nullptr);
+    nb->ids.assign(bands, nullptr);
+    nb->root = m_slots.front()->device;
+    for (auto& sp : m_slots) {
+        nb->devices.push_back(sp->device);
+    }
+    auto alloc = [](auto*& p, std::size_t count, const char* what) {
+        void* q = nullptr;
+        HipCheck(hipMalloc(&q, (count == 0 ? 1 : count) * sizeof(*p)), what);
+        p = static_cast<std::remove_reference_t<decltype(p)>>(q);
+    };
     try {
         for (std::size_t i = 0; i < bands; ++i) {
             DeviceGuard guard(m_slots[i]->device);
-            offs[i] = DeviceAlloc<float>(band_rows * width * 2, "hipMalloc(band offsets)");
-            outs[i] = DeviceAlloc<float>(band_rows * width * 4, "hipMalloc(band framebuffer)");
+            alloc(nb->offsets[i], band_rows * width * 2, "hipMalloc(band offsets)");
             if (m_in_half) {
-                offs16[i] = DeviceAlloc<std::uint16_t>(band_rows * width * 2, "hipMalloc(band offsets f16)");
+                alloc(nb->offsets16[i], band_rows * width * 2, "hipMalloc(band offsets f16)");
             }
-            if (m_out_half) {
-                outs16[i] = DeviceAlloc<std::uint16_t>(band_rows * width * 4, "hipMalloc(band framebuffer f16)");
+            if (gather) {
+                alloc(nb->ids[i], band_rows * width, "hipMalloc(band ids)");
+            } else {
+                alloc(nb->rgba[i], band_rows * width * 4, "hipMalloc(band framebuffer)");
+                if (m_out_half) {
+                    alloc(nb->rgba16[i], band_rows * width * 4, "hipMalloc(band framebuffer f16)");
+                }
             }
         }
-        if (m_gather_mode != GatherMode::kDirect) {
-            DeviceGuard guard(m_slots.front()->device);
-            gather = DeviceAlloc<unsigned char>(bands * plan.BandBytes(), "hipMalloc(gather framebuffer)");
+        if (gather) {
+            DeviceGuard guard(nb->root);
+            alloc(nb->full, height * width * 2, "hipMalloc(frame offsets)");
+            if (m_in_half) {
+                alloc(nb->full16, height * width * 2, "hipMalloc(frame offsets f16)");
+            }
+            alloc(nb->gather, bands * band_rows * width, "hipMalloc(gathered ids)");
+            alloc(nb->frame, height * width * 4, "hipMalloc(frame)");
+            if (m_out_half) {
+                alloc(nb->frame16, height * width * 4, "hipMalloc(frame f16)");
+            }
         }
     } catch (...) {
-        for (std::size_t i = 0; i < bands; ++i) {
-            (void)hipSetDevice(m_slots[i]->device);
-            (void)hipFree(offs[i]);
-            (void)hipFree(outs[i]);
-            (void)hipFree(offs16[i]);
-            (void)hipFree(outs16[i]);
-        }
-        (void)hipFree(gather);
+        ReleaseBuffers(*nb);
         throw;
     }
-    ReleaseBuffers();
-    for (std::size_t i = 0; i < bands; ++i) {
-        Slot& s = *m_slots[i];
-        s.offsets = offs[i];
-        s.rgba = outs[i];
-        s.offsets16 = offs16[i];
-        s.rgba16 = outs16[i];
-        s.row_begin = plan.RowBegin(i);
-        s.row_count = plan.RowCount(i);
+    if (m_buf) {
+        SyncAll();
+        ReleaseBuffers(*m_buf);
     }
-    m_gather = gather;
+    m_buf = std::move(nb);
+    for (std::size_t i = 0; i < bands; ++i) {
+        m_slots[i]->row_begin = split.RowBegin(i);
+        m_slots[i]->row_count = split.RowCount(i);
+    }
+    m_band_rows = band_rows;
     m_width = width;
     m_height = height;
-    m_plan = plan;
 }
 
 // On an exception mid-frame, copies already queued may still target the caller's host
@@ -658,86 +671,121 @@ void Renderer::Render(const void* host_offsets, void* host_rgba) {
         }
         throw;
     }
+    if (prev >= 0) {
+        (void)hipSetDevice(prev);
+    }
 }
 
-// One band per device: H2D of the band's offsets, prepare + trace, then the frame assembled on
-// the host image by the gather mode (GatherPlan: the same offsets for RCCL and device copies).
+// Copies band i's rows between a host frame (row_bytes per frame row) and a band-local device
+// buffer: interleaved bands move one 16-row tile row per copy, contiguous bands one copy.
+void Renderer::CopyBandRows(std::size_t i, const unsigned char* host, std::size_t row_bytes, unsigned char* dev,
+                            hipMemcpyKind kind, bool to_host, hipStream_t stream) const {
+    const Slot& s = *m_slots[i];
+    const std::size_t interleave = m_interleaved && m_slots.size() > 1 ? m_slots.size() : 1;
+    const std::size_t step = interleave > 1 ? static_cast<std::size_t>(kCullTileRows) : s.row_count;
+    for (std::size_t l = 0; l < s.row_count; l += step) {
+        const std::size_t n = std::min(step, s.row_count - l);
+        const std::size_t fr = BandFrameRow(s.row_begin, interleave, l);
+        unsigned char* h = const_cast<unsigned char*>(host) + fr * row_bytes;
+        if (to_host) {
+            HipCheck(hipMemcpyAsync(h, dev + l * row_bytes, n * row_bytes, kind, stream), "hipMemcpyAsync(band rows D2H)");
+        } else {
+            HipCheck(hipMemcpyAsync(dev + l * row_bytes, h, n * row_bytes, kind, stream), "hipMemcpyAsync(band rows H2D)");
+        }
+    }
+}
+
+// One band per device (module doc): band offsets in, hit ids traced, gathered to the first device,
+// shaded there and copied out; "direct": every device shades its own rows and copies them out.
 void Renderer::RenderBands(const void* host_offsets, void* host_rgba) {
-    const std::size_t w = m_width;
-    const std::size_t in_elem = m_in_half ? 2 : 4, out_elem = m_plan.elem;
+    Buffers& b = *m_buf;
+    const std::size_t w = m_width, h = m_height, P = m_slots.size();
+    const std::size_t in_elem = m_in_half ? 2 : 4, out_elem = m_out_half ? 2 : 4;
     const auto* in_bytes = static_cast<const unsigned char*>(host_offsets);
     auto* out_bytes = static_cast<unsigned char*>(host_rgba);
-    auto band_out = [this](const Slot& s) {
-        return m_out_half ? static_cast<void*>(s.rgba16) : static_cast<void*>(s.rgba);
-    };
-    for (auto& sp : m_slots) {
-        Slot& s = *sp;
+    const std::size_t interleave = m_interleaved && P > 1 ? P : 1;
+    const bool direct = P == 1 || m_gather_mode == GatherMode::kDirect;
+    for (std::size_t i = 0; i < P; ++i) {
+        Slot& s = *m_slots[i];
         DeviceGuard guard(s.device);
         if (s.row_count != 0) {
-            const std::size_t count = s.row_count * w * 2;
-            void* dst = m_in_half ? static_cast<void*>(s.offsets16) : static_cast<void*>(s.offsets);
-            HipCheck(hipMemcpyAsync(dst, in_bytes + s.row_begin * w * 2 * in_elem, count * in_elem,
-                                    hipMemcpyHostToDevice, s.stream),
-                     "hipMemcpyAsync(offsets H2D)");
+            auto* dst = m_in_half ? reinterpret_cast<unsigned char*>(b.offsets16[i])
+                                  : reinterpret_cast<unsigned char*>(b.offsets[i]);
+            CopyBandRows(i, in_bytes, w * 2 * in_elem, dst, hipMemcpyHostToDevice, false, s.stream);
             if (m_in_half) {
-                HipCheck(LaunchHalfToFloat(s.offsets16, s.offsets, count, s.stream), "offsets f16 -> f32");
+                HipCheck(LaunchHalfToFloat(b.offsets16[i], b.offsets[i], s.row_count * w * 2, s.stream),
+                         "offsets f16 -> f32");
             }
         }
-        s.scene->Prepare(w, m_height, s.stream);
-        s.scene->Trace(s.offsets, s.rgba, s.row_begin, s.row_count, m_variant, s.stream);
-        if (m_out_half) {
-            // Whole padded band (rows past row_count are gathered but never copied out).
-            HipCheck(LaunchFloatToHalf(s.rgba, s.rgba16, m_plan.BandElems(), s.stream), "framebuffer f32 -> f16");
+        s.scene->Prepare(w, h, s.stream);
+        if (direct) {
+            s.scene->Trace(b.offsets[i], b.rgba[i], s.row_begin, s.row_count, m_variant, s.stream, nullptr, interleave);
+            auto* src = reinterpret_cast<unsigned char*>(b.rgba[i]);
+            if (m_out_half) {
+                HipCheck(LaunchFloatToHalf(b.rgba[i], b.rgba16[i], s.row_count * w * 4, s.stream),
+                         "framebuffer f32 -> f16");
+                src = reinterpret_cast<unsigned char*>(b.rgba16[i]);
+            }
+            CopyBandRows(i, out_bytes, w * 4 * out_elem, src, hipMemcpyDeviceToHost, true, s.stream);
+        } else {
+            s.scene->Trace(b.offsets[i], nullptr, s.row_begin, s.row_count, m_variant, s.stream, b.ids[i], interleave);
         }
     }
-    Slot& root = *m_slots.front();
-    if (m_gather_mode == GatherMode::kRccl) {
-        // Equal-size bands (the last one padded) gathered to the first device over xGMI.
-        NcclCheck(ncclGroupStart(), "ncclGroupStart");
-        for (std::size_t i = 0; i < m_slots.size(); ++i) {
-            Slot& s = *m_slots[i];
-            NcclCheck(ncclGather(band_out(s), i == 0 ? m_gather : nullptr, m_plan.BandElems(),
-                                 m_out_half ? ncclFloat16 : ncclFloat32, 0, static_cast<ncclComm_t>(m_comms[i]),
-                                 s.stream),
-                      "ncclGather");
+    if (!direct) {
+        Slot& root = *m_slots.front();
+        const std::size_t band_pixels = m_band_rows * w;
+        {
+            DeviceGuard guard(root.device);  // the frame's offsets for shading
+            void* dst = m_in_half ? static_cast<void*>(b.full16) : static_cast<void*>(b.full);
+            HipCheck(hipMemcpyAsync(dst, in_bytes, h * w * 2 * in_elem, hipMemcpyHostToDevice, root.stream),
+                     "hipMemcpyAsync(frame offsets H2D)");
+            if (m_in_half) {
+                HipCheck(LaunchHalfToFloat(b.full16, b.full, h * w * 2, root.stream), "offsets f16 -> f32");
+            }
         }
-        NcclCheck(ncclGroupEnd(), "ncclGroupEnd");
-    } else if (m_gather_mode == GatherMode::kCopy) {
-        // The same gather as device copies into the root's buffer at ncclGather's offsets; the
-        // root's stream then waits for every band's copy (an event per band).
-        for (std::size_t i = 0; i < m_slots.size(); ++i) {
-            Slot& s = *m_slots[i];
-            DeviceGuard guard(s.device);
-            HipCheck(hipMemcpyPeerAsync(static_cast<unsigned char*>(m_gather) + m_plan.RecvOffset(i), root.device,
-                                        band_out(s), s.device, m_plan.BandBytes(), s.stream),
-                     "hipMemcpyPeerAsync(band gather)");
-            if (i != 0) {
-                if (s.traced.empty()) {
-                    hipEvent_t e = nullptr;
-                    HipCheck(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate(band gather)");
-                    s.traced.push_back(e);
+        if (m_gather_mode == GatherMode::kRccl) {
+            // Equal-size id bands (buffer rows each) gathered to the first device over xGMI.
+            NcclCheck(ncclGroupStart(), "ncclGroupStart");
+            for (std::size_t i = 0; i < P; ++i) {
+                Slot& s = *m_slots[i];
+                const ncclResult_t r = ncclGather(b.ids[i], i == 0 ? b.gather : nullptr, band_pixels, ncclInt32, 0,
+                                                  static_cast<ncclComm_t>(m_comms[i]), s.stream);
+                if (r != ncclSuccess) {
+                    (void)ncclGroupEnd();
+                    NcclCheck(r, "ncclGather");
                 }
-                HipCheck(hipEventRecord(s.traced[0], s.stream), "hipEventRecord(band gather)");
-                DeviceGuard root_guard(root.device);
-                HipCheck(hipStreamWaitEvent(root.stream, s.traced[0], 0), "hipStreamWaitEvent(band gather)");
+            }
+            NcclCheck(ncclGroupEnd(), "ncclGroupEnd");
+        } else {
+            // The same gather as device copies into the root's buffer (band i at i x buffer rows);
+            // the root's stream then waits for every band's copy (an event per band).
+            for (std::size_t i = 0; i < P; ++i) {
+                Slot& s = *m_slots[i];
+                DeviceGuard guard(s.device);
+                HipCheck(hipMemcpyPeerAsync(b.gather + i * band_pixels, root.device, b.ids[i], s.device,
+                                            band_pixels * sizeof(int), s.stream),
+                         "hipMemcpyPeerAsync(band gather)");
+                if (i != 0) {
+                    if (s.traced.empty()) {
+                        hipEvent_t e = nullptr;
+                        HipCheck(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate(band gather)");
+                        s.traced.push_back(e);
+                    }
+                    HipCheck(hipEventRecord(s.traced[0], s.stream), "hipEventRecord(band gather)");
+                    DeviceGuard root_guard(root.device);
+                    HipCheck(hipStreamWaitEvent(root.stream, s.traced[0], 0), "hipStreamWaitEvent(band gather)");
+                }
             }
         }
-    }
-    if (m_gather_mode != GatherMode::kDirect) {
         DeviceGuard guard(root.device);
-        HipCheck(hipMemcpyAsync(out_bytes, m_gather, m_plan.FrameBytes(), hipMemcpyDeviceToHost, root.stream),
-                 "hipMemcpyAsync(frame D2H)");
-    } else {
-        for (auto& sp : m_slots) {
-            Slot& s = *sp;
-            if (s.row_count == 0) {
-                continue;
-            }
-            DeviceGuard guard(s.device);
-            HipCheck(hipMemcpyAsync(out_bytes + s.row_begin * w * 4 * out_elem, band_out(s),
-                                    s.row_count * w * 4 * out_elem, hipMemcpyDeviceToHost, s.stream),
-                     "hipMemcpyAsync(band D2H)");
+        root.scene->Shade(b.full, b.gather, b.frame, 0, h, root.stream, 1, m_band_rows, interleave > 1 ? P : 0);
+        const void* src = b.frame;
+        if (m_out_half) {
+            HipCheck(LaunchFloatToHalf(b.frame, b.frame16, h * w * 4, root.stream), "framebuffer f32 -> f16");
+            src = b.frame16;
         }
+        HipCheck(hipMemcpyAsync(out_bytes, src, h * w * 4 * out_elem, hipMemcpyDeviceToHost, root.stream),
+                 "hipMemcpyAsync(frame D2H)");
     }
     for (auto& sp : m_slots) {
         DeviceGuard guard(sp->device);
@@ -750,6 +798,7 @@ void Renderer::RenderBands(const void* host_offsets, void* host_rgba) {
 // the same prepared frame, so the image is bit-identical to the unchunked render.
 void Renderer::RenderPipelined(const void* host_offsets, void* host_rgba, std::size_t chunks) {
     Slot& s = *m_slots.front();
+    Buffers& b = *m_buf;
     DeviceGuard guard(s.device);
     const std::size_t w = m_width, h = m_height;
     const std::size_t in_elem = m_in_half ? 2 : 4, out_elem = m_out_half ? 2 : 4;
@@ -760,12 +809,14 @@ void Renderer::RenderPipelined(const void* host_offsets, void* host_rgba, std::s
         HipCheck(hipStreamCreateWithFlags(&s.copy_out, hipStreamNonBlocking), "hipStreamCreate(copy out)");
     }
     while (s.in_done.size() < chunks) {
-        hipEvent_t a = nullptr, b = nullptr;
-        HipCheck(hipEventCreateWithFlags(&a, hipEventDisableTiming), "hipEventCreate(chunk)");
-        HipCheck(hipEventCreateWithFlags(&b, hipEventDisableTiming), "hipEventCreate(chunk)");
-        s.in_done.push_back(a);
-        s.traced.push_back(b);
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        HipCheck(hipEventCreateWithFlags(&e0, hipEventDisableTiming), "hipEventCreate(chunk)");
+        HipCheck(hipEventCreateWithFlags(&e1, hipEventDisableTiming), "hipEventCreate(chunk)");
+        s.in_done.push_back(e0);
+        s.traced.push_back(e1);
     }
+    float* offsets = b.offsets[0];
+    float* rgba = b.rgba[0];
     const std::size_t rows = (h + chunks - 1) / chunks;
     s.scene->Prepare(w, h, s.stream);
     for (std::size_t c = 0; c < chunks; ++c) {
@@ -775,24 +826,24 @@ void Renderer::RenderPipelined(const void* host_offsets, void* host_rgba, std::s
         }
         const std::size_t n = std::min(rows, h - r0);
         const std::size_t count = n * w * 2;
-        void* dst = m_in_half ? static_cast<void*>(s.offsets16 + r0 * w * 2) : static_cast<void*>(s.offsets + r0 * w * 2);
+        void* dst = m_in_half ? static_cast<void*>(b.offsets16[0] + r0 * w * 2) : static_cast<void*>(offsets + r0 * w * 2);
         HipCheck(hipMemcpyAsync(dst, in_bytes + r0 * w * 2 * in_elem, count * in_elem, hipMemcpyHostToDevice, s.copy_in),
                  "hipMemcpyAsync(offsets chunk H2D)");
         HipCheck(hipEventRecord(s.in_done[c], s.copy_in), "hipEventRecord(chunk in)");
         HipCheck(hipStreamWaitEvent(s.stream, s.in_done[c], 0), "hipStreamWaitEvent(chunk in)");
         if (m_in_half) {
-            HipCheck(LaunchHalfToFloat(s.offsets16 + r0 * w * 2, s.offsets + r0 * w * 2, count, s.stream),
+            HipCheck(LaunchHalfToFloat(b.offsets16[0] + r0 * w * 2, offsets + r0 * w * 2, count, s.stream),
                      "offsets f16 -> f32");
         }
-        s.scene->Trace(s.offsets + r0 * w * 2, s.rgba + r0 * w * 4, r0, n, m_variant, s.stream);
+        s.scene->Trace(offsets + r0 * w * 2, rgba + r0 * w * 4, r0, n, m_variant, s.stream);
         if (m_out_half) {
-            HipCheck(LaunchFloatToHalf(s.rgba + r0 * w * 4, s.rgba16 + r0 * w * 4, n * w * 4, s.stream),
+            HipCheck(LaunchFloatToHalf(rgba + r0 * w * 4, b.rgba16[0] + r0 * w * 4, n * w * 4, s.stream),
                      "framebuffer f32 -> f16");
         }
         HipCheck(hipEventRecord(s.traced[c], s.stream), "hipEventRecord(chunk traced)");
         HipCheck(hipStreamWaitEvent(s.copy_out, s.traced[c], 0), "hipStreamWaitEvent(chunk traced)");
-        const void* src = m_out_half ? static_cast<const void*>(s.rgba16 + r0 * w * 4)
-                                     : static_cast<const void*>(s.rgba + r0 * w * 4);
+        const void* src = m_out_half ? static_cast<const void*>(b.rgba16[0] + r0 * w * 4)
+                                     : static_cast<const void*>(rgba + r0 * w * 4);
         HipCheck(hipMemcpyAsync(out_bytes + r0 * w * 4 * out_elem, src, n * w * 4 * out_elem, hipMemcpyDeviceToHost,
                                 s.copy_out),
                  "hipMemcpyAsync(frame chunk D2H)");

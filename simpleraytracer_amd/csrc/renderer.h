@@ -23,6 +23,28 @@ struct StageEvents;  // render.h
 // Throws std::runtime_error("HIP error: <what>: <reason>") on failure.
 void HipCheck(hipError_t err, const char* what);
 
+// Restores the caller's current HIP device on scope exit (the C ABI must not leak a
+// hipSetDevice into the host application).
+class DeviceGuard {
+public:
+    explicit DeviceGuard(int device) {
+        if (hipGetDevice(&m_prev) != hipSuccess) {
+            m_prev = -1;
+        }
+        HipCheck(hipSetDevice(device), "hipSetDevice");
+    }
+    ~DeviceGuard() {
+        if (m_prev >= 0) {
+            (void)hipSetDevice(m_prev);
+        }
+    }
+    DeviceGuard(const DeviceGuard&) = delete;
+    DeviceGuard& operator=(const DeviceGuard&) = delete;
+
+private:
+    int m_prev = -1;
+};
+
 // GPU list from env ML_VISIBLE_DEVICES ("0,1,2"; unset or empty = device 0). Validated
 // against hipGetDeviceCount; throws when no HIP device is present.
 std::vector<int> VisibleDevices();
@@ -52,10 +74,11 @@ public:
     // ids (as Trace writes them) and sample offsets: the RGBA the fused trace would store.
     // frames > 1: a batch of that many frames of this camera, ids band-major as a gather of
     // band_rows-row bands leaves them (render.h LaunchShade), rgba [frames][row_count][width].
-    // interleaved > 0: the gathered bands are that many interleaved bands.
+    // interleaved > 0: the gathered bands are that many interleaved bands. offsets_stride: floats
+    // between consecutive frames' offsets (0: the batch shares d_offsets).
     void Shade(const float* d_offsets, const int* d_ids, float* d_rgba, std::size_t row_begin, std::size_t row_count,
                hipStream_t stream, std::size_t frames = 1, std::size_t band_rows = 0,
-               std::size_t interleaved = 0) const;
+               std::size_t interleaved = 0, std::size_t offsets_stride = 0) const;
     // `frames` (<= kMaxBatch) frames of the prepared camera, rows [row_begin, row_begin +
     // row_count) each: frame f's offsets d_offsets[f], its RGBA d_rgba[f] or (d_ids non-null) its
     // hit ids d_ids[f]. Each frame gets the whole per-frame pipeline (record setup, bins, work
@@ -122,6 +145,7 @@ private:
     // Calls on one scene are stream-ordered: the per-frame edge records and the cull work buffer
     // are shared state, so a call on another stream than the previous one first waits for it.
     void OrderAfterPrevious(hipStream_t stream) const;
+    void RecordOrder(hipStream_t stream) const;
     void NormalsIfStale(hipStream_t stream) const;
     mutable hipStream_t m_last_stream = nullptr;
     mutable bool m_used = false;
@@ -138,35 +162,19 @@ private:
 // Trace kernel variant from env SRT_TRACE_VARIANT ("lds" | "scalar" | "cull", default cull).
 int TraceVariantFromEnv();
 
-// Row bands of a frame over `bands` devices and the layout of their gather:
-// equal bands of band_rows = ceil(H / bands) rows (the last padded), band i = frame rows
-// [RowBegin(i), RowBegin(i) + RowCount(i)); band i's padded buffer (BandBytes) lands at
-// RecvOffset(i) of the root's gather buffer, exactly where ncclGather puts it, so the frame is
-// the buffer's first FrameBytes. Every gather path (RCCL, device copies, the host self-test)
-// moves bytes with these numbers.
-struct GatherPlan {
-    std::size_t width = 0, height = 0, bands = 1, band_rows = 0;
-    std::size_t elem = 4;  // bytes per channel of the output image (4: float, 2: half)
-    static GatherPlan Make(std::size_t width, std::size_t height, std::size_t bands, std::size_t elem);
-    std::size_t RowBegin(std::size_t i) const { return i * band_rows < height ? i * band_rows : height; }
-    std::size_t RowCount(std::size_t i) const;
-    std::size_t BandElems() const { return band_rows * width * 4; }  // RGBA channels of one padded band
-    std::size_t BandBytes() const { return BandElems() * elem; }
-    std::size_t RecvOffset(std::size_t i) const { return i * BandBytes(); }
-    std::size_t FrameBytes() const { return height * width * 4 * elem; }
-};
-
-// The gather on host memory (self-test of the plan, no device): bands[i] = band i's padded
-// buffer, gathered into `gather_buf` (bands x BandBytes) as ncclGather would, then the frame
-// copied out to `frame`.
-void GatherOnHost(const GatherPlan& plan, const void* const* bands, void* gather_buf, void* frame);
-
-// How Renderer assembles a multi-device frame (env SRT_GATHER): "rccl" = ncclGather of the
-// bands to the first device, then one D2H (default for distinct devices); "copy" = the same
-// gather by device-to-device copies (default when a device repeats: RCCL needs distinct
-// devices); "direct" = per-device D2H into disjoint rows of the host image.
+// How Renderer assembles a multi-device frame (env SRT_GATHER): "rccl" = the devices' hit-id bands
+// gathered to the first device with ncclGather, which shades the frame and copies it out
+// (default for distinct devices); "copy" = the same gather by device-to-device copies (default
+// when a device repeats: RCCL needs distinct devices); "direct" = every device traces and shades
+// its own band and copies its rows straight into the host image (no gather).
 enum class GatherMode { kRccl, kCopy, kDirect };
 
+// The device side of an ml_model (mlInfer). One device: the frame in row chunks, copies in and out
+// overlapping the traces. Several (ML_VISIBLE_DEVICES): the frame's 16-row tile rows dealt
+// round-robin to the devices (env SRT_BAND_ROWS=contiguous: one block each), every device traces
+// its band into hit ids (4 B per pixel), the bands are gathered to the first device, which shades
+// the whole frame from them (bit-identical to the fused trace) and copies it out. All launches
+// from the calling thread; the RCCL gathers of all devices in one group.
 class Renderer {
 public:
     Renderer(const Scene& scene, std::vector<int> devices);
@@ -181,8 +189,7 @@ public:
 
     // Render one frame: host offsets (H x W x 2) -> host RGBA (H x W x 4). Synchronous.
     // Element types from the scene's flags (kFlagInputFloat16 / kFlagOutputFloat16): float,
-    // or IEEE binary16 bit patterns, converted on the device (the gather and the D2H then
-    // move half the bytes).
+    // or IEEE binary16 bit patterns, converted on the device (the copies then move half the bytes).
     void Render(const void* host_offsets, void* host_rgba);
     bool input_half() const { return m_in_half; }
     bool output_half() const { return m_out_half; }
@@ -192,20 +199,24 @@ public:
 
 private:
     struct Slot;
-    void ReleaseBuffers();
+    struct Buffers;
+    void ReleaseBuffers(Buffers& b) noexcept;
     void RenderPipelined(const void* host_offsets, void* host_rgba, std::size_t chunks);
-
     void RenderBands(const void* host_offsets, void* host_rgba);
     void SyncAll() noexcept;
+    // Host-to-device copy of rows [0, rows) of band `i` (band-local order) from a host frame.
+    void CopyBandRows(std::size_t i, const unsigned char* host, std::size_t row_bytes, unsigned char* dst,
+                      hipMemcpyKind kind, bool to_host, hipStream_t stream) const;
 
     std::vector<std::unique_ptr<Slot>> m_slots;
     std::vector<void*> m_comms;  // ncclComm_t per slot when gathering with RCCL
     GatherMode m_gather_mode = GatherMode::kDirect;
-    GatherPlan m_plan;
+    bool m_interleaved = true;
+    std::size_t m_band_rows = 0;  // rows of every band buffer
     int m_variant = 0;
     std::size_t m_width = 0;
     std::size_t m_height = 0;
-    void* m_gather = nullptr;  // root device: bands x band_rows x W x 4 (float, or half)
+    std::unique_ptr<Buffers> m_buf;
     bool m_in_half = false;
     bool m_out_half = false;
 };

@@ -6,6 +6,7 @@
 #include <string>
 #include <vector>
 
+#include "engine.h"
 #include "render.h"
 #include "renderer.h"
 #include "scene.h"
@@ -310,18 +311,6 @@ ML_API_ENTRY int srtShadeBandsAsync(srt_device_scene scene, const float* d_offse
     });
 }
 
-ML_API_ENTRY int srtGatherBandsHost(const void* const* bands, size_t band_count, size_t width, size_t height,
-                                    int element_bytes, void* frame) {
-    return Guarded([&] {
-        if (bands == nullptr || frame == nullptr || band_count == 0 || (element_bytes != 2 && element_bytes != 4)) {
-            throw std::runtime_error("Bad argument");
-        }
-        const srt::GatherPlan plan = srt::GatherPlan::Make(width, height, band_count, element_bytes);
-        std::vector<unsigned char> gather(plan.bands * plan.BandBytes());
-        srt::GatherOnHost(plan, bands, gather.data(), frame);
-    });
-}
-
 ML_API_ENTRY int srtSetStageTiming(srt_device_scene scene, int enable) {
     return Guarded([&] {
         if (scene == nullptr) {
@@ -351,6 +340,224 @@ ML_API_ENTRY int srtTakeStageTimes(srt_device_scene scene, unsigned* launches, d
         }
         if (trace_ms != nullptr) {
             *trace_ms = t.kernel_ms;
+        }
+    });
+}
+
+static_assert(SRT_SPLIT_BANDS == srt::EngineOptions::kBands && SRT_SPLIT_FRAMES == srt::EngineOptions::kFrames,
+              "include/srt_render.h SRT_SPLIT_*");
+static_assert(SRT_EXCHANGE_ALLTOALL == srt::EngineOptions::kAllToAll &&
+                  SRT_EXCHANGE_ROTATING == srt::EngineOptions::kRotatingGather &&
+                  SRT_EXCHANGE_ROOT == srt::EngineOptions::kRootGather,
+              "include/srt_render.h SRT_EXCHANGE_*");
+
+}  // extern "C"
+
+namespace {
+srt::FrameEngine* FromHandle(srt_engine e) { return reinterpret_cast<srt::FrameEngine*>(e); }
+
+srt::EngineOptions EngineOptionsFrom(const srt_engine_options* o) {
+    srt::EngineOptions opt;
+    if (o != nullptr) {
+        opt.variant = o->variant;
+        opt.queues = o->queues == 0 ? opt.queues : o->queues;
+        opt.batch = o->batch == 0 ? opt.batch : o->batch;
+        if (o->rows != SRT_ROWS_INTERLEAVED && o->rows != SRT_ROWS_CONTIGUOUS) {
+            throw std::runtime_error("Unknown rows mode " + std::to_string(o->rows));
+        }
+        opt.interleaved = o->rows == SRT_ROWS_INTERLEAVED;
+        opt.exchange = o->exchange;
+        opt.split = o->split;
+    }
+    return opt;
+}
+
+void CheckDevices(const int* devices, std::size_t count) {
+    int present = 0;
+    if (hipGetDeviceCount(&present) != hipSuccess || present <= 0) {
+        throw std::runtime_error("HIP error: no HIP device available; the frame engine has no CPU path");
+    }
+    for (std::size_t i = 0; i < count; ++i) {
+        if (devices[i] < 0 || devices[i] >= present) {
+            throw std::runtime_error("HIP error: device " + std::to_string(devices[i]) + " not available (" +
+                                     std::to_string(present) + " present)");
+        }
+    }
+}
+}  // namespace
+
+extern "C" {
+
+ML_API_ENTRY int srtEngineUniqueId(void* id128) {
+    return Guarded([&] {
+        if (id128 == nullptr) {
+            throw std::runtime_error("Bad argument");
+        }
+        srt::FrameEngine::UniqueId(id128);
+    });
+}
+
+ML_API_ENTRY srt_engine srtEngineCreate(const char* scene_path, const int* devices, size_t device_count, size_t width,
+                                        size_t height, const srt_engine_options* options) {
+    srt::FrameEngine* out = nullptr;
+    Guarded([&] {
+        if (scene_path == nullptr || devices == nullptr || device_count == 0) {
+            throw std::runtime_error("Bad argument");
+        }
+        CheckDevices(devices, device_count);
+        const srt::Scene scene = srt::LoadScene(scene_path);
+        out = new srt::FrameEngine(scene, std::vector<int>(devices, devices + device_count), width, height,
+                                   EngineOptionsFrom(options));
+    });
+    return reinterpret_cast<srt_engine>(out);
+}
+
+ML_API_ENTRY srt_engine srtEngineCreateRank(const char* scene_path, int device, int rank, int world,
+                                            const void* unique_id128, size_t width, size_t height,
+                                            const srt_engine_options* options) {
+    srt::FrameEngine* out = nullptr;
+    Guarded([&] {
+        if (scene_path == nullptr) {
+            throw std::runtime_error("Bad argument");
+        }
+        CheckDevices(&device, 1);
+        const srt::Scene scene = srt::LoadScene(scene_path);
+        out = new srt::FrameEngine(scene, device, rank, world, unique_id128, width, height, EngineOptionsFrom(options));
+    });
+    return reinterpret_cast<srt_engine>(out);
+}
+
+ML_API_ENTRY void srtEngineRelease(srt_engine engine) { delete FromHandle(engine); }
+
+ML_API_ENTRY int srtEngineSetInputs(srt_engine engine, const float* host_offsets, size_t count) {
+    return Guarded([&] {
+        if (engine == nullptr) {
+            throw std::runtime_error("Bad engine handle");
+        }
+        FromHandle(engine)->SetInputs(host_offsets, count);
+    });
+}
+
+ML_API_ENTRY int srtEngineRun(srt_engine engine, size_t batches) {
+    return Guarded([&] {
+        if (engine == nullptr) {
+            throw std::runtime_error("Bad engine handle");
+        }
+        FromHandle(engine)->Run(batches);
+    });
+}
+
+ML_API_ENTRY int srtEngineVerify(srt_engine engine, size_t* mismatches, size_t* checked) {
+    return Guarded([&] {
+        if (engine == nullptr) {
+            throw std::runtime_error("Bad engine handle");
+        }
+        const std::size_t bad = FromHandle(engine)->Verify(checked);
+        if (mismatches != nullptr) {
+            *mismatches = bad;
+        }
+    });
+}
+
+ML_API_ENTRY int srtEngineReadFrame(srt_engine engine, size_t frame, float* host_rgba) {
+    return Guarded([&] {
+        if (engine == nullptr || host_rgba == nullptr) {
+            throw std::runtime_error("Bad argument");
+        }
+        if (!FromHandle(engine)->ReadFrame(frame, host_rgba)) {
+            throw std::runtime_error("Frame " + std::to_string(frame) + " is not resident on this process's devices");
+        }
+    });
+}
+
+ML_API_ENTRY int srtEngineStageTimes(srt_engine engine, size_t local, size_t launches, unsigned* launched,
+                                     double* prepare_ms, double* bin_ms, double* trace_ms) {
+    return Guarded([&] {
+        if (engine == nullptr) {
+            throw std::runtime_error("Bad engine handle");
+        }
+        const srt::DeviceScene::StageTimes t = FromHandle(engine)->MeasureStages(local, launches);
+        if (launched != nullptr) {
+            *launched = t.launches;
+        }
+        if (prepare_ms != nullptr) {
+            *prepare_ms = t.prepare_ms;
+        }
+        if (bin_ms != nullptr) {
+            *bin_ms = t.bin_ms;
+        }
+        if (trace_ms != nullptr) {
+            *trace_ms = t.kernel_ms;
+        }
+    });
+}
+
+ML_API_ENTRY int srtEngineInfo(srt_engine engine, size_t* devices, size_t* local_devices, size_t* band_rows,
+                               size_t* buffer_rows, int* rccl, double* exchange_bytes_per_frame) {
+    return Guarded([&] {
+        if (engine == nullptr) {
+            throw std::runtime_error("Bad engine handle");
+        }
+        const srt::FrameEngine* e = FromHandle(engine);
+        if (devices != nullptr) {
+            *devices = e->devices();
+        }
+        if (local_devices != nullptr) {
+            *local_devices = e->local_devices();
+        }
+        if (band_rows != nullptr) {
+            *band_rows = e->band_rows(0);
+        }
+        if (buffer_rows != nullptr) {
+            *buffer_rows = e->buffer_rows();
+        }
+        if (rccl != nullptr) {
+            *rccl = e->uses_rccl() ? 1 : 0;
+        }
+        if (exchange_bytes_per_frame != nullptr) {
+            *exchange_bytes_per_frame = e->exchange_bytes_per_frame();
+        }
+    });
+}
+
+ML_API_ENTRY int srtExchangeHost(const int* const* band_ids, size_t bands, size_t width, size_t height, int rows,
+                                 int exchange, size_t batch, size_t batch_index, int* const* recv,
+                                 size_t* recv_frames, size_t* buffer_rows) {
+    return Guarded([&] {
+        if (bands == 0 || width == 0 || height == 0 || batch == 0 ||
+            (rows != SRT_ROWS_INTERLEAVED && rows != SRT_ROWS_CONTIGUOUS) || exchange < SRT_EXCHANGE_ALLTOALL ||
+            exchange > SRT_EXCHANGE_ROOT) {
+            throw std::runtime_error("Bad argument");
+        }
+        const srt::BandSplit split = srt::BandSplit::Make(height, bands, rows == SRT_ROWS_INTERLEAVED);
+        srt::ExchangePlan plan;
+        plan.bands = bands;
+        plan.batch = batch;
+        plan.exchange = exchange;
+        if (buffer_rows != nullptr) {
+            *buffer_rows = split.BufferRows();
+        }
+        if (recv_frames != nullptr) {
+            for (size_t c = 0; c < bands; ++c) {
+                recv_frames[c] = plan.FramesFor(batch_index, c);
+            }
+        }
+        if (recv == nullptr) {
+            return;
+        }
+        if (band_ids == nullptr) {
+            throw std::runtime_error("Bad argument");
+        }
+        const size_t pixels = batch * split.BufferRows() * width;
+        std::vector<std::vector<int>> in(bands);
+        for (size_t d = 0; d < bands; ++d) {
+            in[d].assign(band_ids[d], band_ids[d] + pixels);
+        }
+        const std::vector<std::vector<int>> out = srt::ExchangeOnHost(split, plan, width, batch_index, in);
+        for (size_t c = 0; c < bands; ++c) {
+            if (!out[c].empty()) {
+                std::copy(out[c].begin(), out[c].end(), recv[c]);
+            }
         }
     });
 }

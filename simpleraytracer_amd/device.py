@@ -227,7 +227,10 @@ class DeviceScene:
         bands = interleaved if interleaved else (self.height + band_rows - 1) // band_rows
         frames = ids.shape[1] if hasattr(ids, "shape") and len(ids.shape) == 4 else 0
         self._check_buffer("offsets", offsets, self.height, 2, "f32")
-        if hasattr(ids, "shape") and tuple(ids.shape) != (bands, frames, band_rows, self.width):
+        # contiguous bands: a gather over P ranks may carry more (empty, trailing) bands than the
+        # ceil(H / band_rows) that hold rows; the kernel never reads them
+        if hasattr(ids, "shape") and (len(ids.shape) != 4 or tuple(ids.shape[2:]) != (band_rows, self.width) or
+                                      (ids.shape[0] != bands if interleaved else ids.shape[0] < bands)):
             raise ValueError(f"ids must be {(bands, 'frames', band_rows, self.width)}, got {tuple(ids.shape)}")
         if hasattr(rgba, "shape") and tuple(rgba.shape) != (frames, self.height, self.width, 4):
             raise ValueError(f"rgba must be {(frames, self.height, self.width, 4)}, got {tuple(rgba.shape)}")

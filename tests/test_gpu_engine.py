@@ -1,0 +1,116 @@
+"""GPU: the frame engine (csrc/engine.cpp) -- the native path bench.py times at every N.
+
+Frames rendered by the engine, wherever they were composited, are compared with the oracle
+(tri_id bit-exact, RGB <= 1e-5) and with a single-device render, bit for bit. Multi-device runs use
+"fake devices" (device 0 repeated: the bands are exchanged by device copies, everything else is
+the multi-GPU code path), since this box has one GPU.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from test_gpu_parity import assert_parity, oracle_render, torch_render
+
+pytestmark = pytest.mark.gpu
+
+
+def engine(path, w, h, devices=(0,), **kw):
+    from simpleraytracer_amd.engine import FrameEngine
+
+    return FrameEngine(path, w, h, devices=list(devices), **kw)
+
+
+def random_inputs(n, h, w, seed=77):
+    return np.random.default_rng(seed).random((n, h, w, 2), dtype=np.float32)
+
+
+@pytest.mark.parametrize("variant", ["cull", "lds"])
+def test_engine_one_device_matches_oracle(gpu, scenes, variant):
+    w, h, F = 97, 61, 3
+    inputs = random_inputs(F, h, w)
+    with engine(scenes["soup2k"], w, h, variant=variant, queues=2, batch=F) as e:
+        e.set_inputs(inputs)
+        e.run(3)  # batches 0..2: frames 0..8; queues hold batches 1 and 2
+        for k in range(3, 9):
+            assert_parity(e.read_frame(k), oracle_render(scenes["soup2k"], w, h, inputs[k % F]))
+        bad, checked = e.verify()
+        assert bad == 0 and checked == 2 * F
+        with pytest.raises(Exception):
+            e.read_frame(0)  # no longer resident
+
+
+@pytest.mark.parametrize("p", [2, 3, 8])
+@pytest.mark.parametrize("rows", ["interleaved", "contiguous"])
+@pytest.mark.parametrize("exchange", ["alltoall", "rotating", "root"])
+def test_engine_fake_devices_bitwise(gpu, scenes, p, rows, exchange):
+    """P fake devices: every frame of the last batches equals a one-device render bit for bit."""
+    w, h, F = 130, 100, 4
+    inputs = random_inputs(1, h, w, seed=p)
+    ref = torch_render(scenes["soup2k"], w, h, inputs[0])
+    assert_parity(ref, oracle_render(scenes["soup2k"], w, h, inputs[0]))
+    with engine(scenes["soup2k"], w, h, devices=[0] * p, rows=rows, exchange=exchange, queues=2, batch=F) as e:
+        assert e.info()["devices"] == p and not e.info()["rccl"]
+        e.set_inputs(inputs)
+        e.run(3)
+        for k in range(F, 3 * F):
+            got = e.read_frame(k)
+            assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), k
+        bad, checked = e.verify()
+        assert bad == 0 and checked == 2 * F
+
+
+def test_engine_fake_devices_rotating_inputs(gpu, scenes):
+    """Distinct inputs per frame through the all-to-all exchange (the compositors' strided offsets)."""
+    w, h, p, F = 70, 90, 2, 4
+    inputs = random_inputs(2 * F, h, w, seed=5)
+    with engine(scenes["soup2k"], w, h, devices=[0] * p, queues=2, batch=F) as e:
+        e.set_inputs(inputs)
+        e.run(3)
+        for k in range(F, 3 * F):
+            assert_parity(e.read_frame(k), oracle_render(scenes["soup2k"], w, h, inputs[k % (2 * F)]))
+        assert e.verify() == (0, 2 * F)
+
+
+def test_engine_inputs_must_stride_evenly(gpu, scenes):
+    from simpleraytracer_amd.device import SrtError
+
+    with engine(scenes["soup300"], 40, 40, devices=[0, 0], batch=4) as e:
+        with pytest.raises(SrtError, match="multiple of the batch"):
+            e.set_inputs(random_inputs(3, 40, 40))
+
+
+def test_engine_frames_split(gpu, scenes):
+    w, h, F = 64, 48, 2
+    inputs = random_inputs(1, h, w, seed=9)
+    ref = oracle_render(scenes["soup300"], w, h, inputs[0])
+    with engine(scenes["soup300"], w, h, devices=[0, 0, 0], split="frames", batch=F) as e:
+        e.set_inputs(inputs)
+        e.run(2)
+        assert_parity(e.read_frame(2), ref)
+        assert e.verify() == (0, 3 * 2 * F)  # every device's two queues
+
+
+def test_engine_c3_bands_of_8_bitwise(gpu, scenes):
+    """The headline frame (1080p, 100k triangles) as 8 interleaved bands exchanged all-to-all over
+    fake devices: every frame equals the one-device frame, which matches the oracle on rows."""
+    w, h = 1920, 1080
+    inputs = np.full((1, h, w, 2), 0.5, np.float32)
+    with engine(scenes["soup100k"], w, h, devices=[0] * 8, batch=16, queues=2) as e:
+        e.set_inputs(inputs)
+        e.run(2)
+        assert e.verify() == (0, 32)
+        got = e.read_frame(17)
+    rows = np.arange(5, 1080, 90)
+    ref = oracle_render(scenes["soup100k"], w, h, row_begin=5, row_count=1075, row_step=90)
+    assert_parity(got, ref, rows=rows)
+
+
+def test_engine_stage_times(gpu, scenes):
+    w, h = 320, 200
+    with engine(scenes["soup2k"], w, h, devices=[0, 0]) as e:
+        e.set_inputs(np.full((1, h, w, 2), 0.5, np.float32))
+        n, prep, binned, trace = e.stage_times(1, 5)
+        assert n == 5 and prep > 0 and binned > 0 and trace > 0
+        e.run(1)
+        assert e.verify()[0] == 0

@@ -304,17 +304,20 @@ def test_repeat_render_deterministic(gpu, scenes):
 
 @pytest.mark.parametrize("devices", ["0,0", "0,0,0", "0,0,0,0,0,0,0,0"])
 @pytest.mark.parametrize("mode", ["copy", "direct"])
-def test_ml_gather_modes_bitwise(gpu, scenes, monkeypatch, devices, mode):
-    """mlInfer over P row bands on device 0 ("fake devices": one device listed P times), the
-    frame assembled by the band gather (device copies to ncclGather's receive offsets, then one
-    D2H) or by per-band D2H, equals the one-band frame bit for bit; 8 bands of 100 rows leave a
-    padded last band."""
+@pytest.mark.parametrize("rows", ["interleaved", "contiguous"])
+def test_ml_gather_modes_bitwise(gpu, scenes, monkeypatch, devices, mode, rows):
+    """mlInfer over P row bands on device 0 ("fake devices": one device listed P times): hit-id
+    bands gathered to device 0 by device copies at ncclGather's receive offsets, shaded there, one
+    D2H -- or every band shaded and copied out by its device ("direct") -- equals the one-band frame
+    bit for bit; interleaved 16-row tile rows and contiguous bands (8 bands of 100 rows leave a
+    padded last band)."""
     import simpleraytracer_amd as srt
 
     monkeypatch.delenv("ML_VISIBLE_DEVICES", raising=False)
     ref = srt.render(scenes["soup2k"], 160, 100)
     monkeypatch.setenv("ML_VISIBLE_DEVICES", devices)
     monkeypatch.setenv("SRT_GATHER", mode)
+    monkeypatch.setenv("SRT_BAND_ROWS", rows)
     got = srt.render(scenes["soup2k"], 160, 100)
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
     for variant in ("scalar", "cull", "bvh"):
