@@ -171,6 +171,8 @@ def lib() -> ctypes.CDLL:
                 "`python -c 'import __graft_entry__ as g; g.build()'`); there is no CPU fallback")
         handle = ctypes.CDLL(os.fspath(LIB_PATH))
         for name, (restype, argtypes) in _SIGNATURES.items():
+            if os.environ.get("SRT_LIB") and not hasattr(handle, name):
+                continue  # an older build under measurement (A/B): bind what it has
             fn = getattr(handle, name)
             fn.restype = restype
             fn.argtypes = argtypes

@@ -170,8 +170,10 @@ DeviceScene::~DeviceScene() {
     for (hipEvent_t e : m_prep_events) {
         (void)hipEventDestroy(e);
     }
-    if (m_order_event != nullptr) {
-        (void)hipEventDestroy(m_order_event);
+    for (hipEvent_t e : m_order_events) {
+        if (e != nullptr) {
+            (void)hipEventDestroy(e);
+        }
     }
     if (prev >= 0) {
         (void)hipSetDevice(prev);
@@ -194,20 +196,38 @@ void DeviceScene::Prepare(std::size_t width, std::size_t height, hipStream_t str
 
 void DeviceScene::OrderAfterPrevious(hipStream_t stream) const {
     if (m_used && stream != m_last_stream) {
-        HipCheck(hipStreamWaitEvent(stream, m_order_event, 0), "hipStreamWaitEvent(scene order)");
+#if SRT_ORDER_EVENTS == 0
+        HipCheck(hipEventRecord(m_order_events[0], m_last_stream), "hipEventRecord(scene order)");
+#endif
+        HipCheck(hipStreamWaitEvent(stream, m_order_events[m_order_next], 0), "hipStreamWaitEvent(scene order)");
     }
+#if SRT_ORDER_EVENTS == 0
+    if (m_order_events[0] == nullptr) {
+        HipCheck(hipEventCreateWithFlags(&m_order_events[0], hipEventDisableTiming), "hipEventCreate(scene order)");
+    }
+    m_used = true;
+    m_last_stream = stream;
+#endif
 }
 
 // Marks the end of this call's work on `stream`: the next call on another stream waits for it. The
 // event is recorded on the call's own stream, so the library never touches a stream after the call
-// that was given it has returned (the caller may destroy it).
+// that was given it has returned (the caller may destroy it). A ring of events: recording an
+// event whose previous record is still pending can stall the host, so consecutive calls use
+// different events and only the newest is waited on.
 void DeviceScene::RecordOrder(hipStream_t stream) const {
-    if (m_order_event == nullptr) {
-        HipCheck(hipEventCreateWithFlags(&m_order_event, hipEventDisableTiming), "hipEventCreate(scene order)");
+#if SRT_ORDER_EVENTS > 0
+    const std::size_t k = (m_order_next + 1) % kOrderEvents;
+    if (m_order_events[k] == nullptr) {
+        HipCheck(hipEventCreateWithFlags(&m_order_events[k], hipEventDisableTiming), "hipEventCreate(scene order)");
     }
-    HipCheck(hipEventRecord(m_order_event, stream), "hipEventRecord(scene order)");
+    HipCheck(hipEventRecord(m_order_events[k], stream), "hipEventRecord(scene order)");
+    m_order_next = k;
     m_used = true;
     m_last_stream = stream;
+#else
+    (void)stream;
+#endif
 }
 
 // The shading normals of the prepared frame, when no trace has written them yet (a Shade first):

@@ -149,7 +149,12 @@ private:
     void NormalsIfStale(hipStream_t stream) const;
     mutable hipStream_t m_last_stream = nullptr;
     mutable bool m_used = false;
-    mutable hipEvent_t m_order_event = nullptr;
+#ifndef SRT_ORDER_EVENTS
+#define SRT_ORDER_EVENTS 4
+#endif
+    static constexpr std::size_t kOrderEvents = SRT_ORDER_EVENTS > 0 ? SRT_ORDER_EVENTS : 1;
+    mutable hipEvent_t m_order_events[kOrderEvents] = {};
+    mutable std::size_t m_order_next = 0;
     mutable std::vector<hipEvent_t> m_prep_events;
     mutable std::vector<hipEvent_t> m_events;
     mutable std::vector<bool> m_binned;
