@@ -16,8 +16,8 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -fno-s
             -fvisibility=hidden -DRADEONPROML_BUILD -Iinclude -Wall -Wno-unused-result
 LDFLAGS  := -shared -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib -Wl,--no-undefined
 
-OBJS := $(BUILD)/render.o $(BUILD)/spatial.o $(BUILD)/renderer.o $(BUILD)/engine.o $(BUILD)/scene.o \
-        $(BUILD)/image.o $(BUILD)/model.o $(BUILD)/context.o $(BUILD)/srt_api.o
+OBJS := $(BUILD)/render.o $(BUILD)/spatial.o $(BUILD)/renderer.o $(BUILD)/engine.o $(BUILD)/cpu_render.o \
+        $(BUILD)/scene.o $(BUILD)/image.o $(BUILD)/model.o $(BUILD)/context.o $(BUILD)/srt_api.o
 
 HEADERS := $(wildcard $(CSRC)/*.h) include/model_runner.h include/srt_render.h
 
@@ -36,6 +36,11 @@ $(BUILD)/%.o: $(CSRC)/%.hip $(HEADERS)
 $(BUILD)/%.o: $(CSRC)/%.cpp $(HEADERS)
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+# The CPU backend: hardware fma (x86-64-v3) for its explicit fmaf; still no contraction.
+$(BUILD)/cpu_render.o: $(CSRC)/cpu_render.cpp $(HEADERS)
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -mfma -c $< -o $@
 
 $(LIB): $(OBJS)
 	@mkdir -p $(LIBDIR)

@@ -46,6 +46,13 @@ bool GatherByCopies(const std::vector<int>& devices) {
     return false;
 }
 
+// Setup launches of the batched traces on their own stream per queue: env SRT_SETUP_STREAM
+// (0 = off; 1 = a second stream of default priority; 2 = of the highest priority).
+int SetupStreamMode() {
+    const char* v = std::getenv("SRT_SETUP_STREAM");
+    return v == nullptr || *v == '\0' ? 0 : std::atoi(v);
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------------------------
@@ -262,6 +269,7 @@ private:
 struct FrameEngine::Queue {
     std::unique_ptr<DeviceScene> scene;
     hipStream_t stream = nullptr;
+    hipStream_t setup = nullptr;     // the setup launches of batched traces (SetupStreamMode)
     hipEvent_t traced = nullptr;     // the batch's trace done (queue stream)
     hipEvent_t exchanged = nullptr;  // the batch's exchange done (comm stream)
     int* send = nullptr;             // bands: ids for the other compositors
@@ -388,6 +396,14 @@ void FrameEngine::AllocateQueues() {
             HipCheck(hipEventCreateWithFlags(&q.exchanged, hipEventDisableTiming), "hipEventCreate(exchanged)");
             q.scene = std::make_unique<DeviceScene>(*m_scene, d.device);
             q.scene->Prepare(m_width, m_height, q.stream);
+            const int mode = SetupStreamMode();
+            if (mode != 0) {
+                int least = 0, greatest = 0;
+                HipCheck(hipDeviceGetStreamPriorityRange(&least, &greatest), "hipDeviceGetStreamPriorityRange");
+                HipCheck(hipStreamCreateWithPriority(&q.setup, hipStreamNonBlocking, mode == 2 ? greatest : least),
+                         "hipStreamCreate(setup)");
+                q.scene->SetSetupStream(q.setup);
+            }
             if (exchange) {
                 const std::size_t send_frames = m_plan.exchange == EngineOptions::kAllToAll
                                                     ? m_world * m_plan.MaxFramesPerCompositor()
@@ -416,6 +432,9 @@ void FrameEngine::Release() noexcept {
         for (Queue& q : dp->queues) {
             if (q.stream != nullptr) {
                 (void)hipStreamSynchronize(q.stream);
+            }
+            if (q.setup != nullptr) {
+                (void)hipStreamSynchronize(q.setup);
             }
         }
         if (dp->comm != nullptr) {
@@ -447,6 +466,10 @@ void FrameEngine::Release() noexcept {
             if (q.stream != nullptr) {
                 (void)hipStreamDestroy(q.stream);
             }
+            if (q.setup != nullptr) {
+                (void)hipStreamDestroy(q.setup);
+            }
+            q.setup = nullptr;
             q.traced = q.exchanged = nullptr;
             q.stream = nullptr;
         }

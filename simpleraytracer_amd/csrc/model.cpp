@@ -80,14 +80,23 @@ ml_status Model::SetInputInfo(ml_image_info const* info) {
         return ML_FAIL;
     }
     const bool same = ForEachDim([this, info](auto dim, char const*) { return m_input_info.*dim == info->*dim; });
-    if (same && m_renderer && m_renderer->configured()) {
+    if (same && ((m_renderer && m_renderer->configured()) || (m_cpu && m_cpu->configured()))) {
         return ML_OK;  // nothing changed
     }
     try {
-        if (!m_renderer) {
-            m_renderer = std::make_unique<srt::Renderer>(m_scene, srt::VisibleDevices());
+        // The backend is chosen once, by the first call: the CPU only when selected explicitly.
+        if (!m_renderer && !m_cpu) {
+            if (srt::CpuBackendSelected()) {
+                m_cpu = std::make_unique<srt::CpuRenderer>(m_scene);
+            } else {
+                m_renderer = std::make_unique<srt::Renderer>(m_scene, srt::VisibleDevices());
+            }
         }
-        m_renderer->Configure(info->width, info->height);
+        if (m_cpu) {
+            m_cpu->Configure(info->width, info->height);
+        } else {
+            m_renderer->Configure(info->width, info->height);
+        }
     } catch (std::exception& e) {
         m_error_cache << e.what();
         return ML_FAIL;
@@ -164,7 +173,11 @@ bool Model::RenderToImage(Image& input, Image& output) {
     }
     bool ok = true;
     try {
-        m_renderer->Render(in_data, out_data);
+        if (m_cpu) {
+            m_cpu->Render(in_data, out_data);
+        } else {
+            m_renderer->Render(in_data, out_data);
+        }
     } catch (std::exception& e) {
         m_error_cache << "Render error: " << e.what();
         ok = false;

@@ -1,4 +1,5 @@
-// ML::Model -- a triangle scene plus its GPU renderer behind an ml_model handle.
+// ML::Model -- a triangle scene plus its renderer (GPU, or the explicitly selected CPU backend)
+// behind an ml_model handle.
 // Reference: /root/reference/model_runner/model.{h,cpp} (TF GraphDef + Session there).
 #pragma once
 
@@ -6,6 +7,7 @@
 #include <sstream>
 #include <string>
 
+#include "cpu_render.h"
 #include "model_runner.h"
 #include "renderer.h"
 #include "scene.h"
@@ -35,7 +37,8 @@ private:
     // Input: per-pixel sample offsets (2 channels); output: RGBA framebuffer (4 channels).
     ml_image_info m_input_info{ML_FLOAT32, 0, 0, 2};
     ml_image_info m_output_info{ML_FLOAT32, 0, 0, 4};
-    std::unique_ptr<srt::Renderer> m_renderer;
+    std::unique_ptr<srt::Renderer> m_renderer;  // HIP devices (ML_VISIBLE_DEVICES list; unset = device 0)
+    std::unique_ptr<srt::CpuRenderer> m_cpu;    // ML_VISIBLE_DEVICES=cpu (config C1 without a GPU)
     std::ostringstream m_error_cache;
 };
 

@@ -199,9 +199,12 @@ struct CullFrame {
 // work as `count` single-frame calls, with a quarter of the launches per frame. The records are
 // computed in the bin launch every call (bins->order: position -> id; d_rank unused). Events
 // (optional): prep = tile info, bin = record setup + bins + work list, trace.
+// setup_stream (optional): the three setup launches go there (after the work already on `stream`:
+// setup_events[0]), the trace back on `stream` after them (setup_events[1]).
 hipError_t LaunchCullFrames(const CullFrame* frames, std::size_t count, std::uint64_t n, const float* d_vertices,
                             const float* d_albedo, const Frame& frame, const float background[3], const unsigned* d_rank,
-                            hipStream_t stream, const StageEvents* events);
+                            hipStream_t stream, const StageEvents* events, hipStream_t setup_stream = nullptr,
+                            const hipEvent_t* setup_events = nullptr);
 
 // Deferred shading of a band from hit ids (band.ids) and sample offsets into band.rgba, with the
 // edge buffer's shading normals of the prepared frame: bit-identical to the fused trace.

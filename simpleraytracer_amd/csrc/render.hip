@@ -1956,14 +1956,20 @@ __global__ __launch_bounds__(kBinThreads) void PrepareBinKernel(const PrepareBin
 #endif
 constexpr int kOrderThreads = SRT_ORDER_THREADS;  // the work-order block (kOrderUnroll tiles per thread per
                                                   // pass; 512 / 256 threads: 9.0 / 12.2 instead of 8.1 us)
+// LDS sized to the band (dynamic): a block that fits beside the trace blocks of other frames
+// starts sooner (a 1024-thread block with 40 KB of static LDS waited for whole CUs to drain).
 __global__ __launch_bounds__(kOrderThreads) void WorkOrderKernel(const BinBatch batch) {
     __shared__ unsigned start[64];
     __shared__ unsigned sum[2];
-    __shared__ unsigned cnt[kMaxBinTiles];
-    __shared__ unsigned char meta[kMaxBinTiles];
     __shared__ CullRecord lrec[kEmptyTest];
-    BuildWorkOrder(batch.f[blockIdx.z], start, cnt, meta, sum, lrec);
+    extern __shared__ unsigned order_lds[];
+    const BinParams& p = batch.f[blockIdx.z];
+    unsigned* cnt = order_lds;
+    unsigned char* meta = reinterpret_cast<unsigned char*>(order_lds + p.tiles_x * p.tiles_y);
+    BuildWorkOrder(p, start, cnt, meta, sum, lrec);
 }
+
+std::size_t OrderLdsBytes(int tiles) { return static_cast<std::size_t>(tiles) * 5 + 16; }
 
 #ifndef SRT_TRACE_OCC
 #define SRT_TRACE_OCC 6
@@ -2909,7 +2915,22 @@ BinParams BindBins(TraceParams& p, const CullBins& bins, std::uint64_t n) {
 
 hipError_t LaunchCullFrames(const CullFrame* frames, std::size_t count, std::uint64_t n, const float* d_vertices,
                             const float* d_albedo, const Frame& frame, const float background[3], const unsigned* d_rank,
-                            hipStream_t stream, const StageEvents* events) {
+                            hipStream_t stream, const StageEvents* events, hipStream_t setup_stream,
+                            const hipEvent_t* setup_events) {
+    hipStream_t trace_stream = stream;
+    if (setup_stream != nullptr) {  // setup kernels on their own stream, after the caller's earlier work
+        if (setup_events == nullptr) {
+            return hipErrorInvalidValue;
+        }
+        hipError_t e = hipEventRecord(setup_events[0], stream);
+        if (e == hipSuccess) {
+            e = hipStreamWaitEvent(setup_stream, setup_events[0], 0);
+        }
+        if (e != hipSuccess) {
+            return e;
+        }
+        stream = setup_stream;
+    }
     if (frames == nullptr || count == 0 || count > static_cast<std::size_t>(kMaxBatch)) {
         return hipErrorInvalidValue;
     }
@@ -2953,7 +2974,19 @@ hipError_t LaunchCullFrames(const CullFrame* frames, std::size_t count, std::uin
     const unsigned blocks = (pb.f[0].prep.n_pad + kBinThreads - 1) / kBinThreads;
     LaunchLds(PrepareBinKernel, dim3(blocks, 1, z), dim3(kBinThreads),
               BinLdsBytes(static_cast<int>(gx), static_cast<int>(gy)), stream, ev.bin_begin, nullptr, pb);
-    Launch(WorkOrderKernel, dim3(1, 1, z), dim3(kOrderThreads), stream, nullptr, ev.bin_end, bb);
+    LaunchLds(WorkOrderKernel, dim3(1, 1, z), dim3(kOrderThreads), OrderLdsBytes(static_cast<int>(gx * gy)), stream,
+              nullptr, ev.bin_end, bb);
+    if (setup_stream != nullptr) {  // the trace on the caller's stream, after the setup
+        const hipError_t e = hipEventRecord(setup_events[1], stream);
+        if (e != hipSuccess) {
+            return e;
+        }
+        stream = trace_stream;
+        const hipError_t w = hipStreamWaitEvent(stream, setup_events[1], 0);
+        if (w != hipSuccess) {
+            return w;
+        }
+    }
     Launch(TraceCullKernel, dim3(frames[0].bins->descs, 1, z), dim3(kWave * kCullWaves), stream, ev.begin, ev.end, tb);
     return hipGetLastError();
 }

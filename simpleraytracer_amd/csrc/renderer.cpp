@@ -67,7 +67,7 @@ std::vector<int> VisibleDevices() {
     if (err != hipSuccess || count <= 0) {
         throw std::runtime_error(std::string("HIP error: no HIP device available (") +
                                  (err != hipSuccess ? hipGetErrorString(err) : "device count 0") +
-                                 "); this renderer has no CPU path");
+                                 "); set ML_VISIBLE_DEVICES=cpu to render on the CPU backend");
     }
     std::vector<int> devices;
     const char* env = std::getenv("ML_VISIBLE_DEVICES");
@@ -171,6 +171,11 @@ DeviceScene::~DeviceScene() {
         (void)hipEventDestroy(e);
     }
     for (hipEvent_t e : m_order_events) {
+        if (e != nullptr) {
+            (void)hipEventDestroy(e);
+        }
+    }
+    for (hipEvent_t e : m_setup_events) {
         if (e != nullptr) {
             (void)hipEventDestroy(e);
         }
@@ -360,8 +365,13 @@ void DeviceScene::TraceBatch(const float* const* d_offsets, float* const* d_rgba
                               row_count, d_ids != nullptr ? d_ids[f] : nullptr, row_interleave};
     }
     const StageEvents ev = BindStageEvents(true, true);
+    if (m_setup_stream != nullptr && m_setup_events[0] == nullptr) {
+        for (hipEvent_t& e : m_setup_events) {
+            HipCheck(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate(setup)");
+        }
+    }
     HipCheck(LaunchCullFrames(cf, frames, m_n, m_vertices, m_albedo, m_frame, m_background, m_rank, stream,
-                              m_timing ? &ev : nullptr),
+                              m_timing ? &ev : nullptr, m_setup_stream, m_setup_events),
              "batched trace launch");
     m_normals_current = true;  // slot 0's normals (the tile-planar records are the full pass's)
     RecordOrder(stream);
@@ -437,6 +447,8 @@ hipEvent_t DeviceScene::TimingEvent(std::vector<hipEvent_t>& pool, std::size_t i
     }
     return pool[i];
 }
+
+void DeviceScene::SetSetupStream(hipStream_t setup_stream) { m_setup_stream = setup_stream; }
 
 void DeviceScene::SetTiming(bool on) {
     m_timing = on;
