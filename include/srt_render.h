@@ -179,8 +179,9 @@ ML_API_ENTRY void srtEngineRelease(srt_engine engine);
 ML_API_ENTRY int srtEngineSetInputs(srt_engine engine, const float* host_offsets, size_t count);
 /* Render `batches` x batch frames, continuing the frame sequence; synchronous. */
 ML_API_ENTRY int srtEngineRun(srt_engine engine, size_t batches);
-/* Every locally composited frame of each queue's last batch vs a single-device full-frame render of
- * its input (another trace variant), bit for bit: mismatching and checked frame counts. */
+/* The locally composited frames of each queue's last batch (up to 4 per queue) vs a single-device
+ * full-frame render of their inputs (another trace variant), bit for bit: mismatching and checked
+ * frame counts. */
 ML_API_ENTRY int srtEngineVerify(srt_engine engine, size_t* mismatches, size_t* checked);
 /* Frame k of the last `queues` batches into host RGBA (height x width x 4 floats); fails when another
  * rank composited it (bands) or it is no longer resident. */

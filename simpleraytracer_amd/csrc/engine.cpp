@@ -46,13 +46,6 @@ bool GatherByCopies(const std::vector<int>& devices) {
     return false;
 }
 
-// Setup launches of the batched traces on their own stream per queue: env SRT_SETUP_STREAM
-// (0 = off; 1 = a second stream of default priority; 2 = of the highest priority).
-int SetupStreamMode() {
-    const char* v = std::getenv("SRT_SETUP_STREAM");
-    return v == nullptr || *v == '\0' ? 0 : std::atoi(v);
-}
-
 }  // namespace
 
 // ---------------------------------------------------------------------------------------------
@@ -269,7 +262,6 @@ private:
 struct FrameEngine::Queue {
     std::unique_ptr<DeviceScene> scene;
     hipStream_t stream = nullptr;
-    hipStream_t setup = nullptr;     // the setup launches of batched traces (SetupStreamMode)
     hipEvent_t traced = nullptr;     // the batch's trace done (queue stream)
     hipEvent_t exchanged = nullptr;  // the batch's exchange done (comm stream)
     int* send = nullptr;             // bands: ids for the other compositors
@@ -396,14 +388,6 @@ void FrameEngine::AllocateQueues() {
             HipCheck(hipEventCreateWithFlags(&q.exchanged, hipEventDisableTiming), "hipEventCreate(exchanged)");
             q.scene = std::make_unique<DeviceScene>(*m_scene, d.device);
             q.scene->Prepare(m_width, m_height, q.stream);
-            const int mode = SetupStreamMode();
-            if (mode != 0) {
-                int least = 0, greatest = 0;
-                HipCheck(hipDeviceGetStreamPriorityRange(&least, &greatest), "hipDeviceGetStreamPriorityRange");
-                HipCheck(hipStreamCreateWithPriority(&q.setup, hipStreamNonBlocking, mode == 2 ? greatest : least),
-                         "hipStreamCreate(setup)");
-                q.scene->SetSetupStream(q.setup);
-            }
             if (exchange) {
                 const std::size_t send_frames = m_plan.exchange == EngineOptions::kAllToAll
                                                     ? m_world * m_plan.MaxFramesPerCompositor()
@@ -432,9 +416,6 @@ void FrameEngine::Release() noexcept {
         for (Queue& q : dp->queues) {
             if (q.stream != nullptr) {
                 (void)hipStreamSynchronize(q.stream);
-            }
-            if (q.setup != nullptr) {
-                (void)hipStreamSynchronize(q.setup);
             }
         }
         if (dp->comm != nullptr) {
@@ -466,10 +447,6 @@ void FrameEngine::Release() noexcept {
             if (q.stream != nullptr) {
                 (void)hipStreamDestroy(q.stream);
             }
-            if (q.setup != nullptr) {
-                (void)hipStreamDestroy(q.setup);
-            }
-            q.setup = nullptr;
             q.traced = q.exchanged = nullptr;
             q.stream = nullptr;
         }
@@ -757,7 +734,7 @@ bool FrameEngine::ReadFrame(std::size_t k, float* host_rgba) {
     return true;
 }
 
-std::size_t FrameEngine::Verify(std::size_t* checked) {
+std::size_t FrameEngine::Verify(std::size_t* checked, std::size_t per_queue) {
     const std::size_t F = m_opt.batch;
     const std::size_t frame_floats4 = m_width * m_height * 4;
     const bool exchange = m_bands && m_world > 1;
@@ -781,7 +758,8 @@ std::size_t FrameEngine::Verify(std::size_t* checked) {
                 }
                 HipCheck(hipStreamSynchronize(q.stream), "hipStreamSynchronize(verify)");
                 const std::size_t b = q.last_batch;
-                for (std::size_t f = 0; f < F; ++f) {
+                std::size_t taken = 0;
+                for (std::size_t f = 0; f < F && taken < per_queue; ++f) {
                     std::size_t slot = f;
                     if (exchange) {
                         if (m_plan.Compositor(b, f) != d.band) {
@@ -789,6 +767,7 @@ std::size_t FrameEngine::Verify(std::size_t* checked) {
                         }
                         slot = m_plan.Slot(f);
                     }
+                    ++taken;
                     const std::size_t r = (b * F + f) % m_inputs;
                     if (refs[r].empty()) {
                         ref_scene.Trace(FullInput(local, r), ref_dev, 0, m_height, m_opt.variant == kTraceCull ? kTraceLds

@@ -99,10 +99,10 @@ public:
     // Render `batches` batches (batch x frames each), continuing the frame sequence; returns when
     // every local device has finished.
     void Run(std::size_t batches);
-    // Every frame composited locally in each queue's last batch, compared bit for bit with a
-    // single-device full-frame render of its input. Returns the number of mismatching frames;
-    // `checked` receives the number compared.
-    std::size_t Verify(std::size_t* checked);
+    // The frames composited locally in each queue's last batch (the first `per_queue` of them),
+    // compared bit for bit with a single-device full-frame render of their inputs. Returns the
+    // number of mismatching frames; `checked` receives the number compared.
+    std::size_t Verify(std::size_t* checked, std::size_t per_queue = 4);
     // Frame k (of the last Q batches) into host RGBA (H x W x 4 floats); false when frame k is not
     // resident on a local device (another rank composited it, or it is older).
     bool ReadFrame(std::size_t k, float* host_rgba);

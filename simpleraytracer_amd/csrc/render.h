@@ -80,6 +80,12 @@ struct BandArgs {
 
 // Frame row of band-local row `local` (BandArgs::row_interleave).
 inline std::size_t BandFrameRow(std::size_t row_begin, std::size_t interleave, std::size_t local);
+// Whether a binned cull frame computes its tile info inside the bin launch (one launch fewer, the
+// tile info and the bins concurrent): full frames (the band is the whole frame), unless env
+// SRT_FUSED_INFO=0. Its bins then use the analytic tile bounds (valid for offsets in [0, 1]) and
+// write every cull record; a frame with an offset outside [0, 1] streams every record in every
+// tile (the work order sees the range tag), which is exact.
+bool CullFusedInfo(std::size_t row_begin, std::size_t row_count, std::size_t height, std::size_t interleave);
 // Whether a band fits a frame of `height` rows (row_count may be 0).
 bool BandFits(std::size_t row_begin, std::size_t row_count, std::size_t interleave, std::size_t height);
 // Rows of band `band` of `bands` interleaved bands of a `height`-row frame.
@@ -199,12 +205,9 @@ struct CullFrame {
 // work as `count` single-frame calls, with a quarter of the launches per frame. The records are
 // computed in the bin launch every call (bins->order: position -> id; d_rank unused). Events
 // (optional): prep = tile info, bin = record setup + bins + work list, trace.
-// setup_stream (optional): the three setup launches go there (after the work already on `stream`:
-// setup_events[0]), the trace back on `stream` after them (setup_events[1]).
 hipError_t LaunchCullFrames(const CullFrame* frames, std::size_t count, std::uint64_t n, const float* d_vertices,
                             const float* d_albedo, const Frame& frame, const float background[3], const unsigned* d_rank,
-                            hipStream_t stream, const StageEvents* events, hipStream_t setup_stream = nullptr,
-                            const hipEvent_t* setup_events = nullptr);
+                            hipStream_t stream, const StageEvents* events);
 
 // Deferred shading of a band from hit ids (band.ids) and sample offsets into band.rgba, with the
 // edge buffer's shading normals of the prepared frame: bit-identical to the fused trace.

@@ -483,7 +483,11 @@ __device__ __forceinline__ void StorePixel(const TraceParams& p, int x, int y, f
     if (p.out_ids != nullptr) {
         __builtin_nontemporal_store(id, p.out_ids + at);
     } else {
+#ifdef SRT_EXP_NO_SHADE  // measurement builds only: store without shading
+        const float4 v = make_float4(fx, fy, 0.f, static_cast<float>(id));
+#else
         const float4 v = ShadePixel(p, fx, fy, id);
+#endif
         __builtin_nontemporal_store(F4{v.x, v.y, v.z, v.w}, reinterpret_cast<F4*>(p.out + at));
     }
 }
@@ -1186,7 +1190,11 @@ __device__ __forceinline__ void PacketBatch(CullShared& sh, const Box& bb, const
     const unsigned last_slot = n_surv == 0u ? 0u : n_surv - 1u;
     unsigned ended = 0u;  // ranges that end before the window (block-uniform)
 #pragma unroll 1
+#ifdef SRT_EXP_NO_WALK  // measurement builds only: filter and compact, no pixel tests
+    for (unsigned w0 = 0; w0 < 0u; w0 += kWindowPixels) {
+#else
     for (unsigned w0 = 0; w0 < n_pk; w0 += kWindowPixels) {
+#endif
         const unsigned wn = min(kWindowPixels, n_pk - w0);
         const unsigned npk_w = (wn + kWave - 1u) / kWave;
         if (w0 != 0u) {  // a later window (rare: > kWindowPixels pixels in the batch): rebuild its bitmap
@@ -1339,6 +1347,7 @@ struct BinParams {
     unsigned min_chunk;  // smallest candidate chunk of a split part
     unsigned n;
     unsigned exp;  // diagnostic build: experiment bits (env SRT_EXP), 0 in the product
+    unsigned fused;  // tile info computed in the bin launch (CullFusedInfo): bins assume offsets in [0, 1]
     int tiles_x;
     int tiles_y;
     int width;
@@ -1478,11 +1487,7 @@ __device__ __forceinline__ void TileInfoBlock(const BinParams& p, int bx, int by
         ti.regular = irregular[sub] == 0u ? 1u : 0u;
         ti.usable = ScreenBoxUsable(box) ? 1u : 0u;
         const unsigned tile = ty * p.tiles_x + bx;
-        p.tile_info[tile] = ti;
-        p.counts[tile] = 0u;  // the bin kernel runs after this one (stream order)
-        if (tile == 0) {
-            p.counts[p.tiles_x * p.tiles_y] = 0u;  // large list
-        }
+        p.tile_info[tile] = ti;  // (the bin counts are reset by the work order that reads them)
     }
     if (tid == 0 && out_of_range != 0u) {
         *p.range_tag = p.gen;  // this frame's bin blocks reduce the tile boxes (BinTileBounds)
@@ -1555,9 +1560,9 @@ struct OrderItem {
     unsigned cand, flags, parts;
 };
 __device__ __forceinline__ OrderItem MakeOrderItem(const BinParams& p, unsigned t, unsigned cnt, unsigned large,
-                                                   const TileInfo& ti) {
+                                                   const TileInfo& ti, bool bins_invalid) {
     OrderItem it;
-    const bool full = ti.usable == 0u || cnt > p.capacity;
+    const bool full = ti.usable == 0u || cnt > p.capacity || bins_invalid;
     it.flags = (full ? kItemFull : 0u) | (ti.regular != 0u ? kItemRegular : 0u);
     it.cand = full ? 0u : cnt + large;
     const int rows_left = p.row_count - static_cast<int>(t / static_cast<unsigned>(p.tiles_x)) * kTileRows;
@@ -1589,6 +1594,9 @@ __device__ void BuildWorkOrder(const BinParams& p, unsigned* start, unsigned* cn
         sum[tid] = 0u;
     }
     const unsigned large = p.counts[tiles];
+    // A fused launch binned with the analytic tile bounds, which hold only for offsets in [0, 1]:
+    // if a tile-info block found one outside (the range tag), every tile streams every record.
+    const bool bins_invalid = p.fused != 0u && *p.range_tag == p.gen;
     if (tid < kEmptyTest && static_cast<unsigned>(tid) < large && large <= static_cast<unsigned>(kEmptyTest)) {
         lrec[tid] = p.cull[p.large_list[tid]];  // read after the barriers below
     }
@@ -1607,7 +1615,8 @@ __device__ void BuildWorkOrder(const BinParams& p, unsigned* start, unsigned* cn
         for (int u = 0; u < kOrderUnroll; ++u) {
             const unsigned t = t0 + u * nthreads;
             if (t < tiles) {
-                const OrderItem it = MakeOrderItem(p, t, c[u], large, ti[u]);
+                p.counts[t] = 0u;  // the next frame of this slot bins from zero (stream order)
+                const OrderItem it = MakeOrderItem(p, t, c[u], large, ti[u], bins_invalid);
                 cnt[t] = it.cand;
                 meta[t] = static_cast<unsigned char>(it.flags | it.parts << 2);
                 my_cand += static_cast<unsigned long long>(it.parts) * it.cand;
@@ -1655,6 +1664,7 @@ __device__ void BuildWorkOrder(const BinParams& p, unsigned* start, unsigned* cn
         }
         start[lane] = suf - c;
         if (lane == 0) {
+            p.counts[tiles] = 0u;  // the large list (every thread read it before the barriers above)
             p.work_count[0] = suf;
             sum[0] = 0u;  // split slots handed out (sum[] read by every thread before the barrier above)
             sum[1] = suf;
@@ -1729,7 +1739,7 @@ __device__ void BinTileBounds(const BinParams& p, unsigned* scratch, float2* out
     const int lane = tid & (kWave - 1);
     const int wave = tid / kWave;
     const int nx = p.tiles_x, ny = p.tiles_y;
-    if (*p.range_tag != p.gen) {  // written by the previous launch's tile blocks
+    if (p.fused != 0u || *p.range_tag != p.gen) {  // tag: written by the previous launch's tile blocks
         for (int i = tid; i < nx + ny; i += nthreads) {
             const bool col = i < nx;
             const int r0 = FrameRow(p.row_begin, p.row_interleave, (i - nx) * kTileRows);  // the tile row's first
@@ -1822,6 +1832,15 @@ __global__ __launch_bounds__(kBinThreads) void PrepareBinKernel(const PrepareBin
     const PrepareBinParams& pb = batch.f[blockIdx.z];
     const BinParams& p = pb.bin;
     const PrepareParams& pp = pb.prep;
+    if (p.fused != 0u) {  // the blocks past the record blocks compute the tile info (CullFusedInfo)
+        const unsigned rec_blocks = (pp.n_pad + kBinThreads - 1) / kBinThreads;
+        if (blockIdx.x >= rec_blocks) {
+            const unsigned k = blockIdx.x - rec_blocks;
+            TileInfoBlock(p, static_cast<int>(k % static_cast<unsigned>(p.tiles_x)),
+                          static_cast<int>(k / static_cast<unsigned>(p.tiles_x)));
+            return;
+        }
+    }
     const int tid = threadIdx.x;
     const int nx = p.tiles_x, ny = p.tiles_y;
     const int tiles = nx * ny;
@@ -1849,7 +1868,7 @@ __global__ __launch_bounds__(kBinThreads) void PrepareBinKernel(const PrepareBin
         if (real) {
             pp.normals[id] = ShadingNormal(v);
         }
-        bool needed = !real || *p.range_tag == p.gen;
+        bool needed = !real || p.fused != 0u || *p.range_tag == p.gen;  // fused: a full frame, every record
         if (!needed) {  // does the quantized box meet a tile row of the band (analytic row bounds)?
             // Quantisation keeps both bound sequences nondecreasing: the first row whose quantized
             // hi reaches the box's lo has the smallest lo of the rows that can meet it.
@@ -1904,9 +1923,15 @@ __global__ __launch_bounds__(kBinThreads) void PrepareBinKernel(const PrepareBin
 #pragma unroll
         for (int k = 0; k < kBinAhead; ++k) {
             const int kc = min(k, w * h - 1);
-            const TileInfo& ti = p.tile_info[(r0 + kc / w) * nx + c0 + kc % w];
-            box[k] = ti.box;
-            usable[k] = ti.usable;
+            if (p.fused != 0u) {  // the analytic tile box (contains the tile's rays for offsets in [0, 1])
+                const float2 bx = b[c0 + kc % w], by = b[nx + r0 + kc / w];
+                box[k] = make_float4(bx.x, bx.y, by.x, by.y);
+                usable[k] = 1u;
+            } else {
+                const TileInfo& ti = p.tile_info[(r0 + kc / w) * nx + c0 + kc % w];
+                box[k] = ti.box;
+                usable[k] = ti.usable;
+            }
         }
 #pragma unroll
         for (int k = 0; k < kBinAhead; ++k) {
@@ -1917,9 +1942,17 @@ __global__ __launch_bounds__(kBinThreads) void PrepareBinKernel(const PrepareBin
         }
 #pragma unroll 1
         for (int k = kBinAhead; k < w * h; ++k) {
-            const TileInfo ti = p.tile_info[(r0 + k / w) * nx + c0 + k % w];
-            const Box tb{ti.box.x, ti.box.y, ti.box.z, ti.box.w};
-            if (ti.usable != 0u && ScreenBoxOverlaps(tb, sb) && BoxMayHit(tb, rec)) {
+            Box tb;
+            unsigned use = 1u;
+            if (p.fused != 0u) {
+                const float2 bx = b[c0 + k % w], by = b[nx + r0 + k / w];
+                tb = Box{bx.x, bx.y, by.x, by.y};
+            } else {
+                const TileInfo ti = p.tile_info[(r0 + k / w) * nx + c0 + k % w];
+                tb = Box{ti.box.x, ti.box.y, ti.box.z, ti.box.w};
+                use = ti.usable;
+            }
+            if (use != 0u && ScreenBoxOverlaps(tb, sb) && BoxMayHit(tb, rec)) {
                 mask |= 1u << k;
             }
         }
@@ -2063,7 +2096,11 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(c
     }
     // LIST: the first batch's records are requested before the rays are set up (its loads
     // are the block's longest dependency chain: list entry, then the 64-B record).
+#ifdef SRT_EXP_NO_LIST  // measurement builds only: no candidates (rays, tables, shading, stores)
+    const unsigned total = 0u;
+#else
     const unsigned total = src.end - src.begin;
+#endif
     CullRecord nxt[kSlices];
     auto load_list = [&](unsigned b0) {
 #pragma unroll
@@ -2915,22 +2952,7 @@ BinParams BindBins(TraceParams& p, const CullBins& bins, std::uint64_t n) {
 
 hipError_t LaunchCullFrames(const CullFrame* frames, std::size_t count, std::uint64_t n, const float* d_vertices,
                             const float* d_albedo, const Frame& frame, const float background[3], const unsigned* d_rank,
-                            hipStream_t stream, const StageEvents* events, hipStream_t setup_stream,
-                            const hipEvent_t* setup_events) {
-    hipStream_t trace_stream = stream;
-    if (setup_stream != nullptr) {  // setup kernels on their own stream, after the caller's earlier work
-        if (setup_events == nullptr) {
-            return hipErrorInvalidValue;
-        }
-        hipError_t e = hipEventRecord(setup_events[0], stream);
-        if (e == hipSuccess) {
-            e = hipStreamWaitEvent(setup_stream, setup_events[0], 0);
-        }
-        if (e != hipSuccess) {
-            return e;
-        }
-        stream = setup_stream;
-    }
+                            hipStream_t stream, const StageEvents* events) {
     if (frames == nullptr || count == 0 || count > static_cast<std::size_t>(kMaxBatch)) {
         return hipErrorInvalidValue;
     }
@@ -2966,27 +2988,27 @@ hipError_t LaunchCullFrames(const CullFrame* frames, std::size_t count, std::uin
     }
     const unsigned z = static_cast<unsigned>(count);
     const unsigned gx = static_cast<unsigned>(tb.f[0].tiles_x), gy = tb.f[0].tiles / gx;
-    // Tile info; records + bins (every padded position: the FULL stream reads them all); the
-    // trace work list; the trace: one block per work descriptor (grid z = frame; interleaving the
-    // frames' descriptors so every frame's heaviest work starts first measured no faster).
-    Launch(TileInfoKernel, dim3(gx, (gy + kInfoTiles - 1) / kInfoTiles, z), dim3(kBinThreads), stream, ev.prep_begin,
-           ev.prep_end, bb);
-    const unsigned blocks = (pb.f[0].prep.n_pad + kBinThreads - 1) / kBinThreads;
+    const unsigned info_blocks = gx * ((gy + kInfoTiles - 1) / kInfoTiles);
+    const bool fused = CullFusedInfo(band0.row_begin, band0.row_count, band0.height, band0.row_interleave);
+    // Tile info (fused: extra blocks of the bin launch); records + bins (every padded position: the
+    // FULL stream reads them all); the trace work list; the trace: one block per work descriptor
+    // (grid z = frame; interleaving the frames' descriptors so every frame's heaviest work starts
+    // first measured no faster).
+    unsigned blocks = (pb.f[0].prep.n_pad + kBinThreads - 1) / kBinThreads;
+    if (fused) {
+        for (std::size_t i = 0; i < count; ++i) {
+            bb.f[i].fused = 1u;
+            pb.f[i].bin.fused = 1u;
+        }
+        blocks += info_blocks;
+    } else {
+        Launch(TileInfoKernel, dim3(gx, (gy + kInfoTiles - 1) / kInfoTiles, z), dim3(kBinThreads), stream,
+               ev.prep_begin, ev.prep_end, bb);
+    }
     LaunchLds(PrepareBinKernel, dim3(blocks, 1, z), dim3(kBinThreads),
               BinLdsBytes(static_cast<int>(gx), static_cast<int>(gy)), stream, ev.bin_begin, nullptr, pb);
     LaunchLds(WorkOrderKernel, dim3(1, 1, z), dim3(kOrderThreads), OrderLdsBytes(static_cast<int>(gx * gy)), stream,
               nullptr, ev.bin_end, bb);
-    if (setup_stream != nullptr) {  // the trace on the caller's stream, after the setup
-        const hipError_t e = hipEventRecord(setup_events[1], stream);
-        if (e != hipSuccess) {
-            return e;
-        }
-        stream = trace_stream;
-        const hipError_t w = hipStreamWaitEvent(stream, setup_events[1], 0);
-        if (w != hipSuccess) {
-            return w;
-        }
-    }
     Launch(TraceCullKernel, dim3(frames[0].bins->descs, 1, z), dim3(kWave * kCullWaves), stream, ev.begin, ev.end, tb);
     return hipGetLastError();
 }
@@ -3053,6 +3075,14 @@ hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_ver
         Launch(TraceLdsKernel, dim3(gx, gy), dim3(kWave * kLdsWaves), stream, ev.begin, ev.end, p);
     }
     return hipGetLastError();
+}
+
+bool CullFusedInfo(std::size_t row_begin, std::size_t row_count, std::size_t height, std::size_t interleave) {
+    static const bool enabled = [] {
+        const char* v = std::getenv("SRT_FUSED_INFO");
+        return v == nullptr || std::strcmp(v, "0") != 0;
+    }();
+    return enabled && row_begin == 0 && row_count == height && interleave == 1;
 }
 
 bool BandFits(std::size_t row_begin, std::size_t row_count, std::size_t interleave, std::size_t height) {

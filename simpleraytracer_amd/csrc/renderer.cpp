@@ -175,11 +175,6 @@ DeviceScene::~DeviceScene() {
             (void)hipEventDestroy(e);
         }
     }
-    for (hipEvent_t e : m_setup_events) {
-        if (e != nullptr) {
-            (void)hipEventDestroy(e);
-        }
-    }
     if (prev >= 0) {
         (void)hipSetDevice(prev);
     }
@@ -364,14 +359,9 @@ void DeviceScene::TraceBatch(const float* const* d_offsets, float* const* d_rgba
         cf[f].band = BandArgs{d_offsets[f], d_rgba != nullptr ? d_rgba[f] : nullptr, m_width, m_height, row_begin,
                               row_count, d_ids != nullptr ? d_ids[f] : nullptr, row_interleave};
     }
-    const StageEvents ev = BindStageEvents(true, true);
-    if (m_setup_stream != nullptr && m_setup_events[0] == nullptr) {
-        for (hipEvent_t& e : m_setup_events) {
-            HipCheck(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate(setup)");
-        }
-    }
+    const StageEvents ev = BindStageEvents(!CullFusedInfo(row_begin, row_count, m_height, row_interleave), true);
     HipCheck(LaunchCullFrames(cf, frames, m_n, m_vertices, m_albedo, m_frame, m_background, m_rank, stream,
-                              m_timing ? &ev : nullptr, m_setup_stream, m_setup_events),
+                              m_timing ? &ev : nullptr),
              "batched trace launch");
     m_normals_current = true;  // slot 0's normals (the tile-planar records are the full pass's)
     RecordOrder(stream);
@@ -400,7 +390,8 @@ void DeviceScene::Trace(const float* d_offsets, float* d_rgba, std::size_t row_b
     // The full record pass for every path but the binned cull one, which computes its records in
     // its bin kernel (its "prepare" stage is the tile-info kernel).
     const bool prepare = use_bins == nullptr && m_prepare_pending && row_count != 0;
-    const StageEvents ev = BindStageEvents(prepare || (use_bins != nullptr && row_count != 0),
+    const bool fused_info = use_bins != nullptr && CullFusedInfo(row_begin, row_count, m_height, row_interleave);
+    const StageEvents ev = BindStageEvents(prepare || (use_bins != nullptr && row_count != 0 && !fused_info),
                                            use_bins != nullptr || (variant == kTraceBvh && m_n != 0));
     HipCheck(LaunchTrace(m_edges, m_n, m_vertices, m_albedo, m_frame, m_background, band, variant, use_bins, stream,
                          m_timing ? &ev : nullptr, prepare ? m_rank : nullptr, m_bvh),
@@ -447,8 +438,6 @@ hipEvent_t DeviceScene::TimingEvent(std::vector<hipEvent_t>& pool, std::size_t i
     }
     return pool[i];
 }
-
-void DeviceScene::SetSetupStream(hipStream_t setup_stream) { m_setup_stream = setup_stream; }
 
 void DeviceScene::SetTiming(bool on) {
     m_timing = on;

@@ -106,10 +106,6 @@ public:
     };
     void SetTiming(bool on);
     StageTimes TakeTimes();
-    // A stream (owned by the caller, outliving this scene's calls on it) for the setup launches of
-    // batched cull traces (TraceBatch): e.g. a higher-priority stream, so a batch's setup does not
-    // queue behind other frames' trace blocks. Null: everything on the call's stream.
-    void SetSetupStream(hipStream_t setup_stream);
 
 private:
     int m_device;
@@ -160,8 +156,6 @@ private:
     static constexpr std::size_t kOrderEvents = SRT_ORDER_EVENTS > 0 ? SRT_ORDER_EVENTS : 1;
     mutable hipEvent_t m_order_events[kOrderEvents] = {};
     mutable std::size_t m_order_next = 0;
-    hipStream_t m_setup_stream = nullptr;
-    mutable hipEvent_t m_setup_events[2] = {};
     mutable std::vector<hipEvent_t> m_prep_events;
     mutable std::vector<hipEvent_t> m_events;
     mutable std::vector<bool> m_binned;
