@@ -163,6 +163,7 @@ typedef struct srt_engine_options {
     int rows;       /* SRT_ROWS_* */
     int exchange;   /* SRT_EXCHANGE_* */
     int split;      /* SRT_SPLIT_* */
+    int simulate;   /* measurement: srtEngineCreateRank without peers, the exchange skipped (0 = off) */
 } srt_engine_options;
 
 /* 128-byte RCCL unique id for srtEngineCreateRank (call on one rank, share with the others). */

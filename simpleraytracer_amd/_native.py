@@ -73,6 +73,7 @@ class EngineOptions(ctypes.Structure):
         ("rows", ctypes.c_int),
         ("exchange", ctypes.c_int),
         ("split", ctypes.c_int),
+        ("simulate", ctypes.c_int),
     ]
 
 

@@ -317,7 +317,7 @@ FrameEngine::FrameEngine(const Scene& scene, int device, int rank, int world, co
     }
     Init(scene, std::vector<int>{device});
     try {
-        if (m_bands && m_world > 1) {
+        if (m_bands && m_world > 1 && !m_opt.simulate) {
             if (unique_id == nullptr) {
                 throw std::runtime_error("FrameEngine: a multi-rank band split needs the RCCL unique id");
             }
@@ -533,7 +533,7 @@ void FrameEngine::TracePhase(std::size_t local, std::size_t b) {
     Queue& q = d.queues[qi];
     const std::size_t F = m_opt.batch, k0 = b * F;
     const bool exchange = m_bands && m_world > 1;
-    if (exchange && q.used) {
+    if (exchange && q.used && !m_opt.simulate) {
         // This queue's send / receive buffers are free once its previous batch's exchange is done
         // (RCCL: on this device's comm stream; copies: every peer read our send buffer on its own).
         HipCheck(hipStreamWaitEvent(q.stream, q.exchanged, 0), "hipStreamWaitEvent(exchanged)");
@@ -639,7 +639,9 @@ void FrameEngine::ShadePhase(std::size_t local, std::size_t b) {
     if (n_self == 0) {
         return;
     }
-    HipCheck(hipStreamWaitEvent(q.stream, q.exchanged, 0), "hipStreamWaitEvent(exchanged)");
+    if (!m_opt.simulate) {
+        HipCheck(hipStreamWaitEvent(q.stream, q.exchanged, 0), "hipStreamWaitEvent(exchanged)");
+    }
     // The compositor's frames in slot order read evenly strided inputs (SetInputs' condition).
     const std::size_t F = m_opt.batch, k0 = b * F;
     const bool a2a = m_plan.exchange == EngineOptions::kAllToAll;
@@ -659,6 +661,10 @@ void FrameEngine::RunWorker(std::size_t local, std::size_t b0, std::size_t batch
             continue;
         }
         Queue& q = d.queues[b % m_opt.queues];
+        if (m_opt.simulate) {
+            ShadePhase(local, b);  // no peers: the exchange is skipped (measurement)
+            continue;
+        }
         if (m_copy) {
             Barrier();  // every device's trace of batch b is enqueued (its `traced` recorded)
             CopyPhase(local, b);

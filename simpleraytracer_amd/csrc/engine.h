@@ -45,6 +45,10 @@ struct EngineOptions {
     bool interleaved = true;   // bands: tile rows dealt round-robin (else contiguous blocks)
     int exchange = kAllToAll;  // bands at P > 1
     int split = kBands;
+    // Measurement only: one rank of a world-device job with no peers -- the rank's whole stream
+    // (band traces, its share of the compositing) without the exchange, which is skipped (its
+    // composited frames are then garbage). The per-rank GPU time of the multi-GPU pipeline on one GPU.
+    bool simulate = false;
 };
 
 // Row bands of an H-row frame over P devices (interleaved or contiguous), the layout every

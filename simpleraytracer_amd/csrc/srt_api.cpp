@@ -368,6 +368,7 @@ srt::EngineOptions EngineOptionsFrom(const srt_engine_options* o) {
         opt.interleaved = o->rows == SRT_ROWS_INTERLEAVED;
         opt.exchange = o->exchange;
         opt.split = o->split;
+        opt.simulate = o->simulate != 0;
     }
     return opt;
 }

@@ -31,8 +31,9 @@ def _check(rc: int):
         raise SrtError(_native.last_error())
 
 
-def _options(variant, queues, batch, rows, exchange, split):
-    return EngineOptions(TRACE_VARIANTS[variant], queues, batch, ROWS[rows], EXCHANGES[exchange], SPLITS[split])
+def _options(variant, queues, batch, rows, exchange, split, simulate=False):
+    return EngineOptions(TRACE_VARIANTS[variant], queues, batch, ROWS[rows], EXCHANGES[exchange], SPLITS[split],
+                         1 if simulate else 0)
 
 
 def unique_id() -> bytes:
@@ -65,10 +66,11 @@ class FrameEngine:
     @classmethod
     def rank(cls, path: str, width: int, height: int, device: int, rank: int, world: int, uid: bytes | None,
              variant: str = "cull", queues: int = 2, batch: int = 16, rows: str = "interleaved",
-             exchange: str = "alltoall", split: str = "bands"):
-        """This process's rank of a `world`-rank job on `device`; every rank calls it concurrently."""
+             exchange: str = "alltoall", split: str = "bands", simulate: bool = False):
+        """This process's rank of a `world`-rank job on `device`; every rank calls it concurrently.
+        simulate=True (measurement): no peers, no unique id -- the rank's stream without the exchange."""
         lib = _native.lib()
-        opt = _options(variant, queues, batch, rows, exchange, split)
+        opt = _options(variant, queues, batch, rows, exchange, split, simulate)
         idbuf = ctypes.create_string_buffer(uid, 128) if uid is not None else None
         h = lib.srtEngineCreateRank(os.fsencode(path), device, rank, world, idbuf, width, height, ctypes.byref(opt))
         if not h:
