@@ -44,11 +44,10 @@ constexpr float kQuantScale = 4096.0f;
 
 // Cull records (render.hip CullRecord): 64 B per record, at the record's rank in the scene's
 // spatial order, after the quantized boxes.
-// Shading normals (render.hip PrepareRecord): one float4 (n = e1 x e2, |n|) per triangle id,
-// after the cull records; the shade epilogue reads 16 B per hit instead of 36 B of vertices.
 // Floats per record in the edge allocation: 10 (tiles) + 4 (screen box) + 2 (quantized box)
-// + 16 (cull record) + 4 (shading normal).
-constexpr int kEdgeFloatsPerTriangle = 36;
+// + 16 (cull record). (Shading computes a hit triangle's normal from its vertices: no per-frame
+// normal buffer -- round 2 scattered one, 16 B by triangle id, in every band's record pass.)
+constexpr int kEdgeFloatsPerTriangle = 32;
 
 inline std::uint64_t PaddedTriangleCount(std::uint64_t n) {
     const std::uint64_t p = (n + kPadTriangles - 1) / kPadTriangles * kPadTriangles;
@@ -209,8 +208,8 @@ hipError_t LaunchCullFrames(const CullFrame* frames, std::size_t count, std::uin
                             const float* d_albedo, const Frame& frame, const float background[3], const unsigned* d_rank,
                             hipStream_t stream, const StageEvents* events);
 
-// Deferred shading of a band from hit ids (band.ids) and sample offsets into band.rgba, with the
-// edge buffer's shading normals of the prepared frame: bit-identical to the fused trace.
+// Deferred shading of a band from hit ids (band.ids) and sample offsets into band.rgba (normals
+// from the vertices, d_edges unused): bit-identical to the fused trace.
 // frames > 1 shades a batch whose ids are band-major, ids[band][frame][band_rows][width] (a
 // gather of `frames` frames of band_rows-row bands; band_rows 0 = one band of row_count rows),
 // into band.rgba[frame][row_count][width].

@@ -57,7 +57,6 @@ struct TraceParams {
     const uint2* __restrict__ qboxes;
     const float* __restrict__ vertices;
     const float* __restrict__ albedo;
-    const float4* __restrict__ normals;  // shading normals (PrepareRecord), by triangle id
     const float2* __restrict__ offsets;
     float4* __restrict__ out;
     int* __restrict__ out_ids;  // non-null: store the hit id per pixel (-1 = miss) instead of RGBA
@@ -107,7 +106,6 @@ struct PrepareParams {
     float4* __restrict__ screen_boxes;
     uint2* __restrict__ qboxes;
     CullRecord* __restrict__ cull;
-    float4* __restrict__ normals;  // shading normal (e1 x e2, |e1 x e2|) per triangle id
     unsigned n;
     unsigned n_pad;
     float origin[3];
@@ -324,9 +322,6 @@ __device__ __forceinline__ void PrepareRecord(const PrepareParams& p, unsigned i
     r.x = make_float4(c[8], vol, __uint_as_float(i), 0.f);
     r.sb = sb;
     p.cull[pos] = r;
-    if (real) {
-        p.normals[i] = ShadingNormal(p.vertices + 9ull * i);
-    }
 }
 
 __global__ __launch_bounds__(256) void PrepareKernel(PrepareParams p) {
@@ -465,7 +460,10 @@ __device__ __forceinline__ float4 ShadePixel(const TraceParams& p, float fx, flo
     const float dx = fmaf(fy, p.dv[0], fmaf(fx, p.du[0], p.base[0]));
     const float dy = fmaf(fy, p.dv[1], fmaf(fx, p.du[1], p.base[1]));
     const float dz = fmaf(fy, p.dv[2], fmaf(fx, p.du[2], p.base[2]));
-    const float4 nr = p.normals[id];  // (e1 x e2, |e1 x e2|) from the prepare kernel
+    // The normal from the triangle's vertices (static scene data, cache-resident): no per-frame
+    // normal buffer for the record pass to scatter (by id) and every band of a multi-GPU frame to
+    // repeat; the same expressions as always, so the same bits.
+    const float4 nr = ShadingNormal(p.vertices + 9ull * static_cast<unsigned>(id));
     const float nd = Dot3(nr.x, nr.y, nr.z, dx, dy, dz);
     const float dd = Dot3(dx, dy, dz, dx, dy, dz);
     const float cosv = fminf(fabsf(nd) / (nr.w * sqrtf(dd)), 1.f);
@@ -1551,6 +1549,10 @@ __device__ __forceinline__ int LastLoAtMost(const float2* b, int n, float v, con
 // (Gathering whole empty tiles four to a descriptor, one block storing all their misses, cut the
 // trace grid by ~950 blocks at C3 and measured no faster: an empty part's block is cheap.)
 // One block on one CU: every per-tile instruction costs the whole chip's wait, hence shifts.
+// Work-order state (BinParams::work_count, zeroed at allocation, reset by the last order block of
+// each frame): 64 per-bucket descriptor cursors, split slots handed out, order blocks arrived.
+constexpr int kOrderBuckets = 64, kOrderSlots = 64, kOrderArrived = 65;
+constexpr int kOrderWords = 72;
 constexpr unsigned kItemRegular = 1u;
 constexpr unsigned kItemFull = 2u;
 constexpr unsigned kItemEmpty = 4u;  // no candidate can hit a ray of the tile: every pixel misses
@@ -1580,6 +1582,7 @@ __device__ __forceinline__ void ItemChunks(unsigned cand, unsigned flags, unsign
 // Called by every thread of the order block; start = 64 LDS words, cnt / meta = tiles LDS
 // words / bytes, sum = 2 LDS words. (1) lengths + tile flags into LDS, the candidate total;
 // (2) the chunk size, the bucket histogram (LDS only); (3) tile info again -> descriptors.
+#ifdef SRT_ORDER_SINGLE
 constexpr int kOrderUnroll = 4;
 __device__ void BuildWorkOrder(const BinParams& p, unsigned* start, unsigned* cnt, unsigned char* meta,
                                unsigned* sum, CullRecord* lrec) {
@@ -1721,6 +1724,8 @@ __device__ void BuildWorkOrder(const BinParams& p, unsigned* start, unsigned* cn
         }
     }
 }
+
+#endif  // SRT_ORDER_SINGLE
 
 // A bin block's monotone tile-column and tile-row bounds (lo' nondecreasing, hi' nondecreasing)
 // into out[0 .. nx + ny) in LDS; `scratch` = 2 (nx + ny) LDS words; ends with a barrier.
@@ -1865,9 +1870,6 @@ __global__ __launch_bounds__(kBinThreads) void PrepareBinKernel(const PrepareBin
     }
     if (i < pp.n_pad) {
         pp.qboxes[i] = QuantizeBox(sb);
-        if (real) {
-            pp.normals[id] = ShadingNormal(v);
-        }
         bool needed = !real || p.fused != 0u || *p.range_tag == p.gen;  // fused: a full frame, every record
         if (!needed) {  // does the quantized box meet a tile row of the band (analytic row bounds)?
             // Quantisation keeps both bound sequences nondecreasing: the first row whose quantized
@@ -1979,18 +1981,19 @@ __global__ __launch_bounds__(kBinThreads) void PrepareBinKernel(const PrepareBin
     }
 }
 
-// The trace work list: one 1024-thread block after the bin kernel. Built instead by the bin
-// kernel's last block (self-resetting arrival counter, sc1 count loads) the frame has one
-// launch fewer but the ~5 us single-block tail inside the bin launch cost 10 % of the
-// three-queue throughput at C3 (60.9 vs 67.3 Grays/s; plain, no-wait and two-level arrivals
-// alike: profiles/r02/ab_order/).
+// The trace work list after the bin kernel: one 256-thread block per 256 tiles. Every block reads
+// every tile's list length and flags (8 KB of counts, 64 KB of tile info at 1080p: cheap next to
+// the serial latency of one block doing it all, ~9 us), so every block knows the frame's chunk size
+// and the whole longest-first counting sort's bucket bases without waiting for another block; each
+// then places its own tiles' descriptors through per-bucket cursors (one global atomic per block and
+// bucket), writes its share of the end marks, and the last block to arrive resets the cursors and
+// the bin counts for the frame slot's next use.
+constexpr int kOrderBlock = 256;
+#ifdef SRT_ORDER_SINGLE  // measurement builds only: round 2's single-block counting sort
 #ifndef SRT_ORDER_THREADS
 #define SRT_ORDER_THREADS 1024
 #endif
-constexpr int kOrderThreads = SRT_ORDER_THREADS;  // the work-order block (kOrderUnroll tiles per thread per
-                                                  // pass; 512 / 256 threads: 9.0 / 12.2 instead of 8.1 us)
-// LDS sized to the band (dynamic): a block that fits beside the trace blocks of other frames
-// starts sooner (a 1024-thread block with 40 KB of static LDS waited for whole CUs to drain).
+constexpr int kOrderThreads = SRT_ORDER_THREADS;
 __global__ __launch_bounds__(kOrderThreads) void WorkOrderKernel(const BinBatch batch) {
     __shared__ unsigned start[64];
     __shared__ unsigned sum[2];
@@ -2001,6 +2004,174 @@ __global__ __launch_bounds__(kOrderThreads) void WorkOrderKernel(const BinBatch 
     unsigned char* meta = reinterpret_cast<unsigned char*>(order_lds + p.tiles_x * p.tiles_y);
     BuildWorkOrder(p, start, cnt, meta, sum, lrec);
 }
+#else
+__global__ __launch_bounds__(kOrderBlock) void WorkOrderKernel(const BinBatch batch) {
+    const BinParams& p = batch.f[blockIdx.z];
+    __shared__ CullRecord lrec[kEmptyTest];
+    __shared__ unsigned hist[kOrderBuckets];   // descriptors per bucket (the frame), then bucket bases
+    __shared__ unsigned local[kOrderBuckets];  // this block's descriptors per bucket, then its global offsets
+    __shared__ unsigned sums[3];               // candidates / 16, parts; this block's split slots
+    __shared__ unsigned is_last;
+    extern __shared__ unsigned order_lds[];    // per tile: candidates, then flags | parts << 2 (bytes)
+    const int tid = threadIdx.x;
+    const int lane = tid & (kWave - 1);
+    const unsigned tiles = static_cast<unsigned>(p.tiles_x * p.tiles_y);
+    unsigned* cnt = order_lds;
+    unsigned char* meta = reinterpret_cast<unsigned char*>(order_lds + tiles);
+    if (tid < kOrderBuckets) {
+        hist[tid] = 0u;
+        local[tid] = 0u;
+    }
+    if (tid < 3) {
+        sums[tid] = 0u;
+    }
+    const unsigned large = p.counts[tiles];
+    const bool bins_invalid = p.fused != 0u && *p.range_tag == p.gen;  // MakeOrderItem: every tile FULL
+    if (tid < kEmptyTest && static_cast<unsigned>(tid) < large && large <= static_cast<unsigned>(kEmptyTest)) {
+        lrec[tid] = p.cull[p.large_list[tid]];
+    }
+    // (1) every tile's item into LDS, the frame's candidate and part totals
+    unsigned long long my_cand = 0ull;
+    unsigned my_parts = 0u;
+    constexpr int kU = 4;
+    for (unsigned t0 = tid; t0 < tiles; t0 += kU * kOrderBlock) {
+        unsigned c[kU];
+        unsigned us[kU], rg[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const unsigned t = min(t0 + u * kOrderBlock, tiles - 1u);
+            c[u] = p.counts[t];
+            us[u] = p.tile_info[t].usable;
+            rg[u] = p.tile_info[t].regular;
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const unsigned t = t0 + u * kOrderBlock;
+            if (t < tiles) {
+                TileInfo ti{};
+                ti.usable = us[u];
+                ti.regular = rg[u];
+                const OrderItem it = MakeOrderItem(p, t, c[u], large, ti, bins_invalid);
+                cnt[t] = it.cand;
+                meta[t] = static_cast<unsigned char>(it.flags | it.parts << 2);
+                my_cand += static_cast<unsigned long long>(it.parts) * it.cand;
+                my_parts += it.parts;
+            }
+        }
+    }
+    unsigned v16 = static_cast<unsigned>((my_cand + 15ull) >> 4), vp = my_parts;
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+        v16 += __shfl_xor(v16, o);
+        vp += __shfl_xor(vp, o);
+    }
+    __syncthreads();  // hist / local / sums zeroed
+    if (lane == 0) {
+        atomicAdd(&sums[0], v16);
+        atomicAdd(&sums[1], vp);
+    }
+    __syncthreads();
+    // (2) chunk size S = the power of two >= max(min_chunk, C / (D - P)), so that sum ceil(c / S)
+    // <= P + C / S <= D fits the grid; the frame's bucket histogram (longest first)
+    unsigned shift = 31u;
+    if (p.descs > sums[1]) {
+        const unsigned room = p.descs - sums[1];
+        const unsigned long long want = (16ull * sums[0] + room - 1ull) / room;
+        const unsigned long long size = want > p.min_chunk ? want : p.min_chunk;
+        shift = size >= (1ull << 31) ? 31u : 64u - static_cast<unsigned>(__builtin_clzll(size - 1ull));
+        shift = size <= 1ull ? 0u : shift;
+    }
+    const unsigned mine = blockIdx.x * kOrderBlock + static_cast<unsigned>(tid);  // this thread's own tile
+    unsigned my_n = 0u, my_nch = 1u, my_bucket = 0u, my_at = 0u;
+    for (unsigned t = tid; t < tiles; t += kOrderBlock) {
+        const unsigned parts = meta[t] >> 2;
+        if (parts != 0u) {
+            unsigned nch, bucket;
+            ItemChunks(cnt[t], meta[t] & 3u, shift, nch, bucket);
+            atomicAdd(&hist[bucket], parts * nch);
+            if (t == mine) {
+                my_n = parts * nch;
+                my_nch = nch;
+                my_bucket = bucket;
+                my_at = atomicAdd(&local[bucket], my_n);  // offset inside this block's share of the bucket
+            }
+        }
+    }
+    unsigned my_slot = 0u;
+    if (my_nch > 1u) {
+        my_slot = atomicAdd(&sums[2], my_n);
+    }
+    __syncthreads();
+    unsigned used = 0u;
+    if (tid < kWave) {  // bucket b's first descriptor: those of the heavier buckets (suffix sum, exclusive)
+        const unsigned c = hist[lane];
+        unsigned suf = c;
+#pragma unroll
+        for (int o = 1; o < kWave; o <<= 1) {
+            const unsigned u = __shfl_down(suf, o);
+            suf += lane + o < kWave ? u : 0u;
+        }
+        used = __shfl(suf, 0);
+        hist[lane] = suf - c;
+        // this block's share of bucket `lane`: one global atomic per nonempty bucket
+        local[lane] = local[lane] != 0u ? atomicAdd(&p.work_count[lane], local[lane]) : 0u;
+        if (lane == 0) {
+            sums[2] = sums[2] != 0u ? atomicAdd(&p.work_count[kOrderSlots], sums[2]) : 0u;
+            sums[0] = used;
+        }
+    }
+    __syncthreads();
+    used = sums[0];
+    // (3) this block's tiles' descriptors
+    if (my_n != 0u) {
+        const unsigned t = mine;
+        const TileInfo ti = p.tile_info[t];
+        const unsigned at = hist[my_bucket] + local[my_bucket] + my_at;
+        const unsigned slot = my_nch > 1u ? sums[2] + my_slot : 0u;
+        const unsigned flags = meta[t] & 3u, cand = cnt[t], parts = meta[t] >> 2;
+        const unsigned list_len = (flags & kItemFull) ? 0u : cand - large;
+        unsigned out_flags = flags;
+        if ((flags & kItemFull) == 0u && list_len == 0u && large <= static_cast<unsigned>(kEmptyTest)) {
+            const Box tb{ti.box.x, ti.box.y, ti.box.z, ti.box.w};
+            bool may = false;
+            for (unsigned k = 0; k < large; ++k) {
+                const CullRecord& r = lrec[k];
+                const Record q{r.a.x, r.a.y, r.a.z, r.a.w, r.b.x, r.b.y, r.b.z, r.b.w, r.x.x};
+                may = may || (ScreenBoxOverlaps(tb, r.sb) && BoxMayHit(tb, q));
+            }
+            out_flags |= may ? 0u : kItemEmpty;
+        }
+        for (unsigned part = 0; part < parts; ++part) {
+            for (unsigned ch = 0; ch < my_nch; ++ch) {
+                const unsigned d = at + part * my_nch + ch;
+                p.work[2 * d] = make_uint4(t * kParts + part, cand, list_len, out_flags);
+                p.work[2 * d + 1] = make_uint4(__float_as_uint(ti.ox), __float_as_uint(ti.oy), ch | my_nch << 16,
+                                               slot + part * my_nch);
+            }
+        }
+    }
+    // descriptors past the list: end marks (every block a share; a trace block reads nothing first)
+    for (unsigned d = used + blockIdx.x * kOrderBlock + static_cast<unsigned>(tid); d < p.descs;
+         d += gridDim.x * kOrderBlock) {
+        p.work[2 * d] = make_uint4(kWorkEnd, 0u, 0u, 0u);
+    }
+    // the last block to arrive resets the cursors and the bin counts (every block has read them)
+    __syncthreads();
+    if (tid == 0) {
+        __threadfence();
+        is_last = atomicAdd(&p.work_count[kOrderArrived], 1u) == gridDim.x - 1u ? 1u : 0u;
+    }
+    __syncthreads();
+    if (is_last != 0u) {
+        for (unsigned t = tid; t <= tiles; t += kOrderBlock) {
+            p.counts[t] = 0u;
+        }
+        if (tid < kOrderWords) {
+            p.work_count[tid] = 0u;
+        }
+    }
+}
+#endif
 
 std::size_t OrderLdsBytes(int tiles) { return static_cast<std::size_t>(tiles) * 5 + 16; }
 
@@ -2655,7 +2826,6 @@ struct EdgeLayout {
     float4* screen_boxes;
     uint2* qboxes;
     CullRecord* cull;
-    float4* normals;
 };
 EdgeLayout EdgeBuffers(const float* d_edges, std::uint64_t n) {
     EdgeLayout e;
@@ -2664,7 +2834,6 @@ EdgeLayout EdgeBuffers(const float* d_edges, std::uint64_t n) {
     e.screen_boxes = e.tiles + n_pad / kTileTriangles * kTileFloat4;
     e.qboxes = reinterpret_cast<uint2*>(e.screen_boxes + n_pad);
     e.cull = reinterpret_cast<CullRecord*>(e.qboxes + n_pad);
-    e.normals = reinterpret_cast<float4*>(e.cull + n_pad);
     return e;
 }
 }  // namespace
@@ -2680,7 +2849,6 @@ PrepareParams MakePrepareParams(const float* d_vertices, const unsigned* d_rank,
     p.screen_boxes = e.screen_boxes;
     p.qboxes = e.qboxes;
     p.cull = e.cull;
-    p.normals = e.normals;
     p.n = static_cast<unsigned>(n);
     p.n_pad = static_cast<unsigned>(PaddedTriangleCount(n));
     for (int k = 0; k < 3; ++k) {
@@ -2814,7 +2982,7 @@ BinSizes CullBinSizes(std::uint64_t n, std::size_t width, std::size_t row_count)
     z.lists = al(tiles * static_cast<std::size_t>(CullBinCapacity(n, tiles)) * 4);
     z.large = al(PaddedTriangleCount(n) * 4);
     z.work = al(descs * 2 * sizeof(uint4));
-    z.work_count = al(4);
+    z.work_count = al(kOrderWords * 4);
     z.arrive = split ? al(descs * 4) : 0;
     z.split_keys = split ? al(descs * kBlockRows * kWave * 8) : 0;
     z.range_tag = al(4);
@@ -2879,7 +3047,6 @@ TraceParams MakeTraceParams(const float* d_edges, std::uint64_t n, const float* 
     p.screen_boxes = e.screen_boxes;
     p.qboxes = e.qboxes;
     p.cull = e.cull;
-    p.normals = e.normals;
     p.vertices = d_vertices;
     p.albedo = d_albedo;
     p.offsets = reinterpret_cast<const float2*>(band.offsets);
@@ -3007,8 +3174,13 @@ hipError_t LaunchCullFrames(const CullFrame* frames, std::size_t count, std::uin
     }
     LaunchLds(PrepareBinKernel, dim3(blocks, 1, z), dim3(kBinThreads),
               BinLdsBytes(static_cast<int>(gx), static_cast<int>(gy)), stream, ev.bin_begin, nullptr, pb);
+#ifdef SRT_ORDER_SINGLE
     LaunchLds(WorkOrderKernel, dim3(1, 1, z), dim3(kOrderThreads), OrderLdsBytes(static_cast<int>(gx * gy)), stream,
               nullptr, ev.bin_end, bb);
+#else
+    LaunchLds(WorkOrderKernel, dim3((gx * gy + kOrderBlock - 1) / kOrderBlock, 1, z), dim3(kOrderBlock),
+              OrderLdsBytes(static_cast<int>(gx * gy)), stream, nullptr, ev.bin_end, bb);
+#endif
     Launch(TraceCullKernel, dim3(frames[0].bins->descs, 1, z), dim3(kWave * kCullWaves), stream, ev.begin, ev.end, tb);
     return hipGetLastError();
 }
@@ -3122,9 +3294,9 @@ hipError_t LaunchShade(const float* d_vertices, const float* d_albedo, const flo
         return hipErrorInvalidValue;
     }
     TraceParams p{};
-    p.normals = EdgeBuffers(d_edges, n).normals;
+    (void)d_edges;
     p.n = static_cast<unsigned>(n);
-    (void)d_vertices;
+    p.vertices = d_vertices;
     p.albedo = d_albedo;
     p.offsets = reinterpret_cast<const float2*>(band.offsets);
     p.out = reinterpret_cast<float4*>(band.rgba);

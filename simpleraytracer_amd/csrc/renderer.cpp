@@ -191,7 +191,6 @@ void DeviceScene::Prepare(std::size_t width, std::size_t height, hipStream_t str
     // computes the records inside its bin kernel on every call, render.hip PrepareBinKernel).
     (void)stream;
     m_prepare_pending = true;
-    m_normals_current = false;
 }
 
 void DeviceScene::OrderAfterPrevious(hipStream_t stream) const {
@@ -230,16 +229,6 @@ void DeviceScene::RecordOrder(hipStream_t stream) const {
 #endif
 }
 
-// The shading normals of the prepared frame, when no trace has written them yet (a Shade first):
-// the full record pass.
-void DeviceScene::NormalsIfStale(hipStream_t stream) const {
-    if (!m_normals_current) {
-        HipCheck(LaunchPrepare(m_vertices, m_rank, m_n, m_frame, m_edges, stream), "prepare kernel launch");
-        m_prepare_pending = false;
-        m_normals_current = true;
-    }
-}
-
 void DeviceScene::Shade(const float* d_offsets, const int* d_ids, float* d_rgba, std::size_t row_begin,
                         std::size_t row_count, hipStream_t stream, std::size_t frames, std::size_t band_rows,
                         std::size_t interleaved, std::size_t offsets_stride) const {
@@ -259,7 +248,6 @@ void DeviceScene::Shade(const float* d_offsets, const int* d_ids, float* d_rgba,
         return;
     }
     OrderAfterPrevious(stream);
-    NormalsIfStale(stream);
     BandArgs band{d_offsets, d_rgba, m_width, m_height, row_begin, row_count, const_cast<int*>(d_ids)};
     HipCheck(LaunchShade(m_vertices, m_albedo, m_edges, m_n, m_frame, m_background, band, stream, frames, band_rows,
                          interleaved, offsets_stride),
@@ -316,7 +304,6 @@ void DeviceScene::EnsureEdgeSlots(std::size_t slots, hipStream_t stream) const {
     m_edges = grown;
     m_edge_slots = slots;
     m_prepare_pending = true;
-    m_normals_current = false;
 }
 
 void DeviceScene::TraceBatch(const float* const* d_offsets, float* const* d_rgba, int* const* d_ids, std::size_t frames,
@@ -363,7 +350,6 @@ void DeviceScene::TraceBatch(const float* const* d_offsets, float* const* d_rgba
     HipCheck(LaunchCullFrames(cf, frames, m_n, m_vertices, m_albedo, m_frame, m_background, m_rank, stream,
                               m_timing ? &ev : nullptr),
              "batched trace launch");
-    m_normals_current = true;  // slot 0's normals (the tile-planar records are the full pass's)
     RecordOrder(stream);
 }
 
@@ -398,10 +384,6 @@ void DeviceScene::Trace(const float* d_offsets, float* d_rgba, std::size_t row_b
              "trace kernel launch");
     if (prepare) {
         m_prepare_pending = false;
-        m_normals_current = true;
-    }
-    if (use_bins != nullptr && row_count != 0) {
-        m_normals_current = true;
     }
     RecordOrder(stream);
 }

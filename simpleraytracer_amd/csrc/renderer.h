@@ -147,7 +147,6 @@ private:
     // are shared state, so a call on another stream than the previous one first waits for it.
     void OrderAfterPrevious(hipStream_t stream) const;
     void RecordOrder(hipStream_t stream) const;
-    void NormalsIfStale(hipStream_t stream) const;
     mutable hipStream_t m_last_stream = nullptr;
     mutable bool m_used = false;
 #ifndef SRT_ORDER_EVENTS
@@ -161,7 +160,6 @@ private:
     mutable std::vector<bool> m_binned;
     mutable std::size_t m_prep_timed = 0;
     mutable bool m_prepare_pending = false;  // the full record pass has not run for the prepared frame
-    mutable bool m_normals_current = false;  // slot 0's shading normals written since the last Prepare
     mutable std::size_t m_timed = 0;
 };
 
