@@ -84,3 +84,25 @@ ref:
 clean:
 	rm -rf build bin $(LIBDIR) $(dir $(DIAG_LIB)) simpleraytracer_amd/lib_exp
 	$(MAKE) -C oracle clean
+
+# A/B builds of the whole library (measurement only): make ab AB_NAME=x AB_FLAGS="-DSRT_...=..." ->
+# simpleraytracer_amd/lib_ab/x/libModelRunner.so (every object compiled with the flags; SRT_LIB).
+AB_NAME  ?= default
+AB_FLAGS ?=
+AB_BUILD := build/ab/$(AB_NAME)
+AB_LIB   := simpleraytracer_amd/lib_ab/$(AB_NAME)/libModelRunner.so
+AB_OBJS  := $(patsubst $(BUILD)/%,$(AB_BUILD)/%,$(OBJS))
+$(AB_BUILD)/%.o: $(CSRC)/%.hip $(HEADERS)
+	@mkdir -p $(AB_BUILD)
+	$(HIPCC) $(HIPFLAGS) $(AB_FLAGS) -c $< -o $@
+$(AB_BUILD)/cpu_render.o: $(CSRC)/cpu_render.cpp $(HEADERS)
+	@mkdir -p $(AB_BUILD)
+	$(HIPCC) $(HIPFLAGS) $(AB_FLAGS) -mfma -c $< -o $@
+$(AB_BUILD)/%.o: $(CSRC)/%.cpp $(HEADERS)
+	@mkdir -p $(AB_BUILD)
+	$(HIPCC) $(HIPFLAGS) $(AB_FLAGS) -c $< -o $@
+$(AB_LIB): $(AB_OBJS)
+	@mkdir -p $(dir $(AB_LIB))
+	$(HIPCC) --offload-arch=$(ARCH) $(AB_OBJS) -o $@ $(LDFLAGS)
+.PHONY: ab
+ab: $(AB_LIB)

@@ -80,6 +80,8 @@ def parse():
                    help="batches in flight per GPU (own scene buffers and HIP stream each)")
     p.add_argument("--offsets", default="uniform", choices=["uniform", "random"],
                    help="sample offsets: uniform 0.5 (headline) or seeded U[0,1) per-pixel jitter")
+    p.add_argument("--launch", type=int, default=0,
+                   help="frames per trace launch (0: the library's default, env SRT_LAUNCH_FRAMES)")
     p.add_argument("--inputs", type=int, default=1, help="distinct resident input images frames cycle through")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample length")
     p.add_argument("--brute-steps", type=int, default=5, help="timed frames of the brute-force LDS kernel (0 = skip)")
@@ -160,7 +162,7 @@ class Job:
         from simpleraytracer_amd.engine import FrameEngine, unique_id
 
         kw = dict(variant=variant or a.variant, queues=queues or a.queues, batch=batch or a.frames_per_step,
-                  rows=rows or a.rows, exchange=exchange or a.exchange, split=mode or a.mode)
+                  rows=rows or a.rows, exchange=exchange or a.exchange, split=mode or a.mode, launch=a.launch)
         w, h = width or a.width, height or a.height
         if not self.ranked:
             return FrameEngine(path, w, h, devices=self.devices, **kw)
@@ -523,6 +525,10 @@ def main():
                 "trace_variant": a.variant,
                 "frames_per_step": a.frames_per_step,
                 "frame_queues": a.queues,
+                # engine.h EngineOptions::launch defaults when neither --launch nor SRT_LAUNCH_FRAMES is set
+                "frames_per_launch": min(a.launch or int(os.environ.get("SRT_LAUNCH_FRAMES") or
+                                                         (64 if world > 1 and a.mode == "bands" else 8)),
+                                         a.frames_per_step, 256),
                 "inputs": max(1, a.inputs),
                 "offsets": a.offsets,
             },

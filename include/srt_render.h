@@ -164,6 +164,8 @@ typedef struct srt_engine_options {
     int exchange;   /* SRT_EXCHANGE_* */
     int split;      /* SRT_SPLIT_* */
     int simulate;   /* measurement: srtEngineCreateRank without peers, the exchange skipped (0 = off) */
+    size_t launch;  /* frames per trace launch, <= 256 (0 = env SRT_LAUNCH_FRAMES, else 8 for whole
+                       frames, 64 for bands over more than one device) */
 } srt_engine_options;
 
 /* 128-byte RCCL unique id for srtEngineCreateRank (call on one rank, share with the others). */

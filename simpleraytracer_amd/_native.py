@@ -74,6 +74,7 @@ class EngineOptions(ctypes.Structure):
         ("exchange", ctypes.c_int),
         ("split", ctypes.c_int),
         ("simulate", ctypes.c_int),
+        ("launch", ctypes.c_size_t),
     ]
 
 

@@ -356,6 +356,13 @@ void FrameEngine::Init(const Scene& scene, const std::vector<int>& devices) {
         (m_opt.split != EngineOptions::kBands && m_opt.split != EngineOptions::kFrames)) {
         throw std::runtime_error("FrameEngine: unknown exchange or split");
     }
+    if (m_opt.launch == 0) {
+        const char* v = std::getenv("SRT_LAUNCH_FRAMES");
+        const long l = v == nullptr || *v == '\0' ? 0 : std::strtol(v, nullptr, 10);
+        const bool bands = m_opt.split == EngineOptions::kBands && m_world > 1;
+        m_opt.launch = l > 0 ? static_cast<std::size_t>(l) : bands ? kDefaultBandLaunch : kMaxBatch;
+    }
+    m_opt.launch = std::min({m_opt.launch, m_opt.batch, static_cast<std::size_t>(kMaxTableFrames)});
     m_bands = m_opt.split == EngineOptions::kBands;
     m_split = BandSplit::Make(m_height, m_bands ? m_world : 1, m_opt.interleaved);
     m_plan.bands = m_split.bands;
@@ -548,18 +555,19 @@ void FrameEngine::TracePhase(std::size_t local, std::size_t b) {
     }
     q.used = true;
     q.last_batch = b;
-    const float* offs[kMaxBatch];
-    float* rgba[kMaxBatch];
-    int* ids[kMaxBatch];
+    const std::size_t L = m_opt.launch;
+    std::vector<const float*> offs(L);
+    std::vector<float*> rgba(L);
+    std::vector<int*> ids(L);
     const std::size_t frame_floats4 = m_width * m_height * 4;
     if (!exchange) {  // whole frames, traced and shaded in one kernel
-        for (std::size_t f0 = 0; f0 < F; f0 += kMaxBatch) {
-            const std::size_t n = std::min<std::size_t>(kMaxBatch, F - f0);
+        for (std::size_t f0 = 0; f0 < F; f0 += L) {
+            const std::size_t n = std::min(L, F - f0);
             for (std::size_t j = 0; j < n; ++j) {
                 offs[j] = FullInput(local, k0 + f0 + j);
                 rgba[j] = q.rgba + (f0 + j) * frame_floats4;
             }
-            q.scene->TraceBatch(offs, rgba, nullptr, n, 0, m_height, m_opt.variant, q.stream, 1);
+            q.scene->TraceBatch(offs.data(), rgba.data(), nullptr, n, 0, m_height, m_opt.variant, q.stream, 1);
         }
         return;
     }
@@ -567,8 +575,8 @@ void FrameEngine::TracePhase(std::size_t local, std::size_t b) {
     const std::size_t self = d.band;
     const std::size_t n_self = m_plan.FramesFor(b, self);
     if (d.rows != 0) {
-        for (std::size_t f0 = 0; f0 < F; f0 += kMaxBatch) {
-            const std::size_t n = std::min<std::size_t>(kMaxBatch, F - f0);
+        for (std::size_t f0 = 0; f0 < F; f0 += L) {
+            const std::size_t n = std::min(L, F - f0);
             for (std::size_t j = 0; j < n; ++j) {
                 const std::size_t f = f0 + j;
                 const std::size_t c = m_plan.Compositor(b, f), slot = m_plan.Slot(f);
@@ -576,7 +584,7 @@ void FrameEngine::TracePhase(std::size_t local, std::size_t b) {
                 ids[j] = c == self ? q.recv + (self * n_self + slot) * band_pixels
                                    : q.send + SendPixels(m_plan, c, slot, band_pixels);
             }
-            q.scene->TraceBatch(offs, nullptr, ids, n, d.row_begin, d.rows, m_opt.variant, q.stream,
+            q.scene->TraceBatch(offs.data(), nullptr, ids.data(), n, d.row_begin, d.rows, m_opt.variant, q.stream,
                                 m_split.Interleave());
         }
     }

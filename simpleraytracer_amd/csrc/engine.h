@@ -49,6 +49,13 @@ struct EngineOptions {
     // (band traces, its share of the compositing) without the exchange, which is skipped (its
     // composited frames are then garbage). The per-rank GPU time of the multi-GPU pipeline on one GPU.
     bool simulate = false;
+    // Frames per trace launch (a batch is traced in ceil(batch / launch) launch sets of four
+    // kernels; more than render.h kMaxBatch frames take their parameters from a device table).
+    // 0: env SRT_LAUNCH_FRAMES, else the default: kMaxBatch for whole frames (larger launches of
+    // full frames measured slower: C3 114.4 / 107.0 / 101.9 / 105.1 Grays/s at 8 / 16 / 32 / 64),
+    // FrameEngine::kDefaultBandLaunch for bands at P > 1 (per-rank time at P = 8: 6.05 / 5.81 /
+    // 5.84 / 5.66 us per frame).
+    std::size_t launch = 0;
 };
 
 // Row bands of an H-row frame over P devices (interleaved or contiguous), the layout every
@@ -94,6 +101,7 @@ public:
     FrameEngine& operator=(const FrameEngine&) = delete;
 
     static void UniqueId(void* out128);
+    static constexpr std::size_t kDefaultBandLaunch = 64;
 
     // `count` full-frame sample-offset images (count x H x W x 2 floats, host), resident on every
     // local device from now on (each device keeps the frames and its band's rows of each); frame k

@@ -108,7 +108,7 @@ constexpr int kCullTileRows = SRT_TILE_ROWS;
 inline std::size_t BandFrameRow(std::size_t row_begin, std::size_t interleave, std::size_t local) {
     return row_begin + local + local / kCullTileRows * kCullTileRows * (interleave - 1);
 }
-constexpr int kMaxBatch = 8;          // frames of one batched cull launch (LaunchCullFrames)
+constexpr int kMaxBatch = 8;          // frames of a batched cull launch with its parameters as kernel arguments
 constexpr int kMaxBoundTiles = 2048;  // binning needs tiles_x + tiles_y <= this
 constexpr int kMaxBinTiles = 8192;    // and tiles_x * tiles_y <= this (bin kernel LDS histogram)
 
@@ -199,14 +199,28 @@ struct CullFrame {
     const CullBins* bins;
     BandArgs band;
 };
-// The cull pipeline for `count` (<= kMaxBatch) frames of one camera in four launches (tile info;
-// record setup + bins; work lists; trace), block z of each working on frame z: the same per-frame
-// work as `count` single-frame calls, with a quarter of the launches per frame. The records are
-// computed in the bin launch every call (bins->order: position -> id; d_rank unused). Events
-// (optional): prep = tile info, bin = record setup + bins + work list, trace.
+// Frames of one launch whose parameters travel in a device table instead of the kernel
+// arguments (count > kMaxBatch): `device` and `host` (page-locked) of CullTableBytes(frames) bytes
+// each, caller-owned. LaunchCullFrames fills `host` and copies it to `device` on the stream; the
+// caller must not rewrite `host` before that copy has executed (an event after the call), and the
+// stream order keeps the device copy alive for the launches that read it.
+constexpr int kMaxTableFrames = 256;
+struct CullTable {
+    void* device;
+    void* host;
+    std::size_t frames;  // capacity
+};
+std::size_t CullTableBytes(std::size_t frames);
+
+// The cull pipeline for `count` frames of one camera in four launches (tile info; record setup +
+// bins; work lists; trace), block z of each working on frame z: the same per-frame work as
+// `count` single-frame calls, with four launches per call. Up to kMaxBatch frames carry their
+// parameters as kernel arguments; up to kMaxTableFrames through `table` (required then). The
+// records are computed in the bin launch every call (bins->order: position -> id; d_rank unused).
+// Events (optional): prep = tile info, bin = record setup + bins + work list, trace.
 hipError_t LaunchCullFrames(const CullFrame* frames, std::size_t count, std::uint64_t n, const float* d_vertices,
                             const float* d_albedo, const Frame& frame, const float background[3], const unsigned* d_rank,
-                            hipStream_t stream, const StageEvents* events);
+                            hipStream_t stream, const StageEvents* events, const CullTable* table = nullptr);
 
 // Deferred shading of a band from hit ids (band.ids) and sample offsets into band.rgba (normals
 // from the vertices, d_edges unused): bit-identical to the fused trace.

@@ -91,11 +91,25 @@ struct TraceParams {
     float bg[3];
 };
 
-// Frames of one batched launch (render.h kMaxBatch): block (x, y, z) works on frame z, reading
-// its parameters from the kernel-argument segment (uniform loads).
-struct TraceBatch {
-    TraceParams f[kMaxBatch];
+// Frames of one batched launch: block (x, y, z) works on frame z. Up to kMaxBatch frames carry
+// their parameters in the kernel-argument segment (FrameArgs); larger launches (up to
+// kMaxTableFrames) read them from a device table the host uploads once per launch (FrameTable),
+// through a constant-address-space pointer, so they compile to the same uniform scalar loads as
+// kernel arguments (loads the compiler may treat as invariant and hoist).
+template <class T>
+using ConstantPtr = const __attribute__((address_space(4))) T*;
+template <class T>
+struct FrameArgs {
+    T f[kMaxBatch];
+    __device__ __forceinline__ const T& operator[](unsigned z) const { return f[z]; }
 };
+template <class T>
+struct FrameTable {
+    ConstantPtr<T> f;
+    __device__ __forceinline__ const T& operator[](unsigned z) const { return *(const T*)(f + z); }
+};
+using TraceBatch = FrameArgs<TraceParams>;
+using TraceTable = FrameTable<TraceParams>;
 
 struct PrepareParams {
     const float* __restrict__ vertices;
@@ -1492,12 +1506,12 @@ __device__ __forceinline__ void TileInfoBlock(const BinParams& p, int bx, int by
     }
 }
 
-struct BinBatch {
-    BinParams f[kMaxBatch];
-};
+using BinBatch = FrameArgs<BinParams>;
+using BinTable = FrameTable<BinParams>;
 
-__global__ __launch_bounds__(kBinThreads) void TileInfoKernel(const BinBatch batch) {
-    TileInfoBlock(batch.f[blockIdx.z], blockIdx.x, blockIdx.y);
+template <class Frames>
+__global__ __launch_bounds__(kBinThreads) void TileInfoKernel(const Frames batch) {
+    TileInfoBlock(batch[blockIdx.z], blockIdx.x, blockIdx.y);
 }
 
 // Searches in a bin block's monotone tile bounds b[0..n) (lo' = .x, hi' = .y, both
@@ -1825,16 +1839,16 @@ struct PrepareBinParams {
     PrepareParams prep;
     BinParams bin;
 };
-struct PrepareBinBatch {
-    PrepareBinParams f[kMaxBatch];
-};
+using PrepareBinBatch = FrameArgs<PrepareBinParams>;
+using PrepareBinTable = FrameTable<PrepareBinParams>;
 #ifndef SRT_BIN_AHEAD
 #define SRT_BIN_AHEAD 4
 #endif
 constexpr int kBinAhead = SRT_BIN_AHEAD;  // tile boxes a bin thread loads at once
-__global__ __launch_bounds__(kBinThreads) void PrepareBinKernel(const PrepareBinBatch batch) {
+template <class Frames>
+__global__ __launch_bounds__(kBinThreads) void PrepareBinKernel(const Frames batch) {
     extern __shared__ float2 bin_lds[];
-    const PrepareBinParams& pb = batch.f[blockIdx.z];
+    const PrepareBinParams& pb = batch[blockIdx.z];
     const BinParams& p = pb.bin;
     const PrepareParams& pp = pb.prep;
     if (p.fused != 0u) {  // the blocks past the record blocks compute the tile info (CullFusedInfo)
@@ -1994,19 +2008,21 @@ constexpr int kOrderBlock = 256;
 #define SRT_ORDER_THREADS 1024
 #endif
 constexpr int kOrderThreads = SRT_ORDER_THREADS;
-__global__ __launch_bounds__(kOrderThreads) void WorkOrderKernel(const BinBatch batch) {
+template <class Frames>
+__global__ __launch_bounds__(kOrderThreads) void WorkOrderKernel(const Frames batch) {
     __shared__ unsigned start[64];
     __shared__ unsigned sum[2];
     __shared__ CullRecord lrec[kEmptyTest];
     extern __shared__ unsigned order_lds[];
-    const BinParams& p = batch.f[blockIdx.z];
+    const BinParams& p = batch[blockIdx.z];
     unsigned* cnt = order_lds;
     unsigned char* meta = reinterpret_cast<unsigned char*>(order_lds + p.tiles_x * p.tiles_y);
     BuildWorkOrder(p, start, cnt, meta, sum, lrec);
 }
 #else
-__global__ __launch_bounds__(kOrderBlock) void WorkOrderKernel(const BinBatch batch) {
-    const BinParams& p = batch.f[blockIdx.z];
+template <class Frames>
+__global__ __launch_bounds__(kOrderBlock) void WorkOrderKernel(const Frames batch) {
+    const BinParams& p = batch[blockIdx.z];
     __shared__ CullRecord lrec[kEmptyTest];
     __shared__ unsigned hist[kOrderBuckets];   // descriptors per bucket (the frame), then bucket bases
     __shared__ unsigned local[kOrderBuckets];  // this block's descriptors per bucket, then its global offsets
@@ -2178,9 +2194,16 @@ std::size_t OrderLdsBytes(int tiles) { return static_cast<std::size_t>(tiles) * 
 #ifndef SRT_TRACE_OCC
 #define SRT_TRACE_OCC 6
 #endif
+#ifndef SRT_TRACE_PRIO
+#define SRT_TRACE_PRIO 0
+#endif
+#ifndef SRT_TRACE_PRIO_HEAVY
+#define SRT_TRACE_PRIO_HEAVY 256
+#endif
 
-__global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(const TraceBatch batch) {
-    const TraceParams& p = batch.f[blockIdx.z];
+template <class Frames>
+__global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(const Frames batch) {
+    const TraceParams& p = batch[blockIdx.z];
     constexpr int R = kCullR;
     __shared__ CullShared sh;
 #ifdef SRT_EXP_SETUP_ONLY  // measurement builds only (make exp): the frame's setup without its trace
@@ -2237,6 +2260,15 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(c
             src.count1 = w0.z;
             src.begin = chunk * q + chunk * r / nchunks;
             src.end = (chunk + 1u) * q + (chunk + 1u) * r / nchunks;
+#if SRT_TRACE_PRIO
+            // the frame's critical path: heavy chunks' waves issue first on a shared SIMD
+            const unsigned work = src.end - src.begin;
+            if (work >= SRT_TRACE_PRIO_HEAVY) {
+                __builtin_amdgcn_s_setprio(2);
+            } else if (work >= SRT_TRACE_PRIO_HEAVY / 4) {
+                __builtin_amdgcn_s_setprio(1);
+            }
+#endif
         }
     } else {
         item = blockIdx.y * gridDim.x + blockIdx.x;
@@ -2953,7 +2985,7 @@ unsigned TraceSlots() {
     int dev = 0;
     if (hipGetDevice(&dev) == hipSuccess && dev != cached_device) {
         int per_cu = 0, cus = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, TraceCullKernel, kCullThreads, 0) == hipSuccess &&
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, TraceCullKernel<TraceBatch>, kCullThreads, 0) == hipSuccess &&
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess) {
             slots = static_cast<unsigned>(per_cu * cus);
             cached_device = dev;
@@ -3117,10 +3149,52 @@ BinParams BindBins(TraceParams& p, const CullBins& bins, std::uint64_t n) {
 }
 }  // namespace
 
+namespace {
+// The four stage launches of a batched cull frame set; TB / BB / PB: the frames' parameters as
+// kernel arguments (FrameArgs) or a device table (FrameTable).
+template <class TB, class BB, class PB>
+void LaunchCullStages(const TB& tb, const BB& bb, const PB& pb, unsigned z, unsigned gx, unsigned gy, unsigned blocks,
+                      bool fused, unsigned descs, hipStream_t stream, const StageEvents& ev) {
+    if (!fused) {
+        Launch(TileInfoKernel<BB>, dim3(gx, (gy + kInfoTiles - 1) / kInfoTiles, z), dim3(kBinThreads), stream,
+               ev.prep_begin, ev.prep_end, bb);
+    }
+    LaunchLds(PrepareBinKernel<PB>, dim3(blocks, 1, z), dim3(kBinThreads),
+              BinLdsBytes(static_cast<int>(gx), static_cast<int>(gy)), stream, ev.bin_begin, nullptr, pb);
+#ifdef SRT_ORDER_SINGLE
+    LaunchLds(WorkOrderKernel<BB>, dim3(1, 1, z), dim3(kOrderThreads), OrderLdsBytes(static_cast<int>(gx * gy)),
+              stream, nullptr, ev.bin_end, bb);
+#else
+    LaunchLds(WorkOrderKernel<BB>, dim3((gx * gy + kOrderBlock - 1) / kOrderBlock, 1, z), dim3(kOrderBlock),
+              OrderLdsBytes(static_cast<int>(gx * gy)), stream, nullptr, ev.bin_end, bb);
+#endif
+    Launch(TraceCullKernel<TB>, dim3(descs, 1, z), dim3(kWave * kCullWaves), stream, ev.begin, ev.end, tb);
+}
+
+// Layout of a parameter table (CullTableBytes): PrepareBinParams, BinParams, TraceParams arrays.
+struct TableLayout {
+    std::size_t prep, bin, trace, bytes;
+};
+TableLayout MakeTableLayout(std::size_t frames) {
+    const auto al = [](std::size_t b) { return (b + 255) / 256 * 256; };
+    TableLayout t;
+    t.prep = 0;
+    t.bin = al(frames * sizeof(PrepareBinParams));
+    t.trace = t.bin + al(frames * sizeof(BinParams));
+    t.bytes = t.trace + al(frames * sizeof(TraceParams));
+    return t;
+}
+}  // namespace
+
+std::size_t CullTableBytes(std::size_t frames) { return MakeTableLayout(frames).bytes; }
+
 hipError_t LaunchCullFrames(const CullFrame* frames, std::size_t count, std::uint64_t n, const float* d_vertices,
                             const float* d_albedo, const Frame& frame, const float background[3], const unsigned* d_rank,
-                            hipStream_t stream, const StageEvents* events) {
-    if (frames == nullptr || count == 0 || count > static_cast<std::size_t>(kMaxBatch)) {
+                            hipStream_t stream, const StageEvents* events, const CullTable* table) {
+    const bool use_table = count > static_cast<std::size_t>(kMaxBatch);
+    if (frames == nullptr || count == 0 || count > static_cast<std::size_t>(kMaxTableFrames) ||
+        (use_table && (table == nullptr || table->device == nullptr || table->host == nullptr ||
+                       count > table->frames))) {
         return hipErrorInvalidValue;
     }
     const BandArgs& band0 = frames[0].band;
@@ -3134,6 +3208,12 @@ hipError_t LaunchCullFrames(const CullFrame* frames, std::size_t count, std::uin
     TraceBatch tb{};
     BinBatch bb{};
     PrepareBinBatch pb{};
+    const TableLayout lay = MakeTableLayout(count);
+    unsigned char* host = use_table ? static_cast<unsigned char*>(table->host) : nullptr;
+    PrepareBinParams* pp = use_table ? reinterpret_cast<PrepareBinParams*>(host + lay.prep) : pb.f;
+    BinParams* bp = use_table ? reinterpret_cast<BinParams*>(host + lay.bin) : bb.f;
+    TraceParams* tp = use_table ? reinterpret_cast<TraceParams*>(host + lay.trace) : tb.f;
+    const bool fused = CullFusedInfo(band0.row_begin, band0.row_count, band0.height, band0.row_interleave);
     for (std::size_t i = 0; i < count; ++i) {
         const CullFrame& f = frames[i];
         if (f.bins == nullptr || f.edges == nullptr || f.bins->order == nullptr || f.bins->svertices == nullptr ||
@@ -3143,45 +3223,40 @@ hipError_t LaunchCullFrames(const CullFrame* frames, std::size_t count, std::uin
             f.band.height != band0.height || f.bins->descs != frames[0].bins->descs) {
             return hipErrorInvalidValue;  // one band shape per batch
         }
-        tb.f[i] = MakeTraceParams(f.edges, n, d_vertices, d_albedo, frame, background, f.band);
-        if (f.bins->tiles != tb.f[i].tiles) {
+        tp[i] = MakeTraceParams(f.edges, n, d_vertices, d_albedo, frame, background, f.band);
+        if (f.bins->tiles != tp[i].tiles) {
             return hipErrorInvalidValue;  // bins sized for another band shape
         }
-        bb.f[i] = BindBins(tb.f[i], *f.bins, n);
-        pb.f[i].prep = MakePrepareParams(d_vertices, d_rank, n, frame, const_cast<float*>(f.edges));
-        pb.f[i].prep.order = f.bins->order;
-        pb.f[i].prep.svertices = f.bins->svertices;
-        pb.f[i].bin = bb.f[i];
+        bp[i] = BindBins(tp[i], *f.bins, n);
+        bp[i].fused = fused ? 1u : 0u;
+        pp[i].prep = MakePrepareParams(d_vertices, d_rank, n, frame, const_cast<float*>(f.edges));
+        pp[i].prep.order = f.bins->order;
+        pp[i].prep.svertices = f.bins->svertices;
+        pp[i].bin = bp[i];
     }
     const unsigned z = static_cast<unsigned>(count);
-    const unsigned gx = static_cast<unsigned>(tb.f[0].tiles_x), gy = tb.f[0].tiles / gx;
+    const unsigned gx = static_cast<unsigned>(tp[0].tiles_x), gy = tp[0].tiles / gx;
     const unsigned info_blocks = gx * ((gy + kInfoTiles - 1) / kInfoTiles);
-    const bool fused = CullFusedInfo(band0.row_begin, band0.row_count, band0.height, band0.row_interleave);
     // Tile info (fused: extra blocks of the bin launch); records + bins (every padded position: the
     // FULL stream reads them all); the trace work list; the trace: one block per work descriptor
     // (grid z = frame; interleaving the frames' descriptors so every frame's heaviest work starts
     // first measured no faster).
-    unsigned blocks = (pb.f[0].prep.n_pad + kBinThreads - 1) / kBinThreads;
-    if (fused) {
-        for (std::size_t i = 0; i < count; ++i) {
-            bb.f[i].fused = 1u;
-            pb.f[i].bin.fused = 1u;
-        }
-        blocks += info_blocks;
-    } else {
-        Launch(TileInfoKernel, dim3(gx, (gy + kInfoTiles - 1) / kInfoTiles, z), dim3(kBinThreads), stream,
-               ev.prep_begin, ev.prep_end, bb);
+    const unsigned blocks = (pp[0].prep.n_pad + kBinThreads - 1) / kBinThreads + (fused ? info_blocks : 0u);
+    const unsigned descs = frames[0].bins->descs;
+    if (!use_table) {
+        LaunchCullStages(tb, bb, pb, z, gx, gy, blocks, fused, descs, stream, ev);
+        return hipGetLastError();
     }
-    LaunchLds(PrepareBinKernel, dim3(blocks, 1, z), dim3(kBinThreads),
-              BinLdsBytes(static_cast<int>(gx), static_cast<int>(gy)), stream, ev.bin_begin, nullptr, pb);
-#ifdef SRT_ORDER_SINGLE
-    LaunchLds(WorkOrderKernel, dim3(1, 1, z), dim3(kOrderThreads), OrderLdsBytes(static_cast<int>(gx * gy)), stream,
-              nullptr, ev.bin_end, bb);
-#else
-    LaunchLds(WorkOrderKernel, dim3((gx * gy + kOrderBlock - 1) / kOrderBlock, 1, z), dim3(kOrderBlock),
-              OrderLdsBytes(static_cast<int>(gx * gy)), stream, nullptr, ev.bin_end, bb);
-#endif
-    Launch(TraceCullKernel, dim3(frames[0].bins->descs, 1, z), dim3(kWave * kCullWaves), stream, ev.begin, ev.end, tb);
+    // One upload of every frame's parameters, then the same four launches reading them from it.
+    const hipError_t e = hipMemcpyAsync(table->device, table->host, lay.bytes, hipMemcpyHostToDevice, stream);
+    if (e != hipSuccess) {
+        return e;
+    }
+    unsigned char* dev = static_cast<unsigned char*>(table->device);
+    const PrepareBinTable pt{(ConstantPtr<PrepareBinParams>)(dev + lay.prep)};
+    const BinTable bt{(ConstantPtr<BinParams>)(dev + lay.bin)};
+    const TraceTable tt{(ConstantPtr<TraceParams>)(dev + lay.trace)};
+    LaunchCullStages(tt, bt, pt, z, gx, gy, blocks, fused, descs, stream, ev);
     return hipGetLastError();
 }
 
@@ -3194,7 +3269,7 @@ hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_ver
     }
     if (variant == kTraceCull && bins != nullptr) {  // computes the records itself, every call
         const CullFrame f{d_edges, bins, band};
-        return LaunchCullFrames(&f, 1, n, d_vertices, d_albedo, frame, background, nullptr, stream, events);
+        return LaunchCullFrames(&f, 1, n, d_vertices, d_albedo, frame, background, nullptr, stream, events, nullptr);
     }
     const StageEvents ev = events != nullptr ? *events : StageEvents{};
     if (prepare_rank != nullptr) {
@@ -3239,7 +3314,7 @@ hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_ver
         // parts; every block streams every record.
         TraceBatch tb{};
         tb.f[0] = p;
-        Launch(TraceCullKernel, dim3(gx, p.tiles / gx * kParts), dim3(kWave * kCullWaves), stream, ev.begin, ev.end,
+        Launch(TraceCullKernel<TraceBatch>, dim3(gx, p.tiles / gx * kParts), dim3(kWave * kCullWaves), stream, ev.begin, ev.end,
                tb);
     } else {
         constexpr int kRowsPerBlock = kRowsPerLane * kLdsWaves;

@@ -175,6 +175,14 @@ DeviceScene::~DeviceScene() {
             (void)hipEventDestroy(e);
         }
     }
+    for (ParamTable& t : m_tables) {
+        if (t.uploaded != nullptr) {
+            (void)hipEventSynchronize(t.uploaded);
+            (void)hipEventDestroy(t.uploaded);
+        }
+        (void)hipFree(t.device);
+        (void)hipHostFree(t.host);
+    }
     if (prev >= 0) {
         (void)hipSetDevice(prev);
     }
@@ -306,6 +314,32 @@ void DeviceScene::EnsureEdgeSlots(std::size_t slots, hipStream_t stream) const {
     m_prepare_pending = true;
 }
 
+DeviceScene::ParamTable& DeviceScene::AcquireTable(std::size_t frames) const {
+    ParamTable& t = m_tables[m_table_next];
+    m_table_next = (m_table_next + 1) % kParamTables;
+    if (t.pending) {
+        HipCheck(hipEventSynchronize(t.uploaded), "hipEventSynchronize(parameter table)");
+        t.pending = false;
+    }
+    if (t.frames < frames) {
+        // Launches queued earlier may still read the old device table: let the device drain first.
+        HipCheck(hipDeviceSynchronize(), "hipDeviceSynchronize(parameter table)");
+        (void)hipFree(t.device);
+        (void)hipHostFree(t.host);
+        t.device = nullptr;
+        t.host = nullptr;
+        t.frames = 0;
+        const std::size_t bytes = CullTableBytes(frames);
+        HipCheck(hipMalloc(&t.device, bytes), "hipMalloc(parameter table)");
+        HipCheck(hipHostMalloc(&t.host, bytes, hipHostMallocDefault), "hipHostMalloc(parameter table)");
+        t.frames = frames;
+    }
+    if (t.uploaded == nullptr) {
+        HipCheck(hipEventCreateWithFlags(&t.uploaded, hipEventDisableTiming), "hipEventCreate(parameter table)");
+    }
+    return t;
+}
+
 void DeviceScene::TraceBatch(const float* const* d_offsets, float* const* d_rgba, int* const* d_ids, std::size_t frames,
                              std::size_t row_begin, std::size_t row_count, int variant, hipStream_t stream,
                              std::size_t row_interleave) const {
@@ -315,8 +349,8 @@ void DeviceScene::TraceBatch(const float* const* d_offsets, float* const* d_rgba
     if (!BandFits(row_begin, row_count, row_interleave, m_height)) {
         throw std::runtime_error("TraceBatch: row band outside the frame");
     }
-    if (frames > static_cast<std::size_t>(kMaxBatch)) {
-        throw std::runtime_error("TraceBatch: at most " + std::to_string(kMaxBatch) + " frames per batch");
+    if (frames > static_cast<std::size_t>(kMaxTableFrames)) {
+        throw std::runtime_error("TraceBatch: at most " + std::to_string(kMaxTableFrames) + " frames per batch");
     }
     if (frames == 0 || row_count == 0) {
         return;
@@ -332,8 +366,8 @@ void DeviceScene::TraceBatch(const float* const* d_offsets, float* const* d_rgba
     OrderAfterPrevious(stream);
     EnsureEdgeSlots(frames, stream);
     EnsureCullWork(frames, row_count, stream);
-    CullBins bins[kMaxBatch];
-    CullFrame cf[kMaxBatch];
+    std::vector<CullBins> bins(frames);
+    std::vector<CullFrame> cf(frames);
     const std::size_t floats = PaddedTriangleCount(m_n) * kEdgeFloatsPerTriangle;
     // The trace grid for the whole batch: its frames' parts together fill the chip sooner (a
     // 135-row band alone splits 5 ways; eight of them do not need to).
@@ -347,9 +381,16 @@ void DeviceScene::TraceBatch(const float* const* d_offsets, float* const* d_rgba
                               row_count, d_ids != nullptr ? d_ids[f] : nullptr, row_interleave};
     }
     const StageEvents ev = BindStageEvents(!CullFusedInfo(row_begin, row_count, m_height, row_interleave), true);
-    HipCheck(LaunchCullFrames(cf, frames, m_n, m_vertices, m_albedo, m_frame, m_background, m_rank, stream,
-                              m_timing ? &ev : nullptr),
+    ParamTable* table = frames > static_cast<std::size_t>(kMaxBatch) ? &AcquireTable(frames) : nullptr;
+    const CullTable ct{table != nullptr ? table->device : nullptr, table != nullptr ? table->host : nullptr,
+                       table != nullptr ? table->frames : 0};
+    HipCheck(LaunchCullFrames(cf.data(), frames, m_n, m_vertices, m_albedo, m_frame, m_background, m_rank, stream,
+                              m_timing ? &ev : nullptr, table != nullptr ? &ct : nullptr),
              "batched trace launch");
+    if (table != nullptr) {
+        HipCheck(hipEventRecord(table->uploaded, stream), "hipEventRecord(parameter table)");
+        table->pending = true;
+    }
     RecordOrder(stream);
 }
 

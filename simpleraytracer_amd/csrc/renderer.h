@@ -80,11 +80,12 @@ public:
     void Shade(const float* d_offsets, const int* d_ids, float* d_rgba, std::size_t row_begin, std::size_t row_count,
                hipStream_t stream, std::size_t frames = 1, std::size_t band_rows = 0,
                std::size_t interleaved = 0, std::size_t offsets_stride = 0) const;
-    // `frames` (<= kMaxBatch) frames of the prepared camera, rows [row_begin, row_begin +
-    // row_count) each: frame f's offsets d_offsets[f], its RGBA d_rgba[f] or (d_ids non-null) its
-    // hit ids d_ids[f]. Each frame gets the whole per-frame pipeline (record setup, bins, work
-    // list, trace), as `frames` Prepare + Trace calls would; the cull variant runs all frames in
-    // one launch per stage (render.h LaunchCullFrames), the others frame by frame.
+    // `frames` (<= render.h kMaxTableFrames) frames of the prepared camera, rows [row_begin,
+    // row_begin + row_count) each: frame f's offsets d_offsets[f], its RGBA d_rgba[f] or (d_ids
+    // non-null) its hit ids d_ids[f]. Each frame gets the whole per-frame pipeline (record setup,
+    // bins, work list, trace), as `frames` Prepare + Trace calls would; the cull variant runs all
+    // frames in one launch per stage (render.h LaunchCullFrames; more than kMaxBatch frames read
+    // their parameters from a device table uploaded once per call), the others frame by frame.
     void TraceBatch(const float* const* d_offsets, float* const* d_rgba, int* const* d_ids, std::size_t frames,
                     std::size_t row_begin, std::size_t row_count, int variant, hipStream_t stream,
                     std::size_t row_interleave = 1) const;
@@ -138,6 +139,20 @@ private:
     void EnsureEdgeSlots(std::size_t slots, hipStream_t stream) const;
     // BVH variant: node boxes + depth bounds (render.h BvhLayout), allocated by the first bvh Trace.
     mutable unsigned char* m_bvh = nullptr;
+    // Parameter tables of TraceBatch calls of more than kMaxBatch frames (render.h CullTable): a
+    // ring of device tables with page-locked host staging; a staging buffer is rewritten only after
+    // its previous upload has executed (its event), the device copy is protected by stream order.
+    struct ParamTable {
+        void* device = nullptr;
+        void* host = nullptr;
+        hipEvent_t uploaded = nullptr;
+        std::size_t frames = 0;
+        bool pending = false;
+    };
+    static constexpr std::size_t kParamTables = 4;
+    mutable ParamTable m_tables[kParamTables];
+    mutable std::size_t m_table_next = 0;
+    ParamTable& AcquireTable(std::size_t frames) const;
     // Stage-timing events, reused: per timed Prepare (begin, end), per timed Trace (bin begin,
     // bin end, begin, end); the first m_prep_timed / m_timed entries hold pending launches.
     hipEvent_t TimingEvent(std::vector<hipEvent_t>& pool, std::size_t i) const;

@@ -369,6 +369,7 @@ srt::EngineOptions EngineOptionsFrom(const srt_engine_options* o) {
         opt.exchange = o->exchange;
         opt.split = o->split;
         opt.simulate = o->simulate != 0;
+        opt.launch = o->launch;
     }
     return opt;
 }

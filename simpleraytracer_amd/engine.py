@@ -31,9 +31,9 @@ def _check(rc: int):
         raise SrtError(_native.last_error())
 
 
-def _options(variant, queues, batch, rows, exchange, split, simulate=False):
+def _options(variant, queues, batch, rows, exchange, split, simulate=False, launch=0):
     return EngineOptions(TRACE_VARIANTS[variant], queues, batch, ROWS[rows], EXCHANGES[exchange], SPLITS[split],
-                         1 if simulate else 0)
+                         1 if simulate else 0, launch)
 
 
 def unique_id() -> bytes:
@@ -48,14 +48,14 @@ class FrameEngine:
 
     def __init__(self, path: str, width: int, height: int, devices=(0,), variant: str = "cull", queues: int = 2,
                  batch: int = 16, rows: str = "interleaved", exchange: str = "alltoall", split: str = "bands",
-                 _handle=None):
+                 launch: int = 0, _handle=None):
         self._lib = _native.lib()
         self.width, self.height, self.batch = width, height, batch
         self.options = {"variant": variant, "queues": queues, "batch": batch, "rows": rows, "exchange": exchange,
-                        "split": split}
+                        "split": split, "launch": launch}
         if _handle is None:
             devs = (ctypes.c_int * len(devices))(*devices)
-            opt = _options(variant, queues, batch, rows, exchange, split)
+            opt = _options(variant, queues, batch, rows, exchange, split, launch=launch)
             _handle = self._lib.srtEngineCreate(os.fsencode(path), devs, len(devices), width, height, ctypes.byref(opt))
         if not _handle:
             raise SrtError(_native.last_error())
@@ -66,17 +66,17 @@ class FrameEngine:
     @classmethod
     def rank(cls, path: str, width: int, height: int, device: int, rank: int, world: int, uid: bytes | None,
              variant: str = "cull", queues: int = 2, batch: int = 16, rows: str = "interleaved",
-             exchange: str = "alltoall", split: str = "bands", simulate: bool = False):
+             exchange: str = "alltoall", split: str = "bands", simulate: bool = False, launch: int = 0):
         """This process's rank of a `world`-rank job on `device`; every rank calls it concurrently.
         simulate=True (measurement): no peers, no unique id -- the rank's stream without the exchange."""
         lib = _native.lib()
-        opt = _options(variant, queues, batch, rows, exchange, split, simulate)
+        opt = _options(variant, queues, batch, rows, exchange, split, simulate, launch)
         idbuf = ctypes.create_string_buffer(uid, 128) if uid is not None else None
         h = lib.srtEngineCreateRank(os.fsencode(path), device, rank, world, idbuf, width, height, ctypes.byref(opt))
         if not h:
             raise SrtError(_native.last_error())
         return cls(path, width, height, variant=variant, queues=queues, batch=batch, rows=rows, exchange=exchange,
-                   split=split, _handle=h)
+                   split=split, launch=launch, _handle=h)
 
     def set_inputs(self, offsets):
         """offsets: (count, H, W, 2) or (H, W, 2) float32 host array (numpy or CPU tensor)."""

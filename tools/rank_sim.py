@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--triangles", type=int, default=100_000)
     ap.add_argument("--rows", default="interleaved")
+    ap.add_argument("--launch", type=int, default=0, help="frames per trace launch (0: library default)")
     ap.add_argument("--all-ranks", action="store_true", help="every rank (default: ranks 0, P/2 and P-1)")
     a = ap.parse_args()
     import numpy as np
@@ -41,17 +42,18 @@ def main():
     tmp = tempfile.TemporaryDirectory()
     path = write_scene(os.path.join(tmp.name, "soup.srt"), "soup", a.triangles)
     inputs = np.full((1, a.height, a.width, 2), 0.5, np.float32)
-    out = {"batch": a.batch, "queues": a.queues, "triangles": a.triangles, "width": a.width, "height": a.height,
+    out = {"batch": a.batch, "launch": a.launch, "queues": a.queues, "triangles": a.triangles, "width": a.width, "height": a.height,
            "rows": a.rows, "ranks": {}}
     for P in [int(x) for x in a.ranks.split(",")]:
         per = {}
         ranks = range(P) if a.all_ranks else sorted({0, P // 2, P - 1})
         for r in ranks:
             if P == 1:
-                eng = FrameEngine(path, a.width, a.height, devices=[0], queues=a.queues, batch=a.batch)
+                eng = FrameEngine(path, a.width, a.height, devices=[0], queues=a.queues, batch=a.batch,
+                                  launch=a.launch)
             else:
                 eng = FrameEngine.rank(path, a.width, a.height, 0, r, P, None, queues=a.queues, batch=a.batch,
-                                       rows=a.rows, simulate=True)
+                                       rows=a.rows, simulate=True, launch=a.launch)
             eng.set_inputs(inputs)
             eng.run(a.warmup)
             torch.cuda.synchronize()
