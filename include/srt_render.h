@@ -204,6 +204,12 @@ ML_API_ENTRY int srtEngineInfo(srt_engine engine, size_t* devices, size_t* local
 ML_API_ENTRY int srtExchangeHost(const int* const* band_ids, size_t bands, size_t width, size_t height, int rows,
                                  int exchange, size_t batch, size_t batch_index, int* const* recv,
                                  size_t* recv_frames, size_t* buffer_rows);
+/* Host self-test of a record's screen box (render.hip ComputeRecord): c = the
+ * 9 edge coefficients (c0A, cxA, cyA, c0B, cxB, cyB, c0C, cxC, cyC); mode 0 = the float fast path
+ * where it applies, else the double solve (what the kernels do), 1 = the double solve, 2 = the fast
+ * path only. box = (xlo, xhi, ylo, yhi). Returns 0, or -1 with mode 2 where the fast path does
+ * not apply. */
+ML_API_ENTRY int srtScreenBoxHost(const float* c, int mode, float* box);
 
 #ifdef __cplusplus
 }

@@ -1,5 +1,7 @@
 #include "cpu_render.h"
 
+#include "screen_box.h"
+
 #include <algorithm>
 #include <atomic>
 #include <cmath>
@@ -133,7 +135,8 @@ Rec MakeRecord(const float* v, const Frame& f) {
             r.c[3 * e + 2] = Dot3(nx, ny, nz, f.dv[0], f.dv[1], f.dv[2]);
         }
         r.vol = vol;
-        r.sb = ScreenBox(r.c);
+        float fb[4];
+        r.sb = ScreenBoxFast(r.c, kScreenRange, fb) ? Box{fb[0], fb[1], fb[2], fb[3]} : ScreenBox(r.c);
     }
     const float e1x = v[3] - v[0], e1y = v[4] - v[1], e1z = v[5] - v[2];
     const float e2x = v[6] - v[0], e2y = v[7] - v[1], e2z = v[8] - v[2];
@@ -170,6 +173,21 @@ void ParallelFor(std::size_t n, std::size_t chunk, F&& f) {
 }
 
 }  // namespace
+
+bool HostScreenBox(const float c[9], int mode, float box[4]) {
+    if (mode != 1 && ScreenBoxFast(c, kScreenRange, box)) {
+        return true;
+    }
+    if (mode == 2) {
+        return false;
+    }
+    const Box b = ScreenBox(c);
+    box[0] = b.xlo;
+    box[1] = b.xhi;
+    box[2] = b.ylo;
+    box[3] = b.yhi;
+    return true;
+}
 
 bool CpuBackendSelected() {
     const char* v = std::getenv("ML_VISIBLE_DEVICES");

@@ -20,6 +20,11 @@
 
 namespace srt {
 
+// A record's screen box on the host (the kernels' ComputeRecord choice): mode 0 = the float fast
+// path (screen_box.h) where it applies, else the double solve; 1 = the double solve; 2 = the fast
+// path only (false where it does not apply). box = (xlo, xhi, ylo, yhi).
+bool HostScreenBox(const float c[9], int mode, float box[4]);
+
 // Whether env ML_VISIBLE_DEVICES selects the CPU backend ("cpu", or set to the empty string).
 bool CpuBackendSelected();
 

@@ -4,6 +4,7 @@
 // DESIGN.md. Built with -ffp-contract=off: every fused multiply-add below is an explicit
 // fmaf, so CPU (oracle/srt_oracle.c) and GPU evaluate bit-identical float expressions.
 #include "render.h"
+#include "screen_box.h"
 
 #include <hip/hip_ext.h>
 
@@ -79,7 +80,7 @@ struct TraceParams {
     unsigned long long* __restrict__ split_keys;  // key slices of split parts: one per split slot, kBlockRows x 64 each
     unsigned* __restrict__ arrive;            // per split part (its first slot): chunks finished (self-resetting)
     const unsigned* __restrict__ bin_lists;   // per tile: candidate positions (PrepareBinKernel)
-    const unsigned* __restrict__ bin_counts;  // per tile: list length; [tiles]: large-list length
+    unsigned* __restrict__ bin_counts;  // per tile: list length; [tiles]: large-list length (reset by the trace)
     const unsigned* __restrict__ large_list;  // ids of records binned to every tile
     unsigned bin_capacity;
     unsigned exp;                                // diagnostic build: experiment bits (env SRT_EXP), 0 in the product
@@ -282,14 +283,16 @@ __device__ __forceinline__ void ComputeRecord(const PrepareParams& p, const floa
     sb = disabled ? make_float4(__builtin_inff(), -__builtin_inff(), __builtin_inff(), -__builtin_inff())
                   : make_float4(0.f, 0.f, 0.f, 0.f);
 #ifdef SRT_DIAG
-    if ((p.exp & 512u) == 0u && !disabled) {  // timing experiment: 512 skips the screen box
-        sb = ScreenBox(c);
-    }
-#else
-    if (!disabled) {
-        sb = ScreenBox(c);
-    }
+    disabled = disabled || (p.exp & 512u) != 0u;  // timing experiment: 512 skips the screen box
 #endif
+    if (!disabled) {
+        // The float solve with proven error bounds where it applies (screen_box.h: every record of
+        // the soups), else the double one. (Measured: the double solve alone was ~3.8 us of a
+        // single frame's 13 us record + bin launch -- a dependent chain of ~300 f64 instructions
+        // at 1.5 waves per SIMD -- and ~0.6 us per frame of a P = 8 band rank's 5.7.)
+        float fb[4];
+        sb = ScreenBoxFast(c, kScreenBoxRange, fb) ? make_float4(fb[0], fb[1], fb[2], fb[3]) : ScreenBox(c);
+    }
 }
 
 // Stored as (hi, -lo) pairs so the cull test is one saturating packed add per axis.
@@ -1562,10 +1565,8 @@ __device__ __forceinline__ int LastLoAtMost(const float2* b, int n, float v, con
 // split part's chunks own consecutive split slots (key slices; the arrival counter at the first).
 // (Gathering whole empty tiles four to a descriptor, one block storing all their misses, cut the
 // trace grid by ~950 blocks at C3 and measured no faster: an empty part's block is cheap.)
-// One block on one CU: every per-tile instruction costs the whole chip's wait, hence shifts.
-// Work-order state (BinParams::work_count, zeroed at allocation, reset by the last order block of
-// each frame): 64 per-bucket descriptor cursors, split slots handed out, order blocks arrived.
-constexpr int kOrderBuckets = 64, kOrderSlots = 64, kOrderArrived = 65;
+// (BinParams::work_count: the single-block measurement build's list length; kOrderWords words.)
+constexpr int kOrderBuckets = 64;
 constexpr int kOrderWords = 72;
 constexpr unsigned kItemRegular = 1u;
 constexpr unsigned kItemFull = 2u;
@@ -1996,13 +1997,15 @@ __global__ __launch_bounds__(kBinThreads) void PrepareBinKernel(const Frames bat
 }
 
 // The trace work list after the bin kernel: one 256-thread block per 256 tiles. Every block reads
-// every tile's list length and flags (8 KB of counts, 64 KB of tile info at 1080p: cheap next to
-// the serial latency of one block doing it all, ~9 us), so every block knows the frame's chunk size
-// and the whole longest-first counting sort's bucket bases without waiting for another block; each
-// then places its own tiles' descriptors through per-bucket cursors (one global atomic per block and
-// bucket), writes its share of the end marks, and the last block to arrive resets the cursors and
-// the bin counts for the frame slot's next use.
+// every tile's list length and flags (8 KB of counts, 16 KB of tile flags at 1080p: cheap next to
+// the serial latency of one block doing it all, ~9 us), so every block knows the frame's chunk size,
+// the whole longest-first counting sort's bucket bases and how many descriptors and split slots the
+// tiles of the blocks before it take, without waiting for another block: each places its own tiles'
+// descriptors and writes its share of the end marks with no global atomic, and the trace blocks
+// reset the bin counts they consume. (Per-bucket global cursors plus a last-block reset, this
+// kernel's first multi-block form: 11.0 us one frame in flight, three dependent atomic round trips.)
 constexpr int kOrderBlock = 256;
+constexpr int kOrderTilesPerThread = 8;  // tiles' loads in flight per thread (one pass at 1080p: 2040 tiles)
 #ifdef SRT_ORDER_SINGLE  // measurement builds only: round 2's single-block counting sort
 #ifndef SRT_ORDER_THREADS
 #define SRT_ORDER_THREADS 1024
@@ -2024,49 +2027,54 @@ template <class Frames>
 __global__ __launch_bounds__(kOrderBlock) void WorkOrderKernel(const Frames batch) {
     const BinParams& p = batch[blockIdx.z];
     __shared__ CullRecord lrec[kEmptyTest];
-    __shared__ unsigned hist[kOrderBuckets];   // descriptors per bucket (the frame), then bucket bases
-    __shared__ unsigned local[kOrderBuckets];  // this block's descriptors per bucket, then its global offsets
-    __shared__ unsigned sums[3];               // candidates / 16, parts; this block's split slots
-    __shared__ unsigned is_last;
-    extern __shared__ unsigned order_lds[];    // per tile: candidates, then flags | parts << 2 (bytes)
+    __shared__ unsigned hist[kOrderBuckets];    // descriptors per bucket (the frame), then bucket bases
+    __shared__ unsigned before[kOrderBuckets];  // descriptors per bucket of the tiles of earlier blocks
+    __shared__ unsigned local[kOrderBuckets];   // this block's descriptors per bucket
+    __shared__ unsigned sums[4];  // candidates / 16, parts, this block's split slots, earlier blocks' slots
+    extern __shared__ unsigned order_lds[];     // per tile: candidates, then flags | parts << 2 (bytes)
+    constexpr int kU = kOrderTilesPerThread;
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
     const unsigned tiles = static_cast<unsigned>(p.tiles_x * p.tiles_y);
+    const unsigned first = blockIdx.x * kOrderBlock;  // this block's tiles: [first, first + kOrderBlock)
     unsigned* cnt = order_lds;
     unsigned char* meta = reinterpret_cast<unsigned char*>(order_lds + tiles);
-    if (tid < kOrderBuckets) {
-        hist[tid] = 0u;
-        local[tid] = 0u;
-    }
-    if (tid < 3) {
-        sums[tid] = 0u;
-    }
+    // Every load the block needs, issued together: this thread's own tile's info (its descriptor),
+    // the large list's length and first records, and every tile's list length and flags.
+    const unsigned mine = first + static_cast<unsigned>(tid);
+    const TileInfo my_ti = p.tile_info[min(mine, tiles - 1u)];
     const unsigned large = p.counts[tiles];
     const bool bins_invalid = p.fused != 0u && *p.range_tag == p.gen;  // MakeOrderItem: every tile FULL
+    if (tid < kOrderBuckets) {
+        hist[tid] = 0u;
+        before[tid] = 0u;
+        local[tid] = 0u;
+    }
+    if (tid < 4) {
+        sums[tid] = 0u;
+    }
     if (tid < kEmptyTest && static_cast<unsigned>(tid) < large && large <= static_cast<unsigned>(kEmptyTest)) {
-        lrec[tid] = p.cull[p.large_list[tid]];
+        lrec[tid] = p.cull[p.large_list[tid]];  // read after the barriers below
     }
     // (1) every tile's item into LDS, the frame's candidate and part totals
     unsigned long long my_cand = 0ull;
     unsigned my_parts = 0u;
-    constexpr int kU = 4;
     for (unsigned t0 = tid; t0 < tiles; t0 += kU * kOrderBlock) {
         unsigned c[kU];
-        unsigned us[kU], rg[kU];
+        uint2 ru[kU];  // (regular, usable)
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
             const unsigned t = min(t0 + u * kOrderBlock, tiles - 1u);
             c[u] = p.counts[t];
-            us[u] = p.tile_info[t].usable;
-            rg[u] = p.tile_info[t].regular;
+            ru[u] = *reinterpret_cast<const uint2*>(&p.tile_info[t].regular);
         }
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
             const unsigned t = t0 + u * kOrderBlock;
             if (t < tiles) {
                 TileInfo ti{};
-                ti.usable = us[u];
-                ti.regular = rg[u];
+                ti.regular = ru[u].x;
+                ti.usable = ru[u].y;
                 const OrderItem it = MakeOrderItem(p, t, c[u], large, ti, bins_invalid);
                 cnt[t] = it.cand;
                 meta[t] = static_cast<unsigned char>(it.flags | it.parts << 2);
@@ -2081,14 +2089,16 @@ __global__ __launch_bounds__(kOrderBlock) void WorkOrderKernel(const Frames batc
         v16 += __shfl_xor(v16, o);
         vp += __shfl_xor(vp, o);
     }
-    __syncthreads();  // hist / local / sums zeroed
+    __syncthreads();  // hist / before / local / sums zeroed
     if (lane == 0) {
         atomicAdd(&sums[0], v16);
         atomicAdd(&sums[1], vp);
     }
     __syncthreads();
     // (2) chunk size S = the power of two >= max(min_chunk, C / (D - P)), so that sum ceil(c / S)
-    // <= P + C / S <= D fits the grid; the frame's bucket histogram (longest first)
+    // <= P + C / S <= D fits the grid; the frame's bucket histogram (longest first), and the
+    // descriptors and split slots of the tiles before this block's: every block derives the same
+    // counting sort from the same LDS copy, so its tiles' places need no global atomics.
     unsigned shift = 31u;
     if (p.descs > sums[1]) {
         const unsigned room = p.descs - sums[1];
@@ -2097,28 +2107,34 @@ __global__ __launch_bounds__(kOrderBlock) void WorkOrderKernel(const Frames batc
         shift = size >= (1ull << 31) ? 31u : 64u - static_cast<unsigned>(__builtin_clzll(size - 1ull));
         shift = size <= 1ull ? 0u : shift;
     }
-    const unsigned mine = blockIdx.x * kOrderBlock + static_cast<unsigned>(tid);  // this thread's own tile
-    unsigned my_n = 0u, my_nch = 1u, my_bucket = 0u, my_at = 0u;
+    unsigned my_n = 0u, my_nch = 1u, my_bucket = 0u, my_at = 0u, slots_before = 0u;
     for (unsigned t = tid; t < tiles; t += kOrderBlock) {
         const unsigned parts = meta[t] >> 2;
         if (parts != 0u) {
             unsigned nch, bucket;
             ItemChunks(cnt[t], meta[t] & 3u, shift, nch, bucket);
-            atomicAdd(&hist[bucket], parts * nch);
-            if (t == mine) {
-                my_n = parts * nch;
+            const unsigned n = parts * nch;
+            atomicAdd(&hist[bucket], n);
+            if (t < first) {
+                atomicAdd(&before[bucket], n);
+                slots_before += nch > 1u ? n : 0u;
+            } else if (t == mine) {
+                my_n = n;
                 my_nch = nch;
                 my_bucket = bucket;
-                my_at = atomicAdd(&local[bucket], my_n);  // offset inside this block's share of the bucket
+                my_at = atomicAdd(&local[bucket], n);  // offset inside this block's share of the bucket
             }
         }
     }
-    unsigned my_slot = 0u;
-    if (my_nch > 1u) {
-        my_slot = atomicAdd(&sums[2], my_n);
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+        slots_before += __shfl_xor(slots_before, o);
     }
+    if (lane == 0 && slots_before != 0u) {
+        atomicAdd(&sums[3], slots_before);
+    }
+    const unsigned my_slot = my_nch > 1u ? atomicAdd(&sums[2], my_n) : 0u;
     __syncthreads();
-    unsigned used = 0u;
     if (tid < kWave) {  // bucket b's first descriptor: those of the heavier buckets (suffix sum, exclusive)
         const unsigned c = hist[lane];
         unsigned suf = c;
@@ -2127,28 +2143,23 @@ __global__ __launch_bounds__(kOrderBlock) void WorkOrderKernel(const Frames batc
             const unsigned u = __shfl_down(suf, o);
             suf += lane + o < kWave ? u : 0u;
         }
-        used = __shfl(suf, 0);
-        hist[lane] = suf - c;
-        // this block's share of bucket `lane`: one global atomic per nonempty bucket
-        local[lane] = local[lane] != 0u ? atomicAdd(&p.work_count[lane], local[lane]) : 0u;
+        hist[lane] = suf - c + before[lane];  // this block's first descriptor in bucket `lane`
         if (lane == 0) {
-            sums[2] = sums[2] != 0u ? atomicAdd(&p.work_count[kOrderSlots], sums[2]) : 0u;
-            sums[0] = used;
+            sums[0] = suf;  // descriptors listed
         }
     }
     __syncthreads();
-    used = sums[0];
-    // (3) this block's tiles' descriptors
+    const unsigned used = sums[0];
+    // (3) this thread's tile's descriptors
     if (my_n != 0u) {
         const unsigned t = mine;
-        const TileInfo ti = p.tile_info[t];
-        const unsigned at = hist[my_bucket] + local[my_bucket] + my_at;
-        const unsigned slot = my_nch > 1u ? sums[2] + my_slot : 0u;
+        const unsigned at = hist[my_bucket] + my_at;
+        const unsigned slot = my_nch > 1u ? sums[3] + my_slot : 0u;
         const unsigned flags = meta[t] & 3u, cand = cnt[t], parts = meta[t] >> 2;
         const unsigned list_len = (flags & kItemFull) ? 0u : cand - large;
         unsigned out_flags = flags;
         if ((flags & kItemFull) == 0u && list_len == 0u && large <= static_cast<unsigned>(kEmptyTest)) {
-            const Box tb{ti.box.x, ti.box.y, ti.box.z, ti.box.w};
+            const Box tb{my_ti.box.x, my_ti.box.y, my_ti.box.z, my_ti.box.w};
             bool may = false;
             for (unsigned k = 0; k < large; ++k) {
                 const CullRecord& r = lrec[k];
@@ -2161,31 +2172,16 @@ __global__ __launch_bounds__(kOrderBlock) void WorkOrderKernel(const Frames batc
             for (unsigned ch = 0; ch < my_nch; ++ch) {
                 const unsigned d = at + part * my_nch + ch;
                 p.work[2 * d] = make_uint4(t * kParts + part, cand, list_len, out_flags);
-                p.work[2 * d + 1] = make_uint4(__float_as_uint(ti.ox), __float_as_uint(ti.oy), ch | my_nch << 16,
+                p.work[2 * d + 1] = make_uint4(__float_as_uint(my_ti.ox), __float_as_uint(my_ti.oy), ch | my_nch << 16,
                                                slot + part * my_nch);
             }
         }
     }
     // descriptors past the list: end marks (every block a share; a trace block reads nothing first)
-    for (unsigned d = used + blockIdx.x * kOrderBlock + static_cast<unsigned>(tid); d < p.descs;
-         d += gridDim.x * kOrderBlock) {
+    for (unsigned d = used + first + static_cast<unsigned>(tid); d < p.descs; d += gridDim.x * kOrderBlock) {
         p.work[2 * d] = make_uint4(kWorkEnd, 0u, 0u, 0u);
     }
-    // the last block to arrive resets the cursors and the bin counts (every block has read them)
-    __syncthreads();
-    if (tid == 0) {
-        __threadfence();
-        is_last = atomicAdd(&p.work_count[kOrderArrived], 1u) == gridDim.x - 1u ? 1u : 0u;
-    }
-    __syncthreads();
-    if (is_last != 0u) {
-        for (unsigned t = tid; t <= tiles; t += kOrderBlock) {
-            p.counts[t] = 0u;
-        }
-        if (tid < kOrderWords) {
-            p.work_count[tid] = 0u;
-        }
-    }
+    // (the bin counts are reset by the trace blocks that consume these descriptors)
 }
 #endif
 
@@ -2206,9 +2202,6 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(c
     const TraceParams& p = batch[blockIdx.z];
     constexpr int R = kCullR;
     __shared__ CullShared sh;
-#ifdef SRT_EXP_SETUP_ONLY  // measurement builds only (make exp): the frame's setup without its trace
-    return;
-#endif
 #ifdef SRT_DIAG
     const unsigned long long d_rt0 = __builtin_amdgcn_s_memrealtime();
     const unsigned d_blk = blockIdx.y * gridDim.x + blockIdx.x;
@@ -2250,6 +2243,17 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(c
         chunk = w1.z & 0xFFFFu;
         nchunks = w1.z >> 16;
         slot = w1.w;
+        // The bin counts this launch's work order read, zeroed for the slot's next frame: each
+        // tile's by its first part's first chunk, the large list's by the first descriptor.
+        if (threadIdx.x == 0 && chunk == 0u && item % kParts == 0u) {
+            p.bin_counts[item / kParts] = 0u;
+        }
+        if (threadIdx.x == 0 && d == 0u) {
+            p.bin_counts[p.tiles] = 0u;
+        }
+#ifdef SRT_EXP_SETUP_ONLY  // measurement builds only (make exp): the frame's setup without its trace
+        return;
+#endif
         src.full = (flags & kItemFull) != 0u;
         if (!src.full) {
             // candidates cut into n chunks: chunk c = [c q + c r / n, (c + 1) q + (c + 1) r / n), q r = c_t / n, % n

@@ -6,6 +6,7 @@
 #include <string>
 #include <vector>
 
+#include "cpu_render.h"
 #include "engine.h"
 #include "render.h"
 #include "renderer.h"
@@ -560,6 +561,17 @@ ML_API_ENTRY int srtExchangeHost(const int* const* band_ids, size_t bands, size_
             if (!out[c].empty()) {
                 std::copy(out[c].begin(), out[c].end(), recv[c]);
             }
+        }
+    });
+}
+
+ML_API_ENTRY int srtScreenBoxHost(const float* c, int mode, float* box) {
+    return Guarded([&] {
+        if (c == nullptr || box == nullptr || mode < 0 || mode > 2) {
+            throw std::runtime_error("Bad argument");
+        }
+        if (!srt::HostScreenBox(c, mode, box)) {
+            throw std::runtime_error("screen box: the float fast path does not apply");
         }
     });
 }
