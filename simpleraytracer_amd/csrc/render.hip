@@ -27,8 +27,20 @@ constexpr int kDiagBlocks = 65536;
 constexpr int kDiagCols = 16;
 __device__ unsigned long long g_srt_diag[kDiagBlocks][kDiagCols];
 #define SRT_STAMP(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+// Setup-kernel timelines (s_memrealtime, 100 MHz) of frame z = 0, thread 0 of each block:
+// rows kDiagOrderRow + block (WorkOrderKernel), kDiagBinRow + block (PrepareBinKernel); column 0
+// = block start, then one stamp per phase boundary (SRT_SETUP_MARK), column 15 = phases marked.
+constexpr int kDiagOrderRow = 60000, kDiagBinRow = 61000;
+#define SRT_SETUP_MARK(row, k)                                                                       \
+    do {                                                                                             \
+        if (threadIdx.x == 0 && blockIdx.z == 0 && (row) < kDiagBlocks) {                           \
+            g_srt_diag[(row)][(k)] = __builtin_amdgcn_s_memrealtime();                               \
+            g_srt_diag[(row)][15] = (k) + 1;                                                         \
+        }                                                                                            \
+    } while (0)
 #else
 #define SRT_STAMP(v)
+#define SRT_SETUP_MARK(row, k)
 #endif
 
 namespace {
@@ -1852,12 +1864,14 @@ __global__ __launch_bounds__(kBinThreads) void PrepareBinKernel(const Frames bat
     const PrepareBinParams& pb = batch[blockIdx.z];
     const BinParams& p = pb.bin;
     const PrepareParams& pp = pb.prep;
+    SRT_SETUP_MARK(kDiagBinRow + blockIdx.x, 0);
     if (p.fused != 0u) {  // the blocks past the record blocks compute the tile info (CullFusedInfo)
         const unsigned rec_blocks = (pp.n_pad + kBinThreads - 1) / kBinThreads;
         if (blockIdx.x >= rec_blocks) {
             const unsigned k = blockIdx.x - rec_blocks;
             TileInfoBlock(p, static_cast<int>(k % static_cast<unsigned>(p.tiles_x)),
                           static_cast<int>(k / static_cast<unsigned>(p.tiles_x)));
+            SRT_SETUP_MARK(kDiagBinRow + blockIdx.x, 1);
             return;
         }
     }
@@ -1879,7 +1893,9 @@ __global__ __launch_bounds__(kBinThreads) void PrepareBinKernel(const Frames bat
     }
     // The monotone tile-column and tile-row bounds (the histogram's LDS is the reduction's
     // scratch), then the histogram zeroed.
+    SRT_SETUP_MARK(kDiagBinRow + blockIdx.x, 1);
     BinTileBounds(p, hist, b);
+    SRT_SETUP_MARK(kDiagBinRow + blockIdx.x, 2);
     for (int t = tid; t < tiles; t += kBinThreads) {
         hist[t] = 0u;
     }
@@ -1911,6 +1927,7 @@ __global__ __launch_bounds__(kBinThreads) void PrepareBinKernel(const Frames bat
         }
     }
     __syncthreads();  // histogram zeroed
+    SRT_SETUP_MARK(kDiagBinRow + blockIdx.x, 3);
 
     // The record's tile range (bit k of the mask below = tile (r0 + k / w, c0 + k % w) of the
     // range, at most kLargeTiles of them).
@@ -1974,11 +1991,12 @@ __global__ __launch_bounds__(kBinThreads) void PrepareBinKernel(const Frames bat
             }
         }
     }
-    for (unsigned m = mask; m != 0u; m &= m - 1u) {
+    for (unsigned m = (p.exp & 8u) ? 0u : mask; m != 0u; m &= m - 1u) {  // diag timing: 8 skips the counts
         const int k = __builtin_ctz(m);
         atomicAdd(&hist[(r0 + k / w) * nx + c0 + k % w], 1u);
     }
     __syncthreads();
+    SRT_SETUP_MARK(kDiagBinRow + blockIdx.x, 4);
     for (int t = tid; t < tiles; t += kBinThreads) {
         const unsigned h = hist[t];
         if (h != 0u) {
@@ -1986,6 +2004,7 @@ __global__ __launch_bounds__(kBinThreads) void PrepareBinKernel(const Frames bat
         }
     }
     __syncthreads();
+    SRT_SETUP_MARK(kDiagBinRow + blockIdx.x, 5);
     for (unsigned m = mask; m != 0u; m &= m - 1u) {
         const int k = __builtin_ctz(m);
         const unsigned t = static_cast<unsigned>((r0 + k / w) * nx + c0 + k % w);
@@ -1994,6 +2013,10 @@ __global__ __launch_bounds__(kBinThreads) void PrepareBinKernel(const Frames bat
             p.lists[static_cast<size_t>(t) * p.capacity + at] = i;
         }
     }
+#ifdef SRT_DIAG
+    __syncthreads();
+    SRT_SETUP_MARK(kDiagBinRow + blockIdx.x, 6);
+#endif
 }
 
 // The trace work list after the bin kernel: one 256-thread block per 256 tiles. Every block reads
@@ -2006,6 +2029,7 @@ __global__ __launch_bounds__(kBinThreads) void PrepareBinKernel(const Frames bat
 // kernel's first multi-block form: 11.0 us one frame in flight, three dependent atomic round trips.)
 constexpr int kOrderBlock = 256;
 constexpr int kOrderTilesPerThread = 8;  // tiles' loads in flight per thread (one pass at 1080p: 2040 tiles)
+constexpr int kOrderCopies = 8;          // LDS copies of the bucket histograms (lanes spread over them)
 #ifdef SRT_ORDER_SINGLE  // measurement builds only: round 2's single-block counting sort
 #ifndef SRT_ORDER_THREADS
 #define SRT_ORDER_THREADS 1024
@@ -2027,8 +2051,9 @@ template <class Frames>
 __global__ __launch_bounds__(kOrderBlock) void WorkOrderKernel(const Frames batch) {
     const BinParams& p = batch[blockIdx.z];
     __shared__ CullRecord lrec[kEmptyTest];
-    __shared__ unsigned hist[kOrderBuckets];    // descriptors per bucket (the frame), then bucket bases
-    __shared__ unsigned before[kOrderBuckets];  // descriptors per bucket of the tiles of earlier blocks
+    __shared__ unsigned hist8[kOrderCopies][kOrderBuckets];    // descriptors per bucket (the frame)
+    __shared__ unsigned before8[kOrderCopies][kOrderBuckets];  // ... of the tiles of earlier blocks
+    __shared__ unsigned hist[kOrderBuckets];    // this block's first descriptor per bucket
     __shared__ unsigned local[kOrderBuckets];   // this block's descriptors per bucket
     __shared__ unsigned sums[4];  // candidates / 16, parts, this block's split slots, earlier blocks' slots
     extern __shared__ unsigned order_lds[];     // per tile: candidates, then flags | parts << 2 (bytes)
@@ -2039,6 +2064,7 @@ __global__ __launch_bounds__(kOrderBlock) void WorkOrderKernel(const Frames batc
     const unsigned first = blockIdx.x * kOrderBlock;  // this block's tiles: [first, first + kOrderBlock)
     unsigned* cnt = order_lds;
     unsigned char* meta = reinterpret_cast<unsigned char*>(order_lds + tiles);
+    SRT_SETUP_MARK(kDiagOrderRow + blockIdx.x, 0);
     // Every load the block needs, issued together: this thread's own tile's info (its descriptor),
     // the large list's length and first records, and every tile's list length and flags.
     const unsigned mine = first + static_cast<unsigned>(tid);
@@ -2046,9 +2072,11 @@ __global__ __launch_bounds__(kOrderBlock) void WorkOrderKernel(const Frames batc
     const unsigned large = p.counts[tiles];
     const bool bins_invalid = p.fused != 0u && *p.range_tag == p.gen;  // MakeOrderItem: every tile FULL
     if (tid < kOrderBuckets) {
-        hist[tid] = 0u;
-        before[tid] = 0u;
         local[tid] = 0u;
+    }
+    for (int k = tid; k < kOrderCopies * kOrderBuckets; k += kOrderBlock) {
+        (&hist8[0][0])[k] = 0u;
+        (&before8[0][0])[k] = 0u;
     }
     if (tid < 4) {
         sums[tid] = 0u;
@@ -2090,11 +2118,13 @@ __global__ __launch_bounds__(kOrderBlock) void WorkOrderKernel(const Frames batc
         vp += __shfl_xor(vp, o);
     }
     __syncthreads();  // hist / before / local / sums zeroed
+    SRT_SETUP_MARK(kDiagOrderRow + blockIdx.x, 1);
     if (lane == 0) {
         atomicAdd(&sums[0], v16);
         atomicAdd(&sums[1], vp);
     }
     __syncthreads();
+    SRT_SETUP_MARK(kDiagOrderRow + blockIdx.x, 2);
     // (2) chunk size S = the power of two >= max(min_chunk, C / (D - P)), so that sum ceil(c / S)
     // <= P + C / S <= D fits the grid; the frame's bucket histogram (longest first), and the
     // descriptors and split slots of the tiles before this block's: every block derives the same
@@ -2107,22 +2137,25 @@ __global__ __launch_bounds__(kOrderBlock) void WorkOrderKernel(const Frames batc
         shift = size >= (1ull << 31) ? 31u : 64u - static_cast<unsigned>(__builtin_clzll(size - 1ull));
         shift = size <= 1ull ? 0u : shift;
     }
-    unsigned my_n = 0u, my_nch = 1u, my_bucket = 0u, my_at = 0u, slots_before = 0u;
+    // The frame's histogram and the earlier blocks' share in kOrderCopies LDS copies, lane l adding
+    // to copy l % kOrderCopies (per-tile atomics into one copy serialised on the few busy buckets:
+    // ~3.7 us of this kernel's ~9 us one frame in flight), summed after the barrier.
+    unsigned my_n = 0u, my_nch = 1u, my_bucket = 0u, slots_before = 0u;
+    const unsigned copy = static_cast<unsigned>(lane) % kOrderCopies;
     for (unsigned t = tid; t < tiles; t += kOrderBlock) {
         const unsigned parts = meta[t] >> 2;
         if (parts != 0u) {
             unsigned nch, bucket;
             ItemChunks(cnt[t], meta[t] & 3u, shift, nch, bucket);
             const unsigned n = parts * nch;
-            atomicAdd(&hist[bucket], n);
+            atomicAdd(&hist8[copy][bucket], n);
             if (t < first) {
-                atomicAdd(&before[bucket], n);
+                atomicAdd(&before8[copy][bucket], n);
                 slots_before += nch > 1u ? n : 0u;
             } else if (t == mine) {
                 my_n = n;
                 my_nch = nch;
                 my_bucket = bucket;
-                my_at = atomicAdd(&local[bucket], n);  // offset inside this block's share of the bucket
             }
         }
     }
@@ -2133,22 +2166,29 @@ __global__ __launch_bounds__(kOrderBlock) void WorkOrderKernel(const Frames batc
     if (lane == 0 && slots_before != 0u) {
         atomicAdd(&sums[3], slots_before);
     }
+    const unsigned my_at = my_n != 0u ? atomicAdd(&local[my_bucket], my_n) : 0u;  // place in this block's share
     const unsigned my_slot = my_nch > 1u ? atomicAdd(&sums[2], my_n) : 0u;
     __syncthreads();
     if (tid < kWave) {  // bucket b's first descriptor: those of the heavier buckets (suffix sum, exclusive)
-        const unsigned c = hist[lane];
+        unsigned c = 0u, bf = 0u;
+#pragma unroll
+        for (int k = 0; k < kOrderCopies; ++k) {
+            c += hist8[k][lane];
+            bf += before8[k][lane];
+        }
         unsigned suf = c;
 #pragma unroll
         for (int o = 1; o < kWave; o <<= 1) {
             const unsigned u = __shfl_down(suf, o);
             suf += lane + o < kWave ? u : 0u;
         }
-        hist[lane] = suf - c + before[lane];  // this block's first descriptor in bucket `lane`
+        hist[lane] = suf - c + bf;  // this block's first descriptor in bucket `lane`
         if (lane == 0) {
             sums[0] = suf;  // descriptors listed
         }
     }
     __syncthreads();
+    SRT_SETUP_MARK(kDiagOrderRow + blockIdx.x, 3);
     const unsigned used = sums[0];
     // (3) this thread's tile's descriptors
     if (my_n != 0u) {
@@ -2181,6 +2221,10 @@ __global__ __launch_bounds__(kOrderBlock) void WorkOrderKernel(const Frames batc
     for (unsigned d = used + first + static_cast<unsigned>(tid); d < p.descs; d += gridDim.x * kOrderBlock) {
         p.work[2 * d] = make_uint4(kWorkEnd, 0u, 0u, 0u);
     }
+#ifdef SRT_DIAG
+    __syncthreads();
+    SRT_SETUP_MARK(kDiagOrderRow + blockIdx.x, 4);
+#endif
     // (the bin counts are reset by the trace blocks that consume these descriptors)
 }
 #endif
