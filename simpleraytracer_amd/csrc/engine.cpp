@@ -364,6 +364,10 @@ void FrameEngine::Init(const Scene& scene, const std::vector<int>& devices) {
     }
     m_opt.launch = std::min({m_opt.launch, m_opt.batch, static_cast<std::size_t>(kMaxTableFrames)});
     m_bands = m_opt.split == EngineOptions::kBands;
+    {  // measurement only: whole frames (P = 1, or split frames) with deferred shading
+        const char* v = std::getenv("SRT_DEFER_SHADE");
+        m_defer_shade = v != nullptr && std::strcmp(v, "1") == 0 && !(m_bands && m_world > 1);
+    }
     m_split = BandSplit::Make(m_height, m_bands ? m_world : 1, m_opt.interleaved);
     m_plan.bands = m_split.bands;
     m_plan.batch = m_opt.batch;
@@ -405,6 +409,9 @@ void FrameEngine::AllocateQueues() {
                 q.rgba_frames = m_plan.MaxFramesPerCompositor();
             } else {
                 q.rgba_frames = m_opt.batch;
+                if (m_defer_shade) {  // measurement: whole frames traced to ids, shaded by a second launch
+                    q.recv = DeviceAlloc<int>(m_opt.batch * m_width * m_height, "hipMalloc(frame ids)");
+                }
             }
             q.rgba = DeviceAlloc<float>(q.rgba_frames * frame_floats4, "hipMalloc(frames)");
         }
@@ -561,13 +568,20 @@ void FrameEngine::TracePhase(std::size_t local, std::size_t b) {
     std::vector<int*> ids(L);
     const std::size_t frame_floats4 = m_width * m_height * 4;
     if (!exchange) {  // whole frames, traced and shaded in one kernel
+        const std::size_t frame_pixels = m_width * m_height;
         for (std::size_t f0 = 0; f0 < F; f0 += L) {
             const std::size_t n = std::min(L, F - f0);
             for (std::size_t j = 0; j < n; ++j) {
                 offs[j] = FullInput(local, k0 + f0 + j);
                 rgba[j] = q.rgba + (f0 + j) * frame_floats4;
+                ids[j] = m_defer_shade ? q.recv + (f0 + j) * frame_pixels : nullptr;
             }
-            q.scene->TraceBatch(offs.data(), rgba.data(), nullptr, n, 0, m_height, m_opt.variant, q.stream, 1);
+            q.scene->TraceBatch(offs.data(), m_defer_shade ? nullptr : rgba.data(), m_defer_shade ? ids.data() : nullptr,
+                                n, 0, m_height, m_opt.variant, q.stream, 1);
+        }
+        if (m_defer_shade) {  // inputs of one batch are evenly strided (SetInputs' condition)
+            const std::size_t stride = m_inputs == 1 ? 0 : FrameFloats();
+            q.scene->Shade(FullInput(local, k0), q.recv, q.rgba, 0, m_height, q.stream, F, m_height, 0, stride);
         }
         return;
     }

@@ -155,6 +155,7 @@ private:
     std::uint64_t m_n = 0;
     bool m_bands = true;       // bands split at P > 1 (exchange + shading)
     bool m_copy = false;       // exchange by device copies (repeated device / SRT_GATHER=copy)
+    bool m_defer_shade = false;  // env SRT_DEFER_SHADE=1 (measurement): whole frames as ids + a shading launch
     BandSplit m_split;
     ExchangePlan m_plan;
     std::vector<std::unique_ptr<Device>> m_dev;

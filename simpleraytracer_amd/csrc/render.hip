@@ -541,33 +541,54 @@ __device__ __forceinline__ void ShadeAndStore(const TraceParams& p, int x, int y
 // band of row_count rows: the plain (row_count, width) layout); out[g][row_count][width]. With
 // `interleaved` bands the bands took the frame's tile rows round-robin: row y is row
 // (t / bands) * kCullTileRows + y % kCullTileRows of band t % bands, t = y / kCullTileRows.
-__global__ __launch_bounds__(256) void ShadeIdsKernel(TraceParams p, const int* __restrict__ ids,
-                                                      unsigned band_rows, unsigned frames, unsigned interleaved,
-                                                      size_t offsets_stride) {
-    const size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-    const size_t pixels = static_cast<size_t>(p.width) * p.row_count;
-    if (i >= pixels) {
+// Grid (ceil(W / kShadeThreads), ceil(row_count / kShadeRows), frames): block (bx, by, g) shades
+// kShadeThreads columns x kShadeRows rows of frame g, a thread one column of kShadeRows rows with all
+// their id and offset loads in flight together (no per-pixel division for x and y: the former 1-D
+// grid's 64-bit i % W and i / W were most of the kernel's instructions).
+constexpr int kShadeThreads = 128;
+#ifndef SRT_SHADE_ROWS
+#define SRT_SHADE_ROWS 4
+#endif
+constexpr int kShadeRows = SRT_SHADE_ROWS;
+__global__ __launch_bounds__(kShadeThreads) void ShadeIdsKernel(TraceParams p, const int* __restrict__ ids,
+                                                                unsigned band_rows, unsigned frames,
+                                                                unsigned interleaved, size_t offsets_stride) {
+    const int x = static_cast<int>(blockIdx.x * kShadeThreads + threadIdx.x);
+    if (x >= p.width) {
         return;
     }
-    const unsigned g = blockIdx.y;
-    const int x = static_cast<int>(i % static_cast<unsigned>(p.width));
-    const int y = static_cast<int>(i / static_cast<unsigned>(p.width));
-    unsigned band, local;
-    if (interleaved != 0u) {
-        const unsigned t = static_cast<unsigned>(y) / kCullTileRows;
-        band = t % interleaved;
-        local = t / interleaved * kCullTileRows + static_cast<unsigned>(y) % kCullTileRows;
-    } else {
-        band = static_cast<unsigned>(y) / band_rows;
-        local = static_cast<unsigned>(y) - band * band_rows;
+    const int y0 = static_cast<int>(blockIdx.y) * kShadeRows;
+    const unsigned g = blockIdx.z;
+    const size_t pixels = static_cast<size_t>(p.width) * p.row_count;
+    int id[kShadeRows];
+    float2 o[kShadeRows];
+#pragma unroll
+    for (int r = 0; r < kShadeRows; ++r) {
+        const int y = min(y0 + r, p.row_count - 1);
+        unsigned band, local;
+        if (interleaved != 0u) {
+            const unsigned t = static_cast<unsigned>(y) / kCullTileRows;
+            band = t % interleaved;
+            local = t / interleaved * kCullTileRows + static_cast<unsigned>(y) % kCullTileRows;
+        } else {
+            band = static_cast<unsigned>(y) / band_rows;
+            local = static_cast<unsigned>(y) - band * band_rows;
+        }
+        const size_t at = ((static_cast<size_t>(band) * frames + g) * band_rows + local) * p.width + x;
+        id[r] = __builtin_nontemporal_load(ids + at);
+        o[r] = p.offsets[static_cast<size_t>(y) * p.width + x + g * offsets_stride];  // frame g's offsets (stride 0: shared)
     }
-    const size_t at = ((static_cast<size_t>(band) * frames + g) * band_rows + local) * p.width + x;
-    const float2 o = p.offsets[i + g * offsets_stride];  // frame g's sample offsets (stride 0: shared)
-    const float fx = (static_cast<float>(x) + o.x) / p.wf;
-    const float fy = (static_cast<float>(FrameRow(p.row_begin, p.row_interleave, y)) + o.y) / p.hf;
-    const int id = ids[at];
-    const float4 v = ShadePixel(p, fx, fy, static_cast<unsigned>(id) < p.n ? id : -1);  // no id outside the scene
-    __builtin_nontemporal_store(F4{v.x, v.y, v.z, v.w}, reinterpret_cast<F4*>(p.out + g * pixels + i));
+#pragma unroll
+    for (int r = 0; r < kShadeRows; ++r) {
+        const int y = y0 + r;
+        if (y < p.row_count) {
+            const float fx = (static_cast<float>(x) + o[r].x) / p.wf;
+            const float fy = (static_cast<float>(FrameRow(p.row_begin, p.row_interleave, y)) + o[r].y) / p.hf;
+            const float4 v = ShadePixel(p, fx, fy, static_cast<unsigned>(id[r]) < p.n ? id[r] : -1);  // no id outside the scene
+            __builtin_nontemporal_store(F4{v.x, v.y, v.z, v.w},
+                                        reinterpret_cast<F4*>(p.out + g * pixels + static_cast<size_t>(y) * p.width + x));
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1848,6 +1869,20 @@ std::size_t BinLdsBytes(int nx, int ny) {
 // loading its tiles' boxes one after another, measured 1.4 us slower: two more barriers and a
 // reduction for loads that hit the L2.) An LDS histogram of (tile, record) pairs reserves each touched tile's share of
 // its list with ONE global atomic (per-pair global atomics serialise on the busy tiles).
+// k / w and k % w for the bit index k < 32 of a record's tile range (w <= kLargeTiles): (k + 1/2) / w
+// lies >= 1/(2w) from an integer, so the truncated float product is exact (the integer division
+// was ~30 instructions per (record, tile) pair in each of the bin kernel's three tile loops).
+struct RangeDiv {
+    float inv_w;
+    int w;
+    __device__ __forceinline__ explicit RangeDiv(int width) : inv_w(width > 0 ? 1.0f / static_cast<float>(width) : 0.f), w(width) {}
+    __device__ __forceinline__ int Row(int k) const { return static_cast<int>((static_cast<float>(k) + 0.5f) * inv_w); }
+    __device__ __forceinline__ int Tile(int k, int r0, int c0, int nx) const {
+        const int kr = Row(k);
+        return (r0 + kr) * nx + c0 + (k - kr * w);
+    }
+};
+
 struct PrepareBinParams {
     PrepareParams prep;
     BinParams bin;
@@ -1947,6 +1982,7 @@ __global__ __launch_bounds__(kBinThreads) void PrepareBinKernel(const Frames bat
         }
     }
     const bool listed = w * h > 0 && w * h <= kLargeTiles && (p.exp & 2u) == 0u;
+    const RangeDiv rd(w);
     unsigned mask = 0u;
     if (listed) {
         const Record rec{c[0], c[1], c[2], c[3], c[4], c[5], c[6], c[7], c[8]};
@@ -1957,12 +1993,13 @@ __global__ __launch_bounds__(kBinThreads) void PrepareBinKernel(const Frames bat
 #pragma unroll
         for (int k = 0; k < kBinAhead; ++k) {
             const int kc = min(k, w * h - 1);
+            const int kr = rd.Row(kc);
             if (p.fused != 0u) {  // the analytic tile box (contains the tile's rays for offsets in [0, 1])
-                const float2 bx = b[c0 + kc % w], by = b[nx + r0 + kc / w];
+                const float2 bx = b[c0 + kc - kr * w], by = b[nx + r0 + kr];
                 box[k] = make_float4(bx.x, bx.y, by.x, by.y);
                 usable[k] = 1u;
             } else {
-                const TileInfo& ti = p.tile_info[(r0 + kc / w) * nx + c0 + kc % w];
+                const TileInfo& ti = p.tile_info[(r0 + kr) * nx + c0 + kc - kr * w];
                 box[k] = ti.box;
                 usable[k] = ti.usable;
             }
@@ -1978,11 +2015,12 @@ __global__ __launch_bounds__(kBinThreads) void PrepareBinKernel(const Frames bat
         for (int k = kBinAhead; k < w * h; ++k) {
             Box tb;
             unsigned use = 1u;
+            const int kr = rd.Row(k);
             if (p.fused != 0u) {
-                const float2 bx = b[c0 + k % w], by = b[nx + r0 + k / w];
+                const float2 bx = b[c0 + k - kr * w], by = b[nx + r0 + kr];
                 tb = Box{bx.x, bx.y, by.x, by.y};
             } else {
-                const TileInfo ti = p.tile_info[(r0 + k / w) * nx + c0 + k % w];
+                const TileInfo ti = p.tile_info[(r0 + kr) * nx + c0 + k - kr * w];
                 tb = Box{ti.box.x, ti.box.y, ti.box.z, ti.box.w};
                 use = ti.usable;
             }
@@ -1993,7 +2031,7 @@ __global__ __launch_bounds__(kBinThreads) void PrepareBinKernel(const Frames bat
     }
     for (unsigned m = (p.exp & 8u) ? 0u : mask; m != 0u; m &= m - 1u) {  // diag timing: 8 skips the counts
         const int k = __builtin_ctz(m);
-        atomicAdd(&hist[(r0 + k / w) * nx + c0 + k % w], 1u);
+        atomicAdd(&hist[rd.Tile(k, r0, c0, nx)], 1u);
     }
     __syncthreads();
     SRT_SETUP_MARK(kDiagBinRow + blockIdx.x, 4);
@@ -2007,7 +2045,7 @@ __global__ __launch_bounds__(kBinThreads) void PrepareBinKernel(const Frames bat
     SRT_SETUP_MARK(kDiagBinRow + blockIdx.x, 5);
     for (unsigned m = mask; m != 0u; m &= m - 1u) {
         const int k = __builtin_ctz(m);
-        const unsigned t = static_cast<unsigned>((r0 + k / w) * nx + c0 + k % w);
+        const unsigned t = static_cast<unsigned>(rd.Tile(k, r0, c0, nx));
         const unsigned at = atomicAdd(&hist[t], 1u);
         if (at < p.capacity) {
             p.lists[static_cast<size_t>(t) * p.capacity + at] = i;
@@ -3412,7 +3450,7 @@ hipError_t LaunchShade(const float* d_vertices, const float* d_albedo, const flo
     if (band_rows == 0) {
         band_rows = band.row_count;
     }
-    if (band.ids == nullptr || band.rgba == nullptr || band.offsets == nullptr || frames > 65535 ||
+    if (band.ids == nullptr || band.rgba == nullptr || band.offsets == nullptr || frames > 65535 || band.row_count > 65535 ||
         band_rows > band.row_count) {
         return hipErrorInvalidValue;
     }
@@ -3435,10 +3473,13 @@ hipError_t LaunchShade(const float* d_vertices, const float* d_albedo, const flo
         p.dv[k] = frame.dv[k];
         p.bg[k] = background[k];
     }
-    const std::size_t pixels = band.width * band.row_count;
-    hipLaunchKernelGGL(ShadeIdsKernel, dim3(static_cast<unsigned>((pixels + 255) / 256), static_cast<unsigned>(frames)),
-                       dim3(256), 0, stream, p, static_cast<const int*>(band.ids), static_cast<unsigned>(band_rows),
-                       static_cast<unsigned>(frames), static_cast<unsigned>(interleaved), offsets_stride / 2);
+    hipLaunchKernelGGL(ShadeIdsKernel,
+                       dim3(static_cast<unsigned>((band.width + kShadeThreads - 1) / kShadeThreads),
+                            static_cast<unsigned>((band.row_count + kShadeRows - 1) / kShadeRows),
+                            static_cast<unsigned>(frames)),
+                       dim3(kShadeThreads), 0, stream, p, static_cast<const int*>(band.ids),
+                       static_cast<unsigned>(band_rows), static_cast<unsigned>(frames),
+                       static_cast<unsigned>(interleaved), offsets_stride / 2);
     return hipGetLastError();
 }
 
