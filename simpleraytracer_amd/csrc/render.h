@@ -173,7 +173,7 @@ struct StageEvents {
 // Launch the trace kernel over one band (cull variant: bin + trace; bins == nullptr streams
 // every record for every tile). prepare_rank != null: first (re)compute the edge records for
 // `frame` (LaunchPrepare's work; fused with the tile-info blocks when binning).
-hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_vertices, const float* d_albedo,
+hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_vertices, const float* d_shade,
                        const Frame& frame, const float background[3], const BandArgs& band, int variant,
                        const CullBins* bins, hipStream_t stream, const StageEvents* events = nullptr,
                        const unsigned* prepare_rank = nullptr, void* bvh = nullptr);
@@ -219,7 +219,7 @@ std::size_t CullTableBytes(std::size_t frames);
 // records are computed in the bin launch every call (bins->order: position -> id; d_rank unused).
 // Events (optional): prep = tile info, bin = record setup + bins + work list, trace.
 hipError_t LaunchCullFrames(const CullFrame* frames, std::size_t count, std::uint64_t n, const float* d_vertices,
-                            const float* d_albedo, const Frame& frame, const float background[3], const unsigned* d_rank,
+                            const float* d_shade, const Frame& frame, const float background[3], const unsigned* d_rank,
                             hipStream_t stream, const StageEvents* events, const CullTable* table = nullptr);
 
 // Deferred shading of a band from hit ids (band.ids) and sample offsets into band.rgba (normals
@@ -230,7 +230,13 @@ hipError_t LaunchCullFrames(const CullFrame* frames, std::size_t count, std::uin
 // interleaved > 0: the ids' bands are that many interleaved bands (BandArgs::row_interleave).
 // offsets_stride: floats between consecutive frames' sample offsets (0: every frame of the batch
 // shares band.offsets; a multiple of 2).
-hipError_t LaunchShade(const float* d_vertices, const float* d_albedo, const float* d_edges, std::uint64_t n,
+// The scene's shading table (once, at load): per triangle two float4, (the shading normal
+// cross(v1 - v0, v2 - v0), its length) and (albedo, 0); d_table holds 8 floats per triangle. The
+// d_shade arguments of the launches below take it.
+hipError_t LaunchShadeTable(const float* d_vertices, const float* d_albedo, std::uint64_t n, float* d_table,
+                            hipStream_t stream);
+
+hipError_t LaunchShade(const float* d_vertices, const float* d_shade, const float* d_edges, std::uint64_t n,
                        const Frame& frame, const float background[3], const BandArgs& band, hipStream_t stream,
                        std::size_t frames = 1, std::size_t band_rows = 0, std::size_t interleaved = 0,
                        std::size_t offsets_stride = 0);

@@ -69,7 +69,7 @@ struct TraceParams {
     const float4* __restrict__ screen_boxes;
     const uint2* __restrict__ qboxes;
     const float* __restrict__ vertices;
-    const float* __restrict__ albedo;
+    const float4* __restrict__ shade;  // per triangle: (shading normal, |normal|), (albedo, 0) -- ShadeTableKernel
     const float2* __restrict__ offsets;
     float4* __restrict__ out;
     int* __restrict__ out_ids;  // non-null: store the hit id per pixel (-1 = miss) instead of RGBA
@@ -322,6 +322,17 @@ __device__ __forceinline__ float4 ShadingNormal(const float* __restrict__ v) {
     return make_float4(nx, ny, nz, sqrtf(Dot3(nx, ny, nz, nx, ny, nz)));
 }
 
+// Shading table of a scene (once, at load): triangle i -> (ShadingNormal, (albedo, 0)).
+__global__ __launch_bounds__(256) void ShadeTableKernel(const float* __restrict__ vertices,
+                                                        const float* __restrict__ albedo, unsigned n,
+                                                        float4* __restrict__ table) {
+    const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        table[2ull * i] = ShadingNormal(vertices + 9ull * i);
+        table[2ull * i + 1] = make_float4(albedo[3ull * i], albedo[3ull * i + 1], albedo[3ull * i + 2], 0.f);
+    }
+}
+
 // The full record pass (every variant but the binned cull path, which fuses it into its bin
 // kernel): one thread per record id i, writing the tile-planar edge record, the screen box, and
 // at the record's spatial position (rank[i]; padding ids are their own position) its quantized
@@ -489,15 +500,16 @@ __device__ __forceinline__ float4 ShadePixel(const TraceParams& p, float fx, flo
     const float dx = fmaf(fy, p.dv[0], fmaf(fx, p.du[0], p.base[0]));
     const float dy = fmaf(fy, p.dv[1], fmaf(fx, p.du[1], p.base[1]));
     const float dz = fmaf(fy, p.dv[2], fmaf(fx, p.du[2], p.base[2]));
-    // The normal from the triangle's vertices (static scene data, cache-resident): no per-frame
-    // normal buffer for the record pass to scatter (by id) and every band of a multi-GPU frame to
-    // repeat; the same expressions as always, so the same bits.
-    const float4 nr = ShadingNormal(p.vertices + 9ull * static_cast<unsigned>(id));
+    // The triangle's shading record, built once at scene load from its vertices and albedo (static
+    // scene data, like the vertices themselves: 32 B, one line, instead of 36 B of vertices, 12 B
+    // of albedo and a cross product and square root per pixel); the same expressions, so the same
+    // bits.
+    const float4* sr = p.shade + 2ull * static_cast<unsigned>(id);
+    const float4 nr = sr[0], a = sr[1];
     const float nd = Dot3(nr.x, nr.y, nr.z, dx, dy, dz);
     const float dd = Dot3(dx, dy, dz, dx, dy, dz);
     const float cosv = fminf(fabsf(nd) / (nr.w * sqrtf(dd)), 1.f);
-    const float* a = p.albedo + 3ull * id;
-    return make_float4(a[0] * cosv, a[1] * cosv, a[2] * cosv, static_cast<float>(id));
+    return make_float4(a.x * cosv, a.y * cosv, a.z * cosv, static_cast<float>(id));
 }
 
 // Store one pixel of the band: its shaded RGBA (one float4, 1 KiB contiguous per wave
@@ -3157,7 +3169,7 @@ CullBins CullBinLayout(void* base, std::uint64_t n, std::size_t width, std::size
 }
 
 namespace {
-TraceParams MakeTraceParams(const float* d_edges, std::uint64_t n, const float* d_vertices, const float* d_albedo,
+TraceParams MakeTraceParams(const float* d_edges, std::uint64_t n, const float* d_vertices, const float* d_shade,
                             const Frame& frame, const float background[3], const BandArgs& band) {
     TraceParams p{};
     const EdgeLayout e = EdgeBuffers(d_edges, n);
@@ -3166,7 +3178,7 @@ TraceParams MakeTraceParams(const float* d_edges, std::uint64_t n, const float* 
     p.qboxes = e.qboxes;
     p.cull = e.cull;
     p.vertices = d_vertices;
-    p.albedo = d_albedo;
+    p.shade = reinterpret_cast<const float4*>(d_shade);
     p.offsets = reinterpret_cast<const float2*>(band.offsets);
     p.out = reinterpret_cast<float4*>(band.rgba);
     p.out_ids = band.ids;
@@ -3275,7 +3287,7 @@ TableLayout MakeTableLayout(std::size_t frames) {
 std::size_t CullTableBytes(std::size_t frames) { return MakeTableLayout(frames).bytes; }
 
 hipError_t LaunchCullFrames(const CullFrame* frames, std::size_t count, std::uint64_t n, const float* d_vertices,
-                            const float* d_albedo, const Frame& frame, const float background[3], const unsigned* d_rank,
+                            const float* d_shade, const Frame& frame, const float background[3], const unsigned* d_rank,
                             hipStream_t stream, const StageEvents* events, const CullTable* table) {
     const bool use_table = count > static_cast<std::size_t>(kMaxBatch);
     if (frames == nullptr || count == 0 || count > static_cast<std::size_t>(kMaxTableFrames) ||
@@ -3309,7 +3321,7 @@ hipError_t LaunchCullFrames(const CullFrame* frames, std::size_t count, std::uin
             f.band.height != band0.height || f.bins->descs != frames[0].bins->descs) {
             return hipErrorInvalidValue;  // one band shape per batch
         }
-        tp[i] = MakeTraceParams(f.edges, n, d_vertices, d_albedo, frame, background, f.band);
+        tp[i] = MakeTraceParams(f.edges, n, d_vertices, d_shade, frame, background, f.band);
         if (f.bins->tiles != tp[i].tiles) {
             return hipErrorInvalidValue;  // bins sized for another band shape
         }
@@ -3346,7 +3358,7 @@ hipError_t LaunchCullFrames(const CullFrame* frames, std::size_t count, std::uin
     return hipGetLastError();
 }
 
-hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_vertices, const float* d_albedo,
+hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_vertices, const float* d_shade,
                        const Frame& frame, const float background[3], const BandArgs& band, int variant,
                        const CullBins* bins, hipStream_t stream, const StageEvents* events,
                        const unsigned* prepare_rank, void* bvh) {
@@ -3355,7 +3367,7 @@ hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_ver
     }
     if (variant == kTraceCull && bins != nullptr) {  // computes the records itself, every call
         const CullFrame f{d_edges, bins, band};
-        return LaunchCullFrames(&f, 1, n, d_vertices, d_albedo, frame, background, nullptr, stream, events, nullptr);
+        return LaunchCullFrames(&f, 1, n, d_vertices, d_shade, frame, background, nullptr, stream, events, nullptr);
     }
     const StageEvents ev = events != nullptr ? *events : StageEvents{};
     if (prepare_rank != nullptr) {
@@ -3365,7 +3377,7 @@ hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_ver
             return e;
         }
     }
-    const TraceParams p = MakeTraceParams(d_edges, n, d_vertices, d_albedo, frame, background, band);
+    const TraceParams p = MakeTraceParams(d_edges, n, d_vertices, d_shade, frame, background, band);
     const unsigned gx = static_cast<unsigned>(p.tiles_x);
     if (variant == kTraceBvh) {
         if (bvh == nullptr) {
@@ -3440,7 +3452,17 @@ std::size_t InterleavedBandRows(std::size_t height, std::size_t bands, std::size
     return rows;
 }
 
-hipError_t LaunchShade(const float* d_vertices, const float* d_albedo, const float* d_edges, std::uint64_t n,
+hipError_t LaunchShadeTable(const float* d_vertices, const float* d_albedo, std::uint64_t n, float* d_table,
+                            hipStream_t stream) {
+    if (n == 0) {
+        return hipSuccess;
+    }
+    hipLaunchKernelGGL(ShadeTableKernel, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, stream, d_vertices,
+                       d_albedo, static_cast<unsigned>(n), reinterpret_cast<float4*>(d_table));
+    return hipGetLastError();
+}
+
+hipError_t LaunchShade(const float* d_vertices, const float* d_shade, const float* d_edges, std::uint64_t n,
                        const Frame& frame, const float background[3], const BandArgs& band, hipStream_t stream,
                        std::size_t frames, std::size_t band_rows, std::size_t interleaved,
                        std::size_t offsets_stride) {
@@ -3458,7 +3480,7 @@ hipError_t LaunchShade(const float* d_vertices, const float* d_albedo, const flo
     (void)d_edges;
     p.n = static_cast<unsigned>(n);
     p.vertices = d_vertices;
-    p.albedo = d_albedo;
+    p.shade = reinterpret_cast<const float4*>(d_shade);
     p.offsets = reinterpret_cast<const float2*>(band.offsets);
     p.out = reinterpret_cast<float4*>(band.rgba);
     p.width = static_cast<int>(band.width);

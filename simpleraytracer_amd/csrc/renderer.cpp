@@ -112,7 +112,7 @@ DeviceScene::DeviceScene(const Scene& scene, int device)
     DeviceGuard guard(device);
     try {
         m_vertices = DeviceAlloc<float>(m_n * 9, "hipMalloc(vertices)");
-        m_albedo = DeviceAlloc<float>(m_n * 3, "hipMalloc(albedo)");
+        m_shade = DeviceAlloc<float>(m_n == 0 ? 8 : m_n * 8, "hipMalloc(shading table)");
         m_edges = DeviceAlloc<float>(PaddedTriangleCount(m_n) * kEdgeFloatsPerTriangle, "hipMalloc(edges)");
         m_order = DeviceAlloc<unsigned>(m_n == 0 ? 1 : m_n, "hipMalloc(order)");
         m_rank = DeviceAlloc<unsigned>(m_n == 0 ? 1 : m_n, "hipMalloc(rank)");
@@ -139,11 +139,21 @@ DeviceScene::DeviceScene(const Scene& scene, int device)
         }
         (void)hipEventDestroy(b0);
         (void)hipEventDestroy(b1);
-        HipCheck(hipMemcpy(m_albedo, scene.albedo.data(), m_n * 3 * sizeof(float), hipMemcpyHostToDevice),
-                 "hipMemcpy(albedo)");
+        if (m_n != 0) {  // the shading table from the vertices and the albedo (staged, then freed)
+            float* albedo = DeviceAlloc<float>(m_n * 3, "hipMalloc(albedo)");
+            hipError_t e = hipMemcpy(albedo, scene.albedo.data(), m_n * 3 * sizeof(float), hipMemcpyHostToDevice);
+            if (e == hipSuccess) {
+                e = LaunchShadeTable(m_vertices, albedo, m_n, m_shade, nullptr);
+            }
+            if (e == hipSuccess) {
+                e = hipStreamSynchronize(nullptr);
+            }
+            (void)hipFree(albedo);
+            HipCheck(e, "shading table");
+        }
     } catch (...) {
         (void)hipFree(m_vertices);
-        (void)hipFree(m_albedo);
+        (void)hipFree(m_shade);
         (void)hipFree(m_edges);
         (void)hipFree(m_order);
         (void)hipFree(m_rank);
@@ -157,7 +167,7 @@ DeviceScene::~DeviceScene() {
     (void)hipGetDevice(&prev);
     (void)hipSetDevice(m_device);
     (void)hipFree(m_vertices);
-    (void)hipFree(m_albedo);
+    (void)hipFree(m_shade);
     (void)hipFree(m_edges);
     (void)hipFree(m_order);
     (void)hipFree(m_rank);
@@ -257,7 +267,7 @@ void DeviceScene::Shade(const float* d_offsets, const int* d_ids, float* d_rgba,
     }
     OrderAfterPrevious(stream);
     BandArgs band{d_offsets, d_rgba, m_width, m_height, row_begin, row_count, const_cast<int*>(d_ids)};
-    HipCheck(LaunchShade(m_vertices, m_albedo, m_edges, m_n, m_frame, m_background, band, stream, frames, band_rows,
+    HipCheck(LaunchShade(m_vertices, m_shade, m_edges, m_n, m_frame, m_background, band, stream, frames, band_rows,
                          interleaved, offsets_stride),
              "shade kernel launch");
     RecordOrder(stream);
@@ -384,7 +394,7 @@ void DeviceScene::TraceBatch(const float* const* d_offsets, float* const* d_rgba
     ParamTable* table = frames > static_cast<std::size_t>(kMaxBatch) ? &AcquireTable(frames) : nullptr;
     const CullTable ct{table != nullptr ? table->device : nullptr, table != nullptr ? table->host : nullptr,
                        table != nullptr ? table->frames : 0};
-    HipCheck(LaunchCullFrames(cf.data(), frames, m_n, m_vertices, m_albedo, m_frame, m_background, m_rank, stream,
+    HipCheck(LaunchCullFrames(cf.data(), frames, m_n, m_vertices, m_shade, m_frame, m_background, m_rank, stream,
                               m_timing ? &ev : nullptr, table != nullptr ? &ct : nullptr),
              "batched trace launch");
     if (table != nullptr) {
@@ -420,7 +430,7 @@ void DeviceScene::Trace(const float* d_offsets, float* d_rgba, std::size_t row_b
     const bool fused_info = use_bins != nullptr && CullFusedInfo(row_begin, row_count, m_height, row_interleave);
     const StageEvents ev = BindStageEvents(prepare || (use_bins != nullptr && row_count != 0 && !fused_info),
                                            use_bins != nullptr || (variant == kTraceBvh && m_n != 0));
-    HipCheck(LaunchTrace(m_edges, m_n, m_vertices, m_albedo, m_frame, m_background, band, variant, use_bins, stream,
+    HipCheck(LaunchTrace(m_edges, m_n, m_vertices, m_shade, m_frame, m_background, band, variant, use_bins, stream,
                          m_timing ? &ev : nullptr, prepare ? m_rank : nullptr, m_bvh),
              "trace kernel launch");
     if (prepare) {

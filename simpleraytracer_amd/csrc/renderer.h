@@ -114,7 +114,7 @@ private:
     Camera m_camera;
     float m_background[3];
     float* m_vertices = nullptr;
-    float* m_albedo = nullptr;
+    float* m_shade = nullptr;  // shading table: 8 floats per triangle (LaunchShadeTable)
     mutable float* m_edges = nullptr;        // kEdgeFloatsPerTriangle per padded record, per frame slot
     mutable std::size_t m_edge_slots = 1;    // frame slots of m_edges (TraceBatch grows it; slot 0 = Trace's)
     unsigned* m_order = nullptr;  // record ids in spatial order (BuildSpatialOrder), for the cull bins
