@@ -858,7 +858,10 @@ constexpr int kTileRows = kCullTileRows;
 #endif
 constexpr int kBlockRows = SRT_BLOCK_ROWS;
 constexpr int kParts = kTileRows / kBlockRows;
-constexpr int kCullWaves = 4;
+#ifndef SRT_CULL_WAVES
+#define SRT_CULL_WAVES 4
+#endif
+constexpr int kCullWaves = SRT_CULL_WAVES;
 constexpr int kCullThreads = kWave * kCullWaves;
 constexpr int kCullR = kBlockRows / kCullWaves;  // rays per lane
 #ifndef SRT_PACKET_BATCH

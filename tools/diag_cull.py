@@ -97,6 +97,18 @@ def main():
     top = sorted(chains.items(), key=lambda kv: -kv[1][1])[:8]
     summary["split_chains_latest"] = [{"item": k, "first_start": round(v[0], 2), "end": round(v[1], 2), "chunks": v[2]}
                                       for k, v in top]
+    # where a block's time goes (gather / walk in shader cycles at the measured clock ratio, the rest
+    # = descriptor / epilogue: split merge, shading loads, stores)
+    cyc = b[:, 1] + b[:, 2]
+    ok = (dur > 0.5) & (cyc > 0)
+    ghz = float(np.median(cyc[ok] / (dur[ok] * 1e3))) if ok.any() else 0.0
+    summary["phases_us"] = {"clock_ghz_lower_bound": round(ghz, 3)}
+    for name, sel in (("split", nch > 1), ("whole", (nch <= 1) & (buf[ran, 7] & 8 != 0))):
+        if sel.any():
+            g = b[sel, 1] / 2400.0
+            wk = b[sel, 2] / 2400.0
+            summary["phases_us"][name] = {"blocks": int(sel.sum()), "dur": stats(dur[sel]), "gather": stats(g),
+                                          "walk": stats(wk), "rest": stats(dur[sel] - g - wk)}
     order = np.argsort(-end)[:12]
     summary["last_to_finish"] = [{"grid_block": int(ran[i]), "item": int(item[i]), "chunk": int(chunk[i]),
                                   "chunks": int(nch[i]), "last": int(last[i]), "start": round(float(start[i]), 2),
