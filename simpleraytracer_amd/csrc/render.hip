@@ -2292,6 +2292,12 @@ std::size_t OrderLdsBytes(int tiles) { return static_cast<std::size_t>(tiles) * 
 #ifndef SRT_TRACE_OCC
 #define SRT_TRACE_OCC 6
 #endif
+#ifndef SRT_SPLIT_ARRIVE_FIRST
+#define SRT_SPLIT_ARRIVE_FIRST 0  // split parts: 1 = arrive, then publish unless last (measured: trace 19.7 -> 21.6 us)
+#endif
+constexpr unsigned kSplitReady = 1u << 16;         // split part word: arrivals (low bits), readies (x kSplitReady)
+constexpr unsigned kSplitPollCap = 1u << 22;       // last arriver's polls of the word (hang guard)
+static_assert(kMaxChunks < 65536, "split part word: arrival count in 16 bits");
 #ifndef SRT_TRACE_PRIO
 #define SRT_TRACE_PRIO 0
 #endif
@@ -2590,21 +2596,59 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(c
         key[r] = sh.keys[wave * R + r][lane];
     }
     if (nchunks > 1u) {
-        // Split part: publish this chunk's keys (write-through sc1 stores), count the arrival;
-        // the last of the part's chunks takes the minimum over every chunk's keys (sc1 loads)
-        // and shades. Hand-off form: MI355X_MICROARCH.md "Valid forms", table row 1 (sc1
-        // stores, every storing wave's vmcnt(0), barrier, one agent-scope add; the last
-        // adder's block loads sc1 after a barrier).
         constexpr int kPix = kBlockRows * kWave;
         unsigned long long* slices = p.split_keys + static_cast<size_t>(slot) * kPix;
         const int pix = wave * R * kWave + lane;
+        auto publish = [&] {  // this chunk's keys, write-through (sc1) stores, complete before the barrier
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-            __hip_atomic_store(slices + static_cast<size_t>(chunk) * kPix + pix + r * kWave, key[r], __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
+            for (int r = 0; r < R; ++r) {
+                __hip_atomic_store(slices + static_cast<size_t>(chunk) * kPix + pix + r * kWave, key[r],
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+        };
+#if SRT_SPLIT_ARRIVE_FIRST
+        // Split part: the chunk counts its arrival first (low 16 bits of the part's word). Every
+        // chunk but the last then publishes its keys and adds kSplitReady (hand-off form:
+        // MI355X_MICROARCH.md "Valid forms", sc1 stores, every storing wave's vmcnt(0), barrier,
+        // one agent-scope add); the last polls the word (sc1 loads) until every other chunk is
+        // ready -- they have all arrived, so they are running and get there -- and takes the
+        // minimum over their keys (sc1 loads after a barrier). The last chunk's own keys never
+        // leave the block (half the slice traffic of a two-chunk part), but the chunks of a part
+        // finish together, so the last one mostly waits for the others' arrival round trip plus
+        // their publish: one frame in flight, 19.7 -> 21.6 us; off by default. The poll is capped
+        // (a hang guard: it only ends early if a chunk never readies, which no path does).
+        if (tid == 0) {
+            const unsigned before = __hip_atomic_fetch_add(&p.arrive[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            sh.last = (before & (kSplitReady - 1u)) == nchunks - 1u ? 1u : 0u;
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
+        if (sh.last == 0u) {
+            publish();
+            if (tid == 0) {
+                __hip_atomic_fetch_add(&p.arrive[slot], kSplitReady, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            SRT_DIAG_END(item, chunk, nchunks, 0u, src.full);
+            return;
+        }
+        if (tid == 0) {
+            const unsigned want = (nchunks - 1u) * kSplitReady + nchunks;  // every arrival, every other chunk ready
+            for (unsigned it = 0; it < kSplitPollCap; ++it) {
+                if (__hip_atomic_load(&p.arrive[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == want) {
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+            __hip_atomic_store(&p.arrive[slot], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // the next frame's
+        }
+        __syncthreads();
+#else
+        // Split part: publish this chunk's keys, count the arrival; the last of the part's chunks
+        // takes the minimum over every chunk's keys (sc1 loads) and shades. Hand-off form:
+        // MI355X_MICROARCH.md "Valid forms", table row 1 (sc1 stores, every storing wave's
+        // vmcnt(0), barrier, one agent-scope add; the last adder's block loads sc1 after a barrier).
+        publish();
         if (tid == 0) {
             const unsigned before = __hip_atomic_fetch_add(&p.arrive[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const unsigned last = before == nchunks - 1u ? 1u : 0u;
@@ -2618,6 +2662,7 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(c
             SRT_DIAG_END(item, chunk, nchunks, 0u, src.full);
             return;
         }
+#endif
         for (unsigned c = 0; c < nchunks; ++c) {
             if (c == chunk) {
                 continue;
