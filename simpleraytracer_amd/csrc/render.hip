@@ -2295,9 +2295,11 @@ std::size_t OrderLdsBytes(int tiles) { return static_cast<std::size_t>(tiles) * 
 #ifndef SRT_SPLIT_ARRIVE_FIRST
 #define SRT_SPLIT_ARRIVE_FIRST 0  // split parts: 1 = arrive, then publish unless last (measured: trace 19.7 -> 21.6 us)
 #endif
+#if SRT_SPLIT_ARRIVE_FIRST
 constexpr unsigned kSplitReady = 1u << 16;         // split part word: arrivals (low bits), readies (x kSplitReady)
 constexpr unsigned kSplitPollCap = 1u << 22;       // last arriver's polls of the word (hang guard)
 static_assert(kMaxChunks < 65536, "split part word: arrival count in 16 bits");
+#endif
 #ifndef SRT_TRACE_PRIO
 #define SRT_TRACE_PRIO 0
 #endif
