@@ -2142,17 +2142,26 @@ __global__ __launch_bounds__(kOrderBlock) void WorkOrderKernel(const Frames batc
     if (tid < kEmptyTest && static_cast<unsigned>(tid) < large && large <= static_cast<unsigned>(kEmptyTest)) {
         lrec[tid] = p.cull[p.large_list[tid]];  // read after the barriers below
     }
-    // (1) every tile's item into LDS, the frame's candidate and part totals
+    // (1) every tile's item into LDS, the frame's candidate and part totals; the next step's loads
+    // are issued before this step's items are made (4K frames: 8100 tiles, four steps of 2048, whose
+    // load round trips would otherwise follow one another)
     unsigned long long my_cand = 0ull;
     unsigned my_parts = 0u;
-    for (unsigned t0 = tid; t0 < tiles; t0 += kU * kOrderBlock) {
-        unsigned c[kU];
-        uint2 ru[kU];  // (regular, usable)
+    unsigned c[kU], cn[kU];
+    uint2 ru[kU], rn[kU];  // (regular, usable)
+    auto load_step = [&](unsigned t0, unsigned (&cc)[kU], uint2 (&rr)[kU]) {
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
             const unsigned t = min(t0 + u * kOrderBlock, tiles - 1u);
-            c[u] = p.counts[t];
-            ru[u] = *reinterpret_cast<const uint2*>(&p.tile_info[t].regular);
+            cc[u] = p.counts[t];
+            rr[u] = *reinterpret_cast<const uint2*>(&p.tile_info[t].regular);
+        }
+    };
+    load_step(tid, c, ru);
+    for (unsigned t0 = tid; t0 < tiles; t0 += kU * kOrderBlock) {
+        const unsigned next = t0 + kU * kOrderBlock;
+        if (next < tiles) {
+            load_step(next, cn, rn);
         }
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
@@ -2167,6 +2176,11 @@ __global__ __launch_bounds__(kOrderBlock) void WorkOrderKernel(const Frames batc
                 my_cand += static_cast<unsigned long long>(it.parts) * it.cand;
                 my_parts += it.parts;
             }
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            c[u] = cn[u];
+            ru[u] = rn[u];
         }
     }
     unsigned v16 = static_cast<unsigned>((my_cand + 15ull) >> 4), vp = my_parts;
