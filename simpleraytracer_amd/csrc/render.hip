@@ -1930,6 +1930,11 @@ __global__ __launch_bounds__(kBinThreads) void PrepareBinKernel(const Frames bat
     const int tiles = nx * ny;
     float2* b = bin_lds;
     unsigned* hist = reinterpret_cast<unsigned*>(bin_lds + nx + ny);
+    __shared__ unsigned bin_span[2];  // the block's lowest and highest binned tile (ordered by BinTileBounds' barrier)
+    if (tid == 0) {
+        bin_span[0] = ~0u;
+        bin_span[1] = 0u;
+    }
 
     // This thread's record (its loads in flight while the block builds the tile bounds).
     const unsigned i = blockIdx.x * kBinThreads + tid;  // spatial-order position (list entry)
@@ -1946,9 +1951,6 @@ __global__ __launch_bounds__(kBinThreads) void PrepareBinKernel(const Frames bat
     SRT_SETUP_MARK(kDiagBinRow + blockIdx.x, 1);
     BinTileBounds(p, hist, b);
     SRT_SETUP_MARK(kDiagBinRow + blockIdx.x, 2);
-    for (int t = tid; t < tiles; t += kBinThreads) {
-        hist[t] = 0u;
-    }
     if (i < pp.n_pad) {
         pp.qboxes[i] = QuantizeBox(sb);
         bool needed = !real || p.fused != 0u || *p.range_tag == p.gen;  // fused: a full frame, every record
@@ -1976,8 +1978,6 @@ __global__ __launch_bounds__(kBinThreads) void PrepareBinKernel(const Frames bat
             pp.cull[i] = r;
         }
     }
-    __syncthreads();  // histogram zeroed
-    SRT_SETUP_MARK(kDiagBinRow + blockIdx.x, 3);
 
     // The record's tile range (bit k of the mask below = tile (r0 + k / w, c0 + k % w) of the
     // range, at most kLargeTiles of them).
@@ -2049,13 +2049,37 @@ __global__ __launch_bounds__(kBinThreads) void PrepareBinKernel(const Frames bat
             }
         }
     }
+    // The block's tile span: its records are spatial neighbours (Morton order), so the tiles they
+    // are binned to lie in a few tile rows -- the histogram is zeroed and scanned only there (a
+    // pass over every tile per block was O(blocks x tiles): 3907 x 8100 at C5).
+    unsigned t_lo = mask != 0u ? static_cast<unsigned>(rd.Tile(__builtin_ctz(mask), r0, c0, nx)) : ~0u;
+    unsigned t_hi = mask != 0u ? static_cast<unsigned>(rd.Tile(31 - __builtin_clz(mask), r0, c0, nx)) : 0u;
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+        t_lo = min(t_lo, static_cast<unsigned>(__shfl_xor(static_cast<int>(t_lo), o)));
+        t_hi = max(t_hi, static_cast<unsigned>(__shfl_xor(static_cast<int>(t_hi), o)));
+    }
+    if ((tid & (kWave - 1)) == 0) {
+        atomicMin(&bin_span[0], t_lo);
+        atomicMax(&bin_span[1], t_hi);
+    }
+    __syncthreads();
+    t_lo = bin_span[0];
+    t_hi = bin_span[1];
+    const unsigned span_n = t_lo <= t_hi ? t_hi - t_lo + 1u : 0u;  // no listed record: empty
+    for (unsigned k = static_cast<unsigned>(tid); k < span_n; k += kBinThreads) {
+        hist[t_lo + k] = 0u;
+    }
+    __syncthreads();  // the span's histogram zeroed
+    SRT_SETUP_MARK(kDiagBinRow + blockIdx.x, 3);
     for (unsigned m = (p.exp & 8u) ? 0u : mask; m != 0u; m &= m - 1u) {  // diag timing: 8 skips the counts
         const int k = __builtin_ctz(m);
         atomicAdd(&hist[rd.Tile(k, r0, c0, nx)], 1u);
     }
     __syncthreads();
     SRT_SETUP_MARK(kDiagBinRow + blockIdx.x, 4);
-    for (int t = tid; t < tiles; t += kBinThreads) {
+    for (unsigned k = static_cast<unsigned>(tid); k < span_n; k += kBinThreads) {
+        const unsigned t = t_lo + k;
         const unsigned h = hist[t];
         if (h != 0u) {
             hist[t] = (p.exp & 4u) ? 0u : atomicAdd(&p.counts[t], h);  // this block's base in the list
