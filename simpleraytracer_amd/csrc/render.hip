@@ -2139,7 +2139,6 @@ __global__ __launch_bounds__(kOrderBlock) void WorkOrderKernel(const Frames batc
     __shared__ unsigned local[kOrderBuckets];   // this block's descriptors per bucket
     __shared__ unsigned sums[4];  // candidates / 16, parts, this block's split slots, earlier blocks' slots
     extern __shared__ unsigned order_lds[];     // per tile: candidates, then flags | parts << 2 (bytes)
-    constexpr int kU = kOrderTilesPerThread;
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
     const unsigned tiles = static_cast<unsigned>(p.tiles_x * p.tiles_y);
@@ -2147,8 +2146,22 @@ __global__ __launch_bounds__(kOrderBlock) void WorkOrderKernel(const Frames batc
     unsigned* cnt = order_lds;
     unsigned char* meta = reinterpret_cast<unsigned char*>(order_lds + tiles);
     SRT_SETUP_MARK(kDiagOrderRow + blockIdx.x, 0);
-    // Every load the block needs, issued together: this thread's own tile's info (its descriptor),
-    // the large list's length and first records, and every tile's list length and flags.
+    // The loads on the block's critical path first -- every tile's list length and flags, this
+    // thread's own tile's info (its descriptor), the large list's length --, the rest after them
+    // (the large list's first records, read after the items: a dependent chain of three round
+    // trips that would otherwise delay the tiles' loads).
+    constexpr int kU = kOrderTilesPerThread;
+    unsigned c[kU], cn[kU];
+    uint2 ru[kU], rn[kU];  // (regular, usable)
+    auto load_step = [&](unsigned t0, unsigned (&cc)[kU], uint2 (&rr)[kU]) {
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const unsigned t = min(t0 + u * kOrderBlock, tiles - 1u);
+            cc[u] = p.counts[t];
+            rr[u] = *reinterpret_cast<const uint2*>(&p.tile_info[t].regular);
+        }
+    };
+    load_step(tid, c, ru);
     const unsigned mine = first + static_cast<unsigned>(tid);
     const TileInfo my_ti = p.tile_info[min(mine, tiles - 1u)];
     const unsigned large = p.counts[tiles];
@@ -2163,25 +2176,11 @@ __global__ __launch_bounds__(kOrderBlock) void WorkOrderKernel(const Frames batc
     if (tid < 4) {
         sums[tid] = 0u;
     }
-    if (tid < kEmptyTest && static_cast<unsigned>(tid) < large && large <= static_cast<unsigned>(kEmptyTest)) {
-        lrec[tid] = p.cull[p.large_list[tid]];  // read after the barriers below
-    }
     // (1) every tile's item into LDS, the frame's candidate and part totals; the next step's loads
     // are issued before this step's items are made (4K frames: 8100 tiles, four steps of 2048, whose
     // load round trips would otherwise follow one another)
     unsigned long long my_cand = 0ull;
     unsigned my_parts = 0u;
-    unsigned c[kU], cn[kU];
-    uint2 ru[kU], rn[kU];  // (regular, usable)
-    auto load_step = [&](unsigned t0, unsigned (&cc)[kU], uint2 (&rr)[kU]) {
-#pragma unroll
-        for (int u = 0; u < kU; ++u) {
-            const unsigned t = min(t0 + u * kOrderBlock, tiles - 1u);
-            cc[u] = p.counts[t];
-            rr[u] = *reinterpret_cast<const uint2*>(&p.tile_info[t].regular);
-        }
-    };
-    load_step(tid, c, ru);
     for (unsigned t0 = tid; t0 < tiles; t0 += kU * kOrderBlock) {
         const unsigned next = t0 + kU * kOrderBlock;
         if (next < tiles) {
@@ -2206,6 +2205,9 @@ __global__ __launch_bounds__(kOrderBlock) void WorkOrderKernel(const Frames batc
             c[u] = cn[u];
             ru[u] = rn[u];
         }
+    }
+    if (tid < kEmptyTest && static_cast<unsigned>(tid) < large && large <= static_cast<unsigned>(kEmptyTest)) {
+        lrec[tid] = p.cull[p.large_list[tid]];  // read after the barriers below
     }
     unsigned v16 = static_cast<unsigned>((my_cand + 15ull) >> 4), vp = my_parts;
 #pragma unroll
