@@ -2111,7 +2111,11 @@ __global__ __launch_bounds__(kBinThreads) void PrepareBinKernel(const Frames bat
 // kernel's first multi-block form: 11.0 us one frame in flight, three dependent atomic round trips.)
 constexpr int kOrderBlock = 256;
 constexpr int kOrderTilesPerThread = 8;  // tiles' loads in flight per thread (one pass at 1080p: 2040 tiles)
-constexpr int kOrderCopies = 8;          // LDS copies of the bucket histograms (lanes spread over them)
+#ifndef SRT_ORDER_COPIES
+#define SRT_ORDER_COPIES 16
+#endif
+constexpr int kOrderCopies = SRT_ORDER_COPIES;  // LDS copies of the bucket histograms (lane l: copy l % copies)
+constexpr int kOrderStride = kOrderBuckets + 1;  // words per copy: the copies of one bucket in different banks
 #ifdef SRT_ORDER_SINGLE  // measurement builds only: round 2's single-block counting sort
 #ifndef SRT_ORDER_THREADS
 #define SRT_ORDER_THREADS 1024
@@ -2133,8 +2137,8 @@ template <class Frames>
 __global__ __launch_bounds__(kOrderBlock) void WorkOrderKernel(const Frames batch) {
     const BinParams& p = batch[blockIdx.z];
     __shared__ CullRecord lrec[kEmptyTest];
-    __shared__ unsigned hist8[kOrderCopies][kOrderBuckets];    // descriptors per bucket (the frame)
-    __shared__ unsigned before8[kOrderCopies][kOrderBuckets];  // ... of the tiles of earlier blocks
+    __shared__ unsigned hist8[kOrderCopies][kOrderStride];    // descriptors per bucket (the frame)
+    __shared__ unsigned before8[kOrderCopies][kOrderStride];  // ... of the tiles of earlier blocks
     __shared__ unsigned hist[kOrderBuckets];    // this block's first descriptor per bucket
     __shared__ unsigned local[kOrderBuckets];   // this block's descriptors per bucket
     __shared__ unsigned sums[4];  // candidates / 16, parts, this block's split slots, earlier blocks' slots
@@ -2169,7 +2173,7 @@ __global__ __launch_bounds__(kOrderBlock) void WorkOrderKernel(const Frames batc
     if (tid < kOrderBuckets) {
         local[tid] = 0u;
     }
-    for (int k = tid; k < kOrderCopies * kOrderBuckets; k += kOrderBlock) {
+    for (int k = tid; k < kOrderCopies * kOrderStride; k += kOrderBlock) {
         (&hist8[0][0])[k] = 0u;
         (&before8[0][0])[k] = 0u;
     }
@@ -2236,24 +2240,37 @@ __global__ __launch_bounds__(kOrderBlock) void WorkOrderKernel(const Frames batc
         shift = size <= 1ull ? 0u : shift;
     }
     // The frame's histogram and the earlier blocks' share in kOrderCopies LDS copies, lane l adding
-    // to copy l % kOrderCopies (per-tile atomics into one copy serialised on the few busy buckets:
-    // ~3.7 us of this kernel's ~9 us one frame in flight), summed after the barrier.
+    // to copy l % kOrderCopies, summed after the barrier: most tiles fall in a few buckets, and the
+    // lanes adding to one word serialise (one copy: ~3.7 us of this kernel's ~9 us one frame in
+    // flight); the copies are kOrderStride = 65 words apart, so one bucket's copies lie in
+    // different banks. A thread's kU tiles' items are read from LDS together.
     unsigned my_n = 0u, my_nch = 1u, my_bucket = 0u, slots_before = 0u;
     const unsigned copy = static_cast<unsigned>(lane) % kOrderCopies;
-    for (unsigned t = tid; t < tiles; t += kOrderBlock) {
-        const unsigned parts = meta[t] >> 2;
-        if (parts != 0u) {
-            unsigned nch, bucket;
-            ItemChunks(cnt[t], meta[t] & 3u, shift, nch, bucket);
-            const unsigned n = parts * nch;
-            atomicAdd(&hist8[copy][bucket], n);
-            if (t < first) {
-                atomicAdd(&before8[copy][bucket], n);
-                slots_before += nch > 1u ? n : 0u;
-            } else if (t == mine) {
-                my_n = n;
-                my_nch = nch;
-                my_bucket = bucket;
+    for (unsigned t0 = tid; t0 < tiles; t0 += kU * kOrderBlock) {
+        unsigned m[kU], cc[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const unsigned t = t0 + u * kOrderBlock;
+            m[u] = t < tiles ? meta[t] : 0u;
+            cc[u] = t < tiles ? cnt[t] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const unsigned t = t0 + u * kOrderBlock;
+            const unsigned parts = m[u] >> 2;
+            if (parts != 0u) {
+                unsigned nch, bucket;
+                ItemChunks(cc[u], m[u] & 3u, shift, nch, bucket);
+                const unsigned n = parts * nch;
+                atomicAdd(&hist8[copy][bucket], n);
+                if (t < first) {
+                    atomicAdd(&before8[copy][bucket], n);
+                    slots_before += nch > 1u ? n : 0u;
+                } else if (t == mine) {
+                    my_n = n;
+                    my_nch = nch;
+                    my_bucket = bucket;
+                }
             }
         }
     }
