@@ -16,7 +16,7 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -fno-s
             -fvisibility=hidden -DRADEONPROML_BUILD -Iinclude -Wall -Wno-unused-result
 LDFLAGS  := -shared -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib -Wl,--no-undefined
 
-OBJS := $(BUILD)/render.o $(BUILD)/spatial.o $(BUILD)/renderer.o $(BUILD)/engine.o $(BUILD)/cpu_render.o \
+OBJS := $(BUILD)/render.o $(BUILD)/spatial.o $(BUILD)/renderer.o $(BUILD)/engine.o $(BUILD)/comm.o $(BUILD)/cpu_render.o \
         $(BUILD)/scene.o $(BUILD)/image.o $(BUILD)/model.o $(BUILD)/context.o $(BUILD)/srt_api.o
 
 HEADERS := $(wildcard $(CSRC)/*.h) include/model_runner.h include/srt_render.h

@@ -56,6 +56,7 @@ FLOPS_PER_TEST = 12          # 3 edge functions x 2 FMA
 KERNEL_NAMES = {"lds": "TraceLdsKernel", "scalar": "TraceScalarKernel", "cull": "TraceCullKernel",
                 "bvh": "TraceBvhKernel"}
 PROFILES = REPO / "profiles"
+METRIC = "Mrays/s at 1920x1080 on 100k-tri synthetic mesh"
 
 
 def parse():
@@ -129,7 +130,12 @@ class Job:
             self.dist = dist
             self.rank = int(os.environ.get("RANK", "0"))
             local = 0 if self.one_device else int(os.environ.get("LOCAL_RANK", "0"))
-            dist.init_process_group("gloo")  # control plane; the engine's RCCL communicator moves the data
+            import datetime
+
+            # control plane only (the engine's RCCL communicator moves the data); a dead peer ends a
+            # barrier after SRT_DIST_TIMEOUT_S instead of gloo's 30 minutes
+            dist.init_process_group("gloo", timeout=datetime.timedelta(
+                seconds=float(os.environ.get("SRT_DIST_TIMEOUT_S", "300"))))
             self.world = env_world
             self.devices = [local]
         else:
@@ -293,20 +299,36 @@ def committed_profile(name, key):
         return None
 
 
-def profile_key(wl, variant, world, rows_mode):
-    """PMC summaries are keyed by the exact launch shape: the full frame at N = 1, the band at N > 1."""
-    return f"{wl}|{variant}" if world == 1 else f"{wl}|{variant}|bands{world}|{rows_mode}"
+def profile_key(wl, variant, world, rows_mode, launch_frames=1):
+    """PMC summaries are keyed by the exact launch shape: the full frame at N = 1, the band at N > 1,
+    and the frames per launch when more than one."""
+    key = f"{wl}|{variant}" if world == 1 else f"{wl}|{variant}|bands{world}|{rows_mode}"
+    return key if launch_frames == 1 else f"{key}|launch{launch_frames}"
 
 
-def roofline_fields(wl, variant, launch_rays, n_tri, kernel_ms, band_ids, height_frac, key):
-    """The trace kernel's roofline from the latency pass (one frame per launch, one in flight):
-    algorithmic bytes = each ray's offsets in + its output + the cull records it can read (all N at
-    N = 1; the band's pro-rata share at N > 1), over the kernel's HIP-event time; the measured HBM
-    traffic and VALU issue from committed rocprofv3 summaries of the same launch shape, else null."""
+def frames_per_launch(a, world):
+    """engine.h EngineOptions::launch: --launch, else env SRT_LAUNCH_FRAMES, else 8 for whole frames
+    and 64 for bands over more than one GPU; at most the batch and 256."""
+    default = 64 if world > 1 and a.mode == "bands" else 8
+    return min(a.launch or int(os.environ.get("SRT_LAUNCH_FRAMES") or default), a.frames_per_step, 256)
+
+
+def roofline_fields(wl, variant, launch_rays, launch_frames, n_tri, kernel_ms, band_ids, height_frac, key,
+                    offsets_read, measured_in):
+    """The trace kernel's roofline: its algorithmic bytes per launch over its HIP-event time.
+
+    Algorithmic bytes per frame = the framebuffer it must write (16 B RGBA per ray, or the 4-B hit id
+    on the band path) + each cull record read once (64 B; the band's pro-rata share at N > 1) + the
+    sample offsets only where the trace reads them (8 B per ray of an irregular tile: jittered
+    inputs; uniform inputs give regular tiles whose rays are computed, their offsets read once by
+    the tile-info blocks of the bin launch, counted there). Measured traffic and VALU issue from
+    committed rocprofv3 summaries of the same launch shape, else null."""
     kernel_s = kernel_ms * 1e-3
     out_bytes = 4 if band_ids else 16
+    off_bytes = 8 if offsets_read else 0
     rec_bytes = int(round(n_tri * CULL_RECORD_BYTES * height_frac))
-    alg = launch_rays * (8 + out_bytes) + rec_bytes
+    frame_bytes = launch_rays * (off_bytes + out_bytes) + rec_bytes
+    alg = launch_frames * frame_bytes
     achieved = alg / kernel_s / 1e9
     pmc = committed_profile("pmc_traffic.json", key) or {}
     roof = {
@@ -318,14 +340,16 @@ def roofline_fields(wl, variant, launch_rays, n_tri, kernel_ms, band_ids, height
         "traffic": pmc.get("hbm_bytes_per_launch"),
         "kernel": KERNEL_NAMES[variant],
         "kernel_ms": round(kernel_ms, 5),
+        "frames_per_launch": launch_frames,
         "bytes_per_launch": alg,
-        "measured_in": "latency pass: one frame per launch, one frame in flight, HIP events bound to the "
-                       "kernel's dispatch (the overlapped `value` run is timed as a whole: whole_frame below)",
+        "bytes_per_frame": frame_bytes,
+        "measured_in": measured_in,
         "profile_key": key,
-        "note": f"algorithmic bytes = launch rays x (8 B offsets in + {out_bytes} B out) + cull records x 64 B"
-                f"{'' if height_frac == 1 else ' x the band share of the rows'}; traffic = measured HBM bytes per "
-                "launch of this launch shape (rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE, profiles/pmc_traffic.json), "
-                "null when no committed pass matches it",
+        "note": f"algorithmic bytes per frame = rays x ({off_bytes} B offsets read by the trace + {out_bytes} B out) + "
+                f"cull records x 64 B{'' if height_frac == 1 else ' x the band share of the rows'}; offsets count "
+                "only where the trace loads them (irregular tiles); traffic = measured HBM bytes per launch of this "
+                "launch shape (rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE, profiles/pmc_traffic.json), null when no "
+                "committed pass matches it",
     }
     sq = committed_profile("pmc_sq.json", key)
     valu = None
@@ -335,8 +359,8 @@ def roofline_fields(wl, variant, launch_rays, n_tri, kernel_ms, band_ids, height
                 "frac": round(issue_s / kernel_s, 4),
                 "note": "SQ_INSTS_VALU (rocprofv3, profiles/pmc_sq.json) x 2 cycles per wave64 instruction "
                         "/ (1024 SIMDs x 2.4 GHz), over the kernel time"}
-    tests = launch_rays * n_tri
-    bf_bytes = launch_rays * (EDGE_BYTES_PER_TRI * n_tri + PIXEL_IO_BYTES)
+    tests = launch_frames * launch_rays * n_tri
+    bf_bytes = launch_frames * launch_rays * (EDGE_BYTES_PER_TRI * n_tri + PIXEL_IO_BYTES)
     bfe = {"bytes_per_launch": bf_bytes, "tests_per_launch": tests,
            "hbm_equivalent_gbs": round(bf_bytes / kernel_s / 1e9, 1),
            "hbm_equivalent_frac": round(bf_bytes / kernel_s / 1e9 / HBM_PEAK_GBS, 2),
@@ -419,6 +443,11 @@ def main():
     frames = a.steps * a.frames_per_step
     bad, checked = eng.verify()
     verified = job.gather([bad, checked])
+    # The dominant kernel as the timed run launches it (launch_frames frames per launch), one launch
+    # in flight: the roofline's kernel time (HIP events bound to the kernels' dispatches).
+    launch_frames = frames_per_launch(a, world)
+    n_launch = max(20, min(250, frames // launch_frames))
+    st_launch = eng.stage_times(0, n_launch, launch_frames)
     # stage times of every rank's band (single-frame launches, events on the dispatches)
     n_stage = min(1000, max(20, frames))
     st = eng.stage_times(0, n_stage)
@@ -492,8 +521,16 @@ def main():
         band = world > 1 and a.mode == "bands"
         rows0 = info["band_rows"] if band else H
         launch_rays = rows0 * W
-        key = profile_key(wl, a.variant, world if band else 1, a.rows)
-        roof, valu, bfe = roofline_fields(wl, a.variant, launch_rays, n_tri, st[3], band, rows0 / H, key)
+        key = profile_key(wl, a.variant, world if band else 1, a.rows, launch_frames)
+        offsets_read = a.offsets != "uniform"
+        roof, valu, bfe = roofline_fields(
+            wl, a.variant, launch_rays, launch_frames, n_tri, st_launch[3], band, rows0 / H, key, offsets_read,
+            f"the timed run's launch shape ({launch_frames} frames per launch), one launch in flight, "
+            f"{st_launch[0]} launches, HIP events bound to the kernel's dispatch")
+        roof1, _, _ = roofline_fields(
+            wl, a.variant, launch_rays, 1, n_tri, st[3], band, rows0 / H, profile_key(wl, a.variant, world if band
+                                                                                      else 1, a.rows, 1),
+            offsets_read, f"latency pass: one frame per launch, one in flight, {st[0]} launches")
         ms_frame = elapsed / frames * 1e3
         if band:
             par = (f"bands x{world} ({a.rows} rows) + {'RCCL' if info['rccl'] else 'device-copy'} "
@@ -501,7 +538,7 @@ def main():
         else:
             par = f"{a.mode} x{world}"
         line = {
-            "metric": "Mrays/s at 1920x1080 on 100k-tri synthetic mesh",
+            "metric": METRIC,
             "value": round(mrays, 4),
             "unit": "Mrays/s",
             "n_gpus": world,
@@ -526,14 +563,13 @@ def main():
                 "frames_per_step": a.frames_per_step,
                 "frame_queues": a.queues,
                 # engine.h EngineOptions::launch defaults when neither --launch nor SRT_LAUNCH_FRAMES is set
-                "frames_per_launch": min(a.launch or int(os.environ.get("SRT_LAUNCH_FRAMES") or
-                                                         (64 if world > 1 and a.mode == "bands" else 8)),
-                                         a.frames_per_step, 256),
+                "frames_per_launch": launch_frames,
                 "inputs": max(1, a.inputs),
                 "offsets": a.offsets,
             },
             "ms_per_frame": round(ms_frame, 6),
             "roofline": roof,
+            "roofline_single_frame": roof1,
             "whole_frame": whole_frame_fields(W, H, n_tri, ms_frame, world if a.mode == "bands" else 1),
             "stages_ms": {"prepare": round(st[1], 5), "bin": round(st[2], 5), "trace_kernel": round(st[3], 5),
                           "timed_launches": st[0],
@@ -579,5 +615,25 @@ def main():
     job.close()
 
 
+def error_line(e):
+    """A failed run's record: the same keys as the result line with value null and the error.
+    Every rank that fails prints one (the engine turns a dead peer into an error, engine.h)."""
+    return {"metric": METRIC, "value": None, "unit": "Mrays/s", "higher_is_better": True,
+            "n_gpus": int(os.environ.get("WORLD_SIZE", "0") or 0) or None, "rank": int(os.environ.get("RANK", "0") or 0),
+            "error": f"{type(e).__name__}: {e}"}
+
+
 if __name__ == "__main__":
-    main()
+    try:
+        main()
+    except SystemExit:
+        raise
+    except BaseException as exc:  # noqa: BLE001 -- a JSON error record and a non-zero exit, never a hang
+        import traceback
+
+        traceback.print_exc()
+        print(json.dumps(error_line(exc)), flush=True)
+        sys.stderr.flush()
+        # No destructors or atexit hooks: a device left in a failed state must not turn the exit
+        # into a hang (this process is never re-executed; it ends here).
+        os._exit(1)

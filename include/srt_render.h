@@ -156,6 +156,9 @@ typedef struct srt_engine_t* srt_engine;
 #define SRT_EXCHANGE_ROOT 2
 #define SRT_SPLIT_BANDS 0
 #define SRT_SPLIT_FRAMES 1
+/* srt_engine_options.flags */
+#define SRT_ENGINE_RCCL_SELF 1 /* one device: the bands path with the ids sent to itself over a one-rank
+                                  RCCL communicator (the real exchange, waits and abort on one GPU) */
 typedef struct srt_engine_options {
     int variant;    /* SRT_TRACE_* */
     size_t queues;  /* batches in flight per device (0 = 2) */
@@ -166,13 +169,18 @@ typedef struct srt_engine_options {
     int simulate;   /* measurement: srtEngineCreateRank without peers, the exchange skipped (0 = off) */
     size_t launch;  /* frames per trace launch, <= 256 (0 = env SRT_LAUNCH_FRAMES, else 8 for whole
                        frames, 64 for bands over more than one device) */
+    int flags;      /* SRT_ENGINE_* bits (0 = none) */
 } srt_engine_options;
 
 /* 128-byte RCCL unique id for srtEngineCreateRank (call on one rank, share with the others). */
 ML_API_ENTRY int srtEngineUniqueId(void* id128);
 ML_API_ENTRY srt_engine srtEngineCreate(const char* scene_path, const int* devices, size_t device_count, size_t width,
                                         size_t height, const srt_engine_options* options);
-/* Every rank calls this concurrently (RCCL communicator setup synchronises them). */
+/* Every rank calls this concurrently (RCCL communicator setup synchronises them).
+ * Failures: communicators are nonblocking and every wait behind RCCL is polled with a deadline (env
+ * SRT_COMM_TIMEOUT_S, default 60 s); when a device's worker fails, or no device progresses for that
+ * long, every communicator is aborted (ncclCommAbort) and srtEngineRun returns -1 with the first
+ * error in srtGetLastError -- never a hang. The engine then refuses further work. */
 ML_API_ENTRY srt_engine srtEngineCreateRank(const char* scene_path, int device, int rank, int world,
                                             const void* unique_id128, size_t width, size_t height,
                                             const srt_engine_options* options);
@@ -193,6 +201,16 @@ ML_API_ENTRY int srtEngineReadFrame(srt_engine engine, size_t frame, float* host
  * srtTakeStageTimes). */
 ML_API_ENTRY int srtEngineStageTimes(srt_engine engine, size_t local, size_t launches, unsigned* launched,
                                      double* prepare_ms, double* bin_ms, double* trace_ms);
+/* The same for launches of `frames` frames each (1 .. batch): one launch per stage for all of them,
+ * one launch in flight; the times are per launch. */
+ML_API_ENTRY int srtEngineStageTimesBatch(srt_engine engine, size_t local, size_t launches, size_t frames,
+                                          unsigned* launched, double* prepare_ms, double* bin_ms, double* trace_ms);
+/* Host self-test of the engine's worker pool failure handling (no device): `workers` workers, worker
+ * `failing` throws (mode 1) or stalls (mode 2) while every other worker waits for a release only the
+ * abort gives. Writes the error the run ended with into msg (truncated to msg_size - 1), the seconds
+ * it took and how often the abort hook ran. */
+ML_API_ENTRY int srtEnginePoolSelfTest(size_t workers, size_t failing, int mode, double timeout_s, double* elapsed_s,
+                                       int* abort_calls, char* msg, size_t msg_size);
 /* Shape of the run: devices in the job, local devices, rows of local device 0's band, rows of every
  * band buffer, whether the exchange uses RCCL, exchanged bytes per frame (bands, all devices). */
 ML_API_ENTRY int srtEngineInfo(srt_engine engine, size_t* devices, size_t* local_devices, size_t* band_rows,

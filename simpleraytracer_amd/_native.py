@@ -36,6 +36,7 @@ SRT_EXCHANGE_ROTATING = 1
 SRT_EXCHANGE_ROOT = 2
 SRT_SPLIT_BANDS = 0
 SRT_SPLIT_FRAMES = 1
+SRT_ENGINE_RCCL_SELF = 1  # srt_engine_options.flags
 SRT_TILE_ROWS = 16  # include/srt_render.h: rows per tile row (interleaved bands deal these)
 
 
@@ -75,6 +76,7 @@ class EngineOptions(ctypes.Structure):
         ("split", ctypes.c_int),
         ("simulate", ctypes.c_int),
         ("launch", ctypes.c_size_t),
+        ("flags", ctypes.c_int),
     ]
 
 
@@ -139,6 +141,10 @@ _SIGNATURES = {
     "srtEngineVerify": (ctypes.c_int, [ctypes.c_void_p, _PSZ, _PSZ]),
     "srtEngineReadFrame": (ctypes.c_int, [ctypes.c_void_p, _SZ, ctypes.c_void_p]),
     "srtEngineStageTimes": (ctypes.c_int, [ctypes.c_void_p, _SZ, _SZ, ctypes.POINTER(ctypes.c_uint), _PD, _PD, _PD]),
+    "srtEngineStageTimesBatch": (ctypes.c_int, [ctypes.c_void_p, _SZ, _SZ, _SZ, ctypes.POINTER(ctypes.c_uint), _PD, _PD,
+                                                _PD]),
+    "srtEnginePoolSelfTest": (ctypes.c_int, [_SZ, _SZ, ctypes.c_int, ctypes.c_double, _PD, ctypes.POINTER(ctypes.c_int),
+                                             ctypes.c_char_p, _SZ]),
     "srtEngineInfo": (ctypes.c_int, [ctypes.c_void_p, _PSZ, _PSZ, _PSZ, _PSZ, ctypes.POINTER(ctypes.c_int), _PD]),
     "srtExchangeHost": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), _SZ, _SZ, _SZ, ctypes.c_int, ctypes.c_int, _SZ,
                                        _SZ, ctypes.POINTER(ctypes.c_void_p), _PSZ, _PSZ]),

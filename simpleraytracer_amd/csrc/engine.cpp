@@ -3,6 +3,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <condition_variable>
 #include <cstdlib>
 #include <cstring>
@@ -13,16 +14,11 @@
 #include <string>
 #include <thread>
 
+#include "comm.h"
 #include "render.h"
 
 namespace srt {
 namespace {
-
-void NcclCheck(ncclResult_t res, const char* what) {
-    if (res != ncclSuccess) {
-        throw std::runtime_error(std::string("RCCL error: ") + what + ": " + ncclGetErrorString(res));
-    }
-}
 
 template <class T>
 T* DeviceAlloc(std::size_t count, const char* what) {
@@ -163,12 +159,16 @@ std::vector<std::vector<int>> ExchangeOnHost(const BandSplit& split, const Excha
 }
 
 // ---------------------------------------------------------------------------------------------
-// Worker threads: one per local device; a job runs on every worker, the caller waits. The
-// device-copy exchange synchronises the workers at a host barrier (abortable: a worker that fails
-// releases the others with an error).
+// Worker threads: one per local device; a job runs on every worker, the caller waits and watches.
+// The first failure -- a worker's exception, or no progress on any device for the comm timeout --
+// sets the shared abort flag (every worker's wait then throws), releases the host barrier and calls
+// the owner's abort hook once (ncclCommAbort: RCCL kernels waiting on a peer that will never send
+// exit, so the streams drain); the workers then get the same time again to return. Workers that
+// still do not return (stuck in a HIP call behind a hung GPU) leave the pool wedged: it is never
+// destroyed (its threads are never joined) and the engine refuses further work.
 
 struct FrameEngine::Pool {
-    explicit Pool(std::size_t n) : m_n(n) {
+    Pool(std::size_t n, CommCtl* ctl, double timeout_s) : m_n(n), m_ctl(ctl), m_timeout(timeout_s) {
         for (std::size_t i = 0; i < n; ++i) {
             m_threads.emplace_back([this, i] { Loop(i); });
         }
@@ -183,7 +183,9 @@ struct FrameEngine::Pool {
             t.join();
         }
     }
-    void Run(const std::function<void(std::size_t)>& job) {
+    void Run(const std::function<void(std::size_t)>& job, const std::function<void()>& on_abort) {
+        using Clock = std::chrono::steady_clock;
+        const auto timeout = std::chrono::duration<double>(m_timeout);
         std::unique_lock<std::mutex> lk(m_mu);
         m_job = &job;
         m_pending = m_n;
@@ -192,10 +194,61 @@ struct FrameEngine::Pool {
         m_bar_count = 0;
         ++m_gen;
         m_cv.notify_all();
-        m_done.wait(lk, [this] { return m_pending == 0; });
-        m_job = nullptr;
+        unsigned long seen = m_ctl->progress.load(std::memory_order_relaxed);
+        auto last = Clock::now(), aborted_at = last;
+        bool aborting = false;
+        while (m_pending != 0) {
+            m_done.wait_for(lk, std::chrono::milliseconds(20));
+            if (m_pending == 0) {
+                break;
+            }
+            const auto now = Clock::now();
+            const unsigned long p = m_ctl->progress.load(std::memory_order_relaxed);
+            if (p != seen) {
+                seen = p;
+                last = now;
+            }
+            if (!aborting && (m_error || now - last > timeout)) {
+                if (!m_error) {
+                    m_error = std::make_exception_ptr(std::runtime_error(
+                        "frame engine: no device made progress in " + std::to_string(timeout.count()) +
+                        " s (SRT_COMM_TIMEOUT_S); the run was aborted"));
+                }
+                aborting = true;
+                aborted_at = now;
+                m_aborted = true;
+                m_ctl->abort.store(true);
+                m_bar_cv.notify_all();
+                lk.unlock();
+                on_abort();
+                lk.lock();
+                continue;
+            }
+            if (aborting && now - aborted_at > timeout) {
+                m_wedged = true;  // workers still inside HIP calls: never joined (see above)
+                break;
+            }
+        }
+        m_job = m_wedged ? m_job : nullptr;
+        if (m_error && !aborting) {
+            // Every worker returned, one with an error: RCCL work of the others may still wait on it.
+            m_aborted = true;
+            m_ctl->abort.store(true);
+            lk.unlock();
+            on_abort();
+            lk.lock();
+        }
         if (m_error) {
-            std::rethrow_exception(m_error);
+            std::exception_ptr e = m_error;
+            if (m_wedged) {
+                try {
+                    std::rethrow_exception(e);
+                } catch (const std::exception& x) {
+                    throw std::runtime_error(std::string(x.what()) +
+                                             "; a device worker did not return after the abort (GPU unresponsive)");
+                }
+            }
+            std::rethrow_exception(e);
         }
     }
     void Barrier() {
@@ -215,6 +268,7 @@ struct FrameEngine::Pool {
             throw std::runtime_error("another device's worker failed");
         }
     }
+    bool wedged() const { return m_wedged; }
 
 private:
     void Loop(std::size_t i) {
@@ -248,12 +302,14 @@ private:
     }
 
     std::size_t m_n;
+    CommCtl* m_ctl;
+    double m_timeout;
     std::vector<std::thread> m_threads;
     std::mutex m_mu;
     std::condition_variable m_cv, m_done, m_bar_cv;
     const std::function<void(std::size_t)>* m_job = nullptr;
     std::size_t m_gen = 0, m_pending = 0, m_bar_count = 0, m_bar_gen = 0;
-    bool m_stop = false, m_aborted = false;
+    bool m_stop = false, m_aborted = false, m_wedged = false;
     std::exception_ptr m_error;
 };
 
@@ -264,6 +320,7 @@ struct FrameEngine::Queue {
     hipStream_t stream = nullptr;
     hipEvent_t traced = nullptr;     // the batch's trace done (queue stream)
     hipEvent_t exchanged = nullptr;  // the batch's exchange done (comm stream)
+    hipEvent_t drained = nullptr;    // end-of-run marker (queue stream), polled with a deadline
     int* send = nullptr;             // bands: ids for the other compositors
     int* recv = nullptr;             // bands: [P][frames composited here][buffer rows][W] ids
     float* rgba = nullptr;           // frames rendered / composited here per batch, H x W x 4 each
@@ -276,6 +333,7 @@ struct FrameEngine::Device {
     int device = 0;
     std::size_t band = 0;  // global band / rank index
     hipStream_t comm = nullptr;
+    hipEvent_t comm_drained = nullptr;
     std::vector<Queue> queues;
     float* full = nullptr;  // inputs x H x W x 2
     float* band_in = nullptr;  // inputs x band rows x W x 2
@@ -288,19 +346,18 @@ FrameEngine::FrameEngine(const Scene& scene, const std::vector<int>& devices, st
     if (devices.empty()) {
         throw std::runtime_error("FrameEngine: no devices");
     }
+    if (m_opt.rccl_self && devices.size() != 1) {
+        throw std::runtime_error("FrameEngine: the RCCL self-exchange is a one-device option");
+    }
     Init(scene, devices);
-    m_copy = m_bands && m_world > 1 && GatherByCopies(devices);
+    m_copy = m_exchange && m_world > 1 && GatherByCopies(devices);
     try {
-        if (m_bands && m_world > 1 && !m_copy) {
-            std::vector<ncclComm_t> comms(m_world);
-            std::vector<int> devs(devices);
-            NcclCheck(ncclCommInitAll(comms.data(), static_cast<int>(m_world), devs.data()), "ncclCommInitAll");
-            m_comms.assign(comms.begin(), comms.end());
+        if (m_exchange && !m_copy) {
+            m_comms = CommInitAll(devices);
+            m_comms_made = true;
         }
         AllocateQueues();
-        if (m_dev.size() > 1) {
-            m_pool = std::make_unique<Pool>(m_dev.size());
-        }
+        m_pool = std::make_unique<Pool>(m_dev.size(), m_ctl.get(), CommTimeoutSeconds());
     } catch (...) {
         Release();
         throw;
@@ -315,24 +372,61 @@ FrameEngine::FrameEngine(const Scene& scene, int device, int rank, int world, co
         throw std::runtime_error("FrameEngine: rank " + std::to_string(rank) + " outside world " +
                                  std::to_string(world));
     }
+    if (m_opt.rccl_self) {
+        throw std::runtime_error("FrameEngine: the RCCL self-exchange is a one-process option");
+    }
     Init(scene, std::vector<int>{device});
     try {
-        if (m_bands && m_world > 1 && !m_opt.simulate) {
+        if (m_exchange && !m_opt.simulate) {
             if (unique_id == nullptr) {
                 throw std::runtime_error("FrameEngine: a multi-rank band split needs the RCCL unique id");
             }
-            DeviceGuard guard(device);
-            ncclUniqueId id;
-            std::memcpy(&id, unique_id, sizeof(id));
-            ncclComm_t comm = nullptr;
-            NcclCheck(ncclCommInitRank(&comm, world, id, rank), "ncclCommInitRank");
-            m_comms.push_back(comm);
+            m_comms.push_back(CommInitRank(device, world, unique_id, rank));
+            m_comms_made = true;
         }
         AllocateQueues();
+        m_pool = std::make_unique<Pool>(1, m_ctl.get(), CommTimeoutSeconds());
     } catch (...) {
         Release();
         throw;
     }
+}
+
+std::string FrameEngine::PoolSelfTest(std::size_t workers, std::size_t failing, int mode, double timeout_s,
+                                      double* elapsed_s, int* abort_calls) {
+    CommCtl ctl;
+    int calls = 0;
+    const auto start = std::chrono::steady_clock::now();
+    std::string error;
+    {
+        Pool pool(workers, &ctl, timeout_s);
+        const std::function<void(std::size_t)> job = [&](std::size_t i) {
+            if (i == failing && mode == Injection::kFail) {
+                throw std::runtime_error("injected failure of worker " + std::to_string(i));
+            }
+            // Everyone else -- and the stalled worker -- waits like a worker behind a peer that will
+            // never send: only the abort releases it (bounded, so a broken pool fails the test).
+            while (!ctl.abort.load()) {
+                if (std::chrono::steady_clock::now() - start > std::chrono::duration<double>(20 * timeout_s)) {
+                    throw std::runtime_error("worker " + std::to_string(i) + " was never released");
+                }
+                std::this_thread::sleep_for(std::chrono::milliseconds(1));
+            }
+            throw std::runtime_error("worker " + std::to_string(i) + " released by the abort");
+        };
+        try {
+            pool.Run(job, [&calls] { ++calls; });
+        } catch (const std::exception& e) {
+            error = e.what();
+        }
+    }
+    if (elapsed_s != nullptr) {
+        *elapsed_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - start).count();
+    }
+    if (abort_calls != nullptr) {
+        *abort_calls = calls;
+    }
+    return error;
 }
 
 void FrameEngine::UniqueId(void* out128) {
@@ -356,18 +450,23 @@ void FrameEngine::Init(const Scene& scene, const std::vector<int>& devices) {
         (m_opt.split != EngineOptions::kBands && m_opt.split != EngineOptions::kFrames)) {
         throw std::runtime_error("FrameEngine: unknown exchange or split");
     }
+    m_bands = m_opt.split == EngineOptions::kBands;
+    if (m_opt.rccl_self && !m_bands) {
+        throw std::runtime_error("FrameEngine: the RCCL self-exchange needs the bands split");
+    }
+    m_exchange = m_bands && (m_world > 1 || m_opt.rccl_self);
     if (m_opt.launch == 0) {
         const char* v = std::getenv("SRT_LAUNCH_FRAMES");
         const long l = v == nullptr || *v == '\0' ? 0 : std::strtol(v, nullptr, 10);
-        const bool bands = m_opt.split == EngineOptions::kBands && m_world > 1;
-        m_opt.launch = l > 0 ? static_cast<std::size_t>(l) : bands ? kDefaultBandLaunch : kMaxBatch;
+        m_opt.launch = l > 0 ? static_cast<std::size_t>(l) : m_exchange ? kDefaultBandLaunch : kMaxBatch;
     }
     m_opt.launch = std::min({m_opt.launch, m_opt.batch, static_cast<std::size_t>(kMaxTableFrames)});
-    m_bands = m_opt.split == EngineOptions::kBands;
     {  // measurement only: whole frames (P = 1, or split frames) with deferred shading
         const char* v = std::getenv("SRT_DEFER_SHADE");
-        m_defer_shade = v != nullptr && std::strcmp(v, "1") == 0 && !(m_bands && m_world > 1);
+        m_defer_shade = v != nullptr && std::strcmp(v, "1") == 0 && !m_exchange;
     }
+    m_inject = Injection::FromEnv();
+    m_ctl = std::make_unique<CommCtl>();
     m_split = BandSplit::Make(m_height, m_bands ? m_world : 1, m_opt.interleaved);
     m_plan.bands = m_split.bands;
     m_plan.batch = m_opt.batch;
@@ -385,21 +484,22 @@ void FrameEngine::Init(const Scene& scene, const std::vector<int>& devices) {
 }
 
 void FrameEngine::AllocateQueues() {
-    const bool exchange = m_bands && m_world > 1;
     const std::size_t band_pixels = m_split.BufferRows() * m_width;
     const std::size_t frame_floats4 = m_width * m_height * 4;
     for (auto& dp : m_dev) {
         Device& d = *dp;
         DeviceGuard guard(d.device);
         HipCheck(hipStreamCreateWithFlags(&d.comm, hipStreamNonBlocking), "hipStreamCreate(comm)");
+        HipCheck(hipEventCreateWithFlags(&d.comm_drained, hipEventDisableTiming), "hipEventCreate(comm drained)");
         d.queues.resize(m_opt.queues);
         for (Queue& q : d.queues) {
             HipCheck(hipStreamCreateWithFlags(&q.stream, hipStreamNonBlocking), "hipStreamCreate(queue)");
             HipCheck(hipEventCreateWithFlags(&q.traced, hipEventDisableTiming), "hipEventCreate(traced)");
             HipCheck(hipEventCreateWithFlags(&q.exchanged, hipEventDisableTiming), "hipEventCreate(exchanged)");
+            HipCheck(hipEventCreateWithFlags(&q.drained, hipEventDisableTiming), "hipEventCreate(drained)");
             q.scene = std::make_unique<DeviceScene>(*m_scene, d.device);
             q.scene->Prepare(m_width, m_height, q.stream);
-            if (exchange) {
+            if (m_exchange) {
                 const std::size_t send_frames = m_plan.exchange == EngineOptions::kAllToAll
                                                     ? m_world * m_plan.MaxFramesPerCompositor()
                                                     : m_plan.batch;
@@ -420,26 +520,58 @@ void FrameEngine::AllocateQueues() {
 
 FrameEngine::~FrameEngine() { Release(); }
 
+void FrameEngine::AbortComms() noexcept {
+    m_ctl->abort.store(true);
+    std::unique_lock<std::shared_mutex> lk(m_ctl->mu);
+    CommAbortAll(m_comms);
+}
+
 void FrameEngine::Release() noexcept {
+    if (m_pool && m_pool->wedged()) {
+        (void)m_pool.release();  // its threads are stuck in HIP calls: never joined (Pool above)
+        m_wedged = true;
+    }
     m_pool.reset();
+    if (!m_failed.empty() && !m_comms.empty()) {
+        AbortComms();  // a failed run: peers may never send what our RCCL kernels wait for
+    }
+    // Bounded drains: a wedged GPU must not turn the release into a hang.
+    const double t = CommTimeoutSeconds();
+    bool drained = !m_wedged;
     for (auto& dp : m_dev) {
-        if (!dp) {
+        if (!dp || !drained) {
             continue;
         }
         (void)hipSetDevice(dp->device);
         for (Queue& q : dp->queues) {
-            if (q.stream != nullptr) {
-                (void)hipStreamSynchronize(q.stream);
+            if (q.stream != nullptr && !StreamDrain(q.stream, t)) {
+                drained = false;
             }
         }
-        if (dp->comm != nullptr) {
-            (void)hipStreamSynchronize(dp->comm);
+        if (dp->comm != nullptr && drained && !StreamDrain(dp->comm, t)) {
+            drained = false;
         }
     }
-    for (void* c : m_comms) {
-        (void)ncclCommDestroy(static_cast<ncclComm_t>(c));
+    if (!m_comms.empty()) {
+        if (drained) {
+            CommDestroyAll(m_comms);
+        } else {
+            AbortComms();
+        }
     }
-    m_comms.clear();
+    if (!drained) {
+        // Device memory still in use by work that never finished: hipFree would wait for it. Leak it.
+        for (auto& dp : m_dev) {
+            if (dp) {
+                for (Queue& q : dp->queues) {
+                    (void)q.scene.release();
+                }
+                (void)dp.release();
+            }
+        }
+        m_dev.clear();
+        return;
+    }
     for (auto& dp : m_dev) {
         if (!dp) {
             continue;
@@ -452,22 +584,25 @@ void FrameEngine::Release() noexcept {
             (void)hipFree(q.rgba);
             q.send = q.recv = nullptr;
             q.rgba = nullptr;
-            if (q.traced != nullptr) {
-                (void)hipEventDestroy(q.traced);
-            }
-            if (q.exchanged != nullptr) {
-                (void)hipEventDestroy(q.exchanged);
+            for (hipEvent_t* e : {&q.traced, &q.exchanged, &q.drained}) {
+                if (*e != nullptr) {
+                    (void)hipEventDestroy(*e);
+                    *e = nullptr;
+                }
             }
             if (q.stream != nullptr) {
                 (void)hipStreamDestroy(q.stream);
             }
-            q.traced = q.exchanged = nullptr;
             q.stream = nullptr;
         }
         dp->queues.clear();
         (void)hipFree(dp->full);
         (void)hipFree(dp->band_in);
         dp->full = dp->band_in = nullptr;
+        if (dp->comm_drained != nullptr) {
+            (void)hipEventDestroy(dp->comm_drained);
+            dp->comm_drained = nullptr;
+        }
         if (dp->comm != nullptr) {
             (void)hipStreamDestroy(dp->comm);
             dp->comm = nullptr;
@@ -483,22 +618,34 @@ std::size_t FrameEngine::frames_rendered() const {
 }
 
 double FrameEngine::exchange_bytes_per_frame() const {
-    if (!m_bands || m_world == 1) {
+    if (!m_exchange || m_world == 1) {
         return 0.0;
     }
     return static_cast<double>(m_world - 1) * static_cast<double>(m_split.BufferRows() * m_width) * 4.0;
+}
+
+std::size_t FrameEngine::FrameIndex(std::size_t local, std::size_t b, std::size_t f) const {
+    // Split frames: each device renders frames of its own, device d's batch b being frames
+    // (b * world + d) * F + f of the sequence; otherwise every device works on frames b * F + f.
+    const std::size_t F = m_opt.batch;
+    return m_bands ? b * F + f : (b * m_world + m_dev[local]->band) * F + f;
 }
 
 void FrameEngine::SetInputs(const float* host_offsets, std::size_t count) {
     if (host_offsets == nullptr || count == 0) {
         throw std::runtime_error("SetInputs: no input frames");
     }
-    const bool exchange = m_bands && m_world > 1;
-    if (exchange && count > 1 &&
+    CheckUsable();
+    if (m_exchange && count > 1 &&
         (count % m_opt.batch != 0 || (m_plan.exchange == EngineOptions::kAllToAll && m_opt.batch % m_world != 0))) {
         throw std::runtime_error("SetInputs: with bands over " + std::to_string(m_world) + " devices, " +
                                  std::to_string(count) + " inputs need a multiple of the batch (" +
                                  std::to_string(m_opt.batch) + ") and a batch divisible by the devices");
+    }
+    if (m_defer_shade && count > 1 && count % m_opt.batch != 0) {
+        // the deferred shading of a batch reads its inputs as one evenly strided run
+        throw std::runtime_error("SetInputs: with SRT_DEFER_SHADE, " + std::to_string(count) +
+                                 " inputs need a multiple of the batch (" + std::to_string(m_opt.batch) + ")");
     }
     const std::size_t ff = FrameFloats();
     for (auto& dp : m_dev) {
@@ -514,7 +661,7 @@ void FrameEngine::SetInputs(const float* host_offsets, std::size_t count) {
         d.full = DeviceAlloc<float>(count * ff, "hipMalloc(inputs)");
         HipCheck(hipMemcpy(d.full, host_offsets, count * ff * sizeof(float), hipMemcpyHostToDevice),
                  "hipMemcpy(inputs)");
-        if (exchange) {  // the band's rows of every input, band-local and contiguous
+        if (m_exchange) {  // the band's rows of every input, band-local and contiguous
             const std::size_t row_floats = m_width * 2;
             std::vector<float> band(count * d.rows * row_floats);
             for (std::size_t r = 0; r < count; ++r) {
@@ -546,8 +693,7 @@ void FrameEngine::TracePhase(std::size_t local, std::size_t b) {
     const std::size_t qi = b % m_opt.queues;
     Queue& q = d.queues[qi];
     const std::size_t F = m_opt.batch, k0 = b * F;
-    const bool exchange = m_bands && m_world > 1;
-    if (exchange && q.used && !m_opt.simulate) {
+    if (m_exchange && q.used && !m_opt.simulate) {
         // This queue's send / receive buffers are free once its previous batch's exchange is done
         // (RCCL: on this device's comm stream; copies: every peer read our send buffer on its own).
         HipCheck(hipStreamWaitEvent(q.stream, q.exchanged, 0), "hipStreamWaitEvent(exchanged)");
@@ -567,12 +713,12 @@ void FrameEngine::TracePhase(std::size_t local, std::size_t b) {
     std::vector<float*> rgba(L);
     std::vector<int*> ids(L);
     const std::size_t frame_floats4 = m_width * m_height * 4;
-    if (!exchange) {  // whole frames, traced and shaded in one kernel
+    if (!m_exchange) {  // whole frames, traced and shaded in one kernel
         const std::size_t frame_pixels = m_width * m_height;
         for (std::size_t f0 = 0; f0 < F; f0 += L) {
             const std::size_t n = std::min(L, F - f0);
             for (std::size_t j = 0; j < n; ++j) {
-                offs[j] = FullInput(local, k0 + f0 + j);
+                offs[j] = FullInput(local, FrameIndex(local, b, f0 + j));
                 rgba[j] = q.rgba + (f0 + j) * frame_floats4;
                 ids[j] = m_defer_shade ? q.recv + (f0 + j) * frame_pixels : nullptr;
             }
@@ -581,7 +727,8 @@ void FrameEngine::TracePhase(std::size_t local, std::size_t b) {
         }
         if (m_defer_shade) {  // inputs of one batch are evenly strided (SetInputs' condition)
             const std::size_t stride = m_inputs == 1 ? 0 : FrameFloats();
-            q.scene->Shade(FullInput(local, k0), q.recv, q.rgba, 0, m_height, q.stream, F, m_height, 0, stride);
+            q.scene->Shade(FullInput(local, FrameIndex(local, b, 0)), q.recv, q.rgba, 0, m_height, q.stream, F,
+                           m_height, 0, stride);
         }
         return;
     }
@@ -595,8 +742,10 @@ void FrameEngine::TracePhase(std::size_t local, std::size_t b) {
                 const std::size_t f = f0 + j;
                 const std::size_t c = m_plan.Compositor(b, f), slot = m_plan.Slot(f);
                 offs[j] = BandInput(local, k0 + f);
-                ids[j] = c == self ? q.recv + (self * n_self + slot) * band_pixels
-                                   : q.send + SendPixels(m_plan, c, slot, band_pixels);
+                // The compositor's own band lands in its receive buffer directly, unless the
+                // self-exchange option sends it through RCCL like every other band.
+                ids[j] = c == self && !m_opt.rccl_self ? q.recv + (self * n_self + slot) * band_pixels
+                                                       : q.send + SendPixels(m_plan, c, slot, band_pixels);
             }
             q.scene->TraceBatch(offs.data(), nullptr, ids.data(), n, d.row_begin, d.rows, m_opt.variant, q.stream,
                                 m_split.Interleave());
@@ -610,24 +759,42 @@ void FrameEngine::ExchangePhase(std::size_t local, std::size_t b) {
     Queue& q = d.queues[b % m_opt.queues];
     const std::size_t band_pixels = m_split.BufferRows() * m_width;
     const std::size_t self = d.band, n_self = m_plan.FramesFor(b, self);
-    auto comm = static_cast<ncclComm_t>(m_comms[local]);
     HipCheck(hipStreamWaitEvent(d.comm, q.traced, 0), "hipStreamWaitEvent(traced)");
-    for (std::size_t p = 0; p < m_world; ++p) {
-        if (p == self) {
-            continue;
+    {
+        // The communicator is touched only under the shared lock and before an abort (comm.h).
+        std::shared_lock<std::shared_mutex> lk(m_ctl->mu);
+        if (m_ctl->abort.load()) {
+            throw std::runtime_error("exchange: aborted (another device's worker failed)");
         }
-        const std::size_t n_p = m_plan.FramesFor(b, p);
-        if (n_p != 0) {
-            NcclCheck(ncclSend(q.send + SendPixels(m_plan, p, 0, band_pixels), n_p * band_pixels, ncclInt32,
-                               static_cast<int>(p), comm, d.comm),
-                      "ncclSend(band ids)");
+        auto comm = static_cast<ncclComm_t>(m_comms[local]);
+        NcclCheck(ncclGroupStart(), "ncclGroupStart");
+        ncclResult_t first = ncclSuccess;
+        auto note = [&first](ncclResult_t r) {
+            if (r != ncclSuccess && r != ncclInProgress && first == ncclSuccess) {
+                first = r;
+            }
+        };
+        for (std::size_t p = 0; p < m_world; ++p) {
+            if (p == self && !m_opt.rccl_self) {
+                continue;
+            }
+            const std::size_t n_p = m_plan.FramesFor(b, p);
+            if (n_p != 0) {
+                note(ncclSend(q.send + SendPixels(m_plan, p, 0, band_pixels), n_p * band_pixels, ncclInt32,
+                              static_cast<int>(p), comm, d.comm));
+            }
+            if (n_self != 0) {
+                note(ncclRecv(q.recv + p * n_self * band_pixels, n_self * band_pixels, ncclInt32, static_cast<int>(p),
+                              comm, d.comm));
+            }
         }
-        if (n_self != 0) {
-            NcclCheck(ncclRecv(q.recv + p * n_self * band_pixels, n_self * band_pixels, ncclInt32, static_cast<int>(p),
-                               comm, d.comm),
-                      "ncclRecv(band ids)");
-        }
+        const ncclResult_t end = ncclGroupEnd();
+        NcclCheck(first, "ncclSend / ncclRecv (band ids)");
+        NcclCheck(end, "ncclGroupEnd (band ids)", true);
     }
+    // Nonblocking communicator: the group's kernels are on the comm stream once it settles.
+    CommSettle(&m_comms[local], 1, "exchange enqueue (band ids)", m_ctl.get());
+    HipCheck(hipEventRecord(q.exchanged, d.comm), "hipEventRecord(exchanged)");
 }
 
 void FrameEngine::CopyPhase(std::size_t local, std::size_t b) {
@@ -673,41 +840,62 @@ void FrameEngine::ShadePhase(std::size_t local, std::size_t b) {
                    m_split.interleaved ? m_world : 0, stride);
 }
 
+void FrameEngine::Inject(std::size_t local, std::size_t b) {
+    if (m_inject.kind == Injection::kNone || m_inject.local != local || m_inject.batch != b) {
+        return;
+    }
+    const std::string where = "local device " + std::to_string(local) + ", batch " + std::to_string(b);
+    if (m_inject.kind == Injection::kFail) {
+        throw std::runtime_error("injected failure (SRT_ENGINE_INJECT) on " + where);
+    }
+    // A stall: this worker stops making progress, as one stuck behind a dead peer would, until the
+    // run is aborted (bounded, so a broken watchdog shows as a test failure rather than a hang).
+    const auto start = std::chrono::steady_clock::now();
+    while (!m_ctl->abort.load()) {
+        if (std::chrono::steady_clock::now() - start > std::chrono::duration<double>(10 * CommTimeoutSeconds())) {
+            throw std::runtime_error("injected stall (SRT_ENGINE_INJECT) on " + where + " was never aborted");
+        }
+        std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    }
+    throw std::runtime_error("injected stall (SRT_ENGINE_INJECT) on " + where + " ended by the abort");
+}
+
 void FrameEngine::RunWorker(std::size_t local, std::size_t b0, std::size_t batches) {
     Device& d = *m_dev[local];
     DeviceGuard guard(d.device);
-    const bool exchange = m_bands && m_world > 1;
+    const std::size_t nc = m_comms.empty() ? 0 : 1;
+    void* const* comm = nc != 0 ? &m_comms[local] : nullptr;
     for (std::size_t b = b0; b < b0 + batches; ++b) {
+        Inject(local, b);
+        if (m_ctl->abort.load(std::memory_order_relaxed)) {
+            throw std::runtime_error("run aborted: another device's worker failed");
+        }
         TracePhase(local, b);
-        if (!exchange) {
-            continue;
-        }
-        Queue& q = d.queues[b % m_opt.queues];
-        if (m_opt.simulate) {
-            ShadePhase(local, b);  // no peers: the exchange is skipped (measurement)
-            continue;
-        }
-        if (m_copy) {
-            Barrier();  // every device's trace of batch b is enqueued (its `traced` recorded)
-            CopyPhase(local, b);
-            Barrier();  // every `exchanged` recorded before any device reuses a send buffer
-        } else {
-            NcclCheck(ncclGroupStart(), "ncclGroupStart");
-            try {
+        if (m_exchange) {
+            if (m_opt.simulate) {
+                ShadePhase(local, b);  // no peers: the exchange is skipped (measurement)
+            } else if (m_copy) {
+                Barrier();  // every device's trace of batch b is enqueued (its `traced` recorded)
+                CopyPhase(local, b);
+                Barrier();  // every `exchanged` recorded before any device reuses a send buffer
+                ShadePhase(local, b);
+            } else {
                 ExchangePhase(local, b);
-            } catch (...) {
-                (void)ncclGroupEnd();
-                throw;
+                ShadePhase(local, b);
             }
-            NcclCheck(ncclGroupEnd(), "ncclGroupEnd");
-            HipCheck(hipEventRecord(q.exchanged, d.comm), "hipEventRecord(exchanged)");
         }
-        ShadePhase(local, b);
+        m_ctl->progress.fetch_add(1, std::memory_order_relaxed);
     }
+    // The end of the run: every queue and the exchange stream drained, each wait bounded and
+    // abortable (comm.h), never a bare hipStreamSynchronize behind RCCL.
     for (Queue& q : d.queues) {
-        HipCheck(hipStreamSynchronize(q.stream), "render (queue)");
+        HipCheck(hipEventRecord(q.drained, q.stream), "hipEventRecord(drained)");
     }
-    HipCheck(hipStreamSynchronize(d.comm), "render (exchange)");
+    HipCheck(hipEventRecord(d.comm_drained, d.comm), "hipEventRecord(comm drained)");
+    for (Queue& q : d.queues) {
+        CommWaitEvent(q.drained, comm, nc, "render (queue)", m_ctl.get());
+    }
+    CommWaitEvent(d.comm_drained, comm, nc, "render (exchange)", m_ctl.get());
 }
 
 void FrameEngine::Barrier() {
@@ -716,32 +904,53 @@ void FrameEngine::Barrier() {
     }
 }
 
+void FrameEngine::CheckUsable() const {
+    if (!m_failed.empty()) {
+        throw std::runtime_error("frame engine stopped after an earlier failure (" + m_failed +
+                                 "); create a new engine");
+    }
+}
+
 void FrameEngine::Run(std::size_t batches) {
     if (m_inputs == 0) {
         throw std::runtime_error("Run: SetInputs() has not been called");
     }
+    CheckUsable();
     const std::size_t b0 = m_next_batch;
     m_run_batches = batches;
     if (batches == 0) {
         return;
     }
     m_next_batch += batches;
-    if (m_pool) {
-        const std::function<void(std::size_t)> job = [this, b0, batches](std::size_t i) { RunWorker(i, b0, batches); };
-        m_pool->Run(job);
-    } else {
-        RunWorker(0, b0, batches);
+    const std::function<void(std::size_t)> job = [this, b0, batches](std::size_t i) { RunWorker(i, b0, batches); };
+    try {
+        m_pool->Run(job, [this] { AbortComms(); });
+    } catch (const std::exception& e) {
+        m_failed = e.what();
+        if (!m_comms.empty()) {
+            AbortComms();
+        }
+        throw;
     }
 }
 
 bool FrameEngine::ReadFrame(std::size_t k, float* host_rgba) {
-    const std::size_t F = m_opt.batch, b = k / F, f = k % F;
+    const std::size_t F = m_opt.batch;
+    // Frame k's batch and device (FrameIndex inverted): split frames deal each batch's frames to
+    // the devices F at a time.
+    const std::size_t per_batch = m_bands ? F : F * m_world;
+    const std::size_t b = k / per_batch, within = k % per_batch, f = within % F;
     if (b >= m_next_batch || b + m_opt.queues < m_next_batch) {
         return false;
     }
-    const bool exchange = m_bands && m_world > 1;
     std::size_t local = 0, slot = f;
-    if (exchange) {
+    if (!m_bands) {
+        const std::size_t dev = within / F;
+        if (dev < m_rank0 || dev >= m_rank0 + m_dev.size()) {
+            return false;
+        }
+        local = dev - m_rank0;
+    } else if (m_exchange) {
         const std::size_t c = m_plan.Compositor(b, f);
         if (c < m_rank0 || c >= m_rank0 + m_dev.size()) {
             return false;
@@ -755,6 +964,7 @@ bool FrameEngine::ReadFrame(std::size_t k, float* host_rgba) {
         return false;
     }
     DeviceGuard guard(d.device);
+    CheckUsable();
     HipCheck(hipStreamSynchronize(q.stream), "hipStreamSynchronize(read frame)");
     const std::size_t frame_floats4 = m_width * m_height * 4;
     HipCheck(hipMemcpy(host_rgba, q.rgba + slot * frame_floats4, frame_floats4 * sizeof(float), hipMemcpyDeviceToHost),
@@ -765,7 +975,7 @@ bool FrameEngine::ReadFrame(std::size_t k, float* host_rgba) {
 std::size_t FrameEngine::Verify(std::size_t* checked, std::size_t per_queue) {
     const std::size_t F = m_opt.batch;
     const std::size_t frame_floats4 = m_width * m_height * 4;
-    const bool exchange = m_bands && m_world > 1;
+    CheckUsable();
     std::size_t bad = 0, count = 0;
     std::vector<float> got(frame_floats4);
     for (std::size_t local = 0; local < m_dev.size(); ++local) {
@@ -789,14 +999,14 @@ std::size_t FrameEngine::Verify(std::size_t* checked, std::size_t per_queue) {
                 std::size_t taken = 0;
                 for (std::size_t f = 0; f < F && taken < per_queue; ++f) {
                     std::size_t slot = f;
-                    if (exchange) {
+                    if (m_exchange) {
                         if (m_plan.Compositor(b, f) != d.band) {
                             continue;
                         }
                         slot = m_plan.Slot(f);
                     }
                     ++taken;
-                    const std::size_t r = (b * F + f) % m_inputs;
+                    const std::size_t r = FrameIndex(local, b, f) % m_inputs;
                     if (refs[r].empty()) {
                         ref_scene.Trace(FullInput(local, r), ref_dev, 0, m_height, m_opt.variant == kTraceCull ? kTraceLds
                                                                                                               : kTraceCull,
@@ -830,9 +1040,15 @@ std::size_t FrameEngine::Verify(std::size_t* checked, std::size_t per_queue) {
     return bad;
 }
 
-DeviceScene::StageTimes FrameEngine::MeasureStages(std::size_t local, std::size_t launches) {
+DeviceScene::StageTimes FrameEngine::MeasureStages(std::size_t local, std::size_t launches, std::size_t frames) {
     if (local >= m_dev.size()) {
         throw std::runtime_error("MeasureStages: no local device " + std::to_string(local));
+    }
+    CheckUsable();
+    frames = std::max<std::size_t>(1, frames);
+    if (frames > m_opt.batch || frames > static_cast<std::size_t>(kMaxTableFrames)) {
+        throw std::runtime_error("MeasureStages: at most the batch (" + std::to_string(m_opt.batch) +
+                                 ") frames per launch");
     }
     if (m_inputs == 0) {
         throw std::runtime_error("MeasureStages: SetInputs() has not been called");
@@ -844,22 +1060,27 @@ DeviceScene::StageTimes FrameEngine::MeasureStages(std::size_t local, std::size_
         HipCheck(hipStreamSynchronize(qq.stream), "hipStreamSynchronize(stages)");
     }
     HipCheck(hipStreamSynchronize(d.comm), "hipStreamSynchronize(stages)");
-    const bool exchange = m_bands && m_world > 1;
     q.scene->TakeTimes();
     q.scene->SetTiming(true);
+    const std::size_t band_pixels = m_split.BufferRows() * m_width, frame_floats4 = m_width * m_height * 4;
+    std::vector<const float*> offs(frames);
+    std::vector<float*> rgba(frames);
+    std::vector<int*> ids(frames);
     try {
         for (std::size_t i = 0; i < launches; ++i) {
-            if (exchange) {
-                const float* offs[1] = {BandInput(local, i)};
-                int* ids[1] = {q.send};
+            for (std::size_t j = 0; j < frames; ++j) {
+                const std::size_t k = i * frames + j;
+                offs[j] = m_exchange ? BandInput(local, k) : FullInput(local, k);
+                rgba[j] = q.rgba + j * frame_floats4;
+                ids[j] = q.send + j * band_pixels;
+            }
+            if (m_exchange) {
                 if (d.rows != 0) {
-                    q.scene->TraceBatch(offs, nullptr, ids, 1, d.row_begin, d.rows, m_opt.variant, q.stream,
-                                        m_split.Interleave());
+                    q.scene->TraceBatch(offs.data(), nullptr, ids.data(), frames, d.row_begin, d.rows, m_opt.variant,
+                                        q.stream, m_split.Interleave());
                 }
             } else {
-                const float* offs[1] = {FullInput(local, i)};
-                float* rgba[1] = {q.rgba};
-                q.scene->TraceBatch(offs, rgba, nullptr, 1, 0, m_height, m_opt.variant, q.stream, 1);
+                q.scene->TraceBatch(offs.data(), rgba.data(), nullptr, frames, 0, m_height, m_opt.variant, q.stream, 1);
             }
         }
     } catch (...) {

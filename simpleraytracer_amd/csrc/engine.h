@@ -18,10 +18,15 @@
 // P == 1 traces and shades in one kernel (RGBA), no exchange.
 // Split "frames": every device renders whole frames of its own (no exchange; weak scaling).
 //
-// Devices are either all in this process (one worker thread per device, communicators from
-// ncclCommInitAll; a repeated device -- "fake devices" on a one-GPU box -- or SRT_GATHER=copy
-// exchanges by device copies instead), or one per process (rank mode: ncclCommInitRank with a
-// unique id the ranks share, one rank per GPU as torch.distributed.run launches them).
+// Devices are either all in this process (one worker thread per device, one nonblocking RCCL
+// communicator per device from one group of ncclCommInitRankConfig; a repeated device -- "fake
+// devices" on a one-GPU box -- or SRT_GATHER=copy exchanges by device copies instead), or one per
+// process (rank mode: ncclCommInitRankConfig with a unique id the ranks share, one rank per GPU as
+// torch.distributed.run launches them).
+//
+// Failures end in an error, never a hang (comm.h): every wait behind RCCL polls with a deadline
+// (SRT_COMM_TIMEOUT_S), a worker's failure or a stall of every device aborts the communicators
+// (ncclCommAbort) and Run() throws the first error; the engine then refuses further work.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -29,8 +34,10 @@
 #include <cstddef>
 #include <cstdint>
 #include <memory>
+#include <string>
 #include <vector>
 
+#include "comm.h"
 #include "renderer.h"
 #include "scene.h"
 
@@ -56,6 +63,10 @@ struct EngineOptions {
     // FrameEngine::kDefaultBandLaunch for bands at P > 1 (per-rank time at P = 8: 6.05 / 5.81 /
     // 5.84 / 5.66 us per frame).
     std::size_t launch = 0;
+    // Test / measurement: one device, the bands path with the frame's ids sent to itself over a
+    // one-rank RCCL communicator (ncclSend / ncclRecv to self) -- the real exchange, its waits and
+    // its abort path on a one-GPU box. Frames are bit-identical to the fused trace.
+    bool rccl_self = false;
 };
 
 // Row bands of an H-row frame over P devices (interleaved or contiguous), the layout every
@@ -101,6 +112,12 @@ public:
     FrameEngine& operator=(const FrameEngine&) = delete;
 
     static void UniqueId(void* out128);
+    // Host self-test of the worker pool's failure handling (no device): `workers` workers, worker
+    // `failing` throws (mode Injection::kFail) or stalls (kStall) while every other worker waits
+    // for a release only the abort gives. Returns the error Run() threw ("" if none), the seconds
+    // it took and how many times the abort hook ran.
+    static std::string PoolSelfTest(std::size_t workers, std::size_t failing, int mode, double timeout_s,
+                                    double* elapsed_s, int* abort_calls);
     static constexpr std::size_t kDefaultBandLaunch = 64;
 
     // `count` full-frame sample-offset images (count x H x W x 2 floats, host), resident on every
@@ -118,9 +135,10 @@ public:
     // Frame k (of the last Q batches) into host RGBA (H x W x 4 floats); false when frame k is not
     // resident on a local device (another rank composited it, or it is older).
     bool ReadFrame(std::size_t k, float* host_rgba);
-    // Stage times of `launches` single-frame traces of local device `local`'s band (HIP events bound
-    // to the kernels' dispatches): mean ms of tile info, record setup + bins + work list, trace.
-    DeviceScene::StageTimes MeasureStages(std::size_t local, std::size_t launches);
+    // Stage times of `launches` traces of `frames` frames each (1 .. batch; one launch per stage for
+    // all of them) of local device `local`'s band, one launch in flight (HIP events bound to the
+    // kernels' dispatches): mean ms per launch of tile info, record setup + bins + work list, trace.
+    DeviceScene::StageTimes MeasureStages(std::size_t local, std::size_t launches, std::size_t frames = 1);
 
     std::size_t devices() const { return m_world; }
     std::size_t local_devices() const { return m_dev.size(); }
@@ -128,7 +146,7 @@ public:
     std::size_t frames_rendered() const;  // this run's frames over all devices (frames split: x P)
     std::size_t band_rows(std::size_t local) const;
     std::size_t buffer_rows() const { return m_split.BufferRows(); }
-    bool uses_rccl() const { return !m_comms.empty(); }
+    bool uses_rccl() const { return m_exchange && !m_copy && !m_opt.simulate && m_comms_made; }
     std::uint64_t triangles() const { return m_n; }
     // Bytes each device sends per batch on average (bands at P > 1), for the report.
     double exchange_bytes_per_frame() const;
@@ -140,6 +158,10 @@ private:
     void Init(const Scene& scene, const std::vector<int>& devices);
     void Release() noexcept;
     void AllocateQueues();
+    void AbortComms() noexcept;  // sets the abort flag, then ncclCommAbort under the exclusive lock
+    void CheckUsable() const;    // throws once a run has failed
+    void Inject(std::size_t local, std::size_t b);  // SRT_ENGINE_INJECT (comm.h)
+    std::size_t FrameIndex(std::size_t local, std::size_t b, std::size_t f) const;  // frame of the sequence
     void TracePhase(std::size_t local, std::size_t b);
     void ExchangePhase(std::size_t local, std::size_t b);  // RCCL: inside a group
     void CopyPhase(std::size_t local, std::size_t b);      // device-copy exchange
@@ -153,13 +175,19 @@ private:
     EngineOptions m_opt;
     std::size_t m_width = 0, m_height = 0, m_world = 1, m_rank0 = 0;  // m_rank0: global index of local 0
     std::uint64_t m_n = 0;
-    bool m_bands = true;       // bands split at P > 1 (exchange + shading)
+    bool m_bands = true;       // bands split (at P > 1, or rccl_self: exchange + shading)
+    bool m_exchange = false;   // bands with an exchange: P > 1, or the one-device RCCL self-exchange
+    bool m_comms_made = false; // RCCL communicators were created (uses_rccl after an abort too)
     bool m_copy = false;       // exchange by device copies (repeated device / SRT_GATHER=copy)
     bool m_defer_shade = false;  // env SRT_DEFER_SHADE=1 (measurement): whole frames as ids + a shading launch
     BandSplit m_split;
     ExchangePlan m_plan;
     std::vector<std::unique_ptr<Device>> m_dev;
-    std::vector<void*> m_comms;  // ncclComm_t per local device
+    std::vector<void*> m_comms;  // ncclComm_t per local device (nonblocking; empty once aborted)
+    std::unique_ptr<CommCtl> m_ctl;  // abort flag, progress counter, communicator lock (comm.h)
+    Injection m_inject;
+    std::string m_failed;      // the first error of a failed run (the engine is then unusable)
+    bool m_wedged = false;     // a worker never returned from a failed run (its pool is leaked)
     std::unique_ptr<Pool> m_pool;
     std::size_t m_inputs = 0;
     std::size_t m_next_batch = 0;  // batches issued so far (the frame sequence continues across runs)

@@ -8,17 +8,12 @@
 #include <sstream>
 #include <type_traits>
 
+#include "comm.h"
 #include "engine.h"
 #include "render.h"
 
 namespace srt {
 namespace {
-
-void NcclCheck(ncclResult_t res, const char* what) {
-    if (res != ncclSuccess) {
-        throw std::runtime_error(std::string("RCCL error: ") + what + ": " + ncclGetErrorString(res));
-    }
-}
 
 template <class T>
 T* DeviceAlloc(std::size_t count, const char* what) {
@@ -324,7 +319,7 @@ void DeviceScene::EnsureEdgeSlots(std::size_t slots, hipStream_t stream) const {
     m_prepare_pending = true;
 }
 
-DeviceScene::ParamTable& DeviceScene::AcquireTable(std::size_t frames) const {
+DeviceScene::ParamTable& DeviceScene::AcquireTable(std::size_t frames, hipStream_t stream) const {
     ParamTable& t = m_tables[m_table_next];
     m_table_next = (m_table_next + 1) % kParamTables;
     if (t.pending) {
@@ -332,8 +327,11 @@ DeviceScene::ParamTable& DeviceScene::AcquireTable(std::size_t frames) const {
         t.pending = false;
     }
     if (t.frames < frames) {
-        // Launches queued earlier may still read the old device table: let the device drain first.
-        HipCheck(hipDeviceSynchronize(), "hipDeviceSynchronize(parameter table)");
+        // Launches queued earlier may still read the old device table. They all run before `stream`'s
+        // current end (calls on one scene are stream-ordered: OrderAfterPrevious ran first), so draining
+        // this stream suffices -- never a device-wide sync from an engine worker (other workers' queues
+        // and RCCL kernels waiting on peers would be waited for too).
+        HipCheck(hipStreamSynchronize(stream), "hipStreamSynchronize(parameter table)");
         (void)hipFree(t.device);
         (void)hipHostFree(t.host);
         t.device = nullptr;
@@ -391,7 +389,7 @@ void DeviceScene::TraceBatch(const float* const* d_offsets, float* const* d_rgba
                               row_count, d_ids != nullptr ? d_ids[f] : nullptr, row_interleave};
     }
     const StageEvents ev = BindStageEvents(!CullFusedInfo(row_begin, row_count, m_height, row_interleave), true);
-    ParamTable* table = frames > static_cast<std::size_t>(kMaxBatch) ? &AcquireTable(frames) : nullptr;
+    ParamTable* table = frames > static_cast<std::size_t>(kMaxBatch) ? &AcquireTable(frames, stream) : nullptr;
     const CullTable ct{table != nullptr ? table->device : nullptr, table != nullptr ? table->host : nullptr,
                        table != nullptr ? table->frames : 0};
     HipCheck(LaunchCullFrames(cf.data(), frames, m_n, m_vertices, m_shade, m_frame, m_background, m_rank, stream,
@@ -517,6 +515,7 @@ struct Renderer::Slot {
     hipStream_t copy_out = nullptr;
     std::vector<hipEvent_t> in_done;
     std::vector<hipEvent_t> traced;
+    hipEvent_t done = nullptr;  // band path: end of the frame's work on this device (polled, comm.h)
 };
 
 // The buffers of one frame size (Configure builds a new set before releasing the old one).
@@ -573,25 +572,41 @@ Renderer::Renderer(const Scene& scene, std::vector<int> devices)
         m_slots.back()->scene = std::make_unique<DeviceScene>(scene, devices[i]);
     }
     m_gather_mode = m_slots.size() > 1 ? GatherModeFor(devices) : GatherMode::kDirect;
+    if (m_slots.size() == 1) {  // SRT_GATHER=rccl on one device: the band path with a one-rank gather (tests)
+        const char* v = std::getenv("SRT_GATHER");
+        if (v != nullptr && std::strcmp(v, "rccl") == 0) {
+            m_gather_mode = GatherMode::kRccl;
+        }
+    }
     if (m_gather_mode == GatherMode::kRccl) {
-        std::vector<ncclComm_t> comms(m_slots.size());
-        NcclCheck(ncclCommInitAll(comms.data(), static_cast<int>(devices.size()), devices.data()),
-                  "ncclCommInitAll (a repeated device needs SRT_GATHER=copy or direct)");
-        m_comms.assign(comms.begin(), comms.end());
+        try {
+            m_comms = CommInitAll(devices);  // nonblocking communicators (comm.h)
+        } catch (const std::exception& e) {
+            throw std::runtime_error(std::string(e.what()) + " (a repeated device needs SRT_GATHER=copy or direct)");
+        }
     }
 }
 
 Renderer::~Renderer() {
-    SyncAll();
+    if (!SyncAll()) {
+        // Work that never finished still uses the device buffers (hipFree would wait for it): leak them.
+        CommAbortAll(m_comms);
+        for (auto& slot : m_slots) {
+            (void)slot->scene.release();
+        }
+        (void)m_buf.release();
+        return;
+    }
     if (m_buf) {
         ReleaseBuffers(*m_buf);
     }
-    for (void* c : m_comms) {
-        (void)ncclCommDestroy(static_cast<ncclComm_t>(c));
-    }
+    CommDestroyAll(m_comms);
     for (auto& slot : m_slots) {
         (void)hipSetDevice(slot->device);
         slot->scene.reset();
+        if (slot->done != nullptr) {
+            (void)hipEventDestroy(slot->done);
+        }
         for (hipEvent_t e : slot->in_done) {
             (void)hipEventDestroy(e);
         }
@@ -626,7 +641,7 @@ void Renderer::ReleaseBuffers(Buffers& b) noexcept {
 void Renderer::Configure(std::size_t width, std::size_t height) {
     const std::size_t bands = m_slots.size();
     const bool multi = bands > 1;
-    const bool gather = multi && m_gather_mode != GatherMode::kDirect;
+    const bool gather = (multi || m_gather_mode == GatherMode::kRccl) && m_gather_mode != GatherMode::kDirect;
     const BandSplit split = BandSplit::Make(height, bands, m_interleaved);
     const std::size_t band_rows = split.BufferRows();
     // Allocate everything new before releasing the old buffers (strong guarantee).
@@ -678,7 +693,10 @@ void Renderer::Configure(std::size_t width, std::size_t height) {
         throw;
     }
     if (m_buf) {
-        SyncAll();
+        if (!SyncAll()) {
+            ReleaseBuffers(*nb);
+            throw std::runtime_error("Configure: the devices did not finish earlier work");
+        }
         ReleaseBuffers(*m_buf);
     }
     m_buf = std::move(nb);
@@ -692,18 +710,20 @@ void Renderer::Configure(std::size_t width, std::size_t height) {
 }
 
 // On an exception mid-frame, copies already queued may still target the caller's host
-// buffers: wait for every stream used (ignoring their errors) before the error propagates.
-void Renderer::SyncAll() noexcept {
+// buffers: wait for every stream used (ignoring their errors) before the error propagates. Bounded
+// (comm.h): false when a stream did not drain within the comm timeout.
+bool Renderer::SyncAll() noexcept {
+    const double t = CommTimeoutSeconds();
+    bool ok = true;
     for (auto& sp : m_slots) {
         (void)hipSetDevice(sp->device);
-        (void)hipStreamSynchronize(sp->stream);
-        if (sp->copy_in != nullptr) {
-            (void)hipStreamSynchronize(sp->copy_in);
-        }
-        if (sp->copy_out != nullptr) {
-            (void)hipStreamSynchronize(sp->copy_out);
+        for (hipStream_t st : {sp->stream, sp->copy_in, sp->copy_out}) {
+            if (st != nullptr && ok && !StreamDrain(st, t)) {
+                ok = false;
+            }
         }
     }
+    return ok;
 }
 
 void Renderer::Render(const void* host_offsets, void* host_rgba) {
@@ -713,13 +733,20 @@ void Renderer::Render(const void* host_offsets, void* host_rgba) {
     int prev = -1;
     (void)hipGetDevice(&prev);
     try {
-        if (m_slots.size() == 1 && E2eChunks() > 1 && m_height >= 2 * E2eChunks()) {
+        if (m_slots.size() == 1 && m_gather_mode != GatherMode::kRccl && E2eChunks() > 1 &&
+            m_height >= 2 * E2eChunks()) {
             RenderPipelined(host_offsets, host_rgba, E2eChunks());
         } else {
             RenderBands(host_offsets, host_rgba);
         }
     } catch (...) {
-        SyncAll();
+        // A failed gather may leave RCCL kernels waiting on peers: abort the communicators first
+        // (their kernels exit, the streams drain); the model's later renders then fail loudly.
+        if (!m_comms.empty()) {
+            CommAbortAll(m_comms);
+            m_comms_aborted = true;
+        }
+        (void)SyncAll();
         if (prev >= 0) {
             (void)hipSetDevice(prev);
         }
@@ -758,7 +785,10 @@ void Renderer::RenderBands(const void* host_offsets, void* host_rgba) {
     const auto* in_bytes = static_cast<const unsigned char*>(host_offsets);
     auto* out_bytes = static_cast<unsigned char*>(host_rgba);
     const std::size_t interleave = m_interleaved && P > 1 ? P : 1;
-    const bool direct = P == 1 || m_gather_mode == GatherMode::kDirect;
+    const bool direct = (P == 1 && m_gather_mode != GatherMode::kRccl) || m_gather_mode == GatherMode::kDirect;
+    if (m_comms_aborted) {
+        throw std::runtime_error("RCCL communicators were aborted after an earlier failure; create the model again");
+    }
     for (std::size_t i = 0; i < P; ++i) {
         Slot& s = *m_slots[i];
         DeviceGuard guard(s.device);
@@ -798,18 +828,22 @@ void Renderer::RenderBands(const void* host_offsets, void* host_rgba) {
             }
         }
         if (m_gather_mode == GatherMode::kRccl) {
-            // Equal-size id bands (buffer rows each) gathered to the first device over xGMI.
+            // Equal-size id bands (buffer rows each) gathered to the first device over xGMI, one
+            // group; nonblocking communicators, so the gathers are on the streams once they settle.
             NcclCheck(ncclGroupStart(), "ncclGroupStart");
+            ncclResult_t first = ncclSuccess;
             for (std::size_t i = 0; i < P; ++i) {
                 Slot& s = *m_slots[i];
                 const ncclResult_t r = ncclGather(b.ids[i], i == 0 ? b.gather : nullptr, band_pixels, ncclInt32, 0,
                                                   static_cast<ncclComm_t>(m_comms[i]), s.stream);
-                if (r != ncclSuccess) {
-                    (void)ncclGroupEnd();
-                    NcclCheck(r, "ncclGather");
+                if (r != ncclSuccess && r != ncclInProgress && first == ncclSuccess) {
+                    first = r;
                 }
             }
-            NcclCheck(ncclGroupEnd(), "ncclGroupEnd");
+            const ncclResult_t end = ncclGroupEnd();
+            NcclCheck(first, "ncclGather");
+            NcclCheck(end, "ncclGroupEnd (gather)", true);
+            CommSettle(m_comms.data(), m_comms.size(), "gather enqueue");
         } else {
             // The same gather as device copies into the root's buffer (band i at i x buffer rows);
             // the root's stream then waits for every band's copy (an event per band).
@@ -841,9 +875,18 @@ void Renderer::RenderBands(const void* host_offsets, void* host_rgba) {
         HipCheck(hipMemcpyAsync(out_bytes, src, h * w * 4 * out_elem, hipMemcpyDeviceToHost, root.stream),
                  "hipMemcpyAsync(frame D2H)");
     }
+    // Every device's work done: polled with a deadline and the communicators' async errors (a
+    // peer that stopped becomes an error here, not a hang).
     for (auto& sp : m_slots) {
         DeviceGuard guard(sp->device);
-        HipCheck(hipStreamSynchronize(sp->stream), "render");
+        if (sp->done == nullptr) {
+            HipCheck(hipEventCreateWithFlags(&sp->done, hipEventDisableTiming), "hipEventCreate(done)");
+        }
+        HipCheck(hipEventRecord(sp->done, sp->stream), "hipEventRecord(done)");
+    }
+    for (auto& sp : m_slots) {
+        DeviceGuard guard(sp->device);
+        CommWaitEvent(sp->done, m_comms.data(), m_comms.size(), "render");
     }
 }
 

@@ -152,7 +152,7 @@ private:
     static constexpr std::size_t kParamTables = 4;
     mutable ParamTable m_tables[kParamTables];
     mutable std::size_t m_table_next = 0;
-    ParamTable& AcquireTable(std::size_t frames) const;
+    ParamTable& AcquireTable(std::size_t frames, hipStream_t stream) const;  // after OrderAfterPrevious(stream)
     // Stage-timing events, reused: per timed Prepare (begin, end), per timed Trace (bin begin,
     // bin end, begin, end); the first m_prep_timed / m_timed entries hold pending launches.
     hipEvent_t TimingEvent(std::vector<hipEvent_t>& pool, std::size_t i) const;
@@ -183,7 +183,8 @@ int TraceVariantFromEnv();
 
 // How Renderer assembles a multi-device frame (env SRT_GATHER): "rccl" = the devices' hit-id bands
 // gathered to the first device with ncclGather, which shades the frame and copies it out
-// (default for distinct devices); "copy" = the same gather by device-to-device copies (default
+// (default for distinct devices; on ONE device it selects a one-rank gather through the same band
+// path, which puts the RCCL calls, their waits and the abort on a one-GPU box); "copy" = the same gather by device-to-device copies (default
 // when a device repeats: RCCL needs distinct devices); "direct" = every device traces and shades
 // its own band and copies its rows straight into the host image (no gather).
 enum class GatherMode { kRccl, kCopy, kDirect };
@@ -222,13 +223,14 @@ private:
     void ReleaseBuffers(Buffers& b) noexcept;
     void RenderPipelined(const void* host_offsets, void* host_rgba, std::size_t chunks);
     void RenderBands(const void* host_offsets, void* host_rgba);
-    void SyncAll() noexcept;
+    bool SyncAll() noexcept;  // bounded drain of every stream; false when one did not drain
     // Host-to-device copy of rows [0, rows) of band `i` (band-local order) from a host frame.
     void CopyBandRows(std::size_t i, const unsigned char* host, std::size_t row_bytes, unsigned char* dst,
                       hipMemcpyKind kind, bool to_host, hipStream_t stream) const;
 
     std::vector<std::unique_ptr<Slot>> m_slots;
-    std::vector<void*> m_comms;  // ncclComm_t per slot when gathering with RCCL
+    std::vector<void*> m_comms;  // ncclComm_t per slot when gathering with RCCL (nonblocking, comm.h)
+    bool m_comms_aborted = false;  // a failed gather aborted them: later renders fail
     GatherMode m_gather_mode = GatherMode::kDirect;
     bool m_interleaved = true;
     std::size_t m_band_rows = 0;  // rows of every band buffer

@@ -2,6 +2,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstring>
 #include <exception>
 #include <string>
 #include <vector>
@@ -371,6 +372,10 @@ srt::EngineOptions EngineOptionsFrom(const srt_engine_options* o) {
         opt.split = o->split;
         opt.simulate = o->simulate != 0;
         opt.launch = o->launch;
+        if ((o->flags & ~SRT_ENGINE_RCCL_SELF) != 0) {
+            throw std::runtime_error("Unknown engine flags " + std::to_string(o->flags));
+        }
+        opt.rccl_self = (o->flags & SRT_ENGINE_RCCL_SELF) != 0;
     }
     return opt;
 }
@@ -491,6 +496,43 @@ ML_API_ENTRY int srtEngineStageTimes(srt_engine engine, size_t local, size_t lau
         }
         if (trace_ms != nullptr) {
             *trace_ms = t.kernel_ms;
+        }
+    });
+}
+
+ML_API_ENTRY int srtEngineStageTimesBatch(srt_engine engine, size_t local, size_t launches, size_t frames,
+                                          unsigned* launched, double* prepare_ms, double* bin_ms, double* trace_ms) {
+    return Guarded([&] {
+        if (engine == nullptr) {
+            throw std::runtime_error("Bad engine handle");
+        }
+        const srt::DeviceScene::StageTimes t = FromHandle(engine)->MeasureStages(local, launches, frames);
+        if (launched != nullptr) {
+            *launched = t.launches;
+        }
+        if (prepare_ms != nullptr) {
+            *prepare_ms = t.prepare_ms;
+        }
+        if (bin_ms != nullptr) {
+            *bin_ms = t.bin_ms;
+        }
+        if (trace_ms != nullptr) {
+            *trace_ms = t.kernel_ms;
+        }
+    });
+}
+
+ML_API_ENTRY int srtEnginePoolSelfTest(size_t workers, size_t failing, int mode, double timeout_s, double* elapsed_s,
+                                       int* abort_calls, char* msg, size_t msg_size) {
+    return Guarded([&] {
+        if (workers == 0 || workers > 64 || failing >= workers || (mode != 1 && mode != 2) || !(timeout_s > 0)) {
+            throw std::runtime_error("Bad argument");
+        }
+        const std::string e = srt::FrameEngine::PoolSelfTest(workers, failing, mode, timeout_s, elapsed_s, abort_calls);
+        if (msg != nullptr && msg_size != 0) {
+            const std::size_t n = std::min(e.size(), msg_size - 1);
+            std::memcpy(msg, e.data(), n);
+            msg[n] = '\0';
         }
     });
 }

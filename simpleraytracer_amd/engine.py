@@ -17,8 +17,8 @@ import ctypes
 import os
 
 from . import _native
-from ._native import (SRT_EXCHANGE_ALLTOALL, SRT_EXCHANGE_ROOT, SRT_EXCHANGE_ROTATING, SRT_ROWS_CONTIGUOUS,
-                      SRT_ROWS_INTERLEAVED, SRT_SPLIT_BANDS, SRT_SPLIT_FRAMES, EngineOptions)
+from ._native import (SRT_ENGINE_RCCL_SELF, SRT_EXCHANGE_ALLTOALL, SRT_EXCHANGE_ROOT, SRT_EXCHANGE_ROTATING,
+                      SRT_ROWS_CONTIGUOUS, SRT_ROWS_INTERLEAVED, SRT_SPLIT_BANDS, SRT_SPLIT_FRAMES, EngineOptions)
 from .device import TRACE_VARIANTS, SrtError
 
 EXCHANGES = {"alltoall": SRT_EXCHANGE_ALLTOALL, "rotating": SRT_EXCHANGE_ROTATING, "root": SRT_EXCHANGE_ROOT}
@@ -31,9 +31,9 @@ def _check(rc: int):
         raise SrtError(_native.last_error())
 
 
-def _options(variant, queues, batch, rows, exchange, split, simulate=False, launch=0):
+def _options(variant, queues, batch, rows, exchange, split, simulate=False, launch=0, rccl_self=False):
     return EngineOptions(TRACE_VARIANTS[variant], queues, batch, ROWS[rows], EXCHANGES[exchange], SPLITS[split],
-                         1 if simulate else 0, launch)
+                         1 if simulate else 0, launch, SRT_ENGINE_RCCL_SELF if rccl_self else 0)
 
 
 def unique_id() -> bytes:
@@ -48,14 +48,16 @@ class FrameEngine:
 
     def __init__(self, path: str, width: int, height: int, devices=(0,), variant: str = "cull", queues: int = 2,
                  batch: int = 16, rows: str = "interleaved", exchange: str = "alltoall", split: str = "bands",
-                 launch: int = 0, _handle=None):
+                 launch: int = 0, rccl_self: bool = False, _handle=None):
+        """rccl_self (one device, tests): the bands path with the frame's ids sent to itself over a
+        one-rank RCCL communicator -- the real exchange, its waits and its abort path."""
         self._lib = _native.lib()
         self.width, self.height, self.batch = width, height, batch
         self.options = {"variant": variant, "queues": queues, "batch": batch, "rows": rows, "exchange": exchange,
-                        "split": split, "launch": launch}
+                        "split": split, "launch": launch, "rccl_self": rccl_self}
         if _handle is None:
             devs = (ctypes.c_int * len(devices))(*devices)
-            opt = _options(variant, queues, batch, rows, exchange, split, launch=launch)
+            opt = _options(variant, queues, batch, rows, exchange, split, launch=launch, rccl_self=rccl_self)
             _handle = self._lib.srtEngineCreate(os.fsencode(path), devs, len(devices), width, height, ctypes.byref(opt))
         if not _handle:
             raise SrtError(_native.last_error())
@@ -109,12 +111,13 @@ class FrameEngine:
         _check(self._lib.srtEngineReadFrame(self.handle, k, out.ctypes.data))
         return out
 
-    def stage_times(self, local: int = 0, launches: int = 100):
-        """(launches, tile info ms, records + bins + work list ms, trace kernel ms): single-frame
-        traces of local device `local`'s band, HIP events bound to the kernels' dispatches."""
+    def stage_times(self, local: int = 0, launches: int = 100, frames: int = 1):
+        """(launches, tile info ms, records + bins + work list ms, trace kernel ms) per launch:
+        `launches` traces of `frames` frames each (one launch per stage for all of them, one launch
+        in flight) of local device `local`'s band, HIP events bound to the kernels' dispatches."""
         n, p, b, t = ctypes.c_uint(), ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
-        _check(self._lib.srtEngineStageTimes(self.handle, local, launches, ctypes.byref(n), ctypes.byref(p),
-                                             ctypes.byref(b), ctypes.byref(t)))
+        _check(self._lib.srtEngineStageTimesBatch(self.handle, local, launches, frames, ctypes.byref(n),
+                                                  ctypes.byref(p), ctypes.byref(b), ctypes.byref(t)))
         return n.value, p.value, b.value, t.value
 
     def info(self):
@@ -138,6 +141,18 @@ class FrameEngine:
 
     def __del__(self):
         self.close()
+
+
+def pool_self_test(workers: int, failing: int, mode: str = "fail", timeout_s: float = 1.0):
+    """Host self-test of the engine's worker pool failure handling (no device): worker `failing`
+    throws ("fail") or stalls ("stall") while the others wait for a release only the abort gives.
+    Returns (error message the run ended with, seconds taken, abort hook calls)."""
+    lib = _native.lib()
+    el, calls = ctypes.c_double(), ctypes.c_int()
+    msg = ctypes.create_string_buffer(1024)
+    _check(lib.srtEnginePoolSelfTest(workers, failing, {"fail": 1, "stall": 2}[mode], timeout_s, ctypes.byref(el),
+                                     ctypes.byref(calls), msg, len(msg)))
+    return msg.value.decode(), el.value, calls.value
 
 
 def exchange_host(band_ids, height: int, rows: str = "interleaved", exchange: str = "alltoall", batch_index: int = 0):

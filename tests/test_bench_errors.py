@@ -1,0 +1,49 @@
+"""bench.py ends a failed run with a JSON error record and a non-zero exit (never a hang or a bare
+traceback): on this CPU-only container the engine cannot find a HIP device; on the GPU box an injected
+worker failure (SRT_ENGINE_INJECT) stops the run."""
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+REPO = Path(__file__).resolve().parents[1]
+
+
+def run_bench(env_extra, *args, timeout=300):
+    env = dict(os.environ, **env_extra)
+    env.pop("WORLD_SIZE", None)
+    return subprocess.run([sys.executable, str(REPO / "bench.py"), *args], cwd=REPO, env=env, capture_output=True,
+                          text=True, timeout=timeout)
+
+
+def last_json(stdout):
+    lines = [ln for ln in stdout.splitlines() if ln.startswith("{")]
+    assert lines, stdout
+    return json.loads(lines[-1])
+
+
+def test_bench_without_gpu_prints_error_record():
+    from conftest import gpu_available
+
+    if gpu_available():
+        pytest.skip("a GPU is visible: the no-device path is not reachable")
+    r = run_bench({}, "--steps", "1", "--warmup", "0", "--no-extras", "--width", "64", "--height", "32",
+                  "--triangles", "1000")
+    assert r.returncode == 1, r.stderr[-2000:]
+    rec = last_json(r.stdout)
+    assert rec["value"] is None and rec["unit"] == "Mrays/s"
+    assert "HIP" in rec["error"] or "device" in rec["error"], rec
+
+
+@pytest.mark.gpu
+def test_bench_injected_failure_prints_error_record(gpu):
+    r = run_bench({"SRT_ENGINE_INJECT": "fail:0:1", "SRT_COMM_TIMEOUT_S": "5"}, "--steps", "3", "--warmup", "0",
+                  "--no-extras", "--width", "320", "--height", "200", "--triangles", "2000", "--frames-per-step", "8")
+    assert r.returncode == 1, r.stderr[-2000:]
+    rec = last_json(r.stdout)
+    assert rec["value"] is None and "injected failure" in rec["error"], rec
