@@ -106,3 +106,36 @@ $(AB_LIB): $(AB_OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) $(AB_OBJS) -o $@ $(LDFLAGS)
 .PHONY: ab
 ab: $(AB_LIB)
+
+# CPU sanitizer build (SURVEY.md section 5 "Build the CPU oracle with ASan/UBSan"): the library's host
+# code (every hipcc line takes each -fsanitize= after -Xarch_host: the gfx950 code objects are built as
+# usual) and the oracle under AddressSanitizer + UndefinedBehaviorSanitizer, for the CPU test suite on a
+# host without a GPU (ML_VISIBLE_DEVICES=cpu backend, scene files, the ABI, the oracle):
+#   make asan && tools/asan_tests.sh      (log: profiles/r04/asan/)
+ASAN_BUILD  := build/asan
+ASAN_LIB    := simpleraytracer_amd/lib_asan/libModelRunner.so
+ASAN_ORACLE := oracle/build_asan/libsrt_oracle.so
+ASAN_HOST   := -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host -fno-omit-frame-pointer \
+               -Xarch_host -fno-sanitize-recover=undefined
+ASAN_OBJS   := $(patsubst $(BUILD)/%,$(ASAN_BUILD)/%,$(OBJS))
+LLVM_BIN    := /opt/rocm/lib/llvm/bin
+$(ASAN_BUILD)/%.o: $(CSRC)/%.hip $(HEADERS)
+	@mkdir -p $(ASAN_BUILD)
+	$(HIPCC) $(HIPFLAGS) $(ASAN_HOST) -g -c $< -o $@
+$(ASAN_BUILD)/cpu_render.o: $(CSRC)/cpu_render.cpp $(HEADERS)
+	@mkdir -p $(ASAN_BUILD)
+	$(HIPCC) $(HIPFLAGS) $(ASAN_HOST) -g -mfma -c $< -o $@
+$(ASAN_BUILD)/%.o: $(CSRC)/%.cpp $(HEADERS)
+	@mkdir -p $(ASAN_BUILD)
+	$(HIPCC) $(HIPFLAGS) $(ASAN_HOST) -g -c $< -o $@
+# No --no-undefined: the sanitizer runtime is preloaded into the test process (tools/asan_tests.sh).
+$(ASAN_LIB): $(ASAN_OBJS)
+	@mkdir -p $(dir $(ASAN_LIB))
+	$(HIPCC) --offload-arch=$(ARCH) $(ASAN_HOST) $(ASAN_OBJS) -o $@ -shared -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+$(ASAN_ORACLE): oracle/srt_oracle.c oracle/srt_oracle.h
+	@mkdir -p $(dir $(ASAN_ORACLE))
+	$(LLVM_BIN)/clang -O1 -g -std=c11 -fPIC -ffp-contract=off -mfma -fopenmp -Wall -Wextra \
+	    -fsanitize=address,undefined -fno-omit-frame-pointer -fno-sanitize-recover=undefined \
+	    -shared oracle/srt_oracle.c -o $@ -lm -L/opt/rocm/lib/llvm/lib -Wl,-rpath,/opt/rocm/lib/llvm/lib
+.PHONY: asan
+asan: $(ASAN_LIB) $(ASAN_ORACLE)

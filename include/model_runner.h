@@ -17,7 +17,9 @@
  * GPU selection: env ML_VISIBLE_DEVICES="0,1,..." (the semantics of
  * /root/reference/model_runner/ml.h:67-71 `visible_devices`); unset = device 0.
  * Row bands are rendered on each listed device and gathered to the first one with RCCL.
- * There is no CPU fallback: without a HIP device, mlSetModelInputInfo / mlInfer return
+ * ML_VISIBLE_DEVICES=cpu (or empty) selects the CPU backend explicitly (a tile-binned CPU render of
+ * the same canonical math, bit-identical ids). It is never a silent fallback:
+ * with a GPU backend selected and no HIP device present, mlSetModelInputInfo / mlInfer return
  * ML_FAIL with the HIP error text in the model error cache.
  */
 #ifndef SRT_MODEL_RUNNER_H

@@ -14,6 +14,8 @@ import numpy as np
 
 ORACLE_DIR = Path(__file__).resolve().parent
 LIB_PATH = ORACLE_DIR / "build" / "libsrt_oracle.so"
+if os.environ.get("SRT_ORACLE_LIB"):  # the sanitizer build (make asan; tools/asan_tests.sh)
+    LIB_PATH = Path(os.environ["SRT_ORACLE_LIB"])
 
 
 class Scene(ctypes.Structure):

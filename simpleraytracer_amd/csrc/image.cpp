@@ -26,7 +26,7 @@ Image::Image(ml_image_info const* info) {
     if (info == nullptr) {
         throw std::runtime_error("Bad image information argument");
     }
-    const size_t item = DataTypeSize(info->dtype);
+    const size_t item = DataTypeSize(RawDataType(*info));
     ForEachDim([info](auto dim, char const* name) {
         if (info->*dim == 0) {
             throw std::runtime_error(std::string("Unspecified image ") + name + " dimension");

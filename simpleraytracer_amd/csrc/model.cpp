@@ -45,9 +45,9 @@ ml_status Model::SetInputInfo(ml_image_info const* info) {
         m_error_cache << "Bad info parameter";
         return ML_FAIL;
     }
-    if (m_input_info.dtype != info->dtype) {
+    if (static_cast<int>(m_input_info.dtype) != RawDataType(*info)) {
         m_error_cache << "Overriding data type " << static_cast<int>(m_input_info.dtype) << " with "
-                      << static_cast<int>(info->dtype);
+                      << RawDataType(*info);
         return ML_FAIL;
     }
     const bool dims_ok = ForEachDim([this, info](auto dim, char const* name) {
@@ -73,7 +73,7 @@ ml_status Model::SetInputInfo(ml_image_info const* info) {
     // Sizes the kernels can index (32-bit pixel coordinates) and byte counts that fit size_t.
     size_t in_bytes = 0, out_bytes = 0;
     if (info->width > kMaxFrameSide || info->height > kMaxFrameSide ||
-        !ImageBytes(info->width, info->height, info->channels, DataTypeSize(info->dtype), &in_bytes) ||
+        !ImageBytes(info->width, info->height, info->channels, DataTypeSize(RawDataType(*info)), &in_bytes) ||
         !ImageBytes(info->width, info->height, 4, 4, &out_bytes)) {
         m_error_cache << "Input image size " << info->width << " x " << info->height << " x " << info->channels
                       << " exceeds the supported maximum (" << kMaxFrameSide << " per side)";
@@ -130,8 +130,8 @@ ml_status Model::Infer(ml_image input, ml_image output) {
     if (!dims_ok) {
         return ML_FAIL;
     }
-    if (out_info.dtype != m_output_info.dtype) {
-        m_error_cache << "Output image data type " << static_cast<int>(out_info.dtype) << " does not match "
+    if (RawDataType(out_info) != static_cast<int>(m_output_info.dtype)) {
+        m_error_cache << "Output image data type " << RawDataType(out_info) << " does not match "
                       << static_cast<int>(m_output_info.dtype);
         return ML_FAIL;
     }

@@ -2371,10 +2371,10 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(c
     __shared__ CullShared sh;
 #ifdef SRT_DIAG
     const unsigned long long d_rt0 = __builtin_amdgcn_s_memrealtime();
-    const unsigned d_blk = blockIdx.y * gridDim.x + blockIdx.x;
+    const unsigned d_blk = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
     unsigned long long d_gather = 0, d_walk = 0, d_batches = 0, d_cand = 0;
     unsigned long long d_mark = __builtin_amdgcn_s_memtime();
-    auto diag_end = [&](unsigned it, unsigned ch, unsigned nch, unsigned last, unsigned full) {
+    auto diag_end = [&](unsigned it, unsigned ch, unsigned nch, unsigned last, unsigned full, unsigned fl) {
         if (threadIdx.x == 0 && d_blk < kDiagBlocks) {
             unsigned long long* d = g_srt_diag[d_blk];
             d[1] = d_gather;
@@ -2385,9 +2385,10 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(c
             d[9] = __builtin_amdgcn_s_memrealtime();
             d[10] = it;
             d[11] = ch | nch << 16 | static_cast<unsigned long long>(last) << 32;
+            d[12] = fl | static_cast<unsigned long long>(blockIdx.z) << 32;
         }
     };
-#define SRT_DIAG_END(it, ch, nch, last, full) diag_end(it, ch, nch, last, full)
+#define SRT_DIAG_END(it, ch, nch, last, full) diag_end(it, ch, nch, last, full, flags)
 #else
 #define SRT_DIAG_END(it, ch, nch, last, full)
 #endif

@@ -161,7 +161,7 @@ ML_API_ENTRY srt_device_scene srtDeviceSceneCreate(const char* path, int device)
         int count = 0;
         if (hipGetDeviceCount(&count) != hipSuccess || device < 0 || device >= count) {
             throw std::runtime_error("HIP error: device " + std::to_string(device) + " not available (" +
-                                     std::to_string(count) + " present); this renderer has no CPU path");
+                                     std::to_string(count) + " present); the device stages have no CPU path (ml* renders on the CPU with ML_VISIBLE_DEVICES=cpu)");
         }
         out = new srt::DeviceScene(scene, device);
     });
@@ -383,7 +383,8 @@ srt::EngineOptions EngineOptionsFrom(const srt_engine_options* o) {
 void CheckDevices(const int* devices, std::size_t count) {
     int present = 0;
     if (hipGetDeviceCount(&present) != hipSuccess || present <= 0) {
-        throw std::runtime_error("HIP error: no HIP device available; the frame engine has no CPU path");
+        throw std::runtime_error("HIP error: no HIP device available; the frame engine has no CPU path (ml* renders on the CPU "
+                                 "with ML_VISIBLE_DEVICES=cpu)");
     }
     for (std::size_t i = 0; i < count; ++i) {
         if (devices[i] < 0 || devices[i] >= present) {

@@ -16,6 +16,16 @@ REPO = Path(__file__).resolve().parents[1]
 if str(REPO) not in sys.path:
     sys.path.insert(0, str(REPO))
 
+# Sanitizer runs (tools/asan_tests.sh): this process has the ASan runtime preloaded and binds the
+# sanitized libraries (SRT_LIB / SRT_ORACLE_LIB, read when the bindings are imported); child
+# processes (the CLIs, bench.py) are not instrumented and run the normal build without the preload.
+if os.environ.get("SRT_ASAN_RUN"):
+    import oracle.srt_oracle  # noqa: E402,F401
+    import simpleraytracer_amd._native  # noqa: E402,F401
+
+    for _v in ("LD_PRELOAD", "SRT_LIB", "SRT_ORACLE_LIB", "SRT_ASAN_RUN"):
+        os.environ.pop(_v, None)
+
 LIB = REPO / "simpleraytracer_amd" / "lib" / "libModelRunner.so"
 ORACLE_LIB = REPO / "oracle" / "build" / "libsrt_oracle.so"
 REFERENCE = Path("/root/reference/model_runner")
