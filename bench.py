@@ -590,10 +590,16 @@ def main():
             line["ranks_stages_ms"] = [{"rank": i, "prepare": round(s[1], 5), "bin": round(s[2], 5),
                                         "trace_kernel": round(s[3], 5)} for i, s in enumerate(ranks_stages)]
             if band:
+                xb = info["exchange_bytes_per_frame"]
+                id_bytes = round(xb / max(1, (world - 1) * info["buffer_rows"] * W))
                 line["exchange"] = {"pattern": a.exchange, "transport": "RCCL" if info["rccl"] else "device copies",
-                                    "payload": "int32 hit id per pixel (deferred shading on the compositor)",
-                                    "bytes_per_frame": int(info["exchange_bytes_per_frame"]),
-                                    "rgba_f32_equivalent": int(info["exchange_bytes_per_frame"] * 4)}
+                                    "payload": ("16-bit hit-id code per pixel (render.h kId16Period: decoded exactly "
+                                                "by the compositor's shading)" if id_bytes == 2 else
+                                                "int32 hit id per pixel") + " (deferred shading on the compositor)",
+                                    "id_bytes": id_bytes,
+                                    "bytes_per_frame": int(xb),
+                                    "int32_ids_equivalent": int(xb * 4 / id_bytes),
+                                    "rgba_f32_equivalent": int(xb * 16 / id_bytes)}
         for k, v in legs.items():
             line[k] = v
         if world == 1 and not a.no_e2e and extras:

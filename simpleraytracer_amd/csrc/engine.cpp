@@ -321,8 +321,9 @@ struct FrameEngine::Queue {
     hipEvent_t traced = nullptr;     // the batch's trace done (queue stream)
     hipEvent_t exchanged = nullptr;  // the batch's exchange done (comm stream)
     hipEvent_t drained = nullptr;    // end-of-run marker (queue stream), polled with a deadline
-    int* send = nullptr;             // bands: ids for the other compositors
-    int* recv = nullptr;             // bands: [P][frames composited here][buffer rows][W] ids
+    // Id buffers, m_id_bytes per pixel (int32 ids, or 16-bit codes: render.h kId16Period).
+    unsigned char* send = nullptr;   // bands: ids for the other compositors
+    unsigned char* recv = nullptr;   // bands: [P][frames composited here][buffer rows][W] ids
     float* rgba = nullptr;           // frames rendered / composited here per batch, H x W x 4 each
     std::size_t rgba_frames = 0;
     std::size_t last_batch = 0;
@@ -473,6 +474,11 @@ void FrameEngine::Init(const Scene& scene, const std::vector<int>& devices) {
     m_plan.exchange = m_opt.exchange;
     m_scene = std::make_unique<Scene>(scene);
     m_n = scene.triangle_count();
+    {  // the exchange payload: 16-bit id codes where the scene allows them (env SRT_EXCHANGE_IDS=32: int32)
+        const char* v = std::getenv("SRT_EXCHANGE_IDS");
+        const bool force32 = v != nullptr && std::strcmp(v, "32") == 0;
+        m_id_bytes = m_exchange && Ids16Fit(m_n) && !force32 ? 2 : 4;
+    }
     for (std::size_t i = 0; i < devices.size(); ++i) {
         auto d = std::make_unique<Device>();
         d->device = devices[i];
@@ -503,14 +509,15 @@ void FrameEngine::AllocateQueues() {
                 const std::size_t send_frames = m_plan.exchange == EngineOptions::kAllToAll
                                                     ? m_world * m_plan.MaxFramesPerCompositor()
                                                     : m_plan.batch;
-                q.send = DeviceAlloc<int>(send_frames * band_pixels, "hipMalloc(send ids)");
-                q.recv = DeviceAlloc<int>(m_world * m_plan.MaxFramesPerCompositor() * band_pixels,
+                q.send = DeviceAlloc<unsigned char>(send_frames * band_pixels * m_id_bytes, "hipMalloc(send ids)");
+                q.recv = DeviceAlloc<unsigned char>(m_world * m_plan.MaxFramesPerCompositor() * band_pixels * m_id_bytes,
                                           "hipMalloc(receive ids)");
                 q.rgba_frames = m_plan.MaxFramesPerCompositor();
             } else {
                 q.rgba_frames = m_opt.batch;
                 if (m_defer_shade) {  // measurement: whole frames traced to ids, shaded by a second launch
-                    q.recv = DeviceAlloc<int>(m_opt.batch * m_width * m_height, "hipMalloc(frame ids)");
+                    q.recv = DeviceAlloc<unsigned char>(m_opt.batch * m_width * m_height * sizeof(int),
+                                                        "hipMalloc(frame ids)");
                 }
             }
             q.rgba = DeviceAlloc<float>(q.rgba_frames * frame_floats4, "hipMalloc(frames)");
@@ -621,7 +628,12 @@ double FrameEngine::exchange_bytes_per_frame() const {
     if (!m_exchange || m_world == 1) {
         return 0.0;
     }
-    return static_cast<double>(m_world - 1) * static_cast<double>(m_split.BufferRows() * m_width) * 4.0;
+    return static_cast<double>(m_world - 1) * static_cast<double>(m_split.BufferRows() * m_width) *
+           static_cast<double>(m_id_bytes);
+}
+
+int* FrameEngine::Ids(unsigned char* buf, std::size_t pixels) const {
+    return reinterpret_cast<int*>(buf + pixels * m_id_bytes);
 }
 
 std::size_t FrameEngine::FrameIndex(std::size_t local, std::size_t b, std::size_t f) const {
@@ -720,14 +732,15 @@ void FrameEngine::TracePhase(std::size_t local, std::size_t b) {
             for (std::size_t j = 0; j < n; ++j) {
                 offs[j] = FullInput(local, FrameIndex(local, b, f0 + j));
                 rgba[j] = q.rgba + (f0 + j) * frame_floats4;
-                ids[j] = m_defer_shade ? q.recv + (f0 + j) * frame_pixels : nullptr;
+                ids[j] = m_defer_shade ? reinterpret_cast<int*>(q.recv) + (f0 + j) * frame_pixels : nullptr;
             }
             q.scene->TraceBatch(offs.data(), m_defer_shade ? nullptr : rgba.data(), m_defer_shade ? ids.data() : nullptr,
                                 n, 0, m_height, m_opt.variant, q.stream, 1);
         }
         if (m_defer_shade) {  // inputs of one batch are evenly strided (SetInputs' condition)
             const std::size_t stride = m_inputs == 1 ? 0 : FrameFloats();
-            q.scene->Shade(FullInput(local, FrameIndex(local, b, 0)), q.recv, q.rgba, 0, m_height, q.stream, F,
+            q.scene->Shade(FullInput(local, FrameIndex(local, b, 0)), reinterpret_cast<const int*>(q.recv), q.rgba, 0,
+                           m_height, q.stream, F,
                            m_height, 0, stride);
         }
         return;
@@ -744,11 +757,11 @@ void FrameEngine::TracePhase(std::size_t local, std::size_t b) {
                 offs[j] = BandInput(local, k0 + f);
                 // The compositor's own band lands in its receive buffer directly, unless the
                 // self-exchange option sends it through RCCL like every other band.
-                ids[j] = c == self && !m_opt.rccl_self ? q.recv + (self * n_self + slot) * band_pixels
-                                                       : q.send + SendPixels(m_plan, c, slot, band_pixels);
+                ids[j] = c == self && !m_opt.rccl_self ? Ids(q.recv, (self * n_self + slot) * band_pixels)
+                                                       : Ids(q.send, SendPixels(m_plan, c, slot, band_pixels));
             }
             q.scene->TraceBatch(offs.data(), nullptr, ids.data(), n, d.row_begin, d.rows, m_opt.variant, q.stream,
-                                m_split.Interleave());
+                                m_split.Interleave(), m_id_bytes == 2);
         }
     }
     HipCheck(hipEventRecord(q.traced, q.stream), "hipEventRecord(traced)");
@@ -780,11 +793,13 @@ void FrameEngine::ExchangePhase(std::size_t local, std::size_t b) {
             }
             const std::size_t n_p = m_plan.FramesFor(b, p);
             if (n_p != 0) {
-                note(ncclSend(q.send + SendPixels(m_plan, p, 0, band_pixels), n_p * band_pixels, ncclInt32,
+                note(ncclSend(q.send + SendPixels(m_plan, p, 0, band_pixels) * m_id_bytes,
+                              n_p * band_pixels * m_id_bytes, ncclUint8,
                               static_cast<int>(p), comm, d.comm));
             }
             if (n_self != 0) {
-                note(ncclRecv(q.recv + p * n_self * band_pixels, n_self * band_pixels, ncclInt32, static_cast<int>(p),
+                note(ncclRecv(q.recv + p * n_self * band_pixels * m_id_bytes, n_self * band_pixels * m_id_bytes,
+                              ncclUint8, static_cast<int>(p),
                               comm, d.comm));
             }
         }
@@ -812,9 +827,9 @@ void FrameEngine::CopyPhase(std::size_t local, std::size_t b) {
             Device& peer = *m_dev[p];
             Queue& pq = peer.queues[qi];
             HipCheck(hipStreamWaitEvent(d.comm, pq.traced, 0), "hipStreamWaitEvent(peer traced)");
-            HipCheck(hipMemcpyPeerAsync(q.recv + peer.band * n_self * band_pixels, d.device,
-                                        pq.send + SendPixels(m_plan, self, 0, band_pixels), peer.device,
-                                        n_self * band_pixels * sizeof(int), d.comm),
+            HipCheck(hipMemcpyPeerAsync(q.recv + peer.band * n_self * band_pixels * m_id_bytes, d.device,
+                                        pq.send + SendPixels(m_plan, self, 0, band_pixels) * m_id_bytes, peer.device,
+                                        n_self * band_pixels * m_id_bytes, d.comm),
                      "hipMemcpyPeerAsync(band ids)");
         }
     }
@@ -836,8 +851,9 @@ void FrameEngine::ShadePhase(std::size_t local, std::size_t b) {
     const bool a2a = m_plan.exchange == EngineOptions::kAllToAll;
     const std::size_t first = k0 + (a2a ? self : 0);
     const std::size_t stride = m_inputs == 1 ? 0 : (a2a ? m_world : 1) * FrameFloats();
-    q.scene->Shade(FullInput(local, first), q.recv, q.rgba, 0, m_height, q.stream, n_self, m_split.BufferRows(),
-                   m_split.interleaved ? m_world : 0, stride);
+    q.scene->Shade(FullInput(local, first), reinterpret_cast<const int*>(q.recv), q.rgba, 0, m_height, q.stream, n_self,
+                   m_split.BufferRows(),
+                   m_split.interleaved ? m_world : 0, stride, m_id_bytes == 2);
 }
 
 void FrameEngine::Inject(std::size_t local, std::size_t b) {
@@ -1072,12 +1088,12 @@ DeviceScene::StageTimes FrameEngine::MeasureStages(std::size_t local, std::size_
                 const std::size_t k = i * frames + j;
                 offs[j] = m_exchange ? BandInput(local, k) : FullInput(local, k);
                 rgba[j] = q.rgba + j * frame_floats4;
-                ids[j] = q.send + j * band_pixels;
+                ids[j] = Ids(q.send, j * band_pixels);
             }
             if (m_exchange) {
                 if (d.rows != 0) {
                     q.scene->TraceBatch(offs.data(), nullptr, ids.data(), frames, d.row_begin, d.rows, m_opt.variant,
-                                        q.stream, m_split.Interleave());
+                                        q.stream, m_split.Interleave(), m_id_bytes == 2);
                 }
             } else {
                 q.scene->TraceBatch(offs.data(), rgba.data(), nullptr, frames, 0, m_height, m_opt.variant, q.stream, 1);

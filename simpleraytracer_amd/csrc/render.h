@@ -75,7 +75,23 @@ struct BandArgs {
     // k = 0, 1, ..., concatenated (row_begin a multiple of kCullTileRows; only the band's last tile
     // row may be partial, and then it is the frame's last).
     std::size_t row_interleave = 1;
+    // ids holds 16-bit codes (IdCode16) instead of int32 ids: the exchange payload of scenes of at
+    // most kIds16MaxTriangles triangles, half the bytes. Trace stores codes, LaunchShade decodes them.
+    bool ids16 = false;
 };
+
+// 16-bit hit-id codes (the multi-GPU exchange payload, half the bytes of int32 ids): a miss is
+// 0xFFFF, a hit on triangle i is i % 65535 (never 0xFFFF). A code c < 0xFFFF stands for the
+// triangles c, c + 65535, c + 2 * 65535, ... below the triangle count; the compositor re-runs the
+// canonical exact test of each candidate at the pixel (records recomputed from the vertices with
+// the trace's expressions, so the same bits) and takes the lexicographic minimum (t, id) of those
+// that pass. The true winner passes and beats every other triangle that covers the pixel, so the
+// decode is exact. At most kIds16MaxTriangles triangles (two candidates per code); larger scenes
+// exchange int32 ids.
+constexpr unsigned kId16Period = 65535u;
+constexpr unsigned kId16Miss = 0xFFFFu;
+constexpr std::uint64_t kIds16MaxTriangles = 2ull * kId16Period;
+inline bool Ids16Fit(std::uint64_t triangles) { return triangles <= kIds16MaxTriangles; }
 
 // Frame row of band-local row `local` (BandArgs::row_interleave).
 inline std::size_t BandFrameRow(std::size_t row_begin, std::size_t interleave, std::size_t local);

@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <cstring>
 #include <stdexcept>
+#include <type_traits>
 
 namespace srt {
 
@@ -73,6 +74,7 @@ struct TraceParams {
     const float2* __restrict__ offsets;
     float4* __restrict__ out;
     int* __restrict__ out_ids;  // non-null: store the hit id per pixel (-1 = miss) instead of RGBA
+    unsigned short* __restrict__ out_ids16;  // non-null: store the 16-bit id code (render.h IdCode16) instead
     unsigned n_pad;   // records in the edge buffer (multiple of kPadTriangles)
     unsigned n;       // records in the scene
     int tiles_x;         // cull tiles per tile row of the band
@@ -102,6 +104,7 @@ struct TraceParams {
     float du[3];
     float dv[3];
     float bg[3];
+    float eye[3];  // ray origin (the 16-bit id decode recomputes candidate records)
 };
 
 // Frames of one batched launch: block (x, y, z) works on frame z. Up to kMaxBatch frames carry
@@ -252,15 +255,18 @@ __device__ __forceinline__ unsigned PackI16(int low, int high) {
 // E(fx, fy) = n . (base + fx du + fy dv): c = (c0A, cxA, cyA, c0B, cxB, cyB, c0C, cxC, cyC).
 // Disabled (padding, degenerate, plane through the eye): NaN record, empty screen box.
 // v = the triangle's 9 vertex coordinates.
-__device__ __forceinline__ void ComputeRecord(const PrepareParams& p, const float* __restrict__ v, bool real, float c[9],
-                                              float& vol, float4& sb) {
+// The edge coefficients and vol alone (ComputeRecord without the screen box), under the frame
+// (origin, base, du, dv); returns false for a disabled record (c, vol NaN). One definition for the
+// record pass and the 16-bit id decode, so both see the same bits.
+__device__ __forceinline__ bool ComputeEdges(const float* origin, const float* base, const float* du, const float* dv,
+                                             const float* __restrict__ v, bool real, float c[9], float& vol) {
     const float qnan = __builtin_nanf("");
     bool disabled = !real;
     vol = qnan;
     if (!disabled) {
-        const float ax = v[0] - p.origin[0], ay = v[1] - p.origin[1], az = v[2] - p.origin[2];
-        const float bx = v[3] - p.origin[0], by = v[4] - p.origin[1], bz = v[5] - p.origin[2];
-        const float cx = v[6] - p.origin[0], cy = v[7] - p.origin[1], cz = v[8] - p.origin[2];
+        const float ax = v[0] - origin[0], ay = v[1] - origin[1], az = v[2] - origin[2];
+        const float bx = v[3] - origin[0], by = v[4] - origin[1], bz = v[5] - origin[2];
+        const float cx = v[6] - origin[0], cy = v[7] - origin[1], cz = v[8] - origin[2];
         float n[9];
         Cross3(bx, by, bz, cx, cy, cz, n[0], n[1], n[2]);
         Cross3(cx, cy, cz, ax, ay, az, n[3], n[4], n[5]);
@@ -278,9 +284,9 @@ __device__ __forceinline__ void ComputeRecord(const PrepareParams& p, const floa
 #pragma unroll
             for (int e = 0; e < 3; ++e) {
                 const float nx = n[3 * e], ny = n[3 * e + 1], nz = n[3 * e + 2];
-                c[3 * e + 0] = Dot3(nx, ny, nz, p.base[0], p.base[1], p.base[2]);
-                c[3 * e + 1] = Dot3(nx, ny, nz, p.du[0], p.du[1], p.du[2]);
-                c[3 * e + 2] = Dot3(nx, ny, nz, p.dv[0], p.dv[1], p.dv[2]);
+                c[3 * e + 0] = Dot3(nx, ny, nz, base[0], base[1], base[2]);
+                c[3 * e + 1] = Dot3(nx, ny, nz, du[0], du[1], du[2]);
+                c[3 * e + 2] = Dot3(nx, ny, nz, dv[0], dv[1], dv[2]);
             }
         }
     }
@@ -291,6 +297,12 @@ __device__ __forceinline__ void ComputeRecord(const PrepareParams& p, const floa
         }
         vol = qnan;
     }
+    return !disabled;
+}
+
+__device__ __forceinline__ void ComputeRecord(const PrepareParams& p, const float* __restrict__ v, bool real, float c[9],
+                                              float& vol, float4& sb) {
+    bool disabled = !ComputeEdges(p.origin, p.base, p.du, p.dv, v, real, c, vol);
     // Disabled records: an empty box (culled by every ray box the screen boxes apply to).
     sb = disabled ? make_float4(__builtin_inff(), -__builtin_inff(), __builtin_inff(), -__builtin_inff())
                   : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -519,7 +531,10 @@ __device__ __forceinline__ float4 ShadePixel(const TraceParams& p, float fx, flo
 typedef float F4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void StorePixel(const TraceParams& p, int x, int y, float fx, float fy, int id) {
     const size_t at = static_cast<size_t>(y) * p.width + x;
-    if (p.out_ids != nullptr) {
+    if (p.out_ids16 != nullptr) {
+        const unsigned short code = static_cast<unsigned short>(id < 0 ? kId16Miss : static_cast<unsigned>(id) % kId16Period);
+        __builtin_nontemporal_store(code, p.out_ids16 + at);
+    } else if (p.out_ids != nullptr) {
         __builtin_nontemporal_store(id, p.out_ids + at);
     } else {
 #ifdef SRT_EXP_NO_SHADE  // measurement builds only: store without shading
@@ -562,9 +577,49 @@ constexpr int kShadeThreads = 128;
 #define SRT_SHADE_ROWS 4
 #endif
 constexpr int kShadeRows = SRT_SHADE_ROWS;
-__global__ __launch_bounds__(kShadeThreads) void ShadeIdsKernel(TraceParams p, const int* __restrict__ ids,
+
+// (t, id) packed so that unsigned order is lexicographic order: t >= 0 here (vol > 0,
+// det > 0), so its bit pattern orders like the value.
+__device__ __forceinline__ unsigned long long HitKey(float t, int id) {
+    return (static_cast<unsigned long long>(__float_as_uint(t)) << 32) | static_cast<unsigned>(id);
+}
+
+// The hit id of a pixel from its 16-bit code (render.h IdCode16): a miss, the code's only
+// candidate, or the lexicographic minimum (t, id) over the candidates that pass the canonical exact
+// test at (fx, fy) -- EvalPacket's expressions on records ComputeEdges rebuilds from the vertices
+// (the record pass's own function): the trace's bits, so the true winner passes and wins.
+__device__ __forceinline__ int DecodeId16(const TraceParams& p, unsigned code, float fx, float fy) {
+    if (code >= kId16Miss || code >= p.n) {
+        return -1;
+    }
+    if (code + kId16Period >= p.n) {
+        return static_cast<int>(code);  // a single candidate
+    }
+    unsigned long long best = ~0ull;
+    for (unsigned c = code; c < p.n; c += kId16Period) {
+        float e[9], vol;
+        if (!ComputeEdges(p.eye, p.base, p.du, p.dv, p.vertices + 9ull * c, true, e, vol)) {
+            continue;
+        }
+        const float eA = fmaf(fy, e[2], fmaf(fx, e[1], e[0]));
+        const float eB = fmaf(fy, e[5], fmaf(fx, e[4], e[3]));
+        const float eC = fmaf(fy, e[8], fmaf(fx, e[7], e[6]));
+        const float det = (eA + eB) + eC;
+        const float t = vol / det;
+        if (fminf(fminf(eA, eB), eC) >= 0.f && det > 0.f && t < __builtin_inff()) {
+            const unsigned long long k = HitKey(t, static_cast<int>(c));
+            best = k < best ? k : best;
+        }
+    }
+    return best == ~0ull ? -1 : static_cast<int>(static_cast<unsigned>(best));
+}
+
+template <bool ID16>
+__global__ __launch_bounds__(kShadeThreads) void ShadeIdsKernel(TraceParams p, const void* __restrict__ ids_v,
                                                                 unsigned band_rows, unsigned frames,
                                                                 unsigned interleaved, size_t offsets_stride) {
+    using IdT = std::conditional_t<ID16, unsigned short, int>;
+    const IdT* __restrict__ ids = static_cast<const IdT*>(ids_v);
     const int x = static_cast<int>(blockIdx.x * kShadeThreads + threadIdx.x);
     if (x >= p.width) {
         return;
@@ -572,7 +627,7 @@ __global__ __launch_bounds__(kShadeThreads) void ShadeIdsKernel(TraceParams p, c
     const int y0 = static_cast<int>(blockIdx.y) * kShadeRows;
     const unsigned g = blockIdx.z;
     const size_t pixels = static_cast<size_t>(p.width) * p.row_count;
-    int id[kShadeRows];
+    IdT id[kShadeRows];
     float2 o[kShadeRows];
 #pragma unroll
     for (int r = 0; r < kShadeRows; ++r) {
@@ -596,7 +651,13 @@ __global__ __launch_bounds__(kShadeThreads) void ShadeIdsKernel(TraceParams p, c
         if (y < p.row_count) {
             const float fx = (static_cast<float>(x) + o[r].x) / p.wf;
             const float fy = (static_cast<float>(FrameRow(p.row_begin, p.row_interleave, y)) + o[r].y) / p.hf;
-            const float4 v = ShadePixel(p, fx, fy, static_cast<unsigned>(id[r]) < p.n ? id[r] : -1);  // no id outside the scene
+            int hit;
+            if constexpr (ID16) {
+                hit = DecodeId16(p, static_cast<unsigned>(id[r]), fx, fy);
+            } else {
+                hit = static_cast<unsigned>(id[r]) < p.n ? id[r] : -1;  // no id outside the scene
+            }
+            const float4 v = ShadePixel(p, fx, fy, hit);
             __builtin_nontemporal_store(F4{v.x, v.y, v.z, v.w},
                                         reinterpret_cast<F4*>(p.out + g * pixels + static_cast<size_t>(y) * p.width + x));
         }
@@ -920,11 +981,6 @@ static_assert(sizeof(float2) * kWave * kCullWaves <= sizeof(float4) * 2 * kPacke
 static_assert((kPacketBatch + kStreamStep) * 4 <= sizeof(float4) * 3 * kPacketBatch, "stream ids alias the planes");
 constexpr int kFlushBatches = (kPacketBatch + kStreamStep - 1 + kPacketBatch - 1) / kPacketBatch;  // per flush
 
-// (t, id) packed so that unsigned order is lexicographic order: t >= 0 here (vol > 0,
-// det > 0), so its bit pattern orders like the value.
-__device__ __forceinline__ unsigned long long HitKey(float t, int id) {
-    return (static_cast<unsigned long long>(__float_as_uint(t)) << 32) | static_cast<unsigned>(id);
-}
 
 // Candidate source of a block: LIST = positions [begin, end) of the tile's virtual list (its
 // bin list, then the large list of records binned to every tile); FULL = every record.
@@ -3294,7 +3350,8 @@ TraceParams MakeTraceParams(const float* d_edges, std::uint64_t n, const float* 
     p.shade = reinterpret_cast<const float4*>(d_shade);
     p.offsets = reinterpret_cast<const float2*>(band.offsets);
     p.out = reinterpret_cast<float4*>(band.rgba);
-    p.out_ids = band.ids;
+    p.out_ids = band.ids16 ? nullptr : band.ids;
+    p.out_ids16 = band.ids16 ? reinterpret_cast<unsigned short*>(band.ids) : nullptr;
     p.n_pad = static_cast<unsigned>(PaddedTriangleCount(n));
     p.n_tiles = static_cast<unsigned>(n == 0 ? 1 : (n + kTileTriangles - 1) / kTileTriangles);
     p.width = static_cast<int>(band.width);
@@ -3308,6 +3365,7 @@ TraceParams MakeTraceParams(const float* d_edges, std::uint64_t n, const float* 
         p.du[k] = frame.du[k];
         p.dv[k] = frame.dv[k];
         p.bg[k] = background[k];
+        p.eye[k] = frame.origin[k];
     }
     p.n = static_cast<unsigned>(n);
     p.tiles_x = static_cast<int>((band.width + kWave - 1) / kWave);
@@ -3607,14 +3665,23 @@ hipError_t LaunchShade(const float* d_vertices, const float* d_shade, const floa
         p.du[k] = frame.du[k];
         p.dv[k] = frame.dv[k];
         p.bg[k] = background[k];
+        p.eye[k] = frame.origin[k];
     }
-    hipLaunchKernelGGL(ShadeIdsKernel,
-                       dim3(static_cast<unsigned>((band.width + kShadeThreads - 1) / kShadeThreads),
-                            static_cast<unsigned>((band.row_count + kShadeRows - 1) / kShadeRows),
-                            static_cast<unsigned>(frames)),
-                       dim3(kShadeThreads), 0, stream, p, static_cast<const int*>(band.ids),
-                       static_cast<unsigned>(band_rows), static_cast<unsigned>(frames),
-                       static_cast<unsigned>(interleaved), offsets_stride / 2);
+    if (band.ids16 && !Ids16Fit(n)) {
+        return hipErrorInvalidValue;
+    }
+    const dim3 grid(static_cast<unsigned>((band.width + kShadeThreads - 1) / kShadeThreads),
+                    static_cast<unsigned>((band.row_count + kShadeRows - 1) / kShadeRows), static_cast<unsigned>(frames));
+    const void* ids = band.ids;
+    if (band.ids16) {
+        hipLaunchKernelGGL(ShadeIdsKernel<true>, grid, dim3(kShadeThreads), 0, stream, p, ids,
+                           static_cast<unsigned>(band_rows), static_cast<unsigned>(frames),
+                           static_cast<unsigned>(interleaved), offsets_stride / 2);
+    } else {
+        hipLaunchKernelGGL(ShadeIdsKernel<false>, grid, dim3(kShadeThreads), 0, stream, p, ids,
+                           static_cast<unsigned>(band_rows), static_cast<unsigned>(frames),
+                           static_cast<unsigned>(interleaved), offsets_stride / 2);
+    }
     return hipGetLastError();
 }
 

@@ -244,7 +244,11 @@ void DeviceScene::RecordOrder(hipStream_t stream) const {
 
 void DeviceScene::Shade(const float* d_offsets, const int* d_ids, float* d_rgba, std::size_t row_begin,
                         std::size_t row_count, hipStream_t stream, std::size_t frames, std::size_t band_rows,
-                        std::size_t interleaved, std::size_t offsets_stride) const {
+                        std::size_t interleaved, std::size_t offsets_stride, bool ids16) const {
+    if (ids16 && !Ids16Fit(m_n)) {
+        throw std::runtime_error("Shade: 16-bit id codes need at most " + std::to_string(kIds16MaxTriangles) +
+                                 " triangles");
+    }
     if (m_width == 0) {
         throw std::runtime_error("Shade: Prepare() has not been called");
     }
@@ -262,6 +266,7 @@ void DeviceScene::Shade(const float* d_offsets, const int* d_ids, float* d_rgba,
     }
     OrderAfterPrevious(stream);
     BandArgs band{d_offsets, d_rgba, m_width, m_height, row_begin, row_count, const_cast<int*>(d_ids)};
+    band.ids16 = ids16;
     HipCheck(LaunchShade(m_vertices, m_shade, m_edges, m_n, m_frame, m_background, band, stream, frames, band_rows,
                          interleaved, offsets_stride),
              "shade kernel launch");
@@ -350,7 +355,11 @@ DeviceScene::ParamTable& DeviceScene::AcquireTable(std::size_t frames, hipStream
 
 void DeviceScene::TraceBatch(const float* const* d_offsets, float* const* d_rgba, int* const* d_ids, std::size_t frames,
                              std::size_t row_begin, std::size_t row_count, int variant, hipStream_t stream,
-                             std::size_t row_interleave) const {
+                             std::size_t row_interleave, bool ids16) const {
+    if (ids16 && (d_ids == nullptr || !Ids16Fit(m_n))) {
+        throw std::runtime_error("TraceBatch: 16-bit id codes need id outputs and at most " +
+                                 std::to_string(kIds16MaxTriangles) + " triangles");
+    }
     if (m_width == 0) {
         throw std::runtime_error("TraceBatch: Prepare() has not been called");
     }
@@ -367,7 +376,7 @@ void DeviceScene::TraceBatch(const float* const* d_offsets, float* const* d_rgba
         for (std::size_t f = 0; f < frames; ++f) {  // frame by frame, each with its own record setup
             m_prepare_pending = true;
             Trace(d_offsets[f], d_rgba != nullptr ? d_rgba[f] : nullptr, row_begin, row_count, variant, stream,
-                  d_ids != nullptr ? d_ids[f] : nullptr, row_interleave);
+                  d_ids != nullptr ? d_ids[f] : nullptr, row_interleave, ids16);
         }
         return;
     }
@@ -386,7 +395,7 @@ void DeviceScene::TraceBatch(const float* const* d_offsets, float* const* d_rgba
         cf[f].edges = m_edges + f * floats;
         cf[f].bins = &bins[f];
         cf[f].band = BandArgs{d_offsets[f], d_rgba != nullptr ? d_rgba[f] : nullptr, m_width, m_height, row_begin,
-                              row_count, d_ids != nullptr ? d_ids[f] : nullptr, row_interleave};
+                              row_count, d_ids != nullptr ? d_ids[f] : nullptr, row_interleave, ids16};
     }
     const StageEvents ev = BindStageEvents(!CullFusedInfo(row_begin, row_count, m_height, row_interleave), true);
     ParamTable* table = frames > static_cast<std::size_t>(kMaxBatch) ? &AcquireTable(frames, stream) : nullptr;
@@ -403,7 +412,11 @@ void DeviceScene::TraceBatch(const float* const* d_offsets, float* const* d_rgba
 }
 
 void DeviceScene::Trace(const float* d_offsets, float* d_rgba, std::size_t row_begin, std::size_t row_count,
-                        int variant, hipStream_t stream, int* d_ids, std::size_t row_interleave) const {
+                        int variant, hipStream_t stream, int* d_ids, std::size_t row_interleave, bool ids16) const {
+    if (ids16 && (d_ids == nullptr || !Ids16Fit(m_n))) {
+        throw std::runtime_error("Trace: 16-bit id codes need an id output and at most " +
+                                 std::to_string(kIds16MaxTriangles) + " triangles");
+    }
     if (m_width == 0) {
         throw std::runtime_error("Trace: Prepare() has not been called");
     }
@@ -411,7 +424,7 @@ void DeviceScene::Trace(const float* d_offsets, float* d_rgba, std::size_t row_b
         throw std::runtime_error("Trace: row band outside the frame");
     }
     OrderAfterPrevious(stream);
-    BandArgs band{d_offsets, d_rgba, m_width, m_height, row_begin, row_count, d_ids, row_interleave};
+    BandArgs band{d_offsets, d_rgba, m_width, m_height, row_begin, row_count, d_ids, row_interleave, ids16};
     CullBins bins{};
     const CullBins* use_bins = nullptr;
     if (variant == kTraceCull && row_count != 0 && CullBinningEnabled() && CullBinnable(m_width, row_count)) {
@@ -577,6 +590,12 @@ Renderer::Renderer(const Scene& scene, std::vector<int> devices)
         if (v != nullptr && std::strcmp(v, "rccl") == 0) {
             m_gather_mode = GatherMode::kRccl;
         }
+    }
+    // Gathered payload: 16-bit id codes where the scene allows them (render.h kId16Period; env
+    // SRT_EXCHANGE_IDS=32: int32 ids), half the bytes over xGMI.
+    {
+        const char* v = std::getenv("SRT_EXCHANGE_IDS");
+        m_id_bytes = Ids16Fit(scene.triangle_count()) && !(v != nullptr && std::strcmp(v, "32") == 0) ? 2 : 4;
     }
     if (m_gather_mode == GatherMode::kRccl) {
         try {
@@ -812,7 +831,8 @@ void Renderer::RenderBands(const void* host_offsets, void* host_rgba) {
             }
             CopyBandRows(i, out_bytes, w * 4 * out_elem, src, hipMemcpyDeviceToHost, true, s.stream);
         } else {
-            s.scene->Trace(b.offsets[i], nullptr, s.row_begin, s.row_count, m_variant, s.stream, b.ids[i], interleave);
+            s.scene->Trace(b.offsets[i], nullptr, s.row_begin, s.row_count, m_variant, s.stream, b.ids[i], interleave,
+                           m_id_bytes == 2);
         }
     }
     if (!direct) {
@@ -834,7 +854,7 @@ void Renderer::RenderBands(const void* host_offsets, void* host_rgba) {
             ncclResult_t first = ncclSuccess;
             for (std::size_t i = 0; i < P; ++i) {
                 Slot& s = *m_slots[i];
-                const ncclResult_t r = ncclGather(b.ids[i], i == 0 ? b.gather : nullptr, band_pixels, ncclInt32, 0,
+                const ncclResult_t r = ncclGather(b.ids[i], i == 0 ? b.gather : nullptr, band_pixels * m_id_bytes, ncclUint8, 0,
                                                   static_cast<ncclComm_t>(m_comms[i]), s.stream);
                 if (r != ncclSuccess && r != ncclInProgress && first == ncclSuccess) {
                     first = r;
@@ -850,8 +870,8 @@ void Renderer::RenderBands(const void* host_offsets, void* host_rgba) {
             for (std::size_t i = 0; i < P; ++i) {
                 Slot& s = *m_slots[i];
                 DeviceGuard guard(s.device);
-                HipCheck(hipMemcpyPeerAsync(b.gather + i * band_pixels, root.device, b.ids[i], s.device,
-                                            band_pixels * sizeof(int), s.stream),
+                HipCheck(hipMemcpyPeerAsync(reinterpret_cast<unsigned char*>(b.gather) + i * band_pixels * m_id_bytes,
+                                            root.device, b.ids[i], s.device, band_pixels * m_id_bytes, s.stream),
                          "hipMemcpyPeerAsync(band gather)");
                 if (i != 0) {
                     if (s.traced.empty()) {
@@ -866,7 +886,8 @@ void Renderer::RenderBands(const void* host_offsets, void* host_rgba) {
             }
         }
         DeviceGuard guard(root.device);
-        root.scene->Shade(b.full, b.gather, b.frame, 0, h, root.stream, 1, m_band_rows, interleave > 1 ? P : 0);
+        root.scene->Shade(b.full, b.gather, b.frame, 0, h, root.stream, 1, m_band_rows, interleave > 1 ? P : 0, 0,
+                          m_id_bytes == 2);
         const void* src = b.frame;
         if (m_out_half) {
             HipCheck(LaunchFloatToHalf(b.frame, b.frame16, h * w * 4, root.stream), "framebuffer f32 -> f16");

@@ -69,8 +69,9 @@ public:
     // Trace rows [row_begin, row_begin + row_count) of the prepared frame into RGBA, or (d_ids
     // non-null, d_rgba ignored) into hit ids for deferred shading.
     // row_interleave > 1: the band deals the frame's tile rows round-robin (render.h BandArgs).
+    // ids16: d_ids points at 16-bit id codes (render.h kId16Period; Ids16Fit(triangles) must hold).
     void Trace(const float* d_offsets, float* d_rgba, std::size_t row_begin, std::size_t row_count, int variant,
-               hipStream_t stream, int* d_ids = nullptr, std::size_t row_interleave = 1) const;
+               hipStream_t stream, int* d_ids = nullptr, std::size_t row_interleave = 1, bool ids16 = false) const;
     // Deferred shading of rows [row_begin, row_begin + row_count) of the prepared frame from hit
     // ids (as Trace writes them) and sample offsets: the RGBA the fused trace would store.
     // frames > 1: a batch of that many frames of this camera, ids band-major as a gather of
@@ -79,7 +80,7 @@ public:
     // between consecutive frames' offsets (0: the batch shares d_offsets).
     void Shade(const float* d_offsets, const int* d_ids, float* d_rgba, std::size_t row_begin, std::size_t row_count,
                hipStream_t stream, std::size_t frames = 1, std::size_t band_rows = 0,
-               std::size_t interleaved = 0, std::size_t offsets_stride = 0) const;
+               std::size_t interleaved = 0, std::size_t offsets_stride = 0, bool ids16 = false) const;
     // `frames` (<= render.h kMaxTableFrames) frames of the prepared camera, rows [row_begin,
     // row_begin + row_count) each: frame f's offsets d_offsets[f], its RGBA d_rgba[f] or (d_ids
     // non-null) its hit ids d_ids[f]. Each frame gets the whole per-frame pipeline (record setup,
@@ -88,7 +89,7 @@ public:
     // their parameters from a device table uploaded once per call), the others frame by frame.
     void TraceBatch(const float* const* d_offsets, float* const* d_rgba, int* const* d_ids, std::size_t frames,
                     std::size_t row_begin, std::size_t row_count, int variant, hipStream_t stream,
-                    std::size_t row_interleave = 1) const;
+                    std::size_t row_interleave = 1, bool ids16 = false) const;
 
     std::size_t width() const { return m_width; }
     // The spatial order (device, triangles entries) and the time its build took at load (ms).
@@ -231,6 +232,7 @@ private:
     std::vector<std::unique_ptr<Slot>> m_slots;
     std::vector<void*> m_comms;  // ncclComm_t per slot when gathering with RCCL (nonblocking, comm.h)
     bool m_comms_aborted = false;  // a failed gather aborted them: later renders fail
+    std::size_t m_id_bytes = 4;    // gathered bytes per pixel: 2 (16-bit id codes) or 4 (int32 ids)
     GatherMode m_gather_mode = GatherMode::kDirect;
     bool m_interleaved = true;
     std::size_t m_band_rows = 0;  // rows of every band buffer

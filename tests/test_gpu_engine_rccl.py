@@ -239,3 +239,70 @@ def test_engine_frames_split_distinct_frames(gpu, scenes):
             ref = torch_render(scenes["soup300"], w, h, inputs[k])
             assert np.array_equal(e.read_frame(k).view(np.uint32), ref.view(np.uint32)), k
         assert e.verify() == (0, P * 2 * F)
+
+
+# ---------------------------------------------------------------------------------------------
+# 16-bit id codes (render.h kId16Period): the exchange payload of scenes up to 2 x 65535 triangles
+
+
+def collision_scene(path, n=70_000, seed=5):
+    """n triangles where every code with two candidates matters: triangles k and k + 65535 (k <
+    n - 65535) are large overlapping triangles in front of the camera -- sometimes k nearer, sometimes
+    k + 65535, sometimes coplanar and identical (a depth tie: the lower id must win) -- and the
+    rest are small triangles scattered over the view, so codes with one candidate occur too."""
+    from scenefile import write_custom_scene
+
+    rng = np.random.default_rng(seed)
+    v = np.zeros((n, 3, 3), np.float32)
+    cen = np.stack([rng.uniform(-1.2, 1.2, n), rng.uniform(-0.7, 0.7, n), rng.uniform(3.0, 6.0, n)], 1)
+    v[:] = cen[:, None, :] + rng.uniform(-0.03, 0.03, (n, 3, 3))
+    pairs = n - 65535
+    for k in range(pairs):
+        c = np.array([rng.uniform(-1.0, 1.0), rng.uniform(-0.5, 0.5), 0.0])
+        z_a, z_b = rng.uniform(1.5, 2.5), rng.uniform(1.5, 2.5)
+        if k % 7 == 0:
+            z_b = z_a  # coplanar and identical: equal t, the lower id wins
+        tri = np.array([[-0.25, -0.2, 0.0], [0.3, -0.15, 0.0], [0.0, 0.3, 0.0]]) + c
+        a, b = tri.copy(), tri.copy()
+        if k % 7 != 0:
+            b[:, :2] = b[:, :2] * 0.9 + 0.05  # overlapping, not identical
+        a[:, 2] += z_a
+        b[:, 2] += z_b
+        v[k], v[k + 65535] = a, b
+    return write_custom_scene(path, v, rng.uniform(0.2, 1.0, (n, 3)))
+
+
+def test_ids16_codes_decode_exactly(gpu, tmp_path):
+    """70 000 triangles (every code below 4465 has two candidates, and those pairs overlap on
+    screen): the 16-bit id codes through the fake-device exchange (P = 2 and 3) and the one-rank
+    RCCL exchange give the one-device frame bit for bit, with random per-pixel offsets."""
+    from simpleraytracer_amd.engine import FrameEngine
+
+    path = collision_scene(tmp_path / "collide.srt")
+    w, h = 256, 144
+    inputs = np.random.default_rng(9).random((1, h, w, 2), dtype=np.float32)
+    ref = torch_render(path, w, h, inputs[0])
+    ids = ref[..., 3].astype(np.int64)
+    assert (ids >= 65535).sum() > 1000 and ((ids >= 0) & (ids < 70_000 - 65535)).sum() > 1000, \
+        "the scene must put both halves of the colliding pairs on screen"
+    for kw in ({"devices": [0, 0]}, {"devices": [0, 0, 0]}, {"devices": [0], "rccl_self": True}):
+        with FrameEngine(path, w, h, batch=6, queues=2, **kw) as e:
+            e.set_inputs(inputs)
+            e.run(2)
+            for k in range(12):
+                assert np.array_equal(e.read_frame(k).view(np.uint32), ref.view(np.uint32)), (kw, k)
+
+
+def test_ids16_mlinfer_gather_decodes_exactly(gpu, tmp_path, monkeypatch):
+    """The mlInfer gather (fake devices, device copies) carries 16-bit codes for the same scene."""
+    import simpleraytracer_amd as srt
+
+    path = collision_scene(tmp_path / "collide.srt")
+    w, h = 200, 120
+    ref = srt.render(path, w, h)
+    monkeypatch.setenv("ML_VISIBLE_DEVICES", "0,0,0")
+    got = srt.render(path, w, h)
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+    monkeypatch.setenv("SRT_EXCHANGE_IDS", "32")
+    got32 = srt.render(path, w, h)
+    assert np.array_equal(got32.view(np.uint32), ref.view(np.uint32))

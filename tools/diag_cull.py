@@ -3,8 +3,8 @@
 
     make diag && SRT_LIB=simpleraytracer_amd/lib_diag/libModelRunner.so python tools/diag_cull.py
 
-Renders one frame (headline config by default; env W, H, TRI, OFFSETS=random) with the
-`make diag` library, whose trace kernel stamps every block's start and end (s_memrealtime,
+Renders one frame (headline config by default; env W, H, TRI, OFFSETS=random; BATCH=8: one launch
+of 8 frames, the headline's launch shape) with the `make diag` library, whose trace kernel stamps every block's start and end (s_memrealtime,
 100 MHz), its work item (tile part, chunk of a split part, last arriver) and the packet-walk
 phase cycles (render.hip SRT_DIAG). Prints the kernel span, block durations, how many blocks
 run over time, the critical chains of split parts and the blocks that finish last.
@@ -54,10 +54,15 @@ def main():
             off = torch.rand((h, w, 2), generator=g, dtype=torch.float32).cuda()
         else:
             off = torch.full((h, w, 2), 0.5, dtype=torch.float32, device="cuda")
+        nb = int(os.environ.get("BATCH", "1"))
         out = torch.empty((h, w, 4), dtype=torch.float32, device="cuda")
+        outs = [torch.empty((h, w, 4), dtype=torch.float32, device="cuda") for _ in range(nb)]
         for _ in range(3):
             scene.prepare(w, h, stream)
-            scene.trace(off, out, 0, h, variant="cull", stream=stream)
+            if nb == 1:
+                scene.trace(off, out, 0, h, variant="cull", stream=stream)
+            else:
+                scene.trace_batch([off] * nb, outs, 0, h, variant="cull", stream=stream)
         torch.cuda.synchronize()
         buf = np.zeros((65536, COLS), np.uint64)
         assert lib.srtDiagRead(buf.ctypes.data, buf.nbytes) == 0, _native.last_error()
@@ -109,6 +114,17 @@ def main():
             wk = b[sel, 2] / 2400.0
             summary["phases_us"][name] = {"blocks": int(sel.sum()), "dur": stats(dur[sel]), "gather": stats(g),
                                           "walk": stats(wk), "rest": stats(dur[sel] - g - wk)}
+    # block classes by work-item flags (render.hip kItemRegular 1, kItemFull 2, kItemEmpty 4)
+    fl = buf[ran, 12] & 0xFFFFFFFF
+    classes = {"empty": (fl & 4) != 0, "full": ((fl & 2) != 0) & ((fl & 4) == 0),
+               "list_whole": ((fl & 6) == 0) & (nch <= 1), "list_split": ((fl & 6) == 0) & (nch > 1)}
+    summary["classes"] = {k: {"blocks": int(v.sum()), "dur_us": stats(dur[v]),
+                              "gather_us": stats(b[v, 1] / 2400.0), "walk_us": stats(b[v, 2] / 2400.0)}
+                          for k, v in classes.items() if v.any()}
+    slots = int(os.environ.get("SLOTS", "1536"))
+    summary["occupancy"] = {"block_us": round(float(dur.sum()), 1), "slots": slots,
+                            "busy_frac": round(float(dur.sum() / (end.max() * slots)), 3),
+                            "note": "sum of block lifetimes / (span x resident block slots)"}
     order = np.argsort(-end)[:12]
     summary["last_to_finish"] = [{"grid_block": int(ran[i]), "item": int(item[i]), "chunk": int(chunk[i]),
                                   "chunks": int(nch[i]), "last": int(last[i]), "start": round(float(start[i]), 2),

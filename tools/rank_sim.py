@@ -2,9 +2,20 @@
 """Per-rank GPU time of the multi-GPU band pipeline, measured on one GPU with the frame engine
 (srtEngineCreateRank with simulate=1: the rank's exact kernel stream -- its band's batched traces and
 its share of the compositing -- without the exchange). For every P and rank: us of GPU time per
-frame; the slowest rank bounds the job: ceiling = W x H / slowest (Mrays/s, exchange not included).
+frame; the slowest rank bounds the job: gpu ceiling = W x H / slowest (Mrays/s).
 
-    python tools/rank_sim.py [--ranks 1,2,4,8] [--steps 30] [--batch 64] [--queues 2]
+The exchange, modelled (it cannot be measured on a one-GPU box): per frame the P - 1 ranks that do
+not composite it send their band of hit ids (the engine's payload: id_bytes per pixel, 2 for 16-bit
+codes) to its compositor; the all-to-all deals the compositors round-robin, so every one of the
+P (P - 1) directed xGMI links of a fully connected node carries bytes_frame / (P (P - 1)) per frame
+on average, and the link-bound time per frame is that over the per-direction link rate. ASSUMED
+rate, not measured: --link-gbs (default 64 GB/s per direction; MI355X_MICROARCH.md has no xGMI figure,
+SURVEY.md section 5 quotes 153.6 GB/s per link, bidirectional, so about 77 GB/s each way at peak;
+RCCL point-to-point reaching ~85 % of it gives ~64). A sweep of rates is printed beside it. The job
+ceiling = W x H / max(slowest rank's GPU time, link time) -- the exchange overlaps the other queue's
+compute (its RCCL kernels' CU time is inside neither figure).
+
+    python tools/rank_sim.py [--ranks 1,2,4,8] [--steps 30] [--batch 64] [--queues 2] [--link-gbs 64]
 """
 from __future__ import annotations
 
@@ -32,6 +43,8 @@ def main():
     ap.add_argument("--rows", default="interleaved")
     ap.add_argument("--launch", type=int, default=0, help="frames per trace launch (0: library default)")
     ap.add_argument("--all-ranks", action="store_true", help="every rank (default: ranks 0, P/2 and P-1)")
+    ap.add_argument("--link-gbs", type=float, default=64.0, help="ASSUMED xGMI rate per direction (module doc)")
+    ap.add_argument("--sweep-gbs", default="32,64,100,150", help="link rates of the printed sensitivity sweep")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -46,6 +59,7 @@ def main():
            "rows": a.rows, "ranks": {}}
     for P in [int(x) for x in a.ranks.split(",")]:
         per = {}
+        xbytes = 0.0
         ranks = range(P) if a.all_ranks else sorted({0, P // 2, P - 1})
         for r in ranks:
             if P == 1:
@@ -55,6 +69,7 @@ def main():
                 eng = FrameEngine.rank(path, a.width, a.height, 0, r, P, None, queues=a.queues, batch=a.batch,
                                        rows=a.rows, simulate=True, launch=a.launch)
             eng.set_inputs(inputs)
+            xbytes = eng.info()["exchange_bytes_per_frame"] if P > 1 else 0.0
             eng.run(a.warmup)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
@@ -64,9 +79,23 @@ def main():
             per[r] = round(dt / (a.steps * a.batch) * 1e6, 3)
             eng.close()
         slow = max(per.values())
+        link_bytes = xbytes / (P * (P - 1)) if P > 1 else 0.0
+        link_us = link_bytes / (a.link_gbs * 1e3)
+        bound = max(slow, link_us)
         out["ranks"][P] = {"us_per_frame": per, "slowest_us": slow,
-                           "ceiling_mrays": round(a.width * a.height / slow, 1)}
+                           "ceiling_mrays": round(a.width * a.height / slow, 1),
+                           "exchange_bytes_per_frame": int(xbytes), "bytes_per_link_per_frame": int(link_bytes),
+                           "link_us_per_frame": round(link_us, 3), "link_gbs_assumed": a.link_gbs,
+                           "job_ceiling_mrays": round(a.width * a.height / bound, 1),
+                           "bound": "link" if link_us > slow else "gpu",
+                           "job_ceiling_sweep": {g: round(a.width * a.height / max(slow, link_bytes / (float(g) * 1e3)), 1)
+                                                 for g in a.sweep_gbs.split(",")}}
         print(json.dumps({"P": P, **out["ranks"][P]}), flush=True)
+    base = out["ranks"].get(1, {}).get("ceiling_mrays")
+    if base:
+        for P, r in out["ranks"].items():
+            r["gpu_x_p1"] = round(r["ceiling_mrays"] / base, 3)
+            r["job_x_p1"] = round(r["job_ceiling_mrays"] / base, 3)
     print(json.dumps(out))
 
 
