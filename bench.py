@@ -591,15 +591,15 @@ def main():
                                         "trace_kernel": round(s[3], 5)} for i, s in enumerate(ranks_stages)]
             if band:
                 xb = info["exchange_bytes_per_frame"]
-                id_bytes = round(xb / max(1, (world - 1) * info["buffer_rows"] * W))
+                px = max(1, (world - 1) * info["buffer_rows"] * W)
                 line["exchange"] = {"pattern": a.exchange, "transport": "RCCL" if info["rccl"] else "device copies",
-                                    "payload": ("16-bit hit-id code per pixel (render.h kId16Period: decoded exactly "
-                                                "by the compositor's shading)" if id_bytes == 2 else
-                                                "int32 hit id per pixel") + " (deferred shading on the compositor)",
-                                    "id_bytes": id_bytes,
+                                    "payload": "packed hit ids (16 + k bits per pixel: a u16 plane and k bit planes, "
+                                               "render.h PackedIds) or int32 ids; deferred shading on the compositor, "
+                                               "whose own band is traced to RGBA in place",
+                                    "bytes_per_pixel": round(xb / px, 4),
                                     "bytes_per_frame": int(xb),
-                                    "int32_ids_equivalent": int(xb * 4 / id_bytes),
-                                    "rgba_f32_equivalent": int(xb * 16 / id_bytes)}
+                                    "int32_ids_equivalent": int(px * 4),
+                                    "rgba_f32_equivalent": int(px * 16)}
         for k, v in legs.items():
             line[k] = v
         if world == 1 and not a.no_e2e and extras:

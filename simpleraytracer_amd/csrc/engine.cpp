@@ -116,11 +116,14 @@ std::size_t ExchangePlan::MaxFramesPerCompositor() const {
 }
 
 namespace {
-// Offset (in pixels) of compositor c's slot j in a device's send buffer: all-to-all keeps one
-// region of MaxFramesPerCompositor frames per compositor; the gathers send everything to one.
-std::size_t SendPixels(const ExchangePlan& plan, std::size_t c, std::size_t j, std::size_t band_pixels) {
+// Band frame index of compositor c's slot j in a device's send buffer: all-to-all keeps one region
+// of MaxFramesPerCompositor frames per compositor; the gathers send everything to one.
+std::size_t SendFrames(const ExchangePlan& plan, std::size_t c, std::size_t j) {
     const std::size_t region = plan.exchange == EngineOptions::kAllToAll ? c * plan.MaxFramesPerCompositor() : 0;
-    return (region + j) * band_pixels;
+    return region + j;
+}
+std::size_t SendPixels(const ExchangePlan& plan, std::size_t c, std::size_t j, std::size_t band_pixels) {
+    return SendFrames(plan, c, j) * band_pixels;
 }
 }  // namespace
 
@@ -321,7 +324,7 @@ struct FrameEngine::Queue {
     hipEvent_t traced = nullptr;     // the batch's trace done (queue stream)
     hipEvent_t exchanged = nullptr;  // the batch's exchange done (comm stream)
     hipEvent_t drained = nullptr;    // end-of-run marker (queue stream), polled with a deadline
-    // Id buffers, m_id_bytes per pixel (int32 ids, or 16-bit codes: render.h kId16Period).
+    // Id buffers of band frames, m_band_id_bytes each (int32 ids, or packed ids: render.h PackedIds).
     unsigned char* send = nullptr;   // bands: ids for the other compositors
     unsigned char* recv = nullptr;   // bands: [P][frames composited here][buffer rows][W] ids
     float* rgba = nullptr;           // frames rendered / composited here per batch, H x W x 4 each
@@ -474,10 +477,12 @@ void FrameEngine::Init(const Scene& scene, const std::vector<int>& devices) {
     m_plan.exchange = m_opt.exchange;
     m_scene = std::make_unique<Scene>(scene);
     m_n = scene.triangle_count();
-    {  // the exchange payload: 16-bit id codes where the scene allows them (env SRT_EXCHANGE_IDS=32: int32)
+    {  // the exchange payload: packed ids with the cull variant (env SRT_EXCHANGE_IDS=32: int32)
         const char* v = std::getenv("SRT_EXCHANGE_IDS");
         const bool force32 = v != nullptr && std::strcmp(v, "32") == 0;
-        m_id_bytes = m_exchange && Ids16Fit(m_n) && !force32 ? 2 : 4;
+        m_id_planes = m_exchange && m_opt.variant == kTraceCull && !force32 ? IdPlanes(m_n) : -1;
+        const std::size_t rows = m_split.BufferRows();
+        m_band_id_bytes = m_id_planes >= 0 ? PackedIdLayout(m_id_planes, rows, m_width).bytes : rows * m_width * sizeof(int);
     }
     for (std::size_t i = 0; i < devices.size(); ++i) {
         auto d = std::make_unique<Device>();
@@ -490,7 +495,6 @@ void FrameEngine::Init(const Scene& scene, const std::vector<int>& devices) {
 }
 
 void FrameEngine::AllocateQueues() {
-    const std::size_t band_pixels = m_split.BufferRows() * m_width;
     const std::size_t frame_floats4 = m_width * m_height * 4;
     for (auto& dp : m_dev) {
         Device& d = *dp;
@@ -509,8 +513,8 @@ void FrameEngine::AllocateQueues() {
                 const std::size_t send_frames = m_plan.exchange == EngineOptions::kAllToAll
                                                     ? m_world * m_plan.MaxFramesPerCompositor()
                                                     : m_plan.batch;
-                q.send = DeviceAlloc<unsigned char>(send_frames * band_pixels * m_id_bytes, "hipMalloc(send ids)");
-                q.recv = DeviceAlloc<unsigned char>(m_world * m_plan.MaxFramesPerCompositor() * band_pixels * m_id_bytes,
+                q.send = DeviceAlloc<unsigned char>(send_frames * m_band_id_bytes, "hipMalloc(send ids)");
+                q.recv = DeviceAlloc<unsigned char>(m_world * m_plan.MaxFramesPerCompositor() * m_band_id_bytes,
                                           "hipMalloc(receive ids)");
                 q.rgba_frames = m_plan.MaxFramesPerCompositor();
             } else {
@@ -628,12 +632,11 @@ double FrameEngine::exchange_bytes_per_frame() const {
     if (!m_exchange || m_world == 1) {
         return 0.0;
     }
-    return static_cast<double>(m_world - 1) * static_cast<double>(m_split.BufferRows() * m_width) *
-           static_cast<double>(m_id_bytes);
+    return static_cast<double>(m_world - 1) * static_cast<double>(m_band_id_bytes);
 }
 
-int* FrameEngine::Ids(unsigned char* buf, std::size_t pixels) const {
-    return reinterpret_cast<int*>(buf + pixels * m_id_bytes);
+int* FrameEngine::Ids(unsigned char* buf, std::size_t band_frame) const {
+    return reinterpret_cast<int*>(buf + band_frame * m_band_id_bytes);
 }
 
 std::size_t FrameEngine::FrameIndex(std::size_t local, std::size_t b, std::size_t f) const {
@@ -745,9 +748,7 @@ void FrameEngine::TracePhase(std::size_t local, std::size_t b) {
         }
         return;
     }
-    const std::size_t band_pixels = m_split.BufferRows() * m_width;
     const std::size_t self = d.band;
-    const std::size_t n_self = m_plan.FramesFor(b, self);
     if (d.rows != 0) {
         for (std::size_t f0 = 0; f0 < F; f0 += L) {
             const std::size_t n = std::min(L, F - f0);
@@ -755,13 +756,15 @@ void FrameEngine::TracePhase(std::size_t local, std::size_t b) {
                 const std::size_t f = f0 + j;
                 const std::size_t c = m_plan.Compositor(b, f), slot = m_plan.Slot(f);
                 offs[j] = BandInput(local, k0 + f);
-                // The compositor's own band lands in its receive buffer directly, unless the
-                // self-exchange option sends it through RCCL like every other band.
-                ids[j] = c == self && !m_opt.rccl_self ? Ids(q.recv, (self * n_self + slot) * band_pixels)
-                                                       : Ids(q.send, SendPixels(m_plan, c, slot, band_pixels));
+                // The compositor's own band is traced and shaded in one kernel straight into its frame
+                // (RGBA at the band's frame rows; the deferred shading then skips that band), unless
+                // the self-exchange option sends it through RCCL like every other band.
+                const bool own = c == self && !m_opt.rccl_self;
+                ids[j] = own ? nullptr : Ids(q.send, SendFrames(m_plan, c, slot));
+                rgba[j] = own ? q.rgba + slot * frame_floats4 : nullptr;
             }
-            q.scene->TraceBatch(offs.data(), nullptr, ids.data(), n, d.row_begin, d.rows, m_opt.variant, q.stream,
-                                m_split.Interleave(), m_id_bytes == 2);
+            q.scene->TraceBatch(offs.data(), rgba.data(), ids.data(), n, d.row_begin, d.rows, m_opt.variant, q.stream,
+                                m_split.Interleave(), m_id_planes, true);
         }
     }
     HipCheck(hipEventRecord(q.traced, q.stream), "hipEventRecord(traced)");
@@ -770,7 +773,6 @@ void FrameEngine::TracePhase(std::size_t local, std::size_t b) {
 void FrameEngine::ExchangePhase(std::size_t local, std::size_t b) {
     Device& d = *m_dev[local];
     Queue& q = d.queues[b % m_opt.queues];
-    const std::size_t band_pixels = m_split.BufferRows() * m_width;
     const std::size_t self = d.band, n_self = m_plan.FramesFor(b, self);
     HipCheck(hipStreamWaitEvent(d.comm, q.traced, 0), "hipStreamWaitEvent(traced)");
     {
@@ -793,13 +795,12 @@ void FrameEngine::ExchangePhase(std::size_t local, std::size_t b) {
             }
             const std::size_t n_p = m_plan.FramesFor(b, p);
             if (n_p != 0) {
-                note(ncclSend(q.send + SendPixels(m_plan, p, 0, band_pixels) * m_id_bytes,
-                              n_p * band_pixels * m_id_bytes, ncclUint8,
+                note(ncclSend(q.send + SendFrames(m_plan, p, 0) * m_band_id_bytes, n_p * m_band_id_bytes, ncclUint8,
                               static_cast<int>(p), comm, d.comm));
             }
             if (n_self != 0) {
-                note(ncclRecv(q.recv + p * n_self * band_pixels * m_id_bytes, n_self * band_pixels * m_id_bytes,
-                              ncclUint8, static_cast<int>(p),
+                note(ncclRecv(q.recv + p * n_self * m_band_id_bytes, n_self * m_band_id_bytes, ncclUint8,
+                              static_cast<int>(p),
                               comm, d.comm));
             }
         }
@@ -816,7 +817,6 @@ void FrameEngine::CopyPhase(std::size_t local, std::size_t b) {
     Device& d = *m_dev[local];
     const std::size_t qi = b % m_opt.queues;
     Queue& q = d.queues[qi];
-    const std::size_t band_pixels = m_split.BufferRows() * m_width;
     const std::size_t self = d.band, n_self = m_plan.FramesFor(b, self);
     HipCheck(hipStreamWaitEvent(d.comm, q.traced, 0), "hipStreamWaitEvent(traced)");
     if (n_self != 0) {
@@ -827,9 +827,9 @@ void FrameEngine::CopyPhase(std::size_t local, std::size_t b) {
             Device& peer = *m_dev[p];
             Queue& pq = peer.queues[qi];
             HipCheck(hipStreamWaitEvent(d.comm, pq.traced, 0), "hipStreamWaitEvent(peer traced)");
-            HipCheck(hipMemcpyPeerAsync(q.recv + peer.band * n_self * band_pixels * m_id_bytes, d.device,
-                                        pq.send + SendPixels(m_plan, self, 0, band_pixels) * m_id_bytes, peer.device,
-                                        n_self * band_pixels * m_id_bytes, d.comm),
+            HipCheck(hipMemcpyPeerAsync(q.recv + peer.band * n_self * m_band_id_bytes, d.device,
+                                        pq.send + SendFrames(m_plan, self, 0) * m_band_id_bytes, peer.device,
+                                        n_self * m_band_id_bytes, d.comm),
                      "hipMemcpyPeerAsync(band ids)");
         }
     }
@@ -852,8 +852,8 @@ void FrameEngine::ShadePhase(std::size_t local, std::size_t b) {
     const std::size_t first = k0 + (a2a ? self : 0);
     const std::size_t stride = m_inputs == 1 ? 0 : (a2a ? m_world : 1) * FrameFloats();
     q.scene->Shade(FullInput(local, first), reinterpret_cast<const int*>(q.recv), q.rgba, 0, m_height, q.stream, n_self,
-                   m_split.BufferRows(),
-                   m_split.interleaved ? m_world : 0, stride, m_id_bytes == 2);
+                   m_split.BufferRows(), m_split.interleaved ? m_world : 0, stride, m_id_planes,
+                   m_opt.rccl_self ? -1 : static_cast<long>(self));  // the own band is RGBA already
 }
 
 void FrameEngine::Inject(std::size_t local, std::size_t b) {
@@ -1078,7 +1078,7 @@ DeviceScene::StageTimes FrameEngine::MeasureStages(std::size_t local, std::size_
     HipCheck(hipStreamSynchronize(d.comm), "hipStreamSynchronize(stages)");
     q.scene->TakeTimes();
     q.scene->SetTiming(true);
-    const std::size_t band_pixels = m_split.BufferRows() * m_width, frame_floats4 = m_width * m_height * 4;
+    const std::size_t frame_floats4 = m_width * m_height * 4;
     std::vector<const float*> offs(frames);
     std::vector<float*> rgba(frames);
     std::vector<int*> ids(frames);
@@ -1088,12 +1088,12 @@ DeviceScene::StageTimes FrameEngine::MeasureStages(std::size_t local, std::size_
                 const std::size_t k = i * frames + j;
                 offs[j] = m_exchange ? BandInput(local, k) : FullInput(local, k);
                 rgba[j] = q.rgba + j * frame_floats4;
-                ids[j] = Ids(q.send, j * band_pixels);
+                ids[j] = Ids(q.send, j);
             }
             if (m_exchange) {
                 if (d.rows != 0) {
                     q.scene->TraceBatch(offs.data(), nullptr, ids.data(), frames, d.row_begin, d.rows, m_opt.variant,
-                                        q.stream, m_split.Interleave(), m_id_bytes == 2);
+                                        q.stream, m_split.Interleave(), m_id_planes);
                 }
             } else {
                 q.scene->TraceBatch(offs.data(), rgba.data(), nullptr, frames, 0, m_height, m_opt.variant, q.stream, 1);

@@ -150,7 +150,7 @@ public:
     std::uint64_t triangles() const { return m_n; }
     // Bytes the devices exchange per frame (bands at P > 1), for the report.
     double exchange_bytes_per_frame() const;
-    std::size_t id_bytes() const { return m_id_bytes; }  // exchange payload per pixel
+    int id_planes() const { return m_id_planes; }  // exchange payload: packed ids' bit planes, -1 int32
 
 private:
     struct Queue;
@@ -163,7 +163,7 @@ private:
     void CheckUsable() const;    // throws once a run has failed
     void Inject(std::size_t local, std::size_t b);  // SRT_ENGINE_INJECT (comm.h)
     std::size_t FrameIndex(std::size_t local, std::size_t b, std::size_t f) const;  // frame of the sequence
-    int* Ids(unsigned char* buf, std::size_t pixels) const;  // pixel `pixels` of an id buffer (m_id_bytes each)
+    int* Ids(unsigned char* buf, std::size_t band_frame) const;  // band frame `band_frame` of an id buffer
     void TracePhase(std::size_t local, std::size_t b);
     void ExchangePhase(std::size_t local, std::size_t b);  // RCCL: inside a group
     void CopyPhase(std::size_t local, std::size_t b);      // device-copy exchange
@@ -179,7 +179,8 @@ private:
     std::uint64_t m_n = 0;
     bool m_bands = true;       // bands split (at P > 1, or rccl_self: exchange + shading)
     bool m_exchange = false;   // bands with an exchange: P > 1, or the one-device RCCL self-exchange
-    std::size_t m_id_bytes = 4;  // exchange payload per pixel: 2 (16-bit codes, render.h kId16Period) or 4
+    int m_id_planes = -1;          // exchange payload: packed ids with this many bit planes (render.h PackedIds), -1 int32
+    std::size_t m_band_id_bytes = 0;  // one band frame of it
     bool m_comms_made = false; // RCCL communicators were created (uses_rccl after an abort too)
     bool m_copy = false;       // exchange by device copies (repeated device / SRT_GATHER=copy)
     bool m_defer_shade = false;  // env SRT_DEFER_SHADE=1 (measurement): whole frames as ids + a shading launch

@@ -75,23 +75,32 @@ struct BandArgs {
     // k = 0, 1, ..., concatenated (row_begin a multiple of kCullTileRows; only the band's last tile
     // row may be partial, and then it is the frame's last).
     std::size_t row_interleave = 1;
-    // ids holds 16-bit codes (IdCode16) instead of int32 ids: the exchange payload of scenes of at
-    // most kIds16MaxTriangles triangles, half the bytes. Trace stores codes, LaunchShade decodes them.
-    bool ids16 = false;
+    // ids holds packed hit ids (PackedIds) with this many bit planes above the 16-bit low plane;
+    // -1: int32 ids (-1 = miss). The multi-GPU exchange payload (cull variant).
+    int id_planes = -1;
+    // RGBA output only: rgba is the whole frame (height x width x 4) and band row y is stored at its
+    // frame row (BandFrameRow) -- the compositor's own band traced straight into its frame.
+    bool rgba_frame_rows = false;
 };
 
-// 16-bit hit-id codes (the multi-GPU exchange payload, half the bytes of int32 ids): a miss is
-// 0xFFFF, a hit on triangle i is i % 65535 (never 0xFFFF). A code c < 0xFFFF stands for the
-// triangles c, c + 65535, c + 2 * 65535, ... below the triangle count; the compositor re-runs the
-// canonical exact test of each candidate at the pixel (records recomputed from the vertices with
-// the trace's expressions, so the same bits) and takes the lexicographic minimum (t, id) of those
-// that pass. The true winner passes and beats every other triangle that covers the pixel, so the
-// decode is exact. At most kIds16MaxTriangles triangles (two candidates per code); larger scenes
-// exchange int32 ids.
-constexpr unsigned kId16Period = 65535u;
-constexpr unsigned kId16Miss = 0xFFFFu;
-constexpr std::uint64_t kIds16MaxTriangles = 2ull * kId16Period;
-inline bool Ids16Fit(std::uint64_t triangles) { return triangles <= kIds16MaxTriangles; }
+// Packed hit ids (the multi-GPU exchange payload; cull variant): a pixel's code -- its triangle id, or
+// all ones for a miss -- in 16 + k bits, k = the bits the triangle count needs beyond 16 (C3's 100 000
+// triangles: 1, 2.125 B per pixel against int32's 4; under 65 535 triangles: 0; C5's 1M: 4). Row-major
+// rows, each: the row's u16 low 16 bits (padded to 8 B), then per plane j one 64-bit word per 64
+// columns (bit x % 64 of word x / 64 is bit 16 + j of pixel x's code). A band frame is `rows` such rows
+// (padded to 256 B), so a band's actual rows and its buffer's rows index it alike. Written by the trace
+// epilogue (one ballot per plane and row segment), read by the deferred shading: no decode work.
+constexpr int kMaxIdPlanes = 8;
+int IdPlanes(std::uint64_t triangles);  // k; -1 when the ids need more than 16 + kMaxIdPlanes bits
+struct PackedIds {
+    int planes = 0;
+    std::size_t rows = 0, width = 0;
+    std::size_t words = 0;          // 64-bit words per row and plane
+    std::size_t low_row_bytes = 0;  // a row's u16 values, padded to 8 B
+    std::size_t row_bytes = 0;      // a row
+    std::size_t bytes = 0;          // one band frame
+};
+PackedIds PackedIdLayout(int planes, std::size_t rows, std::size_t width);
 
 // Frame row of band-local row `local` (BandArgs::row_interleave).
 inline std::size_t BandFrameRow(std::size_t row_begin, std::size_t interleave, std::size_t local);
@@ -255,7 +264,7 @@ hipError_t LaunchShadeTable(const float* d_vertices, const float* d_albedo, std:
 hipError_t LaunchShade(const float* d_vertices, const float* d_shade, const float* d_edges, std::uint64_t n,
                        const Frame& frame, const float background[3], const BandArgs& band, hipStream_t stream,
                        std::size_t frames = 1, std::size_t band_rows = 0, std::size_t interleaved = 0,
-                       std::size_t offsets_stride = 0);
+                       std::size_t offsets_stride = 0, long skip_band = -1);
 
 // Spatial order of the records (spatial.hip): ids sorted by the Morton code of their centroid's
 // image-plane position under the scene camera, on the device (keys + rocPRIM radix sort), and

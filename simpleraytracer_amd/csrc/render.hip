@@ -74,7 +74,12 @@ struct TraceParams {
     const float2* __restrict__ offsets;
     float4* __restrict__ out;
     int* __restrict__ out_ids;  // non-null: store the hit id per pixel (-1 = miss) instead of RGBA
-    unsigned short* __restrict__ out_ids16;  // non-null: store the 16-bit id code (render.h IdCode16) instead
+    unsigned char* __restrict__ out_packed;  // non-null: store packed ids (render.h PackedIds) instead
+    int id_planes;             // packed ids: bit planes above the low 16 bits
+    unsigned id_words;         // packed ids: 64-bit words per row and plane
+    unsigned id_low_row_bytes; // packed ids: the row's u16 values (padded to 8 B), then its plane words
+    unsigned id_row_bytes;     // packed ids: bytes per row
+    int out_frame_rows;  // RGBA out is a whole frame: band row y stores at its frame row (render.h BandArgs)
     unsigned n_pad;   // records in the edge buffer (multiple of kPadTriangles)
     unsigned n;       // records in the scene
     int tiles_x;         // cull tiles per tile row of the band
@@ -531,10 +536,9 @@ __device__ __forceinline__ float4 ShadePixel(const TraceParams& p, float fx, flo
 typedef float F4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void StorePixel(const TraceParams& p, int x, int y, float fx, float fy, int id) {
     const size_t at = static_cast<size_t>(y) * p.width + x;
-    if (p.out_ids16 != nullptr) {
-        const unsigned short code = static_cast<unsigned short>(id < 0 ? kId16Miss : static_cast<unsigned>(id) % kId16Period);
-        __builtin_nontemporal_store(code, p.out_ids16 + at);
-    } else if (p.out_ids != nullptr) {
+    const size_t rgba_at =
+        p.out_frame_rows != 0 ? static_cast<size_t>(FrameRow(p.row_begin, p.row_interleave, y)) * p.width + x : at;
+    if (p.out_ids != nullptr) {
         __builtin_nontemporal_store(id, p.out_ids + at);
     } else {
 #ifdef SRT_EXP_NO_SHADE  // measurement builds only: store without shading
@@ -542,7 +546,26 @@ __device__ __forceinline__ void StorePixel(const TraceParams& p, int x, int y, f
 #else
         const float4 v = ShadePixel(p, fx, fy, id);
 #endif
-        __builtin_nontemporal_store(F4{v.x, v.y, v.z, v.w}, reinterpret_cast<F4*>(p.out + at));
+        __builtin_nontemporal_store(F4{v.x, v.y, v.z, v.w}, reinterpret_cast<F4*>(p.out + rgba_at));
+    }
+}
+
+// Packed ids (render.h PackedIds) of one band row segment: the wave's 64 lanes are the 64 columns
+// x = tx * 64 + lane of band row y (wave-uniform; called by every lane of the wave). The low 16 bits
+// go to the u16 plane; bit 16 + j of the 64 codes is one ballot, stored by lane 0 as plane j's word.
+__device__ __forceinline__ void StorePackedIds(const TraceParams& p, int tx, int x, int y, int id) {
+    const bool valid = x < p.width;
+    const unsigned code = id < 0 ? 0xFFFFFFFFu : static_cast<unsigned>(id);
+    unsigned char* row = p.out_packed + static_cast<size_t>(y) * p.id_row_bytes;
+    if (valid) {
+        __builtin_nontemporal_store(static_cast<unsigned short>(code & 0xFFFFu), reinterpret_cast<unsigned short*>(row) + x);
+    }
+    unsigned long long* words = reinterpret_cast<unsigned long long*>(row + p.id_low_row_bytes);
+    for (int j = 0; j < p.id_planes; ++j) {
+        const unsigned long long m = __ballot(valid && ((code >> (16 + j)) & 1u) != 0u);
+        if ((threadIdx.x & (kWave - 1)) == 0) {
+            __builtin_nontemporal_store(m, words + static_cast<size_t>(j) * p.id_words + tx);
+        }
     }
 }
 
@@ -584,42 +607,16 @@ __device__ __forceinline__ unsigned long long HitKey(float t, int id) {
     return (static_cast<unsigned long long>(__float_as_uint(t)) << 32) | static_cast<unsigned>(id);
 }
 
-// The hit id of a pixel from its 16-bit code (render.h IdCode16): a miss, the code's only
-// candidate, or the lexicographic minimum (t, id) over the candidates that pass the canonical exact
-// test at (fx, fy) -- EvalPacket's expressions on records ComputeEdges rebuilds from the vertices
-// (the record pass's own function): the trace's bits, so the true winner passes and wins.
-__device__ __forceinline__ int DecodeId16(const TraceParams& p, unsigned code, float fx, float fy) {
-    if (code >= kId16Miss || code >= p.n) {
-        return -1;
-    }
-    if (code + kId16Period >= p.n) {
-        return static_cast<int>(code);  // a single candidate
-    }
-    unsigned long long best = ~0ull;
-    for (unsigned c = code; c < p.n; c += kId16Period) {
-        float e[9], vol;
-        if (!ComputeEdges(p.eye, p.base, p.du, p.dv, p.vertices + 9ull * c, true, e, vol)) {
-            continue;
-        }
-        const float eA = fmaf(fy, e[2], fmaf(fx, e[1], e[0]));
-        const float eB = fmaf(fy, e[5], fmaf(fx, e[4], e[3]));
-        const float eC = fmaf(fy, e[8], fmaf(fx, e[7], e[6]));
-        const float det = (eA + eB) + eC;
-        const float t = vol / det;
-        if (fminf(fminf(eA, eB), eC) >= 0.f && det > 0.f && t < __builtin_inff()) {
-            const unsigned long long k = HitKey(t, static_cast<int>(c));
-            best = k < best ? k : best;
-        }
-    }
-    return best == ~0ull ? -1 : static_cast<int>(static_cast<unsigned>(best));
-}
-
-template <bool ID16>
+// PACKED: the ids arrive as packed band frames (render.h PackedIds, frame_bytes each, the same
+// band-major order): a pixel's code is its u16 plus p.id_planes bits from the bit planes.
+template <bool PACKED>
 __global__ __launch_bounds__(kShadeThreads) void ShadeIdsKernel(TraceParams p, const void* __restrict__ ids_v,
                                                                 unsigned band_rows, unsigned frames,
-                                                                unsigned interleaved, size_t offsets_stride) {
-    using IdT = std::conditional_t<ID16, unsigned short, int>;
-    const IdT* __restrict__ ids = static_cast<const IdT*>(ids_v);
+                                                                unsigned interleaved, size_t offsets_stride,
+                                                                unsigned skip_band, size_t frame_bytes) {
+    using IdT = std::conditional_t<PACKED, unsigned, int>;
+    const int* __restrict__ ids = static_cast<const int*>(ids_v);
+    const unsigned char* __restrict__ packed = static_cast<const unsigned char*>(ids_v);
     const int x = static_cast<int>(blockIdx.x * kShadeThreads + threadIdx.x);
     if (x >= p.width) {
         return;
@@ -629,6 +626,7 @@ __global__ __launch_bounds__(kShadeThreads) void ShadeIdsKernel(TraceParams p, c
     const size_t pixels = static_cast<size_t>(p.width) * p.row_count;
     IdT id[kShadeRows];
     float2 o[kShadeRows];
+    bool mine[kShadeRows];  // rows of band skip_band: the compositor traced them as RGBA already
 #pragma unroll
     for (int r = 0; r < kShadeRows; ++r) {
         const int y = min(y0 + r, p.row_count - 1);
@@ -641,22 +639,34 @@ __global__ __launch_bounds__(kShadeThreads) void ShadeIdsKernel(TraceParams p, c
             band = static_cast<unsigned>(y) / band_rows;
             local = static_cast<unsigned>(y) - band * band_rows;
         }
-        const size_t at = ((static_cast<size_t>(band) * frames + g) * band_rows + local) * p.width + x;
-        id[r] = __builtin_nontemporal_load(ids + at);
-        o[r] = p.offsets[static_cast<size_t>(y) * p.width + x + g * offsets_stride];  // frame g's offsets (stride 0: shared)
+        mine[r] = band == skip_band;
+        if constexpr (PACKED) {
+            const unsigned char* row =
+                packed + (static_cast<size_t>(band) * frames + g) * frame_bytes + static_cast<size_t>(local) * p.id_row_bytes;
+            unsigned code = 0u;
+            if (!mine[r]) {
+                code = __builtin_nontemporal_load(reinterpret_cast<const unsigned short*>(row) + x);
+                const unsigned long long* bits = reinterpret_cast<const unsigned long long*>(row + p.id_low_row_bytes);
+                for (int j = 0; j < p.id_planes; ++j) {
+                    const unsigned long long w = bits[static_cast<size_t>(j) * p.id_words + (x >> 6)];
+                    code |= static_cast<unsigned>((w >> (x & 63)) & 1ull) << (16 + j);
+                }
+            }
+            id[r] = code;
+        } else {
+            const size_t at = ((static_cast<size_t>(band) * frames + g) * band_rows + local) * p.width + x;
+            id[r] = mine[r] ? IdT{} : __builtin_nontemporal_load(ids + at);
+        }
+        o[r] = mine[r] ? float2{} : p.offsets[static_cast<size_t>(y) * p.width + x + g * offsets_stride];  // frame g's (stride 0: shared)
     }
 #pragma unroll
     for (int r = 0; r < kShadeRows; ++r) {
         const int y = y0 + r;
-        if (y < p.row_count) {
+        if (y < p.row_count && !mine[r]) {
             const float fx = (static_cast<float>(x) + o[r].x) / p.wf;
             const float fy = (static_cast<float>(FrameRow(p.row_begin, p.row_interleave, y)) + o[r].y) / p.hf;
-            int hit;
-            if constexpr (ID16) {
-                hit = DecodeId16(p, static_cast<unsigned>(id[r]), fx, fy);
-            } else {
-                hit = static_cast<unsigned>(id[r]) < p.n ? id[r] : -1;  // no id outside the scene
-            }
+            // a miss (-1, or the packed miss code of all ones) and any id outside the scene: background
+            const int hit = static_cast<unsigned>(id[r]) < p.n ? static_cast<int>(id[r]) : -1;
             const float4 v = ShadePixel(p, fx, fy, hit);
             __builtin_nontemporal_store(F4{v.x, v.y, v.z, v.w},
                                         reinterpret_cast<F4*>(p.out + g * pixels + static_cast<size_t>(y) * p.width + x));
@@ -2513,7 +2523,15 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(c
     const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);
     if (flags & kItemEmpty) {  // every pixel misses (BuildWorkOrder): the miss value, no rays
         const int xe = tx * kWave + lane;
-        if (xe < p.width) {
+        if (p.out_packed != nullptr) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int y = row0 + wave * R + r;
+                if (y < p.row_count) {
+                    StorePackedIds(p, tx, xe, y, -1);
+                }
+            }
+        } else if (xe < p.width) {
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const int y = row0 + wave * R + r;
@@ -2791,7 +2809,15 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(c
             }
         }
     }
-    if (x < p.width) {
+    if (p.out_packed != nullptr) {  // packed ids: every lane of the wave takes part (ballots)
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int y = y0 + r;
+            if (y < p.row_count) {
+                StorePackedIds(p, tx, x, y, key[r] != ~0ull ? static_cast<int>(static_cast<unsigned>(key[r])) : -1);
+            }
+        }
+    } else if (x < p.width) {
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const int y = y0 + r;
@@ -3350,8 +3376,17 @@ TraceParams MakeTraceParams(const float* d_edges, std::uint64_t n, const float* 
     p.shade = reinterpret_cast<const float4*>(d_shade);
     p.offsets = reinterpret_cast<const float2*>(band.offsets);
     p.out = reinterpret_cast<float4*>(band.rgba);
-    p.out_ids = band.ids16 ? nullptr : band.ids;
-    p.out_ids16 = band.ids16 ? reinterpret_cast<unsigned short*>(band.ids) : nullptr;
+    const bool packed = band.id_planes >= 0 && band.ids != nullptr;
+    p.out_ids = packed ? nullptr : band.ids;
+    p.out_packed = packed ? reinterpret_cast<unsigned char*>(band.ids) : nullptr;
+    if (packed) {
+        const PackedIds lay = PackedIdLayout(band.id_planes, band.row_count, band.width);
+        p.id_planes = band.id_planes;
+        p.id_words = static_cast<unsigned>(lay.words);
+        p.id_low_row_bytes = static_cast<unsigned>(lay.low_row_bytes);
+        p.id_row_bytes = static_cast<unsigned>(lay.row_bytes);
+    }
+    p.out_frame_rows = band.rgba_frame_rows ? 1 : 0;
     p.n_pad = static_cast<unsigned>(PaddedTriangleCount(n));
     p.n_tiles = static_cast<unsigned>(n == 0 ? 1 : (n + kTileTriangles - 1) / kTileTriangles);
     p.width = static_cast<int>(band.width);
@@ -3623,6 +3658,26 @@ std::size_t InterleavedBandRows(std::size_t height, std::size_t bands, std::size
     return rows;
 }
 
+int IdPlanes(std::uint64_t triangles) {
+    int bits = 16;
+    while (bits < 16 + kMaxIdPlanes && (1ull << bits) - 1ull < triangles) {  // codes 0 .. n - 1, miss = all ones
+        ++bits;
+    }
+    return (1ull << bits) - 1ull >= triangles ? bits - 16 : -1;
+}
+
+PackedIds PackedIdLayout(int planes, std::size_t rows, std::size_t width) {
+    PackedIds l;
+    l.planes = planes < 0 ? 0 : planes;
+    l.rows = rows;
+    l.width = width;
+    l.words = (width + kWave - 1) / kWave;
+    l.low_row_bytes = (width * 2 + 7) / 8 * 8;
+    l.row_bytes = l.low_row_bytes + static_cast<std::size_t>(l.planes) * l.words * 8;
+    l.bytes = (rows * l.row_bytes + 255) / 256 * 256;
+    return l;
+}
+
 hipError_t LaunchShadeTable(const float* d_vertices, const float* d_albedo, std::uint64_t n, float* d_table,
                             hipStream_t stream) {
     if (n == 0) {
@@ -3636,7 +3691,7 @@ hipError_t LaunchShadeTable(const float* d_vertices, const float* d_albedo, std:
 hipError_t LaunchShade(const float* d_vertices, const float* d_shade, const float* d_edges, std::uint64_t n,
                        const Frame& frame, const float background[3], const BandArgs& band, hipStream_t stream,
                        std::size_t frames, std::size_t band_rows, std::size_t interleaved,
-                       std::size_t offsets_stride) {
+                       std::size_t offsets_stride, long skip_band) {
     if (band.row_count == 0 || band.width == 0 || frames == 0) {
         return hipSuccess;
     }
@@ -3667,20 +3722,26 @@ hipError_t LaunchShade(const float* d_vertices, const float* d_shade, const floa
         p.bg[k] = background[k];
         p.eye[k] = frame.origin[k];
     }
-    if (band.ids16 && !Ids16Fit(n)) {
+    if (band.id_planes >= 0 && (band.id_planes > kMaxIdPlanes || IdPlanes(n) != band.id_planes)) {
         return hipErrorInvalidValue;
     }
     const dim3 grid(static_cast<unsigned>((band.width + kShadeThreads - 1) / kShadeThreads),
                     static_cast<unsigned>((band.row_count + kShadeRows - 1) / kShadeRows), static_cast<unsigned>(frames));
     const void* ids = band.ids;
-    if (band.ids16) {
+    const unsigned skip = skip_band < 0 ? 0xFFFFFFFFu : static_cast<unsigned>(skip_band);
+    if (band.id_planes >= 0) {
+        const PackedIds lay = PackedIdLayout(band.id_planes, band_rows, band.width);
+        p.id_planes = band.id_planes;
+        p.id_words = static_cast<unsigned>(lay.words);
+        p.id_low_row_bytes = static_cast<unsigned>(lay.low_row_bytes);
+        p.id_row_bytes = static_cast<unsigned>(lay.row_bytes);
         hipLaunchKernelGGL(ShadeIdsKernel<true>, grid, dim3(kShadeThreads), 0, stream, p, ids,
                            static_cast<unsigned>(band_rows), static_cast<unsigned>(frames),
-                           static_cast<unsigned>(interleaved), offsets_stride / 2);
+                           static_cast<unsigned>(interleaved), offsets_stride / 2, skip, lay.bytes);
     } else {
         hipLaunchKernelGGL(ShadeIdsKernel<false>, grid, dim3(kShadeThreads), 0, stream, p, ids,
                            static_cast<unsigned>(band_rows), static_cast<unsigned>(frames),
-                           static_cast<unsigned>(interleaved), offsets_stride / 2);
+                           static_cast<unsigned>(interleaved), offsets_stride / 2, skip, size_t{0});
     }
     return hipGetLastError();
 }

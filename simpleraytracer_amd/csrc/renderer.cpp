@@ -244,10 +244,9 @@ void DeviceScene::RecordOrder(hipStream_t stream) const {
 
 void DeviceScene::Shade(const float* d_offsets, const int* d_ids, float* d_rgba, std::size_t row_begin,
                         std::size_t row_count, hipStream_t stream, std::size_t frames, std::size_t band_rows,
-                        std::size_t interleaved, std::size_t offsets_stride, bool ids16) const {
-    if (ids16 && !Ids16Fit(m_n)) {
-        throw std::runtime_error("Shade: 16-bit id codes need at most " + std::to_string(kIds16MaxTriangles) +
-                                 " triangles");
+                        std::size_t interleaved, std::size_t offsets_stride, int id_planes, long skip_band) const {
+    if (id_planes >= 0 && id_planes != IdPlanes(m_n)) {
+        throw std::runtime_error("Shade: packed ids of this scene have " + std::to_string(IdPlanes(m_n)) + " bit planes");
     }
     if (m_width == 0) {
         throw std::runtime_error("Shade: Prepare() has not been called");
@@ -266,9 +265,9 @@ void DeviceScene::Shade(const float* d_offsets, const int* d_ids, float* d_rgba,
     }
     OrderAfterPrevious(stream);
     BandArgs band{d_offsets, d_rgba, m_width, m_height, row_begin, row_count, const_cast<int*>(d_ids)};
-    band.ids16 = ids16;
+    band.id_planes = id_planes;
     HipCheck(LaunchShade(m_vertices, m_shade, m_edges, m_n, m_frame, m_background, band, stream, frames, band_rows,
-                         interleaved, offsets_stride),
+                         interleaved, offsets_stride, skip_band),
              "shade kernel launch");
     RecordOrder(stream);
 }
@@ -355,10 +354,10 @@ DeviceScene::ParamTable& DeviceScene::AcquireTable(std::size_t frames, hipStream
 
 void DeviceScene::TraceBatch(const float* const* d_offsets, float* const* d_rgba, int* const* d_ids, std::size_t frames,
                              std::size_t row_begin, std::size_t row_count, int variant, hipStream_t stream,
-                             std::size_t row_interleave, bool ids16) const {
-    if (ids16 && (d_ids == nullptr || !Ids16Fit(m_n))) {
-        throw std::runtime_error("TraceBatch: 16-bit id codes need id outputs and at most " +
-                                 std::to_string(kIds16MaxTriangles) + " triangles");
+                             std::size_t row_interleave, int id_planes, bool rgba_frame_rows) const {
+    if (id_planes >= 0 && (id_planes != IdPlanes(m_n) || variant != kTraceCull)) {
+        throw std::runtime_error("TraceBatch: packed ids need the cull variant and " + std::to_string(IdPlanes(m_n)) +
+                                 " bit planes for this scene");
     }
     if (m_width == 0) {
         throw std::runtime_error("TraceBatch: Prepare() has not been called");
@@ -375,8 +374,9 @@ void DeviceScene::TraceBatch(const float* const* d_offsets, float* const* d_rgba
     if (variant != kTraceCull || !CullBinningEnabled() || !CullBinnable(m_width, row_count)) {
         for (std::size_t f = 0; f < frames; ++f) {  // frame by frame, each with its own record setup
             m_prepare_pending = true;
-            Trace(d_offsets[f], d_rgba != nullptr ? d_rgba[f] : nullptr, row_begin, row_count, variant, stream,
-                  d_ids != nullptr ? d_ids[f] : nullptr, row_interleave, ids16);
+            int* ids_f = d_ids != nullptr ? d_ids[f] : nullptr;
+            Trace(d_offsets[f], d_rgba != nullptr ? d_rgba[f] : nullptr, row_begin, row_count, variant, stream, ids_f,
+                  row_interleave, ids_f != nullptr ? id_planes : -1, rgba_frame_rows);
         }
         return;
     }
@@ -395,7 +395,7 @@ void DeviceScene::TraceBatch(const float* const* d_offsets, float* const* d_rgba
         cf[f].edges = m_edges + f * floats;
         cf[f].bins = &bins[f];
         cf[f].band = BandArgs{d_offsets[f], d_rgba != nullptr ? d_rgba[f] : nullptr, m_width, m_height, row_begin,
-                              row_count, d_ids != nullptr ? d_ids[f] : nullptr, row_interleave, ids16};
+                              row_count, d_ids != nullptr ? d_ids[f] : nullptr, row_interleave, id_planes, rgba_frame_rows};
     }
     const StageEvents ev = BindStageEvents(!CullFusedInfo(row_begin, row_count, m_height, row_interleave), true);
     ParamTable* table = frames > static_cast<std::size_t>(kMaxBatch) ? &AcquireTable(frames, stream) : nullptr;
@@ -412,10 +412,11 @@ void DeviceScene::TraceBatch(const float* const* d_offsets, float* const* d_rgba
 }
 
 void DeviceScene::Trace(const float* d_offsets, float* d_rgba, std::size_t row_begin, std::size_t row_count,
-                        int variant, hipStream_t stream, int* d_ids, std::size_t row_interleave, bool ids16) const {
-    if (ids16 && (d_ids == nullptr || !Ids16Fit(m_n))) {
-        throw std::runtime_error("Trace: 16-bit id codes need an id output and at most " +
-                                 std::to_string(kIds16MaxTriangles) + " triangles");
+                        int variant, hipStream_t stream, int* d_ids, std::size_t row_interleave, int id_planes,
+                        bool rgba_frame_rows) const {
+    if (id_planes >= 0 && (d_ids == nullptr || id_planes != IdPlanes(m_n) || variant != kTraceCull)) {
+        throw std::runtime_error("Trace: packed ids need an id output, the cull variant and " +
+                                 std::to_string(IdPlanes(m_n)) + " bit planes for this scene");
     }
     if (m_width == 0) {
         throw std::runtime_error("Trace: Prepare() has not been called");
@@ -424,7 +425,8 @@ void DeviceScene::Trace(const float* d_offsets, float* d_rgba, std::size_t row_b
         throw std::runtime_error("Trace: row band outside the frame");
     }
     OrderAfterPrevious(stream);
-    BandArgs band{d_offsets, d_rgba, m_width, m_height, row_begin, row_count, d_ids, row_interleave, ids16};
+    BandArgs band{d_offsets, d_rgba, m_width, m_height, row_begin, row_count, d_ids, row_interleave, id_planes,
+                  rgba_frame_rows};
     CullBins bins{};
     const CullBins* use_bins = nullptr;
     if (variant == kTraceCull && row_count != 0 && CullBinningEnabled() && CullBinnable(m_width, row_count)) {
@@ -591,11 +593,12 @@ Renderer::Renderer(const Scene& scene, std::vector<int> devices)
             m_gather_mode = GatherMode::kRccl;
         }
     }
-    // Gathered payload: 16-bit id codes where the scene allows them (render.h kId16Period; env
-    // SRT_EXCHANGE_IDS=32: int32 ids), half the bytes over xGMI.
+    // Gathered payload: packed ids (render.h PackedIds: 16 + k bits per pixel) with the cull variant
+    // (env SRT_EXCHANGE_IDS=32: int32 ids), about half the bytes over xGMI.
     {
         const char* v = std::getenv("SRT_EXCHANGE_IDS");
-        m_id_bytes = Ids16Fit(scene.triangle_count()) && !(v != nullptr && std::strcmp(v, "32") == 0) ? 2 : 4;
+        const bool force32 = v != nullptr && std::strcmp(v, "32") == 0;
+        m_id_planes = m_variant == kTraceCull && !force32 ? IdPlanes(scene.triangle_count()) : -1;
     }
     if (m_gather_mode == GatherMode::kRccl) {
         try {
@@ -640,6 +643,12 @@ Renderer::~Renderer() {
         }
         (void)hipStreamDestroy(slot->stream);
     }
+}
+
+std::size_t Renderer::BandIdBytes(std::size_t rows, std::size_t width) const {
+    // int32 ids, or one packed band frame (a multiple of 256 B) -- in whole ints either way
+    const std::size_t b = m_id_planes >= 0 ? PackedIdLayout(m_id_planes, rows, width).bytes : rows * width * sizeof(int);
+    return (b + sizeof(int) - 1) / sizeof(int) * sizeof(int);
 }
 
 void Renderer::ReleaseBuffers(Buffers& b) noexcept {
@@ -687,7 +696,7 @@ void Renderer::Configure(std::size_t width, std::size_t height) {
                 alloc(nb->offsets16[i], band_rows * width * 2, "hipMalloc(band offsets f16)");
             }
             if (gather) {
-                alloc(nb->ids[i], band_rows * width, "hipMalloc(band ids)");
+                alloc(nb->ids[i], BandIdBytes(band_rows, width) / sizeof(int), "hipMalloc(band ids)");
             } else {
                 alloc(nb->rgba[i], band_rows * width * 4, "hipMalloc(band framebuffer)");
                 if (m_out_half) {
@@ -701,7 +710,7 @@ void Renderer::Configure(std::size_t width, std::size_t height) {
             if (m_in_half) {
                 alloc(nb->full16, height * width * 2, "hipMalloc(frame offsets f16)");
             }
-            alloc(nb->gather, bands * band_rows * width, "hipMalloc(gathered ids)");
+            alloc(nb->gather, bands * BandIdBytes(band_rows, width) / sizeof(int), "hipMalloc(gathered ids)");
             alloc(nb->frame, height * width * 4, "hipMalloc(frame)");
             if (m_out_half) {
                 alloc(nb->frame16, height * width * 4, "hipMalloc(frame f16)");
@@ -832,12 +841,11 @@ void Renderer::RenderBands(const void* host_offsets, void* host_rgba) {
             CopyBandRows(i, out_bytes, w * 4 * out_elem, src, hipMemcpyDeviceToHost, true, s.stream);
         } else {
             s.scene->Trace(b.offsets[i], nullptr, s.row_begin, s.row_count, m_variant, s.stream, b.ids[i], interleave,
-                           m_id_bytes == 2);
+                           m_id_planes);
         }
     }
     if (!direct) {
         Slot& root = *m_slots.front();
-        const std::size_t band_pixels = m_band_rows * w;
         {
             DeviceGuard guard(root.device);  // the frame's offsets for shading
             void* dst = m_in_half ? static_cast<void*>(b.full16) : static_cast<void*>(b.full);
@@ -854,7 +862,7 @@ void Renderer::RenderBands(const void* host_offsets, void* host_rgba) {
             ncclResult_t first = ncclSuccess;
             for (std::size_t i = 0; i < P; ++i) {
                 Slot& s = *m_slots[i];
-                const ncclResult_t r = ncclGather(b.ids[i], i == 0 ? b.gather : nullptr, band_pixels * m_id_bytes, ncclUint8, 0,
+                const ncclResult_t r = ncclGather(b.ids[i], i == 0 ? b.gather : nullptr, BandIdBytes(m_band_rows, w), ncclUint8, 0,
                                                   static_cast<ncclComm_t>(m_comms[i]), s.stream);
                 if (r != ncclSuccess && r != ncclInProgress && first == ncclSuccess) {
                     first = r;
@@ -870,8 +878,8 @@ void Renderer::RenderBands(const void* host_offsets, void* host_rgba) {
             for (std::size_t i = 0; i < P; ++i) {
                 Slot& s = *m_slots[i];
                 DeviceGuard guard(s.device);
-                HipCheck(hipMemcpyPeerAsync(reinterpret_cast<unsigned char*>(b.gather) + i * band_pixels * m_id_bytes,
-                                            root.device, b.ids[i], s.device, band_pixels * m_id_bytes, s.stream),
+                HipCheck(hipMemcpyPeerAsync(reinterpret_cast<unsigned char*>(b.gather) + i * BandIdBytes(m_band_rows, w),
+                                            root.device, b.ids[i], s.device, BandIdBytes(m_band_rows, w), s.stream),
                          "hipMemcpyPeerAsync(band gather)");
                 if (i != 0) {
                     if (s.traced.empty()) {
@@ -887,7 +895,7 @@ void Renderer::RenderBands(const void* host_offsets, void* host_rgba) {
         }
         DeviceGuard guard(root.device);
         root.scene->Shade(b.full, b.gather, b.frame, 0, h, root.stream, 1, m_band_rows, interleave > 1 ? P : 0, 0,
-                          m_id_bytes == 2);
+                          m_id_planes);
         const void* src = b.frame;
         if (m_out_half) {
             HipCheck(LaunchFloatToHalf(b.frame, b.frame16, h * w * 4, root.stream), "framebuffer f32 -> f16");

@@ -69,9 +69,11 @@ public:
     // Trace rows [row_begin, row_begin + row_count) of the prepared frame into RGBA, or (d_ids
     // non-null, d_rgba ignored) into hit ids for deferred shading.
     // row_interleave > 1: the band deals the frame's tile rows round-robin (render.h BandArgs).
-    // ids16: d_ids points at 16-bit id codes (render.h kId16Period; Ids16Fit(triangles) must hold).
+    // id_planes >= 0: d_ids receives packed ids with that many bit planes (render.h PackedIds; the
+    // cull variant; IdPlanes(triangles) must equal it).
     void Trace(const float* d_offsets, float* d_rgba, std::size_t row_begin, std::size_t row_count, int variant,
-               hipStream_t stream, int* d_ids = nullptr, std::size_t row_interleave = 1, bool ids16 = false) const;
+               hipStream_t stream, int* d_ids = nullptr, std::size_t row_interleave = 1, int id_planes = -1,
+               bool rgba_frame_rows = false) const;
     // Deferred shading of rows [row_begin, row_begin + row_count) of the prepared frame from hit
     // ids (as Trace writes them) and sample offsets: the RGBA the fused trace would store.
     // frames > 1: a batch of that many frames of this camera, ids band-major as a gather of
@@ -80,7 +82,8 @@ public:
     // between consecutive frames' offsets (0: the batch shares d_offsets).
     void Shade(const float* d_offsets, const int* d_ids, float* d_rgba, std::size_t row_begin, std::size_t row_count,
                hipStream_t stream, std::size_t frames = 1, std::size_t band_rows = 0,
-               std::size_t interleaved = 0, std::size_t offsets_stride = 0, bool ids16 = false) const;
+               std::size_t interleaved = 0, std::size_t offsets_stride = 0, int id_planes = -1,
+               long skip_band = -1) const;  // skip_band: rows of that band are left as they are
     // `frames` (<= render.h kMaxTableFrames) frames of the prepared camera, rows [row_begin,
     // row_begin + row_count) each: frame f's offsets d_offsets[f], its RGBA d_rgba[f] or (d_ids
     // non-null) its hit ids d_ids[f]. Each frame gets the whole per-frame pipeline (record setup,
@@ -89,7 +92,9 @@ public:
     // their parameters from a device table uploaded once per call), the others frame by frame.
     void TraceBatch(const float* const* d_offsets, float* const* d_rgba, int* const* d_ids, std::size_t frames,
                     std::size_t row_begin, std::size_t row_count, int variant, hipStream_t stream,
-                    std::size_t row_interleave = 1, bool ids16 = false) const;
+                    std::size_t row_interleave = 1, int id_planes = -1, bool rgba_frame_rows = false) const;
+    // (A frame f with d_ids non-null but d_ids[f] null and d_rgba[f] non-null is traced to RGBA;
+    // rgba_frame_rows: RGBA outputs are whole frames, band rows stored at their frame rows.)
 
     std::size_t width() const { return m_width; }
     // The spatial order (device, triangles entries) and the time its build took at load (ms).
@@ -225,6 +230,7 @@ private:
     void RenderPipelined(const void* host_offsets, void* host_rgba, std::size_t chunks);
     void RenderBands(const void* host_offsets, void* host_rgba);
     bool SyncAll() noexcept;  // bounded drain of every stream; false when one did not drain
+    std::size_t BandIdBytes(std::size_t rows, std::size_t width) const;  // one band's id payload
     // Host-to-device copy of rows [0, rows) of band `i` (band-local order) from a host frame.
     void CopyBandRows(std::size_t i, const unsigned char* host, std::size_t row_bytes, unsigned char* dst,
                       hipMemcpyKind kind, bool to_host, hipStream_t stream) const;
@@ -232,7 +238,7 @@ private:
     std::vector<std::unique_ptr<Slot>> m_slots;
     std::vector<void*> m_comms;  // ncclComm_t per slot when gathering with RCCL (nonblocking, comm.h)
     bool m_comms_aborted = false;  // a failed gather aborted them: later renders fail
-    std::size_t m_id_bytes = 4;    // gathered bytes per pixel: 2 (16-bit id codes) or 4 (int32 ids)
+    int m_id_planes = -1;          // gathered ids: packed with this many bit planes (render.h PackedIds), -1 int32
     GatherMode m_gather_mode = GatherMode::kDirect;
     bool m_interleaved = true;
     std::size_t m_band_rows = 0;  // rows of every band buffer

@@ -242,21 +242,22 @@ def test_engine_frames_split_distinct_frames(gpu, scenes):
 
 
 # ---------------------------------------------------------------------------------------------
-# 16-bit id codes (render.h kId16Period): the exchange payload of scenes up to 2 x 65535 triangles
+# Packed ids (render.h PackedIds): the exchange payload, 16 + k bits per pixel
 
 
 def collision_scene(path, n=70_000, seed=5):
-    """n triangles where every code with two candidates matters: triangles k and k + 65535 (k <
-    n - 65535) are large overlapping triangles in front of the camera -- sometimes k nearer, sometimes
-    k + 65535, sometimes coplanar and identical (a depth tie: the lower id must win) -- and the
-    rest are small triangles scattered over the view, so codes with one candidate occur too."""
+    """n triangles where triangles k and k + 65536 share their low 16 bits and overlap on screen
+    (k < n - 65536): large triangles in front of the camera -- sometimes k nearer, sometimes k +
+    65536, sometimes coplanar and identical (a depth tie: the lower id must win) -- so the bit plane
+    above the low 16 bits decides every one of their pixels; the rest are small triangles scattered
+    over the view."""
     from scenefile import write_custom_scene
 
     rng = np.random.default_rng(seed)
     v = np.zeros((n, 3, 3), np.float32)
     cen = np.stack([rng.uniform(-1.2, 1.2, n), rng.uniform(-0.7, 0.7, n), rng.uniform(3.0, 6.0, n)], 1)
     v[:] = cen[:, None, :] + rng.uniform(-0.03, 0.03, (n, 3, 3))
-    pairs = n - 65535
+    pairs = n - 65536
     for k in range(pairs):
         c = np.array([rng.uniform(-1.0, 1.0), rng.uniform(-0.5, 0.5), 0.0])
         z_a, z_b = rng.uniform(1.5, 2.5), rng.uniform(1.5, 2.5)
@@ -268,14 +269,14 @@ def collision_scene(path, n=70_000, seed=5):
             b[:, :2] = b[:, :2] * 0.9 + 0.05  # overlapping, not identical
         a[:, 2] += z_a
         b[:, 2] += z_b
-        v[k], v[k + 65535] = a, b
+        v[k], v[k + 65536] = a, b
     return write_custom_scene(path, v, rng.uniform(0.2, 1.0, (n, 3)))
 
 
-def test_ids16_codes_decode_exactly(gpu, tmp_path):
-    """70 000 triangles (every code below 4465 has two candidates, and those pairs overlap on
-    screen): the 16-bit id codes through the fake-device exchange (P = 2 and 3) and the one-rank
-    RCCL exchange give the one-device frame bit for bit, with random per-pixel offsets."""
+def test_packed_ids_exchange_bitwise(gpu, tmp_path, monkeypatch):
+    """70 000 triangles (one bit plane): ids that differ only above bit 15 cover the same pixels.
+    Packed ids through the fake-device exchange (P = 2 and 3) and the one-rank RCCL exchange, and
+    int32 ids (SRT_EXCHANGE_IDS=32), give the one-device frame bit for bit, random offsets."""
     from simpleraytracer_amd.engine import FrameEngine
 
     path = collision_scene(tmp_path / "collide.srt")
@@ -283,18 +284,24 @@ def test_ids16_codes_decode_exactly(gpu, tmp_path):
     inputs = np.random.default_rng(9).random((1, h, w, 2), dtype=np.float32)
     ref = torch_render(path, w, h, inputs[0])
     ids = ref[..., 3].astype(np.int64)
-    assert (ids >= 65535).sum() > 1000 and ((ids >= 0) & (ids < 70_000 - 65535)).sum() > 1000, \
-        "the scene must put both halves of the colliding pairs on screen"
-    for kw in ({"devices": [0, 0]}, {"devices": [0, 0, 0]}, {"devices": [0], "rccl_self": True}):
-        with FrameEngine(path, w, h, batch=6, queues=2, **kw) as e:
-            e.set_inputs(inputs)
-            e.run(2)
-            for k in range(12):
-                assert np.array_equal(e.read_frame(k).view(np.uint32), ref.view(np.uint32)), (kw, k)
+    assert (ids >= 65536).sum() > 1000 and ((ids >= 0) & (ids < 70_000 - 65536)).sum() > 1000, \
+        "the scene must put both members of the sharing pairs on screen"
+    for ids32 in (False, True):
+        if ids32:
+            monkeypatch.setenv("SRT_EXCHANGE_IDS", "32")
+        for kw in ({"devices": [0, 0]}, {"devices": [0, 0, 0]}, {"devices": [0], "rccl_self": True}):
+            with FrameEngine(path, w, h, batch=6, queues=2, **kw) as e:
+                xb = e.info()["exchange_bytes_per_frame"]
+                e.set_inputs(inputs)
+                e.run(2)
+                for k in range(12):
+                    assert np.array_equal(e.read_frame(k).view(np.uint32), ref.view(np.uint32)), (ids32, kw, k)
+            if len(kw["devices"]) == 2:  # bands of 16-row tile rows: 5 and 4 of the 9, buffers of 80 rows
+                assert xb == (80 * 256 * 4 if ids32 else 80 * 256 * 2 + 80 * 4 * 8), xb  # 4 B or 2.125 B a pixel
 
 
-def test_ids16_mlinfer_gather_decodes_exactly(gpu, tmp_path, monkeypatch):
-    """The mlInfer gather (fake devices, device copies) carries 16-bit codes for the same scene."""
+def test_packed_ids_mlinfer_gather_bitwise(gpu, tmp_path, monkeypatch):
+    """The mlInfer gather (fake devices, device copies) with packed and with int32 ids."""
     import simpleraytracer_amd as srt
 
     path = collision_scene(tmp_path / "collide.srt")
@@ -306,3 +313,16 @@ def test_ids16_mlinfer_gather_decodes_exactly(gpu, tmp_path, monkeypatch):
     monkeypatch.setenv("SRT_EXCHANGE_IDS", "32")
     got32 = srt.render(path, w, h)
     assert np.array_equal(got32.view(np.uint32), ref.view(np.uint32))
+
+
+def test_engine_c5_bands_packed_ids(gpu, paths, ids):
+    """C5 (1M triangles: four bit planes) split over 2 fake devices, every frame on the 64 stored rows."""
+    from simpleraytracer_amd.engine import FrameEngine
+
+    m = META[C5]
+    want = Expected(paths[C5], C5, ids[C5])
+    with FrameEngine(paths[C5], m["width"], m["height"], devices=[0, 0], batch=2, queues=1) as e:
+        e.set_inputs(offsets_for(m))
+        e.run(1)
+        for k in range(2):
+            want.check(e.read_frame(k), f"frame {k}")
