@@ -657,7 +657,16 @@ __global__ __launch_bounds__(kShadeThreads) void ShadeIdsKernel(TraceParams p, c
             const size_t at = ((static_cast<size_t>(band) * frames + g) * band_rows + local) * p.width + x;
             id[r] = mine[r] ? IdT{} : __builtin_nontemporal_load(ids + at);
         }
-        o[r] = mine[r] ? float2{} : p.offsets[static_cast<size_t>(y) * p.width + x + g * offsets_stride];  // frame g's (stride 0: shared)
+    }
+    // Only a hit needs its ray: a miss shades to the background whatever its sample offset, so the
+    // offsets of the miss pixels (72 % of C3's) are never loaded. A miss is -1, the packed miss code
+    // (all ones) or any id outside the scene.
+    int hit[kShadeRows];
+#pragma unroll
+    for (int r = 0; r < kShadeRows; ++r) {
+        const int y = min(y0 + r, p.row_count - 1);
+        hit[r] = !mine[r] && static_cast<unsigned>(id[r]) < p.n ? static_cast<int>(id[r]) : -1;
+        o[r] = hit[r] < 0 ? float2{} : p.offsets[static_cast<size_t>(y) * p.width + x + g * offsets_stride];  // frame g's (stride 0: shared)
     }
 #pragma unroll
     for (int r = 0; r < kShadeRows; ++r) {
@@ -665,9 +674,7 @@ __global__ __launch_bounds__(kShadeThreads) void ShadeIdsKernel(TraceParams p, c
         if (y < p.row_count && !mine[r]) {
             const float fx = (static_cast<float>(x) + o[r].x) / p.wf;
             const float fy = (static_cast<float>(FrameRow(p.row_begin, p.row_interleave, y)) + o[r].y) / p.hf;
-            // a miss (-1, or the packed miss code of all ones) and any id outside the scene: background
-            const int hit = static_cast<unsigned>(id[r]) < p.n ? static_cast<int>(id[r]) : -1;
-            const float4 v = ShadePixel(p, fx, fy, hit);
+            const float4 v = ShadePixel(p, fx, fy, hit[r]);
             __builtin_nontemporal_store(F4{v.x, v.y, v.z, v.w},
                                         reinterpret_cast<F4*>(p.out + g * pixels + static_cast<size_t>(y) * p.width + x));
         }
