@@ -143,10 +143,11 @@ struct CullBins {
     const unsigned* order; // the scene's record ids in spatial order (DeviceScene; not in the buffer)
     const float* svertices;  // the scene's vertices in that order (DeviceScene; not in the buffer)
     void* tile_info;       // tiles x 32 B: ray box, uniform offset (TileInfoKernel)
-    unsigned* counts;      // tiles + 1: list lengths, then the large-list length
+    unsigned* counts;      // tiles + 1: list lengths, then the large-list length (this frame's buffer)
+    unsigned* counts_next; // the slot's other count buffer (its next frame's): zeroed by this frame's trace
     unsigned* lists;       // tiles x capacity candidate ids (BinTrianglesKernel)
     unsigned* large_list;  // PaddedTriangleCount(n) ids binned to every tile
-    void* work;            // trace work list (WorkOrderKernel): descs descriptors, 32 B each
+    void* work;            // trace work plan (WorkOrderKernel): descs descriptors, 32 B each
     unsigned* work_count;  // its length
     unsigned* arrive;      // per split slot: split chunks finished (self-resetting counters)
     void* split_keys;      // key slices of split parts: one per split slot (<= descs), 8 KiB each
@@ -155,6 +156,7 @@ struct CullBins {
     unsigned gen;          // the scene's frame number (never 0): tags are compared with it, not reset
     unsigned capacity;
     std::size_t tiles;
+    bool plan = true;      // (re)build the slot's work plan with this frame (else the trace uses the last one)
 };
 
 // Tiles (64 x 32 rays) of a width x row_count band.
@@ -178,7 +180,8 @@ unsigned CullDescriptors(std::size_t tiles, std::size_t frames);
 
 // Bytes of the bin work buffer for n triangles and a band shape, and its carve-up.
 std::size_t CullBinBytes(std::uint64_t n, std::size_t width, std::size_t row_count);
-CullBins CullBinLayout(void* base, std::uint64_t n, std::size_t width, std::size_t row_count);
+// parity: which of the slot's two count buffers this frame bins into (alternate per frame of a slot).
+CullBins CullBinLayout(void* base, std::uint64_t n, std::size_t width, std::size_t row_count, unsigned parity = 0);
 
 // Optional stage timing events (null = not recorded). They are bound to the kernels' own
 // dispatch packets (hipExtLaunchKernelGGL start / stop events), so timing adds no marker

@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <cstring>
 #include <stdexcept>
+#include <string>
 #include <type_traits>
 
 namespace srt {
@@ -99,8 +100,13 @@ struct TraceParams {
     unsigned long long* __restrict__ split_keys;  // key slices of split parts: one per split slot, kBlockRows x 64 each
     unsigned* __restrict__ arrive;            // per split part (its first slot): chunks finished (self-resetting)
     const unsigned* __restrict__ bin_lists;   // per tile: candidate positions (PrepareBinKernel)
-    unsigned* __restrict__ bin_counts;  // per tile: list length; [tiles]: large-list length (reset by the trace)
+    const unsigned* __restrict__ bin_counts;  // per tile: list length; [tiles]: large-list length (this frame's)
+    unsigned* __restrict__ bin_counts_next;   // the slot's other count buffer: reset by the trace for its next frame
     const unsigned* __restrict__ large_list;  // ids of records binned to every tile
+    const unsigned* __restrict__ range_tag;   // = gen: some sample offset of this frame lies outside [0, 1]
+    unsigned gen;                              // frame number of the scene (never 0)
+    unsigned fused;                            // bins from the analytic tile bounds (BinParams::fused)
+    unsigned plan_only;  // the work list is the slot's plan (no order launch for this frame): read the bins
     unsigned bin_capacity;
     unsigned exp;                                // diagnostic build: experiment bits (env SRT_EXP), 0 in the product
     float wf;
@@ -1672,8 +1678,14 @@ __device__ __forceinline__ int LastLoAtMost(const float2* b, int n, float v, con
     return g - 1;
 }
 
-// Trace work list (WorkOrderKernel, after the bin kernel). One 32-B descriptor per trace block:
-// a tile part, or one candidate chunk of a split part. The grid has room for p.descs
+// Trace work plan (WorkOrderKernel, after the bin kernel of a slot's first frame of a band shape;
+// render.h CullBins::plan). One 32-B descriptor per trace block: a tile part, or one candidate
+// chunk of a split part. The plan is scheduling only: a plan-only trace block (a frame that reuses
+// the slot's plan) takes its part, chunk index, chunk count and split slot from it and everything
+// it computes from its own frame's bins and tile info, so a plan made from any frame of the slot's
+// band shape gives the same frame (the candidate counts of frames with offsets in [0, 1] do not
+// depend on the offsets: analytic tile bounds), and that frame's pipeline is the bin launch and
+// the trace. The grid has room for p.descs
 // descriptors D; with P parts holding C candidates in all (each part counted with its tile's
 // candidates), chunks of S = the power of two >= max(p.min_chunk, C / (D - P)) candidates fit,
 // since sum ceil(c / S) <= P + C / S <= D. So the heavy parts -- which bound a frame's trace
@@ -1684,9 +1696,13 @@ __device__ __forceinline__ int LastLoAtMost(const float2* b, int n, float v, con
 // list length, flags), w1 = (sample offset x, y of the tile's first ray, chunk | chunks << 16,
 // first split slot of the part); flags: 1 = every ray of the tile has that offset, 2 = FULL. A
 // split part's chunks own consecutive split slots (key slices; the arrival counter at the first).
+// A trace launched after this kernel (the same frame) takes the rest from the descriptor too, with
+// flags 4 = empty (no candidate can hit a ray of the tile) and FULL also when the frame's bins are
+// invalid; a plan-only trace (a later frame) reads those facts from its own bins (TraceParams::
+// plan_only). The chunking is made as if every offset were in [0, 1], so it may serve later frames.
 // (Gathering whole empty tiles four to a descriptor, one block storing all their misses, cut the
 // trace grid by ~950 blocks at C3 and measured no faster: an empty part's block is cheap.)
-// (BinParams::work_count: the single-block measurement build's list length; kOrderWords words.)
+// (BinParams::work_count: kOrderWords words, unused by the product kernels.)
 constexpr int kOrderBuckets = 64;
 constexpr int kOrderWords = 72;
 constexpr unsigned kItemRegular = 1u;
@@ -1715,153 +1731,6 @@ __device__ __forceinline__ void ItemChunks(unsigned cand, unsigned flags, unsign
     const unsigned per = cand >> (31u - __builtin_clz(nch));  // ~ candidates per chunk
     bucket = full ? 63u : (per == 0u ? 0u : 32u - __builtin_clz(per));
 }
-// Called by every thread of the order block; start = 64 LDS words, cnt / meta = tiles LDS
-// words / bytes, sum = 2 LDS words. (1) lengths + tile flags into LDS, the candidate total;
-// (2) the chunk size, the bucket histogram (LDS only); (3) tile info again -> descriptors.
-#ifdef SRT_ORDER_SINGLE
-constexpr int kOrderUnroll = 4;
-__device__ void BuildWorkOrder(const BinParams& p, unsigned* start, unsigned* cnt, unsigned char* meta,
-                               unsigned* sum, CullRecord* lrec) {
-    const int tid = threadIdx.x;
-    const int lane = tid & (kWave - 1);
-    const unsigned nthreads = blockDim.x;
-    const unsigned tiles = static_cast<unsigned>(p.tiles_x * p.tiles_y);
-    if (tid < 64) {
-        start[tid] = 0u;
-    }
-    if (tid < 2) {
-        sum[tid] = 0u;
-    }
-    const unsigned large = p.counts[tiles];
-    // A fused launch binned with the analytic tile bounds, which hold only for offsets in [0, 1]:
-    // if a tile-info block found one outside (the range tag), every tile streams every record.
-    const bool bins_invalid = p.fused != 0u && *p.range_tag == p.gen;
-    if (tid < kEmptyTest && static_cast<unsigned>(tid) < large && large <= static_cast<unsigned>(kEmptyTest)) {
-        lrec[tid] = p.cull[p.large_list[tid]];  // read after the barriers below
-    }
-    unsigned long long my_cand = 0ull;
-    unsigned my_parts = 0u;
-    for (unsigned t0 = tid; t0 < tiles; t0 += kOrderUnroll * nthreads) {
-        unsigned c[kOrderUnroll];
-        TileInfo ti[kOrderUnroll];
-#pragma unroll
-        for (int u = 0; u < kOrderUnroll; ++u) {
-            const unsigned t = min(t0 + u * nthreads, tiles - 1u);
-            c[u] = p.counts[t];
-            ti[u] = p.tile_info[t];
-        }
-#pragma unroll
-        for (int u = 0; u < kOrderUnroll; ++u) {
-            const unsigned t = t0 + u * nthreads;
-            if (t < tiles) {
-                p.counts[t] = 0u;  // the next frame of this slot bins from zero (stream order)
-                const OrderItem it = MakeOrderItem(p, t, c[u], large, ti[u], bins_invalid);
-                cnt[t] = it.cand;
-                meta[t] = static_cast<unsigned char>(it.flags | it.parts << 2);
-                my_cand += static_cast<unsigned long long>(it.parts) * it.cand;
-                my_parts += it.parts;
-            }
-        }
-    }
-    // Candidates in units of 16 (a 32-bit total up to 2^36), rounded up; parts.
-    unsigned v16 = static_cast<unsigned>((my_cand + 15ull) >> 4), vp = my_parts;
-#pragma unroll
-    for (int o = 1; o < kWave; o <<= 1) {
-        v16 += __shfl_xor(v16, o);
-        vp += __shfl_xor(vp, o);
-    }
-    __syncthreads();  // start[], sum[] zeroed
-    if (lane == 0) {
-        atomicAdd(&sum[0], v16);
-        atomicAdd(&sum[1], vp);
-    }
-    __syncthreads();
-    unsigned shift = 31u;  // chunk size 2^31: no split
-    if (p.descs > sum[1]) {
-        const unsigned room = p.descs - sum[1];
-        const unsigned long long want = (16ull * sum[0] + room - 1ull) / room;  // C / (D - P), rounded up
-        const unsigned long long size = want > p.min_chunk ? want : p.min_chunk;
-        shift = size >= (1ull << 31) ? 31u : 64u - static_cast<unsigned>(__builtin_clzll(size - 1ull));
-        shift = size <= 1ull ? 0u : shift;
-    }
-    for (unsigned t = tid; t < tiles; t += nthreads) {
-        const unsigned parts = meta[t] >> 2;
-        if (parts != 0u) {
-            unsigned nch, bucket;
-            ItemChunks(cnt[t], meta[t] & 3u, shift, nch, bucket);
-            atomicAdd(&start[bucket], parts * nch);
-        }
-    }
-    __syncthreads();
-    if (tid < kWave) {  // bucket b's first slot: the descriptors in heavier buckets (suffix sum, exclusive)
-        const unsigned c = start[lane];
-        unsigned suf = c;
-#pragma unroll
-        for (int o = 1; o < kWave; o <<= 1) {
-            const unsigned u = __shfl_down(suf, o);
-            suf += lane + o < kWave ? u : 0u;
-        }
-        start[lane] = suf - c;
-        if (lane == 0) {
-            p.counts[tiles] = 0u;  // the large list (every thread read it before the barriers above)
-            p.work_count[0] = suf;
-            sum[0] = 0u;  // split slots handed out (sum[] read by every thread before the barrier above)
-            sum[1] = suf;
-        }
-    }
-    __syncthreads();
-    // Descriptors past the list end: an end mark, so a trace block needs no count load first.
-    for (unsigned d = sum[1] + tid; d < p.descs; d += nthreads) {
-        p.work[2 * d] = make_uint4(kWorkEnd, 0u, 0u, 0u);
-    }
-    for (unsigned t0 = tid; t0 < tiles; t0 += kOrderUnroll * nthreads) {
-        TileInfo ti[kOrderUnroll];
-#pragma unroll
-        for (int u = 0; u < kOrderUnroll; ++u) {
-            ti[u] = p.tile_info[min(t0 + u * nthreads, tiles - 1u)];
-        }
-#pragma unroll
-        for (int u = 0; u < kOrderUnroll; ++u) {
-            const unsigned t = t0 + u * nthreads;
-            if (t >= tiles) {
-                continue;
-            }
-            const unsigned parts = meta[t] >> 2, flags = meta[t] & 3u, cand = cnt[t];
-            if (parts == 0u) {
-                continue;
-            }
-            unsigned nch, bucket;
-            ItemChunks(cand, flags, shift, nch, bucket);
-            const unsigned at = atomicAdd(&start[bucket], parts * nch);
-            const unsigned slot = nch > 1u ? atomicAdd(&sum[0], parts * nch) : 0u;
-            const unsigned list_len = (flags & kItemFull) ? 0u : cand - large;
-            // Empty bin list and few large-list records: if none of those can hit a ray of the
-            // tile box (the tests the trace blocks run against their part boxes, which lie inside
-            // it), every pixel misses (a ray outside the box has a NaN position and misses too).
-            unsigned out_flags = flags;
-            if ((flags & kItemFull) == 0u && list_len == 0u && large <= static_cast<unsigned>(kEmptyTest)) {
-                const Box tb{ti[u].box.x, ti[u].box.y, ti[u].box.z, ti[u].box.w};
-                bool may = false;
-                for (unsigned k = 0; k < large; ++k) {
-                    const CullRecord& r = lrec[k];
-                    const Record q{r.a.x, r.a.y, r.a.z, r.a.w, r.b.x, r.b.y, r.b.z, r.b.w, r.x.x};
-                    may = may || (ScreenBoxOverlaps(tb, r.sb) && BoxMayHit(tb, q));
-                }
-                out_flags |= may ? 0u : kItemEmpty;
-            }
-            for (unsigned part = 0; part < parts; ++part) {
-                for (unsigned ch = 0; ch < nch; ++ch) {
-                    const unsigned d = at + part * nch + ch;
-                    p.work[2 * d] = make_uint4(t * kParts + part, cand, list_len, out_flags);
-                    p.work[2 * d + 1] = make_uint4(__float_as_uint(ti[u].ox), __float_as_uint(ti[u].oy),
-                                                   ch | nch << 16, slot + part * nch);
-                }
-            }
-        }
-    }
-}
-
-#endif  // SRT_ORDER_SINGLE
 
 // A bin block's monotone tile-column and tile-row bounds (lo' nondecreasing, hi' nondecreasing)
 // into out[0 .. nx + ny) in LDS; `scratch` = 2 (nx + ny) LDS words; ends with a barrier.
@@ -2189,23 +2058,6 @@ constexpr int kOrderTilesPerThread = 8;  // tiles' loads in flight per thread (o
 #endif
 constexpr int kOrderCopies = SRT_ORDER_COPIES;  // LDS copies of the bucket histograms (lane l: copy l % copies)
 constexpr int kOrderStride = kOrderBuckets + 1;  // words per copy: the copies of one bucket in different banks
-#ifdef SRT_ORDER_SINGLE  // measurement builds only: round 2's single-block counting sort
-#ifndef SRT_ORDER_THREADS
-#define SRT_ORDER_THREADS 1024
-#endif
-constexpr int kOrderThreads = SRT_ORDER_THREADS;
-template <class Frames>
-__global__ __launch_bounds__(kOrderThreads) void WorkOrderKernel(const Frames batch) {
-    __shared__ unsigned start[64];
-    __shared__ unsigned sum[2];
-    __shared__ CullRecord lrec[kEmptyTest];
-    extern __shared__ unsigned order_lds[];
-    const BinParams& p = batch[blockIdx.z];
-    unsigned* cnt = order_lds;
-    unsigned char* meta = reinterpret_cast<unsigned char*>(order_lds + p.tiles_x * p.tiles_y);
-    BuildWorkOrder(p, start, cnt, meta, sum, lrec);
-}
-#else
 template <class Frames>
 __global__ __launch_bounds__(kOrderBlock) void WorkOrderKernel(const Frames batch) {
     const BinParams& p = batch[blockIdx.z];
@@ -2242,7 +2094,11 @@ __global__ __launch_bounds__(kOrderBlock) void WorkOrderKernel(const Frames batc
     const unsigned mine = first + static_cast<unsigned>(tid);
     const TileInfo my_ti = p.tile_info[min(mine, tiles - 1u)];
     const unsigned large = p.counts[tiles];
-    const bool bins_invalid = p.fused != 0u && *p.range_tag == p.gen;  // MakeOrderItem: every tile FULL
+    // A fused launch binned with the analytic tile bounds, which hold only for offsets in [0, 1]:
+    // if a tile-info block found one outside (the range tag), every tile streams every record (its
+    // descriptors say FULL). The plan itself is made as if the offsets were in range: it may serve
+    // the slot's later frames.
+    const bool bins_invalid = p.fused != 0u && *p.range_tag == p.gen;
     if (tid < kOrderBuckets) {
         local[tid] = 0u;
     }
@@ -2270,7 +2126,7 @@ __global__ __launch_bounds__(kOrderBlock) void WorkOrderKernel(const Frames batc
                 TileInfo ti{};
                 ti.regular = ru[u].x;
                 ti.usable = ru[u].y;
-                const OrderItem it = MakeOrderItem(p, t, c[u], large, ti, bins_invalid);
+                const OrderItem it = MakeOrderItem(p, t, c[u], large, ti, false);
                 cnt[t] = it.cand;
                 meta[t] = static_cast<unsigned char>(it.flags | it.parts << 2);
                 my_cand += static_cast<unsigned long long>(it.parts) * it.cand;
@@ -2385,8 +2241,13 @@ __global__ __launch_bounds__(kOrderBlock) void WorkOrderKernel(const Frames batc
         const unsigned slot = my_nch > 1u ? sums[3] + my_slot : 0u;
         const unsigned flags = meta[t] & 3u, cand = cnt[t], parts = meta[t] >> 2;
         const unsigned list_len = (flags & kItemFull) ? 0u : cand - large;
-        unsigned out_flags = flags;
-        if ((flags & kItemFull) == 0u && list_len == 0u && large <= static_cast<unsigned>(kEmptyTest)) {
+        // This frame's facts (read by a trace of this launch; a plan-only trace reads its own):
+        // FULL when the bins are invalid, and empty when the bin list is empty and none of the
+        // few large-list records can hit a ray of the tile box (the tests the trace blocks run
+        // against their part boxes, which lie inside it: every pixel misses; a ray outside the box
+        // has a NaN position and misses too).
+        unsigned out_flags = flags | (bins_invalid ? kItemFull : 0u);
+        if ((out_flags & kItemFull) == 0u && list_len == 0u && large <= static_cast<unsigned>(kEmptyTest)) {
             const Box tb{my_ti.box.x, my_ti.box.y, my_ti.box.z, my_ti.box.w};
             bool may = false;
             for (unsigned k = 0; k < large; ++k) {
@@ -2415,7 +2276,6 @@ __global__ __launch_bounds__(kOrderBlock) void WorkOrderKernel(const Frames batc
 #endif
     // (the bin counts are reset by the trace blocks that consume these descriptors)
 }
-#endif
 
 std::size_t OrderLdsBytes(int tiles) { return static_cast<std::size_t>(tiles) * 5 + 16; }
 
@@ -2472,37 +2332,85 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(c
     float ox = 0.f, oy = 0.f;
     CullSource src{nullptr, nullptr, 0u, 0u, 0u, true};
     if (p.work != nullptr) {
-        const unsigned d = blockIdx.x;  // < descs: the list, then end marks
+        // The work list (WorkOrderKernel) gives this block its tile part and chunk; with an order
+        // launch for this frame it also holds the frame's facts, else it is the slot's plan
+        // (scheduling only) and the block reads them from the frame's bins and tile info.
+        const unsigned d = blockIdx.x;  // < descs: the plan, then end marks
         const uint4 w0 = p.work[2 * d], w1 = p.work[2 * d + 1];
         if (w0.x == kWorkEnd) {
             return;
         }
         item = w0.x;
-        flags = w0.w;
-        ox = __uint_as_float(w1.x);
-        oy = __uint_as_float(w1.y);
         chunk = w1.z & 0xFFFFu;
-        nchunks = w1.z >> 16;
+        nchunks = max(w1.z >> 16, 1u);
         slot = w1.w;
-        // The bin counts this launch's work order read, zeroed for the slot's next frame: each
-        // tile's by its first part's first chunk, the large list's by the first descriptor.
+        const unsigned t = item / kParts;
+        // The slot's next frame bins into the other count buffer: each tile's count reset by its
+        // first part's first chunk, the large list's by the first descriptor.
         if (threadIdx.x == 0 && chunk == 0u && item % kParts == 0u) {
-            p.bin_counts[item / kParts] = 0u;
+            p.bin_counts_next[t] = 0u;
         }
         if (threadIdx.x == 0 && d == 0u) {
-            p.bin_counts[p.tiles] = 0u;
+            p.bin_counts_next[p.tiles] = 0u;
         }
 #ifdef SRT_EXP_SETUP_ONLY  // measurement builds only (make exp): the frame's setup without its trace
         return;
 #endif
-        src.full = (flags & kItemFull) != 0u;
+        bool full;
+        unsigned c_t, list_len;
+        if (p.plan_only != 0u) {
+            // This frame's facts, which the order kernel would have put in the descriptor.
+            const unsigned cnt = p.bin_counts[t], large = p.bin_counts[p.tiles];
+            const TileInfo ti = p.tile_info[t];
+            unsigned lid[kEmptyTest];  // the large list's first entries (used only when it is that short)
+#pragma unroll
+            for (int k = 0; k < kEmptyTest; ++k) {
+                lid[k] = p.large_list[k];
+            }
+            const bool bins_invalid = p.fused != 0u && *p.range_tag == p.gen;  // (WorkOrderKernel)
+            full = ti.usable == 0u || cnt > p.bin_capacity || bins_invalid;
+            flags = (full ? kItemFull : 0u) | (ti.regular != 0u ? kItemRegular : 0u);
+            ox = ti.ox;
+            oy = ti.oy;
+            c_t = full ? 0u : cnt + large;
+            list_len = full ? 0u : cnt;
+            if (!full && cnt == 0u && large <= static_cast<unsigned>(kEmptyTest) && nchunks == 1u) {
+                const Box tb{ti.box.x, ti.box.y, ti.box.z, ti.box.w};  // the empty test (WorkOrderKernel)
+                CullRecord lr[kEmptyTest];
+#pragma unroll
+                for (int k = 0; k < kEmptyTest; ++k) {
+                    if (static_cast<unsigned>(k) < large) {
+                        lr[k] = p.cull[lid[k]];
+                    }
+                }
+                bool may = false;
+#pragma unroll
+                for (int k = 0; k < kEmptyTest; ++k) {
+                    if (static_cast<unsigned>(k) < large) {
+                        const Record q{lr[k].a.x, lr[k].a.y, lr[k].a.z, lr[k].a.w, lr[k].b.x, lr[k].b.y, lr[k].b.z,
+                                       lr[k].b.w, lr[k].x.x};
+                        may = may || (ScreenBoxOverlaps(tb, lr[k].sb) && BoxMayHit(tb, q));
+                    }
+                }
+                flags |= may ? 0u : kItemEmpty;
+            }
+        } else {
+            flags = w0.w;
+            ox = __uint_as_float(w1.x);
+            oy = __uint_as_float(w1.y);
+            full = (flags & kItemFull) != 0u;
+            c_t = full ? 0u : w0.y;
+            list_len = full ? 0u : w0.z;
+        }
+        // A FULL tile streams every record in its part's first chunk; the plan's other chunks of
+        // the part (the plan is made as if the bins were valid) have no candidates and publish misses.
+        src.full = full && chunk == 0u;
         if (!src.full) {
             // candidates cut into n chunks: chunk c = [c q + c r / n, (c + 1) q + (c + 1) r / n), q r = c_t / n, % n
-            const unsigned c_t = w0.y;
             const unsigned q = c_t / nchunks, r = c_t % nchunks;
-            src.list = p.bin_lists + static_cast<size_t>(item / kParts) * p.bin_capacity;
+            src.list = p.bin_lists + static_cast<size_t>(t) * p.bin_capacity;
             src.list2 = p.large_list;
-            src.count1 = w0.z;
+            src.count1 = list_len;
             src.begin = chunk * q + chunk * r / nchunks;
             src.end = (chunk + 1u) * q + (chunk + 1u) * r / nchunks;
 #if SRT_TRACE_PRIO
@@ -3299,6 +3207,19 @@ long EnvLong(const char* name, long fallback) {
     return v == nullptr || *v == '\0' ? fallback : std::strtol(v, nullptr, 10);
 }
 
+// When a cull launch runs the work order (env SRT_WORK_PLAN): "auto" (default) for launches of
+// several frames, which fill the chip -- there the order launch overlaps other queues' work, while
+// a plan-only trace's extra dependent loads at each block's start cost throughput -- and the slot's
+// plan for single-frame launches, whose latency the order launch would lengthen; "reuse": plans
+// whenever the slots have one; "order": every launch (a slot without a plan for its trace grid
+// always gets the order launch).
+enum class WorkPlan { kAuto, kReuse, kOrder };
+WorkPlan WorkPlanFromEnv() {
+    const char* v = std::getenv("SRT_WORK_PLAN");
+    const std::string m = v == nullptr ? "" : v;
+    return m == "reuse" ? WorkPlan::kReuse : m == "order" ? WorkPlan::kOrder : WorkPlan::kAuto;
+}
+
 struct BinSizes {
     std::size_t info, counts, lists, large, work, work_count, arrive, split_keys, range_tag;
 };
@@ -3310,7 +3231,7 @@ BinSizes CullBinSizes(std::uint64_t n, std::size_t width, std::size_t row_count)
     const bool split = descs > tiles * kParts;
     BinSizes z;
     z.info = al(tiles * sizeof(TileInfo));
-    z.counts = al((tiles + 1) * 4);
+    z.counts = al(2 * (tiles + 1) * 4);  // two buffers: a frame bins into one, its trace resets the other
     z.lists = al(tiles * static_cast<std::size_t>(CullBinCapacity(n, tiles)) * 4);
     z.large = al(PaddedTriangleCount(n) * 4);
     z.work = al(descs * 2 * sizeof(uint4));
@@ -3346,7 +3267,7 @@ std::size_t CullBinBytes(std::uint64_t n, std::size_t width, std::size_t row_cou
     return z.info + z.counts + z.lists + z.large + z.work + z.work_count + z.arrive + z.split_keys + z.range_tag;
 }
 
-CullBins CullBinLayout(void* base, std::uint64_t n, std::size_t width, std::size_t row_count) {
+CullBins CullBinLayout(void* base, std::uint64_t n, std::size_t width, std::size_t row_count, unsigned parity) {
     const BinSizes z = CullBinSizes(n, width, row_count);
     unsigned char* w = static_cast<unsigned char*>(base);
     CullBins b{};
@@ -3356,7 +3277,7 @@ CullBins CullBinLayout(void* base, std::uint64_t n, std::size_t width, std::size
         return at;
     };
     b.tile_info = take(z.info);
-    b.counts = reinterpret_cast<unsigned*>(take(z.counts));
+    unsigned* counts = reinterpret_cast<unsigned*>(take(z.counts));
     b.lists = reinterpret_cast<unsigned*>(take(z.lists));
     b.large_list = reinterpret_cast<unsigned*>(take(z.large));
     b.work = take(z.work);
@@ -3365,6 +3286,8 @@ CullBins CullBinLayout(void* base, std::uint64_t n, std::size_t width, std::size
     b.split_keys = take(z.split_keys);
     b.range_tag = reinterpret_cast<unsigned*>(take(z.range_tag));
     b.tiles = CullTiles(width, row_count);
+    b.counts = counts + (parity & 1u) * (b.tiles + 1);
+    b.counts_next = counts + ((parity & 1u) ^ 1u) * (b.tiles + 1);
     b.capacity = CullBinCapacity(n, b.tiles);
     b.descs = z.split_keys != 0 ? CullDescriptors(b.tiles, 1) : static_cast<unsigned>(b.tiles * kParts);
     return b;
@@ -3454,6 +3377,9 @@ BinParams BindBins(TraceParams& p, const CullBins& bins, std::uint64_t n) {
     p.arrive = bins.arrive;
     p.bin_lists = bins.lists;
     p.bin_counts = bins.counts;
+    p.bin_counts_next = bins.counts_next;
+    p.range_tag = bins.range_tag;
+    p.gen = bins.gen;
     p.large_list = bins.large_list;
     p.bin_capacity = bins.capacity;
     return b;
@@ -3465,20 +3391,20 @@ namespace {
 // kernel arguments (FrameArgs) or a device table (FrameTable).
 template <class TB, class BB, class PB>
 void LaunchCullStages(const TB& tb, const BB& bb, const PB& pb, unsigned z, unsigned gx, unsigned gy, unsigned blocks,
-                      bool fused, unsigned descs, hipStream_t stream, const StageEvents& ev) {
+                      bool fused, bool order, unsigned descs, hipStream_t stream, const StageEvents& ev) {
     if (!fused) {
         Launch(TileInfoKernel<BB>, dim3(gx, (gy + kInfoTiles - 1) / kInfoTiles, z), dim3(kBinThreads), stream,
                ev.prep_begin, ev.prep_end, bb);
     }
     LaunchLds(PrepareBinKernel<PB>, dim3(blocks, 1, z), dim3(kBinThreads),
-              BinLdsBytes(static_cast<int>(gx), static_cast<int>(gy)), stream, ev.bin_begin, nullptr, pb);
-#ifdef SRT_ORDER_SINGLE
-    LaunchLds(WorkOrderKernel<BB>, dim3(1, 1, z), dim3(kOrderThreads), OrderLdsBytes(static_cast<int>(gx * gy)),
-              stream, nullptr, ev.bin_end, bb);
-#else
+              BinLdsBytes(static_cast<int>(gx), static_cast<int>(gy)), stream, ev.bin_begin, order ? nullptr : ev.bin_end,
+              pb);
+    if (!order) {  // the slots' plans are current: the trace follows the bins
+        Launch(TraceCullKernel<TB>, dim3(descs, 1, z), dim3(kWave * kCullWaves), stream, ev.begin, ev.end, tb);
+        return;
+    }
     LaunchLds(WorkOrderKernel<BB>, dim3((gx * gy + kOrderBlock - 1) / kOrderBlock, 1, z), dim3(kOrderBlock),
               OrderLdsBytes(static_cast<int>(gx * gy)), stream, nullptr, ev.bin_end, bb);
-#endif
     Launch(TraceCullKernel<TB>, dim3(descs, 1, z), dim3(kWave * kCullWaves), stream, ev.begin, ev.end, tb);
 }
 
@@ -3525,6 +3451,7 @@ hipError_t LaunchCullFrames(const CullFrame* frames, std::size_t count, std::uin
     BinParams* bp = use_table ? reinterpret_cast<BinParams*>(host + lay.bin) : bb.f;
     TraceParams* tp = use_table ? reinterpret_cast<TraceParams*>(host + lay.trace) : tb.f;
     const bool fused = CullFusedInfo(band0.row_begin, band0.row_count, band0.height, band0.row_interleave);
+    bool order = false;  // some frame's slot needs its work plan (re)built: the order launch runs for all
     for (std::size_t i = 0; i < count; ++i) {
         const CullFrame& f = frames[i];
         if (f.bins == nullptr || f.edges == nullptr || f.bins->order == nullptr || f.bins->svertices == nullptr ||
@@ -3540,10 +3467,17 @@ hipError_t LaunchCullFrames(const CullFrame* frames, std::size_t count, std::uin
         }
         bp[i] = BindBins(tp[i], *f.bins, n);
         bp[i].fused = fused ? 1u : 0u;
+        tp[i].fused = bp[i].fused;
+        order = order || f.bins->plan;
         pp[i].prep = MakePrepareParams(d_vertices, d_rank, n, frame, const_cast<float*>(f.edges));
         pp[i].prep.order = f.bins->order;
         pp[i].prep.svertices = f.bins->svertices;
         pp[i].bin = bp[i];
+    }
+    static const WorkPlan plan_mode = WorkPlanFromEnv();
+    order = order || plan_mode == WorkPlan::kOrder || (plan_mode == WorkPlan::kAuto && count > 1);
+    for (std::size_t i = 0; i < count; ++i) {
+        tp[i].plan_only = order ? 0u : 1u;
     }
     const unsigned z = static_cast<unsigned>(count);
     const unsigned gx = static_cast<unsigned>(tp[0].tiles_x), gy = tp[0].tiles / gx;
@@ -3555,7 +3489,7 @@ hipError_t LaunchCullFrames(const CullFrame* frames, std::size_t count, std::uin
     const unsigned blocks = (pp[0].prep.n_pad + kBinThreads - 1) / kBinThreads + (fused ? info_blocks : 0u);
     const unsigned descs = frames[0].bins->descs;
     if (!use_table) {
-        LaunchCullStages(tb, bb, pb, z, gx, gy, blocks, fused, descs, stream, ev);
+        LaunchCullStages(tb, bb, pb, z, gx, gy, blocks, fused, order, descs, stream, ev);
         return hipGetLastError();
     }
     // One upload of every frame's parameters, then the same four launches reading them from it.
@@ -3567,7 +3501,7 @@ hipError_t LaunchCullFrames(const CullFrame* frames, std::size_t count, std::uin
     const PrepareBinTable pt{(ConstantPtr<PrepareBinParams>)(dev + lay.prep)};
     const BinTable bt{(ConstantPtr<BinParams>)(dev + lay.bin)};
     const TraceTable tt{(ConstantPtr<TraceParams>)(dev + lay.trace)};
-    LaunchCullStages(tt, bt, pt, z, gx, gy, blocks, fused, descs, stream, ev);
+    LaunchCullStages(tt, bt, pt, z, gx, gy, blocks, fused, order, descs, stream, ev);
     return hipGetLastError();
 }
 

@@ -197,6 +197,9 @@ void DeviceScene::Prepare(std::size_t width, std::size_t height, hipStream_t str
     if (width == 0 || height == 0) {
         throw std::runtime_error("Prepare: frame dimensions must be non-zero");
     }
+    if (width != m_width || height != m_height) {
+        DropPlans(m_cull_state.size());  // (a plan is scheduling only; a new shape deserves a new one)
+    }
     m_frame = MakeFrame(m_camera, width, height);
     m_width = width;
     m_height = height;
@@ -295,12 +298,28 @@ void DeviceScene::EnsureCullWork(std::size_t slots, std::size_t row_count, hipSt
     if (slots > m_cull_zeroed) {
         HipCheck(hipMemsetAsync(m_cull_work + m_cull_zeroed * bytes, 0, (slots - m_cull_zeroed) * bytes, stream),
                  "hipMemsetAsync(cull work)");
+        m_cull_state.resize(std::max(m_cull_state.size(), slots));
+        for (std::size_t k = m_cull_zeroed; k < slots; ++k) {
+            m_cull_state[k] = CullSlotState{};  // zeroed: no plan
+        }
         m_cull_zeroed = slots;
     }
 }
 
-CullBins DeviceScene::CullSlot(std::size_t slot, std::size_t row_count) const {
-    CullBins bins = CullBinLayout(m_cull_work + slot * m_cull_layout, m_n, m_width, row_count);
+void DeviceScene::DropPlans(std::size_t slots) const {
+    for (std::size_t k = 0; k < slots && k < m_cull_state.size(); ++k) {
+        m_cull_state[k].plan_descs = 0;
+    }
+}
+
+
+CullBins DeviceScene::CullSlot(std::size_t slot, std::size_t row_count, unsigned descs) const {
+    CullSlotState& st = m_cull_state.at(slot);  // (EnsureCullWork sized it)
+    CullBins bins = CullBinLayout(m_cull_work + slot * m_cull_layout, m_n, m_width, row_count, st.uses & 1u);
+    bins.descs = std::min(bins.descs, descs);
+    bins.plan = st.plan_descs != bins.descs;  // (render.hip WorkPlan: the launch may order anyway)
+    st.plan_descs = bins.descs;
+    ++st.uses;
     bins.order = m_order;
     bins.svertices = m_svertices;
     m_cull_gen = m_cull_gen + 1u == 0u ? 1u : m_cull_gen + 1u;
@@ -390,8 +409,7 @@ void DeviceScene::TraceBatch(const float* const* d_offsets, float* const* d_rgba
     // 135-row band alone splits 5 ways; eight of them do not need to).
     const unsigned batch_descs = CullDescriptors(CullTiles(m_width, row_count), frames);
     for (std::size_t f = 0; f < frames; ++f) {
-        bins[f] = CullSlot(f, row_count);
-        bins[f].descs = std::min(bins[f].descs, batch_descs);
+        bins[f] = CullSlot(f, row_count, batch_descs);
         cf[f].edges = m_edges + f * floats;
         cf[f].bins = &bins[f];
         cf[f].band = BandArgs{d_offsets[f], d_rgba != nullptr ? d_rgba[f] : nullptr, m_width, m_height, row_begin,
@@ -401,9 +419,13 @@ void DeviceScene::TraceBatch(const float* const* d_offsets, float* const* d_rgba
     ParamTable* table = frames > static_cast<std::size_t>(kMaxBatch) ? &AcquireTable(frames, stream) : nullptr;
     const CullTable ct{table != nullptr ? table->device : nullptr, table != nullptr ? table->host : nullptr,
                        table != nullptr ? table->frames : 0};
-    HipCheck(LaunchCullFrames(cf.data(), frames, m_n, m_vertices, m_shade, m_frame, m_background, m_rank, stream,
-                              m_timing ? &ev : nullptr, table != nullptr ? &ct : nullptr),
-             "batched trace launch");
+    const hipError_t launched = LaunchCullFrames(cf.data(), frames, m_n, m_vertices, m_shade, m_frame, m_background,
+                                                 m_rank, stream, m_timing ? &ev : nullptr,
+                                                 table != nullptr ? &ct : nullptr);
+    if (launched != hipSuccess) {
+        DropPlans(frames);
+    }
+    HipCheck(launched, "batched trace launch");
     if (table != nullptr) {
         HipCheck(hipEventRecord(table->uploaded, stream), "hipEventRecord(parameter table)");
         table->pending = true;
@@ -443,9 +465,13 @@ void DeviceScene::Trace(const float* d_offsets, float* d_rgba, std::size_t row_b
     const bool fused_info = use_bins != nullptr && CullFusedInfo(row_begin, row_count, m_height, row_interleave);
     const StageEvents ev = BindStageEvents(prepare || (use_bins != nullptr && row_count != 0 && !fused_info),
                                            use_bins != nullptr || (variant == kTraceBvh && m_n != 0));
-    HipCheck(LaunchTrace(m_edges, m_n, m_vertices, m_shade, m_frame, m_background, band, variant, use_bins, stream,
-                         m_timing ? &ev : nullptr, prepare ? m_rank : nullptr, m_bvh),
-             "trace kernel launch");
+    const hipError_t launched = LaunchTrace(m_edges, m_n, m_vertices, m_shade, m_frame, m_background, band, variant,
+                                            use_bins, stream, m_timing ? &ev : nullptr, prepare ? m_rank : nullptr,
+                                            m_bvh);
+    if (launched != hipSuccess && use_bins != nullptr) {
+        DropPlans(1);
+    }
+    HipCheck(launched, "trace kernel launch");
     if (prepare) {
         m_prepare_pending = false;
     }

@@ -138,10 +138,20 @@ private:
     mutable std::size_t m_cull_layout = 0;   // its bytes (they change with the split width too)
     mutable unsigned m_cull_gen = 0;         // frames binned (render.h CullBins::gen)
     mutable std::size_t m_cull_zeroed = 0;   // frame slots of the current carve-up zero-filled
+    // Per frame slot: frames binned in it (their parity picks the count buffer) and the trace grid
+    // its work plan was built for (0: none; render.h CullBins::plan).
+    struct CullSlotState {
+        unsigned uses = 0;
+        unsigned plan_descs = 0;
+    };
+    mutable std::vector<CullSlotState> m_cull_state;
     // The cull work of frame slots [0, slots) for a row_count-row band (grown, zeroed on first use
-    // of a slot with this carve-up), and slot `slot`'s carve-up with a fresh frame number.
+    // of a slot with this carve-up), and slot `slot`'s carve-up with a fresh frame number for a trace
+    // grid of at most `descs` descriptors; it (re)builds the slot's work plan when the slot has none
+    // for that grid.
     void EnsureCullWork(std::size_t slots, std::size_t row_count, hipStream_t stream) const;
-    CullBins CullSlot(std::size_t slot, std::size_t row_count) const;
+    CullBins CullSlot(std::size_t slot, std::size_t row_count, unsigned descs = ~0u) const;
+    void DropPlans(std::size_t slots) const;  // after a failed launch: slots [0, slots) rebuild theirs
     void EnsureEdgeSlots(std::size_t slots, hipStream_t stream) const;
     // BVH variant: node boxes + depth bounds (render.h BvhLayout), allocated by the first bvh Trace.
     mutable unsigned char* m_bvh = nullptr;

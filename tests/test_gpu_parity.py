@@ -623,6 +623,48 @@ def test_split_items_across_frames(gpu, scenes, monkeypatch, chunk, chunks):
     assert_parity(refs[0], ref, rows=rows)
 
 
+@pytest.mark.parametrize("chunk,plan", [("", ""), ("64", ""), ("", "reuse"), ("64", "reuse"), ("64", "order")])
+def test_work_plan_is_scheduling_only(gpu, scenes, monkeypatch, chunk, plan):
+    """The trace's work plan (tile parts, chunking, split slots, heaviest first) is built once per
+    frame slot and trace grid and reused (SRT_WORK_PLAN: auto = by single-frame launches, reuse =
+    by every launch, order = none): it decides only which block takes which part, so every frame
+    -- whatever frame the plan was made from (the first one here streams every record: offsets
+    outside [0, 1]), batched or not, uniform, jittered or NaN offsets -- equals the brute-force
+    frame bit for bit."""
+    import torch
+
+    import simpleraytracer_amd as srt
+
+    monkeypatch.setenv("SRT_CULL_CHUNK", chunk)
+    monkeypatch.setenv("SRT_WORK_PLAN", plan)
+    w, h = 640, 360
+    rng = np.random.default_rng(81)
+    nan = rng.random((h, w, 2), dtype=np.float32)
+    nan[100:140, 200:260] = np.nan
+    offs = [np.full((h, w, 2), -3.25, np.float32), np.full((h, w, 2), 0.5, np.float32),
+            rng.random((h, w, 2), dtype=np.float32), nan, rng.random((h, w, 2), dtype=np.float32)]
+    refs = [torch_render(scenes["soup100k"], w, h, o, variant="lds") for o in offs]
+    scene = srt.DeviceScene(scenes["soup100k"], 0)
+    stream = torch.cuda.current_stream()
+    scene.prepare(w, h, stream)
+    ins = [torch.from_numpy(o).cuda() for o in offs]
+    for rep in range(2):
+        outs = [torch.full((h, w, 4), float("nan"), dtype=torch.float32, device="cuda") for _ in offs]
+        for o, out in zip(ins, outs):
+            scene.trace(o, out, 0, h, stream=stream)
+        batch = [torch.full((h, w, 4), float("nan"), dtype=torch.float32, device="cuda") for _ in range(3)]
+        scene.trace_batch(ins[2:5], batch, 0, h, stream=stream)  # another trace grid: slots 0-2 re-plan
+        again = torch.full((h, w, 4), float("nan"), dtype=torch.float32, device="cuda")
+        scene.trace(ins[1], again, 0, h, stream=stream)
+        torch.cuda.synchronize()
+        for k, (out, ref) in enumerate(zip(outs, refs)):
+            assert np.array_equal(out.cpu().numpy().view(np.uint32), ref.view(np.uint32)), (rep, k)
+        for k, out in enumerate(batch):
+            assert np.array_equal(out.cpu().numpy().view(np.uint32), refs[2 + k].view(np.uint32)), (rep, "batch", k)
+        assert np.array_equal(again.cpu().numpy().view(np.uint32), refs[1].view(np.uint32)), rep
+    scene.close()
+
+
 @pytest.mark.parametrize("variant", VARIANTS)
 def test_deferred_shading_bitwise(gpu, scenes, variant):
     """srtTraceIdsAsync + srtShadeAsync (the multi-GPU band path: hit ids gathered, shaded by the
