@@ -633,14 +633,20 @@ __global__ __launch_bounds__(kShadeThreads) void ShadeIdsKernel(TraceParams p, c
     IdT id[kShadeRows];
     float2 o[kShadeRows];
     bool mine[kShadeRows];  // rows of band skip_band: the compositor traced them as RGBA already
+    // Interleaved bands: the thread's rows lie in one tile row (kShadeRows divides it), so in one
+    // band (the divisions once per thread, not per row).
+    static_assert(kCullTileRows % kShadeRows == 0, "a thread's rows share a tile row");
+    const unsigned t0 = static_cast<unsigned>(y0) / kCullTileRows;
+    const unsigned band0 = interleaved != 0u ? t0 % interleaved : 0u;
+    const unsigned local0 =
+        interleaved != 0u ? t0 / interleaved * kCullTileRows + static_cast<unsigned>(y0) % kCullTileRows : 0u;
 #pragma unroll
     for (int r = 0; r < kShadeRows; ++r) {
         const int y = min(y0 + r, p.row_count - 1);
         unsigned band, local;
         if (interleaved != 0u) {
-            const unsigned t = static_cast<unsigned>(y) / kCullTileRows;
-            band = t % interleaved;
-            local = t / interleaved * kCullTileRows + static_cast<unsigned>(y) % kCullTileRows;
+            band = band0;
+            local = local0 + static_cast<unsigned>(y - y0);
         } else {
             band = static_cast<unsigned>(y) / band_rows;
             local = static_cast<unsigned>(y) - band * band_rows;
@@ -2282,6 +2288,10 @@ std::size_t OrderLdsBytes(int tiles) { return static_cast<std::size_t>(tiles) * 
 #ifndef SRT_TRACE_OCC
 #define SRT_TRACE_OCC 6
 #endif
+#ifndef SRT_SPLIT_ATOMIC
+#define SRT_SPLIT_ATOMIC 0  // 1: split parts merged with 64-bit atomic maxima in one slice per part (measured:
+                            // one frame in flight, trace 20.4 -> 22.5 us; 8-frame launches unchanged)
+#endif
 #ifndef SRT_SPLIT_ARRIVE_FIRST
 #define SRT_SPLIT_ARRIVE_FIRST 0  // split parts: 1 = arrive, then publish unless last (measured: trace 19.7 -> 21.6 us)
 #endif
@@ -2648,7 +2658,7 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(c
         constexpr int kPix = kBlockRows * kWave;
         unsigned long long* slices = p.split_keys + static_cast<size_t>(slot) * kPix;
         const int pix = wave * R * kWave + lane;
-        auto publish = [&] {  // this chunk's keys, write-through (sc1) stores, complete before the barrier
+        [[maybe_unused]] auto publish = [&] {  // this chunk's keys, write-through (sc1) stores, complete before the barrier
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 __hip_atomic_store(slices + static_cast<size_t>(chunk) * kPix + pix + r * kWave, key[r],
@@ -2692,6 +2702,44 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(c
             __hip_atomic_store(&p.arrive[slot], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // the next frame's
         }
         __syncthreads();
+#elif SRT_SPLIT_ATOMIC
+        // Split part, merged in the L2: every chunk folds the keys it found (hit pixels only) into
+        // the part's first slice with 64-bit atomic maxima of ~key (zero = no hit yet, the state
+        // every slice is in between frames), then counts its arrival; the last of the part's chunks
+        // reads the merged keys once, takes its own into account and zeroes the slice for the
+        // next frame. (Hand-off as below: the atomics complete (vmcnt(0)) before the barrier and the
+        // agent-scope add.)
+        {
+            unsigned long long* merged = slices;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                if (key[r] != ~0ull) {
+                    __hip_atomic_fetch_max(merged + pix + r * kWave, ~key[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (tid == 0) {
+                const unsigned before = __hip_atomic_fetch_add(&p.arrive[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const unsigned last = before == nchunks - 1u ? 1u : 0u;
+                if (last != 0u) {
+                    __hip_atomic_store(&p.arrive[slot], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                sh.last = last;
+            }
+            __syncthreads();
+            if (sh.last == 0u) {
+                SRT_DIAG_END(item, chunk, nchunks, 0u, src.full);
+                return;
+            }
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const unsigned long long m =
+                    ~__hip_atomic_load(merged + pix + r * kWave, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                key[r] = m < key[r] ? m : key[r];
+                __hip_atomic_store(merged + pix + r * kWave, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
 #else
         // Split part: publish this chunk's keys, count the arrival; the last of the part's chunks
         // takes the minimum over every chunk's keys (sc1 loads) and shades. Hand-off form:
@@ -2712,6 +2760,7 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(c
             return;
         }
 #endif
+#if !SRT_SPLIT_ATOMIC || SRT_SPLIT_ARRIVE_FIRST
         for (unsigned c = 0; c < nchunks; ++c) {
             if (c == chunk) {
                 continue;
@@ -2723,6 +2772,7 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(c
                 key[r] = o < key[r] ? o : key[r];
             }
         }
+#endif
     }
     if (p.out_packed != nullptr) {  // packed ids: every lane of the wave takes part (ballots)
 #pragma unroll
@@ -3574,6 +3624,8 @@ bool CullFusedInfo(std::size_t row_begin, std::size_t row_count, std::size_t hei
         const char* v = std::getenv("SRT_FUSED_INFO");
         return v == nullptr || std::strcmp(v, "0") != 0;
     }();
+    // (Bands too -- their bin launch then writing every cull record, as the tile info it would
+    // test them against is not known yet -- measured slower at every P: P = 8 rank 5.35 -> 6.0 us.)
     return enabled && row_begin == 0 && row_count == height && interleave == 1;
 }
 
