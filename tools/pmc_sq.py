@@ -27,8 +27,9 @@ def main():
     ap.add_argument("--kernel", default="TraceCullKernel")
     ap.add_argument("--out", type=Path, default=REPO / "profiles" / "pmc_sq.json")
     ap.add_argument("--source", default="")
+    ap.add_argument("--largest-grid", action="store_true", help="only the dispatches of the largest grid")
     a = ap.parse_args()
-    per = {}
+    per, grid = {}, {}
     for f in sorted(a.dir.rglob("*counter_collection.csv")):
         with open(f, newline="") as fh:
             for r in csv.DictReader(fh):
@@ -36,6 +37,10 @@ def main():
                     continue
                 key = (r["Counter_Name"], r.get("Dispatch_Id"), r.get("Agent_Id"))
                 per[key] = per.get(key, 0.0) + float(r["Counter_Value"])
+                grid[key] = int(r.get("Grid_Size") or 0)
+    if per and a.largest_grid:
+        g = max(grid.values())
+        per = {k: v for k, v in per.items() if grid[k] == g}
     if not per:
         raise SystemExit(f"no {a.kernel} counters under {a.dir}")
     sums, counts = {}, {}
