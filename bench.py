@@ -73,8 +73,10 @@ def parse():
     p.add_argument("--triangles", type=int, default=100_000)
     p.add_argument("--variant", default=os.environ.get("SRT_BENCH_VARIANT", "cull"), choices=list(KERNEL_NAMES))
     p.add_argument("--mode", default="bands", choices=["bands", "frames"], help="multi-GPU split (module doc)")
-    p.add_argument("--exchange", default="alltoall", choices=["alltoall", "rotating", "root"],
-                   help="bands: where frames are composited (module doc)")
+    p.add_argument("--exchange", default="auto", choices=["auto", "alltoall", "rotating", "root", "share"],
+                   help="bands: where frames are composited (module doc; auto: share at 2 GPUs, else alltoall)")
+    p.add_argument("--share", type=int, default=0,
+                   help="share exchange: the compositor's tile rows per cycle of share + N - 1 (0: the library's 3)")
     p.add_argument("--rows", default="interleaved", choices=["interleaved", "contiguous"],
                    help="bands: each GPU's rows, the frame's 16-row tile rows dealt round-robin or one block")
     p.add_argument("--queues", type=int, default=int(os.environ.get("SRT_BENCH_QUEUES", "2")),
@@ -89,7 +91,12 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive ml* API measurement")
     p.add_argument("--no-extras", action="store_true", help="only the main line (no secondary legs)")
-    return p.parse_args()
+    a = p.parse_args()
+    if a.exchange == "auto":
+        # Two GPUs share one link per direction: the compositor traces 3 of every 4 tile rows itself,
+        # so a quarter of the frame's ids cross it (alltoall would send half, link-bound at ~64 GB/s).
+        a.exchange = "share" if a.gpus == 2 else "alltoall"
+    return a
 
 
 def workload_name(a, scene=None, triangles=None, width=None, height=None):
@@ -168,7 +175,8 @@ class Job:
         from simpleraytracer_amd.engine import FrameEngine, unique_id
 
         kw = dict(variant=variant or a.variant, queues=queues or a.queues, batch=batch or a.frames_per_step,
-                  rows=rows or a.rows, exchange=exchange or a.exchange, split=mode or a.mode, launch=a.launch)
+                  rows=rows or a.rows, exchange=exchange or a.exchange, split=mode or a.mode, launch=a.launch,
+                  share=a.share)
         w, h = width or a.width, height or a.height
         if not self.ranked:
             return FrameEngine(path, w, h, devices=self.devices, **kw)
@@ -507,8 +515,10 @@ def main():
     if world > 1 and extras:
         for name, kw in (("frames", {"mode": "frames"}),
                          ("rotating_gather", {"exchange": "rotating"}),
-                         ("contiguous_rows", {"rows": "contiguous"})):
+                         ("alltoall_exchange", {"exchange": "alltoall"}),
+                         ("contiguous_rows", {"rows": "contiguous", "exchange": "alltoall"})):
             if (name == "frames" and a.mode == "frames") or (name == "rotating_gather" and a.exchange != "alltoall") \
+                    or (name == "alltoall_exchange" and a.exchange == "alltoall") \
                     or (name == "contiguous_rows" and a.rows == "contiguous"):
                 continue
             try:
@@ -593,6 +603,7 @@ def main():
                 xb = info["exchange_bytes_per_frame"]
                 px = max(1, (world - 1) * info["buffer_rows"] * W)
                 line["exchange"] = {"pattern": a.exchange, "transport": "RCCL" if info["rccl"] else "device copies",
+                                    "share": (a.share or 3) if a.exchange == "share" else None,
                                     "payload": "packed hit ids (16 + k bits per pixel: a u16 plane and k bit planes, "
                                                "render.h PackedIds) or int32 ids; deferred shading on the compositor, "
                                                "whose own band is traced to RGBA in place",

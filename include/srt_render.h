@@ -143,7 +143,11 @@ ML_API_ENTRY int srtTakeStageTimes(srt_device_scene scene, unsigned* launches, d
  * the bands move over RCCL to the frame's compositor, which shades the frame from the ids (one
  * launch per batch, bit-identical to the fused trace). Exchanges: SRT_EXCHANGE_ALLTOALL (frame f of
  * a batch composited on device f % P; the batch's P gathers fused into one ncclSend / ncclRecv
- * group), SRT_EXCHANGE_ROTATING (the batch gathered to device b % P), SRT_EXCHANGE_ROOT (device 0).
+ * group), SRT_EXCHANGE_ROTATING (the batch gathered to device b % P), SRT_EXCHANGE_ROOT (device 0),
+ * SRT_EXCHANGE_SHARE (batch b composited on device c = b % P, which traces `share` of every
+ * share + P - 1 tile rows itself, straight into its frames; each other device traces one tile row
+ * per such cycle and sends its ids: the exchange and the shading shrink to (P - 1) / (share + P - 1)
+ * of a frame; interleaved rows only).
  * P == 1: trace + shade fused (RGBA). SRT_SPLIT_FRAMES: every device renders whole frames of its
  * own (no exchange). Devices: all in this process (srtEngineCreate; one worker thread per device,
  * ncclCommInitAll; a repeated device exchanges by device copies -- the one-GPU rehearsal), or one
@@ -154,6 +158,7 @@ typedef struct srt_engine_t* srt_engine;
 #define SRT_EXCHANGE_ALLTOALL 0
 #define SRT_EXCHANGE_ROTATING 1
 #define SRT_EXCHANGE_ROOT 2
+#define SRT_EXCHANGE_SHARE 3
 #define SRT_SPLIT_BANDS 0
 #define SRT_SPLIT_FRAMES 1
 /* srt_engine_options.flags */
@@ -170,6 +175,7 @@ typedef struct srt_engine_options {
     size_t launch;  /* frames per trace launch, <= 256 (0 = env SRT_LAUNCH_FRAMES, else 8 for whole
                        frames, 64 for bands over more than one device) */
     int flags;      /* SRT_ENGINE_* bits (0 = none) */
+    size_t share;   /* SRT_EXCHANGE_SHARE: the compositor's tile rows per cycle (0 = 3) */
 } srt_engine_options;
 
 /* 128-byte RCCL unique id for srtEngineCreateRank (call on one rank, share with the others). */

@@ -34,6 +34,7 @@ SRT_ROWS_CONTIGUOUS = 1
 SRT_EXCHANGE_ALLTOALL = 0
 SRT_EXCHANGE_ROTATING = 1
 SRT_EXCHANGE_ROOT = 2
+SRT_EXCHANGE_SHARE = 3
 SRT_SPLIT_BANDS = 0
 SRT_SPLIT_FRAMES = 1
 SRT_ENGINE_RCCL_SELF = 1  # srt_engine_options.flags
@@ -77,6 +78,7 @@ class EngineOptions(ctypes.Structure):
         ("simulate", ctypes.c_int),
         ("launch", ctypes.c_size_t),
         ("flags", ctypes.c_int),
+        ("share", ctypes.c_size_t),
     ]
 
 

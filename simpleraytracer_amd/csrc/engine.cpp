@@ -88,6 +88,7 @@ std::size_t BandSplit::FrameRow(std::size_t band, std::size_t local) const {
 std::size_t ExchangePlan::Compositor(std::size_t batch_index, std::size_t f) const {
     switch (exchange) {
         case EngineOptions::kRotatingGather:
+        case EngineOptions::kShare:
             return batch_index % bands;
         case EngineOptions::kRootGather:
             return 0;
@@ -103,6 +104,7 @@ std::size_t ExchangePlan::Slot(std::size_t f) const {
 std::size_t ExchangePlan::FramesFor(std::size_t batch_index, std::size_t compositor) const {
     switch (exchange) {
         case EngineOptions::kRotatingGather:
+        case EngineOptions::kShare:
             return compositor == batch_index % bands ? batch : 0;
         case EngineOptions::kRootGather:
             return compositor == 0 ? batch : 0;
@@ -113,6 +115,10 @@ std::size_t ExchangePlan::FramesFor(std::size_t batch_index, std::size_t composi
 
 std::size_t ExchangePlan::MaxFramesPerCompositor() const {
     return exchange == EngineOptions::kAllToAll ? (batch + bands - 1) / bands : batch;
+}
+
+std::size_t ExchangePlan::RecvSlot(std::size_t c, std::size_t p) const {
+    return exchange == EngineOptions::kShare ? (p + bands - c - 1) % bands : p;
 }
 
 namespace {
@@ -129,6 +135,9 @@ std::size_t SendPixels(const ExchangePlan& plan, std::size_t c, std::size_t j, s
 
 std::vector<std::vector<int>> ExchangeOnHost(const BandSplit& split, const ExchangePlan& plan, std::size_t width,
                                              std::size_t batch_index, const std::vector<std::vector<int>>& band_ids) {
+    if (plan.exchange == EngineOptions::kShare) {
+        throw std::runtime_error("ExchangeOnHost: the share exchange has per-batch band shapes (no host self-test)");
+    }
     const std::size_t P = split.bands, B = split.BufferRows(), F = plan.batch;
     const std::size_t band_pixels = B * width;
     if (band_ids.size() != P) {
@@ -340,8 +349,9 @@ struct FrameEngine::Device {
     hipEvent_t comm_drained = nullptr;
     std::vector<Queue> queues;
     float* full = nullptr;  // inputs x H x W x 2
-    float* band_in = nullptr;  // inputs x band rows x W x 2
-    std::size_t row_begin = 0, rows = 0;
+    float* band_in = nullptr;  // per role (FrameEngine::Role): inputs x the role's rows x W x 2
+    std::size_t row_begin = 0, rows = 0;  // the band MeasureStages traces (kShare: the sender role)
+    std::vector<Role> roles;
 };
 
 FrameEngine::FrameEngine(const Scene& scene, const std::vector<int>& devices, std::size_t width,
@@ -450,7 +460,7 @@ void FrameEngine::Init(const Scene& scene, const std::vector<int>& devices) {
     if (m_opt.variant < kTraceLds || m_opt.variant > kTraceBvh) {
         throw std::runtime_error("FrameEngine: unknown trace variant " + std::to_string(m_opt.variant));
     }
-    if (m_opt.exchange < EngineOptions::kAllToAll || m_opt.exchange > EngineOptions::kRootGather ||
+    if (m_opt.exchange < EngineOptions::kAllToAll || m_opt.exchange > EngineOptions::kShare ||
         (m_opt.split != EngineOptions::kBands && m_opt.split != EngineOptions::kFrames)) {
         throw std::runtime_error("FrameEngine: unknown exchange or split");
     }
@@ -471,8 +481,21 @@ void FrameEngine::Init(const Scene& scene, const std::vector<int>& devices) {
     }
     m_inject = Injection::FromEnv();
     m_ctl = std::make_unique<CommCtl>();
-    m_split = BandSplit::Make(m_height, m_bands ? m_world : 1, m_opt.interleaved);
-    m_plan.bands = m_split.bands;
+    if (m_opt.exchange == EngineOptions::kShare && m_exchange && m_world > 1) {
+        if (!m_opt.interleaved) {
+            throw std::runtime_error("FrameEngine: the share exchange needs interleaved rows");
+        }
+        m_share = m_opt.share == 0 ? 3 : m_opt.share;
+        if (m_share > 64) {
+            throw std::runtime_error("FrameEngine: share must be 1..64 tile rows per cycle");
+        }
+    } else if (m_opt.exchange == EngineOptions::kShare) {
+        m_opt.exchange = EngineOptions::kRotatingGather;  // one device: nothing to share
+    }
+    // kShare: the frame's tile rows in cycles of k + P - 1 "classes" (the compositor's k, then one
+    // per sender); the ids buffers hold one class.
+    m_split = BandSplit::Make(m_height, m_bands ? (m_share != 0 ? m_share + m_world - 1 : m_world) : 1, m_opt.interleaved);
+    m_plan.bands = m_bands ? m_world : 1;
     m_plan.batch = m_opt.batch;
     m_plan.exchange = m_opt.exchange;
     m_scene = std::make_unique<Scene>(scene);
@@ -488,10 +511,44 @@ void FrameEngine::Init(const Scene& scene, const std::vector<int>& devices) {
         auto d = std::make_unique<Device>();
         d->device = devices[i];
         d->band = m_rank0 + i;
-        d->row_begin = m_split.RowBegin(m_bands ? d->band : 0);
-        d->rows = m_split.RowCount(m_bands ? d->band : 0);
+        if (m_share != 0) {
+            const std::size_t classes = m_split.bands;
+            Role own;
+            own.pattern = RowPattern(classes, m_share);
+            own.rows = PatternBandRows(m_height, 0, own.pattern);
+            d->roles.push_back(own);
+            for (std::size_t j = m_share; j < classes; ++j) {  // sender roles, in class order
+                Role r;
+                r.row_begin = m_split.RowBegin(j);
+                r.rows = m_split.RowCount(j);
+                r.pattern = classes;
+                d->roles.push_back(r);
+            }
+        } else {
+            Role r;
+            r.row_begin = m_split.RowBegin(m_bands ? d->band : 0);
+            r.rows = m_split.RowCount(m_bands ? d->band : 0);
+            r.pattern = m_split.Interleave();
+            d->roles.push_back(r);
+        }
+        const Role& measured = d->roles[m_share != 0 ? 1 : 0];
+        d->row_begin = measured.row_begin;
+        d->rows = measured.rows;
+        std::size_t at = 0;
+        for (Role& r : d->roles) {
+            r.input = at;
+            at += r.rows;
+        }
         m_dev.push_back(std::move(d));
     }
+}
+
+std::size_t FrameEngine::RoleOf(std::size_t local, std::size_t b) const {
+    if (m_share == 0) {
+        return 0;
+    }
+    const std::size_t c = m_plan.Compositor(b, 0), self = m_dev[local]->band;
+    return self == c ? 0 : 1 + m_plan.RecvSlot(c, self);
 }
 
 void FrameEngine::AllocateQueues() {
@@ -676,14 +733,20 @@ void FrameEngine::SetInputs(const float* host_offsets, std::size_t count) {
         d.full = DeviceAlloc<float>(count * ff, "hipMalloc(inputs)");
         HipCheck(hipMemcpy(d.full, host_offsets, count * ff * sizeof(float), hipMemcpyHostToDevice),
                  "hipMemcpy(inputs)");
-        if (m_exchange) {  // the band's rows of every input, band-local and contiguous
+        if (m_exchange) {  // each role's rows of every input, band-local and contiguous
             const std::size_t row_floats = m_width * 2;
-            std::vector<float> band(count * d.rows * row_floats);
-            for (std::size_t r = 0; r < count; ++r) {
-                for (std::size_t y = 0; y < d.rows; ++y) {
-                    const std::size_t fy = m_split.FrameRow(d.band, y);
-                    std::memcpy(band.data() + (r * d.rows + y) * row_floats, host_offsets + r * ff + fy * row_floats,
-                                row_floats * sizeof(float));
+            std::size_t all_rows = 0;
+            for (const Role& role : d.roles) {
+                all_rows += role.rows;
+            }
+            std::vector<float> band(count * all_rows * row_floats);
+            for (const Role& role : d.roles) {
+                for (std::size_t r = 0; r < count; ++r) {
+                    for (std::size_t y = 0; y < role.rows; ++y) {
+                        const std::size_t fy = BandFrameRow(role.row_begin, role.pattern, y);
+                        std::memcpy(band.data() + ((role.input * count) + r * role.rows + y) * row_floats,
+                                    host_offsets + r * ff + fy * row_floats, row_floats * sizeof(float));
+                    }
                 }
             }
             d.band_in = DeviceAlloc<float>(band.size(), "hipMalloc(band inputs)");
@@ -698,9 +761,10 @@ const float* FrameEngine::FullInput(std::size_t local, std::size_t k) const {
     return m_dev[local]->full + (k % m_inputs) * FrameFloats();
 }
 
-const float* FrameEngine::BandInput(std::size_t local, std::size_t k) const {
+const float* FrameEngine::BandInput(std::size_t local, std::size_t k, std::size_t role) const {
     const Device& d = *m_dev[local];
-    return d.band_in + (k % m_inputs) * d.rows * m_width * 2;
+    const Role& r = d.roles[role];
+    return d.band_in + (r.input * m_inputs + (k % m_inputs) * r.rows) * m_width * 2;
 }
 
 void FrameEngine::TracePhase(std::size_t local, std::size_t b) {
@@ -748,14 +812,15 @@ void FrameEngine::TracePhase(std::size_t local, std::size_t b) {
         }
         return;
     }
-    const std::size_t self = d.band;
-    if (d.rows != 0) {
+    const std::size_t self = d.band, ri = RoleOf(local, b);
+    const Role& role = d.roles[ri];
+    if (role.rows != 0) {
         for (std::size_t f0 = 0; f0 < F; f0 += L) {
             const std::size_t n = std::min(L, F - f0);
             for (std::size_t j = 0; j < n; ++j) {
                 const std::size_t f = f0 + j;
                 const std::size_t c = m_plan.Compositor(b, f), slot = m_plan.Slot(f);
-                offs[j] = BandInput(local, k0 + f);
+                offs[j] = BandInput(local, k0 + f, ri);
                 // The compositor's own band is traced and shaded in one kernel straight into its frame
                 // (RGBA at the band's frame rows; the deferred shading then skips that band), unless
                 // the self-exchange option sends it through RCCL like every other band.
@@ -763,8 +828,8 @@ void FrameEngine::TracePhase(std::size_t local, std::size_t b) {
                 ids[j] = own ? nullptr : Ids(q.send, SendFrames(m_plan, c, slot));
                 rgba[j] = own ? q.rgba + slot * frame_floats4 : nullptr;
             }
-            q.scene->TraceBatch(offs.data(), rgba.data(), ids.data(), n, d.row_begin, d.rows, m_opt.variant, q.stream,
-                                m_split.Interleave(), m_id_planes, true);
+            q.scene->TraceBatch(offs.data(), rgba.data(), ids.data(), n, role.row_begin, role.rows, m_opt.variant,
+                                q.stream, role.pattern, m_id_planes, true);
         }
     }
     HipCheck(hipEventRecord(q.traced, q.stream), "hipEventRecord(traced)");
@@ -799,7 +864,8 @@ void FrameEngine::ExchangePhase(std::size_t local, std::size_t b) {
                               static_cast<int>(p), comm, d.comm));
             }
             if (n_self != 0) {
-                note(ncclRecv(q.recv + p * n_self * m_band_id_bytes, n_self * m_band_id_bytes, ncclUint8,
+                note(ncclRecv(q.recv + m_plan.RecvSlot(self, p) * n_self * m_band_id_bytes, n_self * m_band_id_bytes,
+                              ncclUint8,
                               static_cast<int>(p),
                               comm, d.comm));
             }
@@ -827,7 +893,7 @@ void FrameEngine::CopyPhase(std::size_t local, std::size_t b) {
             Device& peer = *m_dev[p];
             Queue& pq = peer.queues[qi];
             HipCheck(hipStreamWaitEvent(d.comm, pq.traced, 0), "hipStreamWaitEvent(peer traced)");
-            HipCheck(hipMemcpyPeerAsync(q.recv + peer.band * n_self * m_band_id_bytes, d.device,
+            HipCheck(hipMemcpyPeerAsync(q.recv + m_plan.RecvSlot(self, peer.band) * n_self * m_band_id_bytes, d.device,
                                         pq.send + SendFrames(m_plan, self, 0) * m_band_id_bytes, peer.device,
                                         n_self * m_band_id_bytes, d.comm),
                      "hipMemcpyPeerAsync(band ids)");
@@ -851,9 +917,11 @@ void FrameEngine::ShadePhase(std::size_t local, std::size_t b) {
     const bool a2a = m_plan.exchange == EngineOptions::kAllToAll;
     const std::size_t first = k0 + (a2a ? self : 0);
     const std::size_t stride = m_inputs == 1 ? 0 : (a2a ? m_world : 1) * FrameFloats();
+    // The compositor's own rows are RGBA already: its band (all-to-all, rotating), or the first
+    // m_share classes (share; the received ids start at class m_share).
+    const long skip = m_opt.rccl_self || m_share != 0 ? -1 : static_cast<long>(self);
     q.scene->Shade(FullInput(local, first), reinterpret_cast<const int*>(q.recv), q.rgba, 0, m_height, q.stream, n_self,
-                   m_split.BufferRows(), m_split.interleaved ? m_world : 0, stride, m_id_planes,
-                   m_opt.rccl_self ? -1 : static_cast<long>(self));  // the own band is RGBA already
+                   m_split.BufferRows(), m_split.interleaved ? m_split.bands : 0, stride, m_id_planes, skip, m_share);
 }
 
 void FrameEngine::Inject(std::size_t local, std::size_t b) {
@@ -1091,9 +1159,14 @@ DeviceScene::StageTimes FrameEngine::MeasureStages(std::size_t local, std::size_
                 ids[j] = Ids(q.send, j);
             }
             if (m_exchange) {
-                if (d.rows != 0) {
-                    q.scene->TraceBatch(offs.data(), nullptr, ids.data(), frames, d.row_begin, d.rows, m_opt.variant,
-                                        q.stream, m_split.Interleave(), m_id_planes);
+                const std::size_t ri = m_share != 0 ? 1 : 0;  // the sender role: its ids fit the send buffer
+                const Role& role = d.roles[ri];
+                for (std::size_t j = 0; j < frames; ++j) {
+                    offs[j] = BandInput(local, i * frames + j, ri);
+                }
+                if (role.rows != 0) {
+                    q.scene->TraceBatch(offs.data(), nullptr, ids.data(), frames, role.row_begin, role.rows, m_opt.variant,
+                                        q.stream, role.pattern, m_id_planes);
                 }
             } else {
                 q.scene->TraceBatch(offs.data(), rgba.data(), nullptr, frames, 0, m_height, m_opt.variant, q.stream, 1);

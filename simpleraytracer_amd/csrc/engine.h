@@ -14,7 +14,13 @@
 //                   (one per compositor) are fused into one group of ncclSend / ncclRecv, so every
 //                   directed xGMI link carries 1/P of the payload;
 //   kRotatingGather the whole batch is gathered to device b % P (one gather per batch);
-//   kRootGather     everything to device 0.
+//   kRootGather     everything to device 0;
+//   kShare          batch b is composited on device c = b % P, which traces `share` (k) of every
+//                   k + P - 1 tile rows of the batch's frames itself -- straight into its frames as
+//                   RGBA -- while every other device traces one tile row of each such cycle and
+//                   sends its ids: the exchange and the deferred shading shrink to (P - 1) / (k + P - 1)
+//                   of a frame (P = 2, k = 3: a quarter). With Q a multiple of P every queue keeps
+//                   one role (compositor, or one sender class) and so one band shape.
 // P == 1 traces and shades in one kernel (RGBA), no exchange.
 // Split "frames": every device renders whole frames of its own (no exchange; weak scaling).
 //
@@ -45,7 +51,7 @@ namespace srt {
 
 struct EngineOptions {
     enum Split { kBands = 0, kFrames = 1 };
-    enum Exchange { kAllToAll = 0, kRotatingGather = 1, kRootGather = 2 };
+    enum Exchange { kAllToAll = 0, kRotatingGather = 1, kRootGather = 2, kShare = 3 };
     int variant = 2;           // render.h TraceVariant (kTraceCull)
     std::size_t queues = 2;    // batches in flight per device
     std::size_t batch = 16;    // frames per batch
@@ -67,6 +73,8 @@ struct EngineOptions {
     // one-rank RCCL communicator (ncclSend / ncclRecv to self) -- the real exchange, its waits and
     // its abort path on a one-GPU box. Frames are bit-identical to the fused trace.
     bool rccl_self = false;
+    // kShare: the compositor's tile rows per cycle (k above; 0: 3).
+    std::size_t share = 0;
 };
 
 // Row bands of an H-row frame over P devices (interleaved or contiguous), the layout every
@@ -84,12 +92,14 @@ struct BandSplit {
 
 // Which device composites frame f of batch b, and that frame's slot among the device's frames.
 struct ExchangePlan {
-    std::size_t bands = 1, batch = 1;
+    std::size_t bands = 1, batch = 1;  // bands: the devices (P)
     int exchange = EngineOptions::kAllToAll;
     std::size_t Compositor(std::size_t batch_index, std::size_t f) const;
     std::size_t Slot(std::size_t f) const;                                      // index among its compositor's frames
     std::size_t FramesFor(std::size_t batch_index, std::size_t compositor) const;  // frames composited there
     std::size_t MaxFramesPerCompositor() const;
+    // Slot of device p's ids in compositor c's receive buffer (kShare: the senders in class order).
+    std::size_t RecvSlot(std::size_t c, std::size_t p) const;
 };
 
 // Host self-test of the exchange (no device): band_ids[d] = device d's traced ids of the batch's F
@@ -164,13 +174,21 @@ private:
     void Inject(std::size_t local, std::size_t b);  // SRT_ENGINE_INJECT (comm.h)
     std::size_t FrameIndex(std::size_t local, std::size_t b, std::size_t f) const;  // frame of the sequence
     int* Ids(unsigned char* buf, std::size_t band_frame) const;  // band frame `band_frame` of an id buffer
+    // A device's band in one role: bands / rotating / root have one role (its band); kShare has role 0
+    // (compositor: k of every k + P - 1 tile rows, RGBA) and roles 1 .. P - 1 (sender of class
+    // k + role - 1: one tile row per cycle, ids).
+    struct Role {
+        std::size_t row_begin = 0, rows = 0, pattern = 1;
+        std::size_t input = 0;  // rows of the earlier roles (Device::band_in: per role, inputs x rows x W x 2)
+    };
+    std::size_t RoleOf(std::size_t local, std::size_t b) const;
     void TracePhase(std::size_t local, std::size_t b);
     void ExchangePhase(std::size_t local, std::size_t b);  // RCCL: inside a group
     void CopyPhase(std::size_t local, std::size_t b);      // device-copy exchange
     void ShadePhase(std::size_t local, std::size_t b);
     void RunWorker(std::size_t local, std::size_t b0, std::size_t batches);
     void Barrier();
-    const float* BandInput(std::size_t local, std::size_t k) const;
+    const float* BandInput(std::size_t local, std::size_t k, std::size_t role = 0) const;
     const float* FullInput(std::size_t local, std::size_t k) const;
     std::size_t FrameFloats() const { return m_width * m_height * 2; }
 
@@ -184,6 +202,7 @@ private:
     bool m_comms_made = false; // RCCL communicators were created (uses_rccl after an abort too)
     bool m_copy = false;       // exchange by device copies (repeated device / SRT_GATHER=copy)
     bool m_defer_shade = false;  // env SRT_DEFER_SHADE=1 (measurement): whole frames as ids + a shading launch
+    std::size_t m_share = 0;     // kShare: the compositor's tile rows per cycle (0: another exchange)
     BandSplit m_split;
     ExchangePlan m_plan;
     std::vector<std::unique_ptr<Device>> m_dev;

@@ -70,10 +70,11 @@ struct BandArgs {
     std::size_t row_begin;  // first frame row of the band
     std::size_t row_count;
     int* ids = nullptr;     // device, row_count x width: non-null = store hit ids (-1 miss), not RGBA
-    // 1: frame rows [row_begin, row_begin + row_count). P > 1: the band deals the frame's tile rows
-    // (kCullTileRows each) round-robin over P bands: frame tile rows row_begin / kCullTileRows + k P,
-    // k = 0, 1, ..., concatenated (row_begin a multiple of kCullTileRows; only the band's last tile
-    // row may be partial, and then it is the frame's last).
+    // The band's row pattern. 1: frame rows [row_begin, row_begin + row_count). P > 1: the band deals
+    // the frame's tile rows (kCullTileRows each) round-robin over P bands: frame tile rows
+    // row_begin / kCullTileRows + k P, k = 0, 1, ..., concatenated (row_begin a multiple of
+    // kCullTileRows; only the band's last tile row may be partial, and then it is the frame's last).
+    // RowPattern(P, g): g consecutive tile rows out of every P (the compositor's share, engine.h).
     std::size_t row_interleave = 1;
     // ids holds packed hit ids (PackedIds) with this many bit planes above the 16-bit low plane;
     // -1: int32 ids (-1 = miss). The multi-GPU exchange payload (cull variant).
@@ -102,8 +103,15 @@ struct PackedIds {
 };
 PackedIds PackedIdLayout(int planes, std::size_t rows, std::size_t width);
 
-// Frame row of band-local row `local` (BandArgs::row_interleave).
-inline std::size_t BandFrameRow(std::size_t row_begin, std::size_t interleave, std::size_t local);
+// A band row pattern (BandArgs::row_interleave) taking `group` consecutive tile rows out of every
+// `interleave`: interleave in the low 16 bits, group - 1 above (group 1: the plain interleave).
+constexpr std::size_t RowPattern(std::size_t interleave, std::size_t group) {
+    return interleave | (group - 1) << 16;
+}
+// Frame row of band-local row `local` (BandArgs::row_interleave: an interleave or a RowPattern).
+inline std::size_t BandFrameRow(std::size_t row_begin, std::size_t pattern, std::size_t local);
+// Rows of the band of pattern `pattern` starting at frame row `row_begin` of a `height`-row frame.
+std::size_t PatternBandRows(std::size_t height, std::size_t row_begin, std::size_t pattern);
 // Whether a binned cull frame computes its tile info inside the bin launch (one launch fewer, the
 // tile info and the bins concurrent): full frames (the band is the whole frame), unless env
 // SRT_FUSED_INFO=0. Its bins then use the analytic tile bounds (valid for offsets in [0, 1]) and
@@ -130,8 +138,10 @@ constexpr int kCullTileCols = 64;
 #endif
 constexpr int kCullTileRows = SRT_TILE_ROWS;
 
-inline std::size_t BandFrameRow(std::size_t row_begin, std::size_t interleave, std::size_t local) {
-    return row_begin + local + local / kCullTileRows * kCullTileRows * (interleave - 1);
+inline std::size_t BandFrameRow(std::size_t row_begin, std::size_t pattern, std::size_t local) {
+    const std::size_t interleave = pattern & 0xFFFFu, group = (pattern >> 16) + 1;
+    const std::size_t lt = local / kCullTileRows;
+    return row_begin + (lt / group * interleave + lt % group) * kCullTileRows + local % kCullTileRows;
 }
 constexpr int kMaxBatch = 8;          // frames of a batched cull launch with its parameters as kernel arguments
 constexpr int kMaxBoundTiles = 2048;  // binning needs tiles_x + tiles_y <= this
@@ -267,7 +277,9 @@ hipError_t LaunchShadeTable(const float* d_vertices, const float* d_albedo, std:
 hipError_t LaunchShade(const float* d_vertices, const float* d_shade, const float* d_edges, std::uint64_t n,
                        const Frame& frame, const float background[3], const BandArgs& band, hipStream_t stream,
                        std::size_t frames = 1, std::size_t band_rows = 0, std::size_t interleaved = 0,
-                       std::size_t offsets_stride = 0, long skip_band = -1);
+                       std::size_t offsets_stride = 0, long skip_band = -1, std::size_t own_bands = 0);
+// (skip_band >= 0: the rows of that band are left as they are; own_bands > 0: so are the rows of
+// bands [0, own_bands), and the ids start at band own_bands -- the compositor's share, engine.h.)
 
 // Spatial order of the records (spatial.hip): ids sorted by the Morton code of their centroid's
 // image-plane position under the scene camera, on the device (keys + rocPRIM radix sort), and

@@ -487,8 +487,14 @@ __device__ __forceinline__ void TestTriangle(Rays<R>& s, const Record& q, unsign
 // pattern; `box` receives the rays' (fx, fy) bounding box (NaN positions drop out: a ray
 // Frame row of band-local row `local`: the band holds frame tile rows row_begin / kCullTileRows
 // + k * interleave, k = 0, 1, ... (interleave 1: the contiguous rows row_begin + local).
+// (interleave: a plain interleave, or a RowPattern taking `group` consecutive tile rows of every
+// interleave: render.h BandFrameRow.)
 __device__ __forceinline__ int FrameRow(int row_begin, int interleave, int local) {
-    return row_begin + local + local / kCullTileRows * kCullTileRows * (interleave - 1);
+    const int lt = local / kCullTileRows, group = (interleave >> 16) + 1;
+    if (group == 1) {
+        return row_begin + local + lt * kCullTileRows * (interleave - 1);
+    }
+    return row_begin + (lt / group * (interleave & 0xFFFF) + lt % group) * kCullTileRows + local % kCullTileRows;
 }
 
 // with a NaN position fails every test).
@@ -619,7 +625,8 @@ template <bool PACKED>
 __global__ __launch_bounds__(kShadeThreads) void ShadeIdsKernel(TraceParams p, const void* __restrict__ ids_v,
                                                                 unsigned band_rows, unsigned frames,
                                                                 unsigned interleaved, size_t offsets_stride,
-                                                                unsigned skip_band, size_t frame_bytes) {
+                                                                unsigned skip_band, unsigned own_bands,
+                                                                size_t frame_bytes) {
     using IdT = std::conditional_t<PACKED, unsigned, int>;
     const int* __restrict__ ids = static_cast<const int*>(ids_v);
     const unsigned char* __restrict__ packed = static_cast<const unsigned char*>(ids_v);
@@ -632,7 +639,9 @@ __global__ __launch_bounds__(kShadeThreads) void ShadeIdsKernel(TraceParams p, c
     const size_t pixels = static_cast<size_t>(p.width) * p.row_count;
     IdT id[kShadeRows];
     float2 o[kShadeRows];
-    bool mine[kShadeRows];  // rows of band skip_band: the compositor traced them as RGBA already
+    // Rows of band skip_band, or of bands [0, own_bands) (whose ids the buffer does not hold: it starts
+    // at band own_bands): the compositor traced them as RGBA already.
+    bool mine[kShadeRows];
     // Interleaved bands: the thread's rows lie in one tile row (kShadeRows divides it), so in one
     // band (the divisions once per thread, not per row).
     static_assert(kCullTileRows % kShadeRows == 0, "a thread's rows share a tile row");
@@ -651,7 +660,8 @@ __global__ __launch_bounds__(kShadeThreads) void ShadeIdsKernel(TraceParams p, c
             band = static_cast<unsigned>(y) / band_rows;
             local = static_cast<unsigned>(y) - band * band_rows;
         }
-        mine[r] = band == skip_band;
+        mine[r] = band == skip_band || band < own_bands;
+        band -= mine[r] ? 0u : own_bands;
         if constexpr (PACKED) {
             const unsigned char* row =
                 packed + (static_cast<size_t>(band) * frames + g) * frame_bytes + static_cast<size_t>(local) * p.id_row_bytes;
@@ -3636,10 +3646,25 @@ bool BandFits(std::size_t row_begin, std::size_t row_count, std::size_t interlea
     if (row_count == 0) {
         return true;
     }
-    if (interleave > 1 && row_begin % kCullTileRows != 0) {
+    const std::size_t every = interleave & 0xFFFFu, group = (interleave >> 16) + 1;
+    if (every == 0 || group > every || (interleave > 1 && row_begin % kCullTileRows != 0)) {
         return false;
     }
     return BandFrameRow(row_begin, interleave, row_count - 1) < height;  // earlier tile rows are full
+}
+
+std::size_t PatternBandRows(std::size_t height, std::size_t row_begin, std::size_t pattern) {
+    if (pattern <= 1) {
+        return row_begin < height ? height - row_begin : 0;
+    }
+    std::size_t rows = 0;
+    for (std::size_t local = 0;; local += kCullTileRows) {
+        const std::size_t fr = BandFrameRow(row_begin, pattern, local);
+        if (fr >= height) {
+            return rows;
+        }
+        rows += std::min<std::size_t>(kCullTileRows, height - fr);
+    }
 }
 
 std::size_t InterleavedBandRows(std::size_t height, std::size_t bands, std::size_t band) {
@@ -3684,7 +3709,7 @@ hipError_t LaunchShadeTable(const float* d_vertices, const float* d_albedo, std:
 hipError_t LaunchShade(const float* d_vertices, const float* d_shade, const float* d_edges, std::uint64_t n,
                        const Frame& frame, const float background[3], const BandArgs& band, hipStream_t stream,
                        std::size_t frames, std::size_t band_rows, std::size_t interleaved,
-                       std::size_t offsets_stride, long skip_band) {
+                       std::size_t offsets_stride, long skip_band, std::size_t own_bands) {
     if (band.row_count == 0 || band.width == 0 || frames == 0) {
         return hipSuccess;
     }
@@ -3730,11 +3755,13 @@ hipError_t LaunchShade(const float* d_vertices, const float* d_shade, const floa
         p.id_row_bytes = static_cast<unsigned>(lay.row_bytes);
         hipLaunchKernelGGL(ShadeIdsKernel<true>, grid, dim3(kShadeThreads), 0, stream, p, ids,
                            static_cast<unsigned>(band_rows), static_cast<unsigned>(frames),
-                           static_cast<unsigned>(interleaved), offsets_stride / 2, skip, lay.bytes);
+                           static_cast<unsigned>(interleaved), offsets_stride / 2, skip,
+                           static_cast<unsigned>(own_bands), lay.bytes);
     } else {
         hipLaunchKernelGGL(ShadeIdsKernel<false>, grid, dim3(kShadeThreads), 0, stream, p, ids,
                            static_cast<unsigned>(band_rows), static_cast<unsigned>(frames),
-                           static_cast<unsigned>(interleaved), offsets_stride / 2, skip, size_t{0});
+                           static_cast<unsigned>(interleaved), offsets_stride / 2, skip,
+                           static_cast<unsigned>(own_bands), size_t{0});
     }
     return hipGetLastError();
 }

@@ -83,7 +83,8 @@ public:
     void Shade(const float* d_offsets, const int* d_ids, float* d_rgba, std::size_t row_begin, std::size_t row_count,
                hipStream_t stream, std::size_t frames = 1, std::size_t band_rows = 0,
                std::size_t interleaved = 0, std::size_t offsets_stride = 0, int id_planes = -1,
-               long skip_band = -1) const;  // skip_band: rows of that band are left as they are
+               long skip_band = -1,  // skip_band: rows of that band are left as they are
+               std::size_t own_bands = 0) const;  // and of bands [0, own_bands) (render.h LaunchShade)
     // `frames` (<= render.h kMaxTableFrames) frames of the prepared camera, rows [row_begin,
     // row_begin + row_count) each: frame f's offsets d_offsets[f], its RGBA d_rgba[f] or (d_ids
     // non-null) its hit ids d_ids[f]. Each frame gets the whole per-frame pipeline (record setup,

@@ -350,7 +350,8 @@ static_assert(SRT_SPLIT_BANDS == srt::EngineOptions::kBands && SRT_SPLIT_FRAMES 
               "include/srt_render.h SRT_SPLIT_*");
 static_assert(SRT_EXCHANGE_ALLTOALL == srt::EngineOptions::kAllToAll &&
                   SRT_EXCHANGE_ROTATING == srt::EngineOptions::kRotatingGather &&
-                  SRT_EXCHANGE_ROOT == srt::EngineOptions::kRootGather,
+                  SRT_EXCHANGE_ROOT == srt::EngineOptions::kRootGather &&
+                  SRT_EXCHANGE_SHARE == srt::EngineOptions::kShare,
               "include/srt_render.h SRT_EXCHANGE_*");
 
 }  // extern "C"
@@ -376,6 +377,7 @@ srt::EngineOptions EngineOptionsFrom(const srt_engine_options* o) {
             throw std::runtime_error("Unknown engine flags " + std::to_string(o->flags));
         }
         opt.rccl_self = (o->flags & SRT_ENGINE_RCCL_SELF) != 0;
+        opt.share = o->share;
     }
     return opt;
 }

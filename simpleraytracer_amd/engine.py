@@ -18,10 +18,11 @@ import os
 
 from . import _native
 from ._native import (SRT_ENGINE_RCCL_SELF, SRT_EXCHANGE_ALLTOALL, SRT_EXCHANGE_ROOT, SRT_EXCHANGE_ROTATING,
-                      SRT_ROWS_CONTIGUOUS, SRT_ROWS_INTERLEAVED, SRT_SPLIT_BANDS, SRT_SPLIT_FRAMES, EngineOptions)
+                      SRT_EXCHANGE_SHARE, SRT_ROWS_CONTIGUOUS, SRT_ROWS_INTERLEAVED, SRT_SPLIT_BANDS, SRT_SPLIT_FRAMES, EngineOptions)
 from .device import TRACE_VARIANTS, SrtError
 
-EXCHANGES = {"alltoall": SRT_EXCHANGE_ALLTOALL, "rotating": SRT_EXCHANGE_ROTATING, "root": SRT_EXCHANGE_ROOT}
+EXCHANGES = {"alltoall": SRT_EXCHANGE_ALLTOALL, "rotating": SRT_EXCHANGE_ROTATING, "root": SRT_EXCHANGE_ROOT,
+             "share": SRT_EXCHANGE_SHARE}
 ROWS = {"interleaved": SRT_ROWS_INTERLEAVED, "contiguous": SRT_ROWS_CONTIGUOUS}
 SPLITS = {"bands": SRT_SPLIT_BANDS, "frames": SRT_SPLIT_FRAMES}
 
@@ -31,9 +32,9 @@ def _check(rc: int):
         raise SrtError(_native.last_error())
 
 
-def _options(variant, queues, batch, rows, exchange, split, simulate=False, launch=0, rccl_self=False):
+def _options(variant, queues, batch, rows, exchange, split, simulate=False, launch=0, rccl_self=False, share=0):
     return EngineOptions(TRACE_VARIANTS[variant], queues, batch, ROWS[rows], EXCHANGES[exchange], SPLITS[split],
-                         1 if simulate else 0, launch, SRT_ENGINE_RCCL_SELF if rccl_self else 0)
+                         1 if simulate else 0, launch, SRT_ENGINE_RCCL_SELF if rccl_self else 0, share)
 
 
 def unique_id() -> bytes:
@@ -48,16 +49,18 @@ class FrameEngine:
 
     def __init__(self, path: str, width: int, height: int, devices=(0,), variant: str = "cull", queues: int = 2,
                  batch: int = 16, rows: str = "interleaved", exchange: str = "alltoall", split: str = "bands",
-                 launch: int = 0, rccl_self: bool = False, _handle=None):
+                 launch: int = 0, rccl_self: bool = False, share: int = 0, _handle=None):
         """rccl_self (one device, tests): the bands path with the frame's ids sent to itself over a
-        one-rank RCCL communicator -- the real exchange, its waits and its abort path."""
+        one-rank RCCL communicator -- the real exchange, its waits and its abort path.
+        exchange="share": the compositor traces `share` of every share + P - 1 tile rows itself (0: 3)."""
         self._lib = _native.lib()
         self.width, self.height, self.batch = width, height, batch
         self.options = {"variant": variant, "queues": queues, "batch": batch, "rows": rows, "exchange": exchange,
-                        "split": split, "launch": launch, "rccl_self": rccl_self}
+                        "split": split, "launch": launch, "rccl_self": rccl_self, "share": share}
         if _handle is None:
             devs = (ctypes.c_int * len(devices))(*devices)
-            opt = _options(variant, queues, batch, rows, exchange, split, launch=launch, rccl_self=rccl_self)
+            opt = _options(variant, queues, batch, rows, exchange, split, launch=launch, rccl_self=rccl_self,
+                           share=share)
             _handle = self._lib.srtEngineCreate(os.fsencode(path), devs, len(devices), width, height, ctypes.byref(opt))
         if not _handle:
             raise SrtError(_native.last_error())
@@ -68,17 +71,18 @@ class FrameEngine:
     @classmethod
     def rank(cls, path: str, width: int, height: int, device: int, rank: int, world: int, uid: bytes | None,
              variant: str = "cull", queues: int = 2, batch: int = 16, rows: str = "interleaved",
-             exchange: str = "alltoall", split: str = "bands", simulate: bool = False, launch: int = 0):
+             exchange: str = "alltoall", split: str = "bands", simulate: bool = False, launch: int = 0,
+             share: int = 0):
         """This process's rank of a `world`-rank job on `device`; every rank calls it concurrently.
         simulate=True (measurement): no peers, no unique id -- the rank's stream without the exchange."""
         lib = _native.lib()
-        opt = _options(variant, queues, batch, rows, exchange, split, simulate, launch)
+        opt = _options(variant, queues, batch, rows, exchange, split, simulate, launch, share=share)
         idbuf = ctypes.create_string_buffer(uid, 128) if uid is not None else None
         h = lib.srtEngineCreateRank(os.fsencode(path), device, rank, world, idbuf, width, height, ctypes.byref(opt))
         if not h:
             raise SrtError(_native.last_error())
         return cls(path, width, height, variant=variant, queues=queues, batch=batch, rows=rows, exchange=exchange,
-                   split=split, launch=launch, _handle=h)
+                   split=split, launch=launch, share=share, _handle=h)
 
     def set_inputs(self, offsets):
         """offsets: (count, H, W, 2) or (H, W, 2) float32 host array (numpy or CPU tensor)."""

@@ -60,6 +60,28 @@ def test_engine_fake_devices_bitwise(gpu, scenes, p, rows, exchange):
         assert bad == 0 and checked == 2 * F
 
 
+@pytest.mark.parametrize("p,share,queues", [(2, 3, 2), (2, 1, 2), (2, 7, 3), (3, 3, 2), (8, 2, 4)])
+def test_engine_fake_devices_share_bitwise(gpu, scenes, p, share, queues):
+    """The share exchange (the compositor of a batch traces `share` of every share + P - 1 tile rows
+    itself, straight into its frames; every other device one tile row per cycle, sent as ids and
+    shaded there): distinct inputs per frame, every frame of the last batches equal to a one-device
+    render of its input, bit for bit -- also with a queue count that makes a queue change roles
+    (and so band shapes) from batch to batch."""
+    w, h, F = 150, 230, 4  # 15 tile rows: cycles of share + P - 1 end in a partial one
+    inputs = random_inputs(2 * F, h, w, seed=11 + p)
+    refs = [torch_render(scenes["soup2k"], w, h, inputs[k]) for k in range(2 * F)]
+    with engine(scenes["soup2k"], w, h, devices=[0] * p, exchange="share", share=share, queues=queues,
+                batch=F) as e:
+        e.set_inputs(inputs)
+        e.run(queues + 1)
+        for k in range(F, (queues + 1) * F):
+            got = e.read_frame(k)
+            assert np.array_equal(got.view(np.uint32), refs[k % (2 * F)].view(np.uint32)), k
+        bad, checked = e.verify()
+        assert bad == 0 and checked == queues * F
+        assert e.info()["exchange_bytes_per_frame"] > 0
+
+
 def test_engine_fake_devices_rotating_inputs(gpu, scenes):
     """Distinct inputs per frame through the all-to-all exchange (the compositors' strided offsets)."""
     w, h, p, F = 70, 90, 2, 4
@@ -101,6 +123,24 @@ def test_engine_c3_bands_of_8_bitwise(gpu, scenes):
         e.run(2)
         assert e.verify() == (0, 32)
         got = e.read_frame(17)
+    rows = np.arange(5, 1080, 90)
+    ref = oracle_render(scenes["soup100k"], w, h, row_begin=5, row_count=1075, row_step=90)
+    assert_parity(got, ref, rows=rows)
+
+
+def test_engine_c3_share_of_2_bitwise(gpu, scenes):
+    """The headline frame over 2 fake devices with the share exchange (each compositor traces 3 of
+    every 4 tile rows itself, the other device the fourth): every frame equals the one-device frame,
+    and a quarter of the frame's ids cross the exchange."""
+    w, h = 1920, 1080
+    inputs = np.full((1, h, w, 2), 0.5, np.float32)
+    with engine(scenes["soup100k"], w, h, devices=[0, 0], batch=16, queues=2, exchange="share") as e:
+        e.set_inputs(inputs)
+        e.run(3)
+        assert e.verify() == (0, 8)
+        got = e.read_frame(40)
+        xb = e.info()["exchange_bytes_per_frame"]
+    assert xb < 0.3 * h * w * 2.125, xb  # one sender, 17 of the 68 tile rows
     rows = np.arange(5, 1080, 90)
     ref = oracle_render(scenes["soup100k"], w, h, row_begin=5, row_count=1075, row_step=90)
     assert_parity(got, ref, rows=rows)

@@ -117,7 +117,7 @@ def _gpus():
     return torch.cuda.device_count()
 
 
-@pytest.mark.parametrize("exchange", ["alltoall", "rotating", "root"])
+@pytest.mark.parametrize("exchange", ["alltoall", "rotating", "root", "share"])
 @pytest.mark.parametrize("which", ["2", "all"])
 def test_engine_rccl_bands_full_c3_fixture(gpu, paths, ids, exchange, which):
     """Distinct GPUs, RCCL between them (BASELINE config C4): P = 2 and P = every visible GPU (at most

@@ -8,7 +8,9 @@ The exchange, modelled (it cannot be measured on a one-GPU box): per frame the P
 not composite it send their band of hit ids (the engine's payload: id_bytes per pixel, 2 for 16-bit
 codes) to its compositor; the all-to-all deals the compositors round-robin, so every one of the
 P (P - 1) directed xGMI links of a fully connected node carries bytes_frame / (P (P - 1)) per frame
-on average, and the link-bound time per frame is that over the per-direction link rate. ASSUMED
+on average (rotating / share: a batch's P - 1 senders use their links into its compositor, the
+min(Q, P) batches in flight distinct ones), and the link-bound time per frame is that over the
+per-direction link rate. ASSUMED
 rate, not measured: --link-gbs (default 64 GB/s per direction; MI355X_MICROARCH.md has no xGMI figure,
 SURVEY.md section 5 quotes 153.6 GB/s per link, bidirectional, so about 77 GB/s each way at peak;
 RCCL point-to-point reaching ~85 % of it gives ~64). A sweep of rates is printed beside it. The job
@@ -41,6 +43,8 @@ def main():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--triangles", type=int, default=100_000)
     ap.add_argument("--rows", default="interleaved")
+    ap.add_argument("--exchange", default="alltoall", choices=["alltoall", "rotating", "share"])
+    ap.add_argument("--share", type=int, default=0, help="share exchange: the compositor's tile rows per cycle (0: 3)")
     ap.add_argument("--launch", type=int, default=0, help="frames per trace launch (0: library default)")
     ap.add_argument("--all-ranks", action="store_true", help="every rank (default: ranks 0, P/2 and P-1)")
     ap.add_argument("--link-gbs", type=float, default=64.0, help="ASSUMED xGMI rate per direction (module doc)")
@@ -56,7 +60,7 @@ def main():
     path = write_scene(os.path.join(tmp.name, "soup.srt"), "soup", a.triangles)
     inputs = np.full((1, a.height, a.width, 2), 0.5, np.float32)
     out = {"batch": a.batch, "launch": a.launch, "queues": a.queues, "triangles": a.triangles, "width": a.width, "height": a.height,
-           "rows": a.rows, "ranks": {}}
+           "rows": a.rows, "exchange": a.exchange, "share": a.share, "ranks": {}}
     for P in [int(x) for x in a.ranks.split(",")]:
         per = {}
         xbytes = 0.0
@@ -67,7 +71,8 @@ def main():
                                   launch=a.launch)
             else:
                 eng = FrameEngine.rank(path, a.width, a.height, 0, r, P, None, queues=a.queues, batch=a.batch,
-                                       rows=a.rows, simulate=True, launch=a.launch)
+                                       rows=a.rows, simulate=True, launch=a.launch, exchange=a.exchange,
+                                       share=a.share)
             eng.set_inputs(inputs)
             xbytes = eng.info()["exchange_bytes_per_frame"] if P > 1 else 0.0
             eng.run(a.warmup)
@@ -79,7 +84,11 @@ def main():
             per[r] = round(dt / (a.steps * a.batch) * 1e6, 3)
             eng.close()
         slow = max(per.values())
-        link_bytes = xbytes / (P * (P - 1)) if P > 1 else 0.0
+        # all-to-all: every directed link carries 1/(P (P - 1)) of a frame's payload; rotating / share:
+        # a batch's P - 1 senders each use their link into its compositor, and the queues' batches in
+        # flight (on min(queues, P) distinct compositors) use distinct links
+        links = P * (P - 1) if a.exchange == "alltoall" else (P - 1) * min(a.queues, P)
+        link_bytes = xbytes / links if P > 1 else 0.0
         link_us = link_bytes / (a.link_gbs * 1e3)
         bound = max(slow, link_us)
         out["ranks"][P] = {"us_per_frame": per, "slowest_us": slow,
