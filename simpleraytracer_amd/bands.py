@@ -48,3 +48,21 @@ def interleaved_frame_rows(height: int, world: int, rank: int):
     tiles = (height + TILE_ROWS - 1) // TILE_ROWS
     return np.concatenate([np.arange(t * TILE_ROWS, min(height, (t + 1) * TILE_ROWS))
                            for t in range(rank, tiles, world)] or [np.zeros(0, np.int64)]).astype(np.int64)
+
+
+def share_frame_rows(height: int, world: int, share: int, rank: int, compositor: int):
+    """The frame rows ``rank`` traces, in band order, for a frame composited on ``compositor`` under
+    the share exchange (csrc/engine.h kShare): the frame's tile rows in cycles of share + P - 1
+    classes; the compositor takes the first ``share`` of every cycle (render.h RowPattern(share +
+    P - 1, share)), each other rank one class, in rank order after the compositor (numpy int64)."""
+    import numpy as np
+
+    classes = share + world - 1
+    tiles = (height + TILE_ROWS - 1) // TILE_ROWS
+    if rank == compositor:
+        mine = [t for t in range(tiles) if t % classes < share]
+    else:
+        cls = share + (rank - compositor - 1) % world
+        mine = list(range(cls, tiles, classes))
+    return np.concatenate([np.arange(t * TILE_ROWS, min(height, (t + 1) * TILE_ROWS)) for t in mine]
+                          or [np.zeros(0, np.int64)]).astype(np.int64)
