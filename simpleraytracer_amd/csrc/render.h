@@ -88,9 +88,13 @@ struct BandArgs {
 // all ones for a miss -- in 16 + k bits, k = the bits the triangle count needs beyond 16 (C3's 100 000
 // triangles: 1, 2.125 B per pixel against int32's 4; under 65 535 triangles: 0; C5's 1M: 4). Row-major
 // rows, each: the row's u16 low 16 bits (padded to 8 B), then per plane j one 64-bit word per 64
-// columns (bit x % 64 of word x / 64 is bit 16 + j of pixel x's code). A band frame is `rows` such rows
-// (padded to 256 B), so a band's actual rows and its buffer's rows index it alike. Written by the trace
-// epilogue (one ballot per plane and row segment), read by the deferred shading: no decode work.
+// columns (bit x % 64 of word x / 64 is bit 16 + j of pixel x's code). Rows come in tile rows of
+// kCullTileRows, each followed by its tiles' sample offset: one float2 per 64-column tile, the
+// offset every ray of the tile has (the tile is "regular"), or NaNs (0.4 % more bytes at 1080p), so
+// the shading of a regular tile reads no per-pixel offsets. A band frame is its tile rows (padded to
+// 256 B), so a band's actual rows and its buffer's rows index it alike. Written by the trace (one
+// ballot per plane and row segment; the tile's offset by its first block), read by the deferred
+// shading: no decode work.
 constexpr int kMaxIdPlanes = 8;
 int IdPlanes(std::uint64_t triangles);  // k; -1 when the ids need more than 16 + kMaxIdPlanes bits
 struct PackedIds {
@@ -99,6 +103,7 @@ struct PackedIds {
     std::size_t words = 0;          // 64-bit words per row and plane
     std::size_t low_row_bytes = 0;  // a row's u16 values, padded to 8 B
     std::size_t row_bytes = 0;      // a row
+    std::size_t tile_row_bytes = 0; // kCullTileRows rows, then words float2 tile offsets
     std::size_t bytes = 0;          // one band frame
 };
 PackedIds PackedIdLayout(int planes, std::size_t rows, std::size_t width);

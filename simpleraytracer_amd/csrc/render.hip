@@ -80,6 +80,7 @@ struct TraceParams {
     unsigned id_words;         // packed ids: 64-bit words per row and plane
     unsigned id_low_row_bytes; // packed ids: the row's u16 values (padded to 8 B), then its plane words
     unsigned id_row_bytes;     // packed ids: bytes per row
+    unsigned id_tile_row_bytes;  // packed ids: bytes per tile row (its rows, then its tiles' offsets)
     int out_frame_rows;  // RGBA out is a whole frame: band row y stores at its frame row (render.h BandArgs)
     unsigned n_pad;   // records in the edge buffer (multiple of kPadTriangles)
     unsigned n;       // records in the scene
@@ -565,10 +566,23 @@ __device__ __forceinline__ void StorePixel(const TraceParams& p, int x, int y, f
 // Packed ids (render.h PackedIds) of one band row segment: the wave's 64 lanes are the 64 columns
 // x = tx * 64 + lane of band row y (wave-uniform; called by every lane of the wave). The low 16 bits
 // go to the u16 plane; bit 16 + j of the 64 codes is one ballot, stored by lane 0 as plane j's word.
+// Band row y of a packed band frame, and the offset entry of tile tx of band tile row y / kCullTileRows
+// (render.h PackedIds).
+template <class Byte>
+__device__ __forceinline__ Byte* PackedRow(Byte* frame, const TraceParams& p, int y) {
+    return frame + static_cast<size_t>(y / kCullTileRows) * p.id_tile_row_bytes +
+           static_cast<size_t>(y % kCullTileRows) * p.id_row_bytes;
+}
+template <class Byte>
+__device__ __forceinline__ Byte* PackedTileOffset(Byte* frame, const TraceParams& p, int y, int tx) {
+    return frame + static_cast<size_t>(y / kCullTileRows) * p.id_tile_row_bytes +
+           static_cast<size_t>(kCullTileRows) * p.id_row_bytes + static_cast<size_t>(tx) * sizeof(float2);
+}
+
 __device__ __forceinline__ void StorePackedIds(const TraceParams& p, int tx, int x, int y, int id) {
     const bool valid = x < p.width;
     const unsigned code = id < 0 ? 0xFFFFFFFFu : static_cast<unsigned>(id);
-    unsigned char* row = p.out_packed + static_cast<size_t>(y) * p.id_row_bytes;
+    unsigned char* row = PackedRow(p.out_packed, p, y);
     if (valid) {
         __builtin_nontemporal_store(static_cast<unsigned short>(code & 0xFFFFu), reinterpret_cast<unsigned short*>(row) + x);
     }
@@ -639,6 +653,7 @@ __global__ __launch_bounds__(kShadeThreads) void ShadeIdsKernel(TraceParams p, c
     const size_t pixels = static_cast<size_t>(p.width) * p.row_count;
     IdT id[kShadeRows];
     float2 o[kShadeRows];
+    float2 tile_o[kShadeRows];  // packed ids: the row's tile offset (NaN: read the pixel's own)
     // Rows of band skip_band, or of bands [0, own_bands) (whose ids the buffer does not hold: it starts
     // at band own_bands): the compositor traced them as RGBA already.
     bool mine[kShadeRows];
@@ -660,13 +675,16 @@ __global__ __launch_bounds__(kShadeThreads) void ShadeIdsKernel(TraceParams p, c
             band = static_cast<unsigned>(y) / band_rows;
             local = static_cast<unsigned>(y) - band * band_rows;
         }
+        tile_o[r] = make_float2(__builtin_nanf(""), __builtin_nanf(""));
         mine[r] = band == skip_band || band < own_bands;
         band -= mine[r] ? 0u : own_bands;
         if constexpr (PACKED) {
-            const unsigned char* row =
-                packed + (static_cast<size_t>(band) * frames + g) * frame_bytes + static_cast<size_t>(local) * p.id_row_bytes;
+            const unsigned char* frame = packed + (static_cast<size_t>(band) * frames + g) * frame_bytes;
+            const unsigned char* row = PackedRow(frame, p, static_cast<int>(local));
             unsigned code = 0u;
             if (!mine[r]) {
+                // the tile's sample offset when every ray of it has that one (regular), else NaNs
+                tile_o[r] = *reinterpret_cast<const float2*>(PackedTileOffset(frame, p, static_cast<int>(local), x >> 6));
                 code = __builtin_nontemporal_load(reinterpret_cast<const unsigned short*>(row) + x);
                 const unsigned long long* bits = reinterpret_cast<const unsigned long long*>(row + p.id_low_row_bytes);
                 for (int j = 0; j < p.id_planes; ++j) {
@@ -683,12 +701,17 @@ __global__ __launch_bounds__(kShadeThreads) void ShadeIdsKernel(TraceParams p, c
     // Only a hit needs its ray: a miss shades to the background whatever its sample offset, so the
     // offsets of the miss pixels (72 % of C3's) are never loaded. A miss is -1, the packed miss code
     // (all ones) or any id outside the scene.
+    // Packed ids carry each tile's offset when every ray of the tile has it: then no pixel of the
+    // tile reads its own (the trace computed those rays from the same offset, bit for bit).
     int hit[kShadeRows];
 #pragma unroll
     for (int r = 0; r < kShadeRows; ++r) {
         const int y = min(y0 + r, p.row_count - 1);
         hit[r] = !mine[r] && static_cast<unsigned>(id[r]) < p.n ? static_cast<int>(id[r]) : -1;
-        o[r] = hit[r] < 0 ? float2{} : p.offsets[static_cast<size_t>(y) * p.width + x + g * offsets_stride];  // frame g's (stride 0: shared)
+        const bool regular = PACKED && tile_o[r].x == tile_o[r].x;
+        o[r] = hit[r] < 0 ? float2{}
+               : regular  ? tile_o[r]
+                          : p.offsets[static_cast<size_t>(y) * p.width + x + g * offsets_stride];  // frame g's (stride 0: shared)
     }
 #pragma unroll
     for (int r = 0; r < kShadeRows; ++r) {
@@ -2453,6 +2476,13 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(c
     if (row0 >= p.row_count) {
         return;  // the last tile row's empty part
     }
+    if (p.out_packed != nullptr && threadIdx.x == 0 && chunk == 0u && item % kParts == 0u) {
+        // The tile's sample offset in the packed ids when every ray of the tile has it (the deferred
+        // shading then reads no per-pixel offsets for the tile), else NaNs (render.h PackedIds).
+        const float qn = __builtin_nanf("");
+        *reinterpret_cast<float2*>(PackedTileOffset(p.out_packed, p, ty * kTileRows, tx)) =
+            (flags & kItemRegular) != 0u ? make_float2(ox, oy) : make_float2(qn, qn);
+    }
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
     const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);
@@ -3375,6 +3405,7 @@ TraceParams MakeTraceParams(const float* d_edges, std::uint64_t n, const float* 
         p.id_words = static_cast<unsigned>(lay.words);
         p.id_low_row_bytes = static_cast<unsigned>(lay.low_row_bytes);
         p.id_row_bytes = static_cast<unsigned>(lay.row_bytes);
+        p.id_tile_row_bytes = static_cast<unsigned>(lay.tile_row_bytes);
     }
     p.out_frame_rows = band.rgba_frame_rows ? 1 : 0;
     p.n_pad = static_cast<unsigned>(PaddedTriangleCount(n));
@@ -3692,7 +3723,8 @@ PackedIds PackedIdLayout(int planes, std::size_t rows, std::size_t width) {
     l.words = (width + kWave - 1) / kWave;
     l.low_row_bytes = (width * 2 + 7) / 8 * 8;
     l.row_bytes = l.low_row_bytes + static_cast<std::size_t>(l.planes) * l.words * 8;
-    l.bytes = (rows * l.row_bytes + 255) / 256 * 256;
+    l.tile_row_bytes = kCullTileRows * l.row_bytes + l.words * 8;
+    l.bytes = ((rows + kCullTileRows - 1) / kCullTileRows * l.tile_row_bytes + 255) / 256 * 256;
     return l;
 }
 
@@ -3753,6 +3785,7 @@ hipError_t LaunchShade(const float* d_vertices, const float* d_shade, const floa
         p.id_words = static_cast<unsigned>(lay.words);
         p.id_low_row_bytes = static_cast<unsigned>(lay.low_row_bytes);
         p.id_row_bytes = static_cast<unsigned>(lay.row_bytes);
+        p.id_tile_row_bytes = static_cast<unsigned>(lay.tile_row_bytes);
         hipLaunchKernelGGL(ShadeIdsKernel<true>, grid, dim3(kShadeThreads), 0, stream, p, ids,
                            static_cast<unsigned>(band_rows), static_cast<unsigned>(frames),
                            static_cast<unsigned>(interleaved), offsets_stride / 2, skip,

@@ -276,12 +276,15 @@ def collision_scene(path, n=70_000, seed=5):
 def test_packed_ids_exchange_bitwise(gpu, tmp_path, monkeypatch):
     """70 000 triangles (one bit plane): ids that differ only above bit 15 cover the same pixels.
     Packed ids through the fake-device exchange (P = 2 and 3) and the one-rank RCCL exchange, and
-    int32 ids (SRT_EXCHANGE_IDS=32), give the one-device frame bit for bit, random offsets."""
+    int32 ids (SRT_EXCHANGE_IDS=32), give the one-device frame bit for bit; random offsets, uniform in
+    some tiles (whose offset the packed ids carry: their shading reads no per-pixel offsets)."""
     from simpleraytracer_amd.engine import FrameEngine
 
     path = collision_scene(tmp_path / "collide.srt")
     w, h = 256, 144
     inputs = np.random.default_rng(9).random((1, h, w, 2), dtype=np.float32)
+    inputs[0, :48] = 0.5  # regular tiles: three tile rows, and one tile column below them
+    inputs[0, 48:, 128:192] = 0.25
     ref = torch_render(path, w, h, inputs[0])
     ids = ref[..., 3].astype(np.int64)
     assert (ids >= 65536).sum() > 1000 and ((ids >= 0) & (ids < 70_000 - 65536)).sum() > 1000, \
@@ -297,7 +300,9 @@ def test_packed_ids_exchange_bitwise(gpu, tmp_path, monkeypatch):
                 for k in range(12):
                     assert np.array_equal(e.read_frame(k).view(np.uint32), ref.view(np.uint32)), (ids32, kw, k)
             if len(kw["devices"]) == 2:  # bands of 16-row tile rows: 5 and 4 of the 9, buffers of 80 rows
-                assert xb == (80 * 256 * 4 if ids32 else 80 * 256 * 2 + 80 * 4 * 8), xb  # 4 B or 2.125 B a pixel
+                # 4 B or 2.125 B a pixel, plus (packed) one 8-B tile offset per tile, padded to 256 B
+                packed = (80 * (256 * 2 + 4 * 8) + 5 * 4 * 8 + 255) // 256 * 256
+                assert xb == (80 * 256 * 4 if ids32 else packed), xb
 
 
 def test_packed_ids_mlinfer_gather_bitwise(gpu, tmp_path, monkeypatch):
