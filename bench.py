@@ -76,7 +76,8 @@ def parse():
     p.add_argument("--exchange", default="auto", choices=["auto", "alltoall", "rotating", "root", "share"],
                    help="bands: where frames are composited (module doc; auto: share at 2 GPUs, else alltoall)")
     p.add_argument("--share", type=int, default=0,
-                   help="share exchange: the compositor's tile rows per cycle of share + N - 1 (0: the library's 3)")
+                   help="share exchange: the compositor's tile rows per cycle of share + N - 1, a power of two "
+                        "(0: the library's 4)")
     p.add_argument("--rows", default="interleaved", choices=["interleaved", "contiguous"],
                    help="bands: each GPU's rows, the frame's 16-row tile rows dealt round-robin or one block")
     p.add_argument("--queues", type=int, default=int(os.environ.get("SRT_BENCH_QUEUES", "2")),
@@ -93,8 +94,8 @@ def parse():
     p.add_argument("--no-extras", action="store_true", help="only the main line (no secondary legs)")
     a = p.parse_args()
     if a.exchange == "auto":
-        # Two GPUs share one link per direction: the compositor traces 3 of every 4 tile rows itself,
-        # so a quarter of the frame's ids cross it (alltoall would send half, link-bound at ~64 GB/s).
+        # Two GPUs share one link per direction: the compositor traces 4 of every 5 tile rows itself,
+        # so a fifth of the frame's ids cross it (alltoall would send half, link-bound at ~64 GB/s).
         a.exchange = "share" if a.gpus == 2 else "alltoall"
     return a
 
@@ -603,7 +604,7 @@ def main():
                 xb = info["exchange_bytes_per_frame"]
                 px = max(1, (world - 1) * info["buffer_rows"] * W)
                 line["exchange"] = {"pattern": a.exchange, "transport": "RCCL" if info["rccl"] else "device copies",
-                                    "share": (a.share or 3) if a.exchange == "share" else None,
+                                    "share": (a.share or 4) if a.exchange == "share" else None,
                                     "payload": "packed hit ids (16 + k bits per pixel: a u16 plane and k bit planes, "
                                                "render.h PackedIds) or int32 ids; deferred shading on the compositor, "
                                                "whose own band is traced to RGBA in place",

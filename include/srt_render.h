@@ -175,7 +175,7 @@ typedef struct srt_engine_options {
     size_t launch;  /* frames per trace launch, <= 256 (0 = env SRT_LAUNCH_FRAMES, else 8 for whole
                        frames, 64 for bands over more than one device) */
     int flags;      /* SRT_ENGINE_* bits (0 = none) */
-    size_t share;   /* SRT_EXCHANGE_SHARE: the compositor's tile rows per cycle (0 = 3) */
+    size_t share;   /* SRT_EXCHANGE_SHARE: the compositor's tile rows per cycle, a power of two (0 = 4) */
 } srt_engine_options;
 
 /* 128-byte RCCL unique id for srtEngineCreateRank (call on one rank, share with the others). */

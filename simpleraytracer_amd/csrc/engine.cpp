@@ -485,9 +485,9 @@ void FrameEngine::Init(const Scene& scene, const std::vector<int>& devices) {
         if (!m_opt.interleaved) {
             throw std::runtime_error("FrameEngine: the share exchange needs interleaved rows");
         }
-        m_share = m_opt.share == 0 ? 3 : m_opt.share;
-        if (m_share > 64) {
-            throw std::runtime_error("FrameEngine: share must be 1..64 tile rows per cycle");
+        m_share = m_opt.share == 0 ? 4 : m_opt.share;
+        if (m_share > 64 || (m_share & (m_share - 1)) != 0) {
+            throw std::runtime_error("FrameEngine: share must be a power of two, 1..64 tile rows per cycle");
         }
     } else if (m_opt.exchange == EngineOptions::kShare) {
         m_opt.exchange = EngineOptions::kRotatingGather;  // one device: nothing to share

@@ -19,7 +19,7 @@
 //                   k + P - 1 tile rows of the batch's frames itself -- straight into its frames as
 //                   RGBA -- while every other device traces one tile row of each such cycle and
 //                   sends its ids: the exchange and the deferred shading shrink to (P - 1) / (k + P - 1)
-//                   of a frame (P = 2, k = 3: a quarter). With Q a multiple of P every queue keeps
+//                   of a frame (P = 2, k = 4: a fifth). With Q a multiple of P every queue keeps
 //                   one role (compositor, or one sender class) and so one band shape.
 // P == 1 traces and shades in one kernel (RGBA), no exchange.
 // Split "frames": every device renders whole frames of its own (no exchange; weak scaling).
@@ -73,7 +73,7 @@ struct EngineOptions {
     // one-rank RCCL communicator (ncclSend / ncclRecv to self) -- the real exchange, its waits and
     // its abort path on a one-GPU box. Frames are bit-identical to the fused trace.
     bool rccl_self = false;
-    // kShare: the compositor's tile rows per cycle (k above; 0: 3).
+    // kShare: the compositor's tile rows per cycle (k above, a power of two; 0: 4).
     std::size_t share = 0;
 };
 

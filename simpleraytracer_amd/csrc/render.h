@@ -109,9 +109,14 @@ struct PackedIds {
 PackedIds PackedIdLayout(int planes, std::size_t rows, std::size_t width);
 
 // A band row pattern (BandArgs::row_interleave) taking `group` consecutive tile rows out of every
-// `interleave`: interleave in the low 16 bits, group - 1 above (group 1: the plain interleave).
+// `interleave`, group a power of two (the kernels split a band's tile row index with a shift and a
+// mask, no division): interleave in the low 16 bits, log2(group) above (group 1: the plain interleave).
 constexpr std::size_t RowPattern(std::size_t interleave, std::size_t group) {
-    return interleave | (group - 1) << 16;
+    std::size_t log2 = 0;
+    while ((std::size_t{2} << log2) <= group) {
+        ++log2;
+    }
+    return interleave | log2 << 16;
 }
 // Frame row of band-local row `local` (BandArgs::row_interleave: an interleave or a RowPattern).
 inline std::size_t BandFrameRow(std::size_t row_begin, std::size_t pattern, std::size_t local);
@@ -144,9 +149,10 @@ constexpr int kCullTileCols = 64;
 constexpr int kCullTileRows = SRT_TILE_ROWS;
 
 inline std::size_t BandFrameRow(std::size_t row_begin, std::size_t pattern, std::size_t local) {
-    const std::size_t interleave = pattern & 0xFFFFu, group = (pattern >> 16) + 1;
+    const std::size_t interleave = pattern & 0xFFFFu, log2 = pattern >> 16;
     const std::size_t lt = local / kCullTileRows;
-    return row_begin + (lt / group * interleave + lt % group) * kCullTileRows + local % kCullTileRows;
+    return row_begin + ((lt >> log2) * interleave + (lt & ((std::size_t{1} << log2) - 1))) * kCullTileRows +
+           local % kCullTileRows;
 }
 constexpr int kMaxBatch = 8;          // frames of a batched cull launch with its parameters as kernel arguments
 constexpr int kMaxBoundTiles = 2048;  // binning needs tiles_x + tiles_y <= this

@@ -488,14 +488,12 @@ __device__ __forceinline__ void TestTriangle(Rays<R>& s, const Record& q, unsign
 // pattern; `box` receives the rays' (fx, fy) bounding box (NaN positions drop out: a ray
 // Frame row of band-local row `local`: the band holds frame tile rows row_begin / kCullTileRows
 // + k * interleave, k = 0, 1, ... (interleave 1: the contiguous rows row_begin + local).
-// (interleave: a plain interleave, or a RowPattern taking `group` consecutive tile rows of every
-// interleave: render.h BandFrameRow.)
+// (interleave: a plain interleave, or a RowPattern taking 2^g consecutive tile rows of every
+// interleave: render.h BandFrameRow; a shift and a mask, no branch.)
 __device__ __forceinline__ int FrameRow(int row_begin, int interleave, int local) {
-    const int lt = local / kCullTileRows, group = (interleave >> 16) + 1;
-    if (group == 1) {
-        return row_begin + local + lt * kCullTileRows * (interleave - 1);
-    }
-    return row_begin + (lt / group * (interleave & 0xFFFF) + lt % group) * kCullTileRows + local % kCullTileRows;
+    const int lt = local / kCullTileRows, g = interleave >> 16;
+    return row_begin + ((lt >> g) * (interleave & 0xFFFF) + (lt & ((1 << g) - 1))) * kCullTileRows +
+           local % kCullTileRows;
 }
 
 // with a NaN position fails every test).
@@ -3677,8 +3675,8 @@ bool BandFits(std::size_t row_begin, std::size_t row_count, std::size_t interlea
     if (row_count == 0) {
         return true;
     }
-    const std::size_t every = interleave & 0xFFFFu, group = (interleave >> 16) + 1;
-    if (every == 0 || group > every || (interleave > 1 && row_begin % kCullTileRows != 0)) {
+    const std::size_t every = interleave & 0xFFFFu, log2 = interleave >> 16;
+    if (every == 0 || log2 > 6 || (std::size_t{1} << log2) > every || (interleave > 1 && row_begin % kCullTileRows != 0)) {
         return false;
     }
     return BandFrameRow(row_begin, interleave, row_count - 1) < height;  // earlier tile rows are full

@@ -67,7 +67,7 @@ def test_interleaved_partition_covers_frame_once(h, p):
 
 
 @pytest.mark.parametrize("h", [1, 31, 230, 1080, 2160])
-@pytest.mark.parametrize("p,share", [(2, 1), (2, 3), (2, 7), (3, 3), (8, 2)])
+@pytest.mark.parametrize("p,share", [(2, 1), (2, 4), (2, 8), (3, 2), (8, 2), (3, 4)])
 def test_share_partition_covers_frame_once(h, p, share):
     """The share exchange (engine.h kShare): for every compositor the ranks' rows partition the frame;
     the compositor's rows follow the grouped row pattern the kernels use (render.h BandFrameRow with
@@ -79,8 +79,8 @@ def test_share_partition_covers_frame_once(h, p, share):
         parts = [share_frame_rows(h, p, share, r, c) for r in range(p)]
         assert np.array_equal(np.sort(np.concatenate(parts)), np.arange(h))
         local = np.arange(len(parts[c]))
-        lt = local // TILE_ROWS
-        assert np.array_equal((lt // share * classes + lt % share) * TILE_ROWS + local % TILE_ROWS, parts[c])
+        lt, g = local // TILE_ROWS, share.bit_length() - 1  # the kernels' shift and mask (share = 2^g)
+        assert np.array_equal(((lt >> g) * classes + (lt & (share - 1))) * TILE_ROWS + local % TILE_ROWS, parts[c])
         for r in range(p):
             if r != c and len(parts[r]):
                 cls = share + (r - c - 1) % p

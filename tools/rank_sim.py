@@ -44,7 +44,7 @@ def main():
     ap.add_argument("--triangles", type=int, default=100_000)
     ap.add_argument("--rows", default="interleaved")
     ap.add_argument("--exchange", default="alltoall", choices=["alltoall", "rotating", "share"])
-    ap.add_argument("--share", type=int, default=0, help="share exchange: the compositor's tile rows per cycle (0: 3)")
+    ap.add_argument("--share", type=int, default=0, help="share exchange: the compositor's tile rows per cycle, a power of two (0: 4)")
     ap.add_argument("--launch", type=int, default=0, help="frames per trace launch (0: library default)")
     ap.add_argument("--all-ranks", action="store_true", help="every rank (default: ranks 0, P/2 and P-1)")
     ap.add_argument("--link-gbs", type=float, default=64.0, help="ASSUMED xGMI rate per direction (module doc)")
