@@ -755,6 +755,40 @@ void FrameEngine::SetInputs(const float* host_offsets, std::size_t count) {
         }
     }
     m_inputs = count;
+    if (m_opt.simulate && m_exchange) {
+        PrimeSimulation();
+    }
+}
+
+// Measurement (simulate: no peers, the exchange skipped): the compositor's deferred shading would
+// read receive buffers nobody fills -- whatever the allocation held, hit statistics unlike a frame's.
+// Fill them once, outside any run, with ids of this device's sender band (its trace of the first
+// input: the hit density, regular tiles and packed layout of a real band), so the simulated shading
+// does a real frame's work.
+void FrameEngine::PrimeSimulation() {
+    const std::size_t ri = m_share != 0 ? 1 : 0;
+    for (auto& dp : m_dev) {
+        Device& d = *dp;
+        DeviceGuard guard(d.device);
+        const std::size_t local = static_cast<std::size_t>(&dp - &m_dev[0]);
+        const Role& role = d.roles[ri];
+        for (Queue& q : d.queues) {
+            if (q.send == nullptr || q.recv == nullptr || role.rows == 0) {
+                continue;
+            }
+            const float* off = BandInput(local, 0, ri);
+            int* ids = Ids(q.send, 0);
+            q.scene->TraceBatch(&off, nullptr, &ids, 1, role.row_begin, role.rows, m_opt.variant, q.stream, role.pattern,
+                                m_id_planes);
+            const std::size_t slots = m_world * m_plan.MaxFramesPerCompositor();
+            for (std::size_t k = 0; k < slots; ++k) {
+                HipCheck(hipMemcpyAsync(q.recv + k * m_band_id_bytes, q.send, m_band_id_bytes, hipMemcpyDeviceToDevice,
+                                        q.stream),
+                         "hipMemcpyAsync(prime receive)");
+            }
+            HipCheck(hipStreamSynchronize(q.stream), "hipStreamSynchronize(prime)");
+        }
+    }
 }
 
 const float* FrameEngine::FullInput(std::size_t local, std::size_t k) const {

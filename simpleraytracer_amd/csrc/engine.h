@@ -191,6 +191,7 @@ private:
     const float* BandInput(std::size_t local, std::size_t k, std::size_t role = 0) const;
     const float* FullInput(std::size_t local, std::size_t k) const;
     std::size_t FrameFloats() const { return m_width * m_height * 2; }
+    void PrimeSimulation();  // simulate: receive buffers hold real ids (the sender role's band)
 
     EngineOptions m_opt;
     std::size_t m_width = 0, m_height = 0, m_world = 1, m_rank0 = 0;  // m_rank0: global index of local 0

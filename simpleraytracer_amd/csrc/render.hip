@@ -521,23 +521,29 @@ __device__ __forceinline__ bool GenerateRays(const TraceParams& p, int x, int y0
 
 // Shade: rgb = albedo * |cos(N, d)| for a hit, background for a miss; alpha carries
 // float(tri_id) (exact for ids < 2^24), -1 for a miss.
-__device__ __forceinline__ float4 ShadePixel(const TraceParams& p, float fx, float fy, int id) {
+// The shading of a hit from its triangle's shading record (nr, a) -- built once at scene load from
+// its vertices and albedo (static scene data, like the vertices themselves: 32 B, one line, instead of
+// 36 B of vertices, 12 B of albedo and a cross product and square root per pixel); the same
+// expressions, so the same bits. A miss (id < 0): the background.
+__device__ __forceinline__ float4 ShadeRecord(const TraceParams& p, float fx, float fy, int id, const float4& nr,
+                                              const float4& a) {
     if (id < 0) {
         return make_float4(p.bg[0], p.bg[1], p.bg[2], -1.f);
     }
     const float dx = fmaf(fy, p.dv[0], fmaf(fx, p.du[0], p.base[0]));
     const float dy = fmaf(fy, p.dv[1], fmaf(fx, p.du[1], p.base[1]));
     const float dz = fmaf(fy, p.dv[2], fmaf(fx, p.du[2], p.base[2]));
-    // The triangle's shading record, built once at scene load from its vertices and albedo (static
-    // scene data, like the vertices themselves: 32 B, one line, instead of 36 B of vertices, 12 B
-    // of albedo and a cross product and square root per pixel); the same expressions, so the same
-    // bits.
-    const float4* sr = p.shade + 2ull * static_cast<unsigned>(id);
-    const float4 nr = sr[0], a = sr[1];
     const float nd = Dot3(nr.x, nr.y, nr.z, dx, dy, dz);
     const float dd = Dot3(dx, dy, dz, dx, dy, dz);
     const float cosv = fminf(fabsf(nd) / (nr.w * sqrtf(dd)), 1.f);
     return make_float4(a.x * cosv, a.y * cosv, a.z * cosv, static_cast<float>(id));
+}
+__device__ __forceinline__ float4 ShadePixel(const TraceParams& p, float fx, float fy, int id) {
+    if (id < 0) {
+        return ShadeRecord(p, fx, fy, id, float4{}, float4{});
+    }
+    const float4* sr = p.shade + 2ull * static_cast<unsigned>(id);
+    return ShadeRecord(p, fx, fy, id, sr[0], sr[1]);
 }
 
 // Store one pixel of the band: its shaded RGBA (one float4, 1 KiB contiguous per wave
@@ -620,6 +626,9 @@ __device__ __forceinline__ void ShadeAndStore(const TraceParams& p, int x, int y
 // their id and offset loads in flight together (no per-pixel division for x and y: the former 1-D
 // grid's 64-bit i % W and i / W were most of the kernel's instructions).
 constexpr int kShadeThreads = 128;
+#ifndef SRT_SHADE_TILE_OFFSETS
+#define SRT_SHADE_TILE_OFFSETS 1  // shade regular tiles from the packed ids' tile offsets
+#endif
 #ifndef SRT_SHADE_ROWS
 #define SRT_SHADE_ROWS 4
 #endif
@@ -633,13 +642,13 @@ __device__ __forceinline__ unsigned long long HitKey(float t, int id) {
 
 // PACKED: the ids arrive as packed band frames (render.h PackedIds, frame_bytes each, the same
 // band-major order): a pixel's code is its u16 plus p.id_planes bits from the bit planes.
-template <bool PACKED>
+template <bool PACKED, int PLANES>
 __global__ __launch_bounds__(kShadeThreads) void ShadeIdsKernel(TraceParams p, const void* __restrict__ ids_v,
                                                                 unsigned band_rows, unsigned frames,
                                                                 unsigned interleaved, size_t offsets_stride,
                                                                 unsigned skip_band, unsigned own_bands,
                                                                 size_t frame_bytes) {
-    using IdT = std::conditional_t<PACKED, unsigned, int>;
+    static_assert(kShadeThreads % kWave == 0, "a wave's lanes are one 64-column tile column");
     const int* __restrict__ ids = static_cast<const int*>(ids_v);
     const unsigned char* __restrict__ packed = static_cast<const unsigned char*>(ids_v);
     const int x = static_cast<int>(blockIdx.x * kShadeThreads + threadIdx.x);
@@ -649,12 +658,12 @@ __global__ __launch_bounds__(kShadeThreads) void ShadeIdsKernel(TraceParams p, c
     const int y0 = static_cast<int>(blockIdx.y) * kShadeRows;
     const unsigned g = blockIdx.z;
     const size_t pixels = static_cast<size_t>(p.width) * p.row_count;
-    IdT id[kShadeRows];
-    float2 o[kShadeRows];
-    float2 tile_o[kShadeRows];  // packed ids: the row's tile offset (NaN: read the pixel's own)
-    // Rows of band skip_band, or of bands [0, own_bands) (whose ids the buffer does not hold: it starts
-    // at band own_bands): the compositor traced them as RGBA already.
-    bool mine[kShadeRows];
+    // Three phases with no control flow between the loads of different rows, so every row's loads are
+    // in flight together: (1) every row's id (packed: its u16, bit-plane words and tile offset --
+    // wave-uniform addresses), (2) every hit's sample offset (irregular tiles) and every row's shading
+    // record, (3) shade and store. (The per-row form waited on each row's planes and each hit's record
+    // in turn: 3 round trips per row.) Rows of the compositor's own bands load from a valid slot and
+    // are not stored.
     // Interleaved bands: the thread's rows lie in one tile row (kShadeRows divides it), so in one
     // band (the divisions once per thread, not per row).
     static_assert(kCullTileRows % kShadeRows == 0, "a thread's rows share a tile row");
@@ -662,6 +671,12 @@ __global__ __launch_bounds__(kShadeThreads) void ShadeIdsKernel(TraceParams p, c
     const unsigned band0 = interleaved != 0u ? t0 % interleaved : 0u;
     const unsigned local0 =
         interleaved != 0u ? t0 / interleaved * kCullTileRows + static_cast<unsigned>(y0) % kCullTileRows : 0u;
+    const int tcol = __builtin_amdgcn_readfirstlane(x >> 6);  // the wave's tile column
+    unsigned code[kShadeRows];
+    float2 tile_o[kShadeRows];  // packed ids: the row's tile offset (NaN: every pixel reads its own)
+    // Rows of band skip_band, or of bands [0, own_bands) (whose ids the buffer does not hold: it starts
+    // at band own_bands): the compositor traced them as RGBA already.
+    bool mine[kShadeRows];
 #pragma unroll
     for (int r = 0; r < kShadeRows; ++r) {
         const int y = min(y0 + r, p.row_count - 1);
@@ -673,43 +688,42 @@ __global__ __launch_bounds__(kShadeThreads) void ShadeIdsKernel(TraceParams p, c
             band = static_cast<unsigned>(y) / band_rows;
             local = static_cast<unsigned>(y) - band * band_rows;
         }
-        tile_o[r] = make_float2(__builtin_nanf(""), __builtin_nanf(""));
         mine[r] = band == skip_band || band < own_bands;
-        band -= mine[r] ? 0u : own_bands;
+        const unsigned slot = mine[r] ? 0u : band - own_bands;
         if constexpr (PACKED) {
-            const unsigned char* frame = packed + (static_cast<size_t>(band) * frames + g) * frame_bytes;
+            const unsigned char* frame = packed + (static_cast<size_t>(slot) * frames + g) * frame_bytes;
             const unsigned char* row = PackedRow(frame, p, static_cast<int>(local));
-            unsigned code = 0u;
-            if (!mine[r]) {
-                // the tile's sample offset when every ray of it has that one (regular), else NaNs
-                tile_o[r] = *reinterpret_cast<const float2*>(PackedTileOffset(frame, p, static_cast<int>(local), x >> 6));
-                code = __builtin_nontemporal_load(reinterpret_cast<const unsigned short*>(row) + x);
-                const unsigned long long* bits = reinterpret_cast<const unsigned long long*>(row + p.id_low_row_bytes);
-                for (int j = 0; j < p.id_planes; ++j) {
-                    const unsigned long long w = bits[static_cast<size_t>(j) * p.id_words + (x >> 6)];
-                    code |= static_cast<unsigned>((w >> (x & 63)) & 1ull) << (16 + j);
-                }
+            code[r] = __builtin_nontemporal_load(reinterpret_cast<const unsigned short*>(row) + x);
+            const unsigned long long* bits = reinterpret_cast<const unsigned long long*>(row + p.id_low_row_bytes);
+#pragma unroll
+            for (int j = 0; j < PLANES; ++j) {
+                const unsigned long long w = bits[static_cast<size_t>(j) * p.id_words + tcol];
+                code[r] |= static_cast<unsigned>((w >> (x & 63)) & 1ull) << (16 + j);
             }
-            id[r] = code;
+            tile_o[r] = *reinterpret_cast<const float2*>(PackedTileOffset(frame, p, static_cast<int>(local), tcol));
         } else {
-            const size_t at = ((static_cast<size_t>(band) * frames + g) * band_rows + local) * p.width + x;
-            id[r] = mine[r] ? IdT{} : __builtin_nontemporal_load(ids + at);
+            const size_t at = ((static_cast<size_t>(slot) * frames + g) * band_rows + local) * p.width + x;
+            code[r] = static_cast<unsigned>(__builtin_nontemporal_load(ids + at));
+            tile_o[r] = make_float2(__builtin_nanf(""), __builtin_nanf(""));
         }
     }
-    // Only a hit needs its ray: a miss shades to the background whatever its sample offset, so the
-    // offsets of the miss pixels (72 % of C3's) are never loaded. A miss is -1, the packed miss code
-    // (all ones) or any id outside the scene.
-    // Packed ids carry each tile's offset when every ray of the tile has it: then no pixel of the
-    // tile reads its own (the trace computed those rays from the same offset, bit for bit).
+    // Only a hit needs its ray: a miss shades to the background whatever its sample offset (a miss is
+    // -1, the packed miss code -- all ones -- or any id outside the scene). A hit in a regular tile
+    // takes the tile's offset (the trace computed its ray from the same one, bit for bit); others
+    // read their own. Every row's shading record is loaded (a miss's: triangle 0's, unused).
     int hit[kShadeRows];
+    float2 o[kShadeRows];
+    float4 nr[kShadeRows], al[kShadeRows];
 #pragma unroll
     for (int r = 0; r < kShadeRows; ++r) {
         const int y = min(y0 + r, p.row_count - 1);
-        hit[r] = !mine[r] && static_cast<unsigned>(id[r]) < p.n ? static_cast<int>(id[r]) : -1;
-        const bool regular = PACKED && tile_o[r].x == tile_o[r].x;
-        o[r] = hit[r] < 0 ? float2{}
-               : regular  ? tile_o[r]
-                          : p.offsets[static_cast<size_t>(y) * p.width + x + g * offsets_stride];  // frame g's (stride 0: shared)
+        hit[r] = !mine[r] && code[r] < p.n ? static_cast<int>(code[r]) : -1;
+        const bool regular = PACKED && SRT_SHADE_TILE_OFFSETS && tile_o[r].x == tile_o[r].x;
+        o[r] = hit[r] < 0 || regular ? tile_o[r]
+                                     : p.offsets[static_cast<size_t>(y) * p.width + x + g * offsets_stride];  // frame g's (stride 0: shared)
+        const float4* sr = p.shade + 2ull * static_cast<unsigned>(max(hit[r], 0));
+        nr[r] = sr[0];
+        al[r] = sr[1];
     }
 #pragma unroll
     for (int r = 0; r < kShadeRows; ++r) {
@@ -717,7 +731,7 @@ __global__ __launch_bounds__(kShadeThreads) void ShadeIdsKernel(TraceParams p, c
         if (y < p.row_count && !mine[r]) {
             const float fx = (static_cast<float>(x) + o[r].x) / p.wf;
             const float fy = (static_cast<float>(FrameRow(p.row_begin, p.row_interleave, y)) + o[r].y) / p.hf;
-            const float4 v = ShadePixel(p, fx, fy, hit[r]);
+            const float4 v = ShadeRecord(p, fx, fy, hit[r], nr[r], al[r]);
             __builtin_nontemporal_store(F4{v.x, v.y, v.z, v.w},
                                         reinterpret_cast<F4*>(p.out + g * pixels + static_cast<size_t>(y) * p.width + x));
         }
@@ -2319,6 +2333,9 @@ std::size_t OrderLdsBytes(int tiles) { return static_cast<std::size_t>(tiles) * 
 #ifndef SRT_TRACE_OCC
 #define SRT_TRACE_OCC 6
 #endif
+#ifndef SRT_PLAN_EMPTY_TEST
+#define SRT_PLAN_EMPTY_TEST 1  // plan-only trace blocks test an empty tile against the large list's records
+#endif
 #ifndef SRT_SPLIT_ATOMIC
 #define SRT_SPLIT_ATOMIC 0  // 1: split parts merged with 64-bit atomic maxima in one slice per part (measured:
                             // one frame in flight, trace 20.4 -> 22.5 us; 8-frame launches unchanged)
@@ -2415,6 +2432,7 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(c
             oy = ti.oy;
             c_t = full ? 0u : cnt + large;
             list_len = full ? 0u : cnt;
+#if SRT_PLAN_EMPTY_TEST
             if (!full && cnt == 0u && large <= static_cast<unsigned>(kEmptyTest) && nchunks == 1u) {
                 const Box tb{ti.box.x, ti.box.y, ti.box.z, ti.box.w};  // the empty test (WorkOrderKernel)
                 CullRecord lr[kEmptyTest];
@@ -2435,6 +2453,13 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(c
                 }
                 flags |= may ? 0u : kItemEmpty;
             }
+#else
+            // (no candidates at all: every pixel misses; a tile with an empty list and a few large-list
+            // records walks them -- the record-testing form of this test measured slower in batched
+            // launches: code size)
+            flags |= !full && cnt == 0u && large == 0u && nchunks == 1u ? kItemEmpty : 0u;
+            (void)lid;
+#endif
         } else {
             flags = w0.w;
             ox = __uint_as_float(w1.x);
@@ -3784,12 +3809,25 @@ hipError_t LaunchShade(const float* d_vertices, const float* d_shade, const floa
         p.id_low_row_bytes = static_cast<unsigned>(lay.low_row_bytes);
         p.id_row_bytes = static_cast<unsigned>(lay.row_bytes);
         p.id_tile_row_bytes = static_cast<unsigned>(lay.tile_row_bytes);
-        hipLaunchKernelGGL(ShadeIdsKernel<true>, grid, dim3(kShadeThreads), 0, stream, p, ids,
-                           static_cast<unsigned>(band_rows), static_cast<unsigned>(frames),
-                           static_cast<unsigned>(interleaved), offsets_stride / 2, skip,
-                           static_cast<unsigned>(own_bands), lay.bytes);
+        const auto launch = [&](auto kernel) {
+            hipLaunchKernelGGL(kernel, grid, dim3(kShadeThreads), 0, stream, p, ids, static_cast<unsigned>(band_rows),
+                               static_cast<unsigned>(frames), static_cast<unsigned>(interleaved), offsets_stride / 2,
+                               skip, static_cast<unsigned>(own_bands), lay.bytes);
+        };
+        switch (band.id_planes) {  // the bit planes as a template argument: their loads unrolled
+            case 0: launch(ShadeIdsKernel<true, 0>); break;
+            case 1: launch(ShadeIdsKernel<true, 1>); break;
+            case 2: launch(ShadeIdsKernel<true, 2>); break;
+            case 3: launch(ShadeIdsKernel<true, 3>); break;
+            case 4: launch(ShadeIdsKernel<true, 4>); break;
+            case 5: launch(ShadeIdsKernel<true, 5>); break;
+            case 6: launch(ShadeIdsKernel<true, 6>); break;
+            case 7: launch(ShadeIdsKernel<true, 7>); break;
+            default: launch(ShadeIdsKernel<true, 8>); break;
+        }
+        static_assert(kMaxIdPlanes == 8, "one kernel per plane count");
     } else {
-        hipLaunchKernelGGL(ShadeIdsKernel<false>, grid, dim3(kShadeThreads), 0, stream, p, ids,
+        hipLaunchKernelGGL((ShadeIdsKernel<false, 0>), grid, dim3(kShadeThreads), 0, stream, p, ids,
                            static_cast<unsigned>(band_rows), static_cast<unsigned>(frames),
                            static_cast<unsigned>(interleaved), offsets_stride / 2, skip,
                            static_cast<unsigned>(own_bands), size_t{0});
