@@ -625,12 +625,15 @@ __device__ __forceinline__ void ShadeAndStore(const TraceParams& p, int x, int y
 // kShadeThreads columns x kShadeRows rows of frame g, a thread one column of kShadeRows rows with all
 // their id and offset loads in flight together (no per-pixel division for x and y: the former 1-D
 // grid's 64-bit i % W and i / W were most of the kernel's instructions).
-constexpr int kShadeThreads = 128;
+#ifndef SRT_SHADE_THREADS
+#define SRT_SHADE_THREADS 128
+#endif
+constexpr int kShadeThreads = SRT_SHADE_THREADS;
 #ifndef SRT_SHADE_TILE_OFFSETS
 #define SRT_SHADE_TILE_OFFSETS 1  // shade regular tiles from the packed ids' tile offsets
 #endif
 #ifndef SRT_SHADE_ROWS
-#define SRT_SHADE_ROWS 4
+#define SRT_SHADE_ROWS 1  // rows per thread (P = 8 rank, 64-frame launches: 1 / 2 / 4 rows 5.31-5.42 / 5.52-5.58 / 5.59-5.63 us per frame; the kernel alone 102 / 97 / 108 / 120 (8) / 162 (16) us)
 #endif
 constexpr int kShadeRows = SRT_SHADE_ROWS;
 
