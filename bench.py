@@ -12,9 +12,10 @@ Runs with or without a launcher:
 SRT_BENCH_ONE_DEVICE=1 puts every "device" on GPU 0 (single process: the bands are then exchanged
 by device copies -- the multi-GPU rehearsal on a one-GPU box).
 
-One step = one batch of --frames-per-step frames (default 64: a 64-frame sequence of the same
-view; 20 steps of 16 frames measured 97.5 Grays/s against 111.7 for long runs -- pipeline fill and
-drain -- so a step carries 64), each frame a complete pass of the hot path on device-resident inputs (SURVEY.md
+One step = one batch of --frames-per-step frames (default 256: a 256-frame sequence of the same
+view; a timed region of a few tens of ms loses a fixed ~1 ms start cost -- 20 steps of 64 frames
+read 114.6-116.5 Grays/s against 120.4 for 50 steps, 20 steps of 256 frames 122.4 -- so a step
+carries 256), each frame a complete pass of the hot path on device-resident inputs (SURVEY.md
 section 8 rows a9-a13): tile info, record setup and bins, the trace work list, the closest-hit
 trace (TraceCullKernel; bit-identical to brute force), shading and the
 framebuffer store. Nothing is cached across frames. Each GPU keeps --queues batches in flight.
@@ -62,10 +63,12 @@ METRIC = "Mrays/s at 1920x1080 on 100k-tri synthetic mesh"
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    # 50 steps x 64 frames = 3200 frames, ~60 ms timed at C3 on one GPU
+    # 50 steps x 256 frames = 12 800 frames, ~0.2 s timed at C3 on one GPU. (256 frames per step: a
+    # timed region of 20 steps of 64 frames, ~23 ms, lost ~5 % to a fixed start cost -- 114.6 / 116.5
+    # against 120.4 Grays/s at 50 steps; 20 steps of 128 / 256 frames: 120.3 / 122.4, profiles/r04/bench)
     p.add_argument("--steps", type=int, default=50, help="timed steps (batches of --frames-per-step frames)")
     p.add_argument("--warmup", type=int, default=2, help="untimed steps first")
-    p.add_argument("--frames-per-step", type=int, default=64,
+    p.add_argument("--frames-per-step", type=int, default=256,
                    help="frames per step = per batch (a multiple of the GPU count for the all-to-all exchange)")
     p.add_argument("--width", type=int, default=1920)
     p.add_argument("--height", type=int, default=1080)
