@@ -551,19 +551,21 @@ __device__ __forceinline__ float4 ShadePixel(const TraceParams& p, float fx, flo
 // Nontemporal (`global_store ... nt`): the frame never reads its framebuffer back, and streaming
 // it past the L2 keeps the cull records, lists and tables resident (+7.8 % at C3).
 typedef float F4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void StoreRgba(const TraceParams& p, int x, int y, const float4& v) {
+    const size_t rgba_at = p.out_frame_rows != 0
+                               ? static_cast<size_t>(FrameRow(p.row_begin, p.row_interleave, y)) * p.width + x
+                               : static_cast<size_t>(y) * p.width + x;
+    __builtin_nontemporal_store(F4{v.x, v.y, v.z, v.w}, reinterpret_cast<F4*>(p.out + rgba_at));
+}
 __device__ __forceinline__ void StorePixel(const TraceParams& p, int x, int y, float fx, float fy, int id) {
-    const size_t at = static_cast<size_t>(y) * p.width + x;
-    const size_t rgba_at =
-        p.out_frame_rows != 0 ? static_cast<size_t>(FrameRow(p.row_begin, p.row_interleave, y)) * p.width + x : at;
     if (p.out_ids != nullptr) {
-        __builtin_nontemporal_store(id, p.out_ids + at);
+        __builtin_nontemporal_store(id, p.out_ids + static_cast<size_t>(y) * p.width + x);
     } else {
 #ifdef SRT_EXP_NO_SHADE  // measurement builds only: store without shading
-        const float4 v = make_float4(fx, fy, 0.f, static_cast<float>(id));
+        StoreRgba(p, x, y, make_float4(fx, fy, 0.f, static_cast<float>(id)));
 #else
-        const float4 v = ShadePixel(p, fx, fy, id);
+        StoreRgba(p, x, y, ShadePixel(p, fx, fy, id));
 #endif
-        __builtin_nontemporal_store(F4{v.x, v.y, v.z, v.w}, reinterpret_cast<F4*>(p.out + rgba_at));
     }
 }
 
@@ -2848,14 +2850,33 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(c
                 StorePackedIds(p, tx, x, y, key[r] != ~0ull ? static_cast<int>(static_cast<unsigned>(key[r])) : -1);
             }
         }
+    } else if (x < p.width && p.out_ids != nullptr) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int y = y0 + r;
+            if (y < p.row_count) {
+                StorePixel(p, x, y, 0.f, 0.f, key[r] != ~0ull ? static_cast<int>(static_cast<unsigned>(key[r])) : -1);
+            }
+        }
     } else if (x < p.width) {
+        // RGBA: every row's shading record is loaded before any is used (a miss loads triangle 0's,
+        // unused), so the rows' loads share one round trip; per row in a branch they took one each,
+        // at the end of every block.
+        int id[R];
+        float4 nr[R], al[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            id[r] = key[r] != ~0ull ? static_cast<int>(static_cast<unsigned>(key[r])) : -1;
+            const float4* sr = p.shade + 2ull * static_cast<unsigned>(max(id[r], 0));
+            nr[r] = sr[0];
+            al[r] = sr[1];
+        }
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const int y = y0 + r;
             if (y < p.row_count) {
                 const float2 f = sh.fxy[wave * R + r][lane];
-                const int id = key[r] != ~0ull ? static_cast<int>(static_cast<unsigned>(key[r])) : -1;
-                StorePixel(p, x, y, f.x, f.y, id);
+                StoreRgba(p, x, y, ShadeRecord(p, f.x, f.y, id[r], nr[r], al[r]));
             }
         }
     }
