@@ -159,7 +159,8 @@ constexpr int kMaxBoundTiles = 2048;  // binning needs tiles_x + tiles_y <= this
 constexpr int kMaxBinTiles = 8192;    // and tiles_x * tiles_y <= this (bin kernel LDS histogram)
 
 // Work buffers of the cull variant's bins for one band shape (one allocation, carved by
-// CullBinLayout; it must be zero-filled when allocated: the counters reset themselves).
+// CullBinLayout; its first CullBinCounterBytes -- the counters, which reset themselves -- must be
+// zero-filled when it is carved up for a shape; every other byte is written before it is read).
 struct CullBins {
     const unsigned* order; // the scene's record ids in spatial order (DeviceScene; not in the buffer)
     const float* svertices;  // the scene's vertices in that order (DeviceScene; not in the buffer)
@@ -201,6 +202,7 @@ unsigned CullDescriptors(std::size_t tiles, std::size_t frames);
 
 // Bytes of the bin work buffer for n triangles and a band shape, and its carve-up.
 std::size_t CullBinBytes(std::uint64_t n, std::size_t width, std::size_t row_count);
+std::size_t CullBinCounterBytes(std::uint64_t n, std::size_t width, std::size_t row_count);  // the leading counters
 // parity: which of the slot's two count buffers this frame bins into (alternate per frame of a slot).
 CullBins CullBinLayout(void* base, std::uint64_t n, std::size_t width, std::size_t row_count, unsigned parity = 0);
 

@@ -551,6 +551,13 @@ __device__ __forceinline__ float4 ShadePixel(const TraceParams& p, float fx, flo
 // Nontemporal (`global_store ... nt`): the frame never reads its framebuffer back, and streaming
 // it past the L2 keeps the cull records, lists and tables resident (+7.8 % at C3).
 typedef float F4 __attribute__((ext_vector_type(4)));
+// A nontemporal float4 store the compiler cannot merge: after ShadeIdsKernel's grid was compacted
+// (its store no longer behind a row test), clang sank the two stores of ShadeRecord's hit / miss
+// paths into one and dropped `nt` on the way (97 -> 112 us per 8-frame launch of a P = 8
+// compositor; a branch-free ShadeRecord kept `nt` but shaded every miss: 104 us).
+__device__ __forceinline__ void StoreNontemporal(F4* at, F4 v) {
+    asm volatile("global_store_dwordx4 %0, %1, off nt" ::"v"(at), "v"(v) : "memory");
+}
 __device__ __forceinline__ void StoreRgba(const TraceParams& p, int x, int y, const float4& v) {
     const size_t rgba_at = p.out_frame_rows != 0
                                ? static_cast<size_t>(FrameRow(p.row_begin, p.row_interleave, y)) * p.width + x
@@ -645,6 +652,28 @@ __device__ __forceinline__ unsigned long long HitKey(float t, int id) {
     return (static_cast<unsigned long long>(__float_as_uint(t)) << 32) | static_cast<unsigned>(id);
 }
 
+#ifndef SRT_SHADE_COMPACT
+#define SRT_SHADE_COMPACT 1  // 0: a grid over every row of the frame (A/B)
+#endif
+// The frame row of the j-th row a shade call stores: the rows of bands [0, own) and of band `skip`
+// (~0u: none) left out. Interleaved (m = interleaved): band b is tile rows b, b + m, ... of 16 rows;
+// else band b is rows [b * band_rows, (b + 1) * band_rows). Past the last stored row the result is
+// past the frame only if the caller's grid (ShadeRowsLaunched) stops at the frame's rows.
+__host__ __device__ inline unsigned ShadeRowOf(unsigned j, unsigned band_rows, unsigned interleaved, unsigned skip,
+                                               unsigned own) {
+    const bool skips = skip != ~0u && skip >= own;
+    if (interleaved != 0u) {
+        const unsigned stored = interleaved - own - (skips && skip < interleaved ? 1u : 0u);  // bands per cycle
+        const unsigned tr = j / kCullTileRows;
+        unsigned band = own + tr % stored;
+        band += skips && band >= skip ? 1u : 0u;
+        return ((tr / stored) * interleaved + band) * kCullTileRows + j % kCullTileRows;
+    }
+    unsigned long long y = static_cast<unsigned long long>(own) * band_rows + j;
+    y += skips && y >= static_cast<unsigned long long>(skip) * band_rows ? band_rows : 0u;
+    return y > 0x7FFFFFFFull ? 0x7FFFFFFFu : static_cast<unsigned>(y);  // (an int row past the frame)
+}
+
 // PACKED: the ids arrive as packed band frames (render.h PackedIds, frame_bytes each, the same
 // band-major order): a pixel's code is its u16 plus p.id_planes bits from the bit planes.
 template <bool PACKED, int PLANES>
@@ -660,17 +689,29 @@ __global__ __launch_bounds__(kShadeThreads) void ShadeIdsKernel(TraceParams p, c
     if (x >= p.width) {
         return;
     }
-    const int y0 = static_cast<int>(blockIdx.y) * kShadeRows;
+    // The grid covers only the rows this call stores (ShadeRowsLaunched): blockIdx.y counts them,
+    // the bands [0, own_bands) and skip_band left out, and ShadeRowOf maps the count to its frame row.
+    // (A grid over every row, whose own-band threads loaded and stored nothing, cost a compositor of
+    // the share exchange -- a fifth of its rows shaded -- 7.3 us per frame, 2.6 us compacted.)
+    const unsigned j0 = blockIdx.y * kShadeRows;
+#if SRT_SHADE_COMPACT
+    const int y0 = static_cast<int>(ShadeRowOf(j0, band_rows, interleaved, skip_band, own_bands));
+#else
+    const int y0 = static_cast<int>(j0);
+#endif
+    if (y0 >= p.row_count) {
+        return;
+    }
     const unsigned g = blockIdx.z;
     const size_t pixels = static_cast<size_t>(p.width) * p.row_count;
     // Three phases with no control flow between the loads of different rows, so every row's loads are
     // in flight together: (1) every row's id (packed: its u16, bit-plane words and tile offset --
     // wave-uniform addresses), (2) every hit's sample offset (irregular tiles) and every row's shading
     // record, (3) shade and store. (The per-row form waited on each row's planes and each hit's record
-    // in turn: 3 round trips per row.) Rows of the compositor's own bands load from a valid slot and
-    // are not stored.
+    // in turn: 3 round trips per row.) A row past the frame loads from a valid one and is not stored.
     // Interleaved bands: the thread's rows lie in one tile row (kShadeRows divides it), so in one
-    // band (the divisions once per thread, not per row).
+    // band (the divisions once per thread, not per row); contiguous bands map row by row (a thread's
+    // rows may straddle skip_band).
     static_assert(kCullTileRows % kShadeRows == 0, "a thread's rows share a tile row");
     const unsigned t0 = static_cast<unsigned>(y0) / kCullTileRows;
     const unsigned band0 = interleaved != 0u ? t0 % interleaved : 0u;
@@ -679,22 +720,29 @@ __global__ __launch_bounds__(kShadeThreads) void ShadeIdsKernel(TraceParams p, c
     const int tcol = __builtin_amdgcn_readfirstlane(x >> 6);  // the wave's tile column
     unsigned code[kShadeRows];
     float2 tile_o[kShadeRows];  // packed ids: the row's tile offset (NaN: every pixel reads its own)
-    // Rows of band skip_band, or of bands [0, own_bands) (whose ids the buffer does not hold: it starts
-    // at band own_bands): the compositor traced them as RGBA already.
-    bool mine[kShadeRows];
+    int yr[kShadeRows];         // frame rows (>= row_count: past the frame, not stored)
+    // (The bands [0, own_bands) hold no ids in the buffer, which starts at band own_bands: the
+    // compositor traced them as RGBA already.)
 #pragma unroll
     for (int r = 0; r < kShadeRows; ++r) {
-        const int y = min(y0 + r, p.row_count - 1);
+        yr[r] = interleaved != 0u || r == 0 || !SRT_SHADE_COMPACT
+                    ? y0 + r
+                    : static_cast<int>(ShadeRowOf(j0 + r, band_rows, interleaved, skip_band, own_bands));
+        const bool past = yr[r] >= p.row_count;
+        const unsigned y = static_cast<unsigned>(past ? y0 : yr[r]);
         unsigned band, local;
         if (interleaved != 0u) {
             band = band0;
-            local = local0 + static_cast<unsigned>(y - y0);
+            local = local0 + (y - static_cast<unsigned>(y0));
         } else {
-            band = static_cast<unsigned>(y) / band_rows;
-            local = static_cast<unsigned>(y) - band * band_rows;
+            band = y / band_rows;
+            local = y - band * band_rows;
         }
-        mine[r] = band == skip_band || band < own_bands;
-        const unsigned slot = mine[r] ? 0u : band - own_bands;
+        if (!SRT_SHADE_COMPACT && (band == skip_band || band < own_bands)) {
+            yr[r] = p.row_count;  // (full grid: the compositor's own rows are not stored)
+            band = own_bands;
+        }
+        const unsigned slot = band - own_bands;
         if constexpr (PACKED) {
             const unsigned char* frame = packed + (static_cast<size_t>(slot) * frames + g) * frame_bytes;
             const unsigned char* row = PackedRow(frame, p, static_cast<int>(local));
@@ -721,8 +769,8 @@ __global__ __launch_bounds__(kShadeThreads) void ShadeIdsKernel(TraceParams p, c
     float4 nr[kShadeRows], al[kShadeRows];
 #pragma unroll
     for (int r = 0; r < kShadeRows; ++r) {
-        const int y = min(y0 + r, p.row_count - 1);
-        hit[r] = !mine[r] && code[r] < p.n ? static_cast<int>(code[r]) : -1;
+        const int y = yr[r] < p.row_count ? yr[r] : y0;
+        hit[r] = code[r] < p.n ? static_cast<int>(code[r]) : -1;
         const bool regular = PACKED && SRT_SHADE_TILE_OFFSETS && tile_o[r].x == tile_o[r].x;
         o[r] = hit[r] < 0 || regular ? tile_o[r]
                                      : p.offsets[static_cast<size_t>(y) * p.width + x + g * offsets_stride];  // frame g's (stride 0: shared)
@@ -732,13 +780,13 @@ __global__ __launch_bounds__(kShadeThreads) void ShadeIdsKernel(TraceParams p, c
     }
 #pragma unroll
     for (int r = 0; r < kShadeRows; ++r) {
-        const int y = y0 + r;
-        if (y < p.row_count && !mine[r]) {
+        const int y = yr[r];
+        if (y < p.row_count) {
             const float fx = (static_cast<float>(x) + o[r].x) / p.wf;
             const float fy = (static_cast<float>(FrameRow(p.row_begin, p.row_interleave, y)) + o[r].y) / p.hf;
             const float4 v = ShadeRecord(p, fx, fy, hit[r], nr[r], al[r]);
-            __builtin_nontemporal_store(F4{v.x, v.y, v.z, v.w},
-                                        reinterpret_cast<F4*>(p.out + g * pixels + static_cast<size_t>(y) * p.width + x));
+            StoreNontemporal(reinterpret_cast<F4*>(p.out + g * pixels + static_cast<size_t>(y) * p.width + x),
+                             F4{v.x, v.y, v.z, v.w});
         }
     }
 }
@@ -3404,6 +3452,17 @@ std::size_t CullBinBytes(std::uint64_t n, std::size_t width, std::size_t row_cou
     return z.info + z.counts + z.lists + z.large + z.work + z.work_count + z.arrive + z.split_keys + z.range_tag;
 }
 
+#ifndef SRT_COUNTERS_FIRST
+#define SRT_COUNTERS_FIRST 1  // 0: the former carve-up (tile info first) and whole slots zeroed (A/B)
+#endif
+std::size_t CullBinCounterBytes(std::uint64_t n, std::size_t width, std::size_t row_count) {
+    const BinSizes z = CullBinSizes(n, width, row_count);
+    if (!SRT_COUNTERS_FIRST) {
+        return CullBinBytes(n, width, row_count);
+    }
+    return z.counts + z.work_count + z.arrive + z.range_tag + (SRT_SPLIT_ATOMIC ? z.split_keys : 0);  // (atomic maxima)
+}
+
 CullBins CullBinLayout(void* base, std::uint64_t n, std::size_t width, std::size_t row_count, unsigned parity) {
     const BinSizes z = CullBinSizes(n, width, row_count);
     unsigned char* w = static_cast<unsigned char*>(base);
@@ -3413,15 +3472,27 @@ CullBins CullBinLayout(void* base, std::uint64_t n, std::size_t width, std::size
         w += bytes;
         return at;
     };
-    b.tile_info = take(z.info);
+    // The counters first (CullBinCounterBytes: the only bytes that must start zero), then the buffers
+    // every frame writes before it reads them.
+    if (!SRT_COUNTERS_FIRST) {
+        b.tile_info = take(z.info);
+    }
     unsigned* counts = reinterpret_cast<unsigned*>(take(z.counts));
+    b.work_count = reinterpret_cast<unsigned*>(take(z.work_count));
+    b.arrive = reinterpret_cast<unsigned*>(take(z.arrive));
+    b.range_tag = reinterpret_cast<unsigned*>(take(z.range_tag));
+    if (SRT_SPLIT_ATOMIC) {
+        b.split_keys = take(z.split_keys);  // slices merged by atomic maxima start zero too
+    }
+    if (SRT_COUNTERS_FIRST) {
+        b.tile_info = take(z.info);
+    }
     b.lists = reinterpret_cast<unsigned*>(take(z.lists));
     b.large_list = reinterpret_cast<unsigned*>(take(z.large));
     b.work = take(z.work);
-    b.work_count = reinterpret_cast<unsigned*>(take(z.work_count));
-    b.arrive = reinterpret_cast<unsigned*>(take(z.arrive));
-    b.split_keys = take(z.split_keys);
-    b.range_tag = reinterpret_cast<unsigned*>(take(z.range_tag));
+    if (!SRT_SPLIT_ATOMIC) {
+        b.split_keys = take(z.split_keys);
+    }
     b.tiles = CullTiles(width, row_count);
     b.counts = counts + (parity & 1u) * (b.tiles + 1);
     b.counts_next = counts + ((parity & 1u) ^ 1u) * (b.tiles + 1);
@@ -3785,6 +3856,22 @@ hipError_t LaunchShadeTable(const float* d_vertices, const float* d_albedo, std:
     return hipGetLastError();
 }
 
+// The rows of the shade grid (ShadeRowOf's j): every row of the bands a call stores, for interleaved
+// bands rounded up to whole cycles of tile rows (the threads past the frame return).
+static std::size_t ShadeRowsLaunched(std::size_t row_count, std::size_t band_rows, std::size_t interleaved,
+                                     unsigned skip, std::size_t own) {
+    const bool skips = skip != ~0u && skip >= own;
+    if (interleaved != 0) {
+        const std::size_t dropped = std::min(own, interleaved) + (skips && skip < interleaved ? 1 : 0);
+        const std::size_t stored = interleaved - std::min(dropped, interleaved);
+        const std::size_t tile_rows = (row_count + kCullTileRows - 1) / kCullTileRows;
+        return (tile_rows + interleaved - 1) / interleaved * stored * kCullTileRows;
+    }
+    const std::size_t own_rows = std::min(own * band_rows, row_count);
+    const std::size_t skip_rows = skips ? std::min(band_rows, row_count - std::min<std::size_t>(skip * band_rows, row_count)) : 0;
+    return row_count - own_rows - skip_rows;
+}
+
 hipError_t LaunchShade(const float* d_vertices, const float* d_shade, const float* d_edges, std::uint64_t n,
                        const Frame& frame, const float background[3], const BandArgs& band, hipStream_t stream,
                        std::size_t frames, std::size_t band_rows, std::size_t interleaved,
@@ -3822,10 +3909,15 @@ hipError_t LaunchShade(const float* d_vertices, const float* d_shade, const floa
     if (band.id_planes >= 0 && (band.id_planes > kMaxIdPlanes || IdPlanes(n) != band.id_planes)) {
         return hipErrorInvalidValue;
     }
-    const dim3 grid(static_cast<unsigned>((band.width + kShadeThreads - 1) / kShadeThreads),
-                    static_cast<unsigned>((band.row_count + kShadeRows - 1) / kShadeRows), static_cast<unsigned>(frames));
-    const void* ids = band.ids;
     const unsigned skip = skip_band < 0 ? 0xFFFFFFFFu : static_cast<unsigned>(skip_band);
+    const std::size_t stored =
+        SRT_SHADE_COMPACT ? ShadeRowsLaunched(band.row_count, band_rows, interleaved, skip, own_bands) : band.row_count;
+    if (stored == 0) {
+        return hipSuccess;
+    }
+    const dim3 grid(static_cast<unsigned>((band.width + kShadeThreads - 1) / kShadeThreads),
+                    static_cast<unsigned>((stored + kShadeRows - 1) / kShadeRows), static_cast<unsigned>(frames));
+    const void* ids = band.ids;
     if (band.id_planes >= 0) {
         const PackedIds lay = PackedIdLayout(band.id_planes, band_rows, band.width);
         p.id_planes = band.id_planes;

@@ -297,8 +297,12 @@ void DeviceScene::EnsureCullWork(std::size_t slots, std::size_t row_count, hipSt
         m_cull_zeroed = 0;
     }
     if (slots > m_cull_zeroed) {
-        HipCheck(hipMemsetAsync(m_cull_work + m_cull_zeroed * bytes, 0, (slots - m_cull_zeroed) * bytes, stream),
-                 "hipMemsetAsync(cull work)");
+        // Only each slot's leading counters (render.h CullBins): a band shape that alternates on one
+        // scene (the share exchange's roles on one frame queue) re-carves every batch, and zeroing
+        // whole slots (~30 MB each, mostly split-key slices) cost 0.4-0.5 ms per 64-frame batch.
+        HipCheck(hipMemset2DAsync(m_cull_work + m_cull_zeroed * bytes, bytes, 0,
+                                  CullBinCounterBytes(m_n, m_width, row_count), slots - m_cull_zeroed, stream),
+                 "hipMemset2DAsync(cull work)");
         m_cull_state.resize(std::max(m_cull_state.size(), slots));
         for (std::size_t k = m_cull_zeroed; k < slots; ++k) {
             m_cull_state[k] = CullSlotState{};  // zeroed: no plan
