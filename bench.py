@@ -77,10 +77,10 @@ def parse():
     p.add_argument("--variant", default=os.environ.get("SRT_BENCH_VARIANT", "cull"), choices=list(KERNEL_NAMES))
     p.add_argument("--mode", default="bands", choices=["bands", "frames"], help="multi-GPU split (module doc)")
     p.add_argument("--exchange", default="auto", choices=["auto", "alltoall", "rotating", "root", "share"],
-                   help="bands: where frames are composited (module doc; auto: share at 2 GPUs, else alltoall)")
+                   help="bands: where frames are composited (module doc; auto: share)")
     p.add_argument("--share", type=int, default=0,
                    help="share exchange: the compositor's tile rows per cycle of share + N - 1, a power of two "
-                        "(0: the library's 4)")
+                        "(0: the library's srtShareAuto, 32 at 1080p)")
     p.add_argument("--rows", default="interleaved", choices=["interleaved", "contiguous"],
                    help="bands: each GPU's rows, the frame's 16-row tile rows dealt round-robin or one block")
     p.add_argument("--queues", type=int, default=int(os.environ.get("SRT_BENCH_QUEUES", "2")),
@@ -97,9 +97,12 @@ def parse():
     p.add_argument("--no-extras", action="store_true", help="only the main line (no secondary legs)")
     a = p.parse_args()
     if a.exchange == "auto":
-        # Two GPUs share one link per direction: the compositor traces 4 of every 5 tile rows itself,
-        # so a fifth of the frame's ids cross it (alltoall would send half, link-bound at ~64 GB/s).
-        a.exchange = "share" if a.gpus == 2 else "alltoall"
+        # share: batch b's compositor traces k of every k + N - 1 tile rows itself, fused with the
+        # shading (k = 32 at 1080p), and the others one each: fewer rows take the ids path (trace to
+        # ids, exchange, deferred shading) than under alltoall, which sends (N - 1) / N of every
+        # frame. Rank simulation, us of GPU time per frame: N = 2 10.9 vs 14.6
+        # (alltoall, link-bound besides), N = 4 6.7 vs 8.2, N = 8 4.4 vs 5.3.
+        a.exchange = "share"
     return a
 
 
@@ -604,10 +607,13 @@ def main():
             line["ranks_stages_ms"] = [{"rank": i, "prepare": round(s[1], 5), "bin": round(s[2], 5),
                                         "trace_kernel": round(s[3], 5)} for i, s in enumerate(ranks_stages)]
             if band:
+                from simpleraytracer_amd import _native
+
+                share_k = a.share or _native.lib().srtShareAuto(H, world)
                 xb = info["exchange_bytes_per_frame"]
                 px = max(1, (world - 1) * info["buffer_rows"] * W)
                 line["exchange"] = {"pattern": a.exchange, "transport": "RCCL" if info["rccl"] else "device copies",
-                                    "share": (a.share or 4) if a.exchange == "share" else None,
+                                    "share": share_k if a.exchange == "share" else None,
                                     "payload": "packed hit ids (16 + k bits per pixel: a u16 plane and k bit planes, "
                                                "render.h PackedIds) or int32 ids; deferred shading on the compositor, "
                                                "whose own band is traced to RGBA in place",

@@ -175,7 +175,7 @@ typedef struct srt_engine_options {
     size_t launch;  /* frames per trace launch, <= 256 (0 = env SRT_LAUNCH_FRAMES, else 8 for whole
                        frames, 64 for bands over more than one device) */
     int flags;      /* SRT_ENGINE_* bits (0 = none) */
-    size_t share;   /* SRT_EXCHANGE_SHARE: the compositor's tile rows per cycle, a power of two (0 = 4) */
+    size_t share;   /* SRT_EXCHANGE_SHARE: the compositor's tile rows per cycle, a power of two (0 = srtShareAuto) */
 } srt_engine_options;
 
 /* 128-byte RCCL unique id for srtEngineCreateRank (call on one rank, share with the others). */
@@ -217,6 +217,9 @@ ML_API_ENTRY int srtEngineStageTimesBatch(srt_engine engine, size_t local, size_
  * it took and how often the abort hook ran. */
 ML_API_ENTRY int srtEnginePoolSelfTest(size_t workers, size_t failing, int mode, double timeout_s, double* elapsed_s,
                                        int* abort_calls, char* msg, size_t msg_size);
+/* SRT_EXCHANGE_SHARE's default tile rows per cycle for a frame of `height` rows over `devices`
+ * devices: the largest power of two <= 32 with share + devices - 1 <= ceil(height / 16). */
+ML_API_ENTRY size_t srtShareAuto(size_t height, size_t devices);
 /* Shape of the run: devices in the job, local devices, rows of local device 0's band, rows of every
  * band buffer, whether the exchange uses RCCL, exchanged bytes per frame (bands, all devices). */
 ML_API_ENTRY int srtEngineInfo(srt_engine engine, size_t* devices, size_t* local_devices, size_t* band_rows,

@@ -50,6 +50,16 @@ def interleaved_frame_rows(height: int, world: int, rank: int):
                            for t in range(rank, tiles, world)] or [np.zeros(0, np.int64)]).astype(np.int64)
 
 
+def share_auto(height: int, world: int) -> int:
+    """The share exchange's default tile rows per cycle (csrc/engine.cpp ShareAuto, srtShareAuto): the
+    largest power of two <= 32 whose cycle of share + P - 1 tile rows fits the frame."""
+    tiles = (height + TILE_ROWS - 1) // TILE_ROWS
+    k = 32
+    while k > 1 and k + world - 1 > tiles:
+        k //= 2
+    return k
+
+
 def share_frame_rows(height: int, world: int, share: int, rank: int, compositor: int):
     """The frame rows ``rank`` traces, in band order, for a frame composited on ``compositor`` under
     the share exchange (csrc/engine.h kShare): the frame's tile rows in cycles of share + P - 1

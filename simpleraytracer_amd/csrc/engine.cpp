@@ -45,6 +45,22 @@ bool GatherByCopies(const std::vector<int>& devices) {
 }  // namespace
 
 // ---------------------------------------------------------------------------------------------
+// The share exchange's default k: the largest power of two <= 32 whose cycle of k + P - 1 tile rows
+// still fits the frame (every sender traces at least one tile row). Measured (tools/rank_sim.py,
+// 1080p, balanced batch counts; profiles/r04/share/): the larger k, the fewer rows take the ids path
+// (trace to ids, exchange, deferred shading) instead of the fused trace-and-shade, so the GPU time
+// per frame falls -- P = 2: k = 4 12.0, 16 10.9 us; P = 4: 8.2 all-to-all, 6.7 at k = 32; P = 8:
+// 5.3 all-to-all, 4.6 at 16, 4.4 at 32 -- and so do the bytes on the links. The price is latency:
+// the compositor traces k / (k + P - 1) of each of its frames.
+std::size_t ShareAuto(std::size_t height, std::size_t world) {
+    const std::size_t tile_rows = (height + kCullTileRows - 1) / kCullTileRows;
+    std::size_t k = 32;
+    while (k > 1 && k + world - 1 > tile_rows) {
+        k /= 2;
+    }
+    return k;
+}
+
 // Band split and exchange plan (pure index math; shared with the host self-test).
 
 BandSplit BandSplit::Make(std::size_t height, std::size_t bands, bool interleaved) {
@@ -485,7 +501,7 @@ void FrameEngine::Init(const Scene& scene, const std::vector<int>& devices) {
         if (!m_opt.interleaved) {
             throw std::runtime_error("FrameEngine: the share exchange needs interleaved rows");
         }
-        m_share = m_opt.share == 0 ? 4 : m_opt.share;
+        m_share = m_opt.share == 0 ? ShareAuto(m_height, m_world) : m_opt.share;
         if (m_share > 64 || (m_share & (m_share - 1)) != 0) {
             throw std::runtime_error("FrameEngine: share must be a power of two, 1..64 tile rows per cycle");
         }

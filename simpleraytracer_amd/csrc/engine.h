@@ -19,8 +19,9 @@
 //                   k + P - 1 tile rows of the batch's frames itself -- straight into its frames as
 //                   RGBA -- while every other device traces one tile row of each such cycle and
 //                   sends its ids: the exchange and the deferred shading shrink to (P - 1) / (k + P - 1)
-//                   of a frame (P = 2, k = 4: a fifth). With Q a multiple of P every queue keeps
-//                   one role (compositor, or one sender class) and so one band shape.
+//                   of a frame (1080p: k = 32, P = 2: 1/33; P = 8: 7/39). With Q a multiple of P
+//                   every queue keeps one role (compositor, or one sender class) and so one band
+//                   shape; otherwise a queue's band shape changes with its batches' roles.
 // P == 1 traces and shades in one kernel (RGBA), no exchange.
 // Split "frames": every device renders whole frames of its own (no exchange; weak scaling).
 //
@@ -73,9 +74,13 @@ struct EngineOptions {
     // one-rank RCCL communicator (ncclSend / ncclRecv to self) -- the real exchange, its waits and
     // its abort path on a one-GPU box. Frames are bit-identical to the fused trace.
     bool rccl_self = false;
-    // kShare: the compositor's tile rows per cycle (k above, a power of two; 0: 4).
+    // kShare: the compositor's tile rows per cycle (k above, a power of two; 0: ShareAuto).
     std::size_t share = 0;
 };
+
+// kShare's default k for an H-row frame over P devices: the largest power of two <= 32 with
+// k + P - 1 <= the frame's tile rows (engine.cpp).
+std::size_t ShareAuto(std::size_t height, std::size_t world);
 
 // Row bands of an H-row frame over P devices (interleaved or contiguous), the layout every
 // exchange path and the shading kernel agree on.

@@ -52,8 +52,8 @@ class FrameEngine:
                  launch: int = 0, rccl_self: bool = False, share: int = 0, _handle=None):
         """rccl_self (one device, tests): the bands path with the frame's ids sent to itself over a
         one-rank RCCL communicator -- the real exchange, its waits and its abort path.
-        exchange="share": the compositor traces `share` (a power of two; 0: 4) of every share + P - 1 tile
-        rows itself."""
+        exchange="share": the compositor traces `share` (a power of two; 0: srtShareAuto, 32 at 1080p)
+        of every share + P - 1 tile rows itself."""
         self._lib = _native.lib()
         self.width, self.height, self.batch = width, height, batch
         self.options = {"variant": variant, "queues": queues, "batch": batch, "rows": rows, "exchange": exchange,

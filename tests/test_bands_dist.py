@@ -66,8 +66,27 @@ def test_interleaved_partition_covers_frame_once(h, p):
             assert np.array_equal(begin + local + local // TILE_ROWS * TILE_ROWS * (p - 1), fr)
 
 
+@pytest.mark.parametrize("h", [1, 16, 17, 100, 230, 500, 1080, 2160])
+@pytest.mark.parametrize("p", [1, 2, 3, 4, 8, 16])
+def test_share_auto_matches_library(h, p):
+    """The default k of the share exchange (engine.cpp ShareAuto through srtShareAuto; no device) is
+    the largest power of two <= 32 whose cycle of k + P - 1 tile rows fits the frame (at least 1),
+    and the Python restatement (bands.share_auto) agrees."""
+    from simpleraytracer_amd import _native
+    from simpleraytracer_amd.bands import share_auto
+
+    k = _native.lib().srtShareAuto(h, p)
+    tiles = -(-h // TILE_ROWS)
+    assert k == share_auto(h, p)
+    assert k in (1, 2, 4, 8, 16, 32)
+    assert k == 1 or k + p - 1 <= tiles
+    assert k == 32 or 2 * k + p - 1 > tiles
+    if (h, p) in ((1080, 2), (1080, 8), (2160, 8)):
+        assert k == 32
+
+
 @pytest.mark.parametrize("h", [1, 31, 230, 1080, 2160])
-@pytest.mark.parametrize("p,share", [(2, 1), (2, 4), (2, 8), (3, 2), (8, 2), (3, 4)])
+@pytest.mark.parametrize("p,share", [(2, 1), (2, 4), (2, 8), (3, 2), (8, 2), (3, 4), (2, 32), (8, 32), (4, 16)])
 def test_share_partition_covers_frame_once(h, p, share):
     """The share exchange (engine.h kShare): for every compositor the ranks' rows partition the frame;
     the compositor's rows follow the grouped row pattern the kernels use (render.h BandFrameRow with

@@ -60,13 +60,15 @@ def test_engine_fake_devices_bitwise(gpu, scenes, p, rows, exchange):
         assert bad == 0 and checked == 2 * F
 
 
-@pytest.mark.parametrize("p,share,queues", [(2, 4, 2), (2, 1, 2), (2, 8, 3), (3, 2, 2), (8, 2, 4)])
+@pytest.mark.parametrize("p,share,queues", [(2, 4, 2), (2, 1, 2), (2, 8, 3), (3, 2, 2), (8, 2, 4), (4, 8, 2),
+                                             (2, 16, 2), (2, 0, 2), (8, 0, 2)])
 def test_engine_fake_devices_share_bitwise(gpu, scenes, p, share, queues):
     """The share exchange (the compositor of a batch traces `share` of every share + P - 1 tile rows
     itself, straight into its frames; every other device one tile row per cycle, sent as ids and
     shaded there): distinct inputs per frame, every frame of the last batches equal to a one-device
     render of its input, bit for bit -- also with a queue count that makes a queue change roles
-    (and so band shapes) from batch to batch."""
+    (and so band shapes) from batch to batch. share = 16 at P = 2: a cycle of 17 tile rows is longer
+    than the frame, so the sender's band is empty; share = 0: the library's choice (srtShareAuto)."""
     w, h, F = 150, 230, 4  # 15 tile rows: cycles of share + P - 1 end in a partial one
     inputs = random_inputs(2 * F, h, w, seed=11 + p)
     refs = [torch_render(scenes["soup2k"], w, h, inputs[k]) for k in range(2 * F)]
@@ -128,13 +130,34 @@ def test_engine_c3_bands_of_8_bitwise(gpu, scenes):
     assert_parity(got, ref, rows=rows)
 
 
-def test_engine_c3_share_of_2_bitwise(gpu, scenes):
-    """The headline frame over 2 fake devices with the share exchange (each compositor traces 4 of
-    every 5 tile rows itself, the other device the fifth): every frame equals the one-device frame,
-    and a fifth of the frame's ids cross the exchange."""
+@pytest.mark.parametrize("p", [2, 8])
+def test_engine_c3_share_bitwise(gpu, scenes, p):
+    """The headline frame over P fake devices with the share exchange at the library's k (32 at 1080p:
+    each compositor traces 32 of every 32 + P - 1 tile rows itself, every other device one): every
+    frame equals the one-device frame, and P - 1 of every 32 + P - 1 tile rows cross the exchange."""
     w, h = 1920, 1080
     inputs = np.full((1, h, w, 2), 0.5, np.float32)
-    with engine(scenes["soup100k"], w, h, devices=[0, 0], batch=16, queues=2, exchange="share") as e:
+    with engine(scenes["soup100k"], w, h, devices=[0] * p, batch=16, queues=2, exchange="share") as e:
+        e.set_inputs(inputs)
+        e.run(p + 1)
+        assert e.verify()[0] == 0
+        got = e.read_frame(16 * p + 3)  # a frame of the last batch (resident on its compositor)
+        xb = e.info()["exchange_bytes_per_frame"]
+    classes = 32 + p - 1
+    sent = (p - 1) * -(-68 // classes)  # the senders' band buffers: ceil(68 / classes) tile rows each
+    assert xb <= sent * 16 * w * 2.2, xb
+    rows = np.arange(5, 1080, 90)
+    ref = oracle_render(scenes["soup100k"], w, h, row_begin=5, row_count=1075, row_step=90)
+    assert_parity(got, ref, rows=rows)
+
+
+def test_engine_c3_share_of_2_bitwise(gpu, scenes):
+    """The headline frame over 2 fake devices with the share exchange at k = 4 (each compositor traces
+    4 of every 5 tile rows itself, the other device the fifth): every frame equals the one-device
+    frame, and a fifth of the frame's ids cross the exchange."""
+    w, h = 1920, 1080
+    inputs = np.full((1, h, w, 2), 0.5, np.float32)
+    with engine(scenes["soup100k"], w, h, devices=[0, 0], batch=16, queues=2, exchange="share", share=4) as e:
         e.set_inputs(inputs)
         e.run(3)
         assert e.verify() == (0, 8)

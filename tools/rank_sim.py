@@ -17,7 +17,7 @@ RCCL point-to-point reaching ~85 % of it gives ~64). A sweep of rates is printed
 ceiling = W x H / max(slowest rank's GPU time, link time) -- the exchange overlaps the other queue's
 compute (its RCCL kernels' CU time is inside neither figure).
 
-    python tools/rank_sim.py [--ranks 1,2,4,8] [--steps 30] [--batch 64] [--queues 2] [--link-gbs 64]
+    python tools/rank_sim.py [--ranks 1,2,4,8] [--steps 32] [--batch 64] [--queues 2] [--link-gbs 64]
 """
 from __future__ import annotations
 
@@ -35,16 +35,19 @@ sys.path.insert(0, REPO)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ranks", default="1,2,4,8")
-    ap.add_argument("--steps", type=int, default=30)
-    ap.add_argument("--warmup", type=int, default=2)
+    # batches (warmup and timed) multiples of 8: under the rotating compositor roles (share,
+    # rotating) every rank then composites the same number of batches at P = 2, 4, 8
+    ap.add_argument("--steps", type=int, default=32)
+    ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--queues", type=int, default=2)
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--triangles", type=int, default=100_000)
     ap.add_argument("--rows", default="interleaved")
-    ap.add_argument("--exchange", default="alltoall", choices=["alltoall", "rotating", "share"])
-    ap.add_argument("--share", type=int, default=0, help="share exchange: the compositor's tile rows per cycle, a power of two (0: 4)")
+    ap.add_argument("--exchange", default="share", choices=["alltoall", "rotating", "share"])
+    ap.add_argument("--share", type=int, default=0,
+                    help="share exchange: the compositor's tile rows per cycle, a power of two (0: srtShareAuto)")
     ap.add_argument("--launch", type=int, default=0, help="frames per trace launch (0: library default)")
     ap.add_argument("--all-ranks", action="store_true", help="every rank (default: ranks 0, P/2 and P-1)")
     ap.add_argument("--link-gbs", type=float, default=64.0, help="ASSUMED xGMI rate per direction (module doc)")
