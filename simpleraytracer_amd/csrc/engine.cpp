@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <chrono>
 #include <condition_variable>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <exception>
@@ -104,7 +105,6 @@ std::size_t BandSplit::FrameRow(std::size_t band, std::size_t local) const {
 std::size_t ExchangePlan::Compositor(std::size_t batch_index, std::size_t f) const {
     switch (exchange) {
         case EngineOptions::kRotatingGather:
-        case EngineOptions::kShare:
             return batch_index % bands;
         case EngineOptions::kRootGather:
             return 0;
@@ -114,13 +114,12 @@ std::size_t ExchangePlan::Compositor(std::size_t batch_index, std::size_t f) con
 }
 
 std::size_t ExchangePlan::Slot(std::size_t f) const {
-    return exchange == EngineOptions::kAllToAll ? f / bands : f;
+    return PerFrame() ? f / bands : f;
 }
 
 std::size_t ExchangePlan::FramesFor(std::size_t batch_index, std::size_t compositor) const {
     switch (exchange) {
         case EngineOptions::kRotatingGather:
-        case EngineOptions::kShare:
             return compositor == batch_index % bands ? batch : 0;
         case EngineOptions::kRootGather:
             return compositor == 0 ? batch : 0;
@@ -130,7 +129,7 @@ std::size_t ExchangePlan::FramesFor(std::size_t batch_index, std::size_t composi
 }
 
 std::size_t ExchangePlan::MaxFramesPerCompositor() const {
-    return exchange == EngineOptions::kAllToAll ? (batch + bands - 1) / bands : batch;
+    return PerFrame() ? (batch + bands - 1) / bands : batch;
 }
 
 std::size_t ExchangePlan::RecvSlot(std::size_t c, std::size_t p) const {
@@ -141,7 +140,7 @@ namespace {
 // Band frame index of compositor c's slot j in a device's send buffer: all-to-all keeps one region
 // of MaxFramesPerCompositor frames per compositor; the gathers send everything to one.
 std::size_t SendFrames(const ExchangePlan& plan, std::size_t c, std::size_t j) {
-    const std::size_t region = plan.exchange == EngineOptions::kAllToAll ? c * plan.MaxFramesPerCompositor() : 0;
+    const std::size_t region = plan.PerFrame() ? c * plan.MaxFramesPerCompositor() : 0;
     return region + j;
 }
 std::size_t SendPixels(const ExchangePlan& plan, std::size_t c, std::size_t j, std::size_t band_pixels) {
@@ -172,7 +171,7 @@ std::vector<std::vector<int>> ExchangeOnHost(const BandSplit& split, const Excha
         // d of c's receive buffer: the device path's ncclSend / ncclRecv pairs, as copies.
         for (std::size_t d = 0; d < P; ++d) {
             const std::size_t send_frames =
-                plan.exchange == EngineOptions::kAllToAll ? P * plan.MaxFramesPerCompositor() : F;
+                plan.PerFrame() ? P * plan.MaxFramesPerCompositor() : F;
             std::vector<int> send(send_frames * band_pixels, -1);
             for (std::size_t f = 0; f < F; ++f) {
                 const std::size_t cf = plan.Compositor(batch_index, f);
@@ -559,11 +558,11 @@ void FrameEngine::Init(const Scene& scene, const std::vector<int>& devices) {
     }
 }
 
-std::size_t FrameEngine::RoleOf(std::size_t local, std::size_t b) const {
+std::size_t FrameEngine::RoleOf(std::size_t local, std::size_t c) const {
     if (m_share == 0) {
         return 0;
     }
-    const std::size_t c = m_plan.Compositor(b, 0), self = m_dev[local]->band;
+    const std::size_t self = m_dev[local]->band;
     return self == c ? 0 : 1 + m_plan.RecvSlot(c, self);
 }
 
@@ -583,9 +582,8 @@ void FrameEngine::AllocateQueues() {
             q.scene = std::make_unique<DeviceScene>(*m_scene, d.device);
             q.scene->Prepare(m_width, m_height, q.stream);
             if (m_exchange) {
-                const std::size_t send_frames = m_plan.exchange == EngineOptions::kAllToAll
-                                                    ? m_world * m_plan.MaxFramesPerCompositor()
-                                                    : m_plan.batch;
+                const std::size_t send_frames =
+                    m_plan.PerFrame() ? m_world * m_plan.MaxFramesPerCompositor() : m_plan.batch;
                 q.send = DeviceAlloc<unsigned char>(send_frames * m_band_id_bytes, "hipMalloc(send ids)");
                 q.recv = DeviceAlloc<unsigned char>(m_world * m_plan.MaxFramesPerCompositor() * m_band_id_bytes,
                                           "hipMalloc(receive ids)");
@@ -725,7 +723,7 @@ void FrameEngine::SetInputs(const float* host_offsets, std::size_t count) {
     }
     CheckUsable();
     if (m_exchange && count > 1 &&
-        (count % m_opt.batch != 0 || (m_plan.exchange == EngineOptions::kAllToAll && m_opt.batch % m_world != 0))) {
+        (count % m_opt.batch != 0 || (m_plan.PerFrame() && m_opt.batch % m_world != 0))) {
         throw std::runtime_error("SetInputs: with bands over " + std::to_string(m_world) + " devices, " +
                                  std::to_string(count) + " inputs need a multiple of the batch (" +
                                  std::to_string(m_opt.batch) + ") and a batch divisible by the devices");
@@ -862,7 +860,13 @@ void FrameEngine::TracePhase(std::size_t local, std::size_t b) {
         }
         return;
     }
-    const std::size_t self = d.band, ri = RoleOf(local, b);
+    const std::size_t self = d.band;
+    if (m_share != 0) {
+        TraceShare(local, b);
+        HipCheck(hipEventRecord(q.traced, q.stream), "hipEventRecord(traced)");
+        return;
+    }
+    const std::size_t ri = 0;
     const Role& role = d.roles[ri];
     if (role.rows != 0) {
         for (std::size_t f0 = 0; f0 < F; f0 += L) {
@@ -883,6 +887,69 @@ void FrameEngine::TracePhase(std::size_t local, std::size_t b) {
         }
     }
     HipCheck(hipEventRecord(q.traced, q.stream), "hipEventRecord(traced)");
+}
+
+// kShare: frame f's compositor c = f % P traces its own class rows (role 0) straight into the frame
+// as RGBA; every other device traces its one class of f (role 1 + RecvSlot(c, self)) as packed ids
+// into c's region of the send buffer. The sender classes of a batch differ only in their first row,
+// so they share launches (per-frame row_begin), grouped by their row count (classes at the end of
+// the frame may hold one tile row fewer).
+void FrameEngine::TraceShare(std::size_t local, std::size_t b) {
+    Device& d = *m_dev[local];
+    Queue& q = d.queues[b % m_opt.queues];
+    const std::size_t F = m_opt.batch, k0 = b * F, L = m_opt.launch, self = d.band;
+    const std::size_t frame_floats4 = m_width * m_height * 4;
+    std::vector<const float*> offs;
+    std::vector<float*> rgba;
+    std::vector<int*> ids;
+    std::vector<std::size_t> begins;
+    const auto flush = [&](const Role& role, bool own) {
+        for (std::size_t f0 = 0; f0 < offs.size(); f0 += L) {
+            const std::size_t n = std::min(L, offs.size() - f0);
+            q.scene->TraceBatch(offs.data() + f0, own ? rgba.data() + f0 : nullptr, own ? nullptr : ids.data() + f0, n,
+                                role.row_begin, role.rows, m_opt.variant, q.stream, role.pattern, m_id_planes, true,
+                                own ? nullptr : begins.data() + f0);
+        }
+        offs.clear();
+        rgba.clear();
+        ids.clear();
+        begins.clear();
+    };
+    // role 0: the frames composited here
+    const Role& mine = d.roles[0];
+    for (std::size_t f = self; f < F && mine.rows != 0; f += m_world) {
+        offs.push_back(BandInput(local, k0 + f, 0));
+        rgba.push_back(q.rgba + m_plan.Slot(f) * frame_floats4);
+    }
+    flush(mine, true);
+    // the sender classes, by row count
+    std::vector<std::size_t> counts;
+    for (std::size_t ri = 1; ri < d.roles.size(); ++ri) {
+        if (d.roles[ri].rows != 0 && std::find(counts.begin(), counts.end(), d.roles[ri].rows) == counts.end()) {
+            counts.push_back(d.roles[ri].rows);
+        }
+    }
+    for (const std::size_t rows : counts) {
+        const Role* shape = nullptr;
+        for (std::size_t f = 0; f < F; ++f) {
+            const std::size_t c = m_plan.Compositor(b, f);
+            if (c == self) {
+                continue;
+            }
+            const std::size_t ri = RoleOf(local, c);
+            const Role& role = d.roles[ri];
+            if (role.rows != rows) {
+                continue;
+            }
+            shape = &role;
+            offs.push_back(BandInput(local, k0 + f, ri));
+            ids.push_back(Ids(q.send, SendFrames(m_plan, c, m_plan.Slot(f))));
+            begins.push_back(role.row_begin);
+        }
+        if (shape != nullptr) {
+            flush(*shape, false);
+        }
+    }
 }
 
 void FrameEngine::ExchangePhase(std::size_t local, std::size_t b) {
@@ -964,7 +1031,7 @@ void FrameEngine::ShadePhase(std::size_t local, std::size_t b) {
     }
     // The compositor's frames in slot order read evenly strided inputs (SetInputs' condition).
     const std::size_t F = m_opt.batch, k0 = b * F;
-    const bool a2a = m_plan.exchange == EngineOptions::kAllToAll;
+    const bool a2a = m_plan.PerFrame();
     const std::size_t first = k0 + (a2a ? self : 0);
     const std::size_t stride = m_inputs == 1 ? 0 : (a2a ? m_world : 1) * FrameFloats();
     // The compositor's own rows are RGBA already: its band (all-to-all, rotating), or the first
@@ -1004,10 +1071,26 @@ void FrameEngine::RunWorker(std::size_t local, std::size_t b0, std::size_t batch
         if (m_ctl->abort.load(std::memory_order_relaxed)) {
             throw std::runtime_error("run aborted: another device's worker failed");
         }
+        static const bool probe = std::getenv("SRT_PROBE_HOST") != nullptr;
+        const auto tp0 = std::chrono::steady_clock::now();
         TracePhase(local, b);
+        const auto tp1 = std::chrono::steady_clock::now();
+        if (probe) {
+            const double us = std::chrono::duration<double, std::micro>(tp1 - tp0).count();
+            if (us > 300.0) {
+                std::fprintf(stderr, "[probe] batch %zu trace phase %.0f us\n", b, us);
+            }
+        }
         if (m_exchange) {
             if (m_opt.simulate) {
                 ShadePhase(local, b);  // no peers: the exchange is skipped (measurement)
+                if (probe) {
+                    const double us =
+                        std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tp1).count();
+                    if (us > 300.0) {
+                        std::fprintf(stderr, "[probe] batch %zu shade phase %.0f us\n", b, us);
+                    }
+                }
             } else if (m_copy) {
                 Barrier();  // every device's trace of batch b is enqueued (its `traced` recorded)
                 CopyPhase(local, b);

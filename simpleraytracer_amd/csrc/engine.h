@@ -15,13 +15,13 @@
 //                   directed xGMI link carries 1/P of the payload;
 //   kRotatingGather the whole batch is gathered to device b % P (one gather per batch);
 //   kRootGather     everything to device 0;
-//   kShare          batch b is composited on device c = b % P, which traces `share` (k) of every
-//                   k + P - 1 tile rows of the batch's frames itself -- straight into its frames as
-//                   RGBA -- while every other device traces one tile row of each such cycle and
-//                   sends its ids: the exchange and the deferred shading shrink to (P - 1) / (k + P - 1)
-//                   of a frame (1080p: k = 32, P = 2: 1/33; P = 8: 7/39). With Q a multiple of P
-//                   every queue keeps one role (compositor, or one sender class) and so one band
-//                   shape; otherwise a queue's band shape changes with its batches' roles.
+//   kShare          frame f of a batch is composited on device c = f % P (as all-to-all), which
+//                   traces `share` (k) of every k + P - 1 tile rows of it itself -- straight into the
+//                   frame as RGBA -- while every other device traces one tile row of each such cycle
+//                   (its class) and sends its ids: the exchange and the deferred shading shrink to
+//                   (P - 1) / (k + P - 1) of a frame (1080p: k = 32, P = 2: 1/33; P = 8: 7/39), and
+//                   every batch loads every device alike (a compositor per batch, rotating, left
+//                   the other devices idle behind its long trace unless P batches were in flight).
 // P == 1 traces and shades in one kernel (RGBA), no exchange.
 // Split "frames": every device renders whole frames of its own (no exchange; weak scaling).
 //
@@ -105,6 +105,8 @@ struct ExchangePlan {
     std::size_t MaxFramesPerCompositor() const;
     // Slot of device p's ids in compositor c's receive buffer (kShare: the senders in class order).
     std::size_t RecvSlot(std::size_t c, std::size_t p) const;
+    // Frames of a batch dealt to compositors round-robin (kAllToAll, kShare), not whole batches.
+    bool PerFrame() const { return exchange == EngineOptions::kAllToAll || exchange == EngineOptions::kShare; }
 };
 
 // Host self-test of the exchange (no device): band_ids[d] = device d's traced ids of the batch's F
@@ -186,8 +188,9 @@ private:
         std::size_t row_begin = 0, rows = 0, pattern = 1;
         std::size_t input = 0;  // rows of the earlier roles (Device::band_in: per role, inputs x rows x W x 2)
     };
-    std::size_t RoleOf(std::size_t local, std::size_t b) const;
+    std::size_t RoleOf(std::size_t local, std::size_t compositor) const;  // role for a frame composited there
     void TracePhase(std::size_t local, std::size_t b);
+    void TraceShare(std::size_t local, std::size_t b);  // kShare's trace: each frame in its compositor's pattern
     void ExchangePhase(std::size_t local, std::size_t b);  // RCCL: inside a group
     void CopyPhase(std::size_t local, std::size_t b);      // device-copy exchange
     void ShadePhase(std::size_t local, std::size_t b);

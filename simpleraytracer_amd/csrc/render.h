@@ -252,14 +252,21 @@ struct CullFrame {
 };
 // Frames of one launch whose parameters travel in a device table instead of the kernel
 // arguments (count > kMaxBatch): `device` and `host` (page-locked) of CullTableBytes(frames) bytes
-// each, caller-owned. LaunchCullFrames fills `host` and copies it to `device` on the stream; the
-// caller must not rewrite `host` before that copy has executed (an event after the call), and the
-// stream order keeps the device copy alive for the launches that read it.
+// each, caller-owned. LaunchCullFrames fills `host` and uploads it to `device` on the stream; the
+// caller must not rewrite `host` before that upload has executed (`uploaded`), and the stream order
+// keeps the device copy alive for the launches that read it.
 constexpr int kMaxTableFrames = 256;
 struct CullTable {
     void* device;
     void* host;
     std::size_t frames;  // capacity
+    // `host` as the device sees it (page-locked, mapped): the upload is then a small kernel reading it
+    // over the bus instead of hipMemcpyAsync, which on ROCm 7.2 blocked the calling thread for 7 ms
+    // at the first upload from some staging buffers (measured: tools/first_run_probe.py). Null: copy.
+    const void* host_device = nullptr;
+    // Recorded on the stream once the upload has read `host` (null: not recorded): the caller may
+    // rewrite `host` after it, while the frames' launches still run.
+    hipEvent_t uploaded = nullptr;
 };
 std::size_t CullTableBytes(std::size_t frames);
 

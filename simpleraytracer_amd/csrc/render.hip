@@ -3634,6 +3634,16 @@ TableLayout MakeTableLayout(std::size_t frames) {
 
 std::size_t CullTableBytes(std::size_t frames) { return MakeTableLayout(frames).bytes; }
 
+// The parameter table's upload: one 16-B word per thread, read from page-locked host memory over the
+// bus (one round trip for the whole table) and stored to the device table.
+__global__ __launch_bounds__(256) void UploadTableKernel(const uint4* __restrict__ host, uint4* __restrict__ dev,
+                                                         size_t n16) {
+    const size_t i = static_cast<size_t>(blockIdx.x) * 256 + threadIdx.x;
+    if (i < n16) {
+        dev[i] = host[i];
+    }
+}
+
 hipError_t LaunchCullFrames(const CullFrame* frames, std::size_t count, std::uint64_t n, const float* d_vertices,
                             const float* d_shade, const Frame& frame, const float background[3], const unsigned* d_rank,
                             hipStream_t stream, const StageEvents* events, const CullTable* table) {
@@ -3665,10 +3675,10 @@ hipError_t LaunchCullFrames(const CullFrame* frames, std::size_t count, std::uin
         const CullFrame& f = frames[i];
         if (f.bins == nullptr || f.edges == nullptr || f.bins->order == nullptr || f.bins->svertices == nullptr ||
             f.band.width != band0.width ||
-            f.band.row_count != band0.row_count || f.band.row_begin != band0.row_begin ||
+            f.band.row_count != band0.row_count || (fused && f.band.row_begin != band0.row_begin) ||
             f.band.row_interleave != band0.row_interleave ||
             f.band.height != band0.height || f.bins->descs != frames[0].bins->descs) {
-            return hipErrorInvalidValue;  // one band shape per batch
+            return hipErrorInvalidValue;  // one band shape per batch (its first row may differ per frame)
         }
         tp[i] = MakeTraceParams(f.edges, n, d_vertices, d_shade, frame, background, f.band);
         if (f.bins->tiles != tp[i].tiles) {
@@ -3702,9 +3712,21 @@ hipError_t LaunchCullFrames(const CullFrame* frames, std::size_t count, std::uin
         return hipGetLastError();
     }
     // One upload of every frame's parameters, then the same four launches reading them from it.
-    const hipError_t e = hipMemcpyAsync(table->device, table->host, lay.bytes, hipMemcpyHostToDevice, stream);
-    if (e != hipSuccess) {
-        return e;
+    if (table->host_device != nullptr) {
+        const std::size_t n16 = (lay.bytes + 15) / 16;
+        hipLaunchKernelGGL(UploadTableKernel, dim3(static_cast<unsigned>((n16 + 255) / 256)), dim3(256), 0, stream,
+                           static_cast<const uint4*>(table->host_device), static_cast<uint4*>(table->device), n16);
+    } else {
+        const hipError_t e = hipMemcpyAsync(table->device, table->host, lay.bytes, hipMemcpyHostToDevice, stream);
+        if (e != hipSuccess) {
+            return e;
+        }
+    }
+    if (table->uploaded != nullptr) {
+        const hipError_t e = hipEventRecord(table->uploaded, stream);
+        if (e != hipSuccess) {
+            return e;
+        }
     }
     unsigned char* dev = static_cast<unsigned char*>(table->device);
     const PrepareBinTable pt{(ConstantPtr<PrepareBinParams>)(dev + lay.prep)};

@@ -167,7 +167,9 @@ DeviceScene::~DeviceScene() {
     (void)hipFree(m_order);
     (void)hipFree(m_rank);
     (void)hipFree(m_svertices);
-    (void)hipFree(m_cull_work);
+    for (CullArena& a : m_arenas) {
+        (void)hipFree(a.work);
+    }
     (void)hipFree(m_bvh);
     for (hipEvent_t e : m_events) {
         (void)hipEventDestroy(e);
@@ -198,7 +200,7 @@ void DeviceScene::Prepare(std::size_t width, std::size_t height, hipStream_t str
         throw std::runtime_error("Prepare: frame dimensions must be non-zero");
     }
     if (width != m_width || height != m_height) {
-        DropPlans(m_cull_state.size());  // (a plan is scheduling only; a new shape deserves a new one)
+        DropPlans(~std::size_t{0});  // (a plan is scheduling only; a new shape deserves a new one)
     }
     m_frame = MakeFrame(m_camera, width, height);
     m_width = width;
@@ -277,50 +279,70 @@ void DeviceScene::Shade(const float* d_offsets, const int* d_ids, float* d_rgba,
 }
 
 // Grow-only cull work for `slots` frame slots of one carve-up (render.h CullBins; counters reset
-// themselves, so a slot is zero-filled only on its first use with this carve-up).
+// themselves, so a slot's counters are zero-filled only on its first use with this carve-up), in the
+// arena of this band shape.
 void DeviceScene::EnsureCullWork(std::size_t slots, std::size_t row_count, hipStream_t stream) const {
     const std::size_t bytes = CullBinBytes(m_n, m_width, row_count);
-    if (slots * bytes > m_cull_bytes) {
-        HipCheck(hipStreamSynchronize(stream), "hipStreamSynchronize(cull work)");
-        (void)hipFree(m_cull_work);
-        m_cull_work = nullptr;
-        m_cull_bytes = 0;
-        m_cull_work = DeviceAlloc<unsigned char>(slots * bytes, "hipMalloc(cull work)");
-        m_cull_bytes = slots * bytes;
-        m_cull_shape = 0;
-    }
-    // A new carve-up (band shape, or the split width and so the layout): zero every slot again.
     const std::uint64_t shape = (static_cast<std::uint64_t>(m_width) << 32) | row_count;
-    if (shape != m_cull_shape || bytes != m_cull_layout) {
-        m_cull_shape = shape;
-        m_cull_layout = bytes;
-        m_cull_zeroed = 0;
-    }
-    if (slots > m_cull_zeroed) {
-        // Only each slot's leading counters (render.h CullBins): a band shape that alternates on one
-        // scene (the share exchange's roles on one frame queue) re-carves every batch, and zeroing
-        // whole slots (~30 MB each, mostly split-key slices) cost 0.4-0.5 ms per 64-frame batch.
-        HipCheck(hipMemset2DAsync(m_cull_work + m_cull_zeroed * bytes, bytes, 0,
-                                  CullBinCounterBytes(m_n, m_width, row_count), slots - m_cull_zeroed, stream),
-                 "hipMemset2DAsync(cull work)");
-        m_cull_state.resize(std::max(m_cull_state.size(), slots));
-        for (std::size_t k = m_cull_zeroed; k < slots; ++k) {
-            m_cull_state[k] = CullSlotState{};  // zeroed: no plan
+    std::size_t pick = m_arenas.size();
+    for (std::size_t i = 0; i < m_arenas.size(); ++i) {
+        if (m_arenas[i].shape == shape && m_arenas[i].layout == bytes) {
+            pick = i;
         }
-        m_cull_zeroed = slots;
     }
+    if (pick == m_arenas.size()) {  // a new shape: a new arena, or the least recently used one re-carved
+        if (m_arenas.size() < kCullArenas) {
+            m_arenas.emplace_back();
+        } else {
+            pick = 0;
+            for (std::size_t i = 1; i < m_arenas.size(); ++i) {
+                pick = m_arenas[i].used < m_arenas[pick].used ? i : pick;
+            }
+        }
+        CullArena& a = m_arenas[pick];
+        a.shape = shape;
+        a.layout = bytes;
+        a.zeroed = 0;  // (stream order: earlier launches on this arena ran before its counters are reset)
+    }
+    CullArena& a = m_arenas[pick];
+    if (slots * bytes > a.bytes) {
+        HipCheck(hipStreamSynchronize(stream), "hipStreamSynchronize(cull work)");
+        (void)hipFree(a.work);
+        a.work = nullptr;
+        a.bytes = 0;
+        a.work = DeviceAlloc<unsigned char>(slots * bytes, "hipMalloc(cull work)");
+        a.bytes = slots * bytes;
+        a.zeroed = 0;
+    }
+    if (slots > a.zeroed) {
+        // Only each slot's leading counters (render.h CullBins): zeroing whole slots (~30 MB each,
+        // mostly split-key slices) cost 0.4-0.5 ms per 64-frame batch whenever a shape was re-carved.
+        HipCheck(hipMemset2DAsync(a.work + a.zeroed * bytes, bytes, 0, CullBinCounterBytes(m_n, m_width, row_count),
+                                  slots - a.zeroed, stream),
+                 "hipMemset2DAsync(cull work)");
+        a.state.resize(std::max(a.state.size(), slots));
+        for (std::size_t k = a.zeroed; k < slots; ++k) {
+            a.state[k] = CullSlotState{};  // zeroed: no plan
+        }
+        a.zeroed = slots;
+    }
+    a.used = ++m_cull_clock;
+    m_arena = pick;
 }
 
 void DeviceScene::DropPlans(std::size_t slots) const {
-    for (std::size_t k = 0; k < slots && k < m_cull_state.size(); ++k) {
-        m_cull_state[k].plan_descs = 0;
+    for (CullArena& a : m_arenas) {
+        for (std::size_t k = 0; k < slots && k < a.state.size(); ++k) {
+            a.state[k].plan_descs = 0;
+        }
     }
 }
 
 
 CullBins DeviceScene::CullSlot(std::size_t slot, std::size_t row_count, unsigned descs) const {
-    CullSlotState& st = m_cull_state.at(slot);  // (EnsureCullWork sized it)
-    CullBins bins = CullBinLayout(m_cull_work + slot * m_cull_layout, m_n, m_width, row_count, st.uses & 1u);
+    CullArena& a = m_arenas.at(m_arena);  // (EnsureCullWork picked and sized it)
+    CullSlotState& st = a.state.at(slot);
+    CullBins bins = CullBinLayout(a.work + slot * a.layout, m_n, m_width, row_count, st.uses & 1u);
     bins.descs = std::min(bins.descs, descs);
     bins.plan = st.plan_descs != bins.descs;  // (render.hip WorkPlan: the launch may order anyway)
     st.plan_descs = bins.descs;
@@ -355,20 +377,29 @@ DeviceScene::ParamTable& DeviceScene::AcquireTable(std::size_t frames, hipStream
         t.pending = false;
     }
     if (t.frames < frames) {
-        // Launches queued earlier may still read the old device table. They all run before `stream`'s
-        // current end (calls on one scene are stream-ordered: OrderAfterPrevious ran first), so draining
-        // this stream suffices -- never a device-wide sync from an engine worker (other workers' queues
-        // and RCCL kernels waiting on peers would be waited for too).
+        // Every table of the ring grows at once (one stall, on the first large call, instead of one at
+        // the first use of each). Launches queued earlier may still read an old device table. They all
+        // run before `stream`'s current end (calls on one scene are stream-ordered: OrderAfterPrevious
+        // ran first), so draining this stream suffices -- never a device-wide sync from an engine worker
+        // (other workers' queues and RCCL kernels waiting on peers would be waited for too).
         HipCheck(hipStreamSynchronize(stream), "hipStreamSynchronize(parameter table)");
-        (void)hipFree(t.device);
-        (void)hipHostFree(t.host);
-        t.device = nullptr;
-        t.host = nullptr;
-        t.frames = 0;
         const std::size_t bytes = CullTableBytes(frames);
-        HipCheck(hipMalloc(&t.device, bytes), "hipMalloc(parameter table)");
-        HipCheck(hipHostMalloc(&t.host, bytes, hipHostMallocDefault), "hipHostMalloc(parameter table)");
-        t.frames = frames;
+        for (ParamTable& r : m_tables) {
+            if (r.frames >= frames) {
+                continue;
+            }
+            r.pending = false;  // (its uploads ran: the stream is drained)
+            (void)hipFree(r.device);
+            (void)hipHostFree(r.host);
+            r.device = nullptr;
+            r.host = nullptr;
+            r.host_device = nullptr;
+            r.frames = 0;
+            HipCheck(hipMalloc(&r.device, bytes), "hipMalloc(parameter table)");
+            HipCheck(hipHostMalloc(&r.host, bytes, hipHostMallocMapped), "hipHostMalloc(parameter table)");
+            HipCheck(hipHostGetDevicePointer(&r.host_device, r.host, 0), "hipHostGetDevicePointer(parameter table)");
+            r.frames = frames;
+        }
     }
     if (t.uploaded == nullptr) {
         HipCheck(hipEventCreateWithFlags(&t.uploaded, hipEventDisableTiming), "hipEventCreate(parameter table)");
@@ -378,7 +409,8 @@ DeviceScene::ParamTable& DeviceScene::AcquireTable(std::size_t frames, hipStream
 
 void DeviceScene::TraceBatch(const float* const* d_offsets, float* const* d_rgba, int* const* d_ids, std::size_t frames,
                              std::size_t row_begin, std::size_t row_count, int variant, hipStream_t stream,
-                             std::size_t row_interleave, int id_planes, bool rgba_frame_rows) const {
+                             std::size_t row_interleave, int id_planes, bool rgba_frame_rows,
+                             const std::size_t* row_begins) const {
     if (id_planes >= 0 && (id_planes != IdPlanes(m_n) || variant != kTraceCull)) {
         throw std::runtime_error("TraceBatch: packed ids need the cull variant and " + std::to_string(IdPlanes(m_n)) +
                                  " bit planes for this scene");
@@ -388,6 +420,15 @@ void DeviceScene::TraceBatch(const float* const* d_offsets, float* const* d_rgba
     }
     if (!BandFits(row_begin, row_count, row_interleave, m_height)) {
         throw std::runtime_error("TraceBatch: row band outside the frame");
+    }
+    for (std::size_t f = 0; row_begins != nullptr && f < frames; ++f) {
+        if (!BandFits(row_begins[f], row_count, row_interleave, m_height) ||
+            CullFusedInfo(row_begins[f], row_count, m_height, row_interleave)) {
+            throw std::runtime_error("TraceBatch: per-frame bands must lie inside the frame and short of all of it");
+        }
+    }
+    if (row_begins != nullptr && (variant != kTraceCull || !CullBinningEnabled() || !CullBinnable(m_width, row_count))) {
+        throw std::runtime_error("TraceBatch: per-frame bands need the binned cull variant");
     }
     if (frames > static_cast<std::size_t>(kMaxTableFrames)) {
         throw std::runtime_error("TraceBatch: at most " + std::to_string(kMaxTableFrames) + " frames per batch");
@@ -417,13 +458,16 @@ void DeviceScene::TraceBatch(const float* const* d_offsets, float* const* d_rgba
         bins[f] = CullSlot(f, row_count, batch_descs);
         cf[f].edges = m_edges + f * floats;
         cf[f].bins = &bins[f];
-        cf[f].band = BandArgs{d_offsets[f], d_rgba != nullptr ? d_rgba[f] : nullptr, m_width, m_height, row_begin,
-                              row_count, d_ids != nullptr ? d_ids[f] : nullptr, row_interleave, id_planes, rgba_frame_rows};
+        cf[f].band = BandArgs{d_offsets[f], d_rgba != nullptr ? d_rgba[f] : nullptr, m_width, m_height,
+                              row_begins != nullptr ? row_begins[f] : row_begin, row_count,
+                              d_ids != nullptr ? d_ids[f] : nullptr, row_interleave, id_planes, rgba_frame_rows};
     }
-    const StageEvents ev = BindStageEvents(!CullFusedInfo(row_begin, row_count, m_height, row_interleave), true);
+    const StageEvents ev = BindStageEvents(
+        !CullFusedInfo(row_begins != nullptr ? row_begins[0] : row_begin, row_count, m_height, row_interleave), true);
     ParamTable* table = frames > static_cast<std::size_t>(kMaxBatch) ? &AcquireTable(frames, stream) : nullptr;
     const CullTable ct{table != nullptr ? table->device : nullptr, table != nullptr ? table->host : nullptr,
-                       table != nullptr ? table->frames : 0};
+                       table != nullptr ? table->frames : 0, table != nullptr ? table->host_device : nullptr,
+                       table != nullptr ? table->uploaded : nullptr};
     const hipError_t launched = LaunchCullFrames(cf.data(), frames, m_n, m_vertices, m_shade, m_frame, m_background,
                                                  m_rank, stream, m_timing ? &ev : nullptr,
                                                  table != nullptr ? &ct : nullptr);
@@ -432,8 +476,7 @@ void DeviceScene::TraceBatch(const float* const* d_offsets, float* const* d_rgba
     }
     HipCheck(launched, "batched trace launch");
     if (table != nullptr) {
-        HipCheck(hipEventRecord(table->uploaded, stream), "hipEventRecord(parameter table)");
-        table->pending = true;
+        table->pending = true;  // (LaunchCullFrames recorded `uploaded` after the upload)
     }
     RecordOrder(stream);
 }

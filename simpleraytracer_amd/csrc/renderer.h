@@ -93,9 +93,12 @@ public:
     // their parameters from a device table uploaded once per call), the others frame by frame.
     void TraceBatch(const float* const* d_offsets, float* const* d_rgba, int* const* d_ids, std::size_t frames,
                     std::size_t row_begin, std::size_t row_count, int variant, hipStream_t stream,
-                    std::size_t row_interleave = 1, int id_planes = -1, bool rgba_frame_rows = false) const;
+                    std::size_t row_interleave = 1, int id_planes = -1, bool rgba_frame_rows = false,
+                    const std::size_t* row_begins = nullptr) const;
     // (A frame f with d_ids non-null but d_ids[f] null and d_rgba[f] non-null is traced to RGBA;
-    // rgba_frame_rows: RGBA outputs are whole frames, band rows stored at their frame rows.)
+    // rgba_frame_rows: RGBA outputs are whole frames, band rows stored at their frame rows;
+    // row_begins: frame f's band starts at row_begins[f] instead -- one row count and pattern, so one
+    // band shape, for every frame; cull variant, bands short of the whole frame.)
 
     std::size_t width() const { return m_width; }
     // The spatial order (device, triangles entries) and the time its build took at load (ms).
@@ -132,27 +135,37 @@ private:
     std::size_t m_width = 0;
     std::size_t m_height = 0;
     // Cull variant work buffers (render.h CullBins: tile info, bin lists, split-tile keys), grown on
-    // demand by Trace; disabled by env SRT_CULL_BIN=0 (every tile then streams every record).
-    mutable unsigned char* m_cull_work = nullptr;
-    mutable std::size_t m_cull_bytes = 0;
-    mutable std::uint64_t m_cull_shape = 0;  // (width << 32) | rows of the current carve-up
-    mutable std::size_t m_cull_layout = 0;   // its bytes (they change with the split width too)
-    mutable unsigned m_cull_gen = 0;         // frames binned (render.h CullBins::gen)
-    mutable std::size_t m_cull_zeroed = 0;   // frame slots of the current carve-up zero-filled
+    // demand by Trace; disabled by env SRT_CULL_BIN=0 (every tile then streams every record). One
+    // arena per band shape in use (a band-sharing engine traces two or three shapes per batch on one
+    // scene; one arena re-carved per call cost a counter fill and a new work plan every call), at most
+    // kCullArenas, the least recently used re-carved for a new shape.
     // Per frame slot: frames binned in it (their parity picks the count buffer) and the trace grid
     // its work plan was built for (0: none; render.h CullBins::plan).
     struct CullSlotState {
         unsigned uses = 0;
         unsigned plan_descs = 0;
     };
-    mutable std::vector<CullSlotState> m_cull_state;
+    struct CullArena {
+        unsigned char* work = nullptr;
+        std::size_t bytes = 0;       // allocated
+        std::uint64_t shape = 0;     // (width << 32) | rows of its carve-up (0: none)
+        std::size_t layout = 0;      // bytes per slot (they change with the split width too)
+        std::size_t zeroed = 0;      // frame slots of the carve-up whose counters are zero-filled
+        std::uint64_t used = 0;      // last use (m_cull_clock)
+        std::vector<CullSlotState> state;
+    };
+    static constexpr std::size_t kCullArenas = 4;
+    mutable std::vector<CullArena> m_arenas;
+    mutable std::size_t m_arena = 0;         // the arena of the current call
+    mutable std::uint64_t m_cull_clock = 0;
+    mutable unsigned m_cull_gen = 0;         // frames binned (render.h CullBins::gen)
     // The cull work of frame slots [0, slots) for a row_count-row band (grown, zeroed on first use
     // of a slot with this carve-up), and slot `slot`'s carve-up with a fresh frame number for a trace
     // grid of at most `descs` descriptors; it (re)builds the slot's work plan when the slot has none
     // for that grid.
     void EnsureCullWork(std::size_t slots, std::size_t row_count, hipStream_t stream) const;
     CullBins CullSlot(std::size_t slot, std::size_t row_count, unsigned descs = ~0u) const;
-    void DropPlans(std::size_t slots) const;  // after a failed launch: slots [0, slots) rebuild theirs
+    void DropPlans(std::size_t slots) const;  // slots [0, slots) of every arena rebuild their plans
     void EnsureEdgeSlots(std::size_t slots, hipStream_t stream) const;
     // BVH variant: node boxes + depth bounds (render.h BvhLayout), allocated by the first bvh Trace.
     mutable unsigned char* m_bvh = nullptr;
@@ -162,6 +175,7 @@ private:
     struct ParamTable {
         void* device = nullptr;
         void* host = nullptr;
+        void* host_device = nullptr;  // `host` mapped into the device's address space (render.h CullTable)
         hipEvent_t uploaded = nullptr;
         std::size_t frames = 0;
         bool pending = false;
