@@ -6,7 +6,7 @@ dir=${1:?usage: tools/save_evidence.sh profiles/rNN/evidence}
 cd "$(dirname "$0")/.."
 rm -rf "$dir"
 mkdir -p "$dir"
-for f in pytest_gpu smoke bench bench_driver_shape bench_c5 rehearse2 rehearse4 rehearse8 rank_sim rank_sim_share rank_sim_c5 rccl2 \
+for f in pytest_gpu smoke bench bench_driver_shape bench_c5 rehearse2 rehearse4 rehearse8 rank_sim rank_sim_share rank_sim_alltoall rank_sim_c5 rccl2 \
          band_sim band_sim_b8 host_bands; do
     [ -f "gpurun_out/$f.log" ] && cp "gpurun_out/$f.log" "$dir/$f.log"
 done
