@@ -8,8 +8,8 @@ The exchange, modelled (it cannot be measured on a one-GPU box): per frame the P
 not composite it send their band of hit ids (the engine's payload: id_bytes per pixel, 2 for 16-bit
 codes) to its compositor; the all-to-all deals the compositors round-robin, so every one of the
 P (P - 1) directed xGMI links of a fully connected node carries bytes_frame / (P (P - 1)) per frame
-on average (rotating / share: a batch's P - 1 senders use their links into its compositor, the
-min(Q, P) batches in flight distinct ones), and the link-bound time per frame is that over the
+on average (share likewise; rotating: a batch's P - 1 senders use their links into its compositor,
+the min(Q, P) batches in flight distinct ones), and the link-bound time per frame is that over the
 per-direction link rate. ASSUMED
 rate, not measured: --link-gbs (default 64 GB/s per direction; MI355X_MICROARCH.md has no xGMI figure,
 SURVEY.md section 5 quotes 153.6 GB/s per link, bidirectional, so about 77 GB/s each way at peak;
@@ -87,10 +87,11 @@ def main():
             per[r] = round(dt / (a.steps * a.batch) * 1e6, 3)
             eng.close()
         slow = max(per.values())
-        # all-to-all: every directed link carries 1/(P (P - 1)) of a frame's payload; rotating / share:
-        # a batch's P - 1 senders each use their link into its compositor, and the queues' batches in
-        # flight (on min(queues, P) distinct compositors) use distinct links
-        links = P * (P - 1) if a.exchange == "alltoall" else (P - 1) * min(a.queues, P)
+        # all-to-all and share (frame f composited on f % P): every directed link carries 1/(P (P - 1))
+        # of a frame's payload; rotating: a batch's P - 1 senders each use their link into its
+        # compositor, and the queues' batches in flight (on min(queues, P) distinct compositors) use
+        # distinct links
+        links = P * (P - 1) if a.exchange in ("alltoall", "share") else (P - 1) * min(a.queues, P)
         link_bytes = xbytes / links if P > 1 else 0.0
         link_us = link_bytes / (a.link_gbs * 1e3)
         bound = max(slow, link_us)
