@@ -331,6 +331,28 @@ __device__ __forceinline__ void ComputeRecord(const PrepareParams& p, const floa
     }
 }
 
+// ComputeRecord for the band record pass: the float solve's y half only, its x half left pending
+// (`xpend`: finish it with ScreenBoxX(bs, sb.x, sb.y)) -- a record the band cannot see never needs
+// it. Any other outcome (disabled, double solve, unbounded) is the whole box, as ComputeRecord's.
+__device__ __forceinline__ void ComputeRecordY(const PrepareParams& p, const float* __restrict__ v, bool real,
+                                               float c[9], float& vol, float4& sb, BoxSolve& bs, bool& xpend) {
+    xpend = false;
+    const bool disabled = !ComputeEdges(p.origin, p.base, p.du, p.dv, v, real, c, vol);
+    sb = make_float4(__builtin_inff(), -__builtin_inff(), __builtin_inff(), -__builtin_inff());
+    if (disabled) {
+        return;
+    }
+    ScreenBoxSetup(c, kScreenBoxRange, bs);
+    if (!bs.ok) {
+        sb = ScreenBox(c);
+    } else if (!bs.spans) {
+        sb = make_float4(-__builtin_inff(), __builtin_inff(), -__builtin_inff(), __builtin_inff());
+    } else {
+        ScreenBoxY(bs, sb.z, sb.w);
+        xpend = true;
+    }
+}
+
 // Stored as (hi, -lo) pairs so the cull test is one saturating packed add per axis.
 __device__ __forceinline__ uint2 QuantizeBox(const float4& sb) {
     return make_uint2(PackI16(QuantHi(sb.y), -QuantLo(sb.x)), PackI16(QuantHi(sb.w), -QuantLo(sb.z)));
@@ -1954,7 +1976,9 @@ using PrepareBinTable = FrameTable<PrepareBinParams>;
 #define SRT_BIN_AHEAD 4
 #endif
 constexpr int kBinAhead = SRT_BIN_AHEAD;  // tile boxes a bin thread loads at once
-template <class Frames>
+// BAND: a band short of the whole frame (the tile info ran first, `fused` is 0): the x half of a
+// record's screen box waits for its band test (ComputeRecordY). Full frames take ComputeRecord.
+template <class Frames, bool BAND>
 __global__ __launch_bounds__(kBinThreads) void PrepareBinKernel(const Frames batch) {
     extern __shared__ float2 bin_lds[];
     const PrepareBinParams& pb = batch[blockIdx.z];
@@ -1989,8 +2013,14 @@ __global__ __launch_bounds__(kBinThreads) void PrepareBinKernel(const Frames bat
     float4 sb = make_float4(__builtin_inff(), -__builtin_inff(), __builtin_inff(), -__builtin_inff());
     const unsigned id = real ? pp.order[i] : i;
     const float* v = pp.svertices + 9ull * (real ? i : 0u);  // by position: no order -> vertex chain
+    BoxSolve bs;
+    bool xpend = false;
     if (i < pp.n_pad) {
-        ComputeRecord(pp, v, real, c, vol, sb);
+        if constexpr (BAND) {
+            ComputeRecordY(pp, v, real, c, vol, sb, bs, xpend);
+        } else {
+            ComputeRecord(pp, v, real, c, vol, sb);
+        }
     }
     // The monotone tile-column and tile-row bounds (the histogram's LDS is the reduction's
     // scratch), then the histogram zeroed.
@@ -1998,7 +2028,6 @@ __global__ __launch_bounds__(kBinThreads) void PrepareBinKernel(const Frames bat
     BinTileBounds(p, hist, b);
     SRT_SETUP_MARK(kDiagBinRow + blockIdx.x, 2);
     if (i < pp.n_pad) {
-        pp.qboxes[i] = QuantizeBox(sb);
         bool needed = !real || p.fused != 0u || *p.range_tag == p.gen;  // fused: a full frame, every record
         if (!needed) {  // does the quantized box meet a tile row of the band (analytic row bounds)?
             // Quantisation keeps both bound sequences nondecreasing: the first row whose quantized
@@ -2015,6 +2044,16 @@ __global__ __launch_bounds__(kBinThreads) void PrepareBinKernel(const Frames bat
             }
             needed = lo < ny && QuantLo(b[nx + lo].x) <= qhi;
         }
+        // The x half of the box for records the band can see; the others get the empty box (their
+        // y extent meets no tile row of the band, so no box test of the band could pass either).
+        if constexpr (BAND) {
+            if (xpend && needed) {
+                ScreenBoxX(bs, sb.x, sb.y);
+            } else if (xpend) {
+                sb = make_float4(__builtin_inff(), -__builtin_inff(), __builtin_inff(), -__builtin_inff());
+            }
+        }
+        pp.qboxes[i] = QuantizeBox(sb);
         if (needed) {
             CullRecord r;
             r.a = make_float4(c[0], c[1], c[2], c[3]);
@@ -3605,9 +3644,15 @@ void LaunchCullStages(const TB& tb, const BB& bb, const PB& pb, unsigned z, unsi
         Launch(TileInfoKernel<BB>, dim3(gx, (gy + kInfoTiles - 1) / kInfoTiles, z), dim3(kBinThreads), stream,
                ev.prep_begin, ev.prep_end, bb);
     }
-    LaunchLds(PrepareBinKernel<PB>, dim3(blocks, 1, z), dim3(kBinThreads),
-              BinLdsBytes(static_cast<int>(gx), static_cast<int>(gy)), stream, ev.bin_begin, order ? nullptr : ev.bin_end,
-              pb);
+    if (fused) {
+        LaunchLds(PrepareBinKernel<PB, false>, dim3(blocks, 1, z), dim3(kBinThreads),
+                  BinLdsBytes(static_cast<int>(gx), static_cast<int>(gy)), stream, ev.bin_begin,
+                  order ? nullptr : ev.bin_end, pb);
+    } else {
+        LaunchLds(PrepareBinKernel<PB, true>, dim3(blocks, 1, z), dim3(kBinThreads),
+                  BinLdsBytes(static_cast<int>(gx), static_cast<int>(gy)), stream, ev.bin_begin,
+                  order ? nullptr : ev.bin_end, pb);
+    }
     if (!order) {  // the slots' plans are current: the trace follows the bins
         Launch(TraceCullKernel<TB>, dim3(descs, 1, z), dim3(kWave * kCullWaves), stream, ev.begin, ev.end, tb);
         return;

@@ -64,58 +64,92 @@ __host__ __device__ inline bool ConstantInRange(float v) {
     return v == 0.f || (a >= 0x1p-40f && a <= 0x1p30f);  // NaN: false
 }
 
-// c = (c0A, cxA, cyA, c0B, cxB, cyB, c0C, cxC, cyC); range = F. true: *box = (xlo, xhi, ylo, yhi),
-// possibly unbounded (the gradients do not span the plane); false: use the double solve.
-__host__ __device__ inline bool ScreenBoxFast(const float c[9], float range, float box[4]) {
+// The solve in two halves sharing one setup, so a caller that may discard the record after its
+// y-extent (a band's record pass: DESIGN.md section 5) skips the x half: ScreenBoxFast is exactly
+// Setup, then Y, then X, the same operations on the same values.
+struct BoxSolve {
     float gx[3], gy[3], c0[3], s[3];
-    bool ok = true;
+    float r[3];    // ApproxRcp of the corner determinants (corner v: lines (v + 1) % 3, (v + 2) % 3)
+    bool ok;       // the float solve applies (else the double one)
+    bool spans;    // the gradients positively span the plane (else the box is unbounded)
+};
+
+__host__ __device__ inline void ScreenBoxSetup(const float c[9], float range, BoxSolve& b) {
+    b.ok = true;
     for (int e = 0; e < 3; ++e) {
-        c0[e] = c[3 * e];
-        gx[e] = c[3 * e + 1];
-        gy[e] = c[3 * e + 2];
-        const float t = std::fmaf(range, std::fabs(gx[e]), std::fabs(c0[e]));
-        s[e] = std::fmaf(0x1.00001p-24f, t, 0x1.1p-120f);
-        ok = ok && ConstantInRange(c0[e]) && GradientInRange(gx[e]) && GradientInRange(gy[e]);
+        b.c0[e] = c[3 * e];
+        b.gx[e] = c[3 * e + 1];
+        b.gy[e] = c[3 * e + 2];
+        const float t = std::fmaf(range, std::fabs(b.gx[e]), std::fabs(b.c0[e]));
+        b.s[e] = std::fmaf(0x1.00001p-24f, t, 0x1.1p-120f);
+        b.ok = b.ok && ConstantInRange(b.c0[e]) && GradientInRange(b.gx[e]) && GradientInRange(b.gy[e]);
     }
-    if (!ok) {
-        return false;
+    if (!b.ok) {
+        b.spans = false;
+        return;
     }
-    const float dAB = KahanDiffOfProducts(gx[0], gy[1], gy[0], gx[1]);
-    const float dBC = KahanDiffOfProducts(gx[1], gy[2], gy[1], gx[2]);
-    const float dCA = KahanDiffOfProducts(gx[2], gy[0], gy[2], gx[0]);
-    const bool spans = (dAB > 0.f && dBC > 0.f && dCA > 0.f) || (dAB < 0.f && dBC < 0.f && dCA < 0.f);
-    const float inf = INFINITY;
-    if (!spans) {
-        box[0] = -inf;
-        box[1] = inf;
-        box[2] = -inf;
-        box[3] = inf;
-        return true;
+    const float dAB = KahanDiffOfProducts(b.gx[0], b.gy[1], b.gy[0], b.gx[1]);
+    const float dBC = KahanDiffOfProducts(b.gx[1], b.gy[2], b.gy[1], b.gx[2]);
+    const float dCA = KahanDiffOfProducts(b.gx[2], b.gy[0], b.gy[2], b.gx[0]);
+    b.spans = (dAB > 0.f && dBC > 0.f && dCA > 0.f) || (dAB < 0.f && dBC < 0.f && dCA < 0.f);
+    const float dv[3] = {dBC, dCA, dAB};
+    for (int v = 0; v < 3; ++v) {
+        b.ok = b.ok && (!b.spans || std::fabs(dv[v]) >= 0x1p-60f);
+        b.r[v] = ApproxRcp(dv[v]);
     }
-    const float dv[3] = {dBC, dCA, dAB};  // corner v: lines (v + 1) % 3 and (v + 2) % 3
-    float xlo = inf, xhi = -inf, ylo = inf, yhi = -inf;
+}
+
+// y = (gx_j k_i - gx_i k_j) / d over the three corners (k = c0 + s), padded: (ylo, yhi). Needs
+// b.ok && b.spans.
+__host__ __device__ inline void ScreenBoxY(const BoxSolve& b, float& ylo, float& yhi) {
+    ylo = INFINITY;
+    yhi = -INFINITY;
     for (int v = 0; v < 3; ++v) {
         const int i = (v + 1) % 3, j = (v + 2) % 3;
-        ok = ok && std::fabs(dv[v]) >= 0x1p-60f;
-        const float r = ApproxRcp(dv[v]), ar = std::fabs(r);
-        // x = (k_j gy_i - k_i gy_j) / d, y = (gx_j k_i - gx_i k_j) / d, k = c0 + s
-        const float sx1 = s[j] * gy[i], sx2 = s[i] * gy[j];
-        const float sy1 = gx[j] * s[i], sy2 = gx[i] * s[j];
-        const float nx = KahanDiffOfProducts(c0[j], gy[i], c0[i], gy[j]) + (sx1 - sx2);
-        const float ny = KahanDiffOfProducts(gx[j], c0[i], gx[i], c0[j]) + (sy1 - sy2);
-        const float x = nx * r, y = ny * r;
-        const float px = std::fmaf(0x1p-18f, std::fabs(x), std::fmaf(0x1p-20f * ar, std::fabs(sx1) + std::fabs(sx2), 0x1p-80f));
+        const float r = b.r[v], ar = std::fabs(r);
+        const float sy1 = b.gx[j] * b.s[i], sy2 = b.gx[i] * b.s[j];
+        const float ny = KahanDiffOfProducts(b.gx[j], b.c0[i], b.gx[i], b.c0[j]) + (sy1 - sy2);
+        const float y = ny * r;
         const float py = std::fmaf(0x1p-18f, std::fabs(y), std::fmaf(0x1p-20f * ar, std::fabs(sy1) + std::fabs(sy2), 0x1p-80f));
-        xlo = std::fmin(xlo, x - px);
-        xhi = std::fmax(xhi, x + px);
         ylo = std::fmin(ylo, y - py);
         yhi = std::fmax(yhi, y + py);
     }
-    box[0] = xlo;
-    box[1] = xhi;
-    box[2] = ylo;
-    box[3] = yhi;
-    return ok;
+}
+
+// x = (k_j gy_i - k_i gy_j) / d over the three corners, padded: (xlo, xhi). Needs b.ok && b.spans.
+__host__ __device__ inline void ScreenBoxX(const BoxSolve& b, float& xlo, float& xhi) {
+    xlo = INFINITY;
+    xhi = -INFINITY;
+    for (int v = 0; v < 3; ++v) {
+        const int i = (v + 1) % 3, j = (v + 2) % 3;
+        const float r = b.r[v], ar = std::fabs(r);
+        const float sx1 = b.s[j] * b.gy[i], sx2 = b.s[i] * b.gy[j];
+        const float nx = KahanDiffOfProducts(b.c0[j], b.gy[i], b.c0[i], b.gy[j]) + (sx1 - sx2);
+        const float x = nx * r;
+        const float px = std::fmaf(0x1p-18f, std::fabs(x), std::fmaf(0x1p-20f * ar, std::fabs(sx1) + std::fabs(sx2), 0x1p-80f));
+        xlo = std::fmin(xlo, x - px);
+        xhi = std::fmax(xhi, x + px);
+    }
+}
+
+// c = (c0A, cxA, cyA, c0B, cxB, cyB, c0C, cxC, cyC); range = F. true: *box = (xlo, xhi, ylo, yhi),
+// possibly unbounded (the gradients do not span the plane); false: use the double solve.
+__host__ __device__ inline bool ScreenBoxFast(const float c[9], float range, float box[4]) {
+    BoxSolve b;
+    ScreenBoxSetup(c, range, b);
+    if (!b.ok) {
+        return false;
+    }
+    if (!b.spans) {
+        box[0] = -INFINITY;
+        box[1] = INFINITY;
+        box[2] = -INFINITY;
+        box[3] = INFINITY;
+        return true;
+    }
+    ScreenBoxY(b, box[2], box[3]);
+    ScreenBoxX(b, box[0], box[1]);
+    return true;
 }
 
 }  // namespace srt
