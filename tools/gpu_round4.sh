@@ -30,7 +30,7 @@ if [[ $STEPS == *ranks* ]]; then  # per-rank GPU time of the band pipeline (exch
     run rank_sim 400 python tools/rank_sim.py --all-ranks
     run rank_sim_alltoall 300 python tools/rank_sim.py --ranks 2,4,8 --exchange alltoall
     run rank_sim_c5 400 python tools/rank_sim.py --ranks 1,8 --width 3840 --height 2160 --triangles 1000000 \
-        --steps 16 --warmup 8
+        --steps 8 --warmup 8
 fi
 if [[ $STEPS == *rccl2* ]]; then  # two ranks on one GPU over torchrun: does RCCL take it at all?
     SRT_BENCH_ONE_DEVICE=1 run rccl2 120 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \

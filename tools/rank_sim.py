@@ -17,7 +17,7 @@ RCCL point-to-point reaching ~85 % of it gives ~64). A sweep of rates is printed
 ceiling = W x H / max(slowest rank's GPU time, link time) -- the exchange overlaps the other queue's
 compute (its RCCL kernels' CU time is inside neither figure).
 
-    python tools/rank_sim.py [--ranks 1,2,4,8] [--steps 32] [--batch 64] [--queues 2] [--link-gbs 64]
+    python tools/rank_sim.py [--ranks 1,2,4,8] [--steps 16] [--batch 256] [--queues 2] [--link-gbs 64]
 """
 from __future__ import annotations
 
@@ -35,11 +35,12 @@ sys.path.insert(0, REPO)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ranks", default="1,2,4,8")
-    # batches (warmup and timed) multiples of 8: under the rotating compositor roles (share,
-    # rotating) every rank then composites the same number of batches at P = 2, 4, 8
-    ap.add_argument("--steps", type=int, default=32)
+    # batches (warmup and timed) multiples of 8: under the rotating compositor roles (rotating)
+    # every rank then composites the same number of batches at P = 2, 4, 8; 256-frame batches, as
+    # bench.py's steps (its --frames-per-step)
+    ap.add_argument("--steps", type=int, default=16)
     ap.add_argument("--warmup", type=int, default=8)
-    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--queues", type=int, default=2)
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
