@@ -903,9 +903,17 @@ void FrameEngine::TraceShare(std::size_t local, std::size_t b) {
     std::vector<float*> rgba;
     std::vector<int*> ids;
     std::vector<std::size_t> begins;
+    // The senders' tile rows are a small band of many frames: their launch sets take up to
+    // SRT_SHARE_THIN_LAUNCH frames (default 256, the table's limit) to keep the launches few.
+    static const std::size_t thin_launch = [] {
+        const char* e = std::getenv("SRT_SHARE_THIN_LAUNCH");
+        const long v = e != nullptr ? std::strtol(e, nullptr, 10) : 0;
+        return v > 0 ? std::min<std::size_t>(static_cast<std::size_t>(v), kMaxTableFrames) : std::size_t{kMaxTableFrames};
+    }();
     const auto flush = [&](const Role& role, bool own) {
-        for (std::size_t f0 = 0; f0 < offs.size(); f0 += L) {
-            const std::size_t n = std::min(L, offs.size() - f0);
+        const std::size_t LL = own ? L : std::max(L, thin_launch);
+        for (std::size_t f0 = 0; f0 < offs.size(); f0 += LL) {
+            const std::size_t n = std::min(LL, offs.size() - f0);
             q.scene->TraceBatch(offs.data() + f0, own ? rgba.data() + f0 : nullptr, own ? nullptr : ids.data() + f0, n,
                                 role.row_begin, role.rows, m_opt.variant, q.stream, role.pattern, m_id_planes, true,
                                 own ? nullptr : begins.data() + f0);
