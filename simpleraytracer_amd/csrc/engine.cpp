@@ -910,8 +910,17 @@ void FrameEngine::TraceShare(std::size_t local, std::size_t b) {
         const long v = e != nullptr ? std::strtol(e, nullptr, 10) : 0;
         return v > 0 ? std::min<std::size_t>(static_cast<std::size_t>(v), kMaxTableFrames) : std::size_t{kMaxTableFrames};
     }();
+    // The frames composited here are nearly whole frames: launch sets of SRT_SHARE_OWN_LAUNCH frames
+    // (default 8, their parameters in the kernel arguments, as whole frames at P = 1; rank simulation
+    // P = 2 / 4: 9.97 / 5.73 us per frame against 10.13 / 5.88 at 64, profiles/r04/share/ol_*).
+    static const std::size_t own_launch = [] {
+        const char* e = std::getenv("SRT_SHARE_OWN_LAUNCH");
+        const long v = e != nullptr ? std::strtol(e, nullptr, 10) : 0;
+        return v > 0 ? std::min<std::size_t>(static_cast<std::size_t>(v), kMaxTableFrames)
+                     : static_cast<std::size_t>(kMaxBatch);
+    }();
     const auto flush = [&](const Role& role, bool own) {
-        const std::size_t LL = own ? L : std::max(L, thin_launch);
+        const std::size_t LL = own ? own_launch : std::max(L, thin_launch);
         for (std::size_t f0 = 0; f0 < offs.size(); f0 += LL) {
             const std::size_t n = std::min(LL, offs.size() - f0);
             q.scene->TraceBatch(offs.data() + f0, own ? rgba.data() + f0 : nullptr, own ? nullptr : ids.data() + f0, n,
