@@ -21,11 +21,12 @@ trace (TraceCullKernel; bit-identical to brute force), shad
 framebuffer store. Nothing is cached across frames. Each GPU keeps --queues batches in flight.
 
 Multi-GPU (BASELINE config C4), --mode bands (default): every frame is split
-into N row bands (the frame's 16-row tile rows dealt round-robin, --rows interleaved), GPU d traces
-band d of every frame of the batch (hit ids, 4 B per pixel), the bands go to the frames'
-compositors over RCCL -- --exchange alltoall (default): frame f of a batch to GPU f % N, the
-batch's N gathers fused into one ncclSend/ncclRecv group --, and each compositor shades its frames
-in one launch (deferred shading, bit-identical). value = frames x W x H / the max-over-ranks time
+over the N GPUs in its 16-row tile rows, frame f composited on GPU f % N -- --exchange share
+(default): the compositor traces k of every k + N - 1 tile rows itself (k = 32 at 1080p), fused with
+the shading, every other GPU one, as packed hit ids; alltoall: N even interleaved bands --; the
+bands go to the compositors over RCCL (the batch's N gathers fused into one ncclSend/ncclRecv
+group), and each compositor shades its frames' received rows in one launch (deferred shading,
+bit-identical). value = frames x W x H / the max-over-ranks time
 of the timed steps: "scaling": "strong". --mode frames: every GPU renders whole frames of its own
 (no exchange): "scaling": "weak" (a leg of the N > 1 line). After the timed steps every compositor
 compares its last batches' frames with a single-GPU render by another kernel, bit for bit
@@ -97,11 +98,11 @@ def parse():
     p.add_argument("--no-extras", action="store_true", help="only the main line (no secondary legs)")
     a = p.parse_args()
     if a.exchange == "auto":
-        # share: batch b's compositor traces k of every k + N - 1 tile rows itself, fused with the
-        # shading (k = 32 at 1080p), and the others one each: fewer rows take the ids path (trace to
-        # ids, exchange, deferred shading) than under alltoall, which sends (N - 1) / N of every
-        # frame. Rank simulation, us of GPU time per frame: N = 2 10.9 vs 14.6
-        # (alltoall, link-bound besides), N = 4 6.7 vs 8.2, N = 8 4.4 vs 5.3.
+        # share: frame f's compositor (GPU f % N) traces k of every k + N - 1 tile rows itself, fused
+        # with the shading (k = 32 at 1080p), and the others one each: fewer rows take the ids path
+        # (trace to ids, exchange, deferred shading) than under alltoall, which sends (N - 1) / N of
+        # every frame. Rank simulation, us of GPU time per frame: N = 2 9.9 vs
+        # 13.2 (alltoall, link-bound besides), N = 4 5.8 vs 8.2, N = 8 3.7 vs 4.8.
         a.exchange = "share"
     return a
 

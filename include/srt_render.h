@@ -144,10 +144,10 @@ ML_API_ENTRY int srtTakeStageTimes(srt_device_scene scene, unsigned* launches, d
  * launch per batch, bit-identical to the fused trace). Exchanges: SRT_EXCHANGE_ALLTOALL (frame f of
  * a batch composited on device f % P; the batch's P gathers fused into one ncclSend / ncclRecv
  * group), SRT_EXCHANGE_ROTATING (the batch gathered to device b % P), SRT_EXCHANGE_ROOT (device 0),
- * SRT_EXCHANGE_SHARE (batch b composited on device c = b % P, which traces `share` of every
- * share + P - 1 tile rows itself, straight into its frames; each other device traces one tile row
- * per such cycle and sends its ids: the exchange and the shading shrink to (P - 1) / (share + P - 1)
- * of a frame; interleaved rows only).
+ * SRT_EXCHANGE_SHARE (frame f composited on device c = f % P, which traces `share` of every
+ * share + P - 1 tile rows of it itself, straight into the frame; each other device traces one tile
+ * row per such cycle and sends its ids: the exchange and the shading shrink to (P - 1) / (share +
+ * P - 1) of a frame; interleaved rows only; bench.py's default).
  * P == 1: trace + shade fused (RGBA). SRT_SPLIT_FRAMES: every device renders whole frames of its
  * own (no exchange). Devices: all in this process (srtEngineCreate; one worker thread per device,
  * ncclCommInitAll; a repeated device exchanges by device copies -- the one-GPU rehearsal), or one
