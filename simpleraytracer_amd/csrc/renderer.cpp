@@ -396,7 +396,10 @@ DeviceScene::ParamTable& DeviceScene::AcquireTable(std::size_t frames, hipStream
             r.host_device = nullptr;
             r.frames = 0;
             HipCheck(hipMalloc(&r.device, bytes), "hipMalloc(parameter table)");
-            HipCheck(hipHostMalloc(&r.host, bytes, hipHostMallocMapped), "hipHostMalloc(parameter table)");
+            // Mapped and fine-grained (coherent): the upload kernel reads it over the bus, uncached,
+            // so a table rewritten for a later launch is never read stale from the L2.
+            HipCheck(hipHostMalloc(&r.host, bytes, hipHostMallocMapped | hipHostMallocCoherent),
+                     "hipHostMalloc(parameter table)");
             HipCheck(hipHostGetDevicePointer(&r.host_device, r.host, 0), "hipHostGetDevicePointer(parameter table)");
             r.frames = frames;
         }
