@@ -181,9 +181,10 @@ def test_cull_modes(gpu, scenes, monkeypatch, mode):
 def test_cull_setup_state_across_frames(gpu, scenes):
     """The per-frame setup hands off between blocks through self-resetting state (tile-box
     accumulators and the last tile block's bounds, the bin blocks' arrival count and the last
-    bin block's work list): one scene over frames whose band shape (the layout is re-zeroed)
-    and offsets (uniform, random, far outside the frame, NaN) change, each frame bit-identical
-    to a fresh brute-force render, twice in a row."""
+    bin block's work list): one scene over frames whose band shape (one cull arena per shape, at
+    most four: seven shapes re-carve the least recently used ones) and offsets (uniform, random,
+    far outside the frame, NaN) change, each frame bit-identical to a fresh brute-force render,
+    twice in a row."""
     import torch
 
     import simpleraytracer_amd as srt
@@ -194,7 +195,8 @@ def test_cull_setup_state_across_frames(gpu, scenes):
     nan = rng.random((h, w, 2), dtype=np.float32)
     nan[5:40, 70:90] = np.nan
     cases = [(0, h, None), (40, 77, rng.random((h, w, 2), dtype=np.float32)), (0, h, far), (17, 1, None),
-             (0, h, nan), (0, h, None)]
+             (0, h, nan), (5, 33, None), (60, 100, rng.random((h, w, 2), dtype=np.float32)), (100, 16, None),
+             (3, 150, far), (40, 77, None), (0, h, None)]
     scene = srt.DeviceScene(scenes["soup2k"], 0)
     stream = torch.cuda.current_stream()
     for rep in range(2):
