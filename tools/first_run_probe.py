@@ -3,6 +3,9 @@
 engine), to find one-time costs that land inside a timed region.
 
     python tools/first_run_probe.py [--ranks 2] [--rank 0] [--exchange share] [--runs 4]
+
+With SRT_PROBE_HOST=1 the engine also prints every trace / shade phase whose host time exceeds
+300 us (engine.cpp RunWorker).
 """
 import argparse
 import os
