@@ -3850,9 +3850,23 @@ bool CullFusedInfo(std::size_t row_begin, std::size_t row_count, std::size_t hei
         const char* v = std::getenv("SRT_FUSED_INFO");
         return v == nullptr || std::strcmp(v, "0") != 0;
     }();
-    // (Bands too -- their bin launch then writing every cull record, as the tile info it would
-    // test them against is not known yet -- measured slower at every P: P = 8 rank 5.35 -> 6.0 us.)
-    return enabled && row_begin == 0 && row_count == height && interleave == 1;
+    // Bands of at least SRT_FUSED_BAND_PCT % of the frame's rows too (default 75: the share
+    // compositor's own band): their bin launch then writes every cull record, as the tile info it
+    // would test them against is not known yet -- nearly all of them are needed anyway. (Every band
+    // fused measured slower at every P, the thin ones paying for all records: P = 8 rank 5.35 -> 6.0
+    // us, round 4.)
+    static const std::size_t band_pct = [] {
+        const char* v = std::getenv("SRT_FUSED_BAND_PCT");
+        const long n = v != nullptr ? std::strtol(v, nullptr, 10) : 75;
+        return static_cast<std::size_t>(n < 0 ? 0 : n);
+    }();
+    if (!enabled || height == 0) {
+        return false;
+    }
+    if (row_begin == 0 && row_count == height && interleave == 1) {
+        return true;
+    }
+    return band_pct <= 100 && row_count * 100 >= band_pct * height;
 }
 
 bool BandFits(std::size_t row_begin, std::size_t row_count, std::size_t interleave, std::size_t height) {
