@@ -155,6 +155,8 @@ ML_API_ENTRY int srtTakeStageTimes(srt_device_scene scene, unsigned* launches, d
 typedef struct srt_engine_t* srt_engine;
 #define SRT_ROWS_INTERLEAVED 0
 #define SRT_ROWS_CONTIGUOUS 1
+#define SRT_ROWS_ROTATED 2 /* contiguous bands, device p tracing band (p + c) % P of a frame composited on
+                              device c (SRT_EXCHANGE_ALLTOALL): even load, one block of rows per band */
 #define SRT_EXCHANGE_ALLTOALL 0
 #define SRT_EXCHANGE_ROTATING 1
 #define SRT_EXCHANGE_ROOT 2
@@ -165,6 +167,8 @@ typedef struct srt_engine_t* srt_engine;
 #define SRT_ENGINE_RCCL_SELF 1 /* one device: the bands path with the ids sent to itself over a one-rank
                                   RCCL communicator (the real exchange, waits and abort on one GPU) */
 typedef struct srt_engine_options {
+    size_t struct_size; /* sizeof(srt_engine_options) as the caller was compiled (checked: a caller built
+                           against another layout is refused, never read past its struct) */
     int variant;    /* SRT_TRACE_* */
     size_t queues;  /* batches in flight per device (0 = 2) */
     size_t batch;   /* frames per batch (0 = 16) */
@@ -231,6 +235,14 @@ ML_API_ENTRY int srtEngineInfo(srt_engine engine, size_t* devices, size_t* local
 ML_API_ENTRY int srtExchangeHost(const int* const* band_ids, size_t bands, size_t width, size_t height, int rows,
                                  int exchange, size_t batch, size_t batch_index, int* const* recv,
                                  size_t* recv_frames, size_t* buffer_rows);
+/* The same for SRT_EXCHANGE_SHARE at `share` tile rows per cycle (0 = srtShareAuto): band_ids[d] =
+ * device d's traced ids of the batch's frames (batch x buffer rows x width int32, buffer rows = one
+ * class of share + bands - 1 interleaved classes): of frame f its sender class (share + (d - c - 1)
+ * mod bands for compositor c = f % bands; unused when d = c); recv[c]: [bands][frames of c][buffer
+ * rows][width], sender d at slot (d - c - 1) mod bands (slot bands - 1: unused). */
+ML_API_ENTRY int srtExchangeHostShare(const int* const* band_ids, size_t bands, size_t width, size_t height,
+                                      size_t share, size_t batch, size_t batch_index, int* const* recv,
+                                      size_t* recv_frames, size_t* buffer_rows);
 /* Host self-test of a record's screen box (render.hip ComputeRecord): c = the
  * 9 edge coefficients (c0A, cxA, cyA, c0B, cxB, cyB, c0C, cxC, cyC); mode 0 = the float fast path
  * where it applies, else the double solve (what the kernels do), 1 = the double solve, 2 = the fast

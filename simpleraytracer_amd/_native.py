@@ -31,6 +31,7 @@ SRT_TRACE_BVH = 3
 SRT_MAX_BATCH = 8  # include/srt_render.h: frames per srtTraceBatchAsync call
 SRT_ROWS_INTERLEAVED = 0
 SRT_ROWS_CONTIGUOUS = 1
+SRT_ROWS_ROTATED = 2  # contiguous bands rotated per compositor (all-to-all)
 SRT_EXCHANGE_ALLTOALL = 0
 SRT_EXCHANGE_ROTATING = 1
 SRT_EXCHANGE_ROOT = 2
@@ -69,6 +70,7 @@ class EngineOptions(ctypes.Structure):
     """``srt_engine_options`` (include/srt_render.h)."""
 
     _fields_ = [
+        ("struct_size", ctypes.c_size_t),
         ("variant", ctypes.c_int),
         ("queues", ctypes.c_size_t),
         ("batch", ctypes.c_size_t),
@@ -151,6 +153,8 @@ _SIGNATURES = {
     "srtEngineInfo": (ctypes.c_int, [ctypes.c_void_p, _PSZ, _PSZ, _PSZ, _PSZ, ctypes.POINTER(ctypes.c_int), _PD]),
     "srtExchangeHost": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), _SZ, _SZ, _SZ, ctypes.c_int, ctypes.c_int, _SZ,
                                        _SZ, ctypes.POINTER(ctypes.c_void_p), _PSZ, _PSZ]),
+    "srtExchangeHostShare": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), _SZ, _SZ, _SZ, _SZ, _SZ, _SZ,
+                                            ctypes.POINTER(ctypes.c_void_p), _PSZ, _PSZ]),
     "srtScreenBoxHost": (ctypes.c_int, [ctypes.POINTER(ctypes.c_float), ctypes.c_int, ctypes.POINTER(ctypes.c_float)]),
 }
 

@@ -50,6 +50,14 @@ def interleaved_frame_rows(height: int, world: int, rank: int):
                            for t in range(rank, tiles, world)] or [np.zeros(0, np.int64)]).astype(np.int64)
 
 
+def rotated_band(world: int, device: int, compositor: int) -> int:
+    """The contiguous band ``device`` traces of a frame composited on ``compositor`` under the
+    rotated all-to-all (csrc/engine.h ExchangePlan::BandOf): (device + compositor) % P, so every
+    device traces every band once over P consecutive frames; the compositor's receive buffer holds
+    device p's ids at slot (p + c) % P = the band (RecvSlot), i.e. band-major in band order."""
+    return (device + compositor) % world
+
+
 def share_auto(height: int, world: int) -> int:
     """The share exchange's default tile rows per cycle (csrc/engine.cpp ShareAuto, srtShareAuto): the
     largest power of two <= 32 whose cycle of share + P - 1 tile rows fits the frame."""
@@ -76,3 +84,54 @@ def share_frame_rows(height: int, world: int, share: int, rank: int, compositor:
         mine = list(range(cls, tiles, classes))
     return np.concatenate([np.arange(t * TILE_ROWS, min(height, (t + 1) * TILE_ROWS)) for t in mine]
                           or [np.zeros(0, np.int64)]).astype(np.int64)
+
+
+class ExchangePlan:
+    """Python restatement of csrc/engine.h ExchangePlan for the per-frame exchanges (all-to-all over
+    interleaved, contiguous or rotated bands, and share): which device composites frame f of a batch,
+    the frame's slot there, and where a device's ids sit in its send and receive buffers. The tests
+    move real band ids between processes with it (tests/test_bands_dist.py) and compare the result
+    with the library's own layout (srtExchangeHost / srtExchangeHostShare)."""
+
+    def __init__(self, world: int, batch: int, exchange: str = "alltoall", rows: str = "interleaved"):
+        if exchange not in ("alltoall", "share"):
+            raise ValueError("per-frame exchanges only: alltoall, share")
+        self.world, self.batch, self.exchange = world, batch, exchange
+        self.rotate = rows == "rotated" and world > 1
+
+    def compositor(self, f: int) -> int:
+        return f % self.world
+
+    def slot(self, f: int) -> int:
+        return f // self.world
+
+    def frames_for(self, c: int) -> int:
+        return (self.batch - c + self.world - 1) // self.world if c < self.batch else 0
+
+    def max_frames(self) -> int:
+        return (self.batch + self.world - 1) // self.world
+
+    def send_frame(self, c: int, j: int) -> int:
+        """Band frame index of compositor c's j-th frame in a device's send buffer (SendFrames)."""
+        return c * self.max_frames() + j
+
+    def recv_slot(self, c: int, p: int) -> int:
+        """Slot of device p's ids in compositor c's receive buffer (RecvSlot)."""
+        if self.rotate:
+            return rotated_band(self.world, p, c)
+        if self.exchange == "share":
+            return (p + self.world - c - 1) % self.world
+        return p
+
+
+def traced_rows(height: int, world: int, exchange: str, rows: str, device: int, compositor: int, share: int = 0):
+    """The frame rows ``device`` traces, in band order, of a frame composited on ``compositor``."""
+    import numpy as np
+
+    if exchange == "share":
+        return share_frame_rows(height, world, share, device, compositor)
+    if rows == "interleaved":
+        return interleaved_frame_rows(height, world, device)
+    band = rotated_band(world, device, compositor) if rows == "rotated" else device
+    b, c = band_range(height, world, band)
+    return np.arange(b, b + c, dtype=np.int64)

@@ -219,25 +219,46 @@ void CommAbortAll(std::vector<void*>& comms) noexcept {
 }
 
 void CommDestroyAll(std::vector<void*>& comms) noexcept {
-    std::vector<void*> stuck;
+    // Every finalize first, inside one group (the ranks of one ncclCommInitAll world may wait for
+    // their peers' finalize: one at a time, each would wait out its settle limit), then one settle
+    // for all of them, then the destroys. Anything that fails is aborted instead.
+    std::vector<void*> live;
     for (void* c : comms) {
-        if (c == nullptr) {
-            continue;
-        }
-        auto comm = static_cast<ncclComm_t>(c);
-        bool ok = false;
-        try {
-            NcclCheck(ncclCommFinalize(comm), "ncclCommFinalize", true);
-            CommSettle(&c, 1, "ncclCommFinalize", nullptr, 10.0);
-            ok = ncclCommDestroy(comm) == ncclSuccess;
-        } catch (...) {
-            ok = false;
-        }
-        if (!ok) {
-            stuck.push_back(c);
+        if (c != nullptr) {
+            live.push_back(c);
         }
     }
     comms.clear();
+    if (live.empty()) {
+        return;
+    }
+    bool ok = true;
+    try {
+        NcclCheck(ncclGroupStart(), "ncclGroupStart(finalize)");
+        ncclResult_t first = ncclSuccess;
+        for (void* c : live) {
+            const ncclResult_t r = ncclCommFinalize(static_cast<ncclComm_t>(c));
+            if (r != ncclSuccess && r != ncclInProgress && first == ncclSuccess) {
+                first = r;
+            }
+        }
+        const ncclResult_t end = ncclGroupEnd();
+        NcclCheck(first, "ncclCommFinalize");
+        NcclCheck(end, "ncclGroupEnd(finalize)", true);
+        CommSettle(live.data(), live.size(), "ncclCommFinalize", nullptr, 10.0);
+    } catch (...) {
+        ok = false;
+    }
+    if (!ok) {
+        CommAbortAll(live);
+        return;
+    }
+    std::vector<void*> stuck;
+    for (void* c : live) {
+        if (ncclCommDestroy(static_cast<ncclComm_t>(c)) != ncclSuccess) {
+            stuck.push_back(c);
+        }
+    }
     CommAbortAll(stuck);
 }
 

@@ -95,7 +95,17 @@ std::size_t BandSplit::BufferRows() const {
     if (bands == 1) {
         return height;
     }
-    return interleaved ? InterleavedBandRows(height, bands, 0) : (height + bands - 1) / bands;
+    if (!interleaved) {
+        return (height + bands - 1) / bands;
+    }
+    // The largest band that travels (interleaved bands need not shrink with the index: the one
+    // holding a partial last tile row may be shorter than the next). kShare: the sender classes only
+    // -- sizing by class 0 padded every sender's buffer to 2 tile rows at P = 8 (1080p) for 1 traced.
+    std::size_t rows = 0;
+    for (std::size_t j = first_sent; j < bands; ++j) {
+        rows = std::max(rows, InterleavedBandRows(height, bands, j));
+    }
+    return std::max<std::size_t>(rows, 1);
 }
 
 std::size_t BandSplit::FrameRow(std::size_t band, std::size_t local) const {
@@ -133,6 +143,9 @@ std::size_t ExchangePlan::MaxFramesPerCompositor() const {
 }
 
 std::size_t ExchangePlan::RecvSlot(std::size_t c, std::size_t p) const {
+    if (rotate) {
+        return BandOf(p, c);
+    }
     return exchange == EngineOptions::kShare ? (p + bands - c - 1) % bands : p;
 }
 
@@ -150,10 +163,8 @@ std::size_t SendPixels(const ExchangePlan& plan, std::size_t c, std::size_t j, s
 
 std::vector<std::vector<int>> ExchangeOnHost(const BandSplit& split, const ExchangePlan& plan, std::size_t width,
                                              std::size_t batch_index, const std::vector<std::vector<int>>& band_ids) {
-    if (plan.exchange == EngineOptions::kShare) {
-        throw std::runtime_error("ExchangeOnHost: the share exchange has per-batch band shapes (no host self-test)");
-    }
-    const std::size_t P = split.bands, B = split.BufferRows(), F = plan.batch;
+    // kShare: split holds the share + P - 1 classes, every band buffer one class (the sender's).
+    const std::size_t P = plan.bands, B = split.BufferRows(), F = plan.batch;
     const std::size_t band_pixels = B * width;
     if (band_ids.size() != P) {
         throw std::runtime_error("ExchangeOnHost: one id buffer per band");
@@ -179,7 +190,7 @@ std::vector<std::vector<int>> ExchangeOnHost(const BandSplit& split, const Excha
                             send.begin() + SendPixels(plan, cf, plan.Slot(f), band_pixels));
             }
             std::copy_n(send.begin() + SendPixels(plan, c, 0, band_pixels), n * band_pixels,
-                        recv[c].begin() + d * n * band_pixels);
+                        recv[c].begin() + plan.RecvSlot(c, d) * n * band_pixels);
         }
     }
     return recv;
@@ -507,12 +518,20 @@ void FrameEngine::Init(const Scene& scene, const std::vector<int>& devices) {
     } else if (m_opt.exchange == EngineOptions::kShare) {
         m_opt.exchange = EngineOptions::kRotatingGather;  // one device: nothing to share
     }
+    if (m_opt.rotate) {
+        if (m_opt.interleaved || (m_opt.exchange != EngineOptions::kAllToAll && m_world > 1)) {
+            throw std::runtime_error("FrameEngine: rotated bands need contiguous rows and the all-to-all exchange");
+        }
+        m_rotate = m_exchange && m_world > 1;  // one device: its band is the frame, nothing to rotate
+    }
     // kShare: the frame's tile rows in cycles of k + P - 1 "classes" (the compositor's k, then one
     // per sender); the ids buffers hold one class.
     m_split = BandSplit::Make(m_height, m_bands ? (m_share != 0 ? m_share + m_world - 1 : m_world) : 1, m_opt.interleaved);
+    m_split.first_sent = m_share;
     m_plan.bands = m_bands ? m_world : 1;
     m_plan.batch = m_opt.batch;
     m_plan.exchange = m_opt.exchange;
+    m_plan.rotate = m_rotate;
     m_scene = std::make_unique<Scene>(scene);
     m_n = scene.triangle_count();
     {  // the exchange payload: packed ids with the cull variant (env SRT_EXCHANGE_IDS=32: int32)
@@ -539,6 +558,14 @@ void FrameEngine::Init(const Scene& scene, const std::vector<int>& devices) {
                 r.pattern = classes;
                 d->roles.push_back(r);
             }
+        } else if (m_rotate) {  // role j = band j (contiguous); inputs read from the full frames
+            for (std::size_t j = 0; j < m_world; ++j) {
+                Role r;
+                r.row_begin = m_split.RowBegin(j);
+                r.rows = m_split.RowCount(j);
+                r.pattern = 1;
+                d->roles.push_back(r);
+            }
         } else {
             Role r;
             r.row_begin = m_split.RowBegin(m_bands ? d->band : 0);
@@ -546,7 +573,7 @@ void FrameEngine::Init(const Scene& scene, const std::vector<int>& devices) {
             r.pattern = m_split.Interleave();
             d->roles.push_back(r);
         }
-        const Role& measured = d->roles[m_share != 0 ? 1 : 0];
+        const Role& measured = d->roles[m_share != 0 ? 1 : m_rotate ? d->band : 0];
         d->row_begin = measured.row_begin;
         d->rows = measured.rows;
         std::size_t at = 0;
@@ -559,6 +586,9 @@ void FrameEngine::Init(const Scene& scene, const std::vector<int>& devices) {
 }
 
 std::size_t FrameEngine::RoleOf(std::size_t local, std::size_t c) const {
+    if (m_rotate) {
+        return m_plan.BandOf(m_dev[local]->band, c);
+    }
     if (m_share == 0) {
         return 0;
     }
@@ -747,7 +777,7 @@ void FrameEngine::SetInputs(const float* host_offsets, std::size_t count) {
         d.full = DeviceAlloc<float>(count * ff, "hipMalloc(inputs)");
         HipCheck(hipMemcpy(d.full, host_offsets, count * ff * sizeof(float), hipMemcpyHostToDevice),
                  "hipMemcpy(inputs)");
-        if (m_exchange) {  // each role's rows of every input, band-local and contiguous
+        if (m_exchange && !m_rotate) {  // each role's rows of every input, band-local and contiguous
             const std::size_t row_floats = m_width * 2;
             std::size_t all_rows = 0;
             for (const Role& role : d.roles) {
@@ -780,11 +810,11 @@ void FrameEngine::SetInputs(const float* host_offsets, std::size_t count) {
 // input: the hit density, regular tiles and packed layout of a real band), so the simulated shading
 // does a real frame's work.
 void FrameEngine::PrimeSimulation() {
-    const std::size_t ri = m_share != 0 ? 1 : 0;
     for (auto& dp : m_dev) {
         Device& d = *dp;
         DeviceGuard guard(d.device);
         const std::size_t local = static_cast<std::size_t>(&dp - &m_dev[0]);
+        const std::size_t ri = m_share != 0 ? 1 : m_rotate ? d.band : 0;
         const Role& role = d.roles[ri];
         for (Queue& q : d.queues) {
             if (q.send == nullptr || q.recv == nullptr || role.rows == 0) {
@@ -812,6 +842,9 @@ const float* FrameEngine::FullInput(std::size_t local, std::size_t k) const {
 const float* FrameEngine::BandInput(std::size_t local, std::size_t k, std::size_t role) const {
     const Device& d = *m_dev[local];
     const Role& r = d.roles[role];
+    if (m_rotate) {  // a contiguous band: its rows of the full input
+        return FullInput(local, k) + r.row_begin * m_width * 2;
+    }
     return d.band_in + (r.input * m_inputs + (k % m_inputs) * r.rows) * m_width * 2;
 }
 
@@ -863,6 +896,11 @@ void FrameEngine::TracePhase(std::size_t local, std::size_t b) {
     const std::size_t self = d.band;
     if (m_share != 0) {
         TraceShare(local, b);
+        HipCheck(hipEventRecord(q.traced, q.stream), "hipEventRecord(traced)");
+        return;
+    }
+    if (m_rotate) {
+        TraceRotated(local, b);
         HipCheck(hipEventRecord(q.traced, q.stream), "hipEventRecord(traced)");
         return;
     }
@@ -969,6 +1007,50 @@ void FrameEngine::TraceShare(std::size_t local, std::size_t b) {
     }
 }
 
+// Rotated all-to-all: device `self` traces band BandOf(self, c) of a frame composited on device c --
+// its own frames' band straight into the frame as RGBA, the others' as ids into c's region of the
+// send buffer. Frames whose bands have the same row count share launches (per-frame first rows).
+void FrameEngine::TraceRotated(std::size_t local, std::size_t b) {
+    Device& d = *m_dev[local];
+    Queue& q = d.queues[b % m_opt.queues];
+    const std::size_t F = m_opt.batch, k0 = b * F, L = m_opt.launch, self = d.band;
+    const std::size_t frame_floats4 = m_width * m_height * 4;
+    std::vector<const float*> offs;
+    std::vector<float*> rgba;
+    std::vector<int*> ids;
+    std::vector<std::size_t> begins;
+    std::vector<std::size_t> counts;
+    for (const Role& r : d.roles) {
+        if (r.rows != 0 && std::find(counts.begin(), counts.end(), r.rows) == counts.end()) {
+            counts.push_back(r.rows);
+        }
+    }
+    for (const std::size_t rows : counts) {
+        for (std::size_t f = 0; f < F; ++f) {
+            const std::size_t c = m_plan.Compositor(b, f);
+            const std::size_t j = RoleOf(local, c);
+            const Role& role = d.roles[j];
+            if (role.rows != rows) {
+                continue;
+            }
+            const bool own = c == self;
+            offs.push_back(BandInput(local, k0 + f, j));
+            rgba.push_back(own ? q.rgba + m_plan.Slot(f) * frame_floats4 : nullptr);
+            ids.push_back(own ? nullptr : Ids(q.send, SendFrames(m_plan, c, m_plan.Slot(f))));
+            begins.push_back(role.row_begin);
+        }
+        for (std::size_t f0 = 0; f0 < offs.size(); f0 += L) {
+            const std::size_t n = std::min(L, offs.size() - f0);
+            q.scene->TraceBatch(offs.data() + f0, rgba.data() + f0, ids.data() + f0, n, begins[f0], rows, m_opt.variant,
+                                q.stream, 1, m_id_planes, true, begins.data() + f0);
+        }
+        offs.clear();
+        rgba.clear();
+        ids.clear();
+        begins.clear();
+    }
+}
+
 void FrameEngine::ExchangePhase(std::size_t local, std::size_t b) {
     Device& d = *m_dev[local];
     Queue& q = d.queues[b % m_opt.queues];
@@ -1053,7 +1135,7 @@ void FrameEngine::ShadePhase(std::size_t local, std::size_t b) {
     const std::size_t stride = m_inputs == 1 ? 0 : (a2a ? m_world : 1) * FrameFloats();
     // The compositor's own rows are RGBA already: its band (all-to-all, rotating), or the first
     // m_share classes (share; the received ids start at class m_share).
-    const long skip = m_opt.rccl_self || m_share != 0 ? -1 : static_cast<long>(self);
+    const long skip = m_opt.rccl_self || m_share != 0 ? -1 : static_cast<long>(m_plan.BandOf(self, self));
     q.scene->Shade(FullInput(local, first), reinterpret_cast<const int*>(q.recv), q.rgba, 0, m_height, q.stream, n_self,
                    m_split.BufferRows(), m_split.interleaved ? m_split.bands : 0, stride, m_id_planes, skip, m_share);
 }
@@ -1156,10 +1238,18 @@ void FrameEngine::Run(std::size_t batches) {
         return;
     }
     m_next_batch += batches;
-    const std::function<void(std::size_t)> job = [this, b0, batches](std::size_t i) { RunWorker(i, b0, batches); };
+    // On the heap: a worker that never returns from a failed run (a wedged pool) is still inside this
+    // closure, so it is then leaked with the pool rather than destroyed under it (srtEngineRelease
+    // leaks a wedged engine too: the worker's `this`).
+    auto job = std::make_unique<std::function<void(std::size_t)>>(
+        [this, b0, batches](std::size_t i) { RunWorker(i, b0, batches); });
     try {
-        m_pool->Run(job, [this] { AbortComms(); });
+        m_pool->Run(*job, [this] { AbortComms(); });
     } catch (const std::exception& e) {
+        if (m_pool->wedged()) {
+            (void)job.release();
+            m_wedged = true;
+        }
         m_failed = e.what();
         if (!m_comms.empty()) {
             AbortComms();
@@ -1309,7 +1399,8 @@ DeviceScene::StageTimes FrameEngine::MeasureStages(std::size_t local, std::size_
                 ids[j] = Ids(q.send, j);
             }
             if (m_exchange) {
-                const std::size_t ri = m_share != 0 ? 1 : 0;  // the sender role: its ids fit the send buffer
+                // the sender role (its ids fit the send buffer); rotate: the device's own-index band
+                const std::size_t ri = m_share != 0 ? 1 : m_rotate ? d.band : 0;
                 const Role& role = d.roles[ri];
                 for (std::size_t j = 0; j < frames; ++j) {
                     offs[j] = BandInput(local, i * frames + j, ri);

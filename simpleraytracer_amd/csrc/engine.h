@@ -57,6 +57,11 @@ struct EngineOptions {
     std::size_t queues = 2;    // batches in flight per device
     std::size_t batch = 16;    // frames per batch
     bool interleaved = true;   // bands: tile rows dealt round-robin (else contiguous blocks)
+    // Contiguous bands (interleaved false) with kAllToAll: device p traces band (p + c) % P of a frame
+    // composited on device c, so over any P consecutive frames every device traces every band once
+    // (even load whatever the scene's density profile) while each band stays one contiguous block of
+    // rows, which the band record pass's block skip needs (render.h CullBins::block_ext).
+    bool rotate = false;
     int exchange = kAllToAll;  // bands at P > 1
     int split = kBands;
     // Measurement only: one rank of a world-device job with no peers -- the rank's whole stream
@@ -87,10 +92,11 @@ std::size_t ShareAuto(std::size_t height, std::size_t world);
 struct BandSplit {
     std::size_t height = 0, bands = 1;
     bool interleaved = true;
+    std::size_t first_sent = 0;  // bands below it never travel (kShare: the compositor's own classes)
     static BandSplit Make(std::size_t height, std::size_t bands, bool interleaved);
     std::size_t RowBegin(std::size_t band) const;  // first frame row (interleaved: band * 16)
     std::size_t RowCount(std::size_t band) const;  // rows of the band
-    std::size_t BufferRows() const;                // rows of every band's (padded) buffer
+    std::size_t BufferRows() const;                // rows of every sent band's (padded) buffer: the largest
     std::size_t Interleave() const { return interleaved && bands > 1 ? bands : 1; }
     std::size_t FrameRow(std::size_t band, std::size_t local) const;
 };
@@ -103,15 +109,20 @@ struct ExchangePlan {
     std::size_t Slot(std::size_t f) const;                                      // index among its compositor's frames
     std::size_t FramesFor(std::size_t batch_index, std::size_t compositor) const;  // frames composited there
     std::size_t MaxFramesPerCompositor() const;
-    // Slot of device p's ids in compositor c's receive buffer (kShare: the senders in class order).
+    bool rotate = false;  // EngineOptions::rotate (kAllToAll over contiguous bands)
+    // Slot of device p's ids in compositor c's receive buffer (kShare: the senders in class order;
+    // rotate: the band p traces for c, so the buffer is band-major in band order).
     std::size_t RecvSlot(std::size_t c, std::size_t p) const;
+    // The band device p traces of a frame composited on device c (rotate: (p + c) % P, else p).
+    std::size_t BandOf(std::size_t p, std::size_t c) const { return rotate ? (p + c) % bands : p; }
     // Frames of a batch dealt to compositors round-robin (kAllToAll, kShare), not whole batches.
     bool PerFrame() const { return exchange == EngineOptions::kAllToAll || exchange == EngineOptions::kShare; }
 };
 
 // Host self-test of the exchange (no device): band_ids[d] = device d's traced ids of the batch's F
-// frames, frame-major (F x buffer rows x width int32, its own band). Returns, for compositor c,
-// its receive buffer exactly as the device path lays it out: [P][FramesFor(b, c)][buffer rows][W].
+// frames, frame-major (F x buffer rows x width int32: of frame f its band, plan.BandOf(d, compositor
+// of f) under rotate). Returns, for compositor c, its receive buffer exactly as the device path lays
+// it out: [P][FramesFor(b, c)][buffer rows][W], device d's frames at slot plan.RecvSlot(c, d).
 std::vector<std::vector<int>> ExchangeOnHost(const BandSplit& split, const ExchangePlan& plan, std::size_t width,
                                              std::size_t batch_index, const std::vector<std::vector<int>>& band_ids);
 
@@ -157,6 +168,9 @@ public:
     // kernels' dispatches): mean ms per launch of tile info, record setup + bins + work list, trace.
     DeviceScene::StageTimes MeasureStages(std::size_t local, std::size_t launches, std::size_t frames = 1);
 
+    // A failed run left a device worker stuck in a HIP call (GPU unresponsive): the worker still runs
+    // inside this engine, so its owner must leak it instead of destroying it (srtEngineRelease).
+    bool wedged() const { return m_wedged; }
     std::size_t devices() const { return m_world; }
     std::size_t local_devices() const { return m_dev.size(); }
     std::size_t frames_per_batch() const { return m_opt.batch; }
@@ -189,8 +203,10 @@ private:
         std::size_t input = 0;  // rows of the earlier roles (Device::band_in: per role, inputs x rows x W x 2)
     };
     std::size_t RoleOf(std::size_t local, std::size_t compositor) const;  // role for a frame composited there
+    bool m_rotate = false;  // EngineOptions::rotate at P > 1: roles = the P contiguous bands, inputs from `full`
     void TracePhase(std::size_t local, std::size_t b);
     void TraceShare(std::size_t local, std::size_t b);  // kShare's trace: each frame in its compositor's pattern
+    void TraceRotated(std::size_t local, std::size_t b);  // rotate: each frame's band by its compositor
     void ExchangePhase(std::size_t local, std::size_t b);  // RCCL: inside a group
     void CopyPhase(std::size_t local, std::size_t b);      // device-copy exchange
     void ShadePhase(std::size_t local, std::size_t b);

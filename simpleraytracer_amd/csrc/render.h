@@ -21,6 +21,8 @@ namespace srt {
 // multiple of kPadTriangles (the largest cull step: 256 threads x 16 records) so no trace
 // loop has a tail; the per-ray variants stop after the last tile holding a real record.
 constexpr int kTileTriangles = 256;
+// Records per block of the bin kernel (render.hip kBinThreads): the unit of the band skip hint.
+constexpr int kBinBlockRecords = 256;
 constexpr int kPadTriangles = 4096;
 
 // Edge records, tile-planar: tile t (256 records, 10 KiB) = four planes, each indexed by the
@@ -164,6 +166,10 @@ constexpr int kMaxBinTiles = 8192;    // and tiles_x * tiles_y <= this (bin kern
 struct CullBins {
     const unsigned* order; // the scene's record ids in spatial order (DeviceScene; not in the buffer)
     const float* svertices;  // the scene's vertices in that order (DeviceScene; not in the buffer)
+    // Per 256-position block of the spatial order: (lowest ylo, highest yhi) of its records' screen
+    // boxes under the prepared frame (LaunchBlockExtents; DeviceScene). A band's record pass skips a
+    // block whose extent meets none of its rows (a skip hint, exact: render.hip BandMayReach); null: none.
+    const float2* block_ext = nullptr;
     void* tile_info;       // tiles x 32 B: ray box, uniform offset (TileInfoKernel)
     unsigned* counts;      // tiles + 1: list lengths, then the large-list length (this frame's buffer)
     unsigned* counts_next; // the slot's other count buffer (its next frame's): zeroed by this frame's trace
@@ -291,6 +297,11 @@ hipError_t LaunchCullFrames(const CullFrame* frames, std::size_t count, std::uin
 // The scene's shading table (once, at load): per triangle two float4, (the shading normal
 // cross(v1 - v0, v2 - v0), its length) and (albedo, 0); d_table holds 8 floats per triangle. The
 // d_shade arguments of the launches below take it.
+// Screen-box y extent of every 256-position block of the spatial order under `frame` (records computed
+// as the bin kernel computes them; n_pad / 256 float2 into d_ext): the band record pass's skip hint,
+// keyed to (scene, camera, W x H) like the spatial order itself.
+hipError_t LaunchBlockExtents(const float* d_svertices, std::uint64_t n, const Frame& frame, float2* d_ext,
+                              hipStream_t stream);
 hipError_t LaunchShadeTable(const float* d_vertices, const float* d_albedo, std::uint64_t n, float* d_table,
                             hipStream_t stream);
 

@@ -148,6 +148,7 @@ struct PrepareParams {
     float4* __restrict__ screen_boxes;
     uint2* __restrict__ qboxes;
     CullRecord* __restrict__ cull;
+    const float2* __restrict__ block_ext;  // render.h CullBins::block_ext (null: no block skip)
     unsigned n;
     unsigned n_pad;
     float origin[3];
@@ -1592,6 +1593,7 @@ __device__ __forceinline__ void PacketBatch(CullShared& sh, const Box& bb, const
 // the screen-box range, or whose list overflowed, streams every record instead.
 // ---------------------------------------------------------------------------------------
 constexpr int kBinThreads = 256;
+static_assert(kBinThreads == kBinBlockRecords, "one bin block per skip-hint block (render.h)");
 #ifndef SRT_LARGE_TILES
 #define SRT_LARGE_TILES 16
 #endif
@@ -1966,6 +1968,80 @@ struct RangeDiv {
     }
 };
 
+// Whether any ray of the band can lie in the fy range [ylo, yhi] of a block of records (its screen
+// boxes' union, LaunchBlockExtents), for a frame whose sample offsets all lie in [0, 1] (no range
+// tag): a ray of frame row y has fy = fl(fl(y + sy) / H) in [fl(y / H), fl((y + 1) / H)] (the
+// correctly rounded division is monotone), so rows below floor(ylo H) - 1 or above floor(yhi H) + 1
+// end short of the range (1 / H is far above an ulp of fy). A block none of whose records' screen
+// boxes meets a ray of the band has no record any ray of the band can hit (DESIGN.md section 5,
+// exactness (ii)), so skipping it changes no pixel. Rows: a contiguous band's own; an interleaved or
+// patterned band's whole 16-row tile rows (BandFrameRow), a superset.
+__device__ __forceinline__ bool BandMayReach(const BinParams& p, float ylo, float yhi) {
+    if (ylo > yhi) {
+        return false;  // every record of the block is disabled (empty boxes)
+    }
+    if (!(ylo <= yhi)) {
+        return true;  // NaN: no skip
+    }
+    const int h = static_cast<int>(p.hf);
+    const double a = floor(static_cast<double>(ylo) * static_cast<double>(p.hf)) - 1.0;
+    const double b = floor(static_cast<double>(yhi) * static_cast<double>(p.hf)) + 1.0;
+    if (b < 0.0 || a > static_cast<double>(h - 1)) {
+        return false;  // outside the frame's rows
+    }
+    const int ya = static_cast<int>(fmax(a, 0.0)), yb = static_cast<int>(fmin(b, static_cast<double>(h - 1)));
+    const int every = p.row_interleave & 0xFFFF, g = p.row_interleave >> 16;
+    if (every <= 1) {
+        return yb >= p.row_begin && ya <= p.row_begin + p.row_count - 1;
+    }
+    const int t0 = p.row_begin / kCullTileRows, group = 1 << g;
+    const int last = (p.row_count + kCullTileRows - 1) / kCullTileRows - 1;  // the band's last local tile row
+    const int t_last = t0 + (last >> g) * every + (last & (group - 1));
+    const int ta = max(ya / kCullTileRows, t0), tb = min(yb / kCullTileRows, t_last);
+    for (int t = ta; t <= tb && t < ta + every; ++t) {
+        if ((t - t0) % every < group) {
+            return true;
+        }
+    }
+    return false;
+}
+
+// The block extents (render.h LaunchBlockExtents): block b's records computed as PrepareBinKernel
+// computes them (vertices by position, the one-piece screen box, whose y half ComputeRecordY
+// reproduces bit for bit: screen_box.h), reduced to (min ylo, max yhi); a NaN box end widens the
+// block to everything.
+__global__ __launch_bounds__(kBinThreads) void BlockExtentKernel(PrepareParams pp, float2* __restrict__ ext) {
+    __shared__ float part[2][kBinThreads / kWave];
+    const unsigned i = blockIdx.x * kBinThreads + threadIdx.x;
+    float lo = __builtin_inff(), hi = -__builtin_inff();
+    if (i < pp.n_pad) {
+        const bool real = i < pp.n;
+        float c[9], vol;
+        float4 sb;
+        ComputeRecord(pp, pp.svertices + 9ull * (real ? i : 0u), real, c, vol, sb);
+        lo = sb.z == sb.z ? sb.z : -__builtin_inff();
+        hi = sb.w == sb.w ? sb.w : __builtin_inff();
+    }
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+        lo = fminf(lo, __shfl_xor(lo, o));
+        hi = fmaxf(hi, __shfl_xor(hi, o));
+    }
+    const int wave = threadIdx.x / kWave;
+    if ((threadIdx.x & (kWave - 1)) == 0) {
+        part[0][wave] = lo;
+        part[1][wave] = hi;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < kBinThreads / kWave; ++w) {
+            lo = fminf(lo, part[0][w]);
+            hi = fmaxf(hi, part[1][w]);
+        }
+        ext[blockIdx.x] = make_float2(lo, hi);
+    }
+}
+
 struct PrepareBinParams {
     PrepareParams prep;
     BinParams bin;
@@ -1996,6 +2072,21 @@ __global__ __launch_bounds__(kBinThreads) void PrepareBinKernel(const Frames bat
         }
     }
     const int tid = threadIdx.x;
+    if constexpr (BAND) {
+        // A block of records that cannot reach the band's rows (LaunchBlockExtents' skip hint; frames
+        // whose offsets all lie in [0, 1]) leaves only its quantized boxes, empty, for the FULL stream.
+        if (pp.block_ext != nullptr && *p.range_tag != p.gen) {
+            const float2 e = pp.block_ext[blockIdx.x];
+            if (!BandMayReach(p, e.x, e.y)) {
+                const unsigned i = blockIdx.x * kBinThreads + tid;
+                if (i < pp.n_pad) {
+                    pp.qboxes[i] = QuantizeBox(
+                        make_float4(__builtin_inff(), -__builtin_inff(), __builtin_inff(), -__builtin_inff()));
+                }
+                return;
+            }
+        }
+    }
     const int nx = p.tiles_x, ny = p.tiles_y;
     const int tiles = nx * ny;
     float2* b = bin_lds;
@@ -3714,7 +3805,12 @@ hipError_t LaunchCullFrames(const CullFrame* frames, std::size_t count, std::uin
     PrepareBinParams* pp = use_table ? reinterpret_cast<PrepareBinParams*>(host + lay.prep) : pb.f;
     BinParams* bp = use_table ? reinterpret_cast<BinParams*>(host + lay.bin) : bb.f;
     TraceParams* tp = use_table ? reinterpret_cast<TraceParams*>(host + lay.trace) : tb.f;
-    const bool fused = CullFusedInfo(band0.row_begin, band0.row_count, band0.height, band0.row_interleave);
+    // Fused tile info only when every frame of the launch has the band's shape AND its first row
+    // (per-frame bands -- share senders, rotated bands -- always compute their tile info first).
+    bool fused = CullFusedInfo(band0.row_begin, band0.row_count, band0.height, band0.row_interleave);
+    for (std::size_t i = 1; i < count && fused; ++i) {
+        fused = frames[i].band.row_begin == band0.row_begin;
+    }
     bool order = false;  // some frame's slot needs its work plan (re)built: the order launch runs for all
     for (std::size_t i = 0; i < count; ++i) {
         const CullFrame& f = frames[i];
@@ -3736,6 +3832,7 @@ hipError_t LaunchCullFrames(const CullFrame* frames, std::size_t count, std::uin
         pp[i].prep = MakePrepareParams(d_vertices, d_rank, n, frame, const_cast<float*>(f.edges));
         pp[i].prep.order = f.bins->order;
         pp[i].prep.svertices = f.bins->svertices;
+        pp[i].prep.block_ext = f.bins->block_ext;
         pp[i].bin = bp[i];
     }
     static const WorkPlan plan_mode = WorkPlanFromEnv();
@@ -3842,6 +3939,18 @@ hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_ver
         const unsigned gy = static_cast<unsigned>((band.row_count + kRowsPerBlock - 1) / kRowsPerBlock);
         Launch(TraceLdsKernel, dim3(gx, gy), dim3(kWave * kLdsWaves), stream, ev.begin, ev.end, p);
     }
+    return hipGetLastError();
+}
+
+hipError_t LaunchBlockExtents(const float* d_svertices, std::uint64_t n, const Frame& frame, float2* d_ext,
+                              hipStream_t stream) {
+    if (n == 0 || d_svertices == nullptr || d_ext == nullptr) {
+        return hipErrorInvalidValue;
+    }
+    PrepareParams pp = MakePrepareParams(nullptr, nullptr, n, frame, nullptr);
+    pp.svertices = d_svertices;
+    hipLaunchKernelGGL(BlockExtentKernel, dim3((pp.n_pad + kBinThreads - 1) / kBinThreads), dim3(kBinThreads), 0, stream,
+                       pp, d_ext);
     return hipGetLastError();
 }
 

@@ -167,6 +167,7 @@ DeviceScene::~DeviceScene() {
     (void)hipFree(m_order);
     (void)hipFree(m_rank);
     (void)hipFree(m_svertices);
+    (void)hipFree(m_block_ext);
     for (CullArena& a : m_arenas) {
         (void)hipFree(a.work);
     }
@@ -209,6 +210,24 @@ void DeviceScene::Prepare(std::size_t width, std::size_t height, hipStream_t str
     // computes the records inside its bin kernel on every call, render.hip PrepareBinKernel).
     (void)stream;
     m_prepare_pending = true;
+    m_ext_pending = true;
+}
+
+// The block extents of the prepared frame, once per Prepare (on the first binned trace's stream,
+// before its launches). They depend on the scene, its camera and W x H only, like the spatial order.
+void DeviceScene::EnsureBlockExtents(hipStream_t stream) const {
+    static const bool enabled = [] {
+        const char* v = std::getenv("SRT_BLOCK_SKIP");
+        return v == nullptr || std::strcmp(v, "0") != 0;
+    }();
+    if (!enabled || !m_ext_pending || m_n == 0) {
+        return;
+    }
+    if (m_block_ext == nullptr) {
+        m_block_ext = DeviceAlloc<float2>(PaddedTriangleCount(m_n) / kBinBlockRecords, "hipMalloc(block extents)");
+    }
+    HipCheck(LaunchBlockExtents(m_svertices, m_n, m_frame, m_block_ext, stream), "block extents launch");
+    m_ext_pending = false;
 }
 
 void DeviceScene::OrderAfterPrevious(hipStream_t stream) const {
@@ -349,6 +368,7 @@ CullBins DeviceScene::CullSlot(std::size_t slot, std::size_t row_count, unsigned
     ++st.uses;
     bins.order = m_order;
     bins.svertices = m_svertices;
+    bins.block_ext = m_ext_pending ? nullptr : m_block_ext;
     m_cull_gen = m_cull_gen + 1u == 0u ? 1u : m_cull_gen + 1u;
     bins.gen = m_cull_gen;
     return bins;
@@ -424,11 +444,12 @@ void DeviceScene::TraceBatch(const float* const* d_offsets, float* const* d_rgba
     if (!BandFits(row_begin, row_count, row_interleave, m_height)) {
         throw std::runtime_error("TraceBatch: row band outside the frame");
     }
+    bool same_begin = true;  // render.hip LaunchCullFrames: per-frame first rows compute their tile info first
     for (std::size_t f = 0; row_begins != nullptr && f < frames; ++f) {
-        if (!BandFits(row_begins[f], row_count, row_interleave, m_height) ||
-            CullFusedInfo(row_begins[f], row_count, m_height, row_interleave)) {
-            throw std::runtime_error("TraceBatch: per-frame bands must lie inside the frame and short of all of it");
+        if (!BandFits(row_begins[f], row_count, row_interleave, m_height)) {
+            throw std::runtime_error("TraceBatch: per-frame bands must lie inside the frame");
         }
+        same_begin = same_begin && row_begins[f] == row_begins[0];
     }
     if (row_begins != nullptr && (variant != kTraceCull || !CullBinningEnabled() || !CullBinnable(m_width, row_count))) {
         throw std::runtime_error("TraceBatch: per-frame bands need the binned cull variant");
@@ -451,6 +472,7 @@ void DeviceScene::TraceBatch(const float* const* d_offsets, float* const* d_rgba
     OrderAfterPrevious(stream);
     EnsureEdgeSlots(frames, stream);
     EnsureCullWork(frames, row_count, stream);
+    EnsureBlockExtents(stream);
     std::vector<CullBins> bins(frames);
     std::vector<CullFrame> cf(frames);
     const std::size_t floats = PaddedTriangleCount(m_n) * kEdgeFloatsPerTriangle;
@@ -466,7 +488,8 @@ void DeviceScene::TraceBatch(const float* const* d_offsets, float* const* d_rgba
                               d_ids != nullptr ? d_ids[f] : nullptr, row_interleave, id_planes, rgba_frame_rows};
     }
     const StageEvents ev = BindStageEvents(
-        !CullFusedInfo(row_begins != nullptr ? row_begins[0] : row_begin, row_count, m_height, row_interleave), true);
+        !same_begin || !CullFusedInfo(row_begins != nullptr ? row_begins[0] : row_begin, row_count, m_height, row_interleave),
+        true);
     ParamTable* table = frames > static_cast<std::size_t>(kMaxBatch) ? &AcquireTable(frames, stream) : nullptr;
     const CullTable ct{table != nullptr ? table->device : nullptr, table != nullptr ? table->host : nullptr,
                        table != nullptr ? table->frames : 0, table != nullptr ? table->host_device : nullptr,
@@ -504,6 +527,7 @@ void DeviceScene::Trace(const float* d_offsets, float* d_rgba, std::size_t row_b
     const CullBins* use_bins = nullptr;
     if (variant == kTraceCull && row_count != 0 && CullBinningEnabled() && CullBinnable(m_width, row_count)) {
         EnsureCullWork(1, row_count, stream);
+        EnsureBlockExtents(stream);
         bins = CullSlot(0, row_count);
         use_bins = &bins;
     }

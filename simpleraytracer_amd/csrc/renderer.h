@@ -131,6 +131,12 @@ private:
     unsigned* m_rank = nullptr;   // its inverse: record id -> position
     float* m_svertices = nullptr; // vertices in spatial order (svertices[i] = vertices[order[i]])
     double m_build_ms = 0.0;      // spatial order build (BuildSpatialOrder) at load
+    // Per 256-position block of the spatial order: the y extent of its records' screen boxes under the
+    // prepared frame (render.h LaunchBlockExtents), the band record pass's skip hint; computed on the
+    // first binned trace after a Prepare (m_ext_pending). Env SRT_BLOCK_SKIP=0: never (no skip).
+    mutable float2* m_block_ext = nullptr;
+    mutable bool m_ext_pending = true;
+    void EnsureBlockExtents(hipStream_t stream) const;
     Frame m_frame{};
     std::size_t m_width = 0;
     std::size_t m_height = 0;

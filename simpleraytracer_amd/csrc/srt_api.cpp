@@ -362,13 +362,19 @@ srt::FrameEngine* FromHandle(srt_engine e) { return reinterpret_cast<srt::FrameE
 srt::EngineOptions EngineOptionsFrom(const srt_engine_options* o) {
     srt::EngineOptions opt;
     if (o != nullptr) {
+        if (o->struct_size != sizeof(srt_engine_options)) {
+            throw std::runtime_error("srt_engine_options.struct_size is " + std::to_string(o->struct_size) + ", expected " +
+                                     std::to_string(sizeof(srt_engine_options)) + " (a caller built against another "
+                                     "include/srt_render.h)");
+        }
         opt.variant = o->variant;
         opt.queues = o->queues == 0 ? opt.queues : o->queues;
         opt.batch = o->batch == 0 ? opt.batch : o->batch;
-        if (o->rows != SRT_ROWS_INTERLEAVED && o->rows != SRT_ROWS_CONTIGUOUS) {
+        if (o->rows != SRT_ROWS_INTERLEAVED && o->rows != SRT_ROWS_CONTIGUOUS && o->rows != SRT_ROWS_ROTATED) {
             throw std::runtime_error("Unknown rows mode " + std::to_string(o->rows));
         }
         opt.interleaved = o->rows == SRT_ROWS_INTERLEAVED;
+        opt.rotate = o->rows == SRT_ROWS_ROTATED;
         opt.exchange = o->exchange;
         opt.split = o->split;
         opt.simulate = o->simulate != 0;
@@ -438,7 +444,16 @@ ML_API_ENTRY srt_engine srtEngineCreateRank(const char* scene_path, int device, 
     return reinterpret_cast<srt_engine>(out);
 }
 
-ML_API_ENTRY void srtEngineRelease(srt_engine engine) { delete FromHandle(engine); }
+ML_API_ENTRY void srtEngineRelease(srt_engine engine) {
+    srt::FrameEngine* e = FromHandle(engine);
+    if (e != nullptr && e->wedged()) {
+        // Deliberately leaked: a device worker never returned from the failed run and still executes
+        // inside the engine (its state, communicators' control block and job); freeing any of it
+        // would let that thread touch freed memory if its HIP call ever returns (after a GPU reset).
+        return;
+    }
+    delete e;
+}
 
 ML_API_ENTRY int srtEngineSetInputs(srt_engine engine, const float* host_offsets, size_t count) {
     return Guarded([&] {
@@ -572,20 +587,33 @@ ML_API_ENTRY int srtEngineInfo(srt_engine engine, size_t* devices, size_t* local
     });
 }
 
-ML_API_ENTRY int srtExchangeHost(const int* const* band_ids, size_t bands, size_t width, size_t height, int rows,
-                                 int exchange, size_t batch, size_t batch_index, int* const* recv,
-                                 size_t* recv_frames, size_t* buffer_rows) {
+namespace {
+int ExchangeHost(const int* const* band_ids, size_t bands, size_t width, size_t height, int rows, int exchange,
+                 size_t share, size_t batch, size_t batch_index, int* const* recv, size_t* recv_frames,
+                 size_t* buffer_rows) {
     return Guarded([&] {
         if (bands == 0 || width == 0 || height == 0 || batch == 0 ||
-            (rows != SRT_ROWS_INTERLEAVED && rows != SRT_ROWS_CONTIGUOUS) || exchange < SRT_EXCHANGE_ALLTOALL ||
-            exchange > SRT_EXCHANGE_ROOT) {
+            (rows != SRT_ROWS_INTERLEAVED && rows != SRT_ROWS_CONTIGUOUS && rows != SRT_ROWS_ROTATED) ||
+            exchange < SRT_EXCHANGE_ALLTOALL || exchange > SRT_EXCHANGE_SHARE ||
+            (rows == SRT_ROWS_ROTATED && exchange != SRT_EXCHANGE_ALLTOALL) ||
+            (exchange == SRT_EXCHANGE_SHARE && (rows != SRT_ROWS_INTERLEAVED || bands < 2))) {
             throw std::runtime_error("Bad argument");
         }
-        const srt::BandSplit split = srt::BandSplit::Make(height, bands, rows == SRT_ROWS_INTERLEAVED);
+        if (exchange == SRT_EXCHANGE_SHARE) {
+            share = share == 0 ? srt::ShareAuto(height, bands) : share;
+            if (share > 64 || (share & (share - 1)) != 0) {
+                throw std::runtime_error("share must be a power of two, 1..64");
+            }
+        }
+        // (the engine's layout: kShare splits the frame into share + P - 1 interleaved classes)
+        srt::BandSplit split = srt::BandSplit::Make(height, exchange == SRT_EXCHANGE_SHARE ? share + bands - 1 : bands,
+                                                    rows == SRT_ROWS_INTERLEAVED);
+        split.first_sent = exchange == SRT_EXCHANGE_SHARE ? share : 0;
         srt::ExchangePlan plan;
         plan.bands = bands;
         plan.batch = batch;
         plan.exchange = exchange;
+        plan.rotate = rows == SRT_ROWS_ROTATED && bands > 1;
         if (buffer_rows != nullptr) {
             *buffer_rows = split.BufferRows();
         }
@@ -612,6 +640,24 @@ ML_API_ENTRY int srtExchangeHost(const int* const* band_ids, size_t bands, size_
             }
         }
     });
+}
+}  // namespace
+
+ML_API_ENTRY int srtExchangeHost(const int* const* band_ids, size_t bands, size_t width, size_t height, int rows,
+                                 int exchange, size_t batch, size_t batch_index, int* const* recv,
+                                 size_t* recv_frames, size_t* buffer_rows) {
+    if (exchange == SRT_EXCHANGE_SHARE) {  // needs its share parameter: srtExchangeHostShare
+        return Guarded([] { throw std::runtime_error("Bad argument: the share exchange takes srtExchangeHostShare"); });
+    }
+    return ExchangeHost(band_ids, bands, width, height, rows, exchange, 0, batch, batch_index, recv, recv_frames,
+                        buffer_rows);
+}
+
+ML_API_ENTRY int srtExchangeHostShare(const int* const* band_ids, size_t bands, size_t width, size_t height,
+                                      size_t share, size_t batch, size_t batch_index, int* const* recv,
+                                      size_t* recv_frames, size_t* buffer_rows) {
+    return ExchangeHost(band_ids, bands, width, height, SRT_ROWS_INTERLEAVED, SRT_EXCHANGE_SHARE, share, batch,
+                        batch_index, recv, recv_frames, buffer_rows);
 }
 
 ML_API_ENTRY int srtScreenBoxHost(const float* c, int mode, float* box) {

@@ -18,12 +18,12 @@ import os
 
 from . import _native
 from ._native import (SRT_ENGINE_RCCL_SELF, SRT_EXCHANGE_ALLTOALL, SRT_EXCHANGE_ROOT, SRT_EXCHANGE_ROTATING,
-                      SRT_EXCHANGE_SHARE, SRT_ROWS_CONTIGUOUS, SRT_ROWS_INTERLEAVED, SRT_SPLIT_BANDS, SRT_SPLIT_FRAMES, EngineOptions)
+                      SRT_EXCHANGE_SHARE, SRT_ROWS_CONTIGUOUS, SRT_ROWS_INTERLEAVED, SRT_ROWS_ROTATED, SRT_SPLIT_BANDS, SRT_SPLIT_FRAMES, EngineOptions)
 from .device import TRACE_VARIANTS, SrtError
 
 EXCHANGES = {"alltoall": SRT_EXCHANGE_ALLTOALL, "rotating": SRT_EXCHANGE_ROTATING, "root": SRT_EXCHANGE_ROOT,
              "share": SRT_EXCHANGE_SHARE}
-ROWS = {"interleaved": SRT_ROWS_INTERLEAVED, "contiguous": SRT_ROWS_CONTIGUOUS}
+ROWS = {"interleaved": SRT_ROWS_INTERLEAVED, "contiguous": SRT_ROWS_CONTIGUOUS, "rotated": SRT_ROWS_ROTATED}
 SPLITS = {"bands": SRT_SPLIT_BANDS, "frames": SRT_SPLIT_FRAMES}
 
 
@@ -33,7 +33,8 @@ def _check(rc: int):
 
 
 def _options(variant, queues, batch, rows, exchange, split, simulate=False, launch=0, rccl_self=False, share=0):
-    return EngineOptions(TRACE_VARIANTS[variant], queues, batch, ROWS[rows], EXCHANGES[exchange], SPLITS[split],
+    return EngineOptions(ctypes.sizeof(EngineOptions), TRACE_VARIANTS[variant], queues, batch, ROWS[rows],
+                         EXCHANGES[exchange], SPLITS[split],
                          1 if simulate else 0, launch, SRT_ENGINE_RCCL_SELF if rccl_self else 0, share)
 
 
@@ -160,11 +161,14 @@ def pool_self_test(workers: int, failing: int, mode: str = "fail", timeout_s: fl
     return msg.value.decode(), el.value, calls.value
 
 
-def exchange_host(band_ids, height: int, rows: str = "interleaved", exchange: str = "alltoall", batch_index: int = 0):
+def exchange_host(band_ids, height: int, rows: str = "interleaved", exchange: str = "alltoall", batch_index: int = 0,
+                  share: int = 0):
     """Host self-test of the engine's band exchange (no device): band_ids = list of P arrays
-    (batch, buffer_rows, W) int32, band d's ids of a batch's frames. Returns the list of every
-    compositor's receive buffer, (P, frames composited there, buffer_rows, W) int32, exactly as the
-    device path lays it out for the shading launch."""
+    (batch, buffer_rows, W) int32, band d's ids of a batch's frames (rotated rows: of frame f the band
+    bands.rotated_band(P, d, f % P); share: device d's sender class of frame f, share + (d - f % P - 1)
+    % P, unused when d composites f). Returns the list of every compositor's receive buffer, (P, frames
+    composited there, buffer_rows, W) int32, exactly as the device path lays it out for the shading
+    launch. share: the share exchange's tile rows per cycle (0: srtShareAuto)."""
     import numpy as np
 
     lib = _native.lib()
@@ -172,8 +176,15 @@ def exchange_host(band_ids, height: int, rows: str = "interleaved", exchange: st
     batch, _, width = band_ids[0].shape
     frames = (ctypes.c_size_t * P)()
     brows = ctypes.c_size_t()
-    _check(lib.srtExchangeHost(None, P, width, height, ROWS[rows], EXCHANGES[exchange], batch, batch_index, None,
-                               frames, ctypes.byref(brows)))
+
+    def call(inp, outp):
+        if exchange == "share":
+            return lib.srtExchangeHostShare(inp, P, width, height, share, batch, batch_index, outp, frames,
+                                            ctypes.byref(brows))
+        return lib.srtExchangeHost(inp, P, width, height, ROWS[rows], EXCHANGES[exchange], batch, batch_index, outp,
+                                   frames, ctypes.byref(brows))
+
+    _check(call(None, None))
     ins = [np.ascontiguousarray(b, dtype=np.int32) for b in band_ids]
     for b in ins:
         if b.shape != (batch, brows.value, width):
@@ -181,6 +192,5 @@ def exchange_host(band_ids, height: int, rows: str = "interleaved", exchange: st
     outs = [np.empty((P, frames[c], brows.value, width), np.int32) for c in range(P)]
     inp = (ctypes.c_void_p * P)(*[b.ctypes.data for b in ins])
     outp = (ctypes.c_void_p * P)(*[o.ctypes.data for o in outs])
-    _check(lib.srtExchangeHost(inp, P, width, height, ROWS[rows], EXCHANGES[exchange], batch, batch_index, outp,
-                               frames, ctypes.byref(brows)))
+    _check(call(inp, outp))
     return outs

@@ -1,8 +1,11 @@
 """Row-band partition (simpleraytracer_amd.bands, the Python restatement of csrc/engine.cpp
-BandSplit), the shading kernel's unscrambling of gathered bands, and bench.py's multi-rank control
-plane on CPU with gloo (world size 2 and 3): the RCCL unique id shared from rank 0, max-over-ranks
-timing and the per-rank report gather. The data path itself is native (tests/test_exchange_plan.py
-on host memory, tests/test_gpu_engine.py on the GPU).
+BandSplit), the shading kernel's unscrambling of gathered bands, bench.py's multi-rank control
+plane on CPU with gloo (world size 2 and 3: the RCCL unique id shared from rank 0, max-over-ranks
+timing and the per-rank report gather), and the band data plane over gloo (world sizes 2 and 3):
+real band ids moved between processes in the engine's all-to-all and share layouts, the oracle
+standing in for the GPU stages, checked against the library's layout and the single-process frame.
+The product data path is native (tests/test_exchange_plan.py on host memory, tests/test_gpu_engine.py
+on the GPU).
 """
 from __future__ import annotations
 
@@ -187,3 +190,112 @@ def test_bench_job_single_process(monkeypatch):
     monkeypatch.setenv("WORLD_SIZE", "2")
     with pytest.raises(SystemExit):
         bench.Job(SimpleNamespace(gpus=4))
+
+
+def _rows_ids(oracle, w, h, offs, rows):
+    """The oracle standing in for a rank's trace: hit ids of `rows` (band order), rendering only them
+    (one oracle call per run of consecutive rows)."""
+    out = np.full((len(rows), w), -3, np.int32)
+    i = 0
+    while i < len(rows):
+        j = i
+        while j + 1 < len(rows) and rows[j + 1] == rows[j] + 1:
+            j += 1
+        fr = oracle.render(w, h, offs, row_begin=int(rows[i]), row_count=j - i + 1, threads=1)
+        out[i:j + 1] = fr[rows[i]:rows[j] + 1, :, 3].astype(np.int32)
+        i = j + 1
+    return out
+
+
+def _data_plane_worker(rank, world, port, out_dir, scene, exchange, rows_mode, share):
+    """One rank of a world-size job moving real band ids over gloo in the engine's layout (the
+    restated ExchangePlan: send regions per compositor, receive slots per sender), the oracle standing
+    in for the GPU trace and the deferred shading. Checks: the receive buffer equals the library's
+    own layout of every rank's bands (srtExchangeHost / srtExchangeHostShare), and every frame this
+    rank composites equals the single-process render bit for bit."""
+    sys.path.insert(0, REPO)
+    import torch
+    import torch.distributed as dist
+
+    from oracle.srt_oracle import OracleScene
+    from simpleraytracer_amd.bands import ExchangePlan, share_auto, traced_rows
+    from simpleraytracer_amd.engine import exchange_host
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    w, h, F = 21, 70, 2 * world
+    k = (share or share_auto(h, world)) if exchange == "share" else 0
+    plan = ExchangePlan(world, F, exchange, rows_mode)
+    oracle = OracleScene(scene)
+    offs = [np.random.default_rng(900 + f).random((h, w, 2), dtype=np.float32) for f in range(F)]
+    rows = {(d, c): traced_rows(h, world, exchange, rows_mode, d, c, k) for d in range(world) for c in range(world)}
+    senders = [(d, c) for d in range(world) for c in range(world) if not (exchange == "share" and d == c)]
+    brows = max(1, max(len(rows[d, c]) for d, c in senders))
+    # this rank's traces of the batch, frame-major (the engine's trace phase; its own frames too)
+    mine = np.full((F, brows, w), -7, np.int32)
+    for f in range(F):
+        c = plan.compositor(f)
+        if not (exchange == "share" and c == rank):
+            r = rows[rank, c]
+            mine[f, :len(r)] = _rows_ids(oracle, w, h, offs[f], r)
+    send = np.full((world * plan.max_frames(), brows, w), -7, np.int32)
+    for f in range(F):
+        send[plan.send_frame(plan.compositor(f), plan.slot(f))] = mine[f]
+    n = plan.frames_for(rank)
+    recv = np.full((world, n, brows, w), -1, np.int32)
+    # the exchange: one send / receive pair per peer (the engine's ncclSend / ncclRecv group)
+    reqs, bufs = [], {}
+    for p in range(world):
+        if p == rank:
+            if exchange != "share":
+                recv[plan.recv_slot(rank, rank)] = send[plan.send_frame(rank, 0):plan.send_frame(rank, 0) + n]
+            continue
+        n_p = plan.frames_for(p)
+        s0 = plan.send_frame(p, 0)
+        reqs.append(dist.isend(torch.from_numpy(np.ascontiguousarray(send[s0:s0 + n_p])), dst=p))
+        bufs[p] = torch.empty((n, brows, w), dtype=torch.int32)
+        reqs.append(dist.irecv(bufs[p], src=p))
+    for q in reqs:
+        q.wait()
+    for p, t in bufs.items():
+        recv[plan.recv_slot(rank, p)] = t.numpy()
+    # the library's layout of every rank's bands must be what arrived
+    every = [None] * world
+    dist.all_gather_object(every, mine)
+    lib = exchange_host(every, h, rows_mode if exchange != "share" else "interleaved", exchange, share=k)
+    if exchange == "share":  # the slot of the compositor itself is not a sender's: not compared
+        assert np.array_equal(lib[rank][:world - 1], recv[:world - 1])
+    else:
+        assert np.array_equal(lib[rank], recv)
+    # deferred shading of this rank's frames from the received ids (and its own rows)
+    for f in range(rank, F, world):
+        ref = oracle.render(w, h, offs[f], threads=1)
+        ids = np.full((h, w), -5, np.int32)
+        for d in range(world):
+            r = rows[d, rank]
+            if d == rank:
+                ids[r] = ref[r, :, 3].astype(np.int32)  # the compositor's own rows, traced to RGBA
+            else:
+                ids[r] = recv[plan.recv_slot(rank, d), plan.slot(f), :len(r)]
+        got = oracle.shade(w, h, ids, offs[f])
+        assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), (rank, f)
+    dist.barrier()
+    open(os.path.join(out_dir, f"ok{rank}"), "w").close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("exchange,rows,share", [("alltoall", "interleaved", 0), ("alltoall", "rotated", 0),
+                                                 ("alltoall", "contiguous", 0), ("share", "interleaved", 0),
+                                                 ("share", "interleaved", 1)])
+def test_band_data_plane_over_gloo(tmp_path, scenes, world, exchange, rows, share):
+    """The multi-process band data plane on CPU (world sizes 2 and 3): real band ids move between
+    processes over gloo in the engine's all-to-all (interleaved, contiguous, rotated) and share
+    layouts, the oracle standing in for the GPU stages; every composited frame equals the
+    single-process render (the device path of the same layout: tests/test_gpu_engine.py)."""
+    import torch.multiprocessing as mp
+
+    mp.start_processes(_data_plane_worker,
+                       args=(world, _free_port(), str(tmp_path), scenes["soup300"], exchange, rows, share),
+                       nprocs=world, join=True, start_method="spawn")
+    assert sorted(os.listdir(tmp_path)) == [f"ok{r}" for r in range(world)]

@@ -12,7 +12,8 @@ from __future__ import annotations
 import numpy as np
 import pytest
 
-from simpleraytracer_amd.bands import TILE_ROWS, band_range, band_rows, interleaved_frame_rows, interleaved_range
+from simpleraytracer_amd.bands import (TILE_ROWS, band_range, band_rows, interleaved_frame_rows, interleaved_range,
+                                      rotated_band)
 from simpleraytracer_amd.engine import exchange_host
 
 
@@ -49,11 +50,18 @@ def slot(exchange, p, f):
     return f // p if exchange == "alltoall" else f
 
 
-@pytest.mark.parametrize("rows", ["interleaved", "contiguous"])
+def traced_band(rows, exchange, p, b, d, f):
+    """The band device d traces of frame f of batch b (rotated: by the frame's compositor)."""
+    return rotated_band(p, d, compositor(exchange, p, b, f)) if rows == "rotated" and p > 1 else d
+
+
+@pytest.mark.parametrize("rows", ["interleaved", "contiguous", "rotated"])
 @pytest.mark.parametrize("exchange", ["alltoall", "rotating", "root"])
 @pytest.mark.parametrize("p,h,frames,b", [(1, 37, 3, 0), (2, 70, 4, 1), (3, 37, 8, 2), (4, 170, 3, 5),
                                           (8, 170, 16, 3), (8, 10, 5, 1), (3, 33, 1, 4)])
 def test_exchange_layout_reassembles_every_frame(rows, exchange, p, h, frames, b):
+    if rows == "rotated" and exchange != "alltoall":
+        pytest.skip("rotated bands are an all-to-all layout")
     w = 7
     fr, brows = split_rows(h, p, rows)
     # frame f's "ids": a unique value per (frame, row, column)
@@ -61,7 +69,9 @@ def test_exchange_layout_reassembles_every_frame(rows, exchange, p, h, frames, b
     bands = []
     for r in range(p):
         buf = np.full((frames, brows, w), -7, np.int32)
-        buf[:, :len(fr[r])] = truth[:, fr[r]]
+        for f in range(frames):
+            j = traced_band(rows, exchange, p, b, r, f)
+            buf[f, :len(fr[j])] = truth[f, fr[j]]
         bands.append(buf)
     recv = exchange_host(bands, h, rows, exchange, batch_index=b)
     seen = set()
@@ -96,7 +106,8 @@ def test_exchange_rejects_wrong_buffers():
 
 
 @pytest.mark.parametrize("p,rows,exchange", [(2, "interleaved", "alltoall"), (3, "contiguous", "alltoall"),
-                                             (4, "interleaved", "rotating"), (3, "interleaved", "root")])
+                                             (4, "interleaved", "rotating"), (3, "interleaved", "root"),
+                                             (3, "rotated", "alltoall"), (4, "rotated", "alltoall")])
 def test_oracle_batch_through_the_exchange(scenes, p, rows, exchange):
     """The engine's band path with CPU stand-ins: band r of every frame traced by the oracle (hit
     ids), exchanged by srtExchangeHost, each compositor shading its frames from the unscrambled ids
@@ -111,7 +122,9 @@ def test_oracle_batch_through_the_exchange(scenes, p, rows, exchange):
     bands = []
     for r in range(p):
         buf = np.full((frames, brows, w), -5, np.int32)
-        buf[:, :len(fr[r])] = np.stack([ref[fr[r], :, 3] for ref in refs]).astype(np.int32)
+        for f in range(frames):
+            j = traced_band(rows, exchange, p, 1, r, f)
+            buf[f, :len(fr[j])] = refs[f][fr[j], :, 3].astype(np.int32)
         bands.append(buf)
     recv = exchange_host(bands, h, rows, exchange, batch_index=1)
     for f in range(frames):
@@ -119,3 +132,54 @@ def test_oracle_batch_through_the_exchange(scenes, p, rows, exchange):
         ids = unscramble(recv[c], slot(exchange, p, f), h, rows)
         got = oracle.shade(w, h, ids, offs[f])
         assert np.array_equal(got.view(np.uint32), refs[f].view(np.uint32)), f
+
+
+def unscramble_share(recv, g, h, share, own_rows):
+    """Frame g of a share compositor's receive buffer (P, frames, B, W), ShadeIdsKernel's mapping
+    (ShadeRowOf with own_bands = share over share + P - 1 interleaved classes): row y in tile row
+    t = y / 16 is class t % classes; classes below `share` are the compositor's own (traced to RGBA,
+    taken from own_rows here), class k >= share is at slot k - share, local row (t / classes) * 16 +
+    y % 16."""
+    p, frames, b, w = recv.shape
+    classes = share + p - 1
+    out = np.array(own_rows, copy=True)
+    for y in range(h):
+        t = y // TILE_ROWS
+        k = t % classes
+        if k >= share:
+            out[y] = recv[k - share, g, (t // classes) * TILE_ROWS + y % TILE_ROWS]
+    return out
+
+
+@pytest.mark.parametrize("p,h,share,frames,b", [(2, 230, 4, 4, 0), (2, 230, 1, 2, 3), (3, 230, 2, 6, 1),
+                                                (4, 170, 8, 8, 2), (8, 1080, 32, 16, 0), (8, 230, 2, 8, 5),
+                                                (2, 230, 16, 4, 1), (3, 100, 0, 3, 0)])
+def test_share_exchange_layout_reassembles_every_frame(p, h, share, frames, b):
+    """The share exchange on host memory (srtExchangeHostShare: the engine's ExchangePlan with its
+    SendFrames / RecvSlot, the same functions ExchangePhase's ncclSend / ncclRecv offsets and
+    CopyPhase's copies take): every sender's class rows of every frame land where the compositor's
+    deferred shading reads them; with the compositor's own classes, every frame is whole. share = 16
+    at P = 2: a cycle of 17 tile rows is longer than the 15-row frame, so the sender's band is empty;
+    share = 0: srtShareAuto."""
+    from simpleraytracer_amd.bands import share_auto, share_frame_rows
+
+    w = 5
+    k = share or share_auto(h, p)
+    truth = np.arange(frames * h * w, dtype=np.int32).reshape(frames, h, w)
+    rows = {(d, c): share_frame_rows(h, p, k, d, c) for d in range(p) for c in range(p)}
+    brows = max(1, max(len(rows[d, c]) for d in range(p) for c in range(p) if d != c))  # sender classes only
+    bands = []
+    for d in range(p):
+        buf = np.full((frames, brows, w), -7, np.int32)
+        for f in range(frames):
+            c = f % p
+            if d != c:
+                buf[f, :len(rows[d, c])] = truth[f, rows[d, c]]
+        bands.append(buf)
+    recv = exchange_host(bands, h, "interleaved", "share", batch_index=b, share=share)
+    for f in range(frames):
+        c = f % p
+        own = np.full((h, w), -9, np.int32)
+        own[rows[c, c]] = truth[f, rows[c, c]]
+        got = unscramble_share(recv[c], f // p, h, k, own)
+        assert np.array_equal(got, truth[f]), (c, f)

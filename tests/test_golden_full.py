@@ -171,3 +171,19 @@ def test_gpu_engine_bands_reproduce_full_c3_fixture(gpu, paths, ids):
         e.run(1)
         for k in (0, 5):  # composited on devices 0 and 5
             assert_full_parity(e.read_frame(k), paths[name], m, ids[name], name)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("p", [2, 8])
+def test_gpu_engine_rotated_bands_reproduce_full_c3_fixture(gpu, paths, ids, p):
+    """The headline frame as P rotated contiguous bands (all-to-all, the band record pass skipping the
+    record blocks that cannot reach a band; fake devices on one GPU), every pixel of every frame."""
+    from simpleraytracer_amd.engine import FrameEngine
+
+    name = "c3_soup100k_1080p"
+    m = META[name]
+    with FrameEngine(paths[name], m["width"], m["height"], devices=[0] * p, batch=p, queues=1, rows="rotated") as e:
+        e.set_inputs(offsets_for(m))
+        e.run(1)
+        for k in range(p):  # composited on every device: every device traced every band once
+            assert_full_parity(e.read_frame(k), paths[name], m, ids[name], name)

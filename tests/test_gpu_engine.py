@@ -85,6 +85,32 @@ def test_engine_fake_devices_share_bitwise(gpu, scenes, p, share, queues):
         assert e.info()["exchange_bytes_per_frame"] > 0
 
 
+@pytest.mark.parametrize("p,h", [(2, 100), (3, 100), (8, 230), (4, 61)])
+def test_engine_fake_devices_rotated_bitwise(gpu, scenes, p, h):
+    """Rotated contiguous bands (device d traces band (d + c) % P of a frame composited on device c;
+    the band record pass skipping the record blocks that cannot reach the band): distinct inputs per
+    frame, every frame of the resident batches equal to a one-device render, bit for bit. h = 100 at
+    P = 3: bands of 34, 34 and 32 rows (two launch groups); h = 61 at P = 4: 16, 16, 16, 13."""
+    w, F = 130, 2 * p
+    inputs = random_inputs(2 * F, h, w, seed=31 + p)
+    refs = [torch_render(scenes["soup2k"], w, h, inputs[k]) for k in range(2 * F)]
+    with engine(scenes["soup2k"], w, h, devices=[0] * p, rows="rotated", exchange="alltoall", queues=2,
+                batch=F) as e:
+        e.set_inputs(inputs)
+        e.run(3)
+        for k in range(F, 3 * F):
+            got = e.read_frame(k)
+            assert np.array_equal(got.view(np.uint32), refs[k % (2 * F)].view(np.uint32)), k
+        assert e.verify() == (0, 2 * F)
+
+
+def test_engine_rotated_needs_alltoall(gpu, scenes):
+    from simpleraytracer_amd.device import SrtError
+
+    with pytest.raises(SrtError, match="rotated bands"):
+        engine(scenes["soup300"], 40, 40, devices=[0, 0], rows="rotated", exchange="share")
+
+
 def test_engine_fake_devices_rotating_inputs(gpu, scenes):
     """Distinct inputs per frame through the all-to-all exchange (the compositors' strided offsets)."""
     w, h, p, F = 70, 90, 2, 4
@@ -131,6 +157,21 @@ def test_engine_c3_bands_of_8_bitwise(gpu, scenes):
     assert_parity(got, ref, rows=rows)
 
 
+def test_engine_c3_rotated_bands_of_8_bitwise(gpu, scenes):
+    """The headline frame as 8 rotated contiguous bands of 135 rows (all-to-all; each device skips
+    the record blocks that cannot reach its band): every frame equals the one-device frame."""
+    w, h = 1920, 1080
+    inputs = np.full((1, h, w, 2), 0.5, np.float32)
+    with engine(scenes["soup100k"], w, h, devices=[0] * 8, batch=16, queues=2, rows="rotated") as e:
+        e.set_inputs(inputs)
+        e.run(2)
+        assert e.verify() == (0, 32)
+        got = e.read_frame(19)
+    rows = np.arange(5, 1080, 90)
+    ref = oracle_render(scenes["soup100k"], w, h, row_begin=5, row_count=1075, row_step=90)
+    assert_parity(got, ref, rows=rows)
+
+
 @pytest.mark.parametrize("p", [2, 8])
 def test_engine_c3_share_bitwise(gpu, scenes, p):
     """The headline frame over P fake devices with the share exchange at the library's k (32 at 1080p:
@@ -145,7 +186,10 @@ def test_engine_c3_share_bitwise(gpu, scenes, p):
         got = e.read_frame(16 * p + 3)  # a frame of the last batch (resident on its compositor)
         xb = e.info()["exchange_bytes_per_frame"]
     classes = 32 + p - 1
-    sent = (p - 1) * -(-68 // classes)  # the senders' band buffers: ceil(68 / classes) tile rows each
+    # the senders' band buffers: their largest class's tile rows (P = 2: tile rows 32 and 65 of class
+    # 32; P = 8: one) -- not class 0's (2 at P = 8: the padding of round 4)
+    per = max(len(range(k, 68, classes)) for k in range(32, classes))
+    sent = (p - 1) * per
     assert xb <= sent * 16 * w * 2.2, xb
     rows = np.arange(5, 1080, 90)
     ref = oracle_render(scenes["soup100k"], w, h, row_begin=5, row_count=1075, row_step=90)

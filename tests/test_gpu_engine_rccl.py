@@ -117,7 +117,7 @@ def _gpus():
     return torch.cuda.device_count()
 
 
-@pytest.mark.parametrize("exchange", ["alltoall", "rotating", "root", "share"])
+@pytest.mark.parametrize("exchange", ["alltoall", "rotating", "root", "share", "rotated"])
 @pytest.mark.parametrize("which", ["2", "all"])
 def test_engine_rccl_bands_full_c3_fixture(gpu, paths, ids, exchange, which):
     """Distinct GPUs, RCCL between them (BASELINE config C4): P = 2 and P = every visible GPU (at most
@@ -129,7 +129,8 @@ def test_engine_rccl_bands_full_c3_fixture(gpu, paths, ids, exchange, which):
     P = 2 if which == "2" else min(8, n)
     m = META[C3]
     want = Expected(paths[C3], C3, ids[C3])
-    with engine(paths[C3], m, devices=list(range(P)), batch=2 * P, queues=2, exchange=exchange) as e:
+    kw = {"exchange": "alltoall", "rows": "rotated"} if exchange == "rotated" else {"exchange": exchange}
+    with engine(paths[C3], m, devices=list(range(P)), batch=2 * P, queues=2, **kw) as e:
         assert e.info()["rccl"] and e.info()["devices"] == P
         e.set_inputs(offsets_for(m))
         e.run(3)

@@ -253,10 +253,9 @@ def test_cull_survivor_overflow_and_ties(gpu, tmp_path, monkeypatch):
     assert_parity(torch_render(path, 300, 40, variant="bvh"), ref)
 
 
-def test_cull_nasty_geometry(gpu, tmp_path, monkeypatch):
-    """Triangles around and behind the eye, crossing the camera plane, slivers, needles, huge
-    and tiny ones, near edge-on: the screen boxes (bounded-region case) and the unbounded
-    fallback must never drop a record some ray hits."""
+def nasty_scene(tmp_path):
+    """Triangles around and behind the eye, crossing the camera plane, slivers, needles, huge and tiny
+    ones, near edge-on (test_cull_nasty_geometry; also the band skip tests)."""
     rng = np.random.default_rng(23)
     tris = []
     for _ in range(600):  # crossing / behind / around the eye
@@ -271,7 +270,14 @@ def test_cull_nasty_geometry(gpu, tmp_path, monkeypatch):
         a = rng.uniform([-1, -1, 0.05], [1, 1, 50])
         tris.append(list(np.concatenate([a, a + rng.normal(size=3) * 1e-3, a + rng.normal(size=3) * 1e-3])))
     albedo = rng.uniform(0.2, 1.0, (len(tris), 3))
-    path = write_custom_scene(tmp_path / "nasty.srt", tris, albedo)
+    return write_custom_scene(tmp_path / "nasty.srt", tris, albedo)
+
+
+def test_cull_nasty_geometry(gpu, tmp_path, monkeypatch):
+    """Triangles around and behind the eye, crossing the camera plane, slivers, needles, huge
+    and tiny ones, near edge-on: the screen boxes (bounded-region case) and the unbounded
+    fallback must never drop a record some ray hits."""
+    path = nasty_scene(tmp_path)
     rng2 = np.random.default_rng(8)
     offsets = rng2.random((90, 120, 2), dtype=np.float32)
     for off in (None, offsets):
@@ -970,3 +976,31 @@ def test_split_width_full_frame_bitwise(gpu, scenes, monkeypatch, chunks):
         monkeypatch.setenv("SRT_CULL_CHUNKS", chunks)
         got = torch_render(scenes["soup100k"], 1920, 1080, offs, variant="cull")
         assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+
+
+@pytest.mark.parametrize("world,rows,exchange", [(3, "rotated", "alltoall"), (8, "rotated", "alltoall"),
+                                                 (4, "interleaved", "alltoall"), (3, "interleaved", "share")])
+@pytest.mark.parametrize("kind", ["uniform", "random"])
+def test_band_block_skip_nasty_geometry(gpu, tmp_path, world, rows, exchange, kind):
+    """The band record pass skips 256-record blocks whose screen-box y extent (render.hip
+    LaunchBlockExtents) meets none of the band's rows (BandMayReach): nasty geometry (records around
+    and behind the eye with unbounded boxes, slivers whose boxes the float solve pads) and the dense
+    soup, in contiguous rotated bands, interleaved bands and the share pattern over fake devices,
+    every frame against the oracle. Offsets in [0, 1] (the skip applies) and, in the last frame of
+    each batch, outside it (the range tag turns the skip off)."""
+    from simpleraytracer_amd.engine import FrameEngine
+
+    w, h = 150, 230
+    F = 2 * world
+    rng = np.random.default_rng(world)
+    inputs = (np.full((F, h, w, 2), 0.5, np.float32) if kind == "uniform"
+              else rng.random((F, h, w, 2), dtype=np.float32))
+    inputs[F - 1, 3, 7] = (1.5, -0.25)  # one offset outside [0, 1]: that frame's bands are range-tagged
+    path = nasty_scene(tmp_path)
+    refs = [oracle_render(path, w, h, inputs[k]) for k in range(F)]
+    with FrameEngine(path, w, h, devices=[0] * world, rows=rows, exchange=exchange, queues=2, batch=F) as e:
+        e.set_inputs(inputs)
+        e.run(2)
+        for k in range(2 * F):
+            assert_parity(e.read_frame(k), refs[k % F])
+        assert e.verify() == (0, 2 * F)

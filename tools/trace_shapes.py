@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""Per-launch-shape summary of a rocprofv3 --kernel-trace run: one row per (kernel, grid), so the
+headline launch shape (8 frames per TraceCullKernel launch = the largest grid) has its own mean
+instead of one average over every shape of the run (VERDICT r04 "What's weak" 5).
+
+    python tools/trace_shapes.py gpurun_out/l8_trace [--kernel TraceCullKernel] [--csv out.csv]
+
+Durations are End - Start of each dispatch in the trace CSV (ns), reported in us.
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import glob
+import re
+import statistics
+import sys
+
+
+def short(name: str) -> str:
+    m = re.search(r"(\w+)(<[^(]*)?\(", name)
+    return m.group(1) if m else name[:40]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dirs", nargs="+")
+    ap.add_argument("--kernel", default="", help="only kernels whose name contains this")
+    ap.add_argument("--csv", default="", help="write the table as CSV here")
+    a = ap.parse_args()
+    rows = []
+    for d in a.dirs:
+        files = glob.glob(f"{d}/**/*kernel_trace.csv", recursive=True)
+        if not files:
+            print(f"== {d}: no kernel_trace.csv", file=sys.stderr)
+            continue
+        groups = {}
+        for f in files:
+            for r in csv.DictReader(open(f, newline="")):
+                if a.kernel and a.kernel not in r["Kernel_Name"]:
+                    continue
+                key = (short(r["Kernel_Name"]), int(r["Grid_Size_X"]), int(r["Grid_Size_Y"]), int(r["Grid_Size_Z"]))
+                groups.setdefault(key, []).append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+        for (k, gx, gy, gz), ds in sorted(groups.items(), key=lambda kv: -sum(kv[1])):
+            rows.append({"dir": d, "kernel": k, "grid": f"{gx}x{gy}x{gz}", "calls": len(ds),
+                         "mean_us": round(statistics.fmean(ds), 3), "median_us": round(statistics.median(ds), 3),
+                         "min_us": round(min(ds), 3), "max_us": round(max(ds), 3),
+                         "total_ms": round(sum(ds) / 1e3, 3)})
+    for r in rows:
+        print(f"{r['kernel']:24s} grid {r['grid']:>16s} calls {r['calls']:6d} mean {r['mean_us']:9.2f} "
+              f"median {r['median_us']:9.2f} min {r['min_us']:9.2f} max {r['max_us']:9.2f} us  tot {r['total_ms']:9.3f} ms")
+    if a.csv and rows:
+        with open(a.csv, "w", newline="") as fh:
+            w = csv.DictWriter(fh, fieldnames=list(rows[0]))
+            w.writeheader()
+            w.writerows(rows)
+
+
+if __name__ == "__main__":
+    main()
