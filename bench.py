@@ -82,8 +82,10 @@ def parse():
     p.add_argument("--share", type=int, default=0,
                    help="share exchange: the compositor's tile rows per cycle of share + N - 1, a power of two "
                         "(0: the library's srtShareAuto, 32 at 1080p)")
-    p.add_argument("--rows", default="interleaved", choices=["interleaved", "contiguous"],
-                   help="bands: each GPU's rows, the frame's 16-row tile rows dealt round-robin or one block")
+    p.add_argument("--rows", default="auto", choices=["auto", "interleaved", "contiguous", "rotated"],
+                   help="bands: each GPU's rows -- the frame's 16-row tile rows dealt round-robin (interleaved), one "
+                        "block (contiguous), or one block per GPU rotated by the frame's compositor (rotated; "
+                        "all-to-all only); auto: rotated for all-to-all, interleaved otherwise")
     p.add_argument("--queues", type=int, default=int(os.environ.get("SRT_BENCH_QUEUES", "2")),
                    help="batches in flight per GPU (own scene buffers and HIP stream each)")
     p.add_argument("--offsets", default="uniform", choices=["uniform", "random"],
@@ -98,12 +100,14 @@ def parse():
     p.add_argument("--no-extras", action="store_true", help="only the main line (no secondary legs)")
     a = p.parse_args()
     if a.exchange == "auto":
-        # share: frame f's compositor (GPU f % N) traces k of every k + N - 1 tile rows itself, fused
-        # with the shading (k = 32 at 1080p), and the others one each: fewer rows take the ids path
-        # (trace to ids, exchange, deferred shading) than under alltoall, which sends (N - 1) / N of
-        # every frame. Rank simulation, us of GPU time per frame: N = 2 9.9 vs
-        # 13.2 (alltoall, link-bound besides), N = 4 5.8 vs 8.2, N = 8 3.7 vs 4.8.
-        a.exchange = "share"
+        # Even framebuffer tiling (north_star: tiles over the GPUs + a gather): every frame split into
+        # N contiguous bands of H / N rows, GPU d tracing band (d + c) % N of a frame composited on GPU
+        # c = f % N (even load over any N frames), the bands' hit ids exchanged all-to-all. share
+        # (the compositor tracing k of every k + N - 1 tile rows itself) and frames (whole frames
+        # per GPU, no exchange) are legs beside it.
+        a.exchange = "alltoall"
+    if a.rows == "auto":
+        a.rows = "rotated" if a.exchange == "alltoall" else "interleaved"
     return a
 
 
@@ -398,6 +402,74 @@ def whole_frame_fields(W, H, n_tri, ms_per_frame, world):
                     "the timed (overlapped) run; peak = 8 TB/s x GPUs"}
 
 
+def compositor_fraction(H, world, exchange, rows, share):
+    """Fraction of a frame's rows its compositor traces itself (straight into the frame as RGBA); the
+    rest arrives as hit ids from the other GPUs."""
+    from simpleraytracer_amd import _native
+    from simpleraytracer_amd.bands import band_range, interleaved_range, share_frame_rows
+
+    if exchange == "share":
+        k = share or _native.lib().srtShareAuto(H, world)
+        return round(len(share_frame_rows(H, world, k, 0, 0)) / H, 5)
+    if rows == "interleaved":
+        return round(interleaved_range(H, world, 0)[1] / H, 5)
+    return round(band_range(H, world, 0)[1] / H, 5)
+
+
+def host_link_peaks(nbytes=64 << 20, reps=8):
+    """Pinned host <-> device copy rates on this box (hipMemcpyAsync through torch's pinned copies, the
+    path mlInfer's chunk pipeline takes): H2D alone, D2H alone, and both at once on two streams
+    (duplex). GB/s; the e2e_ml_api roofline's denominator (measured, not the PCIe Gen5 x16 spec)."""
+    import torch
+
+    h_in = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+    h_out = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+    d_a = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    d_b = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    s_in, s_out = torch.cuda.Stream(), torch.cuda.Stream()
+
+    def run(h2d, d2h):
+        for _ in range(2):  # warm-up
+            if h2d:
+                with torch.cuda.stream(s_in):
+                    d_a.copy_(h_in, non_blocking=True)
+            if d2h:
+                with torch.cuda.stream(s_out):
+                    h_out.copy_(d_b, non_blocking=True)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            if h2d:
+                with torch.cuda.stream(s_in):
+                    d_a.copy_(h_in, non_blocking=True)
+            if d2h:
+                with torch.cuda.stream(s_out):
+                    h_out.copy_(d_b, non_blocking=True)
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0
+
+    t_in, t_out, t_both = run(True, False), run(False, True), run(True, True)
+    gbs = lambda b, t: round(b / t / 1e9, 2)
+    return {"h2d_gbs": gbs(nbytes * reps, t_in), "d2h_gbs": gbs(nbytes * reps, t_out),
+            "duplex_gbs_each": gbs(nbytes * reps, t_both), "duplex_gbs_total": gbs(2 * nbytes * reps, t_both),
+            "bytes_per_copy": nbytes, "copies": reps,
+            "note": "torch pinned copies (hipMemcpyAsync) on two non-default streams, wall time of `copies` copies "
+                    "after 2 untimed; duplex = H2D and D2H concurrently"}
+
+
+def e2e_roofline(e2e, peaks, W, H, in_bytes_px=8, out_bytes_px=16):
+    """mlInfer's host-link roofline: its bytes in and out over the measured copy peaks. floor_duplex_ms =
+    max(in / H2D, out / D2H) at the duplex rates (copies overlap perfectly, the render hidden);
+    floor_serial_ms = in / H2D + out / D2H at the one-way rates; frac = floor_duplex / measured."""
+    bin_, bout = W * H * in_bytes_px, W * H * out_bytes_px
+    each = peaks["duplex_gbs_each"] * 1e9
+    duplex = max(bin_ / each, bout / each) * 1e3
+    serial = (bin_ / (peaks["h2d_gbs"] * 1e9) + bout / (peaks["d2h_gbs"] * 1e9)) * 1e3
+    return {"bytes_in": bin_, "bytes_out": bout, "floor_duplex_ms": round(duplex, 4), "floor_serial_ms": round(serial, 4),
+            "frac": round(duplex / e2e["ms_per_frame"], 4), "frac_serial": round(serial / e2e["ms_per_frame"], 4),
+            "achieved_gbs": round((bin_ + bout) / (e2e["ms_per_frame"] * 1e-3) / 1e9, 2)}
+
+
 def e2e_ml_api(scene_path, W, H, reps=10, warmup=3, devices=None):
     """PCIe-inclusive rate through the ml* API (host images in, host framebuffer out): median of
     `reps` frames after `warmup`. devices: ML_VISIBLE_DEVICES for a multi-GPU mlInfer."""
@@ -471,6 +543,10 @@ def main():
         ranks_stages = job.gather(list(st))
     else:  # every device of this process, in band order
         ranks_stages = [list(st)] + [list(eng.stage_times(i, n_stage)) for i in range(1, info["local_devices"])]
+    # the timed run's exchange, per device (HIP events on each device's exchange stream)
+    xstats = [eng.exchange_stats(i) for i in range(info["local_devices"])] if world > 1 else []
+    if job.ranked:
+        xstats = [x for r in job.gather(xstats) for x in r]
     eng.close()
     import simpleraytracer_amd as srt
 
@@ -521,19 +597,32 @@ def main():
                                                           "trace_kernel": round(tm, 5)},
                                             "note": "bit-identical frame (tests/test_gpu_parity.py)"}
     if world > 1 and extras:
+        main = (a.mode, a.exchange, a.rows)
         for name, kw in (("frames", {"mode": "frames"}),
-                         ("rotating_gather", {"exchange": "rotating"}),
-                         ("alltoall_exchange", {"exchange": "alltoall"}),
-                         ("contiguous_rows", {"rows": "contiguous", "exchange": "alltoall"})):
-            if (name == "frames" and a.mode == "frames") or (name == "rotating_gather" and a.exchange != "alltoall") \
-                    or (name == "alltoall_exchange" and a.exchange == "alltoall") \
-                    or (name == "contiguous_rows" and a.rows == "contiguous"):
+                         ("share_exchange", {"mode": "bands", "exchange": "share", "rows": "interleaved"}),
+                         ("interleaved_alltoall", {"mode": "bands", "exchange": "alltoall", "rows": "interleaved"}),
+                         ("rotated_alltoall", {"mode": "bands", "exchange": "alltoall", "rows": "rotated"})):
+            if (kw.get("mode"), kw.get("exchange", a.exchange), kw.get("rows", a.rows)) == main or \
+                    (name == "frames" and a.mode == "frames"):
                 continue
             try:
                 legs[name] = run_leg(job, a, path, inputs, a.steps, a.warmup, **kw)
                 legs[name]["scaling"] = "weak" if name == "frames" else "strong"
+                if name != "frames":
+                    legs[name]["compositor_fraction"] = compositor_fraction(H, world, kw["exchange"], kw["rows"],
+                                                                            a.share)
             except Exception as e:  # noqa: BLE001 -- the primary line must still be printed
                 legs[name] = {"error": f"{type(e).__name__}: {e}"}
+        if a.mode == "bands":
+            # one frame in flight across the N GPUs: the per-frame latency of the split
+            try:
+                legs["one_frame_in_flight"] = {
+                    **run_leg(job, a, path, inputs, min(a.steps * a.frames_per_step, 400), 20, queues=1, batch=1),
+                    "note": "one frame per batch, one batch in flight: every GPU traces its band of it, the bands "
+                            "are exchanged and composited on GPU 0 (per-frame latency across the N GPUs; "
+                            "single_queue at N = 1 is the one-GPU figure)"}
+            except Exception as e:  # noqa: BLE001
+                legs["one_frame_in_flight"] = {"error": f"{type(e).__name__}: {e}"}
 
     if rank == 0:
         band = world > 1 and a.mode == "bands"
@@ -613,8 +702,24 @@ def main():
                 share_k = a.share or _native.lib().srtShareAuto(H, world)
                 xb = info["exchange_bytes_per_frame"]
                 px = max(1, (world - 1) * info["buffer_rows"] * W)
-                line["exchange"] = {"pattern": a.exchange, "transport": "RCCL" if info["rccl"] else "device copies",
+                ms_x = [x["ms_mean"] for x in xstats if x["groups"]]
+                sent = [x["bytes_sent"] for x in xstats if x["groups"]]
+                ms_mean = sum(ms_x) / len(ms_x) if ms_x else None
+                per_link = (sum(sent) / len(sent)) / (world - 1) if sent else None
+                line["exchange"] = {"pattern": a.exchange, "rows": a.rows,
+                                    "transport": "RCCL" if info["rccl"] else "device copies",
                                     "share": share_k if a.exchange == "share" else None,
+                                    "compositor_fraction": compositor_fraction(H, world, a.exchange, a.rows, a.share),
+                                    "ms_per_batch": round(ms_mean, 5) if ms_mean else None,
+                                    "ms_per_batch_by_device": [round(x, 5) for x in ms_x],
+                                    "bytes_per_link_per_batch": int(per_link) if per_link else None,
+                                    "gbs_per_directed_link": round(per_link / (ms_mean * 1e-3) / 1e9, 2)
+                                    if ms_mean and per_link else None,
+                                    "timing_note": "HIP events on each GPU's exchange stream around every batch's "
+                                                   "ncclSend / ncclRecv group (device copies on fake devices), from the "
+                                                   "stream reaching the group to its end -- waits for late peers "
+                                                   "included, so the rate is a lower bound of the link's; per directed "
+                                                   "link = a GPU's bytes sent per batch / (N - 1)",
                                     "payload": "packed hit ids (16 + k bits per pixel: a u16 plane and k bit planes, "
                                                "render.h PackedIds) or int32 ids; deferred shading on the compositor, "
                                                "whose own band is traced to RGBA in place",
@@ -626,16 +731,32 @@ def main():
             line[k] = v
         if world == 1 and not a.no_e2e and extras:
             e2e, _ = e2e_ml_api(path, W, H)
+            peaks = host_link_peaks()
             line["e2e_ml_api"] = {**e2e, "path": "mlInfer: H2D offsets + trace + D2H framebuffer (pinned host images), "
-                                                 "4 row chunks pipelined over three streams"}
+                                                 "row chunks pipelined over three streams (SRT_E2E_CHUNKS)",
+                                  "host_link": peaks, "roofline": e2e_roofline(e2e, peaks, W, H)}
         if world > 1 and not job.ranked and not a.no_e2e and extras:
-            try:
-                e2e, _ = e2e_ml_api(path, W, H, devices=job.devices)
-                line["ml_multi"] = {**e2e, "devices": job.devices,
-                                    "path": "mlInfer over ML_VISIBLE_DEVICES: H2D band offsets + interleaved band traces "
-                                            "(hit ids) + gather to device 0 + shading + D2H"}
-            except Exception as e:  # noqa: BLE001
-                line["ml_multi"] = {"error": f"{type(e).__name__}: {e}"}
+            # the drop-in path over the N GPUs: the bands gathered to GPU 0 (RCCL; device copies on fake
+            # devices) and one D2H, or every GPU copying its rows straight into the host image (direct)
+            line["ml_multi"] = {}
+            old_gather = os.environ.get("SRT_GATHER")
+            for mode in ("copy" if job.one_device else "rccl", "direct"):
+                try:
+                    os.environ["SRT_GATHER"] = mode
+                    e2e, _ = e2e_ml_api(path, W, H, devices=job.devices)
+                    line["ml_multi"][mode] = {
+                        **e2e, "devices": job.devices,
+                        "path": ("mlInfer over ML_VISIBLE_DEVICES: H2D band offsets + interleaved band traces (hit ids) "
+                                 "+ gather to device 0 + shading + one D2H") if mode != "direct" else
+                                ("mlInfer over ML_VISIBLE_DEVICES: H2D band offsets + band traces + shading on every "
+                                 "device + per-device D2H into disjoint rows of the host image (no gather)")}
+                except Exception as e:  # noqa: BLE001
+                    line["ml_multi"][mode] = {"error": f"{type(e).__name__}: {e}"}
+                finally:
+                    if old_gather is None:
+                        os.environ.pop("SRT_GATHER", None)
+                    else:
+                        os.environ["SRT_GATHER"] = old_gather
         if world == 1 and not a.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(path, a)
         print(json.dumps(line), flush=True)

@@ -228,6 +228,12 @@ ML_API_ENTRY size_t srtShareAuto(size_t height, size_t devices);
  * band buffer, whether the exchange uses RCCL, exchanged bytes per frame (bands, all devices). */
 ML_API_ENTRY int srtEngineInfo(srt_engine engine, size_t* devices, size_t* local_devices, size_t* band_rows,
                                size_t* buffer_rows, int* rccl, double* exchange_bytes_per_frame);
+/* The last srtEngineRun's exchange on local device `local`: every batch's send / receive group (RCCL)
+ * or copies (device copies) timed by HIP events on the device's exchange stream -- groups timed, mean
+ * ms per group (from the stream reaching the group to its completion: peers' lateness included), and
+ * the bytes the device sent per group. Zero groups without an exchange. */
+ML_API_ENTRY int srtEngineExchangeStats(srt_engine engine, size_t local, size_t* groups, double* ms_mean,
+                                        double* bytes_sent);
 /* Host self-test of the engine's exchange layout (no device): band_ids[d] = band d's hit ids of a
  * batch's frames (batch x buffer rows x width int32, buffer rows = srtEngineInfo's); recv[c]
  * receives compositor c's buffer as the device path lays it out, [bands][frames of c][buffer rows]

@@ -153,6 +153,7 @@ _SIGNATURES = {
     "srtEngineInfo": (ctypes.c_int, [ctypes.c_void_p, _PSZ, _PSZ, _PSZ, _PSZ, ctypes.POINTER(ctypes.c_int), _PD]),
     "srtExchangeHost": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), _SZ, _SZ, _SZ, ctypes.c_int, ctypes.c_int, _SZ,
                                        _SZ, ctypes.POINTER(ctypes.c_void_p), _PSZ, _PSZ]),
+    "srtEngineExchangeStats": (ctypes.c_int, [ctypes.c_void_p, _SZ, _PSZ, _PD, _PD]),
     "srtExchangeHostShare": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), _SZ, _SZ, _SZ, _SZ, _SZ, _SZ,
                                             ctypes.POINTER(ctypes.c_void_p), _PSZ, _PSZ]),
     "srtScreenBoxHost": (ctypes.c_int, [ctypes.POINTER(ctypes.c_float), ctypes.c_int, ctypes.POINTER(ctypes.c_float)]),

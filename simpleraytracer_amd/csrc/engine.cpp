@@ -373,6 +373,12 @@ struct FrameEngine::Device {
     std::size_t band = 0;  // global band / rank index
     hipStream_t comm = nullptr;
     hipEvent_t comm_drained = nullptr;
+    // Exchange timing of the current run (pairs of timing events around each batch's group on
+    // `comm`), summarised when the run ends (FrameEngine::exchange_stats).
+    std::vector<hipEvent_t> xev;
+    std::size_t xn = 0;
+    double x_ms = 0.0, x_bytes = 0.0;
+    std::size_t x_groups = 0;
     std::vector<Queue> queues;
     float* full = nullptr;  // inputs x H x W x 2
     float* band_in = nullptr;  // per role (FrameEngine::Role): inputs x the role's rows x W x 2
@@ -715,6 +721,10 @@ void FrameEngine::Release() noexcept {
             (void)hipEventDestroy(dp->comm_drained);
             dp->comm_drained = nullptr;
         }
+        for (hipEvent_t e : dp->xev) {
+            (void)hipEventDestroy(e);
+        }
+        dp->xev.clear();
         if (dp->comm != nullptr) {
             (void)hipStreamDestroy(dp->comm);
             dp->comm = nullptr;
@@ -1051,11 +1061,48 @@ void FrameEngine::TraceRotated(std::size_t local, std::size_t b) {
     }
 }
 
+namespace {
+// The next pair of timing events of a device's exchange timing (grown on demand).
+hipEvent_t* ExchangeEvents(std::vector<hipEvent_t>& ev, std::size_t& n) {
+    while (ev.size() < 2 * (n + 1)) {
+        hipEvent_t e = nullptr;
+        HipCheck(hipEventCreate(&e), "hipEventCreate(exchange timing)");
+        ev.push_back(e);
+    }
+    return &ev[2 * n++];
+}
+}  // namespace
+
+double FrameEngine::SentBytes(std::size_t local, std::size_t b) const {
+    const std::size_t self = m_dev[local]->band;
+    double bytes = 0.0;
+    for (std::size_t p = 0; p < m_world; ++p) {
+        if (p != self || m_opt.rccl_self) {
+            bytes += static_cast<double>(m_plan.FramesFor(b, p)) * static_cast<double>(m_band_id_bytes);
+        }
+    }
+    return bytes;
+}
+
+FrameEngine::ExchangeStats FrameEngine::exchange_stats(std::size_t local) const {
+    ExchangeStats st;
+    if (local < m_dev.size()) {
+        const Device& d = *m_dev[local];
+        st.groups = d.x_groups;
+        st.ms_mean = d.x_groups != 0 ? d.x_ms / static_cast<double>(d.x_groups) : 0.0;
+        st.bytes_sent = d.x_groups != 0 ? d.x_bytes / static_cast<double>(d.x_groups) : 0.0;
+    }
+    return st;
+}
+
 void FrameEngine::ExchangePhase(std::size_t local, std::size_t b) {
     Device& d = *m_dev[local];
     Queue& q = d.queues[b % m_opt.queues];
     const std::size_t self = d.band, n_self = m_plan.FramesFor(b, self);
     HipCheck(hipStreamWaitEvent(d.comm, q.traced, 0), "hipStreamWaitEvent(traced)");
+    hipEvent_t* xe = ExchangeEvents(d.xev, d.xn);
+    d.x_bytes += SentBytes(local, b);
+    HipCheck(hipEventRecord(xe[0], d.comm), "hipEventRecord(exchange start)");
     {
         // The communicator is touched only under the shared lock and before an abort (comm.h).
         std::shared_lock<std::shared_mutex> lk(m_ctl->mu);
@@ -1092,6 +1139,7 @@ void FrameEngine::ExchangePhase(std::size_t local, std::size_t b) {
     }
     // Nonblocking communicator: the group's kernels are on the comm stream once it settles.
     CommSettle(&m_comms[local], 1, "exchange enqueue (band ids)", m_ctl.get());
+    HipCheck(hipEventRecord(xe[1], d.comm), "hipEventRecord(exchange end)");
     HipCheck(hipEventRecord(q.exchanged, d.comm), "hipEventRecord(exchanged)");
 }
 
@@ -1101,6 +1149,9 @@ void FrameEngine::CopyPhase(std::size_t local, std::size_t b) {
     Queue& q = d.queues[qi];
     const std::size_t self = d.band, n_self = m_plan.FramesFor(b, self);
     HipCheck(hipStreamWaitEvent(d.comm, q.traced, 0), "hipStreamWaitEvent(traced)");
+    hipEvent_t* xe = ExchangeEvents(d.xev, d.xn);
+    d.x_bytes += SentBytes(local, b);
+    HipCheck(hipEventRecord(xe[0], d.comm), "hipEventRecord(exchange start)");
     if (n_self != 0) {
         for (std::size_t p = 0; p < m_dev.size(); ++p) {
             if (p == local) {
@@ -1115,6 +1166,7 @@ void FrameEngine::CopyPhase(std::size_t local, std::size_t b) {
                      "hipMemcpyPeerAsync(band ids)");
         }
     }
+    HipCheck(hipEventRecord(xe[1], d.comm), "hipEventRecord(exchange end)");
     HipCheck(hipEventRecord(q.exchanged, d.comm), "hipEventRecord(exchanged)");
 }
 
@@ -1163,6 +1215,9 @@ void FrameEngine::Inject(std::size_t local, std::size_t b) {
 void FrameEngine::RunWorker(std::size_t local, std::size_t b0, std::size_t batches) {
     Device& d = *m_dev[local];
     DeviceGuard guard(d.device);
+    d.xn = 0;
+    d.x_ms = d.x_bytes = 0.0;
+    d.x_groups = 0;
     const std::size_t nc = m_comms.empty() ? 0 : 1;
     void* const* comm = nc != 0 ? &m_comms[local] : nullptr;
     for (std::size_t b = b0; b < b0 + batches; ++b) {
@@ -1212,6 +1267,12 @@ void FrameEngine::RunWorker(std::size_t local, std::size_t b0, std::size_t batch
         CommWaitEvent(q.drained, comm, nc, "render (queue)", m_ctl.get());
     }
     CommWaitEvent(d.comm_drained, comm, nc, "render (exchange)", m_ctl.get());
+    for (std::size_t i = 0; i < d.xn; ++i) {  // every exchange of the run has completed (drained above)
+        float ms = 0.f;
+        HipCheck(hipEventElapsedTime(&ms, d.xev[2 * i], d.xev[2 * i + 1]), "hipEventElapsedTime(exchange)");
+        d.x_ms += static_cast<double>(ms);
+    }
+    d.x_groups = d.xn;
 }
 
 void FrameEngine::Barrier() {

@@ -181,6 +181,15 @@ public:
     std::uint64_t triangles() const { return m_n; }
     // Bytes the devices exchange per frame (bands at P > 1), for the report.
     double exchange_bytes_per_frame() const;
+    // The last run's exchange on local device `local`, timed by HIP events on its exchange stream
+    // around each batch's send / receive group (RCCL) or copies (device copies): groups, mean ms per
+    // group, and the bytes the device sent per group (to all peers).
+    struct ExchangeStats {
+        std::size_t groups = 0;
+        double ms_mean = 0.0;
+        double bytes_sent = 0.0;
+    };
+    ExchangeStats exchange_stats(std::size_t local) const;
     int id_planes() const { return m_id_planes; }  // exchange payload: packed ids' bit planes, -1 int32
 
 private:
@@ -208,6 +217,7 @@ private:
     void TraceShare(std::size_t local, std::size_t b);  // kShare's trace: each frame in its compositor's pattern
     void TraceRotated(std::size_t local, std::size_t b);  // rotate: each frame's band by its compositor
     void ExchangePhase(std::size_t local, std::size_t b);  // RCCL: inside a group
+    double SentBytes(std::size_t local, std::size_t b) const;  // ids device `local` sends for batch b
     void CopyPhase(std::size_t local, std::size_t b);      // device-copy exchange
     void ShadePhase(std::size_t local, std::size_t b);
     void RunWorker(std::size_t local, std::size_t b0, std::size_t batches);

@@ -727,6 +727,13 @@ __global__ __launch_bounds__(kShadeThreads) void ShadeIdsKernel(TraceParams p, c
     }
     const unsigned g = blockIdx.z;
     const size_t pixels = static_cast<size_t>(p.width) * p.row_count;
+#ifdef SRT_EXP_SHADE_STORE_ONLY  // measurement builds only (make exp): the stores alone, no loads
+    {
+        StoreNontemporal(reinterpret_cast<F4*>(p.out + g * pixels + static_cast<size_t>(y0) * p.width + x),
+                         F4{static_cast<float>(x), static_cast<float>(y0), static_cast<float>(g), 0.f});
+        return;
+    }
+#endif
     // Three phases with no control flow between the loads of different rows, so every row's loads are
     // in flight together: (1) every row's id (packed: its u16, bit-plane words and tile offset --
     // wave-uniform addresses), (2) every hit's sample offset (irregular tiles) and every row's shading
@@ -797,9 +804,14 @@ __global__ __launch_bounds__(kShadeThreads) void ShadeIdsKernel(TraceParams p, c
         const bool regular = PACKED && SRT_SHADE_TILE_OFFSETS && tile_o[r].x == tile_o[r].x;
         o[r] = hit[r] < 0 || regular ? tile_o[r]
                                      : p.offsets[static_cast<size_t>(y) * p.width + x + g * offsets_stride];  // frame g's (stride 0: shared)
+#ifdef SRT_EXP_SHADE_NO_RECORD  // measurement builds only: no shading-record gather
+        nr[r] = make_float4(1.f, 0.f, 0.f, 1.f);
+        al[r] = make_float4(0.5f, 0.5f, 0.5f, 0.f);
+#else
         const float4* sr = p.shade + 2ull * static_cast<unsigned>(max(hit[r], 0));
         nr[r] = sr[0];
         al[r] = sr[1];
+#endif
     }
 #pragma unroll
     for (int r = 0; r < kShadeRows; ++r) {

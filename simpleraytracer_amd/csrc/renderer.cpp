@@ -276,8 +276,14 @@ void DeviceScene::Shade(const float* d_offsets, const int* d_ids, float* d_rgba,
     if (m_width == 0) {
         throw std::runtime_error("Shade: Prepare() has not been called");
     }
-    if (interleaved > 0 && (row_begin != 0 || band_rows < InterleavedBandRows(m_height, interleaved, 0))) {
-        throw std::runtime_error("Shade: interleaved bands cover the whole frame in band_rows-row buffers");
+    if (interleaved > 0) {  // every band the ids hold (from own_bands on) fits a band_rows-row buffer
+        bool fits = row_begin == 0;
+        for (std::size_t j = own_bands; j < interleaved && fits; ++j) {
+            fits = band_rows >= InterleavedBandRows(m_height, interleaved, j);
+        }
+        if (!fits) {
+            throw std::runtime_error("Shade: interleaved bands cover the whole frame in band_rows-row buffers");
+        }
     }
     if (row_begin + row_count > m_height) {
         throw std::runtime_error("Shade: row band outside the frame");

@@ -587,6 +587,29 @@ ML_API_ENTRY int srtEngineInfo(srt_engine engine, size_t* devices, size_t* local
     });
 }
 
+ML_API_ENTRY int srtEngineExchangeStats(srt_engine engine, size_t local, size_t* groups, double* ms_mean,
+                                        double* bytes_sent) {
+    return Guarded([&] {
+        if (engine == nullptr) {
+            throw std::runtime_error("Bad engine handle");
+        }
+        const srt::FrameEngine* e = FromHandle(engine);
+        if (local >= e->local_devices()) {
+            throw std::runtime_error("srtEngineExchangeStats: no local device " + std::to_string(local));
+        }
+        const srt::FrameEngine::ExchangeStats st = e->exchange_stats(local);
+        if (groups != nullptr) {
+            *groups = st.groups;
+        }
+        if (ms_mean != nullptr) {
+            *ms_mean = st.ms_mean;
+        }
+        if (bytes_sent != nullptr) {
+            *bytes_sent = st.bytes_sent;
+        }
+    });
+}
+
 namespace {
 int ExchangeHost(const int* const* band_ids, size_t bands, size_t width, size_t height, int rows, int exchange,
                  size_t share, size_t batch, size_t batch_index, int* const* recv, size_t* recv_frames,

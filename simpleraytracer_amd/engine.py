@@ -134,6 +134,13 @@ class FrameEngine:
         return {"devices": d.value, "local_devices": ld.value, "band_rows": br.value, "buffer_rows": bufr.value,
                 "rccl": bool(rccl.value), "exchange_bytes_per_frame": xb.value}
 
+    def exchange_stats(self, local: int = 0):
+        """The last run's exchange on local device `local` (srtEngineExchangeStats): groups timed, mean ms
+        per group on the device's exchange stream, bytes the device sent per group."""
+        g, ms, sent = ctypes.c_size_t(), ctypes.c_double(), ctypes.c_double()
+        _check(self._lib.srtEngineExchangeStats(self.handle, local, ctypes.byref(g), ctypes.byref(ms), ctypes.byref(sent)))
+        return {"groups": g.value, "ms_mean": ms.value, "bytes_sent": sent.value}
+
     def close(self):
         if getattr(self, "handle", None):
             self._lib.srtEngineRelease(self.handle)

@@ -108,6 +108,8 @@ def test_engine_rotated_needs_alltoall(gpu, scenes):
     from simpleraytracer_amd.device import SrtError
 
     with pytest.raises(SrtError, match="rotated bands"):
+        engine(scenes["soup300"], 40, 40, devices=[0, 0], rows="rotated", exchange="rotating")
+    with pytest.raises(SrtError, match="interleaved rows"):  # share deals tile rows: interleaved only
         engine(scenes["soup300"], 40, 40, devices=[0, 0], rows="rotated", exchange="share")
 
 
