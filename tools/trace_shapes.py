@@ -27,6 +27,9 @@ def main():
     ap.add_argument("dirs", nargs="+")
     ap.add_argument("--kernel", default="", help="only kernels whose name contains this")
     ap.add_argument("--csv", default="", help="write the table as CSV here")
+    ap.add_argument("--last", type=int, default=0,
+                    help="only the last N dispatches (by start time) of each (kernel, grid): e.g. bench.py's "
+                         "one-launch-in-flight roofline pass, which follows its overlapped timed run")
     a = ap.parse_args()
     rows = []
     for d in a.dirs:
@@ -40,7 +43,11 @@ def main():
                 if a.kernel and a.kernel not in r["Kernel_Name"]:
                     continue
                 key = (short(r["Kernel_Name"]), int(r["Grid_Size_X"]), int(r["Grid_Size_Y"]), int(r["Grid_Size_Z"]))
-                groups.setdefault(key, []).append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+                groups.setdefault(key, []).append((int(r["Start_Timestamp"]),
+                                                   (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3))
+        for key in groups:
+            ds = [d for _, d in sorted(groups[key])]
+            groups[key] = ds[-a.last:] if a.last > 0 else ds
         for (k, gx, gy, gz), ds in sorted(groups.items(), key=lambda kv: -sum(kv[1])):
             rows.append({"dir": d, "kernel": k, "grid": f"{gx}x{gy}x{gz}", "calls": len(ds),
                          "mean_us": round(statistics.fmean(ds), 3), "median_us": round(statistics.median(ds), 3),
