@@ -183,13 +183,15 @@ class Job:
         return self.paths[key]
 
     def engine(self, path, a, mode=None, exchange=None, rows=None, queues=None, batch=None, variant=None,
-               width=None, height=None):
+               width=None, height=None, rccl_self=False):
         from simpleraytracer_amd.engine import FrameEngine, unique_id
 
         kw = dict(variant=variant or a.variant, queues=queues or a.queues, batch=batch or a.frames_per_step,
                   rows=rows or a.rows, exchange=exchange or a.exchange, split=mode or a.mode, launch=a.launch,
                   share=a.share)
         w, h = width or a.width, height or a.height
+        if rccl_self:  # one device, the bands path with its ids sent to itself over a one-rank communicator
+            return FrameEngine(path, w, h, devices=self.devices, rccl_self=True, **kw)
         if not self.ranked:
             return FrameEngine(path, w, h, devices=self.devices, **kw)
         return FrameEngine.rank(path, w, h, self.devices[0], self.rank, self.world, self.share_uid(unique_id), **kw)
@@ -466,9 +468,18 @@ def e2e_roofline(e2e, peaks, W, H, in_bytes_px=8, out_bytes_px=16):
     bin_, bout = W * H * in_bytes_px, W * H * out_bytes_px
     duplex = max(bin_ / (peaks["h2d_gbs"] * 1e9), bout / (peaks["d2h_gbs"] * 1e9)) * 1e3
     serial = (bin_ / (peaks["h2d_gbs"] * 1e9) + bout / (peaks["d2h_gbs"] * 1e9)) * 1e3
+    # what the box delivered with both directions busy at once (host_link.duplex_gbs_total): the link's
+    # measured aggregate, the floor a pipelined frame can reach on this box
+    agg = (bin_ + bout) / (peaks["duplex_gbs_total"] * 1e9) * 1e3
     return {"bytes_in": bin_, "bytes_out": bout, "floor_duplex_ms": round(duplex, 4), "floor_serial_ms": round(serial, 4),
+            "floor_aggregate_ms": round(agg, 4),
             "frac": round(duplex / e2e["ms_per_frame"], 4), "frac_serial": round(serial / e2e["ms_per_frame"], 4),
-            "achieved_gbs": round((bin_ + bout) / (e2e["ms_per_frame"] * 1e-3) / 1e9, 2)}
+            "frac_aggregate": round(agg / e2e["ms_per_frame"], 4),
+            "achieved_gbs": round((bin_ + bout) / (e2e["ms_per_frame"] * 1e-3) / 1e9, 2),
+            "note": "floor_duplex = both directions at their one-way rates at once (a full-duplex link); "
+                    "floor_aggregate = in + out at the rate both directions reached together on this box "
+                    "(host_link.duplex_gbs_total): the copy engines and the CU stores to host memory both "
+                    "measured ~57 GB/s in total, however the bytes split between the directions"}
 
 
 def e2e_ml_api(scene_path, W, H, reps=10, warmup=3, devices=None):
@@ -565,6 +576,27 @@ def main():
                                        "input_bytes": int(ring.nbytes),
                                        "note": "frames cycle through 16 distinct resident input images (265 MB > the "
                                                "256 MB MALL), same values as the headline's"}
+        # The exchange code path over RCCL on one GPU: every frame's ids sent to itself with ncclSend /
+        # ncclRecv inside the group, the groups timed as at N > 1 (a device-local copy through RCCL, not
+        # an xGMI link: the rehearsal of the N > 1 exchange fields on hardware)
+        try:
+            e = job.engine(path, a, rccl_self=True, rows="interleaved", exchange="alltoall", batch=64)
+            e.set_inputs(inputs)
+            _, mr = timed(job, e, min(a.steps, 10), 1)
+            xs, xi = e.exchange_stats(0), e.info()
+            bad, checked = e.verify()
+            e.close()
+            legs["rccl_self_exchange"] = {
+                "mrays_per_s": round(mr, 3), "transport": "RCCL" if xi["rccl"] else "none",
+                "groups": xs["groups"], "ms_per_batch": round(xs["ms_mean"], 5),
+                "bytes_per_batch": int(xs["bytes_sent"]),
+                "gbs": round(xs["bytes_sent"] / (xs["ms_mean"] * 1e-3) / 1e9, 2) if xs["ms_mean"] else None,
+                "verified": bad == 0 and checked > 0,
+                "note": "one GPU, bands path with a one-rank RCCL communicator: each 64-frame batch's packed ids "
+                        "sent to itself (ncclSend / ncclRecv to self inside one group, timed by HIP events on the "
+                        "exchange stream) and shaded from the received copy; a device-local copy, not a link rate"}
+        except Exception as exc:  # noqa: BLE001 -- the primary line must still be printed
+            legs["rccl_self_exchange"] = {"error": f"{type(exc).__name__}: {exc}"}
         if a.offsets == "uniform":
             legs["offsets_random"] = {**run_leg(job, a, path, make_offsets(a, "random"), min(a.steps, 60), a.warmup),
                                       "note": "seeded U[0,1) per-pixel sample offsets (every tile irregular)"}

@@ -675,6 +675,12 @@ __device__ __forceinline__ unsigned long long HitKey(float t, int id) {
     return (static_cast<unsigned long long>(__float_as_uint(t)) << 32) | static_cast<unsigned>(id);
 }
 
+#ifndef SRT_SHADE_NT_IDS
+// The packed ids' u16 plane: plain loads (1: nontemporal, A/B). Received just before the shading, a
+// batch's ids (P = 8: 62 MB) sit in the 256 MB Infinity Cache, which nontemporal loads went past: rank
+// simulation, compositor shading per 32-frame launch at P = 8 318 -> 278 us, P = 2 (282 MB) 772 -> 757.
+#define SRT_SHADE_NT_IDS 0
+#endif
 #ifndef SRT_SHADE_COMPACT
 #define SRT_SHADE_COMPACT 1  // 0: a grid over every row of the frame (A/B)
 #endif
@@ -776,7 +782,11 @@ __global__ __launch_bounds__(kShadeThreads) void ShadeIdsKernel(TraceParams p, c
         if constexpr (PACKED) {
             const unsigned char* frame = packed + (static_cast<size_t>(slot) * frames + g) * frame_bytes;
             const unsigned char* row = PackedRow(frame, p, static_cast<int>(local));
+#if SRT_SHADE_NT_IDS
             code[r] = __builtin_nontemporal_load(reinterpret_cast<const unsigned short*>(row) + x);
+#else
+            code[r] = reinterpret_cast<const unsigned short*>(row)[x];
+#endif
             const unsigned long long* bits = reinterpret_cast<const unsigned long long*>(row + p.id_low_row_bytes);
 #pragma unroll
             for (int j = 0; j < PLANES; ++j) {
