@@ -665,7 +665,11 @@ constexpr int kShadeThreads = SRT_SHADE_THREADS;
 #define SRT_SHADE_TILE_OFFSETS 1  // shade regular tiles from the packed ids' tile offsets
 #endif
 #ifndef SRT_SHADE_ROWS
-#define SRT_SHADE_ROWS 1  // rows per thread (P = 8 rank, 64-frame launches: 1 / 2 / 4 rows 5.31-5.42 / 5.52-5.58 / 5.59-5.63 us per frame; the kernel alone 102 / 97 / 108 / 120 (8) / 162 (16) us)
+// Rows per thread. Round 5, with every row's loads issued before any is used (the tile offsets pinned
+// there, exact float row division): 1 / 2 / 4 rows 690 / 646 / 582 us per 128-frame launch of a P = 2
+// compositor, 263 / 260 / 248 us per 32-frame launch at P = 8 (profiles/r05/shade_ab/rows.txt). (Before,
+// clang serialised the rows' loads behind per-row branches: 2 rows measured slower than 1.)
+#define SRT_SHADE_ROWS 4
 #endif
 constexpr int kShadeRows = SRT_SHADE_ROWS;
 
@@ -684,23 +688,38 @@ __device__ __forceinline__ unsigned long long HitKey(float t, int id) {
 #ifndef SRT_SHADE_COMPACT
 #define SRT_SHADE_COMPACT 1  // 0: a grid over every row of the frame (A/B)
 #endif
+#ifndef SRT_SHADE_PIN_TILE_OFFSET
+#define SRT_SHADE_PIN_TILE_OFFSET 1
+#endif
+// Quotient of small unsigned integers, exact for y < 2^21 and any d >= 1: |fl(y + 1/2) * rcp(d) - (y +
+// 1/2) / d| <= (y + 1/2) / d * 1.5 * 2^-23 (v_rcp_f32 within 1 ulp, one rounding of the product), below
+// the 1 / (2 d) by which (y + 1/2) / d stays from an integer. The shading kernel's row mapping divides
+// wave-uniform values, which clang expanded into ~25 scalar instructions each (117 SALU per wave, 62 % of
+// the CU's scalar issue at a P = 8 compositor; PMC, profiles/r05/shade_pmc/).
+__device__ __forceinline__ unsigned UDivSmall(unsigned y, unsigned d) {
+    if (y >= (1u << 21)) {  // (frames of over 2M rows: the integer division)
+        return y / d;
+    }
+    return static_cast<unsigned>((static_cast<float>(y) + 0.5f) * __builtin_amdgcn_rcpf(static_cast<float>(d)));
+}
 // The frame row of the j-th row a shade call stores: the rows of bands [0, own) and of band `skip`
 // (~0u: none) left out. Interleaved (m = interleaved): band b is tile rows b, b + m, ... of 16 rows;
 // else band b is rows [b * band_rows, (b + 1) * band_rows). Past the last stored row the result is
 // past the frame only if the caller's grid (ShadeRowsLaunched) stops at the frame's rows.
-__host__ __device__ inline unsigned ShadeRowOf(unsigned j, unsigned band_rows, unsigned interleaved, unsigned skip,
+__device__ __forceinline__ unsigned ShadeRowOf(unsigned j, unsigned band_rows, unsigned interleaved, unsigned skip,
                                                unsigned own) {
     const bool skips = skip != ~0u && skip >= own;
     if (interleaved != 0u) {
-        const unsigned stored = interleaved - own - (skips && skip < interleaved ? 1u : 0u);  // bands per cycle
+        const unsigned stored = interleaved - own - (skips && skip < interleaved ? 1u : 0u);
         const unsigned tr = j / kCullTileRows;
-        unsigned band = own + tr % stored;
+        const unsigned q = UDivSmall(tr, stored);
+        unsigned band = own + (tr - q * stored);
         band += skips && band >= skip ? 1u : 0u;
-        return ((tr / stored) * interleaved + band) * kCullTileRows + j % kCullTileRows;
+        return (q * interleaved + band) * kCullTileRows + j % kCullTileRows;
     }
     unsigned long long y = static_cast<unsigned long long>(own) * band_rows + j;
     y += skips && y >= static_cast<unsigned long long>(skip) * band_rows ? band_rows : 0u;
-    return y > 0x7FFFFFFFull ? 0x7FFFFFFFu : static_cast<unsigned>(y);  // (an int row past the frame)
+    return y > 0x7FFFFFFFull ? 0x7FFFFFFFu : static_cast<unsigned>(y);
 }
 
 // PACKED: the ids arrive as packed band frames (render.h PackedIds, frame_bytes each, the same
@@ -750,13 +769,14 @@ __global__ __launch_bounds__(kShadeThreads) void ShadeIdsKernel(TraceParams p, c
     // rows may straddle skip_band).
     static_assert(kCullTileRows % kShadeRows == 0, "a thread's rows share a tile row");
     const unsigned t0 = static_cast<unsigned>(y0) / kCullTileRows;
-    const unsigned band0 = interleaved != 0u ? t0 % interleaved : 0u;
-    const unsigned local0 =
-        interleaved != 0u ? t0 / interleaved * kCullTileRows + static_cast<unsigned>(y0) % kCullTileRows : 0u;
+    const unsigned tq = interleaved != 0u ? UDivSmall(t0, interleaved) : 0u;
+    const unsigned band0 = interleaved != 0u ? t0 - tq * interleaved : 0u;
+    const unsigned local0 = interleaved != 0u ? tq * kCullTileRows + static_cast<unsigned>(y0) % kCullTileRows : 0u;
     const int tcol = __builtin_amdgcn_readfirstlane(x >> 6);  // the wave's tile column
     unsigned code[kShadeRows];
     float2 tile_o[kShadeRows];  // packed ids: the row's tile offset (NaN: every pixel reads its own)
     int yr[kShadeRows];         // frame rows (>= row_count: past the frame, not stored)
+    unsigned long long plane[kShadeRows][PLANES > 0 ? PLANES : 1];  // packed ids: the rows' bit-plane words
     // (The bands [0, own_bands) hold no ids in the buffer, which starts at band own_bands: the
     // compositor traced them as RGBA already.)
 #pragma unroll
@@ -771,7 +791,7 @@ __global__ __launch_bounds__(kShadeThreads) void ShadeIdsKernel(TraceParams p, c
             band = band0;
             local = local0 + (y - static_cast<unsigned>(y0));
         } else {
-            band = y / band_rows;
+            band = UDivSmall(y, band_rows);
             local = y - band * band_rows;
         }
         if (!SRT_SHADE_COMPACT && (band == skip_band || band < own_bands)) {
@@ -790,8 +810,7 @@ __global__ __launch_bounds__(kShadeThreads) void ShadeIdsKernel(TraceParams p, c
             const unsigned long long* bits = reinterpret_cast<const unsigned long long*>(row + p.id_low_row_bytes);
 #pragma unroll
             for (int j = 0; j < PLANES; ++j) {
-                const unsigned long long w = bits[static_cast<size_t>(j) * p.id_words + tcol];
-                code[r] |= static_cast<unsigned>((w >> (x & 63)) & 1ull) << (16 + j);
+                plane[r][j] = bits[static_cast<size_t>(j) * p.id_words + tcol];
             }
             tile_o[r] = *reinterpret_cast<const float2*>(PackedTileOffset(frame, p, static_cast<int>(local), tcol));
         } else {
@@ -800,10 +819,28 @@ __global__ __launch_bounds__(kShadeThreads) void ShadeIdsKernel(TraceParams p, c
             tile_o[r] = make_float2(__builtin_nanf(""), __builtin_nanf(""));
         }
     }
+    // Every row's loads are issued above before any is used (the codes are assembled here). Only a hit
+    // uses the tile offset, so clang sank its (scalar) load into the hit branch, behind the u16 load's
+    // wait: a third round trip in the chain (u16 -> tile offset -> shading record). Pinned here, it is
+    // in flight with the u16s and the bit-plane words.
+    if constexpr (PACKED) {
+#pragma unroll
+        for (int r = 0; r < kShadeRows; ++r) {
+#pragma unroll
+            for (int j = 0; j < PLANES; ++j) {
+                code[r] |= static_cast<unsigned>((plane[r][j] >> (x & 63)) & 1ull) << (16 + j);
+            }
+#if SRT_SHADE_PIN_TILE_OFFSET
+            asm volatile("" ::"s"(tile_o[r].x), "s"(tile_o[r].y));
+#endif
+        }
+    }
     // Only a hit needs its ray: a miss shades to the background whatever its sample offset (a miss is
     // -1, the packed miss code -- all ones -- or any id outside the scene). A hit in a regular tile
-    // takes the tile's offset (the trace computed its ray from the same one, bit for bit); others
-    // read their own. Every row's shading record is loaded (a miss's: triangle 0's, unused).
+    // takes the tile's offset (the trace computed its ray from the same one, bit for bit); in other
+    // rows every lane reads its own (a wave-uniform branch: the tile offset is one scalar per wave and
+    // row, so no lane mask splits the row's loads from the others'). Every row's shading record is
+    // loaded (a miss's: triangle 0's, unused).
     int hit[kShadeRows];
     float2 o[kShadeRows];
     float4 nr[kShadeRows], al[kShadeRows];
@@ -812,8 +849,10 @@ __global__ __launch_bounds__(kShadeThreads) void ShadeIdsKernel(TraceParams p, c
         const int y = yr[r] < p.row_count ? yr[r] : y0;
         hit[r] = code[r] < p.n ? static_cast<int>(code[r]) : -1;
         const bool regular = PACKED && SRT_SHADE_TILE_OFFSETS && tile_o[r].x == tile_o[r].x;
-        o[r] = hit[r] < 0 || regular ? tile_o[r]
-                                     : p.offsets[static_cast<size_t>(y) * p.width + x + g * offsets_stride];  // frame g's (stride 0: shared)
+        o[r] = tile_o[r];
+        if (!regular) {
+            o[r] = p.offsets[static_cast<size_t>(y) * p.width + x + g * offsets_stride];  // frame g's (stride 0: shared)
+        }
 #ifdef SRT_EXP_SHADE_NO_RECORD  // measurement builds only: no shading-record gather
         nr[r] = make_float4(1.f, 0.f, 0.f, 1.f);
         al[r] = make_float4(0.5f, 0.5f, 0.5f, 0.f);
@@ -1140,8 +1179,13 @@ struct CullShared {
     unsigned wave_n[kSlices * kCullWaves];   // survivors per (slice, wave)
     unsigned wave_pk[kSlices * kCullWaves];  // pixels per (slice, wave)
     uint2 pk[2][kWindowPackets];  // window packet k: last-pixel bits (lo, hi); two buffers, alternate batches
+#ifndef SRT_EXP_NO_FXY
     float2 fxy[kBlockRows][kWave];  // ray position (fx, fy) of every pixel of the block (512-B rows:
                                     // rows padded by 8 or 16 B to skew the banks measured 3-6 % slower)
+#endif
+#ifdef SRT_EXP_LDS_PAD  // measurement builds only: fewer blocks per CU
+    unsigned exp_pad[SRT_EXP_LDS_PAD];
+#endif
     float clo[kWave], chi[kWave];    // monotone column bounds of fx (suffix min, prefix max)
     float rlo[kBlockRows], rhi[kBlockRows];  // monotone row bounds of fy
     unsigned counts[2][kCullWaves];            // FULL stream: survivors per wave and step
@@ -1283,7 +1327,9 @@ __device__ __forceinline__ void PacketTables(CullShared& sh, const Rays<kCullR>&
     const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);
 #pragma unroll
     for (int r = 0; r < R; ++r) {
+#ifndef SRT_EXP_NO_FXY
         sh.fxy[wave * R + r][lane] = make_float2(s.fx[r], s.fy[r]);
+#endif
     }
     if (regular) {
         if (tid < kWave) {
@@ -1476,7 +1522,9 @@ __device__ __forceinline__ void PacketBatch(CullShared& sh, const Box& bb, const
     // range. The waves split each window's packets evenly, kPacketIlp at a time (independent
     // chains; a tail repeats the last packet, harmless under the atomic min).
     constexpr int kPacketIlp = SRT_PACKET_ILP;
+#ifndef SRT_EXP_NO_FXY
     const char* fxy = reinterpret_cast<const char*>(&sh.fxy[0][0]);
+#endif
     char* keys = reinterpret_cast<char*>(&sh.keys[0][0]);
     const unsigned last_slot = n_surv == 0u ? 0u : n_surv - 1u;
     unsigned ended = 0u;  // ranges that end before the window (block-uniform)
@@ -1568,7 +1616,11 @@ __device__ __forceinline__ void PacketBatch(CullShared& sh, const Box& bb, const
             for (int u = 0; u < kPacketIlp; ++u) {
 #pragma unroll
                 for (int j = 0; j < kLanePixels; ++j) {
+#ifdef SRT_EXP_NO_FXY  // measurement builds only (regular tiles: the position tables are the positions)
+                    f[u][j] = make_float2(sh.clo[(px[u][j].pixb >> 3) & 63u], sh.rlo[px[u][j].pixb >> 9]);
+#else
                     f[u][j] = *reinterpret_cast<const float2*>(fxy + px[u][j].pixb);
+#endif
                 }
             }
 #pragma unroll
@@ -2538,6 +2590,9 @@ std::size_t OrderLdsBytes(int tiles) { return static_cast<std::size_t>(tiles) * 
 #ifndef SRT_TRACE_OCC
 #define SRT_TRACE_OCC 6
 #endif
+#ifndef SRT_LIST_AHEAD
+#define SRT_LIST_AHEAD 1
+#endif
 #ifndef SRT_PLAN_EMPTY_TEST
 #define SRT_PLAN_EMPTY_TEST 1  // plan-only trace blocks test an empty tile against the large list's records
 #endif
@@ -2744,6 +2799,40 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(c
     const unsigned total = src.end - src.begin;
 #endif
     CullRecord nxt[kSlices];
+#if SRT_LIST_AHEAD
+    // The list entries run one batch ahead of the records: batch b's prefetch loads batch b + 1's
+    // records from entries that arrived during batch b - 1's walk, then requests batch b + 2's
+    // entries (one load chain per batch no longer waits in front of the walk).
+    unsigned nid[kSlices];
+    auto load_ids = [&](unsigned b0) {
+#pragma unroll
+        for (int e = 0; e < kSlices; ++e) {
+            const unsigned v = b0 + e * kCullThreads + tid;
+            if (InBatch(e, tid)) {
+                const unsigned vv = src.begin + (v < total ? v : 0u);
+                nid[e] = vv < src.count1 ? src.list[vv] : src.list2[vv - src.count1];
+            }
+        }
+    };
+    auto load_recs = [&] {
+#pragma unroll
+        for (int e = 0; e < kSlices; ++e) {
+            if (InBatch(e, tid)) {
+                nxt[e] = p.cull[nid[e]];
+            }
+        }
+    };
+    auto load_list = [&](unsigned b0) {  // b0: the batch whose records are loaded now
+        load_recs();
+        if (b0 + kPacketBatch < total) {
+            load_ids(b0 + kPacketBatch);
+        }
+    };
+    if (!src.full && total != 0u) {
+        load_ids(0u);
+        load_list(0u);
+    }
+#else
     auto load_list = [&](unsigned b0) {
 #pragma unroll
         for (int e = 0; e < kSlices; ++e) {
@@ -2757,6 +2846,7 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(c
     if (!src.full && total != 0u) {
         load_list(0u);
     }
+#endif
     // Rays: lane = column x; rows y0 .. y0 + R - 1. A regular tile (every ray with the sample
     // offset (ox, oy)) computes them without reading the offsets: fx per lane, and row r's fy
     // from lane (wave R + r) of fy_lane (the GenerateRays expressions, bit for bit).
@@ -3075,7 +3165,11 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(c
         for (int r = 0; r < R; ++r) {
             const int y = y0 + r;
             if (y < p.row_count) {
+#ifdef SRT_EXP_NO_FXY
+                const float2 f = make_float2(sh.clo[lane], sh.rlo[wave * R + r]);
+#else
                 const float2 f = sh.fxy[wave * R + r][lane];
+#endif
                 StoreRgba(p, x, y, ShadeRecord(p, f.x, f.y, id[r], nr[r], al[r]));
             }
         }
