@@ -408,13 +408,15 @@ def compositor_fraction(H, world, exchange, rows, share):
     """Fraction of a frame's rows its compositor traces itself (straight into the frame as RGBA); the
     rest arrives as hit ids from the other GPUs."""
     from simpleraytracer_amd import _native
-    from simpleraytracer_amd.bands import band_range, interleaved_range, share_frame_rows
+    from simpleraytracer_amd.bands import band_range, interleaved_range, rotate_own_rows, share_frame_rows
 
     if exchange == "share":
         k = share or _native.lib().srtShareAuto(H, world)
         return round(len(share_frame_rows(H, world, k, 0, 0)) / H, 5)
     if rows == "interleaved":
         return round(interleaved_range(H, world, 0)[1] / H, 5)
+    if rows == "rotated" and world == 2:  # the compositor's band 0 (engine.cpp RotateOwnRows)
+        return round(rotate_own_rows(H) / H, 5)
     return round(band_range(H, world, 0)[1] / H, 5)
 
 
@@ -646,6 +648,21 @@ def main():
                                                                             a.share)
             except Exception as e:  # noqa: BLE001 -- the primary line must still be printed
                 legs[name] = {"error": f"{type(e).__name__}: {e}"}
+        if main == ("bands", "alltoall", "rotated") and world == 2:
+            # the two-device split at even halves (the value's split gives the compositor's band 0 3/4 of
+            # the frame: engine.cpp RotateOwnRows)
+            prev = os.environ.get("SRT_ROTATE_OWN")
+            os.environ["SRT_ROTATE_OWN"] = "50"
+            try:
+                legs["rotated_even_halves"] = run_leg(job, a, path, inputs, a.steps, a.warmup)
+                legs["rotated_even_halves"].update(scaling="strong", compositor_fraction=0.5)
+            except Exception as e:  # noqa: BLE001
+                legs["rotated_even_halves"] = {"error": f"{type(e).__name__}: {e}"}
+            finally:
+                if prev is None:
+                    os.environ.pop("SRT_ROTATE_OWN", None)
+                else:
+                    os.environ["SRT_ROTATE_OWN"] = prev
         if a.mode == "bands":
             # one frame in flight across the N GPUs: the per-frame latency of the split
             try:

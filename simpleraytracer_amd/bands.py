@@ -58,6 +58,34 @@ def rotated_band(world: int, device: int, compositor: int) -> int:
     return (device + compositor) % world
 
 
+def rotate_own_rows(height: int, pct: int | None = None) -> int:
+    """Rows of the compositor's own band (band 0) under the rotated all-to-all over two devices
+    (csrc/engine.cpp RotateOwnRows): ``pct`` per cent of the frame (env SRT_ROTATE_OWN, default 75),
+    rounded to whole 16-row tile rows, kept inside [1, H - 1]; the other band takes the rest."""
+    import os
+
+    if pct is None:
+        v = os.environ.get("SRT_ROTATE_OWN", "")
+        pct = int(v) if v.strip() else 75
+    pct = max(1, min(99, pct))
+    rows = (height * pct + 50) // 100
+    if height > 2 * TILE_ROWS:
+        rows = (rows + TILE_ROWS // 2) // TILE_ROWS * TILE_ROWS
+    return max(1, min(rows, height - 1 if height > 1 else 1))
+
+
+def rotated_range(height: int, world: int, band: int, first_rows: int = 0) -> tuple[int, int]:
+    """(row_begin, row_count) of contiguous band ``band`` when band 0 has ``first_rows`` rows (0: the
+    even split of band_range) and the later bands split the rest evenly (csrc/engine.cpp BandSplit
+    with first_rows; the engine sets it to rotate_own_rows(H) for two devices)."""
+    if first_rows == 0 or world == 1:
+        return band_range(height, world, band)
+    first = min(first_rows, height)
+    step = (height - first + world - 2) // (world - 1)
+    begin = 0 if band == 0 else min(height, first + (band - 1) * step)
+    return begin, min(height, first + band * step) - begin
+
+
 def share_auto(height: int, world: int) -> int:
     """The share exchange's default tile rows per cycle (csrc/engine.cpp ShareAuto, srtShareAuto): the
     largest power of two <= 32 whose cycle of share + P - 1 tile rows fits the frame."""
@@ -124,8 +152,11 @@ class ExchangePlan:
         return p
 
 
-def traced_rows(height: int, world: int, exchange: str, rows: str, device: int, compositor: int, share: int = 0):
-    """The frame rows ``device`` traces, in band order, of a frame composited on ``compositor``."""
+def traced_rows(height: int, world: int, exchange: str, rows: str, device: int, compositor: int, share: int = 0,
+                first_rows: int = 0):
+    """The frame rows ``device`` traces, in band order, of a frame composited on ``compositor``
+    (rotated: band 0 of ``first_rows`` rows when nonzero -- the engine's two-device split,
+    rotate_own_rows -- else even bands)."""
     import numpy as np
 
     if exchange == "share":
@@ -133,5 +164,5 @@ def traced_rows(height: int, world: int, exchange: str, rows: str, device: int, 
     if rows == "interleaved":
         return interleaved_frame_rows(height, world, device)
     band = rotated_band(world, device, compositor) if rows == "rotated" else device
-    b, c = band_range(height, world, band)
+    b, c = rotated_range(height, world, band, first_rows if rows == "rotated" else 0)
     return np.arange(b, b + c, dtype=np.int64)

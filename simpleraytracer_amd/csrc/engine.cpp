@@ -62,6 +62,21 @@ std::size_t ShareAuto(std::size_t height, std::size_t world) {
     return k;
 }
 
+// Rows of the compositor's own band under rotated all-to-all over two devices (env SRT_ROTATE_OWN: per
+// cent of the frame, default 75; 50 = even halves), rounded to whole 16-row tile rows. Even halves send
+// half of every frame's ids over the one link: 1.1 MB per frame of the job each way at 1080p, 17 us at an
+// assumed 64 GB/s against 11 us of GPU time (rank simulation) -- link-bound below one GPU; a quarter
+// halves that and the compositor's deferred shading with it.
+std::size_t RotateOwnRows(std::size_t height) {
+    const char* v = std::getenv("SRT_ROTATE_OWN");
+    long pct = v == nullptr || *v == '\0' ? 75 : std::strtol(v, nullptr, 10);
+    pct = std::max(1L, std::min(99L, pct));
+    const std::size_t t = static_cast<std::size_t>(kCullTileRows);
+    std::size_t rows = (height * static_cast<std::size_t>(pct) + 50) / 100;
+    rows = height > 2 * t ? (rows + t / 2) / t * t : rows;
+    return std::max<std::size_t>(1, std::min(rows, height > 1 ? height - 1 : 1));
+}
+
 // Band split and exchange plan (pure index math; shared with the host self-test).
 
 BandSplit BandSplit::Make(std::size_t height, std::size_t bands, bool interleaved) {
@@ -72,12 +87,28 @@ BandSplit BandSplit::Make(std::size_t height, std::size_t bands, bool interleave
     return s;
 }
 
+namespace {
+// Contiguous bands: band 0's rows and every later band's (the last one shorter).
+void ContiguousRows(const BandSplit& s, std::size_t& first, std::size_t& step) {
+    if (s.first_rows != 0 && s.bands > 1) {
+        first = std::min(s.first_rows, s.height);
+        step = (s.height - first + s.bands - 2) / (s.bands - 1);
+    } else {
+        first = step = (s.height + s.bands - 1) / s.bands;
+    }
+}
+}  // namespace
+
 std::size_t BandSplit::RowBegin(std::size_t band) const {
     if (bands == 1) {
         return 0;
     }
-    const std::size_t step = interleaved ? static_cast<std::size_t>(kCullTileRows) : (height + bands - 1) / bands;
-    return std::min(height, band * step);
+    if (interleaved) {
+        return std::min(height, band * static_cast<std::size_t>(kCullTileRows));
+    }
+    std::size_t first = 0, step = 0;
+    ContiguousRows(*this, first, step);
+    return band == 0 ? 0 : std::min(height, first + (band - 1) * step);
 }
 
 std::size_t BandSplit::RowCount(std::size_t band) const {
@@ -87,16 +118,21 @@ std::size_t BandSplit::RowCount(std::size_t band) const {
     if (interleaved) {
         return InterleavedBandRows(height, bands, band);
     }
-    const std::size_t b = (height + bands - 1) / bands;
-    return std::min(height, (band + 1) * b) - RowBegin(band);
+    std::size_t first = 0, step = 0;
+    ContiguousRows(*this, first, step);
+    return std::min(height, first + band * step) - RowBegin(band);
 }
 
 std::size_t BandSplit::BufferRows() const {
     if (bands == 1) {
         return height;
     }
-    if (!interleaved) {
-        return (height + bands - 1) / bands;
+    if (!interleaved) {  // the largest band that travels
+        std::size_t rows = 0;
+        for (std::size_t j = first_sent; j < bands; ++j) {
+            rows = std::max(rows, RowCount(j));
+        }
+        return std::max<std::size_t>(rows, 1);
     }
     // The largest band that travels (interleaved bands need not shrink with the index: the one
     // holding a partial last tile row may be shorter than the next). kShare: the sender classes only
@@ -534,6 +570,13 @@ void FrameEngine::Init(const Scene& scene, const std::vector<int>& devices) {
     // per sender); the ids buffers hold one class.
     m_split = BandSplit::Make(m_height, m_bands ? (m_share != 0 ? m_share + m_world - 1 : m_world) : 1, m_opt.interleaved);
     m_split.first_sent = m_share;
+    if (m_rotate && m_world == 2) {
+        // Two devices: band 0 (the compositor's own: BandOf(c, c) = 0) takes RotateOwnRows of the frame.
+        // Per pair of frames each device still traces one band 0 and one band 1 (one frame's work), but
+        // only band 1 crosses the single link and waits for the deferred shading.
+        m_split.first_rows = RotateOwnRows(m_height);
+        m_split.first_sent = 1;
+    }
     m_plan.bands = m_bands ? m_world : 1;
     m_plan.batch = m_opt.batch;
     m_plan.exchange = m_opt.exchange;
@@ -1189,7 +1232,8 @@ void FrameEngine::ShadePhase(std::size_t local, std::size_t b) {
     // m_share classes (share; the received ids start at class m_share).
     const long skip = m_opt.rccl_self || m_share != 0 ? -1 : static_cast<long>(m_plan.BandOf(self, self));
     q.scene->Shade(FullInput(local, first), reinterpret_cast<const int*>(q.recv), q.rgba, 0, m_height, q.stream, n_self,
-                   m_split.BufferRows(), m_split.interleaved ? m_split.bands : 0, stride, m_id_planes, skip, m_share);
+                   m_split.BufferRows(), m_split.interleaved ? m_split.bands : 0, stride, m_id_planes, skip, m_share,
+                   m_split.interleaved ? 0 : m_split.first_rows);
 }
 
 void FrameEngine::Inject(std::size_t local, std::size_t b) {

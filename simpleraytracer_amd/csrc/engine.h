@@ -87,12 +87,19 @@ struct EngineOptions {
 // k + P - 1 <= the frame's tile rows (engine.cpp).
 std::size_t ShareAuto(std::size_t height, std::size_t world);
 
+// Rows of the compositor's own band under rotated all-to-all over two devices (engine.cpp).
+std::size_t RotateOwnRows(std::size_t height);
+
 // Row bands of an H-row frame over P devices (interleaved or contiguous), the layout every
 // exchange path and the shading kernel agree on.
 struct BandSplit {
     std::size_t height = 0, bands = 1;
     bool interleaved = true;
     std::size_t first_sent = 0;  // bands below it never travel (kShare: the compositor's own classes)
+    // Contiguous bands: rows of band 0 (0: every band ceil(H / P) rows, the last one shorter); the
+    // other bands split the rest evenly. Rotated all-to-all over 2 devices, where band 0 is always the
+    // compositor's own (FrameEngine: the one link carries the other band of every frame).
+    std::size_t first_rows = 0;
     static BandSplit Make(std::size_t height, std::size_t bands, bool interleaved);
     std::size_t RowBegin(std::size_t band) const;  // first frame row (interleaved: band * 16)
     std::size_t RowCount(std::size_t band) const;  // rows of the band

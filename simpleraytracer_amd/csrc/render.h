@@ -308,9 +308,12 @@ hipError_t LaunchShadeTable(const float* d_vertices, const float* d_albedo, std:
 hipError_t LaunchShade(const float* d_vertices, const float* d_shade, const float* d_edges, std::uint64_t n,
                        const Frame& frame, const float background[3], const BandArgs& band, hipStream_t stream,
                        std::size_t frames = 1, std::size_t band_rows = 0, std::size_t interleaved = 0,
-                       std::size_t offsets_stride = 0, long skip_band = -1, std::size_t own_bands = 0);
+                       std::size_t offsets_stride = 0, long skip_band = -1, std::size_t own_bands = 0,
+                       std::size_t first_rows = 0);
 // (skip_band >= 0: the rows of that band are left as they are; own_bands > 0: so are the rows of
-// bands [0, own_bands), and the ids start at band own_bands -- the compositor's share, engine.h.)
+// bands [0, own_bands), and the ids start at band own_bands -- the compositor's share, engine.h.
+// first_rows > 0, contiguous bands only: band 0 has first_rows rows, the later ones band_rows each --
+// BandSplit::first_rows.)
 
 // Spatial order of the records (spatial.hip): ids sorted by the Morton code of their centroid's
 // image-plane position under the scene camera, on the device (keys + rocPRIM radix sort), and

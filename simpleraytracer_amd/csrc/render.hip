@@ -704,10 +704,11 @@ __device__ __forceinline__ unsigned UDivSmall(unsigned y, unsigned d) {
 }
 // The frame row of the j-th row a shade call stores: the rows of bands [0, own) and of band `skip`
 // (~0u: none) left out. Interleaved (m = interleaved): band b is tile rows b, b + m, ... of 16 rows;
-// else band b is rows [b * band_rows, (b + 1) * band_rows). Past the last stored row the result is
+// else band b is rows [b * band_rows, (b + 1) * band_rows), or, with first_rows > 0, band 0 is rows
+// [0, first_rows) and band b >= 1 rows [first_rows + (b - 1) * band_rows, ...). Past the last stored row the result is
 // past the frame only if the caller's grid (ShadeRowsLaunched) stops at the frame's rows.
 __device__ __forceinline__ unsigned ShadeRowOf(unsigned j, unsigned band_rows, unsigned interleaved, unsigned skip,
-                                               unsigned own) {
+                                               unsigned own, unsigned first_rows) {
     const bool skips = skip != ~0u && skip >= own;
     if (interleaved != 0u) {
         const unsigned stored = interleaved - own - (skips && skip < interleaved ? 1u : 0u);
@@ -717,8 +718,11 @@ __device__ __forceinline__ unsigned ShadeRowOf(unsigned j, unsigned band_rows, u
         band += skips && band >= skip ? 1u : 0u;
         return (q * interleaved + band) * kCullTileRows + j % kCullTileRows;
     }
-    unsigned long long y = static_cast<unsigned long long>(own) * band_rows + j;
-    y += skips && y >= static_cast<unsigned long long>(skip) * band_rows ? band_rows : 0u;
+    // contiguous: band b starts at row b == 0 ? 0 : F + (b - 1) S (F = first_rows, or S = band_rows)
+    const unsigned long long F = first_rows != 0u ? first_rows : band_rows, S = band_rows;
+    const auto start = [&](unsigned b) { return b == 0u ? 0ull : F + (b - 1ull) * S; };
+    unsigned long long y = start(own) + j;
+    y += skips && y >= start(skip) ? (skip == 0u ? F : S) : 0ull;
     return y > 0x7FFFFFFFull ? 0x7FFFFFFFu : static_cast<unsigned>(y);
 }
 
@@ -729,7 +733,7 @@ __global__ __launch_bounds__(kShadeThreads) void ShadeIdsKernel(TraceParams p, c
                                                                 unsigned band_rows, unsigned frames,
                                                                 unsigned interleaved, size_t offsets_stride,
                                                                 unsigned skip_band, unsigned own_bands,
-                                                                size_t frame_bytes) {
+                                                                size_t frame_bytes, unsigned first_rows) {
     static_assert(kShadeThreads % kWave == 0, "a wave's lanes are one 64-column tile column");
     const int* __restrict__ ids = static_cast<const int*>(ids_v);
     const unsigned char* __restrict__ packed = static_cast<const unsigned char*>(ids_v);
@@ -743,7 +747,7 @@ __global__ __launch_bounds__(kShadeThreads) void ShadeIdsKernel(TraceParams p, c
     // the share exchange -- a fifth of its rows shaded -- 7.3 us per frame, 2.6 us compacted.)
     const unsigned j0 = blockIdx.y * kShadeRows;
 #if SRT_SHADE_COMPACT
-    const int y0 = static_cast<int>(ShadeRowOf(j0, band_rows, interleaved, skip_band, own_bands));
+    const int y0 = static_cast<int>(ShadeRowOf(j0, band_rows, interleaved, skip_band, own_bands, first_rows));
 #else
     const int y0 = static_cast<int>(j0);
 #endif
@@ -783,13 +787,16 @@ __global__ __launch_bounds__(kShadeThreads) void ShadeIdsKernel(TraceParams p, c
     for (int r = 0; r < kShadeRows; ++r) {
         yr[r] = interleaved != 0u || r == 0 || !SRT_SHADE_COMPACT
                     ? y0 + r
-                    : static_cast<int>(ShadeRowOf(j0 + r, band_rows, interleaved, skip_band, own_bands));
+                    : static_cast<int>(ShadeRowOf(j0 + r, band_rows, interleaved, skip_band, own_bands, first_rows));
         const bool past = yr[r] >= p.row_count;
         const unsigned y = static_cast<unsigned>(past ? y0 : yr[r]);
         unsigned band, local;
         if (interleaved != 0u) {
             band = band0;
             local = local0 + (y - static_cast<unsigned>(y0));
+        } else if (first_rows != 0u) {
+            band = y < first_rows ? 0u : 1u + UDivSmall(y - first_rows, band_rows);
+            local = band == 0u ? y : y - first_rows - (band - 1u) * band_rows;
         } else {
             band = UDivSmall(y, band_rows);
             local = y - band * band_rows;
@@ -4165,7 +4172,7 @@ hipError_t LaunchShadeTable(const float* d_vertices, const float* d_albedo, std:
 // The rows of the shade grid (ShadeRowOf's j): every row of the bands a call stores, for interleaved
 // bands rounded up to whole cycles of tile rows (the threads past the frame return).
 static std::size_t ShadeRowsLaunched(std::size_t row_count, std::size_t band_rows, std::size_t interleaved,
-                                     unsigned skip, std::size_t own) {
+                                     unsigned skip, std::size_t own, std::size_t first_rows) {
     const bool skips = skip != ~0u && skip >= own;
     if (interleaved != 0) {
         const std::size_t dropped = std::min(own, interleaved) + (skips && skip < interleaved ? 1 : 0);
@@ -4173,15 +4180,17 @@ static std::size_t ShadeRowsLaunched(std::size_t row_count, std::size_t band_row
         const std::size_t tile_rows = (row_count + kCullTileRows - 1) / kCullTileRows;
         return (tile_rows + interleaved - 1) / interleaved * stored * kCullTileRows;
     }
-    const std::size_t own_rows = std::min(own * band_rows, row_count);
-    const std::size_t skip_rows = skips ? std::min(band_rows, row_count - std::min<std::size_t>(skip * band_rows, row_count)) : 0;
+    const std::size_t F = first_rows != 0 ? first_rows : band_rows;
+    const auto start = [&](std::size_t b) { return std::min(row_count, b == 0 ? 0 : F + (b - 1) * band_rows); };
+    const std::size_t own_rows = start(own);
+    const std::size_t skip_rows = skips ? std::min(skip == 0 ? F : band_rows, row_count - start(skip)) : 0;
     return row_count - own_rows - skip_rows;
 }
 
 hipError_t LaunchShade(const float* d_vertices, const float* d_shade, const float* d_edges, std::uint64_t n,
                        const Frame& frame, const float background[3], const BandArgs& band, hipStream_t stream,
                        std::size_t frames, std::size_t band_rows, std::size_t interleaved,
-                       std::size_t offsets_stride, long skip_band, std::size_t own_bands) {
+                       std::size_t offsets_stride, long skip_band, std::size_t own_bands, std::size_t first_rows) {
     if (band.row_count == 0 || band.width == 0 || frames == 0) {
         return hipSuccess;
     }
@@ -4189,7 +4198,7 @@ hipError_t LaunchShade(const float* d_vertices, const float* d_shade, const floa
         band_rows = band.row_count;
     }
     if (band.ids == nullptr || band.rgba == nullptr || band.offsets == nullptr || frames > 65535 || band.row_count > 65535 ||
-        band_rows > band.row_count) {
+        band_rows > band.row_count || first_rows > band.row_count || (first_rows != 0 && interleaved != 0)) {
         return hipErrorInvalidValue;
     }
     TraceParams p{};
@@ -4217,7 +4226,7 @@ hipError_t LaunchShade(const float* d_vertices, const float* d_shade, const floa
     }
     const unsigned skip = skip_band < 0 ? 0xFFFFFFFFu : static_cast<unsigned>(skip_band);
     const std::size_t stored =
-        SRT_SHADE_COMPACT ? ShadeRowsLaunched(band.row_count, band_rows, interleaved, skip, own_bands) : band.row_count;
+        SRT_SHADE_COMPACT ? ShadeRowsLaunched(band.row_count, band_rows, interleaved, skip, own_bands, first_rows) : band.row_count;
     if (stored == 0) {
         return hipSuccess;
     }
@@ -4234,7 +4243,7 @@ hipError_t LaunchShade(const float* d_vertices, const float* d_shade, const floa
         const auto launch = [&](auto kernel) {
             hipLaunchKernelGGL(kernel, grid, dim3(kShadeThreads), 0, stream, p, ids, static_cast<unsigned>(band_rows),
                                static_cast<unsigned>(frames), static_cast<unsigned>(interleaved), offsets_stride / 2,
-                               skip, static_cast<unsigned>(own_bands), lay.bytes);
+                               skip, static_cast<unsigned>(own_bands), lay.bytes, static_cast<unsigned>(first_rows));
         };
         switch (band.id_planes) {  // the bit planes as a template argument: their loads unrolled
             case 0: launch(ShadeIdsKernel<true, 0>); break;
@@ -4252,7 +4261,7 @@ hipError_t LaunchShade(const float* d_vertices, const float* d_shade, const floa
         hipLaunchKernelGGL((ShadeIdsKernel<false, 0>), grid, dim3(kShadeThreads), 0, stream, p, ids,
                            static_cast<unsigned>(band_rows), static_cast<unsigned>(frames),
                            static_cast<unsigned>(interleaved), offsets_stride / 2, skip,
-                           static_cast<unsigned>(own_bands), size_t{0});
+                           static_cast<unsigned>(own_bands), size_t{0}, static_cast<unsigned>(first_rows));
     }
     return hipGetLastError();
 }

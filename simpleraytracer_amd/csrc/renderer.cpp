@@ -269,7 +269,7 @@ void DeviceScene::RecordOrder(hipStream_t stream) const {
 void DeviceScene::Shade(const float* d_offsets, const int* d_ids, float* d_rgba, std::size_t row_begin,
                         std::size_t row_count, hipStream_t stream, std::size_t frames, std::size_t band_rows,
                         std::size_t interleaved, std::size_t offsets_stride, int id_planes, long skip_band,
-                        std::size_t own_bands) const {
+                        std::size_t own_bands, std::size_t first_rows) const {
     if (id_planes >= 0 && id_planes != IdPlanes(m_n)) {
         throw std::runtime_error("Shade: packed ids of this scene have " + std::to_string(IdPlanes(m_n)) + " bit planes");
     }
@@ -291,6 +291,9 @@ void DeviceScene::Shade(const float* d_offsets, const int* d_ids, float* d_rgba,
     if (band_rows > row_count || frames > 65535) {
         throw std::runtime_error("Shade: band_rows exceeds the rows shaded, or more than 65535 frames");
     }
+    if (first_rows > row_count || (first_rows != 0 && interleaved > 0)) {
+        throw std::runtime_error("Shade: first_rows exceeds the rows shaded, or with interleaved bands");
+    }
     if (row_count == 0 || frames == 0) {
         return;
     }
@@ -298,7 +301,7 @@ void DeviceScene::Shade(const float* d_offsets, const int* d_ids, float* d_rgba,
     BandArgs band{d_offsets, d_rgba, m_width, m_height, row_begin, row_count, const_cast<int*>(d_ids)};
     band.id_planes = id_planes;
     HipCheck(LaunchShade(m_vertices, m_shade, m_edges, m_n, m_frame, m_background, band, stream, frames, band_rows,
-                         interleaved, offsets_stride, skip_band, own_bands),
+                         interleaved, offsets_stride, skip_band, own_bands, first_rows),
              "shade kernel launch");
     RecordOrder(stream);
 }

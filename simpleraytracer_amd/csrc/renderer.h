@@ -84,7 +84,8 @@ public:
                hipStream_t stream, std::size_t frames = 1, std::size_t band_rows = 0,
                std::size_t interleaved = 0, std::size_t offsets_stride = 0, int id_planes = -1,
                long skip_band = -1,  // skip_band: rows of that band are left as they are
-               std::size_t own_bands = 0) const;  // and of bands [0, own_bands) (render.h LaunchShade)
+               std::size_t own_bands = 0,  // and of bands [0, own_bands) (render.h LaunchShade)
+               std::size_t first_rows = 0) const;  // contiguous: band 0's rows (BandSplit::first_rows)
     // `frames` (<= render.h kMaxTableFrames) frames of the prepared camera, rows [row_begin,
     // row_begin + row_count) each: frame f's offsets d_offsets[f], its RGBA d_rgba[f] or (d_ids
     // non-null) its hit ids d_ids[f]. Each frame gets the whole per-frame pipeline (record setup,

@@ -104,6 +104,34 @@ def test_engine_fake_devices_rotated_bitwise(gpu, scenes, p, h):
         assert e.verify() == (0, 2 * F)
 
 
+@pytest.mark.parametrize("own,h", [("", 100), ("50", 100), ("90", 100), ("1", 100), ("75", 1080), ("99", 61)])
+def test_engine_fake_devices_rotated_two_device_split(gpu, scenes, monkeypatch, own, h):
+    """Two devices, rotated all-to-all: the compositor's own band 0 takes SRT_ROTATE_OWN per cent of the
+    frame (default 75, rounded to tile rows; engine.cpp RotateOwnRows), band 1 -- the one that crosses
+    the link and is shaded from ids -- the rest: every frame bit for bit against a one-device render, and
+    the engine's band-0 rows equal to the restatement (bands.rotate_own_rows)."""
+    from simpleraytracer_amd.bands import rotate_own_rows
+
+    if own:
+        monkeypatch.setenv("SRT_ROTATE_OWN", own)
+    else:
+        monkeypatch.delenv("SRT_ROTATE_OWN", raising=False)
+    p, F = 2, 4
+    w = 130 if h < 1000 else 64
+    inputs = random_inputs(2 * F, h, w, seed=77)
+    refs = [torch_render(scenes["soup2k"], w, h, inputs[k]) for k in range(2 * F)]
+    with engine(scenes["soup2k"], w, h, devices=[0] * p, rows="rotated", exchange="alltoall", queues=2,
+                batch=F) as e:
+        info = e.info()
+        assert info["band_rows"] == rotate_own_rows(h) and info["buffer_rows"] == h - rotate_own_rows(h)
+        e.set_inputs(inputs)
+        e.run(3)
+        for k in range(F, 3 * F):
+            got = e.read_frame(k)
+            assert np.array_equal(got.view(np.uint32), refs[k % (2 * F)].view(np.uint32)), (own, k)
+        assert e.verify() == (0, 2 * F)
+
+
 def test_engine_rotated_needs_alltoall(gpu, scenes):
     from simpleraytracer_amd.device import SrtError
 
