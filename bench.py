@@ -524,6 +524,50 @@ def e2e_ml_api(scene_path, W, H, reps=10, warmup=3, devices=None):
     return {"mrays_per_s": round(W * H / dt / 1e6, 4), "ms_per_frame": round(dt * 1e3, 3)}, frame
 
 
+def ml_multi_fields(path, W, H, devices, one_device):
+    """mlInfer over `devices` (ML_VISIBLE_DEVICES) with the RCCL gather (device copies when a device
+    repeats) and with per-device D2H into disjoint rows (direct): SURVEY 8(e)'s "report both"."""
+    out = {}
+    old_gather = os.environ.get("SRT_GATHER")
+    for mode in ("copy" if one_device else "rccl", "direct"):
+        try:
+            os.environ["SRT_GATHER"] = mode
+            e2e, _ = e2e_ml_api(path, W, H, devices=devices)
+            out[mode] = {
+                **e2e, "devices": devices,
+                "path": ("mlInfer over ML_VISIBLE_DEVICES: H2D band offsets + interleaved band traces (hit ids) "
+                         "+ gather to device 0 + shading + one D2H") if mode != "direct" else
+                        ("mlInfer over ML_VISIBLE_DEVICES: H2D band offsets + band traces + shading on every "
+                         "device + per-device D2H into disjoint rows of the host image (no gather)")}
+        except Exception as e:  # noqa: BLE001
+            out[mode] = {"error": f"{type(e).__name__}: {e}"}
+        finally:
+            if old_gather is None:
+                os.environ.pop("SRT_GATHER", None)
+            else:
+                os.environ["SRT_GATHER"] = old_gather
+    return out
+
+
+def ml_multi_child(path, W, H, devices, timeout_s=240):
+    """ml_multi_fields in a child process (rank 0 of a one-rank-per-GPU job), bounded by timeout_s."""
+    import subprocess
+
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
+                        "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID")}
+    arg = json.dumps({"path": str(path), "W": W, "H": H, "devices": devices})
+    try:
+        r = subprocess.run([sys.executable, os.path.abspath(__file__), "--ml-multi-child", arg], env=env,
+                           capture_output=True, text=True, timeout=timeout_s)
+    except subprocess.TimeoutExpired:
+        return {"error": f"mlInfer over {len(devices)} GPUs did not finish in {timeout_s} s (child killed)"}
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    if r.returncode != 0 or not lines:
+        return {"error": f"child exit {r.returncode}: {(r.stderr or r.stdout)[-400:]}"}
+    return json.loads(lines[-1])
+
+
 def main():
     a = parse()
     if a.frames_per_step < 1 or a.queues < 1:
@@ -786,28 +830,16 @@ def main():
                                                  "SRT_E2E_CHUNKS) + trace storing each chunk's framebuffer rows "
                                                  "straight into the page-locked host image (SRT_E2E_DIRECT)",
                                   "host_link": peaks, "roofline": e2e_roofline(e2e, peaks, W, H)}
-        if world > 1 and not job.ranked and not a.no_e2e and extras:
+        if world > 1 and not a.no_e2e and extras:
             # the drop-in path over the N GPUs: the bands gathered to GPU 0 (RCCL; device copies on fake
-            # devices) and one D2H, or every GPU copying its rows straight into the host image (direct)
-            line["ml_multi"] = {}
-            old_gather = os.environ.get("SRT_GATHER")
-            for mode in ("copy" if job.one_device else "rccl", "direct"):
-                try:
-                    os.environ["SRT_GATHER"] = mode
-                    e2e, _ = e2e_ml_api(path, W, H, devices=job.devices)
-                    line["ml_multi"][mode] = {
-                        **e2e, "devices": job.devices,
-                        "path": ("mlInfer over ML_VISIBLE_DEVICES: H2D band offsets + interleaved band traces (hit ids) "
-                                 "+ gather to device 0 + shading + one D2H") if mode != "direct" else
-                                ("mlInfer over ML_VISIBLE_DEVICES: H2D band offsets + band traces + shading on every "
-                                 "device + per-device D2H into disjoint rows of the host image (no gather)")}
-                except Exception as e:  # noqa: BLE001
-                    line["ml_multi"][mode] = {"error": f"{type(e).__name__}: {e}"}
-                finally:
-                    if old_gather is None:
-                        os.environ.pop("SRT_GATHER", None)
-                    else:
-                        os.environ["SRT_GATHER"] = old_gather
+            # devices) and one D2H, or every GPU copying its rows straight into the host image (direct).
+            # One rank per GPU (the other ranks wait at the barrier below, their engines closed): rank 0
+            # runs it over every GPU in a child process under a time limit, so a stuck GPU call there
+            # cannot hold the job.
+            if job.ranked:
+                line["ml_multi"] = ml_multi_child(path, W, H, list(range(world)))
+            else:
+                line["ml_multi"] = ml_multi_fields(path, W, H, job.devices, job.one_device)
         if world == 1 and not a.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(path, a)
         print(json.dumps(line), flush=True)
@@ -824,6 +856,11 @@ def error_line(e):
 
 
 if __name__ == "__main__":
+    if len(sys.argv) == 3 and sys.argv[1] == "--ml-multi-child":  # bench.ml_multi_child
+        _c = json.loads(sys.argv[2])
+        print(json.dumps(ml_multi_fields(_c["path"], _c["W"], _c["H"], _c["devices"],
+                                         len(set(_c["devices"])) < len(_c["devices"]))), flush=True)
+        sys.exit(0)
     try:
         main()
     except SystemExit:

@@ -1168,6 +1168,16 @@ constexpr int kWindowPackets = SRT_WINDOW_PACKETS;  // packet walk: packets per 
 constexpr unsigned kWindowPixels = kWindowPackets * kWave;
 static_assert(kWindowPackets == 2 * kWave, "window prefix: two packets per lane");
 
+#ifndef SRT_LDS_SWIZZLE
+#define SRT_LDS_SWIZZLE 0
+#endif
+// Column slot of pixel (row, col) in the block's 8-B-per-pixel LDS tables (positions, keys). With
+// SRT_LDS_SWIZZLE the column is XORed with the row: a 512-B row puts column c of every row in the same
+// bank pair, so the lanes of a packet walking a narrow range (several rows, few columns) conflicted.
+__device__ __forceinline__ unsigned PixSlot(unsigned row, unsigned col) {
+    return SRT_LDS_SWIZZLE ? (col ^ row) & (kWave - 1u) : col;
+}
+
 // Batch entry of thread tid's slice e (kPacketBatch < kCullThreads: the first threads only).
 __device__ __forceinline__ bool InBatch(int e, int tid) { return e * kCullThreads + tid < kPacketBatch; }
 
@@ -1335,7 +1345,7 @@ __device__ __forceinline__ void PacketTables(CullShared& sh, const Rays<kCullR>&
 #pragma unroll
     for (int r = 0; r < R; ++r) {
 #ifndef SRT_EXP_NO_FXY
-        sh.fxy[wave * R + r][lane] = make_float2(s.fx[r], s.fy[r]);
+        sh.fxy[wave * R + r][PixSlot(wave * R + r, lane)] = make_float2(s.fx[r], s.fy[r]);
 #endif
     }
     if (regular) {
@@ -1615,7 +1625,12 @@ __device__ __forceinline__ void PacketBatch(CullShared& sh, const Box& bb, const
                         r = wrap ? r + 1u : r;
                     }
                     const bool ok = in && r < nr;
+#if SRT_LDS_SWIZZLE
+                    const unsigned ra = (base >> 9) + r, ca = ((base >> 3) & (kWave - 1u)) + c;
+                    px[u][j] = PacketPixel{ok ? (ra << 9) + (PixSlot(ra, ca) << 3) : 0u, ok};
+#else
                     px[u][j] = PacketPixel{ok ? base + (r << 9) + (c << 3) : 0u, ok};
+#endif
                 }
             }
             PacketHit h[kPacketIlp][kLanePixels];
@@ -1624,7 +1639,8 @@ __device__ __forceinline__ void PacketBatch(CullShared& sh, const Box& bb, const
 #pragma unroll
                 for (int j = 0; j < kLanePixels; ++j) {
 #ifdef SRT_EXP_NO_FXY  // measurement builds only (regular tiles: the position tables are the positions)
-                    f[u][j] = make_float2(sh.clo[(px[u][j].pixb >> 3) & 63u], sh.rlo[px[u][j].pixb >> 9]);
+                    f[u][j] = make_float2(sh.clo[PixSlot(px[u][j].pixb >> 9, (px[u][j].pixb >> 3) & 63u)],
+                                          sh.rlo[px[u][j].pixb >> 9]);
 #else
                     f[u][j] = *reinterpret_cast<const float2*>(fxy + px[u][j].pixb);
 #endif
@@ -3017,7 +3033,7 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(c
     unsigned long long key[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        key[r] = sh.keys[wave * R + r][lane];
+        key[r] = sh.keys[wave * R + r][PixSlot(wave * R + r, lane)];
     }
     if (nchunks > 1u) {
         constexpr int kPix = kBlockRows * kWave;
@@ -3175,7 +3191,7 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(c
 #ifdef SRT_EXP_NO_FXY
                 const float2 f = make_float2(sh.clo[lane], sh.rlo[wave * R + r]);
 #else
-                const float2 f = sh.fxy[wave * R + r][lane];
+                const float2 f = sh.fxy[wave * R + r][PixSlot(wave * R + r, lane)];
 #endif
                 StoreRgba(p, x, y, ShadeRecord(p, f.x, f.y, id[r], nr[r], al[r]));
             }

@@ -47,3 +47,19 @@ def test_bench_injected_failure_prints_error_record(gpu):
     assert r.returncode == 1, r.stderr[-2000:]
     rec = last_json(r.stdout)
     assert rec["value"] is None and "injected failure" in rec["error"], rec
+
+
+@pytest.mark.gpu
+def test_bench_ml_multi_child_process(gpu, scenes):
+    """The N > 1 line's ml_multi in a one-rank-per-GPU job runs in a child process of rank 0 under a time
+    limit (bench.ml_multi_child): here over two fake devices -- both the gather (device copies) and the
+    direct per-device D2H produce a rate, and a child that outlives its limit is reported, not waited for."""
+    sys.path.insert(0, str(REPO))
+    import bench
+
+    out = bench.ml_multi_child(scenes["soup2k"], 320, 200, [0, 0], timeout_s=240)
+    assert set(out) == {"copy", "direct"}, out
+    for mode in ("copy", "direct"):
+        assert out[mode]["mrays_per_s"] > 0 and out[mode]["devices"] == [0, 0], out
+    late = bench.ml_multi_child(scenes["soup2k"], 320, 200, [0, 0], timeout_s=0.01)
+    assert "did not finish" in late["error"], late
