@@ -1168,6 +1168,9 @@ constexpr int kWindowPackets = SRT_WINDOW_PACKETS;  // packet walk: packets per 
 constexpr unsigned kWindowPixels = kWindowPackets * kWave;
 static_assert(kWindowPackets == 2 * kWave, "window prefix: two packets per lane");
 
+#ifndef SRT_PK_READLANE
+#define SRT_PK_READLANE 0
+#endif
 #ifndef SRT_LDS_SWIZZLE
 #define SRT_LDS_SWIZZLE 0
 #endif
@@ -1596,8 +1599,15 @@ __device__ __forceinline__ void PacketBatch(CullShared& sh, const Box& bb, const
                 if (kk & 1u) {
                     z += static_cast<unsigned>(__builtin_amdgcn_readlane(static_cast<int>(ca), src));
                 }
+#if SRT_PK_READLANE
+                // from the scan's registers: lane kk / 2 holds packets 2l (pa) and 2l + 1 (pb)
+                const uint2 e = make_uint2(
+                    static_cast<unsigned>(__builtin_amdgcn_readlane(static_cast<int>((kk & 1u) ? pb.x : pa.x), src)),
+                    static_cast<unsigned>(__builtin_amdgcn_readlane(static_cast<int>((kk & 1u) ? pb.y : pa.y), src)));
+#else
                 const uint2 e = pkb[kk];  // one address: a broadcast read (from the scan's registers by
-                                          // readlane: 2 VGPR spills, measured 3 % slower)
+                                          // readlane: 2 VGPR spills in round 2, measured 3 % slower)
+#endif
                 const unsigned g = w0 + kk * kWave + static_cast<unsigned>(lane);
                 const unsigned sl = min(__builtin_amdgcn_mbcnt_hi(e.y, __builtin_amdgcn_mbcnt_lo(e.x, 0u)) + z,
                                         last_slot);
