@@ -3,12 +3,12 @@
 # host code and of the oracle (`make asan`), on a host without a GPU: the CPU backend
 # (ML_VISIBLE_DEVICES=cpu: cpu_render.cpp's threads and _Float16 paths), scene files and OBJ import,
 # the ml* ABI, the screen-box host solve, the engine's pool failure handling, and the oracle.
-# SURVEY.md section 5. Log: profiles/r04/asan/pytest_cpu_asan.log.
+# SURVEY.md section 5. Log: profiles/r05/asan/pytest_cpu_asan.log (ASAN_OUT).
 set -o pipefail
 cd "$(dirname "$0")/.."
 make -s asan || exit 1
 RT=$(/opt/rocm/lib/llvm/bin/clang -print-file-name=libclang_rt.asan-x86_64.so)
-OUT=profiles/r04/asan
+OUT=${ASAN_OUT:-profiles/r05/asan}
 mkdir -p "$OUT"
 export SRT_LIB="$PWD/simpleraytracer_amd/lib_asan/libModelRunner.so"
 export SRT_ORACLE_LIB="$PWD/oracle/build_asan/libsrt_oracle.so"
