@@ -2653,9 +2653,6 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(c
     const TraceParams& p = batch[blockIdx.z];
     constexpr int R = kCullR;
     __shared__ CullShared sh;
-#ifdef SRT_EXP_TRACE_PRIO_ALL  // measurement builds only: trace waves ahead of the other queue's setup waves
-    __builtin_amdgcn_s_setprio(SRT_EXP_TRACE_PRIO_ALL);
-#endif
 #ifdef SRT_DIAG
     const unsigned long long d_rt0 = __builtin_amdgcn_s_memrealtime();
     const unsigned d_blk = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
