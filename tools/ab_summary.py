@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Summary of a tools/gpu_libs.sh A/B in gpurun_out/: per library the bench value, the single-queue
+"""Summary of a tools/gpu_runs/gpu_libs.sh A/B in gpurun_out/: per library the bench value, the single-queue
 rate, the HIP-event stage times and the one-queue rocprofv3 kernel means / minima.
 
     python tools/ab_summary.py base old ...

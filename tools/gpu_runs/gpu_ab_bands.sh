@@ -1,6 +1,6 @@
 #!/bin/bash
 # GPU tests, a bench A/B of LIBS and the band simulation of each library (C3, and C5 when C5=1).
-LIBS="${LIBS:-base prev}" bash tools/gpu_ab_check.sh || exit $?
+LIBS="${LIBS:-base prev}" bash tools/gpu_runs/gpu_ab_check.sh || exit $?
 source "$(dirname "$0")/gpu_lib.sh"
 for name in ${LIBS:-base prev}; do
     if [ "$name" = base ]; then unset SRT_LIB; else export SRT_LIB=simpleraytracer_amd/lib_ab/$name/libModelRunner.so; fi

@@ -1,4 +1,4 @@
-source tools/gpu_lib.sh
+source tools/gpu_runs/gpu_lib.sh
 for v in ord0 ord1 ord4; do
   SRT_LIB=simpleraytracer_amd/lib_ab/$v/libModelRunner.so run e2e_$v 120 python tools/e2e_probe.py --chunks 4,1 || exit 1
   SRT_LIB=simpleraytracer_amd/lib_ab/$v/libModelRunner.so run bench_$v 200 python bench.py --no-extras --no-cpu-baseline --steps 100 || exit 1

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Same-box A/B of library variants (VARIANTS, as in tools/gpu_ab_variants.sh) on the P = 8 rank
+# Same-box A/B of library variants (VARIANTS, as in tools/gpu_runs/gpu_ab_variants.sh) on the P = 8 rank
 # simulation alone, REPS times interleaved, with QUEUES frame queues.
 source "$(dirname "$0")/gpu_lib.sh"
 for rep in $(seq 1 ${REPS:-2}); do

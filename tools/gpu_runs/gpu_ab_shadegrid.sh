@@ -1,6 +1,6 @@
 #!/bin/bash
 # Compacted shade grid: GPU parity (parity, golden, engine), one-queue kernel statistics of the rank
-# simulations (tools/gpu_prof_share.sh), then rank simulations (2 queues) of lib_ab/old vs the
+# simulations (tools/gpu_runs/gpu_prof_share.sh), then rank simulations (2 queues) of lib_ab/old vs the
 # product at P = 2 share / all-to-all and P = 8, twice interleaved.
 source "$(dirname "$0")/gpu_lib.sh"
 run sg_tests 400 python -u -m pytest tests/test_gpu_parity.py tests/test_golden_full.py tests/test_gpu_engine.py \

@@ -1,7 +1,7 @@
 #!/bin/bash
 # GPU tests, then an A/B of library builds (LIBS) and one SQ counter pass of the product ($PMC:
 # "lds" = the trace kernel's LDS counters, else the bin kernel's wave-cycle split).
-LIBS="${LIBS:-base prev}" bash tools/gpu_ab_check.sh || exit $?
+LIBS="${LIBS:-base prev}" bash tools/gpu_runs/gpu_ab_check.sh || exit $?
 source "$(dirname "$0")/gpu_lib.sh"
 Q="--steps 50 --warmup 5 --queues 1 --batch 1 --no-extras --no-cpu-baseline"
 if [ "${PMC:-bin}" = lds ]; then

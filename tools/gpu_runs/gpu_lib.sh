@@ -3,7 +3,7 @@
 # time limit with output in gpurun_out/NAME.log; a crash-type exit (fault, abort, segfault,
 # timeout: anything but 0 or 1) ends the calling script, test failures (1) do not.
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "${BASH_SOURCE[0]}")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "${BASH_SOURCE[0]}")/../..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 run() {

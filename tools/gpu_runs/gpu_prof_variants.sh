@@ -1,6 +1,6 @@
 #!/bin/bash
 # Same-box kernel statistics of the P = 8 rank simulation for library variants (VARIANTS, as in
-# tools/gpu_ab_variants.sh), with QUEUES frame queues (one: each kernel's own time).
+# tools/gpu_runs/gpu_ab_variants.sh), with QUEUES frame queues (one: each kernel's own time).
 source "$(dirname "$0")/gpu_lib.sh"
 for q in ${QUEUES:-1 2}; do
     for v in ${VARIANTS:-old product}; do

@@ -14,4 +14,4 @@ for P in 8 2; do
   run ps_rot$P 300 rocprofv3 --kernel-trace --stats -d gpurun_out/ps_rot$P -o run --output-format csv -- \
       python3 tools/rank_sim.py --ranks $P --exchange alltoall --rows rotated --queues 1 --steps 10
 done
-bash tools/gpu_r5_stalls.sh
+bash tools/gpu_runs/gpu_r5_stalls.sh

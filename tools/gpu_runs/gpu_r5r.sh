@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 5: bin-launch LDS padding probe (bench A/B) and 8 shading rows per thread (rank simulation).
 source "$(dirname "$0")/gpu_lib.sh"
-VARIANTS="product binpad" ROUNDS="1 2" bash tools/gpu_r5m.sh
+VARIANTS="product binpad" ROUNDS="1 2" bash tools/gpu_runs/gpu_r5m.sh
 for v in product rows8; do
   if [ $v = product ]; then L=simpleraytracer_amd/lib/libModelRunner.so; else L=simpleraytracer_amd/lib_exp/$v/libModelRunner.so; fi
   for P in 2 8; do

@@ -1,4 +1,4 @@
-source tools/gpu_lib.sh
+source tools/gpu_runs/gpu_lib.sh
 Q="--steps 50 --warmup 5 --queues 1 --batch 1 --no-extras --no-cpu-baseline"
 for n in base spatial; do
   if [ $n = base ]; then unset SRT_LIB; else export SRT_LIB=simpleraytracer_amd/lib_ab/$n/libModelRunner.so; fi

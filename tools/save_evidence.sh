@@ -1,5 +1,5 @@
 #!/bin/bash
-# Copy a tools/gpu_round3.sh (or gpu_round.sh) session's outputs from gpurun_out/ into profiles/<dir> (tracked),
+# Copy a tools/gpu_runs/gpu_round3.sh (or gpu_round.sh) session's outputs from gpurun_out/ into profiles/<dir> (tracked),
 # and the PMC summaries bench.py reads into profiles/ itself.
 set -eu
 dir=${1:?usage: tools/save_evidence.sh profiles/rNN/evidence}
