@@ -693,7 +693,7 @@ def main():
             except Exception as e:  # noqa: BLE001 -- the primary line must still be printed
                 legs[name] = {"error": f"{type(e).__name__}: {e}"}
         if main == ("bands", "alltoall", "rotated") and world == 2:
-            # the two-device split at even halves (the value's split gives the compositor's band 0 3/4 of
+            # the two-device split at even halves (the value's split gives the compositor's band 0 4/5 of
             # the frame: engine.cpp RotateOwnRows)
             prev = os.environ.get("SRT_ROTATE_OWN")
             os.environ["SRT_ROTATE_OWN"] = "50"

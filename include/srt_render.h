@@ -158,7 +158,7 @@ typedef struct srt_engine_t* srt_engine;
 #define SRT_ROWS_ROTATED 2 /* contiguous bands, device p tracing band (p + c) % P of a frame composited on
                               device c (SRT_EXCHANGE_ALLTOALL): even load, one block of rows per band; over
                               two devices the compositor's own band 0 takes env SRT_ROTATE_OWN per cent of
-                              the frame (default 75, 50 = halves): only band 1 crosses the one link */
+                              the frame (default 80, 50 = halves): only band 1 crosses the one link */
 #define SRT_EXCHANGE_ALLTOALL 0
 #define SRT_EXCHANGE_ROTATING 1
 #define SRT_EXCHANGE_ROOT 2

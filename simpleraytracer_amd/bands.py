@@ -60,13 +60,13 @@ def rotated_band(world: int, device: int, compositor: int) -> int:
 
 def rotate_own_rows(height: int, pct: int | None = None) -> int:
     """Rows of the compositor's own band (band 0) under the rotated all-to-all over two devices
-    (csrc/engine.cpp RotateOwnRows): ``pct`` per cent of the frame (env SRT_ROTATE_OWN, default 75),
+    (csrc/engine.cpp RotateOwnRows): ``pct`` per cent of the frame (env SRT_ROTATE_OWN, default 80),
     rounded to whole 16-row tile rows, kept inside [1, H - 1]; the other band takes the rest."""
     import os
 
     if pct is None:
         v = os.environ.get("SRT_ROTATE_OWN", "")
-        pct = int(v) if v.strip() else 75
+        pct = int(v) if v.strip() else 80
     pct = max(1, min(99, pct))
     rows = (height * pct + 50) // 100
     if height > 2 * TILE_ROWS:

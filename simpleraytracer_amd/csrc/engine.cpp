@@ -63,13 +63,14 @@ std::size_t ShareAuto(std::size_t height, std::size_t world) {
 }
 
 // Rows of the compositor's own band under rotated all-to-all over two devices (env SRT_ROTATE_OWN: per
-// cent of the frame, default 75; 50 = even halves), rounded to whole 16-row tile rows. Even halves send
+// cent of the frame, default 80; 50 = even halves), rounded to whole 16-row tile rows. Even halves send
 // half of every frame's ids over the one link: 1.1 MB per frame of the job each way at 1080p, 17 us at an
-// assumed 64 GB/s against 11 us of GPU time (rank simulation) -- link-bound below one GPU; a quarter
-// halves that and the compositor's deferred shading with it.
+// assumed 64 GB/s against 11 us of GPU time (rank simulation) -- link-bound below one GPU; a fifth
+// (216 of 1080 rows) cuts that to 7.2 us (GPU-bound down to ~45 GB/s) and the compositor's deferred
+// shading with it.
 std::size_t RotateOwnRows(std::size_t height) {
     const char* v = std::getenv("SRT_ROTATE_OWN");
-    long pct = v == nullptr || *v == '\0' ? 75 : std::strtol(v, nullptr, 10);
+    long pct = v == nullptr || *v == '\0' ? 80 : std::strtol(v, nullptr, 10);
     pct = std::max(1L, std::min(99L, pct));
     const std::size_t t = static_cast<std::size_t>(kCullTileRows);
     std::size_t rows = (height * static_cast<std::size_t>(pct) + 50) / 100;

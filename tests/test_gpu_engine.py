@@ -107,7 +107,7 @@ def test_engine_fake_devices_rotated_bitwise(gpu, scenes, p, h):
 @pytest.mark.parametrize("own,h", [("", 100), ("50", 100), ("90", 100), ("1", 100), ("75", 1080), ("99", 61)])
 def test_engine_fake_devices_rotated_two_device_split(gpu, scenes, monkeypatch, own, h):
     """Two devices, rotated all-to-all: the compositor's own band 0 takes SRT_ROTATE_OWN per cent of the
-    frame (default 75, rounded to tile rows; engine.cpp RotateOwnRows), band 1 -- the one that crosses
+    frame (default 80, rounded to tile rows; engine.cpp RotateOwnRows), band 1 -- the one that crosses
     the link and is shaded from ids -- the rest: every frame bit for bit against a one-device render, and
     the engine's band-0 rows equal to the restatement (bands.rotate_own_rows)."""
     from simpleraytracer_amd.bands import rotate_own_rows
