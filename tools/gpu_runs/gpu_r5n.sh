@@ -2,7 +2,7 @@
 # Round 5: what bounds the deferred shading (ShadeIdsKernel of a P = 8 rank, rotated all-to-all, one
 # queue): SQ wait / issue mix, L2 hit rate, HBM bytes; one --pmc pass each.
 source "$(dirname "$0")/gpu_lib.sh"
-R="python3 tools/rank_sim.py --ranks 8 --exchange alltoall --rows rotated --queues 1 --steps 3 --warmup 1"
+R="python3 tools/rank_sim.py --ranks ${SH_P:-8} --exchange alltoall --rows rotated --queues 1 --steps 3 --warmup 1"
 K="--kernel-include-regex ShadeIdsKernel"
 pass() { local n=$1; shift; run sh_$n 120 timeout -s KILL 100 rocprofv3 --pmc "$@" $K -d gpurun_out/sh_$n -o run --output-format csv -- $R; }
 pass sq SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD
