@@ -226,6 +226,9 @@ ML_API_ENTRY int srtEnginePoolSelfTest(size_t workers, size_t failing, int mode,
 /* SRT_EXCHANGE_SHARE's default tile rows per cycle for a frame of `height` rows over `devices`
  * devices: the largest power of two <= 32 with share + devices - 1 <= ceil(height / 16). */
 ML_API_ENTRY size_t srtShareAuto(size_t height, size_t devices);
+/* SRT_ROWS_ROTATED over two devices: rows of the compositor's own band 0 for a frame of `height` rows
+ * (env SRT_ROTATE_OWN per cent, default 80, rounded to 16-row tile rows, within [1, height - 1]). */
+ML_API_ENTRY size_t srtRotateOwnRows(size_t height);
 /* Shape of the run: devices in the job, local devices, rows of local device 0's band, rows of every
  * band buffer, whether the exchange uses RCCL, exchanged bytes per frame (bands, all devices). */
 ML_API_ENTRY int srtEngineInfo(srt_engine engine, size_t* devices, size_t* local_devices, size_t* band_rows,

@@ -150,6 +150,7 @@ _SIGNATURES = {
     "srtEnginePoolSelfTest": (ctypes.c_int, [_SZ, _SZ, ctypes.c_int, ctypes.c_double, _PD, ctypes.POINTER(ctypes.c_int),
                                              ctypes.c_char_p, _SZ]),
     "srtShareAuto": (_SZ, [_SZ, _SZ]),
+    "srtRotateOwnRows": (_SZ, [_SZ]),
     "srtEngineInfo": (ctypes.c_int, [ctypes.c_void_p, _PSZ, _PSZ, _PSZ, _PSZ, ctypes.POINTER(ctypes.c_int), _PD]),
     "srtExchangeHost": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), _SZ, _SZ, _SZ, ctypes.c_int, ctypes.c_int, _SZ,
                                        _SZ, ctypes.POINTER(ctypes.c_void_p), _PSZ, _PSZ]),

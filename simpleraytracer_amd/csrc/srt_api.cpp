@@ -559,6 +559,10 @@ ML_API_ENTRY size_t srtShareAuto(size_t height, size_t devices) {
     return srt::ShareAuto(height, devices);
 }
 
+ML_API_ENTRY size_t srtRotateOwnRows(size_t height) {
+    return srt::RotateOwnRows(height);
+}
+
 ML_API_ENTRY int srtEngineInfo(srt_engine engine, size_t* devices, size_t* local_devices, size_t* band_rows,
                                size_t* buffer_rows, int* rccl, double* exchange_bytes_per_frame) {
     return Guarded([&] {

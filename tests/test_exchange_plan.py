@@ -183,3 +183,20 @@ def test_share_exchange_layout_reassembles_every_frame(p, h, share, frames, b):
         own[rows[c, c]] = truth[f, rows[c, c]]
         got = unscramble_share(recv[c], f // p, h, k, own)
         assert np.array_equal(got, truth[f]), (c, f)
+
+
+@pytest.mark.parametrize("own", ["", "50", "80", "1", "99", "150", "-5"])
+def test_rotate_own_rows_matches_library(monkeypatch, own):
+    """bands.rotate_own_rows (the Python restatement the bench and the tests use) against the engine's
+    RotateOwnRows (srtRotateOwnRows) over frame heights from 1 row to 4K, default and overridden splits."""
+    from simpleraytracer_amd import _native
+    from simpleraytracer_amd.bands import rotate_own_rows
+
+    if own:
+        monkeypatch.setenv("SRT_ROTATE_OWN", own)
+    else:
+        monkeypatch.delenv("SRT_ROTATE_OWN", raising=False)
+    lib = _native.lib()
+    for h in list(range(1, 70)) + [100, 135, 1079, 1080, 2160, 4321]:
+        assert lib.srtRotateOwnRows(h) == rotate_own_rows(h), (own, h)
+        assert 1 <= rotate_own_rows(h) <= max(1, h - 1)
