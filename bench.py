@@ -258,8 +258,60 @@ def run_leg(job, a, path, inputs, steps, warmup, **kw):
         eng.close()
 
 
+def cpu_binned(scene_path, a, threads, seconds, oracle_rows=None):
+    """The product's own CPU render path -- the backend the GPU path drops in for: mlInfer with
+    ML_VISIBLE_DEVICES=cpu (csrc/cpu_render.cpp: records binned to 16 x 16 pixel tiles, the kernels'
+    canonical math, threads over tiles) -- timed over whole frames on `threads` host threads (env
+    SRT_CPU_THREADS), at least one and as many as fit `seconds`. oracle_rows = (rows, frame) of the
+    brute-force oracle on the same offsets: the binned frame's ids are compared there bit for bit."""
+    import numpy as np
+
+    import simpleraytracer_amd as srt
+
+    keep = {k: os.environ.get(k) for k in ("ML_VISIBLE_DEVICES", "SRT_CPU_THREADS")}
+    os.environ["ML_VISIBLE_DEVICES"] = "cpu"
+    os.environ["SRT_CPU_THREADS"] = str(threads)
+    try:
+        ctx = srt.Context()
+        model = ctx.create_model(scene_path)
+        model.set_input_info(a.width, a.height)
+        (idt, iw, ih, ic), (odt, ow, oh, oc) = model.info()
+        inp = ctx.create_image(idt, iw, ih, ic)
+        out = ctx.create_image(odt, ow, oh, oc)
+        inp.array()[...] = np.float32(0.5)
+        times = []
+        t_end = time.perf_counter() + seconds
+        while not times or time.perf_counter() < t_end:
+            t0 = time.perf_counter()
+            model.infer(inp, out)
+            times.append(time.perf_counter() - t0)
+        frame = out.array().copy()
+        for o in (inp, out, model, ctx):
+            o.close()
+    finally:
+        for k, v in keep.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    dt = sorted(times)[len(times) // 2]
+    res = {"value": round(a.width * a.height / dt / 1e6, 4), "unit": "Mrays/s", "cores": threads,
+           "kind": "port", "frames": len(times), "ms_per_frame": round(dt * 1e3, 2),
+           "sample": f"{len(times)} whole frames of {workload_name(a)} (median), uniform 0.5 offsets",
+           "path": "mlInfer with ML_VISIBLE_DEVICES=cpu (csrc/cpu_render.cpp): screen-box binning to 16x16 pixel "
+                   "tiles, exact canonical test, host threads over tiles -- the algorithm-matched CPU path the GPU "
+                   "path drops in for (same culling idea, same bit-identical output)"}
+    if oracle_rows is not None:
+        rows, ref = oracle_rows
+        res["parity_rows"] = len(rows)
+        res["parity_vs_oracle"] = bool(np.array_equal(frame[rows, :, 3].view(np.uint32),
+                                                      ref[rows, :, 3].view(np.uint32)))
+    return res
+
+
 def cpu_baseline(scene_path, a):
-    """The oracle ('port') on this host's cores over a bounded, evenly spaced row sample."""
+    """The oracle ('port') on this host's cores over a bounded, evenly spaced row sample, and beside it
+    the product's binned CPU path (cpu_binned) on the same threads."""
     from oracle import srt_oracle
 
     # OMP_NUM_THREADS is the GPU box's CPU share for one GPU (16 of its 256 host CPUs; gpurun and
@@ -276,7 +328,7 @@ def cpu_baseline(scene_path, a):
     want_rows = max(rows_cal, min(h, int(a.cpu_seconds / max(per_row, 1e-9))))
     step = max(1, h // want_rows)
     t0 = time.perf_counter()
-    sc.render(a.width, h, row_begin=0, row_count=h, row_step=step, threads=threads)
+    ref = sc.render(a.width, h, row_begin=0, row_count=h, row_step=step, threads=threads)
     dt = time.perf_counter() - t0
     rows = (h + step - 1) // step
     # single-thread scalar variant (BASELINE.md CPU plan (1)): a short row sample
@@ -293,9 +345,15 @@ def cpu_baseline(scene_path, a):
                 break
     except OSError:
         pass
+    try:
+        binned = cpu_binned(scene_path, a, threads, max(1.0, a.cpu_seconds / 2),
+                            (list(range(0, h, step)), ref))
+    except Exception as e:  # noqa: BLE001 -- the baseline beside it must still be reported
+        binned = {"error": f"{type(e).__name__}: {e}"}
     return {
         "single_thread": {"value": round(rows1 * a.width / dt1 / 1e6, 6), "unit": "Mrays/s", "cores": 1,
                           "sample": f"{rows1} rows (every {step1}th), {dt1:.1f} s"},
+        "binned": binned,
         "cpu_model": model,
         "host_cpus": os.cpu_count(),
         "value": round(rows * a.width / dt / 1e6, 6),
@@ -404,9 +462,9 @@ def whole_frame_fields(W, H, n_tri, ms_per_frame, world):
                     "the timed (overlapped) run; peak = 8 TB/s x GPUs"}
 
 
-def compositor_fraction(H, world, exchange, rows, share):
+def compositor_fraction(H, world, exchange, rows, share, own_rows=0):
     """Fraction of a frame's rows its compositor traces itself (straight into the frame as RGBA); the
-    rest arrives as hit ids from the other GPUs."""
+    rest arrives as hit ids from the other GPUs. own_rows: the engine's two-device split (srtEngineSplit)."""
     from simpleraytracer_amd import _native
     from simpleraytracer_amd.bands import band_range, interleaved_range, rotate_own_rows, share_frame_rows
 
@@ -415,8 +473,8 @@ def compositor_fraction(H, world, exchange, rows, share):
         return round(len(share_frame_rows(H, world, k, 0, 0)) / H, 5)
     if rows == "interleaved":
         return round(interleaved_range(H, world, 0)[1] / H, 5)
-    if rows == "rotated" and world == 2:  # the compositor's band 0 (engine.cpp RotateOwnRows)
-        return round(rotate_own_rows(H) / H, 5)
+    if rows == "rotated" and world == 2:  # the compositor's band 0 (engine.cpp EngineSplit)
+        return round((own_rows or rotate_own_rows(H)) / H, 5)
     return round(band_range(H, world, 0)[1] / H, 5)
 
 
@@ -583,6 +641,7 @@ def main():
     # value: the timed steps on the main engine
     eng = job.engine(path, a)
     info = eng.info()
+    split = eng.split()
     n_tri = None
     eng.set_inputs(inputs)
     elapsed, mrays = timed(job, eng, a.steps, a.warmup)
@@ -693,8 +752,8 @@ def main():
             except Exception as e:  # noqa: BLE001 -- the primary line must still be printed
                 legs[name] = {"error": f"{type(e).__name__}: {e}"}
         if main == ("bands", "alltoall", "rotated") and world == 2:
-            # the two-device split at even halves (the value's split gives the compositor's band 0 4/5 of
-            # the frame: engine.cpp RotateOwnRows)
+            # the two-device split at even halves (the value's split keeps the compositor's band 0 at the
+            # share the measured link allows -- engine.cpp RotateSplitForLink -- or 4/5 without RCCL)
             prev = os.environ.get("SRT_ROTATE_OWN")
             os.environ["SRT_ROTATE_OWN"] = "50"
             try:
@@ -803,7 +862,12 @@ def main():
                 line["exchange"] = {"pattern": a.exchange, "rows": a.rows,
                                     "transport": "RCCL" if info["rccl"] else "device copies",
                                     "share": share_k if a.exchange == "share" else None,
-                                    "compositor_fraction": compositor_fraction(H, world, a.exchange, a.rows, a.share),
+                                    "compositor_fraction": compositor_fraction(H, world, a.exchange, a.rows, a.share,
+                                                                               split["own_rows"]),
+                                    "split": {**split, "note": "own_rows: the compositor's own band over two GPUs "
+                                              "(rotated rows); link_gbs: RCCL send/receive groups of 32 MB timed at "
+                                              "engine creation, per direction of the slowest GPU; source 'link' = "
+                                              "the split derived from it (srtRotateSplitForLink, DESIGN.md 7)"},
                                     "ms_per_batch": round(ms_mean, 5) if ms_mean else None,
                                     "ms_per_batch_by_device": [round(x, 5) for x in ms_x],
                                     "bytes_per_link_per_batch": int(per_link) if per_link else None,
@@ -840,7 +904,7 @@ def main():
                 line["ml_multi"] = ml_multi_child(path, W, H, list(range(world)))
             else:
                 line["ml_multi"] = ml_multi_fields(path, W, H, job.devices, job.one_device)
-        if world == 1 and not a.no_cpu_baseline:
+        if not a.no_cpu_baseline:  # on every line, from rank 0 (the other ranks wait at the barrier below)
             line["cpu_baseline"] = cpu_baseline(path, a)
         print(json.dumps(line), flush=True)
     job.barrier()

@@ -182,6 +182,9 @@ typedef struct srt_engine_options {
                        frames, 64 for bands over more than one device) */
     int flags;      /* SRT_ENGINE_* bits (0 = none) */
     size_t share;   /* SRT_EXCHANGE_SHARE: the compositor's tile rows per cycle, a power of two (0 = srtShareAuto) */
+    size_t own_rows; /* SRT_ROWS_ROTATED over two devices: rows of the compositor's own band 0 (0 = env
+                        SRT_ROTATE_OWN if set, else derived from the link measured at creation when RCCL
+                        joins distinct devices -- srtRotateSplitForLink --, else 80 % of the frame) */
 } srt_engine_options;
 
 /* 128-byte RCCL unique id for srtEngineCreateRank (call on one rank, share with the others). */
@@ -226,9 +229,26 @@ ML_API_ENTRY int srtEnginePoolSelfTest(size_t workers, size_t failing, int mode,
 /* SRT_EXCHANGE_SHARE's default tile rows per cycle for a frame of `height` rows over `devices`
  * devices: the largest power of two <= 32 with share + devices - 1 <= ceil(height / 16). */
 ML_API_ENTRY size_t srtShareAuto(size_t height, size_t devices);
-/* SRT_ROWS_ROTATED over two devices: rows of the compositor's own band 0 for a frame of `height` rows
- * (env SRT_ROTATE_OWN per cent, default 80, rounded to 16-row tile rows, within [1, height - 1]). */
+/* SRT_ROWS_ROTATED over two devices without a measured link: rows of the compositor's own band 0 for a
+ * frame of `height` rows (env SRT_ROTATE_OWN, an integer per cent in 1..99, default 80, rounded to 16-row
+ * tile rows, within [1, height - 1]); 0 with srtGetLastError set when SRT_ROTATE_OWN is not such an integer. */
 ML_API_ENTRY size_t srtRotateOwnRows(size_t height);
+/* The two-device split an engine derives from its link: for a link of `link_gbs`
+ * GB/s per direction, a one-GPU frame time of `frame_us` microseconds and an exchange payload of
+ * `bytes_per_pixel`, the smallest own band -- whole 16-row tile rows, at least half the frame -- whose
+ * link time per frame of the job, (height - rows) x width x bytes_per_pixel / 2 / rate, stays within
+ * 80 % of the GPUs' time per frame of the job, frame_us x (0.553 + 0.25 (height - rows) / height); the
+ * largest own band (one tile row sent) when none does. */
+ML_API_ENTRY size_t srtRotateSplitForLink(size_t height, size_t width, double link_gbs, double frame_us,
+                                          double bytes_per_pixel);
+/* The engine's two-device split: own band rows (0 unless rotated bands over two devices), the band
+ * buffers' rows, the link rate measured at creation (GB/s per direction of the slowest device: RCCL
+ * send / receive groups of 32 MB; 0 without RCCL), the one-GPU frame time measured for the split (us; 0
+ * when not derived), and the source: 0 none, 1 the option, 2 env SRT_ROTATE_OWN, 3 the measured link,
+ * 4 the 80 % default. One rank per process: the ranks' splits are compared at creation (a mismatch fails
+ * the create). */
+ML_API_ENTRY int srtEngineSplit(srt_engine engine, size_t* own_rows, size_t* buffer_rows, double* link_gbs,
+                                double* frame_us, int* source);
 /* Shape of the run: devices in the job, local devices, rows of local device 0's band, rows of every
  * band buffer, whether the exchange uses RCCL, exchanged bytes per frame (bands, all devices). */
 ML_API_ENTRY int srtEngineInfo(srt_engine engine, size_t* devices, size_t* local_devices, size_t* band_rows,

@@ -81,6 +81,7 @@ class EngineOptions(ctypes.Structure):
         ("launch", ctypes.c_size_t),
         ("flags", ctypes.c_int),
         ("share", ctypes.c_size_t),
+        ("own_rows", ctypes.c_size_t),
     ]
 
 
@@ -151,6 +152,8 @@ _SIGNATURES = {
                                              ctypes.c_char_p, _SZ]),
     "srtShareAuto": (_SZ, [_SZ, _SZ]),
     "srtRotateOwnRows": (_SZ, [_SZ]),
+    "srtRotateSplitForLink": (_SZ, [_SZ, _SZ, ctypes.c_double, ctypes.c_double, ctypes.c_double]),
+    "srtEngineSplit": (ctypes.c_int, [ctypes.c_void_p, _PSZ, _PSZ, _PD, _PD, ctypes.POINTER(ctypes.c_int)]),
     "srtEngineInfo": (ctypes.c_int, [ctypes.c_void_p, _PSZ, _PSZ, _PSZ, _PSZ, ctypes.POINTER(ctypes.c_int), _PD]),
     "srtExchangeHost": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), _SZ, _SZ, _SZ, ctypes.c_int, ctypes.c_int, _SZ,
                                        _SZ, ctypes.POINTER(ctypes.c_void_p), _PSZ, _PSZ]),

@@ -59,19 +59,52 @@ def rotated_band(world: int, device: int, compositor: int) -> int:
 
 
 def rotate_own_rows(height: int, pct: int | None = None) -> int:
-    """Rows of the compositor's own band (band 0) under the rotated all-to-all over two devices
-    (csrc/engine.cpp RotateOwnRows): ``pct`` per cent of the frame (env SRT_ROTATE_OWN, default 80),
+    """Rows of the compositor's own band (band 0) under the rotated all-to-all over two devices without
+    a measured link (csrc/engine.cpp RotateOwnRows): ``pct`` per cent of the frame (env SRT_ROTATE_OWN,
+    an integer in 1..99 -- anything else raises ValueError, as the library refuses it --, default 80),
     rounded to whole 16-row tile rows, kept inside [1, H - 1]; the other band takes the rest."""
     import os
 
     if pct is None:
         v = os.environ.get("SRT_ROTATE_OWN", "")
-        pct = int(v) if v.strip() else 80
+        if v == "":
+            pct = 80
+        elif not v.lstrip("+-").isdigit() or not 1 <= int(v) <= 99 or v != v.strip():
+            raise ValueError(f"SRT_ROTATE_OWN must be an integer per cent in 1..99, got {v!r}")
+        else:
+            pct = int(v)
     pct = max(1, min(99, pct))
     rows = (height * pct + 50) // 100
     if height > 2 * TILE_ROWS:
         rows = (rows + TILE_ROWS // 2) // TILE_ROWS * TILE_ROWS
     return max(1, min(rows, height - 1 if height > 1 else 1))
+
+
+def rotate_split_for_link(height: int, width: int, link_gbs: float, frame_us: float,
+                          bytes_per_pixel: float) -> int:
+    """The two-device split an engine derives from its measured link (csrc/engine.cpp
+    RotateSplitForLink): the smallest own band -- whole tile rows, at least half the frame -- whose
+    link time per frame of the job, (H - r) W b / 2 / rate, stays within 80 % of the GPUs' time per
+    frame of the job, frame_us (0.553 + 0.25 (H - r) / H) (the rank simulation's P = 2 times over the
+    own share); the largest own band (one tile row sent) when none does."""
+    t = TILE_ROWS
+    if height < 2:
+        return 1
+    tiled = height > 2 * t
+    hi = (height - 1) // t * t if tiled else height - 1
+    if not (link_gbs > 0 and frame_us > 0 and bytes_per_pixel > 0):
+        return hi
+    r = (height + 1) // 2
+    if tiled:
+        r = (r + t - 1) // t * t
+    while r <= hi:
+        sent = height - r
+        link_us = sent * width * bytes_per_pixel / 2.0 / (link_gbs * 1e3)
+        gpu_us = frame_us * (0.553 + 0.25 * sent / height)
+        if link_us <= 0.8 * gpu_us:
+            return min(r, hi)
+        r += t if tiled else 1
+    return hi
 
 
 def rotated_range(height: int, world: int, band: int, first_rows: int = 0) -> tuple[int, int]:

@@ -3,6 +3,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cerrno>
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
@@ -68,14 +69,76 @@ std::size_t ShareAuto(std::size_t height, std::size_t world) {
 // assumed 64 GB/s against 11 us of GPU time (rank simulation) -- link-bound below one GPU; a fifth
 // (216 of 1080 rows) cuts that to 7.2 us (GPU-bound down to ~45 GB/s) and the compositor's deferred
 // shading with it.
-std::size_t RotateOwnRows(std::size_t height) {
+long RotateOwnPercent() {
     const char* v = std::getenv("SRT_ROTATE_OWN");
-    long pct = v == nullptr || *v == '\0' ? 80 : std::strtol(v, nullptr, 10);
-    pct = std::max(1L, std::min(99L, pct));
+    if (v == nullptr || *v == '\0') {
+        return 0;
+    }
+    char* end = nullptr;
+    errno = 0;
+    const long pct = std::strtol(v, &end, 10);
+    if (errno != 0 || end == v || *end != '\0' || pct < 1 || pct > 99 || (*v != '+' && (*v < '0' || *v > '9'))) {
+        throw std::runtime_error(std::string("SRT_ROTATE_OWN must be an integer per cent in 1..99, got '") + v + "'");
+    }
+    return pct;
+}
+
+std::size_t RotateOwnRowsAt(std::size_t height, long pct) {
     const std::size_t t = static_cast<std::size_t>(kCullTileRows);
     std::size_t rows = (height * static_cast<std::size_t>(pct) + 50) / 100;
     rows = height > 2 * t ? (rows + t / 2) / t * t : rows;
     return std::max<std::size_t>(1, std::min(rows, height > 1 ? height - 1 : 1));
+}
+
+std::size_t RotateOwnRows(std::size_t height) {
+    const long pct = RotateOwnPercent();
+    return RotateOwnRowsAt(height, pct == 0 ? 80 : pct);
+}
+
+// The two-device split from a measured link. Per frame of the job, each
+// direction of the one link carries the sent band of every second frame: (H - r) W b / 2 bytes at
+// `link_gbs`; the GPUs spend frame_us (0.553 + 0.25 (H - r) / H) per frame of the job -- the rank
+// simulation's P = 2 times over the own share r / H (profiles/r05/rank_sim/p2_own_split.txt: 11.49 /
+// 10.36 / 10.22 / 10.12 us at 50 / 75 / 80 / 85 %, one GPU 16.96 us), the deferred shading of the sent
+// rows being the part that does not halve. The smallest own band (the most even tiling) whose link
+// time stays within 80 % of that GPU time, so the link is not the bound; the largest own band (at most
+// one tile row sent) when no split reaches it.
+std::size_t RotateSplitForLink(std::size_t height, std::size_t width, double link_gbs, double frame_us,
+                               double bytes_per_pixel) {
+    const std::size_t t = static_cast<std::size_t>(kCullTileRows);
+    if (height < 2) {
+        return 1;
+    }
+    const std::size_t hi = height > 2 * t ? (height - 1) / t * t : height - 1;  // whole tile rows, one row at least sent
+    if (!(link_gbs > 0.0) || !(frame_us > 0.0) || !(bytes_per_pixel > 0.0)) {
+        return hi;
+    }
+    const double H = static_cast<double>(height), W = static_cast<double>(width);
+    std::size_t r = (height + 1) / 2;
+    r = height > 2 * t ? (r + t - 1) / t * t : r;
+    for (; r <= hi; r += height > 2 * t ? t : 1) {
+        const double sent = H - static_cast<double>(r);
+        const double link_us = sent * W * bytes_per_pixel / 2.0 / (link_gbs * 1e3);
+        const double gpu_us = frame_us * (0.553 + 0.25 * sent / H);
+        if (link_us <= 0.8 * gpu_us) {
+            return std::min(r, hi);
+        }
+    }
+    return hi;
+}
+
+BandSplit EngineSplit(std::size_t height, std::size_t world, bool bands, bool interleaved, bool rotate,
+                      std::size_t share, std::size_t own_rows) {
+    BandSplit s = BandSplit::Make(height, bands ? (share != 0 ? share + world - 1 : world) : 1, interleaved);
+    s.first_sent = share;
+    if (bands && rotate && world == 2 && !interleaved) {
+        // Two devices: band 0 (the compositor's own: BandOf(c, c) = 0) takes own_rows of the frame. Per
+        // pair of frames each device still traces one band 0 and one band 1 (one frame's work), but only
+        // band 1 crosses the single link and waits for the deferred shading.
+        s.first_rows = own_rows != 0 ? std::min(own_rows, height > 1 ? height - 1 : 1) : RotateOwnRows(height);
+        s.first_sent = 1;
+    }
+    return s;
 }
 
 // Band split and exchange plan (pure index math; shared with the host self-test).
@@ -413,6 +476,7 @@ struct FrameEngine::Device {
     // Exchange timing of the current run (pairs of timing events around each batch's group on
     // `comm`), summarised when the run ends (FrameEngine::exchange_stats).
     std::vector<hipEvent_t> xev;
+    std::vector<char> xpend;  // per event: [2 slot] = the pair holds a group not yet added
     std::size_t xn = 0;
     double x_ms = 0.0, x_bytes = 0.0;
     std::size_t x_groups = 0;
@@ -439,6 +503,7 @@ FrameEngine::FrameEngine(const Scene& scene, const std::vector<int>& devices, st
             m_comms = CommInitAll(devices);
             m_comms_made = true;
         }
+        SettleSplit();
         AllocateQueues();
         m_pool = std::make_unique<Pool>(m_dev.size(), m_ctl.get(), CommTimeoutSeconds());
     } catch (...) {
@@ -467,6 +532,7 @@ FrameEngine::FrameEngine(const Scene& scene, int device, int rank, int world, co
             m_comms.push_back(CommInitRank(device, world, unique_id, rank));
             m_comms_made = true;
         }
+        SettleSplit();
         AllocateQueues();
         m_pool = std::make_unique<Pool>(1, m_ctl.get(), CommTimeoutSeconds());
     } catch (...) {
@@ -567,17 +633,6 @@ void FrameEngine::Init(const Scene& scene, const std::vector<int>& devices) {
         }
         m_rotate = m_exchange && m_world > 1;  // one device: its band is the frame, nothing to rotate
     }
-    // kShare: the frame's tile rows in cycles of k + P - 1 "classes" (the compositor's k, then one
-    // per sender); the ids buffers hold one class.
-    m_split = BandSplit::Make(m_height, m_bands ? (m_share != 0 ? m_share + m_world - 1 : m_world) : 1, m_opt.interleaved);
-    m_split.first_sent = m_share;
-    if (m_rotate && m_world == 2) {
-        // Two devices: band 0 (the compositor's own: BandOf(c, c) = 0) takes RotateOwnRows of the frame.
-        // Per pair of frames each device still traces one band 0 and one band 1 (one frame's work), but
-        // only band 1 crosses the single link and waits for the deferred shading.
-        m_split.first_rows = RotateOwnRows(m_height);
-        m_split.first_sent = 1;
-    }
     m_plan.bands = m_bands ? m_world : 1;
     m_plan.batch = m_opt.batch;
     m_plan.exchange = m_opt.exchange;
@@ -588,13 +643,41 @@ void FrameEngine::Init(const Scene& scene, const std::vector<int>& devices) {
         const char* v = std::getenv("SRT_EXCHANGE_IDS");
         const bool force32 = v != nullptr && std::strcmp(v, "32") == 0;
         m_id_planes = m_exchange && m_opt.variant == kTraceCull && !force32 ? IdPlanes(m_n) : -1;
-        const std::size_t rows = m_split.BufferRows();
-        m_band_id_bytes = m_id_planes >= 0 ? PackedIdLayout(m_id_planes, rows, m_width).bytes : rows * m_width * sizeof(int);
     }
     for (std::size_t i = 0; i < devices.size(); ++i) {
         auto d = std::make_unique<Device>();
         d->device = devices[i];
         d->band = m_rank0 + i;
+        m_dev.push_back(std::move(d));
+    }
+    // The two-device split of rotated bands: the option, else env SRT_ROTATE_OWN, else (RCCL between
+    // distinct devices) derived from the link measured once the communicators exist (SplitFromLink),
+    // else the 80 % default.
+    if (m_rotate && m_world == 2) {
+        if (m_opt.own_rows != 0) {
+            m_split_source = kSplitOption;
+        } else if (RotateOwnPercent() != 0) {
+            m_opt.own_rows = RotateOwnRows(m_height);
+            m_split_source = kSplitEnv;
+        } else {
+            m_split_source = kSplitDefault;
+        }
+    }
+    Layout(m_opt.own_rows);
+}
+
+// The band split, the id buffers' size and every device's roles for two-device own rows `own_rows`
+// (0: the default; EngineSplit).
+void FrameEngine::Layout(std::size_t own_rows) {
+    // kShare: the frame's tile rows in cycles of k + P - 1 "classes" (the compositor's k, then one
+    // per sender); the ids buffers hold one class.
+    m_split = EngineSplit(m_height, m_world, m_bands, m_opt.interleaved, m_rotate, m_share, own_rows);
+    {
+        const std::size_t rows = m_split.BufferRows();
+        m_band_id_bytes = m_id_planes >= 0 ? PackedIdLayout(m_id_planes, rows, m_width).bytes : rows * m_width * sizeof(int);
+    }
+    for (auto& d : m_dev) {
+        d->roles.clear();
         if (m_share != 0) {
             const std::size_t classes = m_split.bands;
             Role own;
@@ -623,16 +706,32 @@ void FrameEngine::Init(const Scene& scene, const std::vector<int>& devices) {
             r.pattern = m_split.Interleave();
             d->roles.push_back(r);
         }
-        const Role& measured = d->roles[m_share != 0 ? 1 : m_rotate ? d->band : 0];
-        d->row_begin = measured.row_begin;
-        d->rows = measured.rows;
         std::size_t at = 0;
         for (Role& r : d->roles) {
             r.input = at;
             at += r.rows;
         }
-        m_dev.push_back(std::move(d));
     }
+    for (std::size_t local = 0; local < m_dev.size(); ++local) {
+        const Role& measured = m_dev[local]->roles[SenderRole(local)];
+        m_dev[local]->row_begin = measured.row_begin;
+        m_dev[local]->rows = measured.rows;
+    }
+}
+
+// A role whose ids device `local` sends (they fit one band buffer of BufferRows rows): kShare its first
+// sender class, rotate the band it traces for the next device's frames -- (p + c) % P for c = p + 1,
+// never the compositor's own band 2c % P, which over two devices is larger than the buffer --, else its
+// band. MeasureStages and PrimeSimulation trace it into a send buffer (they traced band
+// d.band, the 864-row own band of device 0 at P = 2, into 216-row slots).
+std::size_t FrameEngine::SenderRole(std::size_t local) const {
+    if (m_share != 0) {
+        return 1;
+    }
+    if (m_rotate) {
+        return RoleOf(local, (m_dev[local]->band + 1) % m_world);
+    }
+    return 0;
 }
 
 std::size_t FrameEngine::RoleOf(std::size_t local, std::size_t c) const {
@@ -678,6 +777,220 @@ void FrameEngine::AllocateQueues() {
             q.rgba = DeviceAlloc<float>(q.rgba_frames * frame_floats4, "hipMalloc(frames)");
         }
     }
+}
+
+// Rank mode (fewer local devices than the job has): the element-wise maximum of `v` over every rank
+// (one ncclAllReduce on this process's communicator, waits polled with a deadline); otherwise `v`.
+std::vector<double> FrameEngine::MaxOverRanks(const std::vector<double>& v) {
+    if (m_dev.size() >= m_world || m_comms.empty() || v.empty()) {
+        return v;
+    }
+    Device& d = *m_dev[0];
+    DeviceGuard guard(d.device);
+    double* buf = DeviceAlloc<double>(v.size(), "hipMalloc(allreduce)");
+    hipStream_t st = nullptr;
+    hipEvent_t done = nullptr;
+    std::vector<double> out(v.size());
+    try {
+        HipCheck(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate(allreduce)");
+        HipCheck(hipEventCreateWithFlags(&done, hipEventDisableTiming), "hipEventCreate(allreduce)");
+        HipCheck(hipMemcpyAsync(buf, v.data(), v.size() * sizeof(double), hipMemcpyHostToDevice, st),
+                 "hipMemcpyAsync(allreduce)");
+        NcclCheck(ncclAllReduce(buf, buf, v.size(), ncclDouble, ncclMax, static_cast<ncclComm_t>(m_comms[0]), st),
+                  "ncclAllReduce(engine setup)", true);
+        CommSettle(&m_comms[0], 1, "allreduce enqueue (engine setup)", m_ctl.get());
+        HipCheck(hipEventRecord(done, st), "hipEventRecord(allreduce)");
+        CommWaitEvent(done, &m_comms[0], 1, "allreduce (engine setup)", m_ctl.get());
+        HipCheck(hipMemcpy(out.data(), buf, v.size() * sizeof(double), hipMemcpyDeviceToHost), "hipMemcpy(allreduce)");
+    } catch (...) {
+        (void)hipFree(buf);
+        if (done != nullptr) (void)hipEventDestroy(done);
+        if (st != nullptr) (void)hipStreamDestroy(st);
+        throw;
+    }
+    (void)hipFree(buf);
+    (void)hipEventDestroy(done);
+    (void)hipStreamDestroy(st);
+    return out;
+}
+
+// The link: every local device sends kLinkProbeBytes to the next device of the job and receives as
+// much from the previous one (two devices: both directions of their link at once, as the exchange
+// does; one device with the self-exchange: to itself), in one group; 2 untimed and kLinkProbeReps
+// timed groups, HIP events on each device's probe stream. GB/s per direction of the slowest device,
+// over every rank.
+double FrameEngine::MeasureLink() {
+    constexpr std::size_t kLinkProbeBytes = std::size_t{32} << 20;
+    constexpr int kLinkProbeReps = 5;
+    const std::size_t n = m_dev.size();
+    std::vector<unsigned char*> sbuf(n, nullptr), rbuf(n, nullptr);
+    std::vector<hipStream_t> st(n, nullptr);
+    std::vector<hipEvent_t> ev(2 * n, nullptr);
+    double worst_ms = 0.0;
+    auto release = [&] {
+        for (std::size_t i = 0; i < n; ++i) {
+            (void)hipSetDevice(m_dev[i]->device);
+            (void)hipFree(sbuf[i]);
+            (void)hipFree(rbuf[i]);
+            for (int k = 0; k < 2; ++k) {
+                if (ev[2 * i + k] != nullptr) (void)hipEventDestroy(ev[2 * i + k]);
+            }
+            if (st[i] != nullptr) (void)hipStreamDestroy(st[i]);
+        }
+    };
+    try {
+        for (std::size_t i = 0; i < n; ++i) {
+            DeviceGuard guard(m_dev[i]->device);
+            sbuf[i] = DeviceAlloc<unsigned char>(kLinkProbeBytes, "hipMalloc(link probe)");
+            rbuf[i] = DeviceAlloc<unsigned char>(kLinkProbeBytes, "hipMalloc(link probe)");
+            HipCheck(hipMemset(sbuf[i], 0x5A, kLinkProbeBytes), "hipMemset(link probe)");
+            HipCheck(hipStreamCreateWithFlags(&st[i], hipStreamNonBlocking), "hipStreamCreate(link probe)");
+            HipCheck(hipEventCreate(&ev[2 * i]), "hipEventCreate(link probe)");
+            HipCheck(hipEventCreate(&ev[2 * i + 1]), "hipEventCreate(link probe)");
+        }
+        const auto group = [&] {
+            NcclCheck(ncclGroupStart(), "ncclGroupStart(link probe)");
+            ncclResult_t first = ncclSuccess;
+            for (std::size_t i = 0; i < n; ++i) {
+                const std::size_t self = m_dev[i]->band;
+                const int to = static_cast<int>((self + 1) % m_world), from = static_cast<int>((self + m_world - 1) % m_world);
+                auto comm = static_cast<ncclComm_t>(m_comms[i]);
+                const ncclResult_t a = ncclSend(sbuf[i], kLinkProbeBytes, ncclUint8, to, comm, st[i]);
+                const ncclResult_t b = ncclRecv(rbuf[i], kLinkProbeBytes, ncclUint8, from, comm, st[i]);
+                for (const ncclResult_t r : {a, b}) {
+                    if (r != ncclSuccess && r != ncclInProgress && first == ncclSuccess) {
+                        first = r;
+                    }
+                }
+            }
+            const ncclResult_t end = ncclGroupEnd();
+            NcclCheck(first, "ncclSend / ncclRecv (link probe)");
+            NcclCheck(end, "ncclGroupEnd (link probe)", true);
+            CommSettle(m_comms.data(), m_comms.size(), "link probe enqueue", m_ctl.get());
+        };
+        for (int r = 0; r < 2; ++r) {
+            group();
+        }
+        for (std::size_t i = 0; i < n; ++i) {
+            DeviceGuard guard(m_dev[i]->device);
+            HipCheck(hipEventRecord(ev[2 * i], st[i]), "hipEventRecord(link probe)");
+        }
+        for (int r = 0; r < kLinkProbeReps; ++r) {
+            group();
+        }
+        for (std::size_t i = 0; i < n; ++i) {
+            DeviceGuard guard(m_dev[i]->device);
+            HipCheck(hipEventRecord(ev[2 * i + 1], st[i]), "hipEventRecord(link probe)");
+        }
+        for (std::size_t i = 0; i < n; ++i) {
+            DeviceGuard guard(m_dev[i]->device);
+            CommWaitEvent(ev[2 * i + 1], m_comms.data(), m_comms.size(), "link probe", m_ctl.get());
+            float ms = 0.f;
+            HipCheck(hipEventElapsedTime(&ms, ev[2 * i], ev[2 * i + 1]), "hipEventElapsedTime(link probe)");
+            worst_ms = std::max(worst_ms, static_cast<double>(ms) / kLinkProbeReps);
+        }
+    } catch (...) {
+        release();
+        throw;
+    }
+    release();
+    worst_ms = MaxOverRanks({worst_ms})[0];
+    return worst_ms > 0.0 ? static_cast<double>(kLinkProbeBytes) / (worst_ms * 1e-3) / 1e9 : 0.0;
+}
+
+// One GPU's time per whole frame of this scene and resolution: 8-frame traces (uniform 0.5 offsets,
+// RGBA, the N = 1 launch shape) on a scratch scene of each local device, one untimed and 3 timed
+// launches; microseconds per frame of the slowest device, over every rank.
+double FrameEngine::MeasureFrameUs() {
+    constexpr std::size_t kFrames = kMaxBatch;
+    constexpr int kReps = 3;
+    double worst = 0.0;
+    for (auto& dp : m_dev) {
+        DeviceGuard guard(dp->device);
+        DeviceScene s(*m_scene, dp->device);
+        hipStream_t st = nullptr;
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        float* off = nullptr;
+        float* rgba = nullptr;
+        try {
+            HipCheck(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate(frame probe)");
+            HipCheck(hipEventCreate(&e0), "hipEventCreate(frame probe)");
+            HipCheck(hipEventCreate(&e1), "hipEventCreate(frame probe)");
+            off = DeviceAlloc<float>(FrameFloats(), "hipMalloc(frame probe offsets)");
+            rgba = DeviceAlloc<float>(kFrames * m_width * m_height * 4, "hipMalloc(frame probe frames)");
+            HipCheck(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(off), 0x3F000000, FrameFloats(), st),
+                     "hipMemsetD32Async(frame probe offsets)");  // 0.5f
+            s.Prepare(m_width, m_height, st);
+            std::vector<const float*> offs(kFrames, off);
+            std::vector<float*> outs(kFrames);
+            for (std::size_t j = 0; j < kFrames; ++j) {
+                outs[j] = rgba + j * m_width * m_height * 4;
+            }
+            const int variant = m_opt.variant;
+            s.TraceBatch(offs.data(), outs.data(), nullptr, kFrames, 0, m_height, variant, st, 1);
+            HipCheck(hipEventRecord(e0, st), "hipEventRecord(frame probe)");
+            for (int r = 0; r < kReps; ++r) {
+                s.TraceBatch(offs.data(), outs.data(), nullptr, kFrames, 0, m_height, variant, st, 1);
+            }
+            HipCheck(hipEventRecord(e1, st), "hipEventRecord(frame probe)");
+            CommWaitEvent(e1, nullptr, 0, "frame probe", m_ctl.get());
+            float ms = 0.f;
+            HipCheck(hipEventElapsedTime(&ms, e0, e1), "hipEventElapsedTime(frame probe)");
+            worst = std::max(worst, static_cast<double>(ms) * 1e3 / (kReps * kFrames));
+        } catch (...) {
+            (void)hipStreamSynchronize(st);
+            (void)hipFree(off);
+            (void)hipFree(rgba);
+            if (e0 != nullptr) (void)hipEventDestroy(e0);
+            if (e1 != nullptr) (void)hipEventDestroy(e1);
+            if (st != nullptr) (void)hipStreamDestroy(st);
+            throw;
+        }
+        (void)hipFree(off);
+        (void)hipFree(rgba);
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        (void)hipStreamDestroy(st);
+    }
+    return MaxOverRanks({worst})[0];
+}
+
+// Once the communicators exist (RCCL engines only): the link rate (reported; srtEngineSplit), the
+// two-device split derived from it when neither the option nor SRT_ROTATE_OWN chose one, and -- one
+// rank per process -- a check that every rank uses the same split (ranks reading different
+// environments would post mismatched send / receive sizes).
+void FrameEngine::SettleSplit() {
+    if (!m_comms_made) {
+        return;
+    }
+    m_link_gbs = MeasureLink();
+    if (m_rotate && m_world == 2 && m_split_source == kSplitDefault) {
+        m_frame_us = MeasureFrameUs();
+        const double bpp = static_cast<double>(m_band_id_bytes) / static_cast<double>(m_split.BufferRows() * m_width);
+        m_opt.own_rows = RotateSplitForLink(m_height, m_width, m_link_gbs, m_frame_us, bpp);
+        m_split_source = kSplitLink;
+        Layout(m_opt.own_rows);
+    }
+    if (m_rotate && m_world == 2) {
+        const double own = static_cast<double>(m_split.first_rows);
+        const std::vector<double> r = MaxOverRanks({own, -own});
+        if (r[0] != -r[1]) {
+            throw std::runtime_error("FrameEngine: the ranks chose different two-device splits (own band rows " +
+                                     std::to_string(static_cast<long>(-r[1])) + " .. " +
+                                     std::to_string(static_cast<long>(r[0])) +
+                                     "): set SRT_ROTATE_OWN alike on every rank, or leave it unset");
+        }
+    }
+}
+
+FrameEngine::SplitInfo FrameEngine::split_info() const {
+    SplitInfo s;
+    s.own_rows = m_rotate && m_world == 2 ? m_split.first_rows : 0;
+    s.buffer_rows = m_split.BufferRows();
+    s.link_gbs = m_link_gbs;
+    s.frame_us = m_frame_us;
+    s.source = m_split_source;
+    return s;
 }
 
 FrameEngine::~FrameEngine() { Release(); }
@@ -769,6 +1082,7 @@ void FrameEngine::Release() noexcept {
             (void)hipEventDestroy(e);
         }
         dp->xev.clear();
+        dp->xpend.clear();
         if (dp->comm != nullptr) {
             (void)hipStreamDestroy(dp->comm);
             dp->comm = nullptr;
@@ -868,7 +1182,7 @@ void FrameEngine::PrimeSimulation() {
         Device& d = *dp;
         DeviceGuard guard(d.device);
         const std::size_t local = static_cast<std::size_t>(&dp - &m_dev[0]);
-        const std::size_t ri = m_share != 0 ? 1 : m_rotate ? d.band : 0;
+        const std::size_t ri = SenderRole(local);
         const Role& role = d.roles[ri];
         for (Queue& q : d.queues) {
             if (q.send == nullptr || q.recv == nullptr || role.rows == 0) {
@@ -1105,17 +1419,37 @@ void FrameEngine::TraceRotated(std::size_t local, std::size_t b) {
     }
 }
 
-namespace {
-// The next pair of timing events of a device's exchange timing (grown on demand).
-hipEvent_t* ExchangeEvents(std::vector<hipEvent_t>& ev, std::size_t& n) {
-    while (ev.size() < 2 * (n + 1)) {
+// The next pair of timing events of device `local`'s exchange timing: a ring of 2 Q + 2 pairs (grown
+// on demand up to that), a pair still holding an earlier group's times first waited for (polled with
+// the comm deadline) and added to the run's total -- a bounded number of events however long the run
+// (one new pair per batch, kept until Release).
+hipEvent_t* FrameEngine::ExchangeEvents(std::size_t local) {
+    Device& d = *m_dev[local];
+    const std::size_t ring = 2 * m_opt.queues + 2, slot = d.xn % ring;
+    while (d.xev.size() < 2 * (slot + 1)) {
         hipEvent_t e = nullptr;
         HipCheck(hipEventCreate(&e), "hipEventCreate(exchange timing)");
-        ev.push_back(e);
+        d.xev.push_back(e);
+        d.xpend.push_back(0);
     }
-    return &ev[2 * n++];
+    if (d.xpend[2 * slot]) {
+        AddExchangeTime(local, slot);
+    }
+    d.xpend[2 * slot] = 1;
+    ++d.xn;
+    return &d.xev[2 * slot];
 }
-}  // namespace
+
+void FrameEngine::AddExchangeTime(std::size_t local, std::size_t slot) {
+    Device& d = *m_dev[local];
+    const std::size_t nc = m_comms.empty() ? 0 : 1;
+    CommWaitEvent(d.xev[2 * slot + 1], nc != 0 ? &m_comms[local] : nullptr, nc, "exchange timing", m_ctl.get());
+    float ms = 0.f;
+    HipCheck(hipEventElapsedTime(&ms, d.xev[2 * slot], d.xev[2 * slot + 1]), "hipEventElapsedTime(exchange)");
+    d.x_ms += static_cast<double>(ms);
+    ++d.x_groups;
+    d.xpend[2 * slot] = 0;
+}
 
 double FrameEngine::SentBytes(std::size_t local, std::size_t b) const {
     const std::size_t self = m_dev[local]->band;
@@ -1144,7 +1478,7 @@ void FrameEngine::ExchangePhase(std::size_t local, std::size_t b) {
     Queue& q = d.queues[b % m_opt.queues];
     const std::size_t self = d.band, n_self = m_plan.FramesFor(b, self);
     HipCheck(hipStreamWaitEvent(d.comm, q.traced, 0), "hipStreamWaitEvent(traced)");
-    hipEvent_t* xe = ExchangeEvents(d.xev, d.xn);
+    hipEvent_t* xe = ExchangeEvents(local);
     d.x_bytes += SentBytes(local, b);
     HipCheck(hipEventRecord(xe[0], d.comm), "hipEventRecord(exchange start)");
     {
@@ -1193,7 +1527,7 @@ void FrameEngine::CopyPhase(std::size_t local, std::size_t b) {
     Queue& q = d.queues[qi];
     const std::size_t self = d.band, n_self = m_plan.FramesFor(b, self);
     HipCheck(hipStreamWaitEvent(d.comm, q.traced, 0), "hipStreamWaitEvent(traced)");
-    hipEvent_t* xe = ExchangeEvents(d.xev, d.xn);
+    hipEvent_t* xe = ExchangeEvents(local);
     d.x_bytes += SentBytes(local, b);
     HipCheck(hipEventRecord(xe[0], d.comm), "hipEventRecord(exchange start)");
     if (n_self != 0) {
@@ -1261,6 +1595,7 @@ void FrameEngine::RunWorker(std::size_t local, std::size_t b0, std::size_t batch
     Device& d = *m_dev[local];
     DeviceGuard guard(d.device);
     d.xn = 0;
+    std::fill(d.xpend.begin(), d.xpend.end(), 0);  // a failed run's pairs: not this run's groups
     d.x_ms = d.x_bytes = 0.0;
     d.x_groups = 0;
     const std::size_t nc = m_comms.empty() ? 0 : 1;
@@ -1312,12 +1647,11 @@ void FrameEngine::RunWorker(std::size_t local, std::size_t b0, std::size_t batch
         CommWaitEvent(q.drained, comm, nc, "render (queue)", m_ctl.get());
     }
     CommWaitEvent(d.comm_drained, comm, nc, "render (exchange)", m_ctl.get());
-    for (std::size_t i = 0; i < d.xn; ++i) {  // every exchange of the run has completed (drained above)
-        float ms = 0.f;
-        HipCheck(hipEventElapsedTime(&ms, d.xev[2 * i], d.xev[2 * i + 1]), "hipEventElapsedTime(exchange)");
-        d.x_ms += static_cast<double>(ms);
+    for (std::size_t slot = 0; 2 * slot < d.xev.size(); ++slot) {  // the groups not added yet (drained above)
+        if (d.xpend[2 * slot]) {
+            AddExchangeTime(local, slot);
+        }
     }
-    d.x_groups = d.xn;
 }
 
 void FrameEngine::Barrier() {
@@ -1505,8 +1839,8 @@ DeviceScene::StageTimes FrameEngine::MeasureStages(std::size_t local, std::size_
                 ids[j] = Ids(q.send, j);
             }
             if (m_exchange) {
-                // the sender role (its ids fit the send buffer); rotate: the device's own-index band
-                const std::size_t ri = m_share != 0 ? 1 : m_rotate ? d.band : 0;
+                // a sender role: its ids fit the send buffer's band frames (SenderRole)
+                const std::size_t ri = SenderRole(local);
                 const Role& role = d.roles[ri];
                 for (std::size_t j = 0; j < frames; ++j) {
                     offs[j] = BandInput(local, i * frames + j, ri);

@@ -81,14 +81,26 @@ struct EngineOptions {
     bool rccl_self = false;
     // kShare: the compositor's tile rows per cycle (k above, a power of two; 0: ShareAuto).
     std::size_t share = 0;
+    // Rotated bands over two devices: rows of the compositor's own band 0 (0: env SRT_ROTATE_OWN per cent
+    // if set, else -- RCCL between distinct devices -- derived from the link measured at creation
+    // (RotateSplitForLink), else 80 % of the frame).
+    std::size_t own_rows = 0;
 };
 
 // kShare's default k for an H-row frame over P devices: the largest power of two <= 32 with
 // k + P - 1 <= the frame's tile rows (engine.cpp).
 std::size_t ShareAuto(std::size_t height, std::size_t world);
 
-// Rows of the compositor's own band under rotated all-to-all over two devices (engine.cpp).
+// Rows of the compositor's own band under rotated all-to-all over two devices without a measured
+// link: env SRT_ROTATE_OWN per cent (an integer in 1..99, else std::runtime_error), default 80, rounded
+// to tile rows (engine.cpp).
 std::size_t RotateOwnRows(std::size_t height);
+long RotateOwnPercent();  // env SRT_ROTATE_OWN, validated; 0 when unset
+// The two-device split for a link of `link_gbs` GB/s per direction, a one-GPU frame time of `frame_us`
+// and an exchange payload of `bytes_per_pixel`: the smallest own band (tile rows, >= H / 2) whose link
+// time stays within 80 % of the GPU time per frame of the job (engine.cpp).
+std::size_t RotateSplitForLink(std::size_t height, std::size_t width, double link_gbs, double frame_us,
+                               double bytes_per_pixel);
 
 // Row bands of an H-row frame over P devices (interleaved or contiguous), the layout every
 // exchange path and the shading kernel agree on.
@@ -107,6 +119,11 @@ struct BandSplit {
     std::size_t Interleave() const { return interleaved && bands > 1 ? bands : 1; }
     std::size_t FrameRow(std::size_t band, std::size_t local) const;
 };
+
+// The engine's band split for P = `world` devices (bands: P bands, kShare share + P - 1 classes; rotated
+// over two devices band 0 takes own_rows, 0: RotateOwnRows) -- shared with the host self-test.
+BandSplit EngineSplit(std::size_t height, std::size_t world, bool bands, bool interleaved, bool rotate,
+                      std::size_t share, std::size_t own_rows);
 
 // Which device composites frame f of batch b, and that frame's slot among the device's frames.
 struct ExchangePlan {
@@ -198,6 +215,16 @@ public:
     };
     ExchangeStats exchange_stats(std::size_t local) const;
     int id_planes() const { return m_id_planes; }  // exchange payload: packed ids' bit planes, -1 int32
+    // The two-device split and where it came from (srtEngineSplit): own band rows (0: no two-device
+    // rotated split), the band buffers' rows, the link measured at creation (GB/s per direction, 0: not
+    // measured -- no RCCL), the one-GPU frame time measured for the split (us, 0: not measured).
+    enum SplitSource { kSplitNone = 0, kSplitOption = 1, kSplitEnv = 2, kSplitLink = 3, kSplitDefault = 4 };
+    struct SplitInfo {
+        std::size_t own_rows = 0, buffer_rows = 0;
+        double link_gbs = 0.0, frame_us = 0.0;
+        int source = kSplitNone;
+    };
+    SplitInfo split_info() const;
 
 private:
     struct Queue;
@@ -226,6 +253,8 @@ private:
     void ExchangePhase(std::size_t local, std::size_t b);  // RCCL: inside a group
     double SentBytes(std::size_t local, std::size_t b) const;  // ids device `local` sends for batch b
     void CopyPhase(std::size_t local, std::size_t b);      // device-copy exchange
+    hipEvent_t* ExchangeEvents(std::size_t local);          // the next timing pair (a bounded ring)
+    void AddExchangeTime(std::size_t local, std::size_t slot);  // wait for a pair, add its time
     void ShadePhase(std::size_t local, std::size_t b);
     void RunWorker(std::size_t local, std::size_t b0, std::size_t batches);
     void Barrier();
@@ -233,6 +262,14 @@ private:
     const float* FullInput(std::size_t local, std::size_t k) const;
     std::size_t FrameFloats() const { return m_width * m_height * 2; }
     void PrimeSimulation();  // simulate: receive buffers hold real ids (the sender role's band)
+    void Layout(std::size_t own_rows);  // m_split, m_band_id_bytes and every device's roles
+    std::size_t SenderRole(std::size_t local) const;  // a role whose ids fit one band buffer
+    void SettleSplit();      // after the communicators: link rate, derived / agreed two-device split
+    double MeasureLink();    // GB/s per direction (RCCL send / receive groups), over every rank
+    double MeasureFrameUs();  // one GPU's us per whole frame (8-frame traces), over every rank
+    std::vector<double> MaxOverRanks(const std::vector<double>& v);  // rank mode: ncclAllReduce(max)
+    int m_split_source = kSplitNone;
+    double m_link_gbs = 0.0, m_frame_us = 0.0;
 
     EngineOptions m_opt;
     std::size_t m_width = 0, m_height = 0, m_world = 1, m_rank0 = 0;  // m_rank0: global index of local 0

@@ -384,6 +384,7 @@ srt::EngineOptions EngineOptionsFrom(const srt_engine_options* o) {
         }
         opt.rccl_self = (o->flags & SRT_ENGINE_RCCL_SELF) != 0;
         opt.share = o->share;
+        opt.own_rows = o->own_rows;
     }
     return opt;
 }
@@ -560,7 +561,39 @@ ML_API_ENTRY size_t srtShareAuto(size_t height, size_t devices) {
 }
 
 ML_API_ENTRY size_t srtRotateOwnRows(size_t height) {
-    return srt::RotateOwnRows(height);
+    size_t rows = 0;
+    (void)Guarded([&] { rows = srt::RotateOwnRows(height); });  // 0: SRT_ROTATE_OWN invalid (srtGetLastError)
+    return rows;
+}
+
+ML_API_ENTRY size_t srtRotateSplitForLink(size_t height, size_t width, double link_gbs, double frame_us,
+                                          double bytes_per_pixel) {
+    return srt::RotateSplitForLink(height, width, link_gbs, frame_us, bytes_per_pixel);
+}
+
+ML_API_ENTRY int srtEngineSplit(srt_engine engine, size_t* own_rows, size_t* buffer_rows, double* link_gbs,
+                                double* frame_us, int* source) {
+    return Guarded([&] {
+        if (engine == nullptr) {
+            throw std::runtime_error("Bad engine handle");
+        }
+        const srt::FrameEngine::SplitInfo s = FromHandle(engine)->split_info();
+        if (own_rows != nullptr) {
+            *own_rows = s.own_rows;
+        }
+        if (buffer_rows != nullptr) {
+            *buffer_rows = s.buffer_rows;
+        }
+        if (link_gbs != nullptr) {
+            *link_gbs = s.link_gbs;
+        }
+        if (frame_us != nullptr) {
+            *frame_us = s.frame_us;
+        }
+        if (source != nullptr) {
+            *source = s.source;
+        }
+    });
 }
 
 ML_API_ENTRY int srtEngineInfo(srt_engine engine, size_t* devices, size_t* local_devices, size_t* band_rows,
@@ -632,10 +665,12 @@ int ExchangeHost(const int* const* band_ids, size_t bands, size_t width, size_t 
                 throw std::runtime_error("share must be a power of two, 1..64");
             }
         }
-        // (the engine's layout: kShare splits the frame into share + P - 1 interleaved classes)
-        srt::BandSplit split = srt::BandSplit::Make(height, exchange == SRT_EXCHANGE_SHARE ? share + bands - 1 : bands,
-                                                    rows == SRT_ROWS_INTERLEAVED);
-        split.first_sent = exchange == SRT_EXCHANGE_SHARE ? share : 0;
+        // The engine's layout (EngineSplit: kShare splits the frame into share + P - 1 interleaved classes;
+        // rotated over two devices band 0 takes the split an engine without a measured link uses,
+        // RotateOwnRows -- env SRT_ROTATE_OWN, default 80 %)
+        const srt::BandSplit split =
+            srt::EngineSplit(height, bands, true, rows == SRT_ROWS_INTERLEAVED, rows == SRT_ROWS_ROTATED,
+                             exchange == SRT_EXCHANGE_SHARE ? share : 0, 0);
         srt::ExchangePlan plan;
         plan.bands = bands;
         plan.batch = batch;

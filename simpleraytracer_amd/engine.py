@@ -32,10 +32,14 @@ def _check(rc: int):
         raise SrtError(_native.last_error())
 
 
-def _options(variant, queues, batch, rows, exchange, split, simulate=False, launch=0, rccl_self=False, share=0):
+def _options(variant, queues, batch, rows, exchange, split, simulate=False, launch=0, rccl_self=False, share=0,
+             own_rows=0):
     return EngineOptions(ctypes.sizeof(EngineOptions), TRACE_VARIANTS[variant], queues, batch, ROWS[rows],
                          EXCHANGES[exchange], SPLITS[split],
-                         1 if simulate else 0, launch, SRT_ENGINE_RCCL_SELF if rccl_self else 0, share)
+                         1 if simulate else 0, launch, SRT_ENGINE_RCCL_SELF if rccl_self else 0, share, own_rows)
+
+
+SPLIT_SOURCES = {0: "none", 1: "option", 2: "env", 3: "link", 4: "default"}
 
 
 def unique_id() -> bytes:
@@ -50,19 +54,22 @@ class FrameEngine:
 
     def __init__(self, path: str, width: int, height: int, devices=(0,), variant: str = "cull", queues: int = 2,
                  batch: int = 16, rows: str = "interleaved", exchange: str = "alltoall", split: str = "bands",
-                 launch: int = 0, rccl_self: bool = False, share: int = 0, _handle=None):
+                 launch: int = 0, rccl_self: bool = False, share: int = 0, own_rows: int = 0, _handle=None):
         """rccl_self (one device, tests): the bands path with the frame's ids sent to itself over a
         one-rank RCCL communicator -- the real exchange, its waits and its abort path.
         exchange="share": the compositor traces `share` (a power of two; 0: srtShareAuto, 32 at 1080p)
-        of every share + P - 1 tile rows itself."""
+        of every share + P - 1 tile rows itself. own_rows (rotated rows over two devices): rows of the
+        compositor's own band (0: env SRT_ROTATE_OWN, else the split derived from the measured link, else
+        80 %; split())."""
         self._lib = _native.lib()
         self.width, self.height, self.batch = width, height, batch
         self.options = {"variant": variant, "queues": queues, "batch": batch, "rows": rows, "exchange": exchange,
-                        "split": split, "launch": launch, "rccl_self": rccl_self, "share": share}
+                        "split": split, "launch": launch, "rccl_self": rccl_self, "share": share,
+                        "own_rows": own_rows}
         if _handle is None:
             devs = (ctypes.c_int * len(devices))(*devices)
             opt = _options(variant, queues, batch, rows, exchange, split, launch=launch, rccl_self=rccl_self,
-                           share=share)
+                           share=share, own_rows=own_rows)
             _handle = self._lib.srtEngineCreate(os.fsencode(path), devs, len(devices), width, height, ctypes.byref(opt))
         if not _handle:
             raise SrtError(_native.last_error())
@@ -74,17 +81,17 @@ class FrameEngine:
     def rank(cls, path: str, width: int, height: int, device: int, rank: int, world: int, uid: bytes | None,
              variant: str = "cull", queues: int = 2, batch: int = 16, rows: str = "interleaved",
              exchange: str = "alltoall", split: str = "bands", simulate: bool = False, launch: int = 0,
-             share: int = 0):
+             share: int = 0, own_rows: int = 0):
         """This process's rank of a `world`-rank job on `device`; every rank calls it concurrently.
         simulate=True (measurement): no peers, no unique id -- the rank's stream without the exchange."""
         lib = _native.lib()
-        opt = _options(variant, queues, batch, rows, exchange, split, simulate, launch, share=share)
+        opt = _options(variant, queues, batch, rows, exchange, split, simulate, launch, share=share, own_rows=own_rows)
         idbuf = ctypes.create_string_buffer(uid, 128) if uid is not None else None
         h = lib.srtEngineCreateRank(os.fsencode(path), device, rank, world, idbuf, width, height, ctypes.byref(opt))
         if not h:
             raise SrtError(_native.last_error())
         return cls(path, width, height, variant=variant, queues=queues, batch=batch, rows=rows, exchange=exchange,
-                   split=split, launch=launch, share=share, _handle=h)
+                   split=split, launch=launch, share=share, own_rows=own_rows, _handle=h)
 
     def set_inputs(self, offsets):
         """offsets: (count, H, W, 2) or (H, W, 2) float32 host array (numpy or CPU tensor)."""
@@ -133,6 +140,17 @@ class FrameEngine:
                                        ctypes.byref(bufr), ctypes.byref(rccl), ctypes.byref(xb)))
         return {"devices": d.value, "local_devices": ld.value, "band_rows": br.value, "buffer_rows": bufr.value,
                 "rccl": bool(rccl.value), "exchange_bytes_per_frame": xb.value}
+
+    def split(self):
+        """The two-device split (srtEngineSplit): own band rows (0 unless rotated rows over two devices),
+        band buffer rows, the link measured at creation (GB/s per direction; 0 without RCCL), the one-GPU
+        frame time measured for the split (us; 0 when not derived) and where the split came from."""
+        own, bufr = ctypes.c_size_t(), ctypes.c_size_t()
+        gbs, fus, src = ctypes.c_double(), ctypes.c_double(), ctypes.c_int()
+        _check(self._lib.srtEngineSplit(self.handle, ctypes.byref(own), ctypes.byref(bufr), ctypes.byref(gbs),
+                                        ctypes.byref(fus), ctypes.byref(src)))
+        return {"own_rows": own.value, "buffer_rows": bufr.value, "link_gbs": round(gbs.value, 3),
+                "frame_us": round(fus.value, 3), "source": SPLIT_SOURCES.get(src.value, str(src.value))}
 
     def exchange_stats(self, local: int = 0):
         """The last run's exchange on local device `local` (srtEngineExchangeStats): groups timed, mean ms

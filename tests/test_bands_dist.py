@@ -218,7 +218,7 @@ def _data_plane_worker(rank, world, port, out_dir, scene, exchange, rows_mode, s
     import torch.distributed as dist
 
     from oracle.srt_oracle import OracleScene
-    from simpleraytracer_amd.bands import ExchangePlan, share_auto, traced_rows
+    from simpleraytracer_amd.bands import ExchangePlan, rotate_own_rows, share_auto, traced_rows
     from simpleraytracer_amd.engine import exchange_host
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -228,14 +228,21 @@ def _data_plane_worker(rank, world, port, out_dir, scene, exchange, rows_mode, s
     plan = ExchangePlan(world, F, exchange, rows_mode)
     oracle = OracleScene(scene)
     offs = [np.random.default_rng(900 + f).random((h, w, 2), dtype=np.float32) for f in range(F)]
-    rows = {(d, c): traced_rows(h, world, exchange, rows_mode, d, c, k) for d in range(world) for c in range(world)}
-    senders = [(d, c) for d in range(world) for c in range(world) if not (exchange == "share" and d == c)]
+    # rotated over two devices: the compositor's band 0 takes the engine's default split (4/5 of the frame,
+    # srtExchangeHost's layout; ADVICE r05: this test used to trace even halves there)
+    first = rotate_own_rows(h) if rows_mode == "rotated" and world == 2 else 0
+    rows = {(d, c): traced_rows(h, world, exchange, rows_mode, d, c, k, first) for d in range(world)
+            for c in range(world)}
+    # the compositor's own rows travel (to itself) only where its band fits the buffers: not under share, nor
+    # rotated over two devices (band 0 is larger than the band buffer, first_sent = 1)
+    own_sent = exchange != "share" and not first
+    senders = [(d, c) for d in range(world) for c in range(world) if d != c or own_sent]
     brows = max(1, max(len(rows[d, c]) for d, c in senders))
     # this rank's traces of the batch, frame-major (the engine's trace phase; its own frames too)
     mine = np.full((F, brows, w), -7, np.int32)
     for f in range(F):
         c = plan.compositor(f)
-        if not (exchange == "share" and c == rank):
+        if c != rank or own_sent:
             r = rows[rank, c]
             mine[f, :len(r)] = _rows_ids(oracle, w, h, offs[f], r)
     send = np.full((world * plan.max_frames(), brows, w), -7, np.int32)

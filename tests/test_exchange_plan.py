@@ -62,6 +62,9 @@ def traced_band(rows, exchange, p, b, d, f):
 def test_exchange_layout_reassembles_every_frame(rows, exchange, p, h, frames, b):
     if rows == "rotated" and exchange != "alltoall":
         pytest.skip("rotated bands are an all-to-all layout")
+    if rows == "rotated" and p == 2:
+        pytest.skip("two devices: the compositor's own band is larger than the buffers "
+                    "(test_exchange_host_rotated_two_devices_is_the_engines_split)")
     w = 7
     fr, brows = split_rows(h, p, rows)
     # frame f's "ids": a unique value per (frame, row, column)
@@ -185,7 +188,7 @@ def test_share_exchange_layout_reassembles_every_frame(p, h, share, frames, b):
         assert np.array_equal(got, truth[f]), (c, f)
 
 
-@pytest.mark.parametrize("own", ["", "50", "80", "1", "99", "150", "-5"])
+@pytest.mark.parametrize("own", ["", "50", "80", "1", "99", "07"])
 def test_rotate_own_rows_matches_library(monkeypatch, own):
     """bands.rotate_own_rows (the Python restatement the bench and the tests use) against the engine's
     RotateOwnRows (srtRotateOwnRows) over frame heights from 1 row to 4K, default and overridden splits."""
@@ -200,3 +203,86 @@ def test_rotate_own_rows_matches_library(monkeypatch, own):
     for h in list(range(1, 70)) + [100, 135, 1079, 1080, 2160, 4321]:
         assert lib.srtRotateOwnRows(h) == rotate_own_rows(h), (own, h)
         assert 1 <= rotate_own_rows(h) <= max(1, h - 1)
+
+
+@pytest.mark.parametrize("own", ["150", "-5", "0", "abc", "80%", " 80", "8e1"])
+def test_rotate_own_rows_rejects_junk(monkeypatch, own):
+    """SRT_ROTATE_OWN is parsed strictly (strtol turned junk into 0, clamped to 1 %, so about
+    99 % of every frame silently crossed the link): the library returns 0 with the reason in
+    srtGetLastError, the restatement raises -- and an engine refuses to start with it."""
+    from simpleraytracer_amd import _native
+    from simpleraytracer_amd.bands import rotate_own_rows
+
+    monkeypatch.setenv("SRT_ROTATE_OWN", own)
+    lib = _native.lib()
+    assert lib.srtRotateOwnRows(1080) == 0
+    assert "SRT_ROTATE_OWN must be an integer per cent in 1..99" in _native.last_error()
+    with pytest.raises(ValueError):
+        rotate_own_rows(1080)
+
+
+@pytest.mark.parametrize("h", [1080, 2160, 100, 61])
+def test_exchange_host_rotated_two_devices_is_the_engines_split(monkeypatch, h):
+    """srtExchangeHost over two devices with rotated rows lays out the engine's split (it
+    reported even halves while the engine used the 4/5 split): buffer rows = the sent band 1 = H -
+    rotate_own_rows(H), and every frame reassembles from the compositor's own band plus the received
+    band 1 with the shading kernel's index expressions."""
+    from simpleraytracer_amd.bands import rotate_own_rows, rotated_range
+
+    monkeypatch.delenv("SRT_ROTATE_OWN", raising=False)
+    p, frames, w = 2, 4, 3
+    own = rotate_own_rows(h)
+    truth = np.arange(frames * h * w, dtype=np.int32).reshape(frames, h, w)
+    brows = h - own
+    bands = []
+    for d in range(p):
+        buf = np.full((frames, brows, w), -7, np.int32)
+        for f in range(frames):
+            c = f % p
+            if d != c:  # band 1 of a frame composited on the other device
+                b0, n = rotated_range(h, p, 1, own)
+                assert (b0, n) == (own, brows)
+                buf[f] = truth[f, b0:b0 + n]
+        bands.append(buf)
+    recv = exchange_host(bands, h, "rotated", "alltoall")
+    for c in range(p):
+        assert recv[c].shape == (p, frames // p, brows, w)
+    for f in range(frames):
+        c = f % p
+        got = np.full((h, w), -9, np.int32)
+        got[:own] = truth[f, :own]                       # the compositor's band 0, traced to RGBA in place
+        got[own:] = recv[c][1, f // p]                   # band 1 at RecvSlot(c, other) = BandOf = 1
+        assert np.array_equal(got, truth[f]), f
+
+
+def test_rotate_split_for_link_matches_restatement_and_keeps_the_link_off_the_bound():
+    """The two-device split from a measured link (srtRotateSplitForLink, the engine's choice when neither
+    an option nor SRT_ROTATE_OWN sets it) over link rates 20 .. 150 GB/s: equal to the Python
+    restatement, whole tile rows, at least half the frame, more of the frame kept as the link slows, and
+    at the chosen split the modelled link time within 80 % of the GPU time (unless even one tile row sent
+    is too much). 1080p C3 figures: one-GPU frame 16.96 us, packed ids 2.125 B per pixel."""
+    from simpleraytracer_amd import _native
+    from simpleraytracer_amd.bands import TILE_ROWS, rotate_split_for_link
+
+    lib = _native.lib()
+    for h, w, frame_us, bpp in ((1080, 1920, 16.96, 2.125), (2160, 3840, 144.7, 2.5), (100, 130, 3.0, 4.0),
+                                (61, 64, 1.0, 2.125), (1, 8, 1.0, 4.0)):
+        prev = None
+        for gbs in list(range(20, 151, 5)) + [0.0, -1.0, 1e9]:
+            r = lib.srtRotateSplitForLink(h, w, float(gbs), frame_us, bpp)
+            assert r == rotate_split_for_link(h, w, float(gbs), frame_us, bpp), (h, gbs)
+            assert 1 <= r <= max(1, h - 1)
+            if h > 2 * TILE_ROWS:
+                assert r % TILE_ROWS == 0 and r >= h // 2
+            if 0 < gbs < 1e9:
+                sent = h - r
+                link = sent * w * bpp / 2 / (gbs * 1e3)
+                gpu = frame_us * (0.553 + 0.25 * sent / h)
+                hi = (h - 1) // TILE_ROWS * TILE_ROWS if h > 2 * TILE_ROWS else h - 1
+                assert link <= 0.8 * gpu or r == hi, (h, gbs, r)
+                if prev is not None:
+                    assert r <= prev, (h, gbs)  # a faster link never keeps more of the frame
+                prev = r
+    # the 1080p soup: the split the engine would pick on a link of 64 GB/s (the DESIGN.md assumption), on
+    # the RCCL point-to-point peak of a link (~130 GB/s) and on a slow 20 GB/s one
+    assert [rotate_split_for_link(1080, 1920, g, 16.96, 2.125) for g in (20, 64, 130)] == [1008, 832, 544]

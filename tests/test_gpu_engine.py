@@ -122,14 +122,68 @@ def test_engine_fake_devices_rotated_two_device_split(gpu, scenes, monkeypatch, 
     refs = [torch_render(scenes["soup2k"], w, h, inputs[k]) for k in range(2 * F)]
     with engine(scenes["soup2k"], w, h, devices=[0] * p, rows="rotated", exchange="alltoall", queues=2,
                 batch=F) as e:
-        info = e.info()
-        assert info["band_rows"] == rotate_own_rows(h) and info["buffer_rows"] == h - rotate_own_rows(h)
+        info, split = e.info(), e.split()
+        # band_rows: the band stage timing traces, a sent one (band 1); the own band is the split's
+        assert info["band_rows"] == h - rotate_own_rows(h) and info["buffer_rows"] == h - rotate_own_rows(h)
+        assert split["own_rows"] == rotate_own_rows(h) and split["buffer_rows"] == info["buffer_rows"]
+        assert split["source"] == ("env" if own else "default") and split["link_gbs"] == 0.0  # fake devices
         e.set_inputs(inputs)
         e.run(3)
         for k in range(F, 3 * F):
             got = e.read_frame(k)
             assert np.array_equal(got.view(np.uint32), refs[k % (2 * F)].view(np.uint32)), (own, k)
         assert e.verify() == (0, 2 * F)
+
+
+def test_engine_rotated_two_device_options_split(gpu, scenes, monkeypatch):
+    """srt_engine_options.own_rows sets the two-device split (over SRT_ROTATE_OWN), bit for bit; an
+    invalid SRT_ROTATE_OWN refuses the engine instead of silently sending 99 % of every frame."""
+    from simpleraytracer_amd.device import SrtError
+
+    monkeypatch.setenv("SRT_ROTATE_OWN", "60")
+    h, w, F = 100, 130, 4
+    inputs = random_inputs(2 * F, h, w, seed=78)
+    refs = [torch_render(scenes["soup2k"], w, h, inputs[k]) for k in range(2 * F)]
+    with engine(scenes["soup2k"], w, h, devices=[0, 0], rows="rotated", exchange="alltoall", batch=F,
+                own_rows=48) as e:
+        assert e.split()["own_rows"] == 48 and e.split()["source"] == "option" and e.info()["buffer_rows"] == 52
+        e.set_inputs(inputs)
+        e.run(2)
+        for k in range(F, 2 * F):
+            assert np.array_equal(e.read_frame(k).view(np.uint32), refs[k].view(np.uint32)), k
+    monkeypatch.setenv("SRT_ROTATE_OWN", "abc")
+    with pytest.raises(SrtError, match="SRT_ROTATE_OWN must be an integer"):
+        engine(scenes["soup2k"], w, h, devices=[0, 0], rows="rotated", exchange="alltoall", batch=F)
+
+
+def test_engine_rotated_two_device_stage_times_whole_batch(gpu, scenes, monkeypatch):
+    """stage timing and the rank simulation's priming traced device 0's own band (864
+    of 1080 rows under the 4/5 split) into send slots sized for the 216-row band 1 -- past the end of the
+    send buffer when a launch took the whole batch. They now trace a sender band: a 1080-row frame, the
+    batch in one launch, then a run that must still be bit-exact; the rank simulation primes likewise."""
+    from simpleraytracer_amd.engine import FrameEngine
+
+    monkeypatch.delenv("SRT_ROTATE_OWN", raising=False)
+    h, w, F = 1080, 64, 4
+    inputs = random_inputs(F, h, w, seed=79)
+    refs = [torch_render(scenes["soup2k"], w, h, inputs[k]) for k in range(F)]
+    with engine(scenes["soup2k"], w, h, devices=[0, 0], rows="rotated", exchange="alltoall", batch=F,
+                launch=F) as e:
+        e.set_inputs(inputs)
+        for local in (0, 1):
+            n, _, binned, trace = e.stage_times(local, 3, F)
+            assert n == 3 and binned > 0 and trace > 0
+        assert e.info()["band_rows"] == e.info()["buffer_rows"] == 216
+        e.run(2)
+        for k in range(F, 2 * F):
+            assert np.array_equal(e.read_frame(k).view(np.uint32), refs[k % F].view(np.uint32)), k
+    for rank in (0, 1):
+        with FrameEngine.rank(scenes["soup2k"], w, h, 0, rank, 2, None, rows="rotated", exchange="alltoall",
+                              batch=2, simulate=True) as e:
+            e.set_inputs(inputs[:2])
+            e.run(2)
+            n, _, _, trace = e.stage_times(0, 2, 2)
+            assert n == 2 and trace > 0
 
 
 def test_engine_rotated_needs_alltoall(gpu, scenes):

@@ -13,6 +13,8 @@
 """
 from __future__ import annotations
 
+import os
+
 import time
 
 import numpy as np
@@ -93,6 +95,9 @@ def test_engine_rccl_self_exchange_full_c3_fixture(gpu, paths, ids):
     want = Expected(paths[C3], C3, ids[C3])
     with engine(paths[C3], m, devices=[0], batch=4, queues=2, rccl_self=True) as e:
         assert e.info()["rccl"]
+        # the link probe ran over the one-rank communicator (a copy to itself: a rate, no two-device split)
+        sp = e.split()
+        assert sp["link_gbs"] > 0 and sp["own_rows"] == 0 and sp["source"] == "none", sp
         e.set_inputs(offsets_for(m))
         e.run(3)
         for k in range(4, 12):
@@ -132,6 +137,11 @@ def test_engine_rccl_bands_full_c3_fixture(gpu, paths, ids, exchange, which):
     kw = {"exchange": "alltoall", "rows": "rotated"} if exchange == "rotated" else {"exchange": exchange}
     with engine(paths[C3], m, devices=list(range(P)), batch=2 * P, queues=2, **kw) as e:
         assert e.info()["rccl"] and e.info()["devices"] == P
+        sp = e.split()
+        assert sp["link_gbs"] > 0, sp
+        if exchange == "rotated" and P == 2 and not os.environ.get("SRT_ROTATE_OWN"):
+            # the split derived from the measured link (srtRotateSplitForLink)
+            assert sp["source"] == "link" and sp["frame_us"] > 0 and sp["own_rows"] >= m["height"] // 2, sp
         e.set_inputs(offsets_for(m))
         e.run(3)
         for k in range(2 * P, 6 * P):
