@@ -40,9 +40,13 @@ constexpr int kDiagOrderRow = 60000, kDiagBinRow = 61000;
             g_srt_diag[(row)][15] = (k) + 1;                                                         \
         }                                                                                            \
     } while (0)
+// Timing experiments of the diagnostic build (env SRT_EXP bits, the kernels' `exp` parameter): compiled
+// out of the product, where every SRT_EXP_BIT is false.
+#define SRT_EXP_BIT(p, bit) (((p).exp & (bit)) != 0u)
 #else
 #define SRT_STAMP(v)
 #define SRT_SETUP_MARK(row, k)
+#define SRT_EXP_BIT(p, bit) false
 #endif
 
 namespace {
@@ -320,7 +324,7 @@ __device__ __forceinline__ void ComputeRecord(const PrepareParams& p, const floa
     sb = disabled ? make_float4(__builtin_inff(), -__builtin_inff(), __builtin_inff(), -__builtin_inff())
                   : make_float4(0.f, 0.f, 0.f, 0.f);
 #ifdef SRT_DIAG
-    disabled = disabled || (p.exp & 512u) != 0u;  // timing experiment: 512 skips the screen box
+    disabled = disabled || SRT_EXP_BIT(p, 512u);  // timing experiment: 512 skips the screen box
 #endif
     if (!disabled) {
         // The float solve with proven error bounds where it applies (screen_box.h: every record of
@@ -591,11 +595,7 @@ __device__ __forceinline__ void StorePixel(const TraceParams& p, int x, int y, f
     if (p.out_ids != nullptr) {
         __builtin_nontemporal_store(id, p.out_ids + static_cast<size_t>(y) * p.width + x);
     } else {
-#ifdef SRT_EXP_NO_SHADE  // measurement builds only: store without shading
-        StoreRgba(p, x, y, make_float4(fx, fy, 0.f, static_cast<float>(id)));
-#else
         StoreRgba(p, x, y, ShadePixel(p, fx, fy, id));
-#endif
     }
 }
 
@@ -661,9 +661,6 @@ __device__ __forceinline__ void ShadeAndStore(const TraceParams& p, int x, int y
 #define SRT_SHADE_THREADS 128
 #endif
 constexpr int kShadeThreads = SRT_SHADE_THREADS;
-#ifndef SRT_SHADE_TILE_OFFSETS
-#define SRT_SHADE_TILE_OFFSETS 1  // shade regular tiles from the packed ids' tile offsets
-#endif
 #ifndef SRT_SHADE_ROWS
 // Rows per thread. Round 5, with every row's loads issued before any is used (the tile offsets pinned
 // there, exact float row division): 1 / 2 / 4 rows 690 / 646 / 582 us per 128-frame launch of a P = 2
@@ -679,18 +676,6 @@ __device__ __forceinline__ unsigned long long HitKey(float t, int id) {
     return (static_cast<unsigned long long>(__float_as_uint(t)) << 32) | static_cast<unsigned>(id);
 }
 
-#ifndef SRT_SHADE_NT_IDS
-// The packed ids' u16 plane: plain loads (1: nontemporal, A/B). Received just before the shading, a
-// batch's ids (P = 8: 62 MB) sit in the 256 MB Infinity Cache, which nontemporal loads went past: rank
-// simulation, compositor shading per 32-frame launch at P = 8 318 -> 278 us, P = 2 (282 MB) 772 -> 757.
-#define SRT_SHADE_NT_IDS 0
-#endif
-#ifndef SRT_SHADE_COMPACT
-#define SRT_SHADE_COMPACT 1  // 0: a grid over every row of the frame (A/B)
-#endif
-#ifndef SRT_SHADE_PIN_TILE_OFFSET
-#define SRT_SHADE_PIN_TILE_OFFSET 1
-#endif
 // Quotient of small unsigned integers, exact for y < 2^21 and any d >= 1: |fl(y + 1/2) * rcp(d) - (y +
 // 1/2) / d| <= (y + 1/2) / d * 1.5 * 2^-23 (v_rcp_f32 within 1 ulp, one rounding of the product), below
 // the 1 / (2 d) by which (y + 1/2) / d stays from an integer. The shading kernel's row mapping divides
@@ -746,23 +731,12 @@ __global__ __launch_bounds__(kShadeThreads) void ShadeIdsKernel(TraceParams p, c
     // (A grid over every row, whose own-band threads loaded and stored nothing, cost a compositor of
     // the share exchange -- a fifth of its rows shaded -- 7.3 us per frame, 2.6 us compacted.)
     const unsigned j0 = blockIdx.y * kShadeRows;
-#if SRT_SHADE_COMPACT
     const int y0 = static_cast<int>(ShadeRowOf(j0, band_rows, interleaved, skip_band, own_bands, first_rows));
-#else
-    const int y0 = static_cast<int>(j0);
-#endif
     if (y0 >= p.row_count) {
         return;
     }
     const unsigned g = blockIdx.z;
     const size_t pixels = static_cast<size_t>(p.width) * p.row_count;
-#ifdef SRT_EXP_SHADE_STORE_ONLY  // measurement builds only (make exp): the stores alone, no loads
-    {
-        StoreNontemporal(reinterpret_cast<F4*>(p.out + g * pixels + static_cast<size_t>(y0) * p.width + x),
-                         F4{static_cast<float>(x), static_cast<float>(y0), static_cast<float>(g), 0.f});
-        return;
-    }
-#endif
     // Three phases with no control flow between the loads of different rows, so every row's loads are
     // in flight together: (1) every row's id (packed: its u16, bit-plane words and tile offset --
     // wave-uniform addresses), (2) every hit's sample offset (irregular tiles) and every row's shading
@@ -785,7 +759,7 @@ __global__ __launch_bounds__(kShadeThreads) void ShadeIdsKernel(TraceParams p, c
     // compositor traced them as RGBA already.)
 #pragma unroll
     for (int r = 0; r < kShadeRows; ++r) {
-        yr[r] = interleaved != 0u || r == 0 || !SRT_SHADE_COMPACT
+        yr[r] = interleaved != 0u || r == 0
                     ? y0 + r
                     : static_cast<int>(ShadeRowOf(j0 + r, band_rows, interleaved, skip_band, own_bands, first_rows));
         const bool past = yr[r] >= p.row_count;
@@ -801,19 +775,11 @@ __global__ __launch_bounds__(kShadeThreads) void ShadeIdsKernel(TraceParams p, c
             band = UDivSmall(y, band_rows);
             local = y - band * band_rows;
         }
-        if (!SRT_SHADE_COMPACT && (band == skip_band || band < own_bands)) {
-            yr[r] = p.row_count;  // (full grid: the compositor's own rows are not stored)
-            band = own_bands;
-        }
         const unsigned slot = band - own_bands;
         if constexpr (PACKED) {
             const unsigned char* frame = packed + (static_cast<size_t>(slot) * frames + g) * frame_bytes;
             const unsigned char* row = PackedRow(frame, p, static_cast<int>(local));
-#if SRT_SHADE_NT_IDS
-            code[r] = __builtin_nontemporal_load(reinterpret_cast<const unsigned short*>(row) + x);
-#else
             code[r] = reinterpret_cast<const unsigned short*>(row)[x];
-#endif
             const unsigned long long* bits = reinterpret_cast<const unsigned long long*>(row + p.id_low_row_bytes);
 #pragma unroll
             for (int j = 0; j < PLANES; ++j) {
@@ -837,9 +803,7 @@ __global__ __launch_bounds__(kShadeThreads) void ShadeIdsKernel(TraceParams p, c
             for (int j = 0; j < PLANES; ++j) {
                 code[r] |= static_cast<unsigned>((plane[r][j] >> (x & 63)) & 1ull) << (16 + j);
             }
-#if SRT_SHADE_PIN_TILE_OFFSET
             asm volatile("" ::"s"(tile_o[r].x), "s"(tile_o[r].y));
-#endif
         }
     }
     // Only a hit needs its ray: a miss shades to the background whatever its sample offset (a miss is
@@ -855,19 +819,14 @@ __global__ __launch_bounds__(kShadeThreads) void ShadeIdsKernel(TraceParams p, c
     for (int r = 0; r < kShadeRows; ++r) {
         const int y = yr[r] < p.row_count ? yr[r] : y0;
         hit[r] = code[r] < p.n ? static_cast<int>(code[r]) : -1;
-        const bool regular = PACKED && SRT_SHADE_TILE_OFFSETS && tile_o[r].x == tile_o[r].x;
+        const bool regular = PACKED && tile_o[r].x == tile_o[r].x;
         o[r] = tile_o[r];
         if (!regular) {
             o[r] = p.offsets[static_cast<size_t>(y) * p.width + x + g * offsets_stride];  // frame g's (stride 0: shared)
         }
-#ifdef SRT_EXP_SHADE_NO_RECORD  // measurement builds only: no shading-record gather
-        nr[r] = make_float4(1.f, 0.f, 0.f, 1.f);
-        al[r] = make_float4(0.5f, 0.5f, 0.5f, 0.f);
-#else
         const float4* sr = p.shade + 2ull * static_cast<unsigned>(max(hit[r], 0));
         nr[r] = sr[0];
         al[r] = sr[1];
-#endif
     }
 #pragma unroll
     for (int r = 0; r < kShadeRows; ++r) {
@@ -1168,19 +1127,6 @@ constexpr int kWindowPackets = SRT_WINDOW_PACKETS;  // packet walk: packets per 
 constexpr unsigned kWindowPixels = kWindowPackets * kWave;
 static_assert(kWindowPackets == 2 * kWave, "window prefix: two packets per lane");
 
-#ifndef SRT_PK_READLANE
-#define SRT_PK_READLANE 0
-#endif
-#ifndef SRT_LDS_SWIZZLE
-#define SRT_LDS_SWIZZLE 0
-#endif
-// Column slot of pixel (row, col) in the block's 8-B-per-pixel LDS tables (positions, keys). With
-// SRT_LDS_SWIZZLE the column is XORed with the row: a 512-B row puts column c of every row in the same
-// bank pair, so the lanes of a packet walking a narrow range (several rows, few columns) conflicted.
-__device__ __forceinline__ unsigned PixSlot(unsigned row, unsigned col) {
-    return SRT_LDS_SWIZZLE ? (col ^ row) & (kWave - 1u) : col;
-}
-
 // Batch entry of thread tid's slice e (kPacketBatch < kCullThreads: the first threads only).
 __device__ __forceinline__ bool InBatch(int e, int tid) { return e * kCullThreads + tid < kPacketBatch; }
 
@@ -1199,13 +1145,8 @@ struct CullShared {
     unsigned wave_n[kSlices * kCullWaves];   // survivors per (slice, wave)
     unsigned wave_pk[kSlices * kCullWaves];  // pixels per (slice, wave)
     uint2 pk[2][kWindowPackets];  // window packet k: last-pixel bits (lo, hi); two buffers, alternate batches
-#ifndef SRT_EXP_NO_FXY
     float2 fxy[kBlockRows][kWave];  // ray position (fx, fy) of every pixel of the block (512-B rows:
                                     // rows padded by 8 or 16 B to skew the banks measured 3-6 % slower)
-#endif
-#ifdef SRT_EXP_LDS_PAD  // measurement builds only: fewer blocks per CU
-    unsigned exp_pad[SRT_EXP_LDS_PAD];
-#endif
     float clo[kWave], chi[kWave];    // monotone column bounds of fx (suffix min, prefix max)
     float rlo[kBlockRows], rhi[kBlockRows];  // monotone row bounds of fy
     unsigned counts[2][kCullWaves];            // FULL stream: survivors per wave and step
@@ -1347,9 +1288,7 @@ __device__ __forceinline__ void PacketTables(CullShared& sh, const Rays<kCullR>&
     const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-#ifndef SRT_EXP_NO_FXY
-        sh.fxy[wave * R + r][PixSlot(wave * R + r, lane)] = make_float2(s.fx[r], s.fy[r]);
-#endif
+        sh.fxy[wave * R + r][lane] = make_float2(s.fx[r], s.fy[r]);
     }
     if (regular) {
         if (tid < kWave) {
@@ -1542,18 +1481,12 @@ __device__ __forceinline__ void PacketBatch(CullShared& sh, const Box& bb, const
     // range. The waves split each window's packets evenly, kPacketIlp at a time (independent
     // chains; a tail repeats the last packet, harmless under the atomic min).
     constexpr int kPacketIlp = SRT_PACKET_ILP;
-#ifndef SRT_EXP_NO_FXY
     const char* fxy = reinterpret_cast<const char*>(&sh.fxy[0][0]);
-#endif
     char* keys = reinterpret_cast<char*>(&sh.keys[0][0]);
     const unsigned last_slot = n_surv == 0u ? 0u : n_surv - 1u;
     unsigned ended = 0u;  // ranges that end before the window (block-uniform)
 #pragma unroll 1
-#ifdef SRT_EXP_NO_WALK  // measurement builds only: filter and compact, no pixel tests
-    for (unsigned w0 = 0; w0 < 0u; w0 += kWindowPixels) {
-#else
     for (unsigned w0 = 0; w0 < n_pk; w0 += kWindowPixels) {
-#endif
         const unsigned wn = min(kWindowPixels, n_pk - w0);
         const unsigned npk_w = (wn + kWave - 1u) / kWave;
         if (w0 != 0u) {  // a later window (rare: > kWindowPixels pixels in the batch): rebuild its bitmap
@@ -1599,15 +1532,8 @@ __device__ __forceinline__ void PacketBatch(CullShared& sh, const Box& bb, const
                 if (kk & 1u) {
                     z += static_cast<unsigned>(__builtin_amdgcn_readlane(static_cast<int>(ca), src));
                 }
-#if SRT_PK_READLANE
-                // from the scan's registers: lane kk / 2 holds packets 2l (pa) and 2l + 1 (pb)
-                const uint2 e = make_uint2(
-                    static_cast<unsigned>(__builtin_amdgcn_readlane(static_cast<int>((kk & 1u) ? pb.x : pa.x), src)),
-                    static_cast<unsigned>(__builtin_amdgcn_readlane(static_cast<int>((kk & 1u) ? pb.y : pa.y), src)));
-#else
                 const uint2 e = pkb[kk];  // one address: a broadcast read (from the scan's registers by
                                           // readlane: 2 VGPR spills in round 2, measured 3 % slower)
-#endif
                 const unsigned g = w0 + kk * kWave + static_cast<unsigned>(lane);
                 const unsigned sl = min(__builtin_amdgcn_mbcnt_hi(e.y, __builtin_amdgcn_mbcnt_lo(e.x, 0u)) + z,
                                         last_slot);
@@ -1635,12 +1561,7 @@ __device__ __forceinline__ void PacketBatch(CullShared& sh, const Box& bb, const
                         r = wrap ? r + 1u : r;
                     }
                     const bool ok = in && r < nr;
-#if SRT_LDS_SWIZZLE
-                    const unsigned ra = (base >> 9) + r, ca = ((base >> 3) & (kWave - 1u)) + c;
-                    px[u][j] = PacketPixel{ok ? (ra << 9) + (PixSlot(ra, ca) << 3) : 0u, ok};
-#else
                     px[u][j] = PacketPixel{ok ? base + (r << 9) + (c << 3) : 0u, ok};
-#endif
                 }
             }
             PacketHit h[kPacketIlp][kLanePixels];
@@ -1648,12 +1569,7 @@ __device__ __forceinline__ void PacketBatch(CullShared& sh, const Box& bb, const
             for (int u = 0; u < kPacketIlp; ++u) {
 #pragma unroll
                 for (int j = 0; j < kLanePixels; ++j) {
-#ifdef SRT_EXP_NO_FXY  // measurement builds only (regular tiles: the position tables are the positions)
-                    f[u][j] = make_float2(sh.clo[PixSlot(px[u][j].pixb >> 9, (px[u][j].pixb >> 3) & 63u)],
-                                          sh.rlo[px[u][j].pixb >> 9]);
-#else
                     f[u][j] = *reinterpret_cast<const float2*>(fxy + px[u][j].pixb);
-#endif
                 }
             }
 #pragma unroll
@@ -2265,12 +2181,12 @@ __global__ __launch_bounds__(kBinThreads) void PrepareBinKernel(const Frames bat
     // The record's tile range (bit k of the mask below = tile (r0 + k / w, c0 + k % w) of the
     // range, at most kLargeTiles of them).
     int c0 = 0, r0 = 0, w = 0, h = 0;
-    if (real && sb.x <= sb.y && sb.z <= sb.w && (p.exp & 1u) == 0u) {  // else disabled: empty box
+    if (real && sb.x <= sb.y && sb.z <= sb.w && !SRT_EXP_BIT(p, 1u)) {  // else disabled: empty box
         // Any tile (c, r) whose box overlaps sb has hi'[c] >= hi[c] >= sb.xlo and
         // lo'[c] <= lo[c] <= sb.xhi, so c lies in [c0, c1]; rows likewise.
         const BoundModel mc = MakeBoundModel(b, nx), mr = MakeBoundModel(b + nx, ny);
         int c1, r1;
-        if ((p.exp & 16u) != 0u) {  // diag timing: a fixed one-tile range instead of the searches
+        if (SRT_EXP_BIT(p, 16u)) {  // diag timing: a fixed one-tile range instead of the searches
             c0 = c1 = r0 = r1 = static_cast<int>(i % 4u);
         } else {
             c0 = FirstHiAtLeast(b, nx, sb.x, mc);
@@ -2280,11 +2196,11 @@ __global__ __launch_bounds__(kBinThreads) void PrepareBinKernel(const Frames bat
         }
         w = max(c1 - c0 + 1, 0);
         h = max(r1 - r0 + 1, 0);
-        if (w * h > kLargeTiles && (p.exp & 2u) == 0u) {
+        if (w * h > kLargeTiles && !SRT_EXP_BIT(p, 2u)) {
             p.large_list[atomicAdd(&p.counts[tiles], 1u)] = i;
         }
     }
-    const bool listed = w * h > 0 && w * h <= kLargeTiles && (p.exp & 2u) == 0u;
+    const bool listed = w * h > 0 && w * h <= kLargeTiles && !SRT_EXP_BIT(p, 2u);
     const RangeDiv rd(w);
     unsigned mask = 0u;
     if (listed) {
@@ -2310,7 +2226,7 @@ __global__ __launch_bounds__(kBinThreads) void PrepareBinKernel(const Frames bat
 #pragma unroll
         for (int k = 0; k < kBinAhead; ++k) {
             const Box tb{box[k].x, box[k].y, box[k].z, box[k].w};
-            if (k < w * h && usable[k] != 0u && ((p.exp & 32u) != 0u || (ScreenBoxOverlaps(tb, sb) && BoxMayHit(tb, rec)))) {
+            if (k < w * h && usable[k] != 0u && (SRT_EXP_BIT(p, 32u) || (ScreenBoxOverlaps(tb, sb) && BoxMayHit(tb, rec)))) {
                 mask |= 1u << k;
             }
         }
@@ -2355,7 +2271,7 @@ __global__ __launch_bounds__(kBinThreads) void PrepareBinKernel(const Frames bat
     }
     __syncthreads();  // the span's histogram zeroed
     SRT_SETUP_MARK(kDiagBinRow + blockIdx.x, 3);
-    for (unsigned m = (p.exp & 8u) ? 0u : mask; m != 0u; m &= m - 1u) {  // diag timing: 8 skips the counts
+    for (unsigned m = SRT_EXP_BIT(p, 8u) ? 0u : mask; m != 0u; m &= m - 1u) {  // diag timing: 8 skips the counts
         const int k = __builtin_ctz(m);
         atomicAdd(&hist[rd.Tile(k, r0, c0, nx)], 1u);
     }
@@ -2365,7 +2281,7 @@ __global__ __launch_bounds__(kBinThreads) void PrepareBinKernel(const Frames bat
         const unsigned t = t_lo + k;
         const unsigned h = hist[t];
         if (h != 0u) {
-            hist[t] = (p.exp & 4u) ? 0u : atomicAdd(&p.counts[t], h);  // this block's base in the list
+            hist[t] = SRT_EXP_BIT(p, 4u) ? 0u : atomicAdd(&p.counts[t], h);  // this block's base in the list
         }
     }
     __syncthreads();
@@ -2623,30 +2539,6 @@ std::size_t OrderLdsBytes(int tiles) { return static_cast<std::size_t>(tiles) * 
 #ifndef SRT_TRACE_OCC
 #define SRT_TRACE_OCC 6
 #endif
-#ifndef SRT_LIST_AHEAD
-#define SRT_LIST_AHEAD 1
-#endif
-#ifndef SRT_PLAN_EMPTY_TEST
-#define SRT_PLAN_EMPTY_TEST 1  // plan-only trace blocks test an empty tile against the large list's records
-#endif
-#ifndef SRT_SPLIT_ATOMIC
-#define SRT_SPLIT_ATOMIC 0  // 1: split parts merged with 64-bit atomic maxima in one slice per part (measured:
-                            // one frame in flight, trace 20.4 -> 22.5 us; 8-frame launches unchanged)
-#endif
-#ifndef SRT_SPLIT_ARRIVE_FIRST
-#define SRT_SPLIT_ARRIVE_FIRST 0  // split parts: 1 = arrive, then publish unless last (measured: trace 19.7 -> 21.6 us)
-#endif
-#if SRT_SPLIT_ARRIVE_FIRST
-constexpr unsigned kSplitReady = 1u << 16;         // split part word: arrivals (low bits), readies (x kSplitReady)
-constexpr unsigned kSplitPollCap = 1u << 22;       // last arriver's polls of the word (hang guard)
-static_assert(kMaxChunks < 65536, "split part word: arrival count in 16 bits");
-#endif
-#ifndef SRT_TRACE_PRIO
-#define SRT_TRACE_PRIO 0
-#endif
-#ifndef SRT_TRACE_PRIO_HEAVY
-#define SRT_TRACE_PRIO_HEAVY 256
-#endif
 
 template <class Frames>
 __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(const Frames batch) {
@@ -2704,9 +2596,6 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(c
         if (threadIdx.x == 0 && d == 0u) {
             p.bin_counts_next[p.tiles] = 0u;
         }
-#ifdef SRT_EXP_SETUP_ONLY  // measurement builds only (make exp): the frame's setup without its trace
-        return;
-#endif
         bool full;
         unsigned c_t, list_len;
         if (p.plan_only != 0u) {
@@ -2725,7 +2614,6 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(c
             oy = ti.oy;
             c_t = full ? 0u : cnt + large;
             list_len = full ? 0u : cnt;
-#if SRT_PLAN_EMPTY_TEST
             if (!full && cnt == 0u && large <= static_cast<unsigned>(kEmptyTest) && nchunks == 1u) {
                 const Box tb{ti.box.x, ti.box.y, ti.box.z, ti.box.w};  // the empty test (WorkOrderKernel)
                 CullRecord lr[kEmptyTest];
@@ -2746,13 +2634,6 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(c
                 }
                 flags |= may ? 0u : kItemEmpty;
             }
-#else
-            // (no candidates at all: every pixel misses; a tile with an empty list and a few large-list
-            // records walks them -- the record-testing form of this test measured slower in batched
-            // launches: code size)
-            flags |= !full && cnt == 0u && large == 0u && nchunks == 1u ? kItemEmpty : 0u;
-            (void)lid;
-#endif
         } else {
             flags = w0.w;
             ox = __uint_as_float(w1.x);
@@ -2772,15 +2653,6 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(c
             src.count1 = list_len;
             src.begin = chunk * q + chunk * r / nchunks;
             src.end = (chunk + 1u) * q + (chunk + 1u) * r / nchunks;
-#if SRT_TRACE_PRIO
-            // the frame's critical path: heavy chunks' waves issue first on a shared SIMD
-            const unsigned work = src.end - src.begin;
-            if (work >= SRT_TRACE_PRIO_HEAVY) {
-                __builtin_amdgcn_s_setprio(2);
-            } else if (work >= SRT_TRACE_PRIO_HEAVY / 4) {
-                __builtin_amdgcn_s_setprio(1);
-            }
-#endif
         }
     } else {
         item = blockIdx.y * gridDim.x + blockIdx.x;
@@ -2826,13 +2698,8 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(c
     }
     // LIST: the first batch's records are requested before the rays are set up (its loads
     // are the block's longest dependency chain: list entry, then the 64-B record).
-#ifdef SRT_EXP_NO_LIST  // measurement builds only: no candidates (rays, tables, shading, stores)
-    const unsigned total = 0u;
-#else
     const unsigned total = src.end - src.begin;
-#endif
     CullRecord nxt[kSlices];
-#if SRT_LIST_AHEAD
     // The list entries run one batch ahead of the records: batch b's prefetch loads batch b + 1's
     // records from entries that arrived during batch b - 1's walk, then requests batch b + 2's
     // entries (one load chain per batch no longer waits in front of the walk).
@@ -2865,21 +2732,6 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(c
         load_ids(0u);
         load_list(0u);
     }
-#else
-    auto load_list = [&](unsigned b0) {
-#pragma unroll
-        for (int e = 0; e < kSlices; ++e) {
-            const unsigned v = b0 + e * kCullThreads + tid;
-            if (InBatch(e, tid)) {
-                const unsigned vv = src.begin + (v < total ? v : 0u);
-                nxt[e] = p.cull[vv < src.count1 ? src.list[vv] : src.list2[vv - src.count1]];
-            }
-        }
-    };
-    if (!src.full && total != 0u) {
-        load_list(0u);
-    }
-#endif
     // Rays: lane = column x; rows y0 .. y0 + R - 1. A regular tile (every ray with the sample
     // offset (ox, oy)) computes them without reading the offsets: fx per lane, and row r's fy
     // from lane (wave R + r) of fy_lane (the GenerateRays expressions, bit for bit).
@@ -3043,7 +2895,7 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(c
     unsigned long long key[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        key[r] = sh.keys[wave * R + r][PixSlot(wave * R + r, lane)];
+        key[r] = sh.keys[wave * R + r][lane];
     }
     if (nchunks > 1u) {
         constexpr int kPix = kBlockRows * kWave;
@@ -3058,80 +2910,6 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(c
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
         };
-#if SRT_SPLIT_ARRIVE_FIRST
-        // Split part: the chunk counts its arrival first (low 16 bits of the part's word). Every
-        // chunk but the last then publishes its keys and adds kSplitReady (hand-off form:
-        // MI355X_MICROARCH.md "Valid forms", sc1 stores, every storing wave's vmcnt(0), barrier,
-        // one agent-scope add); the last polls the word (sc1 loads) until every other chunk is
-        // ready -- they have all arrived, so they are running and get there -- and takes the
-        // minimum over their keys (sc1 loads after a barrier). The last chunk's own keys never
-        // leave the block (half the slice traffic of a two-chunk part), but the chunks of a part
-        // finish together, so the last one mostly waits for the others' arrival round trip plus
-        // their publish: one frame in flight, 19.7 -> 21.6 us; off by default. The poll is capped
-        // (a hang guard: it only ends early if a chunk never readies, which no path does).
-        if (tid == 0) {
-            const unsigned before = __hip_atomic_fetch_add(&p.arrive[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            sh.last = (before & (kSplitReady - 1u)) == nchunks - 1u ? 1u : 0u;
-        }
-        __syncthreads();
-        if (sh.last == 0u) {
-            publish();
-            if (tid == 0) {
-                __hip_atomic_fetch_add(&p.arrive[slot], kSplitReady, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            SRT_DIAG_END(item, chunk, nchunks, 0u, src.full);
-            return;
-        }
-        if (tid == 0) {
-            const unsigned want = (nchunks - 1u) * kSplitReady + nchunks;  // every arrival, every other chunk ready
-            for (unsigned it = 0; it < kSplitPollCap; ++it) {
-                if (__hip_atomic_load(&p.arrive[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == want) {
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(2);
-            }
-            __hip_atomic_store(&p.arrive[slot], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // the next frame's
-        }
-        __syncthreads();
-#elif SRT_SPLIT_ATOMIC
-        // Split part, merged in the L2: every chunk folds the keys it found (hit pixels only) into
-        // the part's first slice with 64-bit atomic maxima of ~key (zero = no hit yet, the state
-        // every slice is in between frames), then counts its arrival; the last of the part's chunks
-        // reads the merged keys once, takes its own into account and zeroes the slice for the
-        // next frame. (Hand-off as below: the atomics complete (vmcnt(0)) before the barrier and the
-        // agent-scope add.)
-        {
-            unsigned long long* merged = slices;
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                if (key[r] != ~0ull) {
-                    __hip_atomic_fetch_max(merged + pix + r * kWave, ~key[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            if (tid == 0) {
-                const unsigned before = __hip_atomic_fetch_add(&p.arrive[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const unsigned last = before == nchunks - 1u ? 1u : 0u;
-                if (last != 0u) {
-                    __hip_atomic_store(&p.arrive[slot], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-                sh.last = last;
-            }
-            __syncthreads();
-            if (sh.last == 0u) {
-                SRT_DIAG_END(item, chunk, nchunks, 0u, src.full);
-                return;
-            }
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                const unsigned long long m =
-                    ~__hip_atomic_load(merged + pix + r * kWave, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                key[r] = m < key[r] ? m : key[r];
-                __hip_atomic_store(merged + pix + r * kWave, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-#else
         // Split part: publish this chunk's keys, count the arrival; the last of the part's chunks
         // takes the minimum over every chunk's keys (sc1 loads) and shades. Hand-off form:
         // MI355X_MICROARCH.md "Valid forms", table row 1 (sc1 stores, every storing wave's
@@ -3150,8 +2928,6 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(c
             SRT_DIAG_END(item, chunk, nchunks, 0u, src.full);
             return;
         }
-#endif
-#if !SRT_SPLIT_ATOMIC || SRT_SPLIT_ARRIVE_FIRST
         for (unsigned c = 0; c < nchunks; ++c) {
             if (c == chunk) {
                 continue;
@@ -3163,7 +2939,6 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(c
                 key[r] = o < key[r] ? o : key[r];
             }
         }
-#endif
     }
     if (p.out_packed != nullptr) {  // packed ids: every lane of the wave takes part (ballots)
 #pragma unroll
@@ -3198,11 +2973,7 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(c
         for (int r = 0; r < R; ++r) {
             const int y = y0 + r;
             if (y < p.row_count) {
-#ifdef SRT_EXP_NO_FXY
-                const float2 f = make_float2(sh.clo[lane], sh.rlo[wave * R + r]);
-#else
-                const float2 f = sh.fxy[wave * R + r][PixSlot(wave * R + r, lane)];
-#endif
+                const float2 f = sh.fxy[wave * R + r][lane];
                 StoreRgba(p, x, y, ShadeRecord(p, f.x, f.y, id[r], nr[r], al[r]));
             }
         }
@@ -3731,15 +3502,9 @@ std::size_t CullBinBytes(std::uint64_t n, std::size_t width, std::size_t row_cou
     return z.info + z.counts + z.lists + z.large + z.work + z.work_count + z.arrive + z.split_keys + z.range_tag;
 }
 
-#ifndef SRT_COUNTERS_FIRST
-#define SRT_COUNTERS_FIRST 1  // 0: the former carve-up (tile info first) and whole slots zeroed (A/B)
-#endif
 std::size_t CullBinCounterBytes(std::uint64_t n, std::size_t width, std::size_t row_count) {
     const BinSizes z = CullBinSizes(n, width, row_count);
-    if (!SRT_COUNTERS_FIRST) {
-        return CullBinBytes(n, width, row_count);
-    }
-    return z.counts + z.work_count + z.arrive + z.range_tag + (SRT_SPLIT_ATOMIC ? z.split_keys : 0);  // (atomic maxima)
+    return z.counts + z.work_count + z.arrive + z.range_tag;
 }
 
 CullBins CullBinLayout(void* base, std::uint64_t n, std::size_t width, std::size_t row_count, unsigned parity) {
@@ -3753,25 +3518,15 @@ CullBins CullBinLayout(void* base, std::uint64_t n, std::size_t width, std::size
     };
     // The counters first (CullBinCounterBytes: the only bytes that must start zero), then the buffers
     // every frame writes before it reads them.
-    if (!SRT_COUNTERS_FIRST) {
-        b.tile_info = take(z.info);
-    }
     unsigned* counts = reinterpret_cast<unsigned*>(take(z.counts));
     b.work_count = reinterpret_cast<unsigned*>(take(z.work_count));
     b.arrive = reinterpret_cast<unsigned*>(take(z.arrive));
     b.range_tag = reinterpret_cast<unsigned*>(take(z.range_tag));
-    if (SRT_SPLIT_ATOMIC) {
-        b.split_keys = take(z.split_keys);  // slices merged by atomic maxima start zero too
-    }
-    if (SRT_COUNTERS_FIRST) {
-        b.tile_info = take(z.info);
-    }
+    b.tile_info = take(z.info);
     b.lists = reinterpret_cast<unsigned*>(take(z.lists));
     b.large_list = reinterpret_cast<unsigned*>(take(z.large));
     b.work = take(z.work);
-    if (!SRT_SPLIT_ATOMIC) {
-        b.split_keys = take(z.split_keys);
-    }
+    b.split_keys = take(z.split_keys);
     b.tiles = CullTiles(width, row_count);
     b.counts = counts + (parity & 1u) * (b.tiles + 1);
     b.counts_next = counts + ((parity & 1u) ^ 1u) * (b.tiles + 1);
@@ -4252,7 +4007,7 @@ hipError_t LaunchShade(const float* d_vertices, const float* d_shade, const floa
     }
     const unsigned skip = skip_band < 0 ? 0xFFFFFFFFu : static_cast<unsigned>(skip_band);
     const std::size_t stored =
-        SRT_SHADE_COMPACT ? ShadeRowsLaunched(band.row_count, band_rows, interleaved, skip, own_bands, first_rows) : band.row_count;
+        ShadeRowsLaunched(band.row_count, band_rows, interleaved, skip, own_bands, first_rows);
     if (stored == 0) {
         return hipSuccess;
     }
