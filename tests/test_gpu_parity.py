@@ -787,6 +787,43 @@ def test_trace_batch_bitwise(gpu, scenes, variant):
     scene.close()
 
 
+def test_trace_batch_regular_and_irregular_tiles(gpu, scenes):
+    """Ordered (multi-frame) cull launches over frames that mix regular tiles (one sample offset for every
+    ray: positions from the column / row tables) and irregular ones (columns and row blocks of jitter, a
+    NaN patch), uniform, jittered and FULL-stream regular frames (a uniform offset outside [0, 1]) in one
+    batch, and a band of ids: each equal to the brute-force frame bit for bit."""
+    import torch
+
+    import simpleraytracer_amd as srt
+
+    w, h = 640, 360
+    rng = np.random.default_rng(91)
+    mixed = np.full((h, w, 2), 0.5, np.float32)
+    mixed[:, 64:128, 0] = rng.random((h, 64), dtype=np.float32)
+    mixed[100:180, 300:500] = rng.random((80, 200, 2), dtype=np.float32)
+    mixed2 = np.full((h, w, 2), 0.25, np.float32)
+    mixed2[:, 600:] = rng.random((h, 40, 2), dtype=np.float32)
+    mixed2[200:220, 10:50] = np.nan
+    offs = [mixed, np.full((h, w, 2), 0.5, np.float32), rng.random((h, w, 2), dtype=np.float32),
+            np.full((h, w, 2), 2.0, np.float32), mixed2]
+    refs = [torch_render(scenes["soup100k"], w, h, o, variant="lds") for o in offs]
+    scene = srt.DeviceScene(scenes["soup100k"], 0)
+    stream = torch.cuda.current_stream()
+    scene.prepare(w, h, stream)
+    ins = [torch.from_numpy(o).cuda() for o in offs]
+    for rep in range(2):
+        outs = [torch.full((h, w, 4), float("nan"), dtype=torch.float32, device="cuda") for _ in offs]
+        scene.trace_batch(ins, outs, 0, h, stream=stream)
+        r0, rows = 37, 200
+        ids = [torch.full((rows, w), -7, dtype=torch.int32, device="cuda") for _ in offs]
+        scene.trace_batch([o[r0:r0 + rows].contiguous() for o in ins], ids, r0, rows, stream=stream, ids=True)
+        torch.cuda.synchronize()
+        for k, (out, ref) in enumerate(zip(outs, refs)):
+            assert np.array_equal(out.cpu().numpy().view(np.uint32), ref.view(np.uint32)), (rep, k)
+            assert np.array_equal(ids[k].cpu().numpy().astype(np.float32), ref[r0:r0 + rows, :, 3]), (rep, "ids", k)
+    scene.close()
+
+
 def test_trace_batch_c3_band_of_8(gpu, scenes):
     """The bench's N = 8 band (135 rows of 1080p, C3) batched 8 frames at a time: every frame's
     ids equal a single srtTraceIdsAsync of the band, bit for bit."""
