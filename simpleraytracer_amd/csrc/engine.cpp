@@ -451,11 +451,6 @@ private:
     std::exception_ptr m_error;
 };
 
-static bool ShadeStreamFromEnv() {
-    const char* v = std::getenv("SRT_SHADE_STREAM");
-    return v != nullptr && std::strcmp(v, "1") == 0;
-}
-
 // ---------------------------------------------------------------------------------------------
 
 struct FrameEngine::Queue {
@@ -464,13 +459,6 @@ struct FrameEngine::Queue {
     hipEvent_t traced = nullptr;     // the batch's trace done (queue stream)
     hipEvent_t exchanged = nullptr;  // the batch's exchange done (comm stream)
     hipEvent_t drained = nullptr;    // end-of-run marker (queue stream), polled with a deadline
-    // The compositor's deferred shading on a stream of its own at the lowest priority (the queue streams
-    // at the highest; env SRT_SHADE_STREAM=1), so the bandwidth-bound shading fills the slots the other
-    // queue's latency-bound traces leave; null: the shading runs on `stream`. The scene orders the two
-    // (DeviceScene: an event when the stream changes): a batch's shading after its trace, the queue's
-    // next trace after that shading (it reuses the receive buffer and the frames).
-    hipStream_t shade = nullptr;
-    hipEvent_t shade_drained = nullptr;
     // Id buffers of band frames, m_band_id_bytes each (int32 ids, or packed ids: render.h PackedIds).
     unsigned char* send = nullptr;   // bands: ids for the other compositors
     unsigned char* recv = nullptr;   // bands: [P][frames composited here][buffer rows][W] ids
@@ -766,15 +754,7 @@ void FrameEngine::AllocateQueues() {
         HipCheck(hipEventCreateWithFlags(&d.comm_drained, hipEventDisableTiming), "hipEventCreate(comm drained)");
         d.queues.resize(m_opt.queues);
         for (Queue& q : d.queues) {
-            if (m_exchange && ShadeStreamFromEnv()) {
-                int least = 0, greatest = 0;
-                HipCheck(hipDeviceGetStreamPriorityRange(&least, &greatest), "hipDeviceGetStreamPriorityRange");
-                HipCheck(hipStreamCreateWithPriority(&q.stream, hipStreamNonBlocking, greatest), "hipStreamCreate(queue)");
-                HipCheck(hipStreamCreateWithPriority(&q.shade, hipStreamNonBlocking, least), "hipStreamCreate(shade)");
-                HipCheck(hipEventCreateWithFlags(&q.shade_drained, hipEventDisableTiming), "hipEventCreate(shade drained)");
-            } else {
-                HipCheck(hipStreamCreateWithFlags(&q.stream, hipStreamNonBlocking), "hipStreamCreate(queue)");
-            }
+            HipCheck(hipStreamCreateWithFlags(&q.stream, hipStreamNonBlocking), "hipStreamCreate(queue)");
             HipCheck(hipEventCreateWithFlags(&q.traced, hipEventDisableTiming), "hipEventCreate(traced)");
             HipCheck(hipEventCreateWithFlags(&q.exchanged, hipEventDisableTiming), "hipEventCreate(exchanged)");
             HipCheck(hipEventCreateWithFlags(&q.drained, hipEventDisableTiming), "hipEventCreate(drained)");
@@ -1042,9 +1022,6 @@ void FrameEngine::Release() noexcept {
             if (q.stream != nullptr && !StreamDrain(q.stream, t)) {
                 drained = false;
             }
-            if (q.shade != nullptr && !StreamDrain(q.shade, t)) {
-                drained = false;
-            }
         }
         if (dp->comm != nullptr && drained && !StreamDrain(dp->comm, t)) {
             drained = false;
@@ -1082,7 +1059,7 @@ void FrameEngine::Release() noexcept {
             (void)hipFree(q.rgba);
             q.send = q.recv = nullptr;
             q.rgba = nullptr;
-            for (hipEvent_t* e : {&q.traced, &q.exchanged, &q.drained, &q.shade_drained}) {
+            for (hipEvent_t* e : {&q.traced, &q.exchanged, &q.drained}) {
                 if (*e != nullptr) {
                     (void)hipEventDestroy(*e);
                     *e = nullptr;
@@ -1091,10 +1068,7 @@ void FrameEngine::Release() noexcept {
             if (q.stream != nullptr) {
                 (void)hipStreamDestroy(q.stream);
             }
-            if (q.shade != nullptr) {
-                (void)hipStreamDestroy(q.shade);
-            }
-            q.stream = q.shade = nullptr;
+            q.stream = nullptr;
         }
         dp->queues.clear();
         (void)hipFree(dp->full);
@@ -1115,13 +1089,6 @@ void FrameEngine::Release() noexcept {
         }
     }
     m_dev.clear();
-}
-
-void FrameEngine::SyncQueue(Queue& q, const char* what) {
-    HipCheck(hipStreamSynchronize(q.stream), what);
-    if (q.shade != nullptr) {
-        HipCheck(hipStreamSynchronize(q.shade), what);
-    }
 }
 
 std::size_t FrameEngine::band_rows(std::size_t local) const { return local < m_dev.size() ? m_dev[local]->rows : 0; }
@@ -1169,7 +1136,7 @@ void FrameEngine::SetInputs(const float* host_offsets, std::size_t count) {
         Device& d = *dp;
         DeviceGuard guard(d.device);
         for (Queue& q : d.queues) {
-            SyncQueue(q, "hipStreamSynchronize(inputs)");
+            HipCheck(hipStreamSynchronize(q.stream), "hipStreamSynchronize(inputs)");
             q.used = false;  // frames of the previous inputs are no longer verifiable / readable
         }
         (void)hipFree(d.full);
@@ -1588,9 +1555,8 @@ void FrameEngine::ShadePhase(std::size_t local, std::size_t b) {
     if (n_self == 0) {
         return;
     }
-    hipStream_t st = q.shade != nullptr ? q.shade : q.stream;
     if (!m_opt.simulate) {
-        HipCheck(hipStreamWaitEvent(st, q.exchanged, 0), "hipStreamWaitEvent(exchanged)");
+        HipCheck(hipStreamWaitEvent(q.stream, q.exchanged, 0), "hipStreamWaitEvent(exchanged)");
     }
     // The compositor's frames in slot order read evenly strided inputs (SetInputs' condition).
     const std::size_t F = m_opt.batch, k0 = b * F;
@@ -1600,7 +1566,7 @@ void FrameEngine::ShadePhase(std::size_t local, std::size_t b) {
     // The compositor's own rows are RGBA already: its band (all-to-all, rotating), or the first
     // m_share classes (share; the received ids start at class m_share).
     const long skip = m_opt.rccl_self || m_share != 0 ? -1 : static_cast<long>(m_plan.BandOf(self, self));
-    q.scene->Shade(FullInput(local, first), reinterpret_cast<const int*>(q.recv), q.rgba, 0, m_height, st, n_self,
+    q.scene->Shade(FullInput(local, first), reinterpret_cast<const int*>(q.recv), q.rgba, 0, m_height, q.stream, n_self,
                    m_split.BufferRows(), m_split.interleaved ? m_split.bands : 0, stride, m_id_planes, skip, m_share,
                    m_split.interleaved ? 0 : m_split.first_rows);
 }
@@ -1675,16 +1641,10 @@ void FrameEngine::RunWorker(std::size_t local, std::size_t b0, std::size_t batch
     // abortable (comm.h), never a bare hipStreamSynchronize behind RCCL.
     for (Queue& q : d.queues) {
         HipCheck(hipEventRecord(q.drained, q.stream), "hipEventRecord(drained)");
-        if (q.shade != nullptr) {
-            HipCheck(hipEventRecord(q.shade_drained, q.shade), "hipEventRecord(shade drained)");
-        }
     }
     HipCheck(hipEventRecord(d.comm_drained, d.comm), "hipEventRecord(comm drained)");
     for (Queue& q : d.queues) {
         CommWaitEvent(q.drained, comm, nc, "render (queue)", m_ctl.get());
-        if (q.shade != nullptr) {
-            CommWaitEvent(q.shade_drained, comm, nc, "render (shading)", m_ctl.get());
-        }
     }
     CommWaitEvent(d.comm_drained, comm, nc, "render (exchange)", m_ctl.get());
     for (std::size_t slot = 0; 2 * slot < d.xev.size(); ++slot) {  // the groups not added yet (drained above)
@@ -1769,7 +1729,7 @@ bool FrameEngine::ReadFrame(std::size_t k, float* host_rgba) {
     }
     DeviceGuard guard(d.device);
     CheckUsable();
-    SyncQueue(q, "hipStreamSynchronize(read frame)");
+    HipCheck(hipStreamSynchronize(q.stream), "hipStreamSynchronize(read frame)");
     const std::size_t frame_floats4 = m_width * m_height * 4;
     HipCheck(hipMemcpy(host_rgba, q.rgba + slot * frame_floats4, frame_floats4 * sizeof(float), hipMemcpyDeviceToHost),
              "hipMemcpy(read frame)");
@@ -1798,7 +1758,7 @@ std::size_t FrameEngine::Verify(std::size_t* checked, std::size_t per_queue) {
                 if (!q.used) {
                     continue;
                 }
-                SyncQueue(q, "hipStreamSynchronize(verify)");
+                HipCheck(hipStreamSynchronize(q.stream), "hipStreamSynchronize(verify)");
                 const std::size_t b = q.last_batch;
                 std::size_t taken = 0;
                 for (std::size_t f = 0; f < F && taken < per_queue; ++f) {
@@ -1861,7 +1821,7 @@ DeviceScene::StageTimes FrameEngine::MeasureStages(std::size_t local, std::size_
     DeviceGuard guard(d.device);
     Queue& q = d.queues[0];
     for (Queue& qq : d.queues) {
-        SyncQueue(qq, "hipStreamSynchronize(stages)");
+        HipCheck(hipStreamSynchronize(qq.stream), "hipStreamSynchronize(stages)");
     }
     HipCheck(hipStreamSynchronize(d.comm), "hipStreamSynchronize(stages)");
     q.scene->TakeTimes();

@@ -253,7 +253,6 @@ private:
     void ExchangePhase(std::size_t local, std::size_t b);  // RCCL: inside a group
     double SentBytes(std::size_t local, std::size_t b) const;  // ids device `local` sends for batch b
     void CopyPhase(std::size_t local, std::size_t b);      // device-copy exchange
-    static void SyncQueue(Queue& q, const char* what);     // the queue's streams (trace, shading)
     hipEvent_t* ExchangeEvents(std::size_t local);          // the next timing pair (a bounded ring)
     void AddExchangeTime(std::size_t local, std::size_t slot);  // wait for a pair, add its time
     void ShadePhase(std::size_t local, std::size_t b);
