@@ -258,6 +258,40 @@ def run_leg(job, a, path, inputs, steps, warmup, **kw):
         eng.close()
 
 
+def c5_leg(job, a, steps=10, warmup=2, batch=64):
+    """BASELINE config C5 on this GPU: the 1M-triangle soup (seed 0x5EED + 1) at 3840 x 2160, the
+    headline's frame loop (8-frame launches, 2 queues, 64-frame steps), with a roofline block of its own
+    for the trace kernel in that launch shape (one launch in flight, HIP events on its dispatch) and the
+    whole-frame figure. (C5 proper is 8 GPUs: SCALE runs it; this is its one-GPU leg.)"""
+    import copy
+
+    a5 = copy.copy(a)
+    a5.width, a5.height, a5.triangles, a5.frames_per_step = 3840, 2160, 1_000_000, batch
+    path = job.scene_path("soup", 1_000_000)
+    wl = workload_name(a5)
+    eng = job.engine(path, a5, batch=batch, width=a5.width, height=a5.height)
+    try:
+        eng.set_inputs(make_offsets(a5, a.offsets, 1))
+        el, mr = timed(job, eng, steps, warmup)
+        launch_frames = frames_per_launch(a5, 1)
+        st = eng.stage_times(0, 24, launch_frames)
+        bad, checked = eng.verify()
+    finally:
+        eng.close()
+    import simpleraytracer_amd as srt
+
+    n_tri = srt.scene_triangles(path)
+    ms_frame = el / (steps * batch) * 1e3
+    roof, _, _ = roofline_fields(wl, a.variant, a5.width * a5.height, launch_frames, n_tri, st[3], False, 1.0,
+                                 profile_key(wl, a.variant, 1, a.rows, launch_frames), a.offsets != "uniform",
+                                 f"C5 launch shape ({launch_frames} frames per launch), one launch in flight, {st[0]} "
+                                 "launches, HIP events bound to the kernel's dispatch")
+    return {"workload": wl, "mrays_per_s": round(mr, 3), "ms_per_frame": round(ms_frame, 6), "frames_per_step": batch,
+            "steps": steps, "roofline": roof, "whole_frame": whole_frame_fields(a5.width, a5.height, n_tri, ms_frame, 1),
+            "stages_ms": {"bin": round(st[2], 5), "trace_kernel": round(st[3], 5), "frames_per_launch": launch_frames},
+            "verified": bad == 0 and checked > 0}
+
+
 def cpu_binned(scene_path, a, threads, seconds, oracle_rows=None):
     """The product's own CPU render path -- the backend the GPU path drops in for: mlInfer with
     ML_VISIBLE_DEVICES=cpu (csrc/cpu_render.cpp: records binned to 16 x 16 pixel tiles, the kernels'
@@ -708,6 +742,11 @@ def main():
         if a.scene == "soup":
             legs["c2_cornell"] = {**run_leg(job, a, job.scene_path("cornell"), inputs, min(a.steps, 60), a.warmup),
                                   "workload": workload_name(a, "cornell")}
+        if a.scene == "soup" and a.triangles == 100_000 and (W, H) == (1920, 1080):
+            try:
+                legs["c5_one_gpu"] = c5_leg(job, a)
+            except Exception as exc:  # noqa: BLE001 -- the primary line must still be printed
+                legs["c5_one_gpu"] = {"error": f"{type(exc).__name__}: {exc}"}
         if a.brute_steps > 0 and a.variant != "lds":
             e = job.engine(path, a, variant="lds", queues=1, batch=1)
             e.set_inputs(inputs)
