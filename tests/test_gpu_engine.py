@@ -186,6 +186,24 @@ def test_engine_rotated_two_device_stage_times_whole_batch(gpu, scenes, monkeypa
             assert n == 2 and trace > 0
 
 
+@pytest.mark.parametrize("queues", [1, 2, 3])
+def test_engine_exchange_timing_counts_every_group(gpu, scenes, queues):
+    """srtEngineExchangeStats: every batch's exchange group is timed, through a bounded ring of 2 Q + 2
+    event pairs (a new pair per batch, kept until release) -- a run of more batches than the
+    ring reports one group per batch, a positive mean and the bytes a device sends per batch; a second
+    run reports its own groups only."""
+    w, h, F = 130, 100, 4
+    with engine(scenes["soup2k"], w, h, devices=[0, 0], rows="rotated", exchange="alltoall", queues=queues,
+                batch=F) as e:
+        e.set_inputs(random_inputs(F, h, w, seed=83))
+        for batches in (2 * queues + 7, 3):
+            e.run(batches)
+            for local in (0, 1):
+                st = e.exchange_stats(local)
+                assert st["groups"] == batches and st["ms_mean"] > 0 and st["bytes_sent"] > 0, (batches, st)
+        assert e.verify()[0] == 0
+
+
 def test_engine_rotated_needs_alltoall(gpu, scenes):
     from simpleraytracer_amd.device import SrtError
 
