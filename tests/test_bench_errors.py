@@ -63,3 +63,26 @@ def test_bench_ml_multi_child_process(gpu, scenes):
         assert out[mode]["mrays_per_s"] > 0 and out[mode]["devices"] == [0, 0], out
     late = bench.ml_multi_child(scenes["soup2k"], 320, 200, [0, 0], timeout_s=0.01)
     assert "did not finish" in late["error"], late
+
+
+def test_cpu_baseline_times_the_binned_cpu_path_beside_the_oracle(tmp_path):
+    """bench.cpu_baseline (every line, N = 1 and N > 1): the brute-force oracle over a row sample and,
+    beside it, the product's own CPU render path (ML_VISIBLE_DEVICES=cpu: screen-box binning, the exact
+    test) over whole frames, its ids checked against the oracle's rows; cores / model / host CPUs stated.
+    The environment it sets for the binned path is restored afterwards."""
+    import types
+
+    sys.path.insert(0, str(REPO))
+    import bench
+    import simpleraytracer_amd as srt
+
+    path = srt.write_scene(str(tmp_path / "soup.srt"), "soup", 3000, seed=7)
+    a = types.SimpleNamespace(width=96, height=48, scene="soup", triangles=3000, cpu_seconds=0.5)
+    before = {k: os.environ.get(k) for k in ("ML_VISIBLE_DEVICES", "SRT_CPU_THREADS")}
+    out = bench.cpu_baseline(path, a)
+    assert {k: os.environ.get(k) for k in before} == before
+    b = out["binned"]
+    assert "error" not in b, b
+    assert b["value"] > 0 and b["cores"] >= 1 and b["frames"] >= 1 and b["parity_vs_oracle"] is True, b
+    assert out["value"] > 0 and out["cores"] >= 1 and out["kind"] == "port" and out["host_cpus"] >= 1
+    assert b["value"] > out["value"]  # binning against brute force on the same rows
