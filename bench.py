@@ -258,18 +258,22 @@ def run_leg(job, a, path, inputs, steps, warmup, **kw):
         eng.close()
 
 
-def c5_leg(job, a, steps=10, warmup=2, batch=64):
-    """BASELINE config C5 on this GPU: the 1M-triangle soup (seed 0x5EED + 1) at 3840 x 2160, the
-    headline's frame loop (8-frame launches, 2 queues, 64-frame steps), with a roofline block of its own
-    for the trace kernel in that launch shape (one launch in flight, HIP events on its dispatch) and the
-    whole-frame figure. (C5 proper is 8 GPUs: SCALE runs it; this is its one-GPU leg.)"""
+def c5_leg(job, a, steps=10, warmup=2, batch=64, queues=1, launch=16):
+    """BASELINE config C5 on this GPU: the 1M-triangle soup (seed 0x5EED + 1) at 3840 x 2160 in 64-frame
+    steps, with a roofline block of its own for the trace kernel in the leg's launch shape (one launch in
+    flight, HIP events on its dispatch) and the whole-frame figure. Frame loop: one queue of 16-frame
+    launches -- at 4K a record / bin launch and a trace launch each fill the chip, so a second queue only
+    contends (three alternating rounds, profiles/r06/c5_ab/: 59 111 - 59 335 against 57 925 - 58 271
+    Mrays/s with the headline's 2 queues x 8 frames). (C5 proper is 8 GPUs: SCALE runs it; this is its
+    one-GPU leg.)"""
     import copy
 
     a5 = copy.copy(a)
     a5.width, a5.height, a5.triangles, a5.frames_per_step = 3840, 2160, 1_000_000, batch
+    a5.queues, a5.launch = queues, launch
     path = job.scene_path("soup", 1_000_000)
     wl = workload_name(a5)
-    eng = job.engine(path, a5, batch=batch, width=a5.width, height=a5.height)
+    eng = job.engine(path, a5, batch=batch, width=a5.width, height=a5.height, queues=queues)
     try:
         eng.set_inputs(make_offsets(a5, a.offsets, 1))
         el, mr = timed(job, eng, steps, warmup)
@@ -287,7 +291,7 @@ def c5_leg(job, a, steps=10, warmup=2, batch=64):
                                  f"C5 launch shape ({launch_frames} frames per launch), one launch in flight, {st[0]} "
                                  "launches, HIP events bound to the kernel's dispatch")
     return {"workload": wl, "mrays_per_s": round(mr, 3), "ms_per_frame": round(ms_frame, 6), "frames_per_step": batch,
-            "steps": steps, "roofline": roof, "whole_frame": whole_frame_fields(a5.width, a5.height, n_tri, ms_frame, 1),
+            "queues": queues, "steps": steps, "roofline": roof, "whole_frame": whole_frame_fields(a5.width, a5.height, n_tri, ms_frame, 1),
             "stages_ms": {"bin": round(st[2], 5), "trace_kernel": round(st[3], 5), "frames_per_launch": launch_frames},
             "verified": bad == 0 and checked > 0}
 

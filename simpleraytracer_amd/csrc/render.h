@@ -21,8 +21,6 @@ namespace srt {
 // multiple of kPadTriangles (the largest cull step: 256 threads x 16 records) so no trace
 // loop has a tail; the per-ray variants stop after the last tile holding a real record.
 constexpr int kTileTriangles = 256;
-// Records per block of the bin kernel (render.hip kBinThreads): the unit of the band skip hint.
-constexpr int kBinBlockRecords = 256;
 constexpr int kPadTriangles = 4096;
 
 // Edge records, tile-planar: tile t (256 records, 10 KiB) = four planes, each indexed by the
@@ -300,6 +298,9 @@ hipError_t LaunchCullFrames(const CullFrame* frames, std::size_t count, std::uin
 // Screen-box y extent of every 256-position block of the spatial order under `frame` (records computed
 // as the bin kernel computes them; n_pad / 256 float2 into d_ext): the band record pass's skip hint,
 // keyed to (scene, camera, W x H) like the spatial order itself.
+// Block extents LaunchBlockExtents writes for n triangles (one per bin block of the record pass:
+// render.hip kBinThreads records each): the size of its d_ext.
+std::size_t BlockExtentCount(std::uint64_t n);
 hipError_t LaunchBlockExtents(const float* d_svertices, std::uint64_t n, const Frame& frame, float2* d_ext,
                               hipStream_t stream);
 hipError_t LaunchShadeTable(const float* d_vertices, const float* d_albedo, std::uint64_t n, float* d_table,

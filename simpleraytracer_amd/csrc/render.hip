@@ -1615,8 +1615,11 @@ __device__ __forceinline__ void PacketBatch(CullShared& sh, const Box& bb, const
 // of the tile, so the frame stays bit-identical to brute force. A tile whose box is outside
 // the screen-box range, or whose list overflowed, streams every record instead.
 // ---------------------------------------------------------------------------------------
-constexpr int kBinThreads = 256;
-static_assert(kBinThreads == kBinBlockRecords, "one bin block per skip-hint block (render.h)");
+#ifndef SRT_BIN_THREADS
+#define SRT_BIN_THREADS 256
+#endif
+constexpr int kBinThreads = SRT_BIN_THREADS;  // records per bin block = the band skip hint's unit (BlockExtentCount)
+static_assert(kBinThreads % kWave == 0 && kPadTriangles % kBinThreads == 0, "bin block shape");
 #ifndef SRT_LARGE_TILES
 #define SRT_LARGE_TILES 16
 #endif
@@ -3844,6 +3847,10 @@ hipError_t LaunchTrace(const float* d_edges, std::uint64_t n, const float* d_ver
         Launch(TraceLdsKernel, dim3(gx, gy), dim3(kWave * kLdsWaves), stream, ev.begin, ev.end, p);
     }
     return hipGetLastError();
+}
+
+std::size_t BlockExtentCount(std::uint64_t n) {
+    return static_cast<std::size_t>((PaddedTriangleCount(n) + kBinThreads - 1) / kBinThreads);
 }
 
 hipError_t LaunchBlockExtents(const float* d_svertices, std::uint64_t n, const Frame& frame, float2* d_ext,

@@ -224,7 +224,7 @@ void DeviceScene::EnsureBlockExtents(hipStream_t stream) const {
         return;
     }
     if (m_block_ext == nullptr) {
-        m_block_ext = DeviceAlloc<float2>(PaddedTriangleCount(m_n) / kBinBlockRecords, "hipMalloc(block extents)");
+        m_block_ext = DeviceAlloc<float2>(BlockExtentCount(m_n), "hipMalloc(block extents)");
     }
     HipCheck(LaunchBlockExtents(m_svertices, m_n, m_frame, m_block_ext, stream), "block extents launch");
     m_ext_pending = false;
