@@ -464,7 +464,8 @@ def roofline_fields(wl, variant, launch_rays, launch_frames, n_tri, kernel_ms, b
         "measured_in": measured_in,
         "profile_key": key,
         "note": f"algorithmic bytes per frame = rays x ({off_bytes} B offsets read by the trace + {out_bytes} B out) + "
-                f"cull records x 64 B{'' if height_frac == 1 else ' x the band share of the rows'}; offsets count "
+                f"cull records x 64 B (stored: the 64-B record; recomputed, one-queue engines: 48 B of spatial "
+                f"inputs + the 16-B screen box){'' if height_frac == 1 else ' x the band share of the rows'}; offsets count "
                 "only where the trace loads them (irregular tiles); traffic = measured HBM bytes per launch of this "
                 "launch shape (rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE, profiles/pmc_traffic.json), null when no "
                 "committed pass matches it",

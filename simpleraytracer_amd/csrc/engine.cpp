@@ -759,6 +759,8 @@ void FrameEngine::AllocateQueues() {
             HipCheck(hipEventCreateWithFlags(&q.exchanged, hipEventDisableTiming), "hipEventCreate(exchanged)");
             HipCheck(hipEventCreateWithFlags(&q.drained, hipEventDisableTiming), "hipEventCreate(drained)");
             q.scene = std::make_unique<DeviceScene>(*m_scene, d.device);
+            // one queue: nothing overlaps a batch's bin launches, so the trace recomputes the records
+            q.scene->SetRecordMode(m_opt.queues == 1 ? kRecordsRecompute : kRecordsAuto);
             q.scene->Prepare(m_width, m_height, q.stream);
             if (m_exchange) {
                 const std::size_t send_frames =

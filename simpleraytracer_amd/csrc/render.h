@@ -22,6 +22,9 @@ namespace srt {
 // loop has a tail; the per-ray variants stop after the last tile holding a real record.
 constexpr int kTileTriangles = 256;
 constexpr int kPadTriangles = 4096;
+// Floats per position of the scene's spatial-order record inputs (DeviceScene svertices): the 9
+// vertex coordinates, the record id's bits, two zero words -- 48 B, three 16-B loads.
+constexpr int kSpatialStride = 12;
 
 // Edge records, tile-planar: tile t (256 records, 10 KiB) = four planes, each indexed by the
 // record's position j in the tile, so a lane-per-record load is one coalesced 16-B or 4-B
@@ -183,7 +186,16 @@ struct CullBins {
     unsigned capacity;
     std::size_t tiles;
     bool plan = true;      // (re)build the slot's work plan with this frame (else the trace uses the last one)
+    // Records recomputed by the trace (render.hip TraceRecords<true>): the bin launch writes a 16-B
+    // screen box per position instead of the 64-B cull record, the trace rebuilds the record from the
+    // scene's 48-B spatial inputs. Same frame bit for bit; trades bin-launch bytes for trace VALU, so
+    // it pays where the bin launch is on the critical path (one frame queue, one-frame launches).
+    // One value for every frame of a launch.
+    bool recompute = false;
 };
+// Which records a DeviceScene's binned traces read (DeviceScene::SetRecordMode; env SRT_TRACE_RECORDS
+// = stored | recompute | auto overrides): auto = recomputed for one-frame launches, stored otherwise.
+enum RecordMode : int { kRecordsAuto = 0, kRecordsStored = 1, kRecordsRecompute = 2 };
 
 // Tiles (64 x 32 rays) of a width x row_count band.
 std::size_t CullTiles(std::size_t width, std::size_t row_count);

@@ -100,6 +100,7 @@ struct TraceParams {
     const TileInfo* __restrict__ tile_info;   // per tile: ray box, uniform offset (TileInfoKernel)
     const CullRecord* __restrict__ cull;      // cull records in spatial order (the lists hold positions)
     const unsigned* __restrict__ order;       // spatial-order position -> record id
+    const float* __restrict__ svertices;      // vertices by spatial-order position (binned trace: records recomputed)
     const uint4* __restrict__ work;           // tile parts (2 x uint4 each), most work first (BuildWorkOrder)
     const unsigned* __restrict__ work_count;  // [0]: tile parts listed
     unsigned long long* __restrict__ split_keys;  // key slices of split parts: one per split slot, kBlockRows x 64 each
@@ -1644,6 +1645,7 @@ struct BinParams {
     unsigned n;
     unsigned exp;  // diagnostic build: experiment bits (env SRT_EXP), 0 in the product
     unsigned fused;  // tile info computed in the bin launch (CullFusedInfo): bins assume offsets in [0, 1]
+    unsigned recompute;  // CullBins::recompute: screen boxes by position instead of cull records
     int tiles_x;
     int tiles_y;
     int width;
@@ -2044,7 +2046,7 @@ __global__ __launch_bounds__(kBinThreads) void BlockExtentKernel(PrepareParams p
         const bool real = i < pp.n;
         float c[9], vol;
         float4 sb;
-        ComputeRecord(pp, pp.svertices + 9ull * (real ? i : 0u), real, c, vol, sb);
+        ComputeRecord(pp, pp.svertices + static_cast<size_t>(kSpatialStride) * (real ? i : 0u), real, c, vol, sb);
         lo = sb.z == sb.z ? sb.z : -__builtin_inff();
         hi = sb.w == sb.w ? sb.w : __builtin_inff();
     }
@@ -2128,8 +2130,9 @@ __global__ __launch_bounds__(kBinThreads) void PrepareBinKernel(const Frames bat
     const bool real = i < pp.n;
     float c[9], vol = 0.f;
     float4 sb = make_float4(__builtin_inff(), -__builtin_inff(), __builtin_inff(), -__builtin_inff());
-    const unsigned id = real ? pp.order[i] : i;
-    const float* v = pp.svertices + 9ull * (real ? i : 0u);  // by position: no order -> vertex chain
+    // by position (render.h kSpatialStride): the vertices and the id, no order -> vertex chain
+    const float* v = pp.svertices + static_cast<size_t>(kSpatialStride) * (real ? i : 0u);
+    const unsigned id = real ? __float_as_uint(v[9]) : i;
     BoxSolve bs;
     bool xpend = false;
     if (i < pp.n_pad) {
@@ -2171,7 +2174,9 @@ __global__ __launch_bounds__(kBinThreads) void PrepareBinKernel(const Frames bat
             }
         }
         pp.qboxes[i] = QuantizeBox(sb);
-        if (needed) {
+        if (needed && p.recompute != 0u) {
+            pp.screen_boxes[i] = sb;  // by position: the trace recomputes the rest (TraceRecords<true>)
+        } else if (needed) {
             CullRecord r;
             r.a = make_float4(c[0], c[1], c[2], c[3]);
             r.b = make_float4(c[4], c[5], c[6], c[7]);
@@ -2201,6 +2206,16 @@ __global__ __launch_bounds__(kBinThreads) void PrepareBinKernel(const Frames bat
         h = max(r1 - r0 + 1, 0);
         if (w * h > kLargeTiles && !SRT_EXP_BIT(p, 2u)) {
             p.large_list[atomicAdd(&p.counts[tiles], 1u)] = i;
+            if (p.recompute != 0u) {
+                // the whole record of a large-list entry: the empty tests read it (WorkOrderKernel,
+                // plan-only traces)
+                CullRecord r;
+                r.a = make_float4(c[0], c[1], c[2], c[3]);
+                r.b = make_float4(c[4], c[5], c[6], c[7]);
+                r.x = make_float4(c[8], vol, __uint_as_float(id), 0.f);
+                r.sb = sb;
+                pp.cull[i] = r;
+            }
         }
     }
     const bool listed = w * h > 0 && w * h <= kLargeTiles && !SRT_EXP_BIT(p, 2u);
@@ -2543,9 +2558,54 @@ std::size_t OrderLdsBytes(int tiles) { return static_cast<std::size_t>(tiles) * 
 #define SRT_TRACE_OCC 6
 #endif
 
-template <class Frames>
+// Where a trace block's candidate records come from. RC = false: the 64-B cull record by position
+// (written by the record pass: LaunchPrepare, or the bin kernel of a stored-record launch).
+// RC = true (a binned launch with CullBins::recompute): the bin kernel writes only the screen box
+// by position, and the trace recomputes the edge coefficients and vol from the vertices by position
+// with the record pass's own ComputeEdges under the same frame vectors -- the same bits -- and
+// takes the id from the spatial order (a padding position is its own id, >= n: a disabled record).
+struct RawRecord {
+    float v[9];
+    unsigned id;
+    float4 sb;
+};
+template <bool RC>
+struct TraceRecords {
+    using Raw = CullRecord;
+    static __device__ __forceinline__ Raw Load(const TraceParams& p, unsigned pos) { return p.cull[pos]; }
+    static __device__ __forceinline__ CullRecord Make(const TraceParams&, const Raw& r) { return r; }
+};
+template <>
+struct TraceRecords<true> {
+    using Raw = RawRecord;
+    static __device__ __forceinline__ Raw Load(const TraceParams& p, unsigned pos) {
+        Raw r;
+        const bool real = pos < p.n;
+        const float4* v = reinterpret_cast<const float4*>(p.svertices + static_cast<size_t>(kSpatialStride) * (real ? pos : 0u));
+        const float4 v0 = v[0], v1 = v[1], v2 = v[2];
+        r.v[0] = v0.x, r.v[1] = v0.y, r.v[2] = v0.z, r.v[3] = v0.w;
+        r.v[4] = v1.x, r.v[5] = v1.y, r.v[6] = v1.z, r.v[7] = v1.w;
+        r.v[8] = v2.x;
+        r.id = real ? __float_as_uint(v2.y) : pos;
+        r.sb = p.screen_boxes[pos];
+        return r;
+    }
+    static __device__ __forceinline__ CullRecord Make(const TraceParams& p, const Raw& r) {
+        float c[9], vol;
+        ComputeEdges(p.eye, p.base, p.du, p.dv, r.v, r.id < p.n, c, vol);
+        CullRecord cr;
+        cr.a = make_float4(c[0], c[1], c[2], c[3]);
+        cr.b = make_float4(c[4], c[5], c[6], c[7]);
+        cr.x = make_float4(c[8], vol, __uint_as_float(r.id), 0.f);
+        cr.sb = r.sb;
+        return cr;
+    }
+};
+
+template <class Frames, bool RC = false>
 __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(const Frames batch) {
     const TraceParams& p = batch[blockIdx.z];
+    using Recs = TraceRecords<RC>;
     constexpr int R = kCullR;
     __shared__ CullShared sh;
 #ifdef SRT_DIAG
@@ -2702,7 +2762,7 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(c
     // LIST: the first batch's records are requested before the rays are set up (its loads
     // are the block's longest dependency chain: list entry, then the 64-B record).
     const unsigned total = src.end - src.begin;
-    CullRecord nxt[kSlices];
+    typename Recs::Raw nxt[kSlices];
     // The list entries run one batch ahead of the records: batch b's prefetch loads batch b + 1's
     // records from entries that arrived during batch b - 1's walk, then requests batch b + 2's
     // entries (one load chain per batch no longer waits in front of the walk).
@@ -2721,7 +2781,7 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(c
 #pragma unroll
         for (int e = 0; e < kSlices; ++e) {
             if (InBatch(e, tid)) {
-                nxt[e] = p.cull[nid[e]];
+                nxt[e] = Recs::Load(p, nid[e]);
             }
         }
     };
@@ -2801,7 +2861,7 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(c
             bool valid[kSlices];
 #pragma unroll
             for (int e = 0; e < kSlices; ++e) {
-                cr[e] = nxt[e];
+                cr[e] = Recs::Make(p, nxt[e]);
                 valid[e] = InBatch(e, tid) && b0 + e * kCullThreads + tid < total;
             }
             PacketBatch(sh, bb, pf, cr, valid, pk_buf, [&] {
@@ -2879,7 +2939,7 @@ __global__ __launch_bounds__(kCullThreads, SRT_TRACE_OCC) void TraceCullKernel(c
 #pragma unroll
                 for (int e = 0; e < kSlices; ++e) {
                     valid[e] = InBatch(e, tid) && b0 + e * kCullThreads + tid < listed;
-                    cr[e] = p.cull[my_ids[bi][e]];
+                    cr[e] = Recs::Make(p, Recs::Load(p, my_ids[bi][e]));
                 }
                 PacketBatch(sh, bb, pf, cr, valid, pk_buf, [] {});
                 pk_buf ^= 1u;
@@ -3617,6 +3677,7 @@ BinParams BindBins(TraceParams& p, const CullBins& bins, std::uint64_t n) {
     b.exp = p.exp;
     p.tile_info = b.tile_info;
     p.order = bins.order;
+    p.svertices = bins.svertices;
     p.work = b.work;
     p.work_count = b.work_count;
     p.split_keys = static_cast<unsigned long long*>(bins.split_keys);
@@ -3637,7 +3698,8 @@ namespace {
 // kernel arguments (FrameArgs) or a device table (FrameTable).
 template <class TB, class BB, class PB>
 void LaunchCullStages(const TB& tb, const BB& bb, const PB& pb, unsigned z, unsigned gx, unsigned gy, unsigned blocks,
-                      bool fused, bool order, unsigned descs, hipStream_t stream, const StageEvents& ev) {
+                      bool fused, bool order, bool recompute, unsigned descs, hipStream_t stream,
+                      const StageEvents& ev) {
     if (!fused) {
         Launch(TileInfoKernel<BB>, dim3(gx, (gy + kInfoTiles - 1) / kInfoTiles, z), dim3(kBinThreads), stream,
                ev.prep_begin, ev.prep_end, bb);
@@ -3652,12 +3714,20 @@ void LaunchCullStages(const TB& tb, const BB& bb, const PB& pb, unsigned z, unsi
                   order ? nullptr : ev.bin_end, pb);
     }
     if (!order) {  // the slots' plans are current: the trace follows the bins
-        Launch(TraceCullKernel<TB>, dim3(descs, 1, z), dim3(kWave * kCullWaves), stream, ev.begin, ev.end, tb);
+        if (recompute) {
+            Launch(TraceCullKernel<TB, true>, dim3(descs, 1, z), dim3(kWave * kCullWaves), stream, ev.begin, ev.end, tb);
+        } else {
+            Launch(TraceCullKernel<TB, false>, dim3(descs, 1, z), dim3(kWave * kCullWaves), stream, ev.begin, ev.end, tb);
+        }
         return;
     }
     LaunchLds(WorkOrderKernel<BB>, dim3((gx * gy + kOrderBlock - 1) / kOrderBlock, 1, z), dim3(kOrderBlock),
               OrderLdsBytes(static_cast<int>(gx * gy)), stream, nullptr, ev.bin_end, bb);
-    Launch(TraceCullKernel<TB>, dim3(descs, 1, z), dim3(kWave * kCullWaves), stream, ev.begin, ev.end, tb);
+    if (recompute) {
+        Launch(TraceCullKernel<TB, true>, dim3(descs, 1, z), dim3(kWave * kCullWaves), stream, ev.begin, ev.end, tb);
+    } else {
+        Launch(TraceCullKernel<TB, false>, dim3(descs, 1, z), dim3(kWave * kCullWaves), stream, ev.begin, ev.end, tb);
+    }
 }
 
 // Layout of a parameter table (CullTableBytes): PrepareBinParams, BinParams, TraceParams arrays.
@@ -3725,7 +3795,8 @@ hipError_t LaunchCullFrames(const CullFrame* frames, std::size_t count, std::uin
             f.band.width != band0.width ||
             f.band.row_count != band0.row_count || (fused && f.band.row_begin != band0.row_begin) ||
             f.band.row_interleave != band0.row_interleave ||
-            f.band.height != band0.height || f.bins->descs != frames[0].bins->descs) {
+            f.band.height != band0.height || f.bins->descs != frames[0].bins->descs ||
+            f.bins->recompute != frames[0].bins->recompute) {
             return hipErrorInvalidValue;  // one band shape per batch (its first row may differ per frame)
         }
         tp[i] = MakeTraceParams(f.edges, n, d_vertices, d_shade, frame, background, f.band);
@@ -3734,6 +3805,7 @@ hipError_t LaunchCullFrames(const CullFrame* frames, std::size_t count, std::uin
         }
         bp[i] = BindBins(tp[i], *f.bins, n);
         bp[i].fused = fused ? 1u : 0u;
+        bp[i].recompute = f.bins->recompute ? 1u : 0u;
         tp[i].fused = bp[i].fused;
         order = order || f.bins->plan;
         pp[i].prep = MakePrepareParams(d_vertices, d_rank, n, frame, const_cast<float*>(f.edges));
@@ -3757,7 +3829,7 @@ hipError_t LaunchCullFrames(const CullFrame* frames, std::size_t count, std::uin
     const unsigned blocks = (pp[0].prep.n_pad + kBinThreads - 1) / kBinThreads + (fused ? info_blocks : 0u);
     const unsigned descs = frames[0].bins->descs;
     if (!use_table) {
-        LaunchCullStages(tb, bb, pb, z, gx, gy, blocks, fused, order, descs, stream, ev);
+        LaunchCullStages(tb, bb, pb, z, gx, gy, blocks, fused, order, frames[0].bins->recompute, descs, stream, ev);
         return hipGetLastError();
     }
     // One upload of every frame's parameters, then the same four launches reading them from it.
@@ -3781,7 +3853,7 @@ hipError_t LaunchCullFrames(const CullFrame* frames, std::size_t count, std::uin
     const PrepareBinTable pt{(ConstantPtr<PrepareBinParams>)(dev + lay.prep)};
     const BinTable bt{(ConstantPtr<BinParams>)(dev + lay.bin)};
     const TraceTable tt{(ConstantPtr<TraceParams>)(dev + lay.trace)};
-    LaunchCullStages(tt, bt, pt, z, gx, gy, blocks, fused, order, descs, stream, ev);
+    LaunchCullStages(tt, bt, pt, z, gx, gy, blocks, fused, order, frames[0].bins->recompute, descs, stream, ev);
     return hipGetLastError();
 }
 

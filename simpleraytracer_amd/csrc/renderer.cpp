@@ -111,7 +111,7 @@ DeviceScene::DeviceScene(const Scene& scene, int device)
         m_edges = DeviceAlloc<float>(PaddedTriangleCount(m_n) * kEdgeFloatsPerTriangle, "hipMalloc(edges)");
         m_order = DeviceAlloc<unsigned>(m_n == 0 ? 1 : m_n, "hipMalloc(order)");
         m_rank = DeviceAlloc<unsigned>(m_n == 0 ? 1 : m_n, "hipMalloc(rank)");
-        m_svertices = DeviceAlloc<float>(m_n == 0 ? 9 : m_n * 9, "hipMalloc(spatial vertices)");
+        m_svertices = DeviceAlloc<float>((m_n == 0 ? 1 : m_n) * kSpatialStride, "hipMalloc(spatial vertices)");
         HipCheck(hipMemcpy(m_vertices, scene.vertices.data(), m_n * 9 * sizeof(float), hipMemcpyHostToDevice),
                  "hipMemcpy(vertices)");
         // The records' spatial order, built on the device (spatial.hip), timed.
@@ -488,8 +488,10 @@ void DeviceScene::TraceBatch(const float* const* d_offsets, float* const* d_rgba
     // The trace grid for the whole batch: its frames' parts together fill the chip sooner (a
     // 135-row band alone splits 5 ways; eight of them do not need to).
     const unsigned batch_descs = CullDescriptors(CullTiles(m_width, row_count), frames);
+    const bool recompute = RecomputeRecords(frames);
     for (std::size_t f = 0; f < frames; ++f) {
         bins[f] = CullSlot(f, row_count, batch_descs);
+        bins[f].recompute = recompute;
         cf[f].edges = m_edges + f * floats;
         cf[f].bins = &bins[f];
         cf[f].band = BandArgs{d_offsets[f], d_rgba != nullptr ? d_rgba[f] : nullptr, m_width, m_height,
@@ -538,6 +540,7 @@ void DeviceScene::Trace(const float* d_offsets, float* d_rgba, std::size_t row_b
         EnsureCullWork(1, row_count, stream);
         EnsureBlockExtents(stream);
         bins = CullSlot(0, row_count);
+        bins.recompute = RecomputeRecords(1);
         use_bins = &bins;
     }
     if (variant == kTraceBvh && m_bvh == nullptr && row_count != 0) {
@@ -597,6 +600,45 @@ hipEvent_t DeviceScene::TimingEvent(std::vector<hipEvent_t>& pool, std::size_t i
 
 void DeviceScene::SetTiming(bool on) {
     m_timing = on;
+}
+
+namespace {
+// SRT_TRACE_RECORDS: stored | recompute | auto (render.h RecordMode); -1 when unset. Read per launch
+// (like SRT_CULL_BIN), so a process can compare the modes.
+int RecordModeFromEnv() {
+    const char* e = std::getenv("SRT_TRACE_RECORDS");
+    if (e == nullptr || *e == '\0') {
+        return -1;
+    }
+    const std::string v(e);
+    if (v == "auto") {
+        return static_cast<int>(kRecordsAuto);
+    }
+    if (v == "stored") {
+        return static_cast<int>(kRecordsStored);
+    }
+    if (v == "recompute") {
+        return static_cast<int>(kRecordsRecompute);
+    }
+    throw std::runtime_error("SRT_TRACE_RECORDS must be stored, recompute or auto, got '" + v + "'");
+}
+}  // namespace
+
+void DeviceScene::SetRecordMode(int mode) {
+    if (mode != kRecordsAuto && mode != kRecordsStored && mode != kRecordsRecompute) {
+        throw std::runtime_error("SetRecordMode: unknown record mode " + std::to_string(mode));
+    }
+    m_records = mode;
+}
+
+// Whether a binned launch of `frames` frames has its trace recompute the records: the bin launch
+// then writes 16 B per record instead of 64, which shortens it by a fifth, and the trace rebuilds each
+// candidate's record (~5 % longer). It pays where the bin launch is on the critical path: a launch of one
+// frame, or an engine with one frame queue (nothing overlaps its bin launches).
+bool DeviceScene::RecomputeRecords(std::size_t frames) const {
+    const int env = RecordModeFromEnv();
+    const int mode = env >= 0 ? env : m_records;
+    return mode == kRecordsRecompute || (mode == kRecordsAuto && frames == 1);
 }
 
 DeviceScene::StageTimes DeviceScene::TakeTimes() {

@@ -118,6 +118,9 @@ public:
     };
     void SetTiming(bool on);
     StageTimes TakeTimes();
+    // Records of the binned traces (render.h RecordMode; the env SRT_TRACE_RECORDS overrides it):
+    // the frame engine sets kRecordsRecompute when it keeps one frame queue per device.
+    void SetRecordMode(int mode);
 
 private:
     int m_device;
@@ -196,6 +199,8 @@ private:
     hipEvent_t TimingEvent(std::vector<hipEvent_t>& pool, std::size_t i) const;
     StageEvents BindStageEvents(bool prep, bool staged) const;
     bool m_timing = false;
+    int m_records = 0;  // render.h RecordMode (kRecordsAuto)
+    bool RecomputeRecords(std::size_t frames) const;
     // Calls on one scene are stream-ordered: the per-frame edge records and the cull work buffer
     // are shared state, so a call on another stream than the previous one first waits for it.
     void OrderAfterPrevious(hipStream_t stream) const;

@@ -57,8 +57,9 @@ __global__ __launch_bounds__(256) void MortonKeysKernel(const float* __restrict_
     }
 }
 
-// rank[order[i]] = i; svertices[i] = vertices[order[i]] (the bin kernel's record pass reads
-// the vertices by spatial position: coalesced, and no order -> vertex load chain per frame).
+// rank[order[i]] = i; svertices[i] = (vertices[order[i]], order[i] bits, 0, 0) (render.h kSpatialStride:
+// the bin kernel's record pass and the trace read a record's inputs by spatial position, three 16-B
+// loads: coalesced, and no order -> vertex load chain per frame).
 __global__ __launch_bounds__(256) void RankKernel(const unsigned* __restrict__ order, unsigned n,
                                                   const float* __restrict__ vertices, unsigned* __restrict__ rank,
                                                   float* __restrict__ svertices) {
@@ -66,10 +67,14 @@ __global__ __launch_bounds__(256) void RankKernel(const unsigned* __restrict__ o
     if (i < n) {
         const unsigned id = order[i];
         rank[id] = i;
+        float* sv = svertices + static_cast<unsigned long long>(kSpatialStride) * i;
 #pragma unroll
         for (int k = 0; k < 9; ++k) {
-            svertices[9ull * i + k] = vertices[9ull * id + k];
+            sv[k] = vertices[9ull * id + k];
         }
+        sv[9] = __uint_as_float(id);
+        sv[10] = 0.f;
+        sv[11] = 0.f;
     }
 }
 

@@ -288,6 +288,46 @@ def test_cull_nasty_geometry(gpu, tmp_path, monkeypatch):
         assert_parity(torch_render(path, 120, 90, off, variant="bvh"), ref)
 
 
+@pytest.mark.parametrize("records", ["stored", "recompute"])
+def test_record_modes_bitwise(gpu, scenes, tmp_path, monkeypatch, records):
+    """Both record sources of the binned trace (render.h RecordMode, env SRT_TRACE_RECORDS): the 64-B
+    cull records the bin kernel stores, or records the trace recomputes from the scene's 48-B spatial
+    inputs and the bin kernel's screen boxes. Single frames of the nasty-geometry scene -- plain, with
+    list overflow (FULL tiles stream every position) and with offsets outside [0, 1] (range-tagged:
+    every tile streams) -- against the oracle, and a batched launch against the LDS brute force, bit
+    for bit."""
+    import torch
+
+    import simpleraytracer_amd as srt
+
+    monkeypatch.setenv("SRT_TRACE_RECORDS", records)
+    path = nasty_scene(tmp_path)
+    w, h = 120, 90
+    rng = np.random.default_rng(19)
+    offsets = rng.random((h, w, 2), dtype=np.float32)
+    wild = offsets.copy()
+    wild[::7] *= 3.0
+    for off in (None, offsets, wild):
+        ref = oracle_render(path, w, h, off)
+        for mode in (("1", "", ""), ("1", "", "8")):
+            set_cull_mode(monkeypatch, mode)
+            assert_parity(torch_render(path, w, h, off, variant="cull"), ref)
+    monkeypatch.delenv("SRT_CULL_BIN_CAP", raising=False)
+    w, h, frames = 200, 120, 3
+    offs = [rng.random((h, w, 2), dtype=np.float32) for _ in range(frames)]
+    refs = [torch_render(scenes["soup2k"], w, h, o, variant="lds") for o in offs]
+    scene = srt.DeviceScene(scenes["soup2k"], 0)
+    stream = torch.cuda.current_stream()
+    scene.prepare(w, h, stream)
+    off = [torch.from_numpy(o).cuda() for o in offs]
+    rgba = [torch.full((h, w, 4), float("nan"), dtype=torch.float32, device="cuda") for _ in range(frames)]
+    scene.trace_batch(off, rgba, 0, h, variant="cull", stream=stream)
+    torch.cuda.synchronize()
+    for f in range(frames):
+        assert np.array_equal(rgba[f].cpu().numpy().view(np.uint32), refs[f].view(np.uint32)), f
+    scene.close()
+
+
 def test_extreme_offsets(gpu, scenes):
     """Sample offsets far outside [0,1), negative, huge, +-inf and NaN: the box cull must stay
     conservative (monotone fma bounds, NaN never rejects) and match the oracle bit for bit."""
