@@ -258,14 +258,16 @@ def run_leg(job, a, path, inputs, steps, warmup, **kw):
         eng.close()
 
 
-def c5_leg(job, a, steps=10, warmup=2, batch=64, queues=1, launch=16):
+def c5_leg(job, a, steps=10, warmup=2, batch=64, queues=1, launch=64):
     """BASELINE config C5 on this GPU: the 1M-triangle soup (seed 0x5EED + 1) at 3840 x 2160 in 64-frame
     steps, with a roofline block of its own for the trace kernel in the leg's launch shape (one launch in
-    flight, HIP events on its dispatch) and the whole-frame figure. Frame loop: one queue of 16-frame
-    launches -- at 4K a record / bin launch and a trace launch each fill the chip, so a second queue only
-    contends (three alternating rounds, profiles/r06/c5_ab/: 59 111 - 59 335 against 57 925 - 58 271
-    Mrays/s with the headline's 2 queues x 8 frames). (C5 proper is 8 GPUs: SCALE runs it; this is its
-    one-GPU leg.)"""
+    flight, HIP events on its dispatch) and the whole-frame figure. Frame loop: one queue, one 64-frame
+    launch per step -- at 4K a record / bin launch and a trace launch each fill the chip, so a second queue
+    only contends (three alternating rounds, profiles/r06/c5_ab/: 59 111 - 59 335 against 57 925 - 58 271
+    Mrays/s with the headline's 2 queues x 8 frames), and fewer launch boundaries drain the chip fewer
+    times (profiles/r06/c5_launch/: 16 / 32 / 64 frames per launch 59 576 - 59 653 / 60 003 - 60 127 /
+    60 150 - 60 413); one queue also has the trace recompute its records (render.h RecordMode). (C5 proper
+    is 8 GPUs: SCALE runs it; this is its one-GPU leg.)"""
     import copy
 
     a5 = copy.copy(a)
