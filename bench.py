@@ -279,9 +279,9 @@ def c5_leg(job, a, steps=10, warmup=2, batch=64, queues=1, launch=64):
     try:
         eng.set_inputs(make_offsets(a5, a.offsets, 1))
         el, mr = timed(job, eng, steps, warmup)
+        bad, checked = eng.verify()  # before the stage timing, which reuses queue 0's frames
         launch_frames = frames_per_launch(a5, 1)
         st = eng.stage_times(0, 24, launch_frames)
-        bad, checked = eng.verify()
     finally:
         eng.close()
     import simpleraytracer_amd as srt
