@@ -293,7 +293,7 @@ def c5_leg(job, a, steps=10, warmup=2, batch=64, queues=1, launch=64):
                                  f"C5 launch shape ({launch_frames} frames per launch), one launch in flight, {st[0]} "
                                  "launches, HIP events bound to the kernel's dispatch")
     return {"workload": wl, "mrays_per_s": round(mr, 3), "ms_per_frame": round(ms_frame, 6), "frames_per_step": batch,
-            "queues": queues, "steps": steps, "roofline": roof, "whole_frame": whole_frame_fields(a5.width, a5.height, n_tri, ms_frame, 1),
+            "queues": queues, "records": records_mode(queues, launch_frames, a.variant), "steps": steps, "roofline": roof, "whole_frame": whole_frame_fields(a5.width, a5.height, n_tri, ms_frame, 1),
             "stages_ms": {"bin": round(st[2], 5), "trace_kernel": round(st[3], 5), "frames_per_launch": launch_frames},
             "verified": bad == 0 and checked > 0}
 
@@ -431,6 +431,17 @@ def frames_per_launch(a, world):
     and 64 for bands over more than one GPU; at most the batch and 256."""
     default = 64 if world > 1 and a.mode == "bands" else 8
     return min(a.launch or int(os.environ.get("SRT_LAUNCH_FRAMES") or default), a.frames_per_step, 256)
+
+
+def records_mode(queues, launch_frames, variant="cull"):
+    """Which records the binned trace reads (render.h RecordMode; renderer.cpp RecomputeRecords): env
+    SRT_TRACE_RECORDS, else recomputed by the trace in a one-queue engine or one-frame launches, else stored."""
+    if variant != "cull":
+        return None
+    env = os.environ.get("SRT_TRACE_RECORDS") or "auto"
+    if env in ("stored", "recompute"):
+        return env
+    return "recompute" if queues == 1 or launch_frames == 1 else "stored"
 
 
 def roofline_fields(wl, variant, launch_rays, launch_frames, n_tri, kernel_ms, band_ids, height_frac, key,
@@ -870,6 +881,7 @@ def main():
                 "frame_queues": a.queues,
                 # engine.h EngineOptions::launch defaults when neither --launch nor SRT_LAUNCH_FRAMES is set
                 "frames_per_launch": launch_frames,
+                "records": records_mode(a.queues, launch_frames, a.variant),
                 "inputs": max(1, a.inputs),
                 "offsets": a.offsets,
             },
