@@ -1717,14 +1717,17 @@ __device__ __forceinline__ void TileInfoBlock(const BinParams& p, int bx, int by
         out_of_range = 0u;
     }
     // All loads first (clamped addresses: duplicates of real pixels), then the box. Same
-    // expressions as GenerateRays; NaN positions drop out of the box (fminf / fmaxf).
+    // expressions as GenerateRays, fx = fl(fl(x + ox) / W), but the division comes after the
+    // reduction: the correctly rounded division by W > 0 is monotone, so the extremes of fx are the
+    // quotients of the extremes of fl(x + ox), bit for bit (fl(x + ox) is never -0: x >= +0) -- two
+    // divisions per tile instead of two per pixel. NaN positions drop out (fminf / fmaxf).
     const float2 o0 = p.offsets[static_cast<size_t>(y0) * p.width + x0];
-    Box box{__builtin_inff(), -__builtin_inff(), __builtin_inff(), -__builtin_inff()};
+    Box box{__builtin_inff(), -__builtin_inff(), __builtin_inff(), -__builtin_inff()};  // of the sums
     bool regular = true, in_range = true;
     auto take = [&](int x, int yy, float2 o) {
-        const float fx = (static_cast<float>(x) + o.x) / p.wf;
-        const float fy = (static_cast<float>(FrameRow(p.row_begin, p.row_interleave, yy)) + o.y) / p.hf;
-        box = Box{fminf(box.xlo, fx), fmaxf(box.xhi, fx), fminf(box.ylo, fy), fmaxf(box.yhi, fy)};
+        const float sx = static_cast<float>(x) + o.x;
+        const float sy = static_cast<float>(FrameRow(p.row_begin, p.row_interleave, yy)) + o.y;
+        box = Box{fminf(box.xlo, sx), fmaxf(box.xhi, sx), fminf(box.ylo, sy), fmaxf(box.yhi, sy)};
         regular = regular && __float_as_uint(o.x) == __float_as_uint(o0.x) && __float_as_uint(o.y) == __float_as_uint(o0.y);
         in_range = in_range && o.x >= 0.f && o.x <= 1.f && o.y >= 0.f && o.y <= 1.f;  // NaN: false
     };
@@ -1778,6 +1781,7 @@ __device__ __forceinline__ void TileInfoBlock(const BinParams& p, int bx, int by
             const Box b = boxes[wave + w];
             box = Box{fminf(box.xlo, b.xlo), fmaxf(box.xhi, b.xhi), fminf(box.ylo, b.ylo), fmaxf(box.yhi, b.yhi)};
         }
+        box = Box{box.xlo / p.wf, box.xhi / p.wf, box.ylo / p.hf, box.yhi / p.hf};  // the rays' (fx, fy) box
         TileInfo ti;
         ti.box = make_float4(box.xlo, box.xhi, box.ylo, box.yhi);
         ti.ox = o0.x;
